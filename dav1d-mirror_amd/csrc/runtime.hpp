@@ -1,0 +1,76 @@
+// runtime.hpp -- host-side plumbing for the per-call (drop-in) tier.
+//
+// Each table entry of the reference (src/mc.h, src/ipred.h, src/itx.h) takes
+// borrowed host pointers and must return with its outputs written
+// (synchronous semantics, reentrant from n_tc worker threads).
+// A Stager gathers exactly the byte extents the reference reads (inputs),
+// writes (outputs) or updates in place (in/out), packs them into one pinned
+// buffer, does one H2D copy, runs the kernel on the calling thread's own
+// stream, one D2H copy, and scatters the results back.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <vector>
+
+namespace dgpu {
+
+[[noreturn]] void fatal(const char *what, hipError_t e);
+inline void hip_check(hipError_t e, const char *what) {
+    if (e != hipSuccess) fatal(what, e);
+}
+
+struct ThreadCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint8_t *host = nullptr;  // pinned
+    uint8_t *dev = nullptr;
+    size_t cap = 0;
+    void reserve(size_t bytes);
+};
+ThreadCtx &thread_ctx();
+
+// A rectangle of bytes relative to a caller base pointer:
+// rows [y0, y1), byte columns [bx0, bx1), caller row stride `stride` (may be
+// negative).  The device copy uses a positive, 16-byte aligned pitch.
+struct Rect {
+    const uint8_t *base;
+    ptrdiff_t stride;
+    long bx0, bx1, y0, y1;
+    int dir;        // 1 in, 2 out, 3 in/out
+    size_t off;     // assigned device offset
+    size_t pitch;
+};
+
+class Stager {
+public:
+    // Returns an index; the device pointer for the caller's `base` (byte
+    // (0,0) of the rect's coordinate system) is origin(idx), pitch pitch(idx).
+    int add(const void *base, ptrdiff_t stride, long bx0, long bx1, long y0, long y1, int dir);
+    int in(const void *b, ptrdiff_t s, long bx0, long bx1, long y0, long y1) { return add(b, s, bx0, bx1, y0, y1, 1); }
+    int out(void *b, ptrdiff_t s, long bx0, long bx1, long y0, long y1) { return add(b, s, bx0, bx1, y0, y1, 2); }
+    int inout(void *b, ptrdiff_t s, long bx0, long bx1, long y0, long y1) { return add(b, s, bx0, bx1, y0, y1, 3); }
+    // 1-D helpers (single row)
+    int in1(const void *b, long bytes) { return add(b, 0, 0, bytes, 0, 1, 1); }
+    int out1(void *b, long bytes) { return add(b, 0, 0, bytes, 0, 1, 2); }
+    int inout1(void *b, long bytes) { return add(b, 0, 0, bytes, 0, 1, 3); }
+
+    // Lays out the buffer and uploads the inputs; after this origin()/pitch()
+    // are valid and the caller launches its kernel on stream().
+    void upload();
+    template <typename T> T *origin(int i) const {
+        const Rect &r = rects_[i];
+        return reinterpret_cast<T *>(ctx_->dev + r.off - r.y0 * (long)r.pitch - r.bx0);
+    }
+    ptrdiff_t pitch(int i) const { return (ptrdiff_t)rects_[i].pitch; }
+    hipStream_t stream() const { return ctx_->stream; }
+    // Downloads outputs, waits, scatters them back into the caller's memory.
+    void finish();
+
+private:
+    ThreadCtx *ctx_ = nullptr;
+    std::vector<Rect> rects_;
+    size_t in_end_ = 0, total_ = 0;
+};
+
+}  // namespace dgpu

@@ -1,0 +1,278 @@
+/*
+ * dav1d_gpu.h -- C-ABI drop-in boundary for dav1d's per-block pixel
+ * reconstruction DSP tables, backed by HIP kernels on MI355X (gfx950).
+ *
+ * Two tiers share one set of kernels:
+ *
+ *  1. Per-call tier (literal drop-in).  The init hooks below fill the
+ *     reference's own function-pointer tables with entries that have exactly
+ *     the reference signatures; each entry stages its (host) arguments to HBM,
+ *     runs the HIP kernel and returns synchronously.  Replaces:
+ *       Dav1dMCDSPContext        src/mc.h:116-132   (typedefs src/mc.h:38-114)
+ *       Dav1dIntraPredDSPContext src/ipred.h:81-90  (typedefs src/ipred.h:44-79)
+ *       Dav1dInvTxfmDSPContext   src/itx.h:42-44    (typedef  src/itx.h:37-40)
+ *     init hooks  bitfn(dav1d_mc_dsp_init)         src/mc_tmpl.c:915
+ *                 bitfn(dav1d_intra_pred_dsp_init) src/ipred_tmpl.c:740
+ *                 bitfn(dav1d_itx_dsp_init)        src/itx_tmpl.c:200
+ *     The struct layouts below are layout-identical to the reference ones
+ *     (arrays of function pointers in the same order), so a pointer to the
+ *     reference's context can be passed straight in.
+ *
+ *  2. Batch tier (performance path).  One grid launch reconstructs a whole
+ *     frame (or superblock row) of transform-block units: prediction
+ *     (mc / mct+avg / intra) fused with inv_txfm_add.  All pointers are
+ *     device pointers already resident in HBM; see dav1d_gpu_recon_*.
+ *
+ * Strides are in BYTES and may be negative, as in the reference.  16bpc entry
+ * points take the trailing `bitdepth_max` argument (0x3ff or 0xfff) except
+ * blend*, emu_edge, cfl_ac and pal_pred (src/mc.h:96-108, src/ipred.h:56-78).
+ *
+ * Errors: the per-call entries return void like the reference.  A HIP failure
+ * inside one is fatal (message on stderr, abort()): the tables never silently
+ * fall back to CPU code.  The batch entry points return 0 or a negative error.
+ */
+#ifndef DAV1D_GPU_H
+#define DAV1D_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- enums mirrored from src/levels.h / include/dav1d/headers.h -------- */
+
+enum Dav1dGpuFilter2d {   /* src/levels.h:184-196, order horizontal,vertical */
+    DGPU_FILTER_2D_8TAP_REGULAR, DGPU_FILTER_2D_8TAP_REGULAR_SMOOTH,
+    DGPU_FILTER_2D_8TAP_REGULAR_SHARP, DGPU_FILTER_2D_8TAP_SHARP_REGULAR,
+    DGPU_FILTER_2D_8TAP_SHARP_SMOOTH, DGPU_FILTER_2D_8TAP_SHARP,
+    DGPU_FILTER_2D_8TAP_SMOOTH_REGULAR, DGPU_FILTER_2D_8TAP_SMOOTH,
+    DGPU_FILTER_2D_8TAP_SMOOTH_SHARP, DGPU_FILTER_2D_BILINEAR,
+    DGPU_N_2D_FILTERS
+};
+
+enum Dav1dGpuIntraMode {  /* remapped IntraPredMode, src/levels.h:108-133 */
+    DGPU_DC_PRED, DGPU_VERT_PRED, DGPU_HOR_PRED, DGPU_LEFT_DC_PRED,
+    DGPU_TOP_DC_PRED, DGPU_DC_128_PRED, DGPU_Z1_PRED, DGPU_Z2_PRED,
+    DGPU_Z3_PRED, DGPU_SMOOTH_PRED, DGPU_SMOOTH_V_PRED, DGPU_SMOOTH_H_PRED,
+    DGPU_PAETH_PRED, DGPU_FILTER_PRED, DGPU_N_IMPL_INTRA_PRED_MODES
+};
+
+enum Dav1dGpuTxfmSize {   /* RectTxfmSize, src/levels.h:44-78 */
+    DGPU_TX_4X4, DGPU_TX_8X8, DGPU_TX_16X16, DGPU_TX_32X32, DGPU_TX_64X64,
+    DGPU_RTX_4X8, DGPU_RTX_8X4, DGPU_RTX_8X16, DGPU_RTX_16X8, DGPU_RTX_16X32,
+    DGPU_RTX_32X16, DGPU_RTX_32X64, DGPU_RTX_64X32, DGPU_RTX_4X16,
+    DGPU_RTX_16X4, DGPU_RTX_8X32, DGPU_RTX_32X8, DGPU_RTX_16X64,
+    DGPU_RTX_64X16, DGPU_N_RECT_TX_SIZES
+};
+
+enum Dav1dGpuTxfmType {   /* TxfmType, src/levels.h:80-100 */
+    DGPU_DCT_DCT, DGPU_ADST_DCT, DGPU_DCT_ADST, DGPU_ADST_ADST,
+    DGPU_FLIPADST_DCT, DGPU_DCT_FLIPADST, DGPU_FLIPADST_FLIPADST,
+    DGPU_ADST_FLIPADST, DGPU_FLIPADST_ADST, DGPU_IDTX, DGPU_V_DCT, DGPU_H_DCT,
+    DGPU_V_ADST, DGPU_H_ADST, DGPU_V_FLIPADST, DGPU_H_FLIPADST,
+    DGPU_WHT_WHT, DGPU_N_TX_TYPES_PLUS_LL
+};
+
+/* ---- DSP table layouts, one per bitdepth ABI ----------------------------
+ * DGPU_DSP_TYPES(sfx, pixel, coef, HBD) expands the reference's decl_*_fn
+ * typedefs and context structs for one pixel/coef ABI (include/common/
+ * bitdepth.h:36-91): sfx = 8bpc (uint8_t / int16_t, no extra argument) or
+ * 16bpc (uint16_t / int32_t, trailing `int bitdepth_max`). */
+#define DGPU_HBD_NONE
+#define DGPU_HBD_ARG , int bitdepth_max
+
+#define DGPU_DSP_TYPES(sfx, pixel, coef, HBD)                                  \
+typedef void (*dgpu_mc_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,            \
+    const pixel *src, ptrdiff_t src_stride, int w, int h, int mx, int my HBD);\
+typedef void (*dgpu_mc_scaled_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,     \
+    const pixel *src, ptrdiff_t src_stride, int w, int h, int mx, int my,     \
+    int dx, int dy HBD);                                                      \
+typedef void (*dgpu_warp8x8_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,       \
+    const pixel *src, ptrdiff_t src_stride, const int16_t *abcd, int mx,      \
+    int my HBD);                                                              \
+typedef void (*dgpu_mct_fn_##sfx)(int16_t *tmp, const pixel *src,             \
+    ptrdiff_t src_stride, int w, int h, int mx, int my HBD);                  \
+typedef void (*dgpu_mct_scaled_fn_##sfx)(int16_t *tmp, const pixel *src,      \
+    ptrdiff_t src_stride, int w, int h, int mx, int my, int dx, int dy HBD);  \
+typedef void (*dgpu_warp8x8t_fn_##sfx)(int16_t *tmp, ptrdiff_t tmp_stride,    \
+    const pixel *src, ptrdiff_t src_stride, const int16_t *abcd, int mx,      \
+    int my HBD);                                                              \
+typedef void (*dgpu_avg_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,           \
+    const int16_t *tmp1, const int16_t *tmp2, int w, int h HBD);              \
+typedef void (*dgpu_w_avg_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,         \
+    const int16_t *tmp1, const int16_t *tmp2, int w, int h, int weight HBD);  \
+typedef void (*dgpu_mask_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,          \
+    const int16_t *tmp1, const int16_t *tmp2, int w, int h,                   \
+    const uint8_t *mask HBD);                                                 \
+typedef void (*dgpu_w_mask_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,        \
+    const int16_t *tmp1, const int16_t *tmp2, int w, int h, uint8_t *mask,    \
+    int sign HBD);                                                            \
+typedef void (*dgpu_blend_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,         \
+    const pixel *tmp, int w, int h, const uint8_t *mask);                     \
+typedef void (*dgpu_blend_dir_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,     \
+    const pixel *tmp, int w, int h);                                          \
+typedef void (*dgpu_emu_edge_fn_##sfx)(intptr_t bw, intptr_t bh,              \
+    intptr_t iw, intptr_t ih, intptr_t x, intptr_t y, pixel *dst,             \
+    ptrdiff_t dst_stride, const pixel *src, ptrdiff_t src_stride);            \
+typedef void (*dgpu_resize_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,        \
+    const pixel *src, ptrdiff_t src_stride, int dst_w, int h, int src_w,      \
+    int dx, int mx HBD);                                                      \
+typedef struct Dav1dMCDSPContext_##sfx {                                      \
+    dgpu_mc_fn_##sfx mc[DGPU_N_2D_FILTERS];                                   \
+    dgpu_mc_scaled_fn_##sfx mc_scaled[DGPU_N_2D_FILTERS];                     \
+    dgpu_mct_fn_##sfx mct[DGPU_N_2D_FILTERS];                                 \
+    dgpu_mct_scaled_fn_##sfx mct_scaled[DGPU_N_2D_FILTERS];                   \
+    dgpu_avg_fn_##sfx avg;                                                    \
+    dgpu_w_avg_fn_##sfx w_avg;                                                \
+    dgpu_mask_fn_##sfx mask;                                                  \
+    dgpu_w_mask_fn_##sfx w_mask[3]; /* 444, 422, 420 */                       \
+    dgpu_blend_fn_##sfx blend;                                                \
+    dgpu_blend_dir_fn_##sfx blend_v;                                          \
+    dgpu_blend_dir_fn_##sfx blend_h;                                          \
+    dgpu_warp8x8_fn_##sfx warp8x8;                                            \
+    dgpu_warp8x8t_fn_##sfx warp8x8t;                                          \
+    dgpu_emu_edge_fn_##sfx emu_edge;                                          \
+    dgpu_resize_fn_##sfx resize;                                              \
+} Dav1dMCDSPContext_##sfx;                                                    \
+typedef void (*dgpu_angular_ipred_fn_##sfx)(pixel *dst, ptrdiff_t stride,     \
+    const pixel *topleft, int width, int height, int angle, int max_width,    \
+    int max_height HBD);                                                      \
+typedef void (*dgpu_cfl_ac_fn_##sfx)(int16_t *ac, const pixel *y,             \
+    ptrdiff_t stride, int w_pad, int h_pad, int cw, int ch);                  \
+typedef void (*dgpu_cfl_pred_fn_##sfx)(pixel *dst, ptrdiff_t stride,          \
+    const pixel *topleft, int width, int height, const int16_t *ac,           \
+    int alpha HBD);                                                           \
+typedef void (*dgpu_pal_pred_fn_##sfx)(pixel *dst, ptrdiff_t stride,          \
+    const pixel *pal, const uint8_t *idx, int w, int h);                      \
+typedef struct Dav1dIntraPredDSPContext_##sfx {                               \
+    dgpu_angular_ipred_fn_##sfx intra_pred[DGPU_N_IMPL_INTRA_PRED_MODES];     \
+    dgpu_cfl_ac_fn_##sfx cfl_ac[3];  /* 420, 422, 444 */                      \
+    dgpu_cfl_pred_fn_##sfx cfl_pred[DGPU_DC_128_PRED + 1];                    \
+    dgpu_pal_pred_fn_##sfx pal_pred;                                          \
+} Dav1dIntraPredDSPContext_##sfx;                                             \
+typedef void (*dgpu_itxfm_fn_##sfx)(pixel *dst, ptrdiff_t dst_stride,         \
+    coef *coeff, int eob HBD);                                                \
+typedef struct Dav1dInvTxfmDSPContext_##sfx {                                 \
+    dgpu_itxfm_fn_##sfx itxfm_add[DGPU_N_RECT_TX_SIZES][DGPU_N_TX_TYPES_PLUS_LL]; \
+} Dav1dInvTxfmDSPContext_##sfx;
+
+DGPU_DSP_TYPES(8bpc, uint8_t, int16_t, DGPU_HBD_NONE)
+DGPU_DSP_TYPES(16bpc, uint16_t, int32_t, DGPU_HBD_ARG)
+
+/* ---- per-call tier: init hooks ------------------------------------------
+ * Same names and signatures as the reference's init hooks
+ * (src/mc.h:134, src/ipred.h:92, src/itx.h:46): linking this library in place
+ * of mc_tmpl.c / ipred_tmpl.c / itx_tmpl.c objects makes every table entry
+ * GPU-backed.  The *_gpu_* variants are arch-style override hooks (the
+ * mc_dsp_init_x86 pattern, src/x86/mc.h:108) for builds that keep the C
+ * defaults and overwrite entries when the GPU cpu-flag is set.  Entries that
+ * the reference leaves NULL (unsupported itx size/type pairs) stay NULL. */
+void dav1d_mc_dsp_init_8bpc(Dav1dMCDSPContext_8bpc *c);
+void dav1d_mc_dsp_init_16bpc(Dav1dMCDSPContext_16bpc *c);
+void dav1d_intra_pred_dsp_init_8bpc(Dav1dIntraPredDSPContext_8bpc *c);
+void dav1d_intra_pred_dsp_init_16bpc(Dav1dIntraPredDSPContext_16bpc *c);
+void dav1d_itx_dsp_init_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int bpc);
+void dav1d_itx_dsp_init_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc);
+
+void dav1d_mc_dsp_init_gpu_8bpc(Dav1dMCDSPContext_8bpc *c);
+void dav1d_mc_dsp_init_gpu_16bpc(Dav1dMCDSPContext_16bpc *c);
+void dav1d_intra_pred_dsp_init_gpu_8bpc(Dav1dIntraPredDSPContext_8bpc *c);
+void dav1d_intra_pred_dsp_init_gpu_16bpc(Dav1dIntraPredDSPContext_16bpc *c);
+void dav1d_itx_dsp_init_gpu_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int bpc);
+void dav1d_itx_dsp_init_gpu_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc);
+
+/* ---- runtime -------------------------------------------------------------*/
+/* Number of usable gfx950 devices (0 when no GPU / no HIP runtime). */
+int dav1d_gpu_device_count(void);
+/* Device used by the calling thread's per-call entries (default 0). */
+int dav1d_gpu_set_device(int device);
+/* Library build identification, e.g. "dav1d-gpu gfx950 r1". */
+const char *dav1d_gpu_version(void);
+
+/* ---- batch tier ----------------------------------------------------------
+ * A batch is an array of transform-block "units" (one per inv_txfm_add call
+ * the reference would make, src/recon_tmpl.c:816/1347/1574/1956/2017), each
+ * carrying the prediction that precedes it in recon_b_inter/recon_b_intra
+ * (src/recon_tmpl.c:1195, :1598).  Units are sorted by tx size class by the
+ * producer; dav1d_gpu_recon_* launches ONE grid over all of them. */
+
+enum Dav1dGpuPredKind {
+    DGPU_PRED_NONE = 0,      /* residual only: dst += itx(coef)            */
+    DGPU_PRED_INTER = 1,     /* mc put from ref0                             */
+    DGPU_PRED_INTER_AVG = 2, /* mct(ref0) + mct(ref1) -> avg                 */
+    DGPU_PRED_INTRA = 3,     /* intra_pred from the unit's edge array        */
+};
+
+/* 32 bytes, device-resident, one per transform block.
+ *
+ * Coefficients are stored compactly: the nzw x nzh top-left region that can
+ * be non-zero (what the reference derives from eob and the scan order,
+ * src/recon_tmpl.c:460-470), column-major with stride nzh -- the reference's
+ * own layout (src/itx_tmpl.c:82-85) restricted to that region.  nzw == 0
+ * marks the reference's DC-only call (eob == 0 with DCT_DCT,
+ * src/itx_tmpl.c:53): one coefficient is stored. */
+typedef struct Dav1dGpuUnit {
+    int32_t  dst_off;     /* pixel offset of the unit's top-left in its plane  */
+    int32_t  coef_off;    /* element offset into the coefficient pool        */
+    uint8_t  tx;          /* Dav1dGpuTxfmSize                                */
+    uint8_t  txtp;        /* Dav1dGpuTxfmType                                */
+    uint8_t  plane;       /* 0 = Y, 1 = U, 2 = V                             */
+    uint8_t  pred;        /* Dav1dGpuPredKind                                */
+    uint8_t  nzw, nzh;    /* stored coefficient region (0 x 0 = DC-only)     */
+    uint8_t  bw4, bh4;    /* prediction-block size in 4-px units: the mc
+                             4-tap/8-tap bank choice uses the block w/h
+                             (src/mc_tmpl.c:99-107), not the unit's          */
+    union {
+        struct {          /* INTER / INTER_AVG                               */
+            int32_t src_off[2];      /* pixel offset in the ref plane of the
+                                        unit's top-left integer position   */
+            uint8_t mx[2], my[2];    /* 1/16-pel fraction 0..15              */
+            uint8_t filter2d;        /* Dav1dGpuFilter2d                     */
+            uint8_t ref[2];          /* reference picture slot               */
+            uint8_t pad_;
+        } inter;
+        struct {          /* INTRA                                           */
+            int32_t  edge_off;       /* offset of topleft[0] in the edge pool */
+            uint16_t angle;          /* angle | is_sm<<9 | filt<<10, or
+                                        filter_idx for FILTER_PRED           */
+            uint8_t  mode;           /* Dav1dGpuIntraMode                    */
+            uint8_t  pad_;
+            uint16_t max_w, max_h;   /* Z2 edge-filter limits                */
+        } intra;
+    } p;
+} Dav1dGpuUnit;
+
+typedef struct Dav1dGpuPlane {
+    void    *data;        /* device pointer to pixel (0,0)                   */
+    int64_t  stride;      /* bytes                                           */
+    int32_t  w, h;        /* visible size (reference reads are clamped)      */
+} Dav1dGpuPlane;
+
+#define DGPU_MAX_REFS 8
+
+typedef struct Dav1dGpuFrameBatch {
+    Dav1dGpuPlane dst[3];                    /* reconstructed planes         */
+    Dav1dGpuPlane ref[DGPU_MAX_REFS][3];     /* reference pictures           */
+    const Dav1dGpuUnit *units;               /* device, sorted by tx class   */
+    int32_t  n_units;
+    int32_t  class_start[DGPU_N_RECT_TX_SIZES + 1]; /* unit ranges per class */
+    const void *coef;     /* device pool: int16 (8bpc) / int32 (16bpc)       */
+    const void *edges;    /* device pool of intra topleft arrays (pixels)    */
+    int32_t  bitdepth_max;
+    int32_t  zero_coefs;  /* 1: honour the coefficient-zeroing contract on
+                             device (src/itx_tmpl.c:55/89): consumed
+                             coefficients are written back as zeros          */
+} Dav1dGpuFrameBatch;
+
+/* Launch one frame batch on `stream` (a hipStream_t, NULL = default).
+ * Returns 0 or a negative error.  Asynchronous w.r.t. the host. */
+int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream);
+int dav1d_gpu_recon_16bpc(const Dav1dGpuFrameBatch *b, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DAV1D_GPU_H */

@@ -1,0 +1,1409 @@
+/*
+ * oracle/dsp_ref.c -- CPU restatement of dav1d's per-block reconstruction
+ * DSP (mc / ipred / itx) used ONLY as the parity checker.
+ *
+ * TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this.  The product (dav1d-mirror_amd/) never
+ * links or calls it.
+ *
+ * PARITY UNPINNED against the reference binary: dav1d's C cannot be built in
+ * this image without hand-writing its meson-generated config.h (a stand-in
+ * for generated code, which the build rules forbid), and the reference ships
+ * no known-answer vectors for these functions (its checkasm is purely
+ * differential, tests/checkasm/checkasm.c:808-862).  This file restates the
+ * reference algorithms line-for-line in semantics (citations per function,
+ * dav1d 1.4.1 paths) and is compiled twice, -DBITDEPTH=8 and -DBITDEPTH=16.
+ */
+#include <assert.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dav1d_gpu.h"
+#include "../dav1d-mirror_amd/csrc/dsp_tables.h"
+
+#if BITDEPTH == 8
+typedef uint8_t pixel;
+typedef int16_t coef;
+#define SFX(x) x##_8bpc
+#define BDPARAM
+#define BDARG
+#define BD_DECL const int bdmax_ = 255; (void)bdmax_;
+#define PX(stride) (stride)
+#else
+typedef uint16_t pixel;
+typedef int32_t coef;
+#define SFX(x) x##_16bpc
+#define BDPARAM , const int bitdepth_max
+#define BDARG , bitdepth_max
+#define BD_DECL const int bdmax_ = bitdepth_max; (void)bdmax_;
+#define PX(stride) ((stride) >> 1)
+#endif
+
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+static inline int mini(int a, int b) { return a < b ? a : b; }
+static inline int maxi(int a, int b) { return a > b ? a : b; }
+static inline int log2i(unsigned v) { return __builtin_ctz(v); }
+static inline int bits_of(int bdmax) { return 32 - __builtin_clz((unsigned)bdmax); }
+
+/* src/mc_tmpl.c:39-49 */
+#if BITDEPTH == 8
+#define IBITS(bdmax) 4
+#define PBIAS 0
+#else
+#define IBITS(bdmax) (14 - bits_of(bdmax))
+#define PBIAS 8192
+#endif
+
+/* ===================================================================== mc */
+
+/* 8-tap kernel for 1-D filter type `t` (0 regular, 1 smooth, 2 sharp) at
+ * sub-pel m (1..15); short blocks (<= 4) use the 4-tap banks, where sharp
+ * maps to regular (src/mc_tmpl.c:99-107). */
+static const int8_t *kern8(int t, int m, int len) {
+    if (!m) return NULL;
+    const int bank = len > 4 ? t : 3 + (t & 1);
+    return (const int8_t *)&dspt_subpel[(bank * 15 + m - 1) * 8];
+}
+
+static inline int taps8(const pixel *p, ptrdiff_t step, const int8_t *k) {
+    int s = 0;
+    for (int i = 0; i < 8; i++) s += k[i] * p[(i - 3) * step];
+    return s;
+}
+static inline int taps8_i16(const int16_t *p, ptrdiff_t step, const int8_t *k) {
+    int s = 0;
+    for (int i = 0; i < 8; i++) s += k[i] * p[(i - 3) * step];
+    return s;
+}
+static inline int rshift_rnd(int v, int sh) { return (v + ((1 << sh) >> 1)) >> sh; }
+
+/* put_8tap_c, src/mc_tmpl.c:113-171 (copy path put_c :52-61) */
+static void put_8tap(pixel *dst, ptrdiff_t dst_stride, const pixel *src,
+                     ptrdiff_t src_stride, int w, int h, int mx, int my,
+                     int ftype, int bdmax)
+{
+    const int ib = IBITS(bdmax);
+    const ptrdiff_t ds = PX(dst_stride), ss = PX(src_stride);
+    const int8_t *fh = kern8(ftype & 3, mx, w), *fv = kern8(ftype >> 2, my, h);
+    if (fh && fv) {
+        int16_t mid[(128 + 7) * 128];
+        for (int r = 0; r < h + 7; r++)
+            for (int x = 0; x < w; x++)
+                mid[r * 128 + x] = rshift_rnd(taps8(&src[(r - 3) * ss + x], 1, fh), 6 - ib);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++)
+                dst[y * ds + x] = clampi(rshift_rnd(taps8_i16(&mid[(y + 3) * 128 + x], 128, fv), 6 + ib), 0, bdmax);
+    } else if (fh) {
+        const int rnd = 32 + ((1 << (6 - ib)) >> 1);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++)
+                dst[y * ds + x] = clampi((taps8(&src[y * ss + x], 1, fh) + rnd) >> 6, 0, bdmax);
+    } else if (fv) {
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++)
+                dst[y * ds + x] = clampi(rshift_rnd(taps8(&src[y * ss + x], ss, fv), 6), 0, bdmax);
+    } else {
+        for (int y = 0; y < h; y++)
+            memcpy(&dst[y * ds], &src[y * ss], w * sizeof(pixel));
+    }
+}
+
+/* prep_8tap_c, src/mc_tmpl.c:223-282 (prep_c :64-75) */
+static void prep_8tap(int16_t *tmp, const pixel *src, ptrdiff_t src_stride,
+                      int w, int h, int mx, int my, int ftype, int bdmax)
+{
+    const int ib = IBITS(bdmax);
+    const ptrdiff_t ss = PX(src_stride);
+    const int8_t *fh = kern8(ftype & 3, mx, w), *fv = kern8(ftype >> 2, my, h);
+    if (fh && fv) {
+        int16_t mid[(128 + 7) * 128];
+        for (int r = 0; r < h + 7; r++)
+            for (int x = 0; x < w; x++)
+                mid[r * 128 + x] = rshift_rnd(taps8(&src[(r - 3) * ss + x], 1, fh), 6 - ib);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int t = rshift_rnd(taps8_i16(&mid[(y + 3) * 128 + x], 128, fv), 6) - PBIAS;
+                assert(t >= INT16_MIN && t <= INT16_MAX);
+                tmp[y * w + x] = t;
+            }
+    } else if (fh) {
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++)
+                tmp[y * w + x] = rshift_rnd(taps8(&src[y * ss + x], 1, fh), 6 - ib) - PBIAS;
+    } else if (fv) {
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++)
+                tmp[y * w + x] = rshift_rnd(taps8(&src[y * ss + x], ss, fv), 6 - ib) - PBIAS;
+    } else {
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++)
+                tmp[y * w + x] = (src[y * ss + x] << ib) - PBIAS;
+    }
+}
+
+/* put_8tap_scaled_c / prep_8tap_scaled_c, src/mc_tmpl.c:173-221, :284-328.
+ * Column x samples source column (mx + x*dx) >> 10 with sub-pel
+ * ((mx + x*dx) & 1023) >> 6; rows likewise with my/dy. */
+static void scaled_8tap(pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
+                        const pixel *src, ptrdiff_t src_stride, int w, int h,
+                        int mx, int my, int dx, int dy, int ftype, int bdmax)
+{
+    const int ib = IBITS(bdmax);
+    const ptrdiff_t ss = PX(src_stride), ds = PX(dst_stride);
+    const int rows = (((h - 1) * dy + my) >> 10) + 8;
+    int16_t *mid = malloc(sizeof(int16_t) * 128 * (256 + 7));
+    for (int r = 0; r < rows; r++) {
+        const pixel *s = &src[(r - 3) * ss];
+        for (int x = 0; x < w; x++) {
+            const int pos = mx + x * dx;
+            const int8_t *fh = kern8(ftype & 3, (pos & 1023) >> 6, w);
+            const int off = pos >> 10;
+            mid[r * 128 + x] = fh ? rshift_rnd(taps8(&s[off], 1, fh), 6 - ib) : s[off] << ib;
+        }
+    }
+    for (int y = 0; y < h; y++) {
+        const int pos = my + y * dy;
+        const int16_t *m = &mid[((pos >> 10) + 3) * 128];
+        const int8_t *fv = kern8(ftype >> 2, (pos & 1023) >> 6, h);
+        for (int x = 0; x < w; x++) {
+            if (dst) {
+                dst[y * ds + x] = fv ? clampi(rshift_rnd(taps8_i16(&m[x], 128, fv), 6 + ib), 0, bdmax)
+                                     : clampi(rshift_rnd(m[x], ib), 0, bdmax);
+            } else {
+                tmp[y * w + x] = (fv ? rshift_rnd(taps8_i16(&m[x], 128, fv), 6) : m[x]) - PBIAS;
+            }
+        }
+    }
+    free(mid);
+}
+
+static inline int bilin(int a, int b, int m) { return 16 * a + m * (b - a); }
+
+/* put_bilin_c / prep_bilin_c, src/mc_tmpl.c:395-450, :493-546 */
+static void bilin_mc(pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
+                     const pixel *src, ptrdiff_t src_stride, int w, int h,
+                     int mx, int my, int bdmax)
+{
+    const int ib = IBITS(bdmax);
+    const ptrdiff_t ss = PX(src_stride), ds = PX(dst_stride);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const pixel *s = &src[y * ss + x];
+            int v;
+            if (mx && my) {
+                const int m0 = (int16_t)rshift_rnd(bilin(s[0], s[1], mx), 4 - ib);
+                const int m1 = (int16_t)rshift_rnd(bilin(s[ss], s[ss + 1], mx), 4 - ib);
+                v = dst ? clampi(rshift_rnd(bilin(m0, m1, my), 4 + ib), 0, bdmax)
+                        : rshift_rnd(bilin(m0, m1, my), 4) - PBIAS;
+            } else if (mx) {
+                const int px = rshift_rnd(bilin(s[0], s[1], mx), 4 - ib);
+                v = dst ? clampi(rshift_rnd(px, ib), 0, bdmax) : px - PBIAS;
+            } else if (my) {
+                v = dst ? clampi(rshift_rnd(bilin(s[0], s[ss], my), 4), 0, bdmax)
+                        : rshift_rnd(bilin(s[0], s[ss], my), 4 - ib) - PBIAS;
+            } else {
+                v = dst ? s[0] : (s[0] << ib) - PBIAS;
+            }
+            if (dst) dst[y * ds + x] = v; else tmp[y * w + x] = v;
+        }
+}
+
+/* put_bilin_scaled_c / prep_bilin_scaled_c, src/mc_tmpl.c:452-491, :548-585 */
+static void bilin_scaled(pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
+                         const pixel *src, ptrdiff_t src_stride, int w, int h,
+                         int mx, int my, int dx, int dy, int bdmax)
+{
+    const int ib = IBITS(bdmax);
+    const ptrdiff_t ss = PX(src_stride), ds = PX(dst_stride);
+    const int rows = (((h - 1) * dy + my) >> 10) + 2;
+    int16_t *mid = malloc(sizeof(int16_t) * 128 * (256 + 1));
+    for (int r = 0; r < rows; r++)
+        for (int x = 0; x < w; x++) {
+            const int pos = mx + x * dx;
+            const pixel *s = &src[r * ss + (pos >> 10)];
+            mid[r * 128 + x] = rshift_rnd(bilin(s[0], s[1], (pos & 1023) >> 6), 4 - ib);
+        }
+    for (int y = 0; y < h; y++) {
+        const int pos = my + y * dy;
+        const int16_t *m = &mid[(pos >> 10) * 128];
+        const int f = (pos & 1023) >> 6;
+        for (int x = 0; x < w; x++) {
+            if (dst) dst[y * ds + x] = clampi(rshift_rnd(bilin(m[x], m[x + 128], f), 4 + ib), 0, bdmax);
+            else tmp[y * w + x] = rshift_rnd(bilin(m[x], m[x + 128], f), 4) - PBIAS;
+        }
+    }
+    free(mid);
+}
+
+/* compound blends, src/mc_tmpl.c:587-639 */
+static void avg_blend(pixel *dst, ptrdiff_t dst_stride, const int16_t *t1,
+                      const int16_t *t2, int w, int h, int kind, int weight,
+                      const uint8_t *mask, int bdmax)
+{
+    const int ib = IBITS(bdmax);
+    const ptrdiff_t ds = PX(dst_stride);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const int a = t1[y * w + x], b = t2[y * w + x];
+            int v;
+            if (kind == 0)
+                v = (a + b + (1 << ib) + 2 * PBIAS) >> (ib + 1);
+            else if (kind == 1)
+                v = (a * weight + b * (16 - weight) + (8 << ib) + 16 * PBIAS) >> (ib + 4);
+            else {
+                const int m = mask[y * w + x];
+                v = (a * m + b * (64 - m) + (32 << ib) + 64 * PBIAS) >> (ib + 6);
+            }
+            dst[y * ds + x] = clampi(v, 0, bdmax);
+        }
+}
+
+/* w_mask_c, src/mc_tmpl.c:683-726: derived mask, optional 2x1 / 2x2
+ * sub-sampling of the stored mask with `sign` rounding. */
+static void w_mask(pixel *dst, ptrdiff_t dst_stride, const int16_t *t1,
+                   const int16_t *t2, int w, int h, uint8_t *mask, int sign,
+                   int ssh, int ssv, int bdmax)
+{
+    const int ib = IBITS(bdmax);
+    const int msh = bits_of(bdmax) + ib - 4;
+    const int mrnd = 1 << (msh - 5);
+    const ptrdiff_t ds = PX(dst_stride);
+    const int mw = w >> ssh;
+    for (int y = 0; y < h; y++) {
+        uint8_t *mrow = &mask[(y >> ssv) * mw];
+        for (int x = 0; x < w; x++) {
+            const int a = t1[y * w + x], b = t2[y * w + x];
+            const int m = mini(38 + ((abs(a - b) + mrnd) >> msh), 64);
+            dst[y * ds + x] = clampi((a * m + b * (64 - m) + (32 << ib) + 64 * PBIAS) >> (ib + 6), 0, bdmax);
+            if (!ssh) { mrow[x] = m; continue; }
+            if (x & 1) {
+                const int a0 = t1[y * w + x - 1], b0 = t2[y * w + x - 1];
+                const int m0 = mini(38 + ((abs(a0 - b0) + mrnd) >> msh), 64);
+                const int sum = m0 + m;
+                if (!ssv) mrow[x >> 1] = (sum + 1 - sign) >> 1;
+                else if (!(y & 1)) mrow[x >> 1] = sum;
+                else mrow[x >> 1] = (sum + mrow[x >> 1] + 2 - sign) >> 2;
+            }
+        }
+    }
+}
+
+/* blend_c / blend_v_c / blend_h_c, src/mc_tmpl.c:641-681 */
+static inline int blend_px(int a, int b, int m) { return (a * (64 - m) + b * m + 32) >> 6; }
+
+static void blend(pixel *dst, ptrdiff_t dst_stride, const pixel *tmp, int w, int h,
+                  const uint8_t *mask)
+{
+    const ptrdiff_t ds = PX(dst_stride);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            dst[y * ds + x] = blend_px(dst[y * ds + x], tmp[y * w + x], mask[y * w + x]);
+}
+
+static void blend_v(pixel *dst, ptrdiff_t dst_stride, const pixel *tmp, int w, int h)
+{
+    const ptrdiff_t ds = PX(dst_stride);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < (w * 3) >> 2; x++)
+            dst[y * ds + x] = blend_px(dst[y * ds + x], tmp[y * w + x], dspt_obmc[w + x]);
+}
+
+static void blend_h(pixel *dst, ptrdiff_t dst_stride, const pixel *tmp, int w, int h)
+{
+    const ptrdiff_t ds = PX(dst_stride);
+    for (int y = 0; y < (h * 3) >> 2; y++)
+        for (int x = 0; x < w; x++)
+            dst[y * ds + x] = blend_px(dst[y * ds + x], tmp[y * w + x], dspt_obmc[h + y]);
+}
+
+/* warp_affine_8x8_c / _8x8t_c, src/mc_tmpl.c:758-825 */
+static void warp8x8(pixel *dst, ptrdiff_t dst_stride, int16_t *tmp, ptrdiff_t tmp_stride,
+                    const pixel *src, ptrdiff_t src_stride, const int16_t *abcd,
+                    int mx, int my, int bdmax)
+{
+    const int ib = IBITS(bdmax);
+    const ptrdiff_t ss = PX(src_stride);
+    int16_t mid[15 * 8];
+    for (int r = 0; r < 15; r++) {
+        const pixel *s = &src[(r - 3) * ss];
+        const int rowx = mx + r * abcd[1];
+        for (int x = 0; x < 8; x++) {
+            const int8_t *k = (const int8_t *)&dspt_warp[(64 + ((rowx + x * abcd[0] + 512) >> 10)) * 8];
+            mid[r * 8 + x] = rshift_rnd(taps8(&s[x], 1, k), 7 - ib);
+        }
+    }
+    for (int y = 0; y < 8; y++) {
+        const int coly = my + y * abcd[3];
+        for (int x = 0; x < 8; x++) {
+            const int8_t *k = (const int8_t *)&dspt_warp[(64 + ((coly + x * abcd[2] + 512) >> 10)) * 8];
+            const int s = taps8_i16(&mid[(y + 3) * 8 + x], 8, k);
+            if (dst) dst[y * PX(dst_stride) + x] = clampi(rshift_rnd(s, 7 + ib), 0, bdmax);
+            else tmp[y * tmp_stride + x] = rshift_rnd(s, 7) - PBIAS;
+        }
+    }
+}
+
+/* emu_edge_c, src/mc_tmpl.c:827-875: every output pixel is the source pixel
+ * at the position clamped into the iw x ih picture. */
+static void emu_edge(intptr_t bw, intptr_t bh, intptr_t iw, intptr_t ih,
+                     intptr_t x, intptr_t y, pixel *dst, ptrdiff_t dst_stride,
+                     const pixel *ref, ptrdiff_t ref_stride)
+{
+    const ptrdiff_t ds = PX(dst_stride), rs = PX(ref_stride);
+    for (int yy = 0; yy < bh; yy++) {
+        const int sy = clampi((int)(y + yy), 0, (int)ih - 1);
+        for (int xx = 0; xx < bw; xx++) {
+            const int sx = clampi((int)(x + xx), 0, (int)iw - 1);
+            dst[yy * ds + xx] = ref[sy * rs + sx];
+        }
+    }
+}
+
+/* resize_c, src/mc_tmpl.c:877-903 */
+static void resize(pixel *dst, ptrdiff_t dst_stride, const pixel *src,
+                   ptrdiff_t src_stride, int dst_w, int h, int src_w, int dx,
+                   int mx0, int bdmax)
+{
+    for (int y = 0; y < h; y++) {
+        const pixel *s = &src[y * PX(src_stride)];
+        for (int x = 0; x < dst_w; x++) {
+            const int pos = mx0 + x * dx;          /* 14-bit fixed point */
+            const int sx = (pos >> 14) - 1;
+            const int8_t *k = (const int8_t *)&dspt_resize[((pos & 0x3fff) >> 8) * 8];
+            int sum = 0;
+            for (int i = 0; i < 8; i++) sum += k[i] * s[clampi(sx + i - 3, 0, src_w - 1)];
+            dst[y * PX(dst_stride) + x] = clampi((-sum + 64) >> 7, 0, bdmax);
+        }
+    }
+}
+
+/* ================================================================== ipred */
+
+/* splat_dc / dc_gen*, src/ipred_tmpl.c:39-166 */
+static void fill(pixel *dst, ptrdiff_t stride, int w, int h, int v) {
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) dst[y * PX(stride) + x] = v;
+}
+static unsigned dc_top(const pixel *tl, int w) {
+    unsigned s = w >> 1;
+    for (int i = 1; i <= w; i++) s += tl[i];
+    return s >> log2i(w);
+}
+static unsigned dc_left(const pixel *tl, int h) {
+    unsigned s = h >> 1;
+    for (int i = 1; i <= h; i++) s += tl[-i];
+    return s >> log2i(h);
+}
+static unsigned dc_both(const pixel *tl, int w, int h) {
+    unsigned s = (w + h) >> 1;
+    for (int i = 1; i <= w; i++) s += tl[i];
+    for (int i = 1; i <= h; i++) s += tl[-i];
+    s >>= log2i(w + h);
+    if (w != h) {
+        const int r4 = w > 2 * h || h > 2 * w;
+#if BITDEPTH == 8
+        s = (s * (r4 ? 0x3334u : 0x5556u)) >> 16;
+#else
+        s = (s * (r4 ? 0x6667u : 0xAAABu)) >> 17;
+#endif
+    }
+    return s;
+}
+
+/* cfl_pred, src/ipred_tmpl.c:71-84 */
+static void cfl(pixel *dst, ptrdiff_t stride, int w, int h, int dc,
+                const int16_t *ac, int alpha, int bdmax)
+{
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const int d = alpha * ac[y * w + x];
+            const int mag = (abs(d) + 32) >> 6;
+            dst[y * PX(stride) + x] = clampi(dc + (d < 0 ? -mag : mag), 0, bdmax);
+        }
+}
+
+/* get_filter_strength, src/ipred_tmpl.c:327-360 */
+static int edge_strength(int wh, int angle, int is_sm) {
+    if (is_sm) {
+        if (wh <= 8) return angle >= 64 ? 2 : angle >= 40 ? 1 : 0;
+        if (wh <= 16) return angle >= 48 ? 2 : angle >= 20 ? 1 : 0;
+        if (wh <= 24) return angle >= 4 ? 3 : 0;
+        return 3;
+    }
+    if (wh <= 8) return angle >= 56 ? 1 : 0;
+    if (wh <= 16) return angle >= 40 ? 1 : 0;
+    if (wh <= 24) return angle >= 32 ? 3 : angle >= 16 ? 2 : angle >= 8 ? 1 : 0;
+    if (wh <= 32) return angle >= 32 ? 3 : angle >= 4 ? 2 : 1;
+    return 3;
+}
+
+/* filter_edge, src/ipred_tmpl.c:362-385 */
+static void smooth_edge(pixel *out, int sz, int lim_from, int lim_to,
+                        const pixel *in, int from, int to, int strength)
+{
+    static const uint8_t k[3][5] = { { 0, 4, 8, 4, 0 }, { 0, 5, 6, 5, 0 }, { 2, 4, 4, 4, 2 } };
+    for (int i = 0; i < sz; i++) {
+        if (i < lim_from || i >= lim_to) {
+            out[i] = in[clampi(i, from, to - 1)];
+        } else {
+            int s = 0;
+            for (int j = 0; j < 5; j++) s += in[clampi(i - 2 + j, from, to - 1)] * k[strength - 1][j];
+            out[i] = (s + 8) >> 4;
+        }
+    }
+}
+
+/* get_upsample / upsample_edge, src/ipred_tmpl.c:387-406 */
+static int use_upsample(int wh, int angle, int is_sm) { return angle < 40 && wh <= (16 >> is_sm); }
+
+static void upsample(pixel *out, int hsz, const pixel *in, int from, int to, int bdmax)
+{
+    for (int i = 0; i < hsz - 1; i++) {
+        out[2 * i] = in[clampi(i, from, to - 1)];
+        const int s = -in[clampi(i - 1, from, to - 1)] + 9 * in[clampi(i, from, to - 1)]
+                    + 9 * in[clampi(i + 1, from, to - 1)] - in[clampi(i + 2, from, to - 1)];
+        out[2 * i + 1] = clampi((s + 8) >> 4, 0, bdmax);
+    }
+    out[2 * (hsz - 1)] = in[clampi(hsz - 1, from, to - 1)];
+}
+
+/* ipred_z1_c, src/ipred_tmpl.c:408-460 */
+static void z1(pixel *dst, ptrdiff_t stride, const pixel *tl, int w, int h, int angle, int bdmax)
+{
+    const int is_sm = (angle >> 9) & 1, filt = angle >> 10;
+    angle &= 511;
+    int dx = dspt_dr_deriv[angle >> 1];
+    pixel buf[64 + 64];
+    const pixel *top;
+    int maxb;
+    const int up = filt ? use_upsample(w + h, 90 - angle, is_sm) : 0;
+    if (up) {
+        upsample(buf, w + h, &tl[1], -1, w + mini(w, h), bdmax);
+        top = buf; maxb = 2 * (w + h) - 2; dx <<= 1;
+    } else {
+        const int st = filt ? edge_strength(w + h, 90 - angle, is_sm) : 0;
+        if (st) {
+            smooth_edge(buf, w + h, 0, w + h, &tl[1], -1, w + mini(w, h), st);
+            top = buf; maxb = w + h - 1;
+        } else {
+            top = &tl[1]; maxb = w + mini(w, h) - 1;
+        }
+    }
+    for (int y = 0; y < h; y++) {
+        const int xpos = (y + 1) * dx, frac = xpos & 0x3e;
+        for (int x = 0; x < w; x++) {
+            const int base = (xpos >> 6) + x * (1 + up);
+            dst[y * PX(stride) + x] = base < maxb
+                ? (top[base] * (64 - frac) + top[base + 1] * frac + 32) >> 6
+                : top[maxb];
+        }
+    }
+}
+
+/* ipred_z2_c, src/ipred_tmpl.c:462-540 */
+static void z2(pixel *dst, ptrdiff_t stride, const pixel *tl, int w, int h, int angle,
+               int max_w, int max_h, int bdmax)
+{
+    const int is_sm = (angle >> 9) & 1, filt = angle >> 10;
+    angle &= 511;
+    int dy = dspt_dr_deriv[(angle - 90) >> 1];
+    int dx = dspt_dr_deriv[(180 - angle) >> 1];
+    const int upl = filt ? use_upsample(w + h, 180 - angle, is_sm) : 0;
+    const int upa = filt ? use_upsample(w + h, angle - 90, is_sm) : 0;
+    pixel edge[64 + 64 + 1];
+    pixel *const c = &edge[64];
+    if (upa) {
+        upsample(c, w + 1, tl, 0, w + 1, bdmax);
+        dx <<= 1;
+    } else {
+        const int st = filt ? edge_strength(w + h, angle - 90, is_sm) : 0;
+        if (st) smooth_edge(&c[1], w, 0, max_w, &tl[1], -1, w, st);
+        else memcpy(&c[1], &tl[1], w * sizeof(pixel));
+    }
+    if (upl) {
+        upsample(&c[-2 * h], h + 1, &tl[-h], 0, h + 1, bdmax);
+        dy <<= 1;
+    } else {
+        const int st = filt ? edge_strength(w + h, 180 - angle, is_sm) : 0;
+        if (st) smooth_edge(&c[-h], h, h - max_h, h, &tl[-h], 0, h + 1, st);
+        else memcpy(&c[-h], &tl[-h], h * sizeof(pixel));
+    }
+    c[0] = tl[0];
+    const pixel *left = &c[-(1 + upl)];
+    for (int y = 0; y < h; y++) {
+        const int xpos = ((1 + upa) << 6) - (y + 1) * dx;
+        const int fx = xpos & 0x3e;
+        for (int x = 0; x < w; x++) {
+            const int bx = (xpos >> 6) + x * (1 + upa);
+            int v;
+            if (bx >= 0) {
+                v = c[bx] * (64 - fx) + c[bx + 1] * fx;
+            } else {
+                const int ypos = (y << (6 + upl)) - (x + 1) * dy;
+                const int by = ypos >> 6, fy = ypos & 0x3e;
+                v = left[-by] * (64 - fy) + left[-(by + 1)] * fy;
+            }
+            dst[y * PX(stride) + x] = (v + 32) >> 6;
+        }
+    }
+}
+
+/* ipred_z3_c, src/ipred_tmpl.c:542-599 */
+static void z3(pixel *dst, ptrdiff_t stride, const pixel *tl, int w, int h, int angle, int bdmax)
+{
+    const int is_sm = (angle >> 9) & 1, filt = angle >> 10;
+    angle &= 511;
+    int dy = dspt_dr_deriv[(270 - angle) >> 1];
+    pixel buf[64 + 64];
+    const pixel *left;
+    int maxb;
+    const int up = filt ? use_upsample(w + h, angle - 180, is_sm) : 0;
+    if (up) {
+        upsample(buf, w + h, &tl[-(w + h)], maxi(w - h, 0), w + h + 1, bdmax);
+        left = &buf[2 * (w + h) - 2]; maxb = 2 * (w + h) - 2; dy <<= 1;
+    } else {
+        const int st = filt ? edge_strength(w + h, angle - 180, is_sm) : 0;
+        if (st) {
+            smooth_edge(buf, w + h, 0, w + h, &tl[-(w + h)], maxi(w - h, 0), w + h + 1, st);
+            left = &buf[w + h - 1]; maxb = w + h - 1;
+        } else {
+            left = &tl[-1]; maxb = h + mini(w, h) - 1;
+        }
+    }
+    for (int x = 0; x < w; x++) {
+        const int ypos = (x + 1) * dy, frac = ypos & 0x3e;
+        for (int y = 0; y < h; y++) {
+            const int base = (ypos >> 6) + y * (1 + up);
+            dst[y * PX(stride) + x] = base < maxb
+                ? (left[-base] * (64 - frac) + left[-(base + 1)] * frac + 32) >> 6
+                : left[-maxb];
+        }
+    }
+}
+
+/* ipred_filter_c, src/ipred_tmpl.c:617-655: 4x2 cells in raster order, each
+ * predicted from the 7 pixels above / left of it (reconstructed cells). */
+static void filter_intra(pixel *dst, ptrdiff_t stride, const pixel *tl, int w, int h,
+                         int fidx, int bdmax)
+{
+    fidx &= 511;
+    const signed char *taps = &dspt_filter_intra[fidx * 56];
+    const ptrdiff_t ds = PX(stride);
+    for (int y = 0; y < h; y += 2)
+        for (int x = 0; x < w; x += 4) {
+            int p[7];
+            /* p0 top-left, p1..p4 above, p5..p6 left */
+            if (y == 0) {
+                p[0] = x == 0 ? tl[0] : tl[x];
+                for (int i = 0; i < 4; i++) p[1 + i] = tl[1 + x + i];
+            } else {
+                p[0] = x == 0 ? tl[-y] : dst[(y - 1) * ds + x - 1];
+                for (int i = 0; i < 4; i++) p[1 + i] = dst[(y - 1) * ds + x + i];
+            }
+            for (int i = 0; i < 2; i++)
+                p[5 + i] = x == 0 ? tl[-(y + 1 + i)] : dst[(y + i) * ds + x - 1];
+            for (int k = 0; k < 8; k++) {
+                int acc = 0;
+                for (int i = 0; i < 7; i++) acc += taps[k * 7 + i] * p[i];
+                dst[(y + (k >> 2)) * ds + x + (k & 3)] = clampi((acc + 8) >> 4, 0, bdmax);
+            }
+        }
+}
+
+/* cfl_ac_c, src/ipred_tmpl.c:657-703 */
+static void cfl_ac(int16_t *ac, const pixel *ypx, ptrdiff_t stride, int w_pad, int h_pad,
+                   int cw, int ch, int ssh, int ssv)
+{
+    const ptrdiff_t ys = PX(stride);
+    const int vw = cw - 4 * w_pad, vh = ch - 4 * h_pad;
+    for (int y = 0; y < ch; y++)
+        for (int x = 0; x < cw; x++) {
+            const int sy = mini(y, vh - 1), sx = mini(x, vw - 1);
+            const pixel *p = &ypx[(sy << ssv) * ys + (sx << ssh)];
+            int s = p[0];
+            if (ssh) s += p[1];
+            if (ssv) { s += p[ys]; if (ssh) s += p[ys + 1]; }
+            ac[y * cw + x] = s << (1 + !ssv + !ssh);
+        }
+    const int lg = log2i(cw) + log2i(ch);
+    int sum = (1 << lg) >> 1;
+    for (int i = 0; i < cw * ch; i++) sum += ac[i];
+    sum >>= lg;
+    for (int i = 0; i < cw * ch; i++) ac[i] -= sum;
+}
+
+/* ============================================== DSP table entry wrappers */
+
+static void ipred_dc(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ BD_DECL fill(d, s, w, h, dc_both(tl, w, h)); }
+static void ipred_dc_top(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ BD_DECL fill(d, s, w, h, dc_top(tl, w)); }
+static void ipred_dc_left(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ BD_DECL fill(d, s, w, h, dc_left(tl, h)); }
+static void ipred_dc_128(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ BD_DECL fill(d, s, w, h, (bdmax_ + 1) >> 1); }
+static void ipred_v(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ for (int y = 0; y < h; y++) memcpy(&d[y * PX(s)], &tl[1], w * sizeof(pixel)); }
+static void ipred_h(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ for (int y = 0; y < h; y++) for (int x = 0; x < w; x++) d[y * PX(s) + x] = tl[-(1 + y)]; }
+
+/* ipred_paeth_c, src/ipred_tmpl.c:244-265 */
+static void ipred_paeth(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{
+    const int c = tl[0];
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const int l = tl[-(1 + y)], t = tl[1 + x];
+            const int base = l + t - c;
+            const int dl = abs(l - base), dt = abs(t - base), dc = abs(c - base);
+            d[y * PX(s) + x] = (dl <= dt && dl <= dc) ? l : dt <= dc ? t : c;
+        }
+}
+
+/* ipred_smooth{,_v,_h}_c, src/ipred_tmpl.c:267-325 */
+static void ipred_smooth(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{
+    const uint8_t *wh = &dspt_sm_weights[w], *wv = &dspt_sm_weights[h];
+    const int right = tl[w], bottom = tl[-h];
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const int p = wv[y] * tl[1 + x] + (256 - wv[y]) * bottom
+                        + wh[x] * tl[-(1 + y)] + (256 - wh[x]) * right;
+            d[y * PX(s) + x] = (p + 256) >> 9;
+        }
+}
+static void ipred_smooth_v(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{
+    const uint8_t *wv = &dspt_sm_weights[h];
+    const int bottom = tl[-h];
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            d[y * PX(s) + x] = (wv[y] * tl[1 + x] + (256 - wv[y]) * bottom + 128) >> 8;
+}
+static void ipred_smooth_h(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{
+    const uint8_t *wh = &dspt_sm_weights[w];
+    const int right = tl[w];
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            d[y * PX(s) + x] = (wh[x] * tl[-(1 + y)] + (256 - wh[x]) * right + 128) >> 8;
+}
+static void ipred_z1(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ BD_DECL z1(d, s, tl, w, h, a, bdmax_); }
+static void ipred_z2(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ BD_DECL z2(d, s, tl, w, h, a, mw, mh, bdmax_); }
+static void ipred_z3(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ BD_DECL z3(d, s, tl, w, h, a, bdmax_); }
+static void ipred_filter(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, int a, int mw, int mh BDPARAM)
+{ BD_DECL filter_intra(d, s, tl, w, h, a, bdmax_); }
+
+static void cfl_pred_dc(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, const int16_t *ac, int al BDPARAM)
+{ BD_DECL cfl(d, s, w, h, dc_both(tl, w, h), ac, al, bdmax_); }
+static void cfl_pred_top(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, const int16_t *ac, int al BDPARAM)
+{ BD_DECL cfl(d, s, w, h, dc_top(tl, w), ac, al, bdmax_); }
+static void cfl_pred_left(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, const int16_t *ac, int al BDPARAM)
+{ BD_DECL cfl(d, s, w, h, dc_left(tl, h), ac, al, bdmax_); }
+static void cfl_pred_128(pixel *d, ptrdiff_t s, const pixel *tl, int w, int h, const int16_t *ac, int al BDPARAM)
+{ BD_DECL cfl(d, s, w, h, (bdmax_ + 1) >> 1, ac, al, bdmax_); }
+
+static void cfl_ac_420(int16_t *ac, const pixel *y, ptrdiff_t s, int wp, int hp, int cw, int ch)
+{ cfl_ac(ac, y, s, wp, hp, cw, ch, 1, 1); }
+static void cfl_ac_422(int16_t *ac, const pixel *y, ptrdiff_t s, int wp, int hp, int cw, int ch)
+{ cfl_ac(ac, y, s, wp, hp, cw, ch, 1, 0); }
+static void cfl_ac_444(int16_t *ac, const pixel *y, ptrdiff_t s, int wp, int hp, int cw, int ch)
+{ cfl_ac(ac, y, s, wp, hp, cw, ch, 0, 0); }
+
+/* pal_pred_c, src/ipred_tmpl.c:717-730 */
+static void pal_pred(pixel *d, ptrdiff_t s, const pixel *pal, const uint8_t *idx, int w, int h)
+{
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x += 2) {
+            const int i = *idx++;
+            d[y * PX(s) + x] = pal[i & 7];
+            d[y * PX(s) + x + 1] = pal[i >> 4];
+        }
+}
+
+#define MC_WRAPPERS(name, ft)                                                   \
+static void put_##name(pixel *d, ptrdiff_t ds, const pixel *s, ptrdiff_t ss,    \
+                       int w, int h, int mx, int my BDPARAM)                    \
+{ BD_DECL put_8tap(d, ds, s, ss, w, h, mx, my, ft, bdmax_); }                   \
+static void prep_##name(int16_t *t, const pixel *s, ptrdiff_t ss,               \
+                        int w, int h, int mx, int my BDPARAM)                   \
+{ BD_DECL prep_8tap(t, s, ss, w, h, mx, my, ft, bdmax_); }                      \
+static void put_scaled_##name(pixel *d, ptrdiff_t ds, const pixel *s,           \
+                              ptrdiff_t ss, int w, int h, int mx, int my,       \
+                              int dx, int dy BDPARAM)                           \
+{ BD_DECL scaled_8tap(d, ds, NULL, s, ss, w, h, mx, my, dx, dy, ft, bdmax_); }  \
+static void prep_scaled_##name(int16_t *t, const pixel *s, ptrdiff_t ss,        \
+                               int w, int h, int mx, int my, int dx, int dy     \
+                               BDPARAM)                                         \
+{ BD_DECL scaled_8tap(NULL, 0, t, s, ss, w, h, mx, my, dx, dy, ft, bdmax_); }
+
+/* filter_type = type_h | type_v << 2, REGULAR 0 / SMOOTH 1 / SHARP 2 */
+MC_WRAPPERS(regular,        0 | 0 << 2)
+MC_WRAPPERS(regular_smooth, 0 | 1 << 2)
+MC_WRAPPERS(regular_sharp,  0 | 2 << 2)
+MC_WRAPPERS(sharp_regular,  2 | 0 << 2)
+MC_WRAPPERS(sharp_smooth,   2 | 1 << 2)
+MC_WRAPPERS(sharp,          2 | 2 << 2)
+MC_WRAPPERS(smooth_regular, 1 | 0 << 2)
+MC_WRAPPERS(smooth,         1 | 1 << 2)
+MC_WRAPPERS(smooth_sharp,   1 | 2 << 2)
+
+static void put_bilin(pixel *d, ptrdiff_t ds, const pixel *s, ptrdiff_t ss, int w, int h, int mx, int my BDPARAM)
+{ BD_DECL bilin_mc(d, ds, NULL, s, ss, w, h, mx, my, bdmax_); }
+static void prep_bilin(int16_t *t, const pixel *s, ptrdiff_t ss, int w, int h, int mx, int my BDPARAM)
+{ BD_DECL bilin_mc(NULL, 0, t, s, ss, w, h, mx, my, bdmax_); }
+static void put_scaled_bilin(pixel *d, ptrdiff_t ds, const pixel *s, ptrdiff_t ss, int w, int h,
+                             int mx, int my, int dx, int dy BDPARAM)
+{ BD_DECL bilin_scaled(d, ds, NULL, s, ss, w, h, mx, my, dx, dy, bdmax_); }
+static void prep_scaled_bilin(int16_t *t, const pixel *s, ptrdiff_t ss, int w, int h,
+                              int mx, int my, int dx, int dy BDPARAM)
+{ BD_DECL bilin_scaled(NULL, 0, t, s, ss, w, h, mx, my, dx, dy, bdmax_); }
+
+static void mc_avg(pixel *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h BDPARAM)
+{ BD_DECL avg_blend(d, ds, a, b, w, h, 0, 0, NULL, bdmax_); }
+static void mc_w_avg(pixel *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h, int wt BDPARAM)
+{ BD_DECL avg_blend(d, ds, a, b, w, h, 1, wt, NULL, bdmax_); }
+static void mc_mask(pixel *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h,
+                    const uint8_t *m BDPARAM)
+{ BD_DECL avg_blend(d, ds, a, b, w, h, 2, 0, m, bdmax_); }
+static void mc_w_mask_444(pixel *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h,
+                          uint8_t *m, int sign BDPARAM)
+{ BD_DECL w_mask(d, ds, a, b, w, h, m, sign, 0, 0, bdmax_); }
+static void mc_w_mask_422(pixel *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h,
+                          uint8_t *m, int sign BDPARAM)
+{ BD_DECL w_mask(d, ds, a, b, w, h, m, sign, 1, 0, bdmax_); }
+static void mc_w_mask_420(pixel *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h,
+                          uint8_t *m, int sign BDPARAM)
+{ BD_DECL w_mask(d, ds, a, b, w, h, m, sign, 1, 1, bdmax_); }
+static void mc_warp8x8(pixel *d, ptrdiff_t ds, const pixel *s, ptrdiff_t ss, const int16_t *abcd,
+                       int mx, int my BDPARAM)
+{ BD_DECL warp8x8(d, ds, NULL, 0, s, ss, abcd, mx, my, bdmax_); }
+static void mc_warp8x8t(int16_t *t, ptrdiff_t ts, const pixel *s, ptrdiff_t ss, const int16_t *abcd,
+                        int mx, int my BDPARAM)
+{ BD_DECL warp8x8(NULL, 0, t, ts, s, ss, abcd, mx, my, bdmax_); }
+static void mc_resize(pixel *d, ptrdiff_t ds, const pixel *s, ptrdiff_t ss, int dw, int h, int sw,
+                      int dx, int mx BDPARAM)
+{ BD_DECL resize(d, ds, s, ss, dw, h, sw, dx, mx, bdmax_); }
+
+/* ==================================================================== itx */
+
+#define CLIP(v) clampi(v, mn, mx)
+
+/* 12-bit fixed-point rotation pieces.  The (k - 4096) spellings keep every
+ * intermediate inside 32 bits for 12-bit content exactly like
+ * src/itx_1d.c:39-63; they are algebraically identical to the plain products. */
+static void idct4(int32_t *c, ptrdiff_t s, int mn, int mx, int half)
+{
+    const int i0 = c[0], i1 = c[s];
+    int a, b, p, q;
+    if (half) {
+        a = b = (i0 * 181 + 128) >> 8;
+        p = (i1 * 1567 + 2048) >> 12;
+        q = (i1 * 3784 + 2048) >> 12;
+    } else {
+        const int i2 = c[2 * s], i3 = c[3 * s];
+        a = ((i0 + i2) * 181 + 128) >> 8;
+        b = ((i0 - i2) * 181 + 128) >> 8;
+        p = ((i1 * 1567 - i3 * (3784 - 4096) + 2048) >> 12) - i3;
+        q = ((i1 * (3784 - 4096) + i3 * 1567 + 2048) >> 12) + i1;
+    }
+    c[0] = CLIP(a + q); c[s] = CLIP(b + p); c[2 * s] = CLIP(b - p); c[3 * s] = CLIP(a - q);
+}
+
+/* src/itx_1d.c:98-143 */
+static void idct8(int32_t *c, ptrdiff_t s, int mn, int mx, int half)
+{
+    idct4(c, 2 * s, mn, mx, half);
+    const int i1 = c[s], i3 = c[3 * s];
+    int u4, u5, u6, u7;
+    if (half) {
+        u4 = (i1 * 799 + 2048) >> 12;
+        u5 = (i3 * -2276 + 2048) >> 12;
+        u6 = (i3 * 3406 + 2048) >> 12;
+        u7 = (i1 * 4017 + 2048) >> 12;
+    } else {
+        const int i5 = c[5 * s], i7 = c[7 * s];
+        u4 = ((i1 * 799 - i7 * (4017 - 4096) + 2048) >> 12) - i7;
+        u5 = (i5 * 1703 - i3 * 1138 + 1024) >> 11;
+        u6 = (i5 * 1138 + i3 * 1703 + 1024) >> 11;
+        u7 = ((i1 * (4017 - 4096) + i7 * 799 + 2048) >> 12) + i1;
+    }
+    const int v4 = CLIP(u4 + u5), v5 = CLIP(u4 - u5);
+    const int v7 = CLIP(u7 + u6), v6 = CLIP(u7 - u6);
+    const int w5 = ((v6 - v5) * 181 + 128) >> 8;
+    const int w6 = ((v6 + v5) * 181 + 128) >> 8;
+    const int e0 = c[0], e1 = c[2 * s], e2 = c[4 * s], e3 = c[6 * s];
+    c[0] = CLIP(e0 + v7); c[s] = CLIP(e1 + w6); c[2 * s] = CLIP(e2 + w5); c[3 * s] = CLIP(e3 + v4);
+    c[4 * s] = CLIP(e3 - v4); c[5 * s] = CLIP(e2 - w5); c[6 * s] = CLIP(e1 - w6); c[7 * s] = CLIP(e0 - v7);
+}
+
+/* src/itx_1d.c:151-238 */
+static void idct16(int32_t *c, ptrdiff_t s, int mn, int mx, int half)
+{
+    idct8(c, 2 * s, mn, mx, half);
+    const int i1 = c[s], i3 = c[3 * s], i5 = c[5 * s], i7 = c[7 * s];
+    int a8, a9, a10, a11, a12, a13, a14, a15;
+    if (half) {
+        a8 = (i1 * 401 + 2048) >> 12;   a9 = (i7 * -2598 + 2048) >> 12;
+        a10 = (i5 * 1931 + 2048) >> 12; a11 = (i3 * -1189 + 2048) >> 12;
+        a12 = (i3 * 3920 + 2048) >> 12; a13 = (i5 * 3612 + 2048) >> 12;
+        a14 = (i7 * 3166 + 2048) >> 12; a15 = (i1 * 4076 + 2048) >> 12;
+    } else {
+        const int i9 = c[9 * s], i11 = c[11 * s], i13 = c[13 * s], i15 = c[15 * s];
+        a8 = ((i1 * 401 - i15 * (4076 - 4096) + 2048) >> 12) - i15;
+        a9 = (i9 * 1583 - i7 * 1299 + 1024) >> 11;
+        a10 = ((i5 * 1931 - i11 * (3612 - 4096) + 2048) >> 12) - i11;
+        a11 = ((i13 * (3920 - 4096) - i3 * 1189 + 2048) >> 12) + i13;
+        a12 = ((i13 * 1189 + i3 * (3920 - 4096) + 2048) >> 12) + i3;
+        a13 = ((i5 * (3612 - 4096) + i11 * 1931 + 2048) >> 12) + i5;
+        a14 = (i9 * 1299 + i7 * 1583 + 1024) >> 11;
+        a15 = ((i1 * (4076 - 4096) + i15 * 401 + 2048) >> 12) + i1;
+    }
+    int b8 = CLIP(a8 + a9), b9 = CLIP(a8 - a9), b10 = CLIP(a11 - a10), b11 = CLIP(a11 + a10);
+    int b12 = CLIP(a12 + a13), b13 = CLIP(a12 - a13), b14 = CLIP(a15 - a14), b15 = CLIP(a15 + a14);
+    const int r9 = ((b14 * 1567 - b9 * (3784 - 4096) + 2048) >> 12) - b9;
+    const int r14 = ((b14 * (3784 - 4096) + b9 * 1567 + 2048) >> 12) + b14;
+    const int r10 = ((-(b13 * (3784 - 4096) + b10 * 1567) + 2048) >> 12) - b13;
+    const int r13 = ((b13 * 1567 - b10 * (3784 - 4096) + 2048) >> 12) - b10;
+    const int d8 = CLIP(b8 + b11), d9 = CLIP(r9 + r10), d10 = CLIP(r9 - r10), d11 = CLIP(b8 - b11);
+    const int d12 = CLIP(b15 - b12), d13 = CLIP(r14 - r13), d14 = CLIP(r14 + r13), d15 = CLIP(b15 + b12);
+    const int f10 = ((d13 - d10) * 181 + 128) >> 8, f13 = ((d13 + d10) * 181 + 128) >> 8;
+    const int f11 = ((d12 - d11) * 181 + 128) >> 8, f12 = ((d12 + d11) * 181 + 128) >> 8;
+    const int odd[8] = { d15, d14, f13, f12, f11, f10, d9, d8 };
+    int even[8];
+    for (int i = 0; i < 8; i++) even[i] = c[2 * i * s];
+    for (int i = 0; i < 8; i++) {
+        c[i * s] = CLIP(even[i] + odd[i]);
+        c[(15 - i) * s] = CLIP(even[i] - odd[i]);
+    }
+}
+
+/* src/itx_1d.c:246-428 */
+static void idct32(int32_t *c, ptrdiff_t s, int mn, int mx, int half)
+{
+    idct16(c, 2 * s, mn, mx, half);
+    int in[32];
+    for (int i = 1; i < (half ? 16 : 32); i += 2) in[i] = c[i * s];
+    int t[32];
+    if (half) {
+        t[16] = (in[1] * 201 + 2048) >> 12;    t[17] = (in[15] * -2751 + 2048) >> 12;
+        t[18] = (in[9] * 1751 + 2048) >> 12;   t[19] = (in[7] * -1380 + 2048) >> 12;
+        t[20] = (in[5] * 995 + 2048) >> 12;    t[21] = (in[11] * -2106 + 2048) >> 12;
+        t[22] = (in[13] * 2440 + 2048) >> 12;  t[23] = (in[3] * -601 + 2048) >> 12;
+        t[24] = (in[3] * 4052 + 2048) >> 12;   t[25] = (in[13] * 3290 + 2048) >> 12;
+        t[26] = (in[11] * 3513 + 2048) >> 12;  t[27] = (in[5] * 3973 + 2048) >> 12;
+        t[28] = (in[7] * 3857 + 2048) >> 12;   t[29] = (in[9] * 3703 + 2048) >> 12;
+        t[30] = (in[15] * 3035 + 2048) >> 12;  t[31] = (in[1] * 4091 + 2048) >> 12;
+    } else {
+        t[16] = ((in[1] * 201 - in[31] * (4091 - 4096) + 2048) >> 12) - in[31];
+        t[17] = ((in[17] * (3035 - 4096) - in[15] * 2751 + 2048) >> 12) + in[17];
+        t[18] = ((in[9] * 1751 - in[23] * (3703 - 4096) + 2048) >> 12) - in[23];
+        t[19] = ((in[25] * (3857 - 4096) - in[7] * 1380 + 2048) >> 12) + in[25];
+        t[20] = ((in[5] * 995 - in[27] * (3973 - 4096) + 2048) >> 12) - in[27];
+        t[21] = ((in[21] * (3513 - 4096) - in[11] * 2106 + 2048) >> 12) + in[21];
+        t[22] = (in[13] * 1220 - in[19] * 1645 + 1024) >> 11;
+        t[23] = ((in[29] * (4052 - 4096) - in[3] * 601 + 2048) >> 12) + in[29];
+        t[24] = ((in[29] * 601 + in[3] * (4052 - 4096) + 2048) >> 12) + in[3];
+        t[25] = (in[13] * 1645 + in[19] * 1220 + 1024) >> 11;
+        t[26] = ((in[21] * 2106 + in[11] * (3513 - 4096) + 2048) >> 12) + in[11];
+        t[27] = ((in[5] * (3973 - 4096) + in[27] * 995 + 2048) >> 12) + in[5];
+        t[28] = ((in[25] * 1380 + in[7] * (3857 - 4096) + 2048) >> 12) + in[7];
+        t[29] = ((in[9] * (3703 - 4096) + in[23] * 1751 + 2048) >> 12) + in[9];
+        t[30] = ((in[17] * 2751 + in[15] * (3035 - 4096) + 2048) >> 12) + in[15];
+        t[31] = ((in[1] * (4091 - 4096) + in[31] * 201 + 2048) >> 12) + in[1];
+    }
+    /* stage 1: pairwise sum/difference within groups of four */
+    int u[32];
+    for (int g = 16; g < 32; g += 4) {
+        u[g] = CLIP(t[g] + t[g + 1]);     u[g + 1] = CLIP(t[g] - t[g + 1]);
+        u[g + 2] = CLIP(t[g + 3] - t[g + 2]); u[g + 3] = CLIP(t[g + 3] + t[g + 2]);
+    }
+    /* stage 2 rotations */
+    int v17 = ((u[30] * 799 - u[17] * (4017 - 4096) + 2048) >> 12) - u[17];
+    int v30 = ((u[30] * (4017 - 4096) + u[17] * 799 + 2048) >> 12) + u[30];
+    int v18 = ((-(u[29] * (4017 - 4096) + u[18] * 799) + 2048) >> 12) - u[29];
+    int v29 = ((u[29] * 799 - u[18] * (4017 - 4096) + 2048) >> 12) - u[18];
+    int v21 = (u[26] * 1703 - u[21] * 1138 + 1024) >> 11;
+    int v26 = (u[26] * 1138 + u[21] * 1703 + 1024) >> 11;
+    int v22 = (-(u[25] * 1138 + u[22] * 1703) + 1024) >> 11;
+    int v25 = (u[25] * 1703 - u[22] * 1138 + 1024) >> 11;
+    /* stage 3 */
+    int w16 = CLIP(u[16] + u[19]), w17 = CLIP(v17 + v18), w18 = CLIP(v17 - v18), w19 = CLIP(u[16] - u[19]);
+    int w20 = CLIP(u[23] - u[20]), w21 = CLIP(v22 - v21), w22 = CLIP(v22 + v21), w23 = CLIP(u[23] + u[20]);
+    int w24 = CLIP(u[24] + u[27]), w25 = CLIP(v25 + v26), w26 = CLIP(v25 - v26), w27 = CLIP(u[24] - u[27]);
+    int w28 = CLIP(u[31] - u[28]), w29 = CLIP(v30 - v29), w30 = CLIP(v30 + v29), w31 = CLIP(u[31] + u[28]);
+    /* stage 4 rotations */
+    int x18 = ((w29 * 1567 - w18 * (3784 - 4096) + 2048) >> 12) - w18;
+    int x29 = ((w29 * (3784 - 4096) + w18 * 1567 + 2048) >> 12) + w29;
+    int x19 = ((w28 * 1567 - w19 * (3784 - 4096) + 2048) >> 12) - w19;
+    int x28 = ((w28 * (3784 - 4096) + w19 * 1567 + 2048) >> 12) + w28;
+    int x20 = ((-(w27 * (3784 - 4096) + w20 * 1567) + 2048) >> 12) - w27;
+    int x27 = ((w27 * 1567 - w20 * (3784 - 4096) + 2048) >> 12) - w20;
+    int x21 = ((-(w26 * (3784 - 4096) + w21 * 1567) + 2048) >> 12) - w26;
+    int x26 = ((w26 * 1567 - w21 * (3784 - 4096) + 2048) >> 12) - w21;
+    /* stage 5 */
+    int y16 = CLIP(w16 + w23), y17 = CLIP(w17 + w22), y18 = CLIP(x18 + x21), y19 = CLIP(x19 + x20);
+    int y20 = CLIP(x19 - x20), y21 = CLIP(x18 - x21), y22 = CLIP(w17 - w22), y23 = CLIP(w16 - w23);
+    int y24 = CLIP(w31 - w24), y25 = CLIP(w30 - w25), y26 = CLIP(x29 - x26), y27 = CLIP(x28 - x27);
+    int y28 = CLIP(x28 + x27), y29 = CLIP(x29 + x26), y30 = CLIP(w30 + w25), y31 = CLIP(w31 + w24);
+    /* stage 6: sqrt(1/2) rotations */
+    int z20 = ((y27 - y20) * 181 + 128) >> 8, z27 = ((y27 + y20) * 181 + 128) >> 8;
+    int z21 = ((y26 - y21) * 181 + 128) >> 8, z26 = ((y26 + y21) * 181 + 128) >> 8;
+    int z22 = ((y25 - y22) * 181 + 128) >> 8, z25 = ((y25 + y22) * 181 + 128) >> 8;
+    int z23 = ((y24 - y23) * 181 + 128) >> 8, z24 = ((y24 + y23) * 181 + 128) >> 8;
+    const int odd[16] = { y31, y30, y29, y28, z27, z26, z25, z24, z23, z22, z21, z20, y19, y18, y17, y16 };
+    int even[16];
+    for (int i = 0; i < 16; i++) even[i] = c[2 * i * s];
+    for (int i = 0; i < 16; i++) {
+        c[i * s] = CLIP(even[i] + odd[i]);
+        c[(31 - i) * s] = CLIP(even[i] - odd[i]);
+    }
+}
+
+/* src/itx_1d.c:436-781 (input rows >= 32 are zero) */
+static void idct64(int32_t *c, ptrdiff_t s, int mn, int mx)
+{
+    idct32(c, 2 * s, mn, mx, 1);
+    int in[32];
+    for (int i = 1; i < 32; i += 2) in[i] = c[i * s];
+    int a[64];
+    static const int16_t mul[32][2] = {  /* {input index, constant} for t32a..t63a */
+        { 1, 101 }, { 31, -2824 }, { 17, 1660 }, { 15, -1474 }, { 9, 897 }, { 23, -2191 },
+        { 25, 2359 }, { 7, -700 }, { 5, 501 }, { 27, -2520 }, { 21, 2019 }, { 11, -1092 },
+        { 13, 1285 }, { 19, -1842 }, { 29, 2675 }, { 3, -301 }, { 3, 4085 }, { 29, 3102 },
+        { 19, 3659 }, { 13, 3889 }, { 11, 3948 }, { 21, 3564 }, { 27, 3229 }, { 5, 4065 },
+        { 7, 4036 }, { 25, 3349 }, { 23, 3461 }, { 9, 3996 }, { 15, 3822 }, { 17, 3745 },
+        { 31, 2967 }, { 1, 4095 },
+    };
+    for (int i = 0; i < 32; i++) a[32 + i] = (in[mul[i][0]] * mul[i][1] + 2048) >> 12;
+    int b[64];
+    for (int g = 32; g < 64; g += 4) {
+        b[g] = CLIP(a[g] + a[g + 1]);     b[g + 1] = CLIP(a[g] - a[g + 1]);
+        b[g + 2] = CLIP(a[g + 3] - a[g + 2]); b[g + 3] = CLIP(a[g + 3] + a[g + 2]);
+    }
+    int r[64];
+    r[33] = ((b[33] * (4096 - 4076) + b[62] * 401 + 2048) >> 12) - b[33];
+    r[34] = ((b[34] * -401 + b[61] * (4096 - 4076) + 2048) >> 12) - b[61];
+    r[37] = (b[37] * -1299 + b[58] * 1583 + 1024) >> 11;
+    r[38] = (b[38] * -1583 + b[57] * -1299 + 1024) >> 11;
+    r[41] = ((b[41] * (4096 - 3612) + b[54] * 1931 + 2048) >> 12) - b[41];
+    r[42] = ((b[42] * -1931 + b[53] * (4096 - 3612) + 2048) >> 12) - b[53];
+    r[45] = ((b[45] * -1189 + b[50] * (3920 - 4096) + 2048) >> 12) + b[50];
+    r[46] = ((b[46] * (4096 - 3920) + b[49] * -1189 + 2048) >> 12) - b[46];
+    r[49] = ((b[46] * -1189 + b[49] * (3920 - 4096) + 2048) >> 12) + b[49];
+    r[50] = ((b[45] * (3920 - 4096) + b[50] * 1189 + 2048) >> 12) + b[45];
+    r[53] = ((b[42] * (4096 - 3612) + b[53] * 1931 + 2048) >> 12) - b[42];
+    r[54] = ((b[41] * 1931 + b[54] * (3612 - 4096) + 2048) >> 12) + b[54];
+    r[57] = (b[38] * -1299 + b[57] * 1583 + 1024) >> 11;
+    r[58] = (b[37] * 1583 + b[58] * 1299 + 1024) >> 11;
+    r[61] = ((b[34] * (4096 - 4076) + b[61] * 401 + 2048) >> 12) - b[34];
+    r[62] = ((b[33] * 401 + b[62] * (4076 - 4096) + 2048) >> 12) + b[62];
+    /* r at the untouched positions: carry b through */
+    for (int g = 32; g < 64; g += 4) { r[g] = b[g]; r[g + 3] = b[g + 3]; }
+    int d[64];
+    for (int g = 32; g < 64; g += 8) {
+        d[g] = CLIP(r[g] + r[g + 3]);         d[g + 1] = CLIP(r[g + 1] + r[g + 2]);
+        d[g + 2] = CLIP(r[g + 1] - r[g + 2]); d[g + 3] = CLIP(r[g] - r[g + 3]);
+        d[g + 4] = CLIP(r[g + 7] - r[g + 4]); d[g + 5] = CLIP(r[g + 6] - r[g + 5]);
+        d[g + 6] = CLIP(r[g + 6] + r[g + 5]); d[g + 7] = CLIP(r[g + 7] + r[g + 4]);
+    }
+    int e[64];
+    for (int i = 32; i < 64; i++) e[i] = d[i];
+    e[34] = ((d[34] * (4096 - 4017) + d[61] * 799 + 2048) >> 12) - d[34];
+    e[35] = ((d[35] * (4096 - 4017) + d[60] * 799 + 2048) >> 12) - d[35];
+    e[36] = ((d[36] * -799 + d[59] * (4096 - 4017) + 2048) >> 12) - d[59];
+    e[37] = ((d[37] * -799 + d[58] * (4096 - 4017) + 2048) >> 12) - d[58];
+    e[42] = (d[42] * -1138 + d[53] * 1703 + 1024) >> 11;
+    e[43] = (d[43] * -1138 + d[52] * 1703 + 1024) >> 11;
+    e[44] = (d[44] * -1703 + d[51] * -1138 + 1024) >> 11;
+    e[45] = (d[45] * -1703 + d[50] * -1138 + 1024) >> 11;
+    e[50] = (d[45] * -1138 + d[50] * 1703 + 1024) >> 11;
+    e[51] = (d[44] * -1138 + d[51] * 1703 + 1024) >> 11;
+    e[52] = (d[43] * 1703 + d[52] * 1138 + 1024) >> 11;
+    e[53] = (d[42] * 1703 + d[53] * 1138 + 1024) >> 11;
+    e[58] = ((d[37] * (4096 - 4017) + d[58] * 799 + 2048) >> 12) - d[37];
+    e[59] = ((d[36] * (4096 - 4017) + d[59] * 799 + 2048) >> 12) - d[36];
+    e[60] = ((d[35] * 799 + d[60] * (4017 - 4096) + 2048) >> 12) + d[60];
+    e[61] = ((d[34] * 799 + d[61] * (4017 - 4096) + 2048) >> 12) + d[61];
+    int f[64];
+    for (int g = 32; g < 64; g += 16) {
+        for (int i = 0; i < 4; i++) {
+            f[g + i] = CLIP(e[g + i] + e[g + 7 - i]);
+            f[g + 7 - i] = CLIP(e[g + i] - e[g + 7 - i]);
+            f[g + 8 + i] = CLIP(e[g + 15 - i] - e[g + 8 + i]);
+            f[g + 15 - i] = CLIP(e[g + 15 - i] + e[g + 8 + i]);
+        }
+    }
+    int q[64];
+    for (int i = 32; i < 64; i++) q[i] = f[i];
+    for (int i = 0; i < 4; i++) {
+        /* t36..t39 with t59..t56, then t40..t43 with t55..t52 */
+        const int lo = 36 + i, hi = 59 - i;
+        q[lo] = ((f[lo] * (4096 - 3784) + f[hi] * 1567 + 2048) >> 12) - f[lo];
+        q[hi] = ((f[lo] * 1567 + f[hi] * (3784 - 4096) + 2048) >> 12) + f[hi];
+        const int lo2 = 40 + i, hi2 = 55 - i;
+        q[lo2] = ((f[lo2] * -1567 + f[hi2] * (4096 - 3784) + 2048) >> 12) - f[hi2];
+        q[hi2] = ((f[lo2] * (4096 - 3784) + f[hi2] * 1567 + 2048) >> 12) - f[lo2];
+    }
+    int g2[64];
+    for (int i = 0; i < 8; i++) {
+        g2[32 + i] = CLIP(q[32 + i] + q[47 - i]);
+        g2[47 - i] = CLIP(q[32 + i] - q[47 - i]);
+        g2[48 + i] = CLIP(q[63 - i] - q[48 + i]);
+        g2[63 - i] = CLIP(q[63 - i] + q[48 + i]);
+    }
+    int h2[64];
+    for (int i = 32; i < 64; i++) h2[i] = g2[i];
+    for (int i = 0; i < 8; i++) {
+        const int lo = 40 + i, hi = 55 - i;
+        h2[lo] = ((g2[hi] - g2[lo]) * 181 + 128) >> 8;
+        h2[hi] = ((g2[hi] + g2[lo]) * 181 + 128) >> 8;
+    }
+    int even[32];
+    for (int i = 0; i < 32; i++) even[i] = c[2 * i * s];
+    for (int i = 0; i < 32; i++) {
+        c[i * s] = CLIP(even[i] + h2[63 - i]);
+        c[(63 - i) * s] = CLIP(even[i] - h2[63 - i]);
+    }
+}
+
+/* src/itx_1d.c:783-802 (no clipping) */
+static void iadst4(const int32_t *in, ptrdiff_t is, int32_t *out, ptrdiff_t os)
+{
+    const int a = in[0], b = in[is], c = in[2 * is], d = in[3 * is];
+    const int o0 = ((1321 * a + (3803 - 4096) * c + (2482 - 4096) * d + (3344 - 4096) * b + 2048) >> 12) + c + d + b;
+    const int o1 = (((2482 - 4096) * a - 1321 * c - (3803 - 4096) * d + (3344 - 4096) * b + 2048) >> 12) + a - d + b;
+    const int o2 = (209 * (a - c + d) + 128) >> 8;
+    const int o3 = (((3803 - 4096) * a + (2482 - 4096) * c - 1321 * d - (3344 - 4096) * b + 2048) >> 12) + a + c - b;
+    out[0] = o0; out[os] = o1; out[2 * os] = o2; out[3 * os] = o3;
+}
+
+/* src/itx_1d.c:804-851 */
+static void iadst8(const int32_t *in, ptrdiff_t is, int32_t *out, ptrdiff_t os, int mn, int mx)
+{
+    int i[8];
+    for (int k = 0; k < 8; k++) i[k] = in[k * is];
+    const int t0a = (((4076 - 4096) * i[7] + 401 * i[0] + 2048) >> 12) + i[7];
+    const int t1a = ((401 * i[7] - (4076 - 4096) * i[0] + 2048) >> 12) - i[0];
+    const int t2a = (((3612 - 4096) * i[5] + 1931 * i[2] + 2048) >> 12) + i[5];
+    const int t3a = ((1931 * i[5] - (3612 - 4096) * i[2] + 2048) >> 12) - i[2];
+    const int t4a = (1299 * i[3] + 1583 * i[4] + 1024) >> 11;
+    const int t5a = (1583 * i[3] - 1299 * i[4] + 1024) >> 11;
+    const int t6a = ((1189 * i[1] + (3920 - 4096) * i[6] + 2048) >> 12) + i[6];
+    const int t7a = (((3920 - 4096) * i[1] - 1189 * i[6] + 2048) >> 12) + i[1];
+    const int t0 = CLIP(t0a + t4a), t1 = CLIP(t1a + t5a), t2 = CLIP(t2a + t6a), t3 = CLIP(t3a + t7a);
+    const int t4 = CLIP(t0a - t4a), t5 = CLIP(t1a - t5a), t6 = CLIP(t2a - t6a), t7 = CLIP(t3a - t7a);
+    const int u4 = (((3784 - 4096) * t4 + 1567 * t5 + 2048) >> 12) + t4;
+    const int u5 = ((1567 * t4 - (3784 - 4096) * t5 + 2048) >> 12) - t5;
+    const int u6 = (((3784 - 4096) * t7 - 1567 * t6 + 2048) >> 12) + t7;
+    const int u7 = ((1567 * t7 + (3784 - 4096) * t6 + 2048) >> 12) + t6;
+    int o[8];
+    o[0] = CLIP(t0 + t2);
+    o[7] = -CLIP(t1 + t3);
+    const int v2 = CLIP(t0 - t2), v3 = CLIP(t1 - t3);
+    o[1] = -CLIP(u4 + u6);
+    o[6] = CLIP(u5 + u7);
+    const int v6 = CLIP(u4 - u6), v7 = CLIP(u5 - u7);
+    o[3] = -(((v2 + v3) * 181 + 128) >> 8);
+    o[4] = ((v2 - v3) * 181 + 128) >> 8;
+    o[2] = ((v6 + v7) * 181 + 128) >> 8;
+    o[5] = -(((v6 - v7) * 181 + 128) >> 8);
+    for (int k = 0; k < 8; k++) out[k * os] = o[k];
+}
+
+/* src/itx_1d.c:853-962 */
+static void iadst16(const int32_t *in, ptrdiff_t is, int32_t *out, ptrdiff_t os, int mn, int mx)
+{
+    int i[16];
+    for (int k = 0; k < 16; k++) i[k] = in[k * is];
+    int t0 = ((i[15] * (4091 - 4096) + i[0] * 201 + 2048) >> 12) + i[15];
+    int t1 = ((i[15] * 201 - i[0] * (4091 - 4096) + 2048) >> 12) - i[0];
+    int t2 = ((i[13] * (3973 - 4096) + i[2] * 995 + 2048) >> 12) + i[13];
+    int t3 = ((i[13] * 995 - i[2] * (3973 - 4096) + 2048) >> 12) - i[2];
+    int t4 = ((i[11] * (3703 - 4096) + i[4] * 1751 + 2048) >> 12) + i[11];
+    int t5 = ((i[11] * 1751 - i[4] * (3703 - 4096) + 2048) >> 12) - i[4];
+    int t6 = (i[9] * 1645 + i[6] * 1220 + 1024) >> 11;
+    int t7 = (i[9] * 1220 - i[6] * 1645 + 1024) >> 11;
+    int t8 = ((i[7] * 2751 + i[8] * (3035 - 4096) + 2048) >> 12) + i[8];
+    int t9 = ((i[7] * (3035 - 4096) - i[8] * 2751 + 2048) >> 12) + i[7];
+    int t10 = ((i[5] * 2106 + i[10] * (3513 - 4096) + 2048) >> 12) + i[10];
+    int t11 = ((i[5] * (3513 - 4096) - i[10] * 2106 + 2048) >> 12) + i[5];
+    int t12 = ((i[3] * 1380 + i[12] * (3857 - 4096) + 2048) >> 12) + i[12];
+    int t13 = ((i[3] * (3857 - 4096) - i[12] * 1380 + 2048) >> 12) + i[3];
+    int t14 = ((i[1] * 601 + i[14] * (4052 - 4096) + 2048) >> 12) + i[14];
+    int t15 = ((i[1] * (4052 - 4096) - i[14] * 601 + 2048) >> 12) + i[1];
+    int a0 = CLIP(t0 + t8), a1 = CLIP(t1 + t9), a2 = CLIP(t2 + t10), a3 = CLIP(t3 + t11);
+    int a4 = CLIP(t4 + t12), a5 = CLIP(t5 + t13), a6 = CLIP(t6 + t14), a7 = CLIP(t7 + t15);
+    int a8 = CLIP(t0 - t8), a9 = CLIP(t1 - t9), a10 = CLIP(t2 - t10), a11 = CLIP(t3 - t11);
+    int a12 = CLIP(t4 - t12), a13 = CLIP(t5 - t13), a14 = CLIP(t6 - t14), a15 = CLIP(t7 - t15);
+    int b8 = ((a8 * (4017 - 4096) + a9 * 799 + 2048) >> 12) + a8;
+    int b9 = ((a8 * 799 - a9 * (4017 - 4096) + 2048) >> 12) - a9;
+    int b10 = ((a10 * 2276 + a11 * (3406 - 4096) + 2048) >> 12) + a11;
+    int b11 = ((a10 * (3406 - 4096) - a11 * 2276 + 2048) >> 12) + a10;
+    int b12 = ((a13 * (4017 - 4096) - a12 * 799 + 2048) >> 12) + a13;
+    int b13 = ((a13 * 799 + a12 * (4017 - 4096) + 2048) >> 12) + a12;
+    int b14 = ((a15 * 2276 - a14 * (3406 - 4096) + 2048) >> 12) - a14;
+    int b15 = ((a15 * (3406 - 4096) + a14 * 2276 + 2048) >> 12) + a15;
+    int c0 = CLIP(a0 + a4), c1 = CLIP(a1 + a5), c2 = CLIP(a2 + a6), c3 = CLIP(a3 + a7);
+    int c4 = CLIP(a0 - a4), c5 = CLIP(a1 - a5), c6 = CLIP(a2 - a6), c7 = CLIP(a3 - a7);
+    int c8 = CLIP(b8 + b12), c9 = CLIP(b9 + b13), c10 = CLIP(b10 + b14), c11 = CLIP(b11 + b15);
+    int c12 = CLIP(b8 - b12), c13 = CLIP(b9 - b13), c14 = CLIP(b10 - b14), c15 = CLIP(b11 - b15);
+    int d4 = ((c4 * (3784 - 4096) + c5 * 1567 + 2048) >> 12) + c4;
+    int d5 = ((c4 * 1567 - c5 * (3784 - 4096) + 2048) >> 12) - c5;
+    int d6 = ((c7 * (3784 - 4096) - c6 * 1567 + 2048) >> 12) + c7;
+    int d7 = ((c7 * 1567 + c6 * (3784 - 4096) + 2048) >> 12) + c6;
+    int d12 = ((c12 * (3784 - 4096) + c13 * 1567 + 2048) >> 12) + c12;
+    int d13 = ((c12 * 1567 - c13 * (3784 - 4096) + 2048) >> 12) - c13;
+    int d14 = ((c15 * (3784 - 4096) - c14 * 1567 + 2048) >> 12) + c15;
+    int d15 = ((c15 * 1567 + c14 * (3784 - 4096) + 2048) >> 12) + c14;
+    int o[16];
+    o[0] = CLIP(c0 + c2);
+    o[15] = -CLIP(c1 + c3);
+    const int e2 = CLIP(c0 - c2), e3 = CLIP(c1 - c3);
+    o[3] = -CLIP(d4 + d6);
+    o[12] = CLIP(d5 + d7);
+    const int e6 = CLIP(d4 - d6), e7 = CLIP(d5 - d7);
+    o[1] = -CLIP(c8 + c10);
+    o[14] = CLIP(c9 + c11);
+    const int e10 = CLIP(c8 - c10), e11 = CLIP(c9 - c11);
+    o[2] = CLIP(d12 + d14);
+    o[13] = -CLIP(d13 + d15);
+    const int e14 = CLIP(d12 - d14), e15 = CLIP(d13 - d15);
+    o[7] = -(((e2 + e3) * 181 + 128) >> 8);
+    o[8] = ((e2 - e3) * 181 + 128) >> 8;
+    o[4] = ((e6 + e7) * 181 + 128) >> 8;
+    o[11] = -(((e6 - e7) * 181 + 128) >> 8);
+    o[6] = ((e10 + e11) * 181 + 128) >> 8;
+    o[9] = -(((e10 - e11) * 181 + 128) >> 8);
+    o[5] = -(((e14 + e15) * 181 + 128) >> 8);
+    o[10] = ((e14 - e15) * 181 + 128) >> 8;
+    for (int k = 0; k < 16; k++) out[k * os] = o[k];
+}
+
+/* 1-D kernel kinds, as in the reference's names */
+enum { K_DCT, K_ADST, K_FLIPADST, K_IDENTITY };
+
+/* dispatch one 1-D inverse transform of length n in place (src/itx_1d.c
+ * dav1d_inv_*_1d_c entry points incl. flipadst via reversed output,
+ * :964-979, and the identity scalings :983-1017) */
+static void tx1d(int kind, int n, int32_t *c, ptrdiff_t s, int mn, int mx)
+{
+    if (kind == K_DCT) {
+        if (n == 4) idct4(c, s, mn, mx, 0);
+        else if (n == 8) idct8(c, s, mn, mx, 0);
+        else if (n == 16) idct16(c, s, mn, mx, 0);
+        else if (n == 32) idct32(c, s, mn, mx, 0);
+        else idct64(c, s, mn, mx);
+    } else if (kind == K_ADST || kind == K_FLIPADST) {
+        int32_t *o = kind == K_ADST ? c : &c[(n - 1) * s];
+        const ptrdiff_t os = kind == K_ADST ? s : -s;
+        if (n == 4) iadst4(c, s, o, os);
+        else if (n == 8) iadst8(c, s, o, os, mn, mx);
+        else iadst16(c, s, o, os, mn, mx);
+    } else {
+        for (int i = 0; i < n; i++) {
+            const int v = c[i * s];
+            if (n == 4) c[i * s] = v + ((v * 1697 + 2048) >> 12);
+            else if (n == 8) c[i * s] = v * 2;
+            else if (n == 16) c[i * s] = 2 * v + ((v * 1697 + 1024) >> 11);
+            else c[i * s] = v * 4;
+        }
+    }
+}
+
+/* inv_txfm_add_c, src/itx_tmpl.c:40-100 */
+static void itx_add(pixel *dst, ptrdiff_t stride, coef *coeff, int eob, int w, int h,
+                    int shift, int hk, int vk, int dconly, int bdmax)
+{
+    const int rect2 = w * 2 == h || h * 2 == w;
+    const int rnd = (1 << shift) >> 1;
+    const ptrdiff_t ds = PX(stride);
+    if (eob < dconly) {
+        int dc = coeff[0];
+        coeff[0] = 0;
+        if (rect2) dc = (dc * 181 + 128) >> 8;
+        dc = (dc * 181 + 128) >> 8;
+        dc = (dc + rnd) >> shift;
+        dc = (dc * 181 + 128 + 2048) >> 12;
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) dst[y * ds + x] = clampi(dst[y * ds + x] + dc, 0, bdmax);
+        return;
+    }
+    const int sh = mini(h, 32), sw = mini(w, 32);
+#if BITDEPTH == 8
+    const int rmin = INT16_MIN, cmin = INT16_MIN;
+#else
+    const int rmin = (int)((unsigned)~bdmax << 7), cmin = (int)((unsigned)~bdmax << 5);
+#endif
+    const int rmax = ~rmin, cmax = ~cmin;
+    int32_t *t = calloc(64 * 64, sizeof(int32_t));
+    for (int y = 0; y < sh; y++) {
+        int32_t *row = &t[y * w];
+        for (int x = 0; x < sw; x++)
+            row[x] = rect2 ? (coeff[y + x * sh] * 181 + 128) >> 8 : coeff[y + x * sh];
+        tx1d(hk, w, row, 1, rmin, rmax);
+    }
+    memset(coeff, 0, sizeof(*coeff) * sw * sh);
+    for (int i = 0; i < w * sh; i++) t[i] = clampi((t[i] + rnd) >> shift, cmin, cmax);
+    for (int x = 0; x < w; x++) tx1d(vk, h, &t[x], w, cmin, cmax);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            dst[y * ds + x] = clampi(dst[y * ds + x] + ((t[y * w + x] + 8) >> 4), 0, bdmax);
+    free(t);
+}
+
+/* inv_txfm_add_wht_wht_4x4_c, src/itx_tmpl.c:166-185 */
+static void wht4(int32_t *c, ptrdiff_t s)
+{
+    const int a = c[0], b = c[s], cc = c[2 * s], d = c[3 * s];
+    const int t0 = a + b, t2 = cc - d, t4 = (t0 - t2) >> 1, t3 = t4 - d, t1 = t4 - b;
+    c[0] = t0 - t3; c[s] = t3; c[2 * s] = t1; c[3 * s] = t2 + t1;
+}
+static void itx_wht_wht_4x4(pixel *dst, ptrdiff_t stride, coef *coeff, int eob BDPARAM)
+{
+    BD_DECL
+    int32_t t[16];
+    for (int y = 0; y < 4; y++) {
+        for (int x = 0; x < 4; x++) t[y * 4 + x] = coeff[y + x * 4] >> 2;
+        wht4(&t[y * 4], 1);
+    }
+    memset(coeff, 0, sizeof(*coeff) * 16);
+    for (int x = 0; x < 4; x++) wht4(&t[x], 4);
+    for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++)
+            dst[y * PX(stride) + x] = clampi(dst[y * PX(stride) + x] + t[y * 4 + x], 0, bdmax_);
+}
+
+/* one table entry per (size, type): the 1-D kinds come from the type name,
+ * first word vertical, second horizontal (src/itx_tmpl.c:210-242) */
+typedef struct { int w, h, shift; } TxDim;
+static const TxDim txdim[DGPU_N_RECT_TX_SIZES] = {
+    [DGPU_TX_4X4] = { 4, 4, 0 },     [DGPU_TX_8X8] = { 8, 8, 1 },
+    [DGPU_TX_16X16] = { 16, 16, 2 }, [DGPU_TX_32X32] = { 32, 32, 2 },
+    [DGPU_TX_64X64] = { 64, 64, 2 }, [DGPU_RTX_4X8] = { 4, 8, 0 },
+    [DGPU_RTX_8X4] = { 8, 4, 0 },    [DGPU_RTX_8X16] = { 8, 16, 1 },
+    [DGPU_RTX_16X8] = { 16, 8, 1 },  [DGPU_RTX_16X32] = { 16, 32, 1 },
+    [DGPU_RTX_32X16] = { 32, 16, 1 }, [DGPU_RTX_32X64] = { 32, 64, 1 },
+    [DGPU_RTX_64X32] = { 64, 32, 1 }, [DGPU_RTX_4X16] = { 4, 16, 1 },
+    [DGPU_RTX_16X4] = { 16, 4, 1 },  [DGPU_RTX_8X32] = { 8, 32, 2 },
+    [DGPU_RTX_32X8] = { 32, 8, 2 },  [DGPU_RTX_16X64] = { 16, 64, 2 },
+    [DGPU_RTX_64X16] = { 64, 16, 2 },
+};
+/* {vertical, horizontal} kinds per TxfmType */
+static const uint8_t txkinds[16][2] = {
+    [DGPU_DCT_DCT] = { K_DCT, K_DCT },           [DGPU_ADST_DCT] = { K_ADST, K_DCT },
+    [DGPU_DCT_ADST] = { K_DCT, K_ADST },         [DGPU_ADST_ADST] = { K_ADST, K_ADST },
+    [DGPU_FLIPADST_DCT] = { K_FLIPADST, K_DCT }, [DGPU_DCT_FLIPADST] = { K_DCT, K_FLIPADST },
+    [DGPU_FLIPADST_FLIPADST] = { K_FLIPADST, K_FLIPADST },
+    [DGPU_ADST_FLIPADST] = { K_ADST, K_FLIPADST }, [DGPU_FLIPADST_ADST] = { K_FLIPADST, K_ADST },
+    [DGPU_IDTX] = { K_IDENTITY, K_IDENTITY },    [DGPU_V_DCT] = { K_DCT, K_IDENTITY },
+    [DGPU_H_DCT] = { K_IDENTITY, K_DCT },        [DGPU_V_ADST] = { K_ADST, K_IDENTITY },
+    [DGPU_H_ADST] = { K_IDENTITY, K_ADST },      [DGPU_V_FLIPADST] = { K_FLIPADST, K_IDENTITY },
+    [DGPU_H_FLIPADST] = { K_IDENTITY, K_FLIPADST },
+};
+
+#define ITX_FN(tx, tp)                                                          \
+static void itx_##tx##_##tp(pixel *d, ptrdiff_t s, coef *c, int eob BDPARAM)    \
+{ BD_DECL itx_add(d, s, c, eob, txdim[tx].w, txdim[tx].h, txdim[tx].shift,      \
+                  txkinds[tp][1], txkinds[tp][0], tp == DGPU_DCT_DCT, bdmax_); }
+#define ITX_ALL_TYPES(tx) \
+    ITX_FN(tx, 0) ITX_FN(tx, 1) ITX_FN(tx, 2) ITX_FN(tx, 3) ITX_FN(tx, 4) ITX_FN(tx, 5) \
+    ITX_FN(tx, 6) ITX_FN(tx, 7) ITX_FN(tx, 8) ITX_FN(tx, 9) ITX_FN(tx, 10) ITX_FN(tx, 11) \
+    ITX_FN(tx, 12) ITX_FN(tx, 13) ITX_FN(tx, 14) ITX_FN(tx, 15)
+ITX_ALL_TYPES(0) ITX_ALL_TYPES(1) ITX_ALL_TYPES(2) ITX_ALL_TYPES(3) ITX_ALL_TYPES(4)
+ITX_ALL_TYPES(5) ITX_ALL_TYPES(6) ITX_ALL_TYPES(7) ITX_ALL_TYPES(8) ITX_ALL_TYPES(9)
+ITX_ALL_TYPES(10) ITX_ALL_TYPES(11) ITX_ALL_TYPES(12) ITX_ALL_TYPES(13) ITX_ALL_TYPES(14)
+ITX_ALL_TYPES(15) ITX_ALL_TYPES(16) ITX_ALL_TYPES(17) ITX_ALL_TYPES(18)
+
+#define ROW(tx) { itx_##tx##_0, itx_##tx##_1, itx_##tx##_2, itx_##tx##_3, itx_##tx##_4,  \
+    itx_##tx##_5, itx_##tx##_6, itx_##tx##_7, itx_##tx##_8, itx_##tx##_9, itx_##tx##_10,   \
+    itx_##tx##_11, itx_##tx##_12, itx_##tx##_13, itx_##tx##_14, itx_##tx##_15 }
+typedef void (*itx_entry)(pixel *, ptrdiff_t, coef *, int BDPARAM);
+static const itx_entry itx_all[DGPU_N_RECT_TX_SIZES][16] = {
+    ROW(0), ROW(1), ROW(2), ROW(3), ROW(4), ROW(5), ROW(6), ROW(7), ROW(8), ROW(9),
+    ROW(10), ROW(11), ROW(12), ROW(13), ROW(14), ROW(15), ROW(16), ROW(17), ROW(18),
+};
+
+/* Which (size, type) pairs the reference instantiates (src/itx_tmpl.c:142-160,
+ * assign_* :201-268): 16 types for sides <= 16 with no side == 16 on both
+ * axes, 12 for 16x16, DCT_DCT + IDTX up to 32, DCT_DCT only with a 64 side. */
+int SFX(oracle_itx_supported)(int tx, int tp)
+{
+    if (tp == DGPU_WHT_WHT) return tx == DGPU_TX_4X4;
+    const int w = txdim[tx].w, h = txdim[tx].h, m = maxi(w, h);
+    if (m == 64) return tp == DGPU_DCT_DCT;
+    if (m == 32) return tp == DGPU_DCT_DCT || tp == DGPU_IDTX;
+    if (w == 16 && h == 16) return tp <= DGPU_H_DCT;
+    return 1;
+}
+
+/* ================================================================== init */
+
+#define CTX(kind) kind##_##BITDEPTH##bpc_t
+typedef Dav1dMCDSPContext_8bpc MC8; typedef Dav1dMCDSPContext_16bpc MC16;
+typedef Dav1dIntraPredDSPContext_8bpc IP8; typedef Dav1dIntraPredDSPContext_16bpc IP16;
+typedef Dav1dInvTxfmDSPContext_8bpc IT8; typedef Dav1dInvTxfmDSPContext_16bpc IT16;
+#if BITDEPTH == 8
+#define MCCTX MC8
+#define IPCTX IP8
+#define ITCTX IT8
+#else
+#define MCCTX MC16
+#define IPCTX IP16
+#define ITCTX IT16
+#endif
+
+/* mirrors bitfn(dav1d_mc_dsp_init), src/mc_tmpl.c:915-946 */
+void SFX(oracle_mc_dsp_init)(MCCTX *c)
+{
+#define SET(idx, name) c->mc[idx] = put_##name; c->mct[idx] = prep_##name; \
+    c->mc_scaled[idx] = put_scaled_##name; c->mct_scaled[idx] = prep_scaled_##name
+    SET(DGPU_FILTER_2D_8TAP_REGULAR, regular);
+    SET(DGPU_FILTER_2D_8TAP_REGULAR_SMOOTH, regular_smooth);
+    SET(DGPU_FILTER_2D_8TAP_REGULAR_SHARP, regular_sharp);
+    SET(DGPU_FILTER_2D_8TAP_SHARP_REGULAR, sharp_regular);
+    SET(DGPU_FILTER_2D_8TAP_SHARP_SMOOTH, sharp_smooth);
+    SET(DGPU_FILTER_2D_8TAP_SHARP, sharp);
+    SET(DGPU_FILTER_2D_8TAP_SMOOTH_REGULAR, smooth_regular);
+    SET(DGPU_FILTER_2D_8TAP_SMOOTH, smooth);
+    SET(DGPU_FILTER_2D_8TAP_SMOOTH_SHARP, smooth_sharp);
+    SET(DGPU_FILTER_2D_BILINEAR, bilin);
+#undef SET
+    c->avg = mc_avg; c->w_avg = mc_w_avg; c->mask = mc_mask;
+    c->w_mask[0] = mc_w_mask_444; c->w_mask[1] = mc_w_mask_422; c->w_mask[2] = mc_w_mask_420;
+    c->blend = blend; c->blend_v = blend_v; c->blend_h = blend_h;
+    c->warp8x8 = mc_warp8x8; c->warp8x8t = mc_warp8x8t;
+    c->emu_edge = emu_edge; c->resize = mc_resize;
+}
+
+/* mirrors bitfn(dav1d_intra_pred_dsp_init), src/ipred_tmpl.c:740-766 */
+void SFX(oracle_intra_pred_dsp_init)(IPCTX *c)
+{
+    c->intra_pred[DGPU_DC_PRED] = ipred_dc;       c->intra_pred[DGPU_DC_128_PRED] = ipred_dc_128;
+    c->intra_pred[DGPU_TOP_DC_PRED] = ipred_dc_top; c->intra_pred[DGPU_LEFT_DC_PRED] = ipred_dc_left;
+    c->intra_pred[DGPU_HOR_PRED] = ipred_h;       c->intra_pred[DGPU_VERT_PRED] = ipred_v;
+    c->intra_pred[DGPU_PAETH_PRED] = ipred_paeth; c->intra_pred[DGPU_SMOOTH_PRED] = ipred_smooth;
+    c->intra_pred[DGPU_SMOOTH_V_PRED] = ipred_smooth_v; c->intra_pred[DGPU_SMOOTH_H_PRED] = ipred_smooth_h;
+    c->intra_pred[DGPU_Z1_PRED] = ipred_z1;       c->intra_pred[DGPU_Z2_PRED] = ipred_z2;
+    c->intra_pred[DGPU_Z3_PRED] = ipred_z3;       c->intra_pred[DGPU_FILTER_PRED] = ipred_filter;
+    c->cfl_ac[0] = cfl_ac_420; c->cfl_ac[1] = cfl_ac_422; c->cfl_ac[2] = cfl_ac_444;
+    c->cfl_pred[DGPU_DC_PRED] = cfl_pred_dc;        c->cfl_pred[DGPU_DC_128_PRED] = cfl_pred_128;
+    c->cfl_pred[DGPU_TOP_DC_PRED] = cfl_pred_top;   c->cfl_pred[DGPU_LEFT_DC_PRED] = cfl_pred_left;
+    c->pal_pred = pal_pred;
+}
+
+/* mirrors bitfn(dav1d_itx_dsp_init), src/itx_tmpl.c:200-268 */
+void SFX(oracle_itx_dsp_init)(ITCTX *c, int bpc)
+{
+    (void)bpc;
+    memset(c, 0, sizeof(*c));
+    for (int tx = 0; tx < DGPU_N_RECT_TX_SIZES; tx++)
+        for (int tp = 0; tp < 16; tp++)
+            if (SFX(oracle_itx_supported)(tx, tp))
+                c->itxfm_add[tx][tp] = (void *)itx_all[tx][tp];
+    c->itxfm_add[DGPU_TX_4X4][DGPU_WHT_WHT] = itx_wht_wht_4x4;
+}

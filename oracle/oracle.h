@@ -1,0 +1,13 @@
+/* oracle.h -- entry points of the CPU restatement (oracle/dsp_ref.c).
+ * TEST INFRASTRUCTURE ONLY (see dsp_ref.c header). */
+#ifndef DAV1D_ORACLE_H
+#define DAV1D_ORACLE_H
+#include "dav1d_gpu.h"
+void oracle_mc_dsp_init_8bpc(Dav1dMCDSPContext_8bpc *c);
+void oracle_mc_dsp_init_16bpc(Dav1dMCDSPContext_16bpc *c);
+void oracle_intra_pred_dsp_init_8bpc(Dav1dIntraPredDSPContext_8bpc *c);
+void oracle_intra_pred_dsp_init_16bpc(Dav1dIntraPredDSPContext_16bpc *c);
+void oracle_itx_dsp_init_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int bpc);
+void oracle_itx_dsp_init_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc);
+int oracle_itx_supported_8bpc(int tx, int tp);
+#endif

@@ -1,0 +1,205 @@
+/*
+ * checkasm_gpu.c -- differential parity harness, the reference's checkasm
+ * strategy (tests/checkasm/checkasm.c:808-862) with the CPU oracle as
+ * func_ref and the GPU-backed DSP tables (include/dav1d_gpu.h) as func_new.
+ *
+ *   checkasm_gpu [--test=mc|ipred|itx|all] [--bpc=8|16|all] [--seed=N] [--quick]
+ *
+ * Prints one line per failing case and a summary line per function:
+ *   RESULT <name>_<bpc>bpc pass=<n> fail=<n>
+ * Exit status 0 iff every case passed.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdarg.h>
+
+#include "dav1d_gpu.h"
+#include "oracle.h"
+
+static int g_quick;
+static int g_bpc_now;
+
+/* xor128 PRNG as in tests/checkasm/checkasm.c:184-206 */
+static uint32_t xs_x, xs_y, xs_z, xs_w;
+static void rnd_seed(uint32_t s) { xs_x = s; xs_y = 362436069; xs_z = 521288629; xs_w = 88675123; }
+static uint32_t rnd(void) {
+    const uint32_t t = xs_x ^ (xs_x << 11);
+    xs_x = xs_y; xs_y = xs_z; xs_z = xs_w;
+    return xs_w = xs_w ^ (xs_w >> 19) ^ (t ^ (t >> 8));
+}
+static inline int imin(int a, int b) { return a < b ? a : b; }
+static inline int imax(int a, int b) { return a > b ? a : b; }
+static inline int ctz(unsigned v) { return __builtin_ctz(v); }
+
+#define MAXF 64
+static struct { char name[48]; long pass, fail; } g_stats[MAXF];
+static int g_nstats;
+static long g_total_fail;
+
+static void report(const char *name, int ok, const char *fmt, ...) {
+    char full[48];
+    snprintf(full, sizeof(full), "%s_%dbpc", name, g_bpc_now);
+    int i;
+    for (i = 0; i < g_nstats; i++)
+        if (!strcmp(g_stats[i].name, full)) break;
+    if (i == g_nstats) { snprintf(g_stats[i].name, 48, "%s", full); g_nstats++; }
+    if (ok) { g_stats[i].pass++; return; }
+    g_stats[i].fail++;
+    g_total_fail++;
+    if (g_stats[i].fail <= 5) {
+        va_list ap;
+        va_start(ap, fmt);
+        fprintf(stdout, "FAIL %s: ", full);
+        vfprintf(stdout, fmt, ap);
+        fprintf(stdout, "\n");
+        va_end(ap);
+    }
+}
+
+/* Z2 max_width / max_height edge cases, tests/checkasm/ipred.c:69-76 */
+static int z2_max_wh(int sz) {
+    const int n = rnd();
+    if (n & (1 << 17)) return (n & (sz - 1)) + 1;
+    if (n & (1 << 16)) return 65536;
+    return (n & 65535) + 1;
+}
+
+/* random_offset_for_edge, tests/checkasm/mc.c:648-676 */
+static void emu_offsets(int *x, int *y, int bw, int bh, int *iw, int *ih, int edge) {
+    for (int dim = 0; dim < 2; dim++) {
+        const int e1 = dim ? 1 : 4, e2 = dim ? 2 : 8;   /* TOP/BOTTOM, LEFT/RIGHT */
+        const int b = dim ? bh : bw;
+        int *i_ = dim ? ih : iw, *pos = dim ? y : x;
+        *i_ = (edge & (e1 | e2)) ? 160 : 1 + (int)(rnd() % (b - 2));
+        switch (edge & (e1 | e2)) {
+        case 0: *pos = -(1 + (int)(rnd() % (b - *i_ - 1))); break;
+        default:
+            if ((edge & (e1 | e2)) == (e1 | e2)) *pos = rnd() % (*i_ - b + 1);
+            else if (edge & e1) *pos = (*i_ - b) + 1 + rnd() % (b - 1);
+            else *pos = -(1 + (int)(rnd() % (b - 1)));
+        }
+    }
+}
+
+static int mc_h_next(int h) {  /* tests/checkasm/mc.c:43-56 */
+    switch (h) {
+    case 4: case 8: case 16: return (h * 3) >> 1;
+    case 6: case 12: case 24: return (h & (h - 1)) * 2;
+    default: return h * 2;
+    }
+}
+
+static const uint8_t g_txwh[19][2] = {
+    { 4, 4 }, { 8, 8 }, { 16, 16 }, { 32, 32 }, { 64, 64 }, { 4, 8 }, { 8, 4 }, { 8, 16 },
+    { 16, 8 }, { 16, 32 }, { 32, 16 }, { 32, 64 }, { 64, 32 }, { 4, 16 }, { 16, 4 },
+    { 8, 32 }, { 32, 8 }, { 16, 64 }, { 64, 16 } };
+static int txw(int tx) { return g_txwh[tx][0]; }
+static int txh(int tx) { return g_txwh[tx][1]; }
+
+/* Coefficients for a residual block: float forward transform of uniform
+ * residuals (the idea of tests/checkasm/itx.c:183-240, restated), then only
+ * the top-left sub-region kept so the reference's eob regions (DC-only,
+ * partial, full) are all exercised.  Returns the eob value to pass. */
+static void fdct(double *o, const double *in, int n) {
+    for (int i = 0; i < n; i++) {
+        double s = 0;
+        for (int j = 0; j < n; j++) s += in[j] * cos(M_PI * (2 * j + 1) * i / (2.0 * n));
+        o[i] = i ? s : s * M_SQRT1_2;
+    }
+}
+static void fadst(double *o, const double *in, int n) {
+    for (int i = 0; i < n; i++) {
+        double s = 0;
+        for (int j = 0; j < n; j++)
+            s += in[j] * sin(M_PI * (n == 4 ? (j + 1) * (2 * i + 1) / 9.0 : (2 * j + 1) * (2 * i + 1) / (4.0 * n)));
+        o[i] = s;
+    }
+}
+static void f1d(int kind, double *o, const double *in, int n) {
+    if (kind == 0) fdct(o, in, n);
+    else if (kind == 3) memcpy(o, in, n * sizeof(double));
+    else fadst(o, in, n);
+}
+static int gen_coefs(void *buf, int tx, int tp, int w, int h, int subsh, int bdmax, int cbytes) {
+    static const double scale[9] = { 4.0, 4.0 * M_SQRT1_2, 2.0, 2.0 * M_SQRT1_2, 1.0,
+                                     0.5 * M_SQRT1_2, 0.25, 0.125 * M_SQRT1_2, 0.0625 };
+    static const uint8_t kv[17] = { 0, 1, 0, 1, 2, 0, 2, 1, 2, 3, 0, 3, 1, 3, 2, 3, 0 };
+    static const uint8_t kh[17] = { 0, 0, 1, 1, 0, 2, 2, 2, 1, 3, 3, 0, 3, 1, 3, 2, 0 };
+    double res[64 * 64], tmp[64 * 64], col[64], out[64];
+    const int sw = imin(w, 32), sh = imin(h, 32);
+    const double sc = scale[ctz(w * h) - 4];
+    for (int i = 0; i < w * h; i++) res[i] = (int)(rnd() & (2 * bdmax + 1)) - bdmax;
+    for (int y = 0; y < h; y++) f1d(kh[tp], &tmp[y * w], &res[y * w], w);
+    int32_t c[32 * 32];
+    for (int x = 0; x < w; x++) {
+        for (int y = 0; y < h; y++) col[y] = tmp[y * w + x] * sc;
+        f1d(kv[tp], out, col, h);
+        if (x < sw)
+            for (int y = 0; y < sh; y++) c[y + x * sh] = (int)floor(out[y] + 0.5);
+    }
+    /* occasionally push coefficients to extremes to exercise the clips */
+    if ((rnd() & 15) == 0)
+        for (int i = 0; i < sw * sh; i++) c[i] = (int)(rnd() % 65536) - 32768;
+    int eob;
+    if (subsh == 0) {
+        for (int i = 1; i < sw * sh; i++) c[i] = 0;
+        eob = (tp == DGPU_DCT_DCT) ? 0 : 1;
+        if (tp == DGPU_DCT_DCT && (rnd() & 1)) eob = 1;  /* DC-only coefs via the full path */
+    } else {
+        const int lim = imin(subsh * 8, 32);
+        const int lx = 1 + rnd() % imin(lim, sw), ly = 1 + rnd() % imin(lim, sh);
+        for (int x = 0; x < sw; x++)
+            for (int y = 0; y < sh; y++)
+                if (x >= lx || y >= ly) c[y + x * sh] = 0;
+        eob = 1 + rnd() % (lx * ly);
+    }
+    if (tp == DGPU_WHT_WHT) eob = 1;
+    for (int i = sw * sh; i < 32 * 32; i++) c[i] = (int)(rnd() & 0xffff) - 0x8000;
+    if (cbytes == 2) {
+        int16_t *o = buf;
+        for (int i = 0; i < 32 * 32; i++) o[i] = (int16_t)(c[i] < -32768 ? -32768 : c[i] > 32767 ? 32767 : c[i]);
+    } else {
+        memcpy(buf, c, sizeof(c));
+    }
+    return eob;
+}
+
+#define BITDEPTH 8
+#include "checkasm_gpu_tmpl.c"
+#undef BITDEPTH
+#define BITDEPTH 16
+#include "checkasm_gpu_tmpl.c"
+#undef BITDEPTH
+
+int main(int argc, char **argv) {
+    const char *test = "all";
+    int bpc = 0;
+    uint32_t seed = 1;
+    for (int i = 1; i < argc; i++) {
+        if (!strncmp(argv[i], "--test=", 7)) test = argv[i] + 7;
+        else if (!strncmp(argv[i], "--bpc=", 6)) bpc = strcmp(argv[i] + 6, "all") ? atoi(argv[i] + 6) : 0;
+        else if (!strncmp(argv[i], "--seed=", 7)) seed = (uint32_t)strtoul(argv[i] + 7, NULL, 0);
+        else if (!strcmp(argv[i], "--quick")) g_quick = 1;
+        else { fprintf(stderr, "unknown option %s\n", argv[i]); return 2; }
+    }
+    if (dav1d_gpu_device_count() <= 0) {
+        fprintf(stderr, "checkasm_gpu: no GPU device\n");
+        return 3;
+    }
+    printf("checkasm_gpu %s seed=%u quick=%d\n", dav1d_gpu_version(), seed, g_quick);
+    const int all = !strcmp(test, "all");
+    for (int b = 8; b <= 16; b += 8) {
+        if (bpc && bpc != b) continue;
+        g_bpc_now = b;
+        if (all || !strcmp(test, "mc")) { rnd_seed(seed); b == 8 ? check_mc_8bpc() : check_mc_16bpc(); }
+        if (all || !strcmp(test, "ipred")) { rnd_seed(seed); b == 8 ? check_ipred_8bpc() : check_ipred_16bpc(); }
+        if (all || !strcmp(test, "itx")) { rnd_seed(seed); b == 8 ? check_itx_8bpc() : check_itx_16bpc(); }
+    }
+    for (int i = 0; i < g_nstats; i++)
+        printf("RESULT %s pass=%ld fail=%ld\n", g_stats[i].name, g_stats[i].pass, g_stats[i].fail);
+    printf("TOTAL fail=%ld\n", g_total_fail);
+    return g_total_fail ? 1 : 0;
+}

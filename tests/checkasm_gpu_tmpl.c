@@ -1,0 +1,399 @@
+/*
+ * checkasm_gpu_tmpl.c -- per-bitdepth body of the differential harness.
+ * Included twice from checkasm_gpu.c with BITDEPTH 8 / 16.
+ *
+ * Mirrors the reference's checkasm iteration spaces
+ * (tests/checkasm/mc.c:58-723, ipred.c:77-283, itx.c:243-318): every
+ * function pointer of the GPU tables is called on the same pseudo-random
+ * inputs as the oracle's entry, outputs compared byte-exactly including an
+ * 8-pixel guard band (checkasm.c:963-1032) and, for itx, the zeroed
+ * coefficient buffer (itx.c:294-295).
+ */
+#if BITDEPTH == 8
+#define pixel uint8_t
+#define coef int16_t
+#define BD(x) x##_8bpc
+#define HBD_ARG(v)
+#define BDMAX_RAND() 0xff
+#else
+#define pixel uint16_t
+#define coef int32_t
+#define BD(x) x##_16bpc
+#define HBD_ARG(v) , v
+#define BDMAX_RAND() ((rnd() & 1) ? 0x3ff : 0xfff)
+#endif
+
+typedef struct {
+    pixel *buf, *p;   /* p = origin inside the guard band */
+    ptrdiff_t stride; /* bytes */
+    int w, h;
+} BD(Rect);
+
+static BD(Rect) BD(rect_alloc)(int w, int h) {
+    BD(Rect) r;
+    const int pw = ((w + 16) * (int)sizeof(pixel) + 63) & ~63;
+    r.stride = pw;
+    r.buf = aligned_alloc(64, (size_t)pw * (h + 16));
+    r.p = (pixel *)((uint8_t *)r.buf + 8 * pw + 8 * sizeof(pixel));
+    r.w = w; r.h = h;
+    return r;
+}
+static void BD(rect_clear)(BD(Rect) *r) { memset(r->buf, 0x99, (size_t)r->stride * (r->h + 16)); }
+static int BD(rect_eq)(const BD(Rect) *a, const BD(Rect) *b) {
+    return !memcmp(a->buf, b->buf, (size_t)a->stride * (a->h + 16));
+}
+static void BD(rect_fill)(BD(Rect) *a, BD(Rect) *b, int w, int h, int bdmax) {
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const pixel v = rnd() & bdmax;
+            a->p[y * (a->stride / sizeof(pixel)) + x] = v;
+            b->p[y * (b->stride / sizeof(pixel)) + x] = v;
+        }
+}
+
+
+static void BD(check_mc)(void) {
+    BD(Dav1dMCDSPContext) ref, gpu;
+    BD(oracle_mc_dsp_init)(&ref);
+    BD(dav1d_mc_dsp_init)(&gpu);
+    pixel *src_buf = malloc(sizeof(pixel) * 263 * 263);
+    BD(Rect) c_dst = BD(rect_alloc)(128, 128), a_dst = BD(rect_alloc)(128, 128);
+    int16_t *ct = malloc(2 * 128 * 128), *at = malloc(2 * 128 * 128);
+    int16_t *tmp[2] = { malloc(2 * 128 * 128), malloc(2 * 128 * 128) };
+    uint8_t *mask = malloc(128 * 128), *cm = malloc(128 * 128), *am = malloc(128 * 128);
+
+    /* mc (put), tests/checkasm/mc.c:58-112 */
+    for (int f = 0; f < DGPU_N_2D_FILTERS; f++)
+        for (int w = 2; w <= 128; w <<= 1)
+            for (int mxy = 0; mxy < 4; mxy++) {
+                const int h_min = w <= 32 ? 2 : w / 4, h_max = imax(imin(w * 4, 128), 32);
+                for (int h = h_min; h <= h_max; h = mc_h_next(h)) {
+                    if (g_quick && (rnd() & 3)) continue;
+                    const int mx = (mxy & 1) ? rnd() % 15 + 1 : 0, my = (mxy & 2) ? rnd() % 15 + 1 : 0;
+                    const int bdmax = BDMAX_RAND();
+                    for (int i = 0; i < 135 * 135; i++) src_buf[i] = rnd() & bdmax;
+                    const pixel *src = src_buf + 135 * 3 + 3;
+                    BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+                    ref.mc[f](c_dst.p, c_dst.stride, src, 135 * sizeof(pixel), w, h, mx, my HBD_ARG(bdmax));
+                    gpu.mc[f](a_dst.p, a_dst.stride, src, 135 * sizeof(pixel), w, h, mx, my HBD_ARG(bdmax));
+                    report("mc", BD(rect_eq)(&c_dst, &a_dst), "f%d w%d h%d mx%d my%d", f, w, h, mx, my);
+                }
+            }
+    /* mct (prep) with the worst-case corner pattern, mc.c:114-167 */
+    for (int f = 0; f < DGPU_N_2D_FILTERS; f++)
+        for (int w = 4; w <= 128; w <<= 1)
+            for (int mxy = 0; mxy < 4; mxy++)
+                for (int h = imax(w / 4, 4); h <= imin(w * 4, 128); h <<= 1) {
+                    if (g_quick && (rnd() & 3)) continue;
+                    const int mx = (mxy & 1) ? rnd() % 15 + 1 : 0, my = (mxy & 2) ? rnd() % 15 + 1 : 0;
+                    const int bdmax = BDMAX_RAND();
+                    static const int8_t pat[8] = { -1, 0, -1, 0, 0, -1, 0, -1 };
+                    const int sign = -(rnd() & 1);
+                    for (int y = 0; y < 135; y++)
+                        for (int x = 0; x < 135; x++)
+                            src_buf[135 * y + x] = ((x | y) < 8 ? (pat[x] ^ pat[y] ^ sign) : (int)rnd()) & bdmax;
+                    const pixel *src = src_buf + 135 * 3 + 3;
+                    memset(ct, 0x55, 2 * 128 * 128); memset(at, 0x55, 2 * 128 * 128);
+                    ref.mct[f](ct, src, 135 * sizeof(pixel), w, h, mx, my HBD_ARG(bdmax));
+                    gpu.mct[f](at, src, 135 * sizeof(pixel), w, h, mx, my HBD_ARG(bdmax));
+                    report("mct", !memcmp(ct, at, 2 * 128 * 128), "f%d w%d h%d mx%d my%d", f, w, h, mx, my);
+                }
+    /* scaled put / prep, mc.c:169-276 */
+    for (int f = 0; f < DGPU_N_2D_FILTERS; f++)
+        for (int w = 2; w <= 128; w <<= 1)
+            for (int p = 0; p < 3; p++) {
+                const int h_min = w <= 32 ? 2 : w / 4, h_max = imax(imin(w * 4, 128), 32);
+                for (int h = h_min; h <= h_max; h = mc_h_next(h)) {
+                    if (g_quick && (rnd() & 7)) continue;
+                    const int mx = rnd() % 1024, my = rnd() % 1024, dx = rnd() % 2048 + 1;
+                    const int dy = !p ? (int)(rnd() % 2048 + 1) : p << 10;
+                    const int bdmax = BDMAX_RAND();
+                    for (int i = 0; i < 263 * 263; i++) src_buf[i] = rnd() & bdmax;
+                    const pixel *src = src_buf + 263 * 3 + 3;
+                    BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+                    ref.mc_scaled[f](c_dst.p, c_dst.stride, src, 263 * sizeof(pixel), w, h, mx, my, dx, dy HBD_ARG(bdmax));
+                    gpu.mc_scaled[f](a_dst.p, a_dst.stride, src, 263 * sizeof(pixel), w, h, mx, my, dx, dy HBD_ARG(bdmax));
+                    report("mc_scaled", BD(rect_eq)(&c_dst, &a_dst), "f%d w%d h%d dy%d", f, w, h, dy);
+                    if (w >= 4 && h >= imax(w / 4, 4) && h <= imin(w * 4, 128)) {
+                        memset(ct, 0x55, 2 * 128 * 128); memset(at, 0x55, 2 * 128 * 128);
+                        ref.mct_scaled[f](ct, src, 263 * sizeof(pixel), w, h, mx, my, dx, dy HBD_ARG(bdmax));
+                        gpu.mct_scaled[f](at, src, 263 * sizeof(pixel), w, h, mx, my, dx, dy HBD_ARG(bdmax));
+                        report("mct_scaled", !memcmp(ct, at, 2 * 128 * 128), "f%d w%d h%d dy%d", f, w, h, dy);
+                    }
+                }
+            }
+    /* compound blends on real mct[SHARP] output, mc.c:278-445 */
+    for (int kind = 0; kind < 6; kind++)
+        for (int w = 4; w <= 128; w <<= 1)
+            for (int h = imax(w / 4, 4); h <= imin(w * 4, 128); h <<= 1) {
+                if (g_quick && (rnd() & 1)) continue;
+                const int bdmax = BDMAX_RAND();
+                for (int i = 0; i < 2; i++) {
+                    for (int k = 0; k < 135 * 135; k++) src_buf[k] = rnd() & bdmax;
+                    ref.mct[DGPU_FILTER_2D_8TAP_SHARP](tmp[i], src_buf + 135 * 3 + 3, 135 * sizeof(pixel),
+                                                      128, 128, 8, 8 HBD_ARG(bdmax));
+                }
+                for (int i = 0; i < 128 * 128; i++) mask[i] = rnd() % 65;
+                BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+                const char *nm;
+                int ok;
+                if (kind == 0) {
+                    nm = "avg";
+                    ref.avg(c_dst.p, c_dst.stride, tmp[0], tmp[1], w, h HBD_ARG(bdmax));
+                    gpu.avg(a_dst.p, a_dst.stride, tmp[0], tmp[1], w, h HBD_ARG(bdmax));
+                    ok = BD(rect_eq)(&c_dst, &a_dst);
+                } else if (kind == 1) {
+                    nm = "w_avg";
+                    const int wt = rnd() % 15 + 1;
+                    ref.w_avg(c_dst.p, c_dst.stride, tmp[0], tmp[1], w, h, wt HBD_ARG(bdmax));
+                    gpu.w_avg(a_dst.p, a_dst.stride, tmp[0], tmp[1], w, h, wt HBD_ARG(bdmax));
+                    ok = BD(rect_eq)(&c_dst, &a_dst);
+                } else if (kind == 2) {
+                    nm = "mask";
+                    ref.mask(c_dst.p, c_dst.stride, tmp[0], tmp[1], w, h, mask HBD_ARG(bdmax));
+                    gpu.mask(a_dst.p, a_dst.stride, tmp[0], tmp[1], w, h, mask HBD_ARG(bdmax));
+                    ok = BD(rect_eq)(&c_dst, &a_dst);
+                } else {
+                    static const char *const wn[3] = { "w_mask_444", "w_mask_422", "w_mask_420" };
+                    const int i = kind - 3, ssh = i > 0, ssv = i > 1, sign = rnd() & 1;
+                    nm = wn[i];
+                    memset(cm, 0x77, 128 * 128); memset(am, 0x77, 128 * 128);
+                    ref.w_mask[i](c_dst.p, c_dst.stride, tmp[0], tmp[1], w, h, cm, sign HBD_ARG(bdmax));
+                    gpu.w_mask[i](a_dst.p, a_dst.stride, tmp[0], tmp[1], w, h, am, sign HBD_ARG(bdmax));
+                    ok = BD(rect_eq)(&c_dst, &a_dst) && !memcmp(cm, am, (w >> ssh) * (h >> ssv));
+                }
+                report(nm, ok, "w%d h%d", w, h);
+            }
+    /* blend / blend_v / blend_h, mc.c:447-563 */
+    {
+        pixel *tb = malloc(sizeof(pixel) * 128 * 128);
+        for (int kind = 0; kind < 3; kind++) {
+            const int wmin = kind == 0 ? 4 : 2, wmax = kind == 1 ? 32 : kind == 0 ? 32 : 128;
+            for (int w = wmin; w <= wmax; w <<= 1) {
+                int hmin, hmax;
+                if (kind == 0) { hmin = imax(w / 2, 4); hmax = imin(w * 2, 32); }
+                else if (kind == 1) { hmin = 2; hmax = w == 2 ? 64 : 128; }
+                else { hmin = w == 128 ? 4 : 2; hmax = 32; }
+                for (int h = hmin; h <= hmax; h <<= 1) {
+                    const int bdmax = BDMAX_RAND();
+                    for (int i = 0; i < 128 * 128; i++) { tb[i] = rnd() & bdmax; mask[i] = rnd() % 65; }
+                    BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+                    BD(rect_fill)(&c_dst, &a_dst, w, h, bdmax);
+                    if (kind == 0) {
+                        ref.blend(c_dst.p, c_dst.stride, tb, w, h, mask);
+                        gpu.blend(a_dst.p, a_dst.stride, tb, w, h, mask);
+                    } else if (kind == 1) {
+                        ref.blend_v(c_dst.p, c_dst.stride, tb, w, h);
+                        gpu.blend_v(a_dst.p, a_dst.stride, tb, w, h);
+                    } else {
+                        ref.blend_h(c_dst.p, c_dst.stride, tb, w, h);
+                        gpu.blend_h(a_dst.p, a_dst.stride, tb, w, h);
+                    }
+                    static const char *const bn[3] = { "blend", "blend_v", "blend_h" };
+                    report(bn[kind], BD(rect_eq)(&c_dst, &a_dst), "w%d h%d", w, h);
+                }
+            }
+        }
+        free(tb);
+    }
+    /* warp8x8 / warp8x8t, mc.c:565-641 */
+    for (int it = 0; it < (g_quick ? 16 : 128); it++) {
+        int16_t abcd[4];
+        const int mx = (rnd() & 0x1fff) - 0xa00, my = (rnd() & 0x1fff) - 0xa00;
+        const int bdmax = BDMAX_RAND();
+        for (int i = 0; i < 4; i++) abcd[i] = (rnd() & 0x1fff) - 0xa00;
+        for (int i = 0; i < 15 * 15; i++) src_buf[i] = rnd() & bdmax;
+        const pixel *src = src_buf + 15 * 3 + 3;
+        BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+        ref.warp8x8(c_dst.p, c_dst.stride, src, 15 * sizeof(pixel), abcd, mx, my HBD_ARG(bdmax));
+        gpu.warp8x8(a_dst.p, a_dst.stride, src, 15 * sizeof(pixel), abcd, mx, my HBD_ARG(bdmax));
+        report("warp8x8", BD(rect_eq)(&c_dst, &a_dst), "it%d", it);
+        memset(ct, 0x55, 2 * 128 * 128); memset(at, 0x55, 2 * 128 * 128);
+        ref.warp8x8t(ct, 8, src, 15 * sizeof(pixel), abcd, mx, my HBD_ARG(bdmax));
+        gpu.warp8x8t(at, 8, src, 15 * sizeof(pixel), abcd, mx, my HBD_ARG(bdmax));
+        report("warp8x8t", !memcmp(ct, at, 2 * 8 * 8), "it%d", it);
+    }
+    /* emu_edge, all 15 edge cases, mc.c:643-721 */
+    {
+        pixel *esrc = malloc(sizeof(pixel) * 160 * 160);
+        pixel *ce = malloc(sizeof(pixel) * 135 * 192), *ae = malloc(sizeof(pixel) * 135 * 192);
+        for (int i = 0; i < 160 * 160; i++) esrc[i] = rnd() & ((1U << BITDEPTH) - 1);
+        for (int w = 4; w <= 128; w <<= 1)
+            for (int h = imax(w / 4, 4); h <= imin(w * 4, 128); h <<= 1)
+                for (int edge = 0; edge < 0xf; edge++) {
+                    const int bw = w + (rnd() & 7), bh = h + (rnd() & 7);
+                    int x, y, iw, ih;
+                    emu_offsets(&x, &y, bw, bh, &iw, &ih, edge);
+                    memset(ce, 0x99, sizeof(pixel) * 135 * 192); memset(ae, 0x99, sizeof(pixel) * 135 * 192);
+                    ref.emu_edge(bw, bh, iw, ih, x, y, ce, 192 * sizeof(pixel), esrc, 160 * sizeof(pixel));
+                    gpu.emu_edge(bw, bh, iw, ih, x, y, ae, 192 * sizeof(pixel), esrc, 160 * sizeof(pixel));
+                    report("emu_edge", !memcmp(ce, ae, sizeof(pixel) * 135 * 192), "w%d h%d edge%d", bw, bh, edge);
+                }
+        free(esrc); free(ce); free(ae);
+    }
+    /* resize, mc.c:723-776 */
+    {
+        pixel *rsrc = malloc(sizeof(pixel) * 512 * 64);
+        BD(Rect) cr = BD(rect_alloc)(1024, 64), ar = BD(rect_alloc)(1024, 64);
+        for (int it = 0; it < (g_quick ? 4 : 16); it++) {
+            const int bdmax = BDMAX_RAND();
+            for (int i = 0; i < 512 * 64; i++) rsrc[i] = rnd() & bdmax;
+            const int w_den = 9 + (rnd() & 7);
+            const int src_w = 16 + (rnd() % (512 - 16 + 1));
+            const int dst_w = w_den * src_w >> 3;
+            const int dx = ((src_w << 14) + (dst_w >> 1)) / dst_w;
+            const int err = dst_w * dx - (src_w << 14);
+            const int mx0 = ((-((dst_w - src_w) << 13) + (dst_w >> 1)) / dst_w + 128 - (err >> 1)) & 0x3fff;
+            BD(rect_clear)(&cr); BD(rect_clear)(&ar);
+            ref.resize(cr.p, cr.stride, rsrc, 512 * sizeof(pixel), dst_w, 64, src_w, dx, mx0 HBD_ARG(bdmax));
+            gpu.resize(ar.p, ar.stride, rsrc, 512 * sizeof(pixel), dst_w, 64, src_w, dx, mx0 HBD_ARG(bdmax));
+            report("resize", BD(rect_eq)(&cr, &ar), "src_w%d dst_w%d", src_w, dst_w);
+        }
+        free(cr.buf); free(ar.buf); free(rsrc);
+    }
+    free(src_buf); free(c_dst.buf); free(a_dst.buf); free(ct); free(at);
+    free(tmp[0]); free(tmp[1]); free(mask); free(cm); free(am);
+}
+
+static void BD(check_ipred)(void) {
+    BD(Dav1dIntraPredDSPContext) ref, gpu;
+    BD(oracle_intra_pred_dsp_init)(&ref);
+    BD(dav1d_intra_pred_dsp_init)(&gpu);
+    BD(Rect) c_dst = BD(rect_alloc)(64, 64), a_dst = BD(rect_alloc)(64, 64);
+    pixel tl_buf[257], *const tl = tl_buf + 128;
+    static const uint8_t z_angles[27] = { 3, 6, 9, 14, 17, 20, 23, 26, 29, 32, 36, 39, 42, 45,
+                                          48, 51, 54, 58, 61, 64, 67, 70, 73, 76, 81, 84, 87 };
+    /* intra_pred, ipred.c:77-155 */
+    for (int mode = 0; mode < DGPU_N_IMPL_INTRA_PRED_MODES; mode++) {
+        const int bpc_lo = (mode == DGPU_FILTER_PRED && BITDEPTH == 16) ? 10 : BITDEPTH;
+        const int bpc_hi = (mode == DGPU_FILTER_PRED && BITDEPTH == 16) ? 12 : BITDEPTH;
+        for (int bpc = bpc_lo; bpc <= bpc_hi; bpc += 2)
+            for (int w = 4; w <= (mode == DGPU_FILTER_PRED ? 32 : 64); w <<= 1)
+                for (int h = imax(w / 4, 4); h <= imin(w * 4, mode == DGPU_FILTER_PRED ? 32 : 64); h <<= 1) {
+                    const int iters = (mode >= DGPU_Z1_PRED && mode <= DGPU_Z3_PRED) ? (g_quick ? 5 : 20) : 1;
+                    for (int it = 0; it < iters; it++) {
+                        int a = 0, maxw = 0, maxh = 0;
+                        if (mode >= DGPU_Z1_PRED && mode <= DGPU_Z3_PRED) {
+                            a = (90 * (mode - DGPU_Z1_PRED) + z_angles[rnd() % 27]) | (rnd() & 0x600);
+                            if (mode == DGPU_Z2_PRED) { maxw = z2_max_wh(w); maxh = z2_max_wh(h); }
+                        } else if (mode == DGPU_FILTER_PRED) {
+                            a = (rnd() % 5) | (rnd() & ~511);
+                        }
+                        const int bdmax = bpc == 16 ? BDMAX_RAND() : (1 << bpc) - 1;
+                        for (int i = -2 * h; i <= 2 * w; i++) tl[i] = rnd() & bdmax;
+                        BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+                        ref.intra_pred[mode](c_dst.p, c_dst.stride, tl, w, h, a, maxw, maxh HBD_ARG(bdmax));
+                        gpu.intra_pred[mode](a_dst.p, a_dst.stride, tl, w, h, a, maxw, maxh HBD_ARG(bdmax));
+                        report("intra_pred", BD(rect_eq)(&c_dst, &a_dst), "mode%d w%d h%d a%d(0x%03x) maxw%d maxh%d",
+                               mode, w, h, a & 511, a & 0x600, maxw, maxh);
+                    }
+                }
+    }
+    /* cfl_ac, ipred.c:157-205 */
+    {
+        int16_t cac[32 * 32], aac[32 * 32];
+        pixel luma[32 * 32];
+        for (int layout = 1; layout <= 3; layout++) {
+            const int ssv = layout == 1, ssh = layout != 3;
+            const int hstep = 2 >> ssh, vstep = 2 >> ssv;
+            for (int w = 4; w <= (32 >> ssh); w <<= 1)
+                for (int h = imax(w / 4, 4); h <= imin(w * 4, 32 >> ssv); h <<= 1)
+                    for (int wp = imax((w >> 2) - hstep, 0); wp >= 0; wp -= hstep)
+                        for (int hp = imax((h >> 2) - vstep, 0); hp >= 0; hp -= vstep) {
+                            const int bdmax = BDMAX_RAND();
+                            for (int y = 0; y < (h << ssv); y++)
+                                for (int x = 0; x < (w << ssh); x++) luma[y * 32 + x] = rnd() & bdmax;
+                            memset(cac, 0x55, sizeof(cac)); memset(aac, 0x55, sizeof(aac));
+                            ref.cfl_ac[layout - 1](cac, luma, 32 * sizeof(pixel), wp, hp, w, h);
+                            gpu.cfl_ac[layout - 1](aac, luma, 32 * sizeof(pixel), wp, hp, w, h);
+                            report("cfl_ac", !memcmp(cac, aac, sizeof(cac)), "layout%d w%d h%d wp%d hp%d",
+                                   layout, w, h, wp, hp);
+                        }
+        }
+    }
+    /* cfl_pred, ipred.c:207-258 */
+    {
+        int16_t ac[32 * 32];
+        for (int mode = 0; mode <= DGPU_DC_128_PRED; mode += 1 + 2 * !mode)
+            for (int w = 4; w <= 32; w <<= 1)
+                for (int h = imax(w / 4, 4); h <= imin(w * 4, 32); h <<= 1) {
+                    const int bdmax = BDMAX_RAND();
+                    const int alpha = ((rnd() & 15) + 1) * (1 - (rnd() & 2));
+                    for (int i = -2 * h; i <= 2 * w; i++) tl[i] = rnd() & bdmax;
+                    int avg = w * h >> 1;
+                    for (int i = 0; i < w * h; i++) avg += ac[i] = rnd() & (bdmax << 3);
+                    avg /= w * h;
+                    for (int i = 0; i < w * h; i++) ac[i] -= avg;
+                    BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+                    ref.cfl_pred[mode](c_dst.p, c_dst.stride, tl, w, h, ac, alpha HBD_ARG(bdmax));
+                    gpu.cfl_pred[mode](a_dst.p, a_dst.stride, tl, w, h, ac, alpha HBD_ARG(bdmax));
+                    report("cfl_pred", BD(rect_eq)(&c_dst, &a_dst), "mode%d w%d h%d", mode, w, h);
+                }
+    }
+    /* pal_pred, ipred.c:260-283 */
+    {
+        uint8_t idx[32 * 64];
+        pixel pal[8];
+        for (int w = 4; w <= 64; w <<= 1)
+            for (int h = imax(w / 4, 4); h <= imin(w * 4, 64); h <<= 1) {
+                const int bdmax = BDMAX_RAND();
+                for (int i = 0; i < 8; i++) pal[i] = rnd() & bdmax;
+                for (int i = 0; i < w * h / 2; i++) idx[i] = rnd() & 0x77;
+                BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+                ref.pal_pred(c_dst.p, c_dst.stride, pal, idx, w, h);
+                gpu.pal_pred(a_dst.p, a_dst.stride, pal, idx, w, h);
+                report("pal_pred", BD(rect_eq)(&c_dst, &a_dst), "w%d h%d", w, h);
+            }
+    }
+    free(c_dst.buf); free(a_dst.buf);
+}
+
+static void BD(check_itx)(void) {
+    BD(Dav1dInvTxfmDSPContext) ref, gpu;
+    static const uint8_t order[19] = {  /* itx.c:304-310 */
+        DGPU_TX_4X4, DGPU_RTX_4X8, DGPU_RTX_4X16, DGPU_RTX_8X4, DGPU_TX_8X8, DGPU_RTX_8X16,
+        DGPU_RTX_8X32, DGPU_RTX_16X4, DGPU_RTX_16X8, DGPU_TX_16X16, DGPU_RTX_16X32,
+        DGPU_RTX_16X64, DGPU_RTX_32X8, DGPU_RTX_32X16, DGPU_TX_32X32, DGPU_RTX_32X64,
+        DGPU_RTX_64X16, DGPU_RTX_64X32, DGPU_TX_64X64 };
+    static const uint8_t subsh_iters[5] = { 2, 2, 3, 5, 5 };
+    coef cc[32 * 32], ac[32 * 32];
+    BD(Rect) c_dst = BD(rect_alloc)(64, 64), a_dst = BD(rect_alloc)(64, 64);
+    const int bpc_lo = BITDEPTH == 16 ? 10 : 8, bpc_hi = BITDEPTH == 16 ? 12 : 8;
+    for (int bpc = bpc_lo; bpc <= bpc_hi; bpc += 2) {
+        BD(oracle_itx_dsp_init)(&ref, bpc);
+        BD(dav1d_itx_dsp_init)(&gpu, bpc);
+        int n_entries = 0;
+        for (int i = 0; i < 19; i++) {
+            const int tx = order[i], w = txw(tx), h = txh(tx);
+            const int lmax = imax(ctz(w), ctz(h)) - 2;
+            for (int tp = 0; tp < DGPU_N_TX_TYPES_PLUS_LL; tp++) {
+                if (!!ref.itxfm_add[tx][tp] != !!gpu.itxfm_add[tx][tp]) {
+                    report("itx_table", 0, "tx%d tp%d presence differs", tx, tp);
+                    continue;
+                }
+                if (!ref.itxfm_add[tx][tp]) continue;
+                n_entries++;
+                for (int subsh = 0; subsh < subsh_iters[lmax]; subsh++)
+                    for (int rep = 0; rep < (g_quick ? 1 : 4); rep++) {
+                        const int bdmax = (1 << bpc) - 1;
+                        const int eob = gen_coefs(cc, tx, tp, w, h, subsh, bdmax, sizeof(coef));
+                        memcpy(ac, cc, sizeof(cc));
+                        BD(rect_clear)(&c_dst); BD(rect_clear)(&a_dst);
+                        BD(rect_fill)(&c_dst, &a_dst, w, h, bdmax);
+                        ref.itxfm_add[tx][tp](c_dst.p, c_dst.stride, cc, eob HBD_ARG(bdmax));
+                        gpu.itxfm_add[tx][tp](a_dst.p, a_dst.stride, ac, eob HBD_ARG(bdmax));
+                        const int ok = BD(rect_eq)(&c_dst, &a_dst) && !memcmp(cc, ac, sizeof(cc));
+                        report("itx", ok, "%dx%d type%d subsh%d eob%d bpc%d", w, h, tp, subsh, eob, bpc);
+                    }
+            }
+        }
+        report("itx_table", n_entries == 156, "entries=%d (want 156) bpc%d", n_entries, bpc);
+    }
+    free(c_dst.buf); free(a_dst.buf);
+}
+
+#undef pixel
+#undef coef
+#undef BD
+#undef HBD_ARG
+#undef BDMAX_RAND
