@@ -1,0 +1,117 @@
+"""ctypes / numpy mirror of include/dav1d_gpu.h (the C-ABI boundary).
+
+Only plain pointers and sizes cross the boundary; torch is used by callers
+for device memory and streams, never in these signatures.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+# RectTxfmSize order (src/levels.h:44-78) -> (w, h)
+TX_WH = [(4, 4), (8, 8), (16, 16), (32, 32), (64, 64), (4, 8), (8, 4), (8, 16),
+         (16, 8), (16, 32), (32, 16), (32, 64), (64, 32), (4, 16), (16, 4),
+         (8, 32), (32, 8), (16, 64), (64, 16)]
+TX_INDEX = {wh: i for i, wh in enumerate(TX_WH)}
+N_TX = len(TX_WH)
+
+DCT_DCT, IDTX, H_DCT, WHT_WHT = 0, 9, 11, 16
+NO_RESIDUAL = 0xFF          # txtp value: prediction only (no inv_txfm_add)
+
+PRED_NONE, PRED_INTER, PRED_INTER_AVG, PRED_INTRA = 0, 1, 2, 3
+FILTER_2D_BILINEAR = 9
+
+(DC_PRED, VERT_PRED, HOR_PRED, LEFT_DC_PRED, TOP_DC_PRED, DC_128_PRED, Z1_PRED,
+ Z2_PRED, Z3_PRED, SMOOTH_PRED, SMOOTH_V_PRED, SMOOTH_H_PRED, PAETH_PRED,
+ FILTER_PRED) = range(14)
+
+MAX_REFS = 8
+
+
+def itx_supported(tx, tp):
+    """The reference's instantiated (size, type) pairs, src/itx_tmpl.c:142-160."""
+    if tp == WHT_WHT:
+        return tx == 0
+    w, h = TX_WH[tx]
+    m = max(w, h)
+    if m == 64:
+        return tp == DCT_DCT
+    if m == 32:
+        return tp in (DCT_DCT, IDTX)
+    if w == 16 and h == 16:
+        return tp <= H_DCT
+    return True
+
+
+# Dav1dGpuUnit, 32 bytes, with the inter / intra union as overlapping fields.
+UNIT_DTYPE = np.dtype({
+    "names": ["dst_off", "coef_off", "tx", "txtp", "plane", "pred", "nzw", "nzh",
+              "bw4", "bh4",
+              "src_off0", "src_off1", "mx0", "mx1", "my0", "my1", "filter2d", "ref0", "ref1",
+              "edge_off", "angle", "mode", "max_w", "max_h"],
+    "formats": ["<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
+                "<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
+                "<i4", "<u2", "u1", "<u2", "<u2"],
+    "offsets": [0, 4, 8, 9, 10, 11, 12, 13, 14, 15,
+                16, 20, 24, 25, 26, 27, 28, 29, 30,
+                16, 20, 22, 24, 26],
+    "itemsize": 32,
+})
+
+
+class Plane(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("stride", ctypes.c_int64),
+                ("w", ctypes.c_int32), ("h", ctypes.c_int32)]
+
+
+class FrameBatch(ctypes.Structure):
+    _fields_ = [("dst", Plane * 3),
+                ("ref", (Plane * 3) * MAX_REFS),
+                ("units", ctypes.c_void_p),
+                ("n_units", ctypes.c_int32),
+                ("class_start", ctypes.c_int32 * (N_TX + 1)),
+                ("coef", ctypes.c_void_p),
+                ("edges", ctypes.c_void_p),
+                ("bitdepth_max", ctypes.c_int32),
+                ("zero_coefs", ctypes.c_int32)]
+
+
+_LIB = None
+
+
+def lib_path():
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdav1d_gpu.so")
+
+
+def load_lib():
+    """Load the in-tree HIP library; raises (never falls back) if it is absent."""
+    global _LIB
+    if _LIB is None:
+        p = lib_path()
+        if not os.path.exists(p):
+            raise RuntimeError(f"{p} missing: build it with __graft_entry__.build() "
+                               "(there is no CPU fallback for the GPU DSP path)")
+        L = ctypes.CDLL(p)
+        L.dav1d_gpu_recon_8bpc.argtypes = [ctypes.POINTER(FrameBatch), ctypes.c_void_p]
+        L.dav1d_gpu_recon_8bpc.restype = ctypes.c_int
+        L.dav1d_gpu_recon_16bpc.argtypes = [ctypes.POINTER(FrameBatch), ctypes.c_void_p]
+        L.dav1d_gpu_recon_16bpc.restype = ctypes.c_int
+        L.dav1d_gpu_device_count.restype = ctypes.c_int
+        L.dav1d_gpu_version.restype = ctypes.c_char_p
+        L.dav1d_gpu_recon_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.dav1d_gpu_recon_lds_bytes.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+# every symbol include/dav1d_gpu.h declares
+EXPORTED_SYMBOLS = [
+    "dav1d_mc_dsp_init_8bpc", "dav1d_mc_dsp_init_16bpc",
+    "dav1d_intra_pred_dsp_init_8bpc", "dav1d_intra_pred_dsp_init_16bpc",
+    "dav1d_itx_dsp_init_8bpc", "dav1d_itx_dsp_init_16bpc",
+    "dav1d_mc_dsp_init_gpu_8bpc", "dav1d_mc_dsp_init_gpu_16bpc",
+    "dav1d_intra_pred_dsp_init_gpu_8bpc", "dav1d_intra_pred_dsp_init_gpu_16bpc",
+    "dav1d_itx_dsp_init_gpu_8bpc", "dav1d_itx_dsp_init_gpu_16bpc",
+    "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version",
+    "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc",
+]

@@ -1,0 +1,86 @@
+"""Device-resident frame batches and the launch of the fused reconstruction.
+
+torch provides device memory and the stream (plumbing only); the pixels are
+produced by libdav1d_gpu.so's HIP kernels through the C ABI
+(dav1d_gpu_recon_{8,16}bpc, include/dav1d_gpu.h).
+"""
+import ctypes
+
+import numpy as np
+
+from . import abi
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class DeviceFrame:
+    """A FrameData uploaded to one GPU, plus its output planes."""
+
+    def __init__(self, fd, device="cuda:0", zero_coefs=False):
+        import torch
+        self.torch = torch
+        self.fd = fd
+        self.device = torch.device(device)
+        dev = self.device
+        pdt = torch.uint8 if fd.cfg.bpc == 8 else torch.int16   # int16 storage for uint16 bits
+        self.units = torch.from_numpy(fd.units.view(np.uint8).copy()).to(dev)
+        cf = fd.coefs.view(np.int16 if fd.cfg.bpc == 8 else np.int32)
+        self.coefs = torch.from_numpy(cf.copy()).to(dev)
+        ed = fd.edges if fd.cfg.bpc == 8 else fd.edges.view(np.int16)
+        self.edges = torch.from_numpy(ed.copy()).to(dev)
+        self.refs = []
+        for rp in fd.refs:
+            planes = []
+            for a in rp:
+                src = a if fd.cfg.bpc == 8 else a.view(np.int16)
+                planes.append(torch.from_numpy(src.copy()).to(dev))
+            self.refs.append(planes)
+        self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fd.plane_wh]
+        self.zero_coefs = zero_coefs
+        self.batch = self._make_batch()
+        self.lib = abi.load_lib()
+
+    def _make_batch(self):
+        fd = self.fd
+        bpp = 1 if fd.cfg.bpc == 8 else 2
+        b = abi.FrameBatch()
+        for p in range(3):
+            w, h = fd.plane_wh[p]
+            b.dst[p].data = self.dst[p].data_ptr()
+            b.dst[p].stride = w * bpp
+            b.dst[p].w, b.dst[p].h = w, h
+            for r in range(len(self.refs)):
+                t = self.refs[r][p]
+                stride = t.shape[1]
+                b.ref[r][p].data = t.data_ptr() + fd.ref_origin_offset(p) * bpp
+                b.ref[r][p].stride = stride * bpp
+                b.ref[r][p].w, b.ref[r][p].h = w, h
+        b.units = self.units.data_ptr()
+        b.n_units = fd.n_units
+        for i in range(abi.N_TX + 1):
+            b.class_start[i] = int(fd.class_start[i])
+        b.coef = self.coefs.data_ptr()
+        b.edges = self.edges.data_ptr()
+        b.bitdepth_max = fd.cfg.bitdepth_max if fd.cfg.bpc == 16 else 255
+        b.zero_coefs = 1 if self.zero_coefs else 0
+        return b
+
+    def launch(self, stream=None):
+        """Enqueue one reconstruction of the whole frame on `stream`
+        (a torch.cuda.Stream; default: the current stream)."""
+        torch = self.torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        fn = self.lib.dav1d_gpu_recon_8bpc if self.fd.cfg.bpc == 8 else self.lib.dav1d_gpu_recon_16bpc
+        rc = fn(ctypes.byref(self.batch), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"dav1d_gpu_recon failed: {rc}")
+
+    def planes_host(self):
+        """Reconstructed planes as numpy arrays (uint8 / uint16)."""
+        out = []
+        for t in self.dst:
+            a = t.cpu().numpy()
+            out.append(a if self.fd.cfg.bpc == 8 else a.view(np.uint16))
+        return out

@@ -1,0 +1,356 @@
+"""Synthetic frame batches for the reconstruction hot path.
+
+A frame is tiled into square prediction blocks by a seeded quadtree over
+64x64 superblocks (luma area mix 8x8 25% / 16x16 35% / 32x32 25% / 64x64
+15%); 4:2:0 chroma blocks follow at half size.  Blocks are inter (single-ref
+put or compound 2x prep + avg, one of the 9 8-tap filter pairs, integer MV
+uniform in +-64 px, 1/16-pel fraction uniform) or intra (one of the 14
+intra_pred modes, per-transform-block edge arrays).  Every block is split
+into transform units of one size <= 32x32 (rect included); each unit gets a
+transform type valid for its size (the reference's 156-entry table) and
+coefficients from a floating-point forward transform of uniform residuals
+(the idea of tests/checkasm/itx.c:183-240), truncated to a DC-only (25%),
+partial (50%) or full (25%) coefficient region.
+
+Blocks are independent: intra edges come from an edge pool, not from
+reconstructed neighbours.  The "mc" config is
+config 2: inter only, prediction-only units (one per block, no residual).
+
+Everything here is host-side numpy; nothing is timed.
+"""
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+
+Z_ANGLES = np.array([3, 6, 9, 14, 17, 20, 23, 26, 29, 32, 36, 39, 42, 45, 48, 51, 54,
+                     58, 61, 64, 67, 70, 73, 76, 81, 84, 87], np.int32)
+
+# leaf probability at each quadtree level, giving the 15/25/35/25 area mix
+_LEVELS = [(64, 0.15), (32, 0.25 / 0.85), (16, 0.35 / 0.60), (8, 1.0)]
+
+REF_PAD = 96   # reference planes carry this many padding pixels on every side
+
+_SCALE = [4.0, 4.0 * 2 ** -0.5, 2.0, 2.0 * 2 ** -0.5, 1.0, 0.5 * 2 ** -0.5, 0.25,
+          0.125 * 2 ** -0.5, 0.0625]
+
+
+@dataclass
+class FrameConfig:
+    width: int = 3840
+    height: int = 2160
+    bpc: int = 8                  # 8 or 16 (ABI); 16 uses bitdepth_max
+    bitdepth_max: int = 255
+    kind: str = "full"            # "full" (mc + ipred + itx) or "mc" (put/avg only)
+    intra_frac: float = 0.30
+    compound_frac: float = 0.50   # of inter blocks
+    seed: int = 0x5EED0001
+
+    @property
+    def pixel_dtype(self):
+        return np.uint8 if self.bpc == 8 else np.uint16
+
+    @property
+    def coef_dtype(self):
+        return np.int16 if self.bpc == 8 else np.int32
+
+
+@dataclass
+class FrameData:
+    cfg: FrameConfig
+    units: np.ndarray
+    class_start: np.ndarray
+    coefs: np.ndarray
+    edges: np.ndarray
+    refs: list                    # [ref][plane] padded 2-D arrays
+    plane_wh: list                # [(w, h)] per plane
+    blk: np.ndarray = None        # prediction-block id of each unit (stats only)
+    stats: dict = field(default_factory=dict)
+
+    @property
+    def n_units(self):
+        return len(self.units)
+
+    def ref_origin_offset(self, plane):
+        stride = self.refs[0][plane].shape[1]
+        return REF_PAD * stride + REF_PAD
+
+
+def _partition(rng, W, H):
+    """Quadtree leaves (x, y, size) covering W x H (multiples of 8)."""
+    ys, xs = np.meshgrid(np.arange(0, H, 64), np.arange(0, W, 64), indexing="ij")
+    xs, ys = xs.ravel(), ys.ravel()
+    out = []
+    for s, p in _LEVELS:
+        inside = (xs + s <= W) & (ys + s <= H)
+        outside = (xs >= W) | (ys >= H)
+        leaf = inside & (rng.random(len(xs)) < p)
+        out.append((xs[leaf], ys[leaf], np.full(leaf.sum(), s)))
+        split = ~outside & ~leaf
+        if s == 8:
+            break
+        h = s // 2
+        sx, sy = xs[split], ys[split]
+        xs = np.concatenate([sx, sx + h, sx, sx + h])
+        ys = np.concatenate([sy, sy, sy + h, sy + h])
+    return (np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out]),
+            np.concatenate([o[2] for o in out]))
+
+
+def _dct_mat(n):
+    k = np.arange(n)[:, None]
+    j = np.arange(n)[None, :]
+    m = np.cos(np.pi * (2 * j + 1) * k / (2.0 * n))
+    m[0] *= 2 ** -0.5
+    return m
+
+
+def _adst_mat(n):
+    i = np.arange(n)[:, None]
+    j = np.arange(n)[None, :]
+    if n == 4:
+        return np.sin(np.pi * (j + 1) * (2 * i + 1) / 9.0)
+    return np.sin(np.pi * (2 * j + 1) * (2 * i + 1) / (4.0 * n))
+
+
+def _fwd_mat(kind, n):
+    if kind == 0:
+        return _dct_mat(n)
+    if kind == 3:
+        return np.eye(n)
+    return _adst_mat(n)
+
+
+# {vertical, horizontal} 1-D kinds per TxfmType (0 dct, 1 adst, 2 flipadst, 3 identity)
+_KV = [0, 1, 0, 1, 2, 0, 2, 1, 2, 3, 0, 3, 1, 3, 2, 3]
+_KH = [0, 0, 1, 1, 0, 2, 2, 2, 1, 3, 3, 0, 3, 1, 3, 2]
+
+
+def _tx_candidates(s):
+    """(tw, th) transform sizes tiling an s x s block: sides in {s, s/2, s/4}
+    within [4, 32], aspect ratio at most 4 (all such pairs are reference
+    transform sizes)."""
+    sides = [v for v in (s, s // 2, s // 4) if 4 <= v <= 32]
+    return [(a, b) for a in sides for b in sides if max(a, b) <= 4 * min(a, b)]
+
+
+def make_frame(cfg: FrameConfig) -> FrameData:
+    rng = np.random.default_rng(cfg.seed)
+    W, H = cfg.width, cfg.height
+    bdmax = cfg.bitdepth_max if cfg.bpc == 16 else 255
+    planes = [(W, H), (W // 2, H // 2), (W // 2, H // 2)]
+
+    # reference pictures: 2 x 3 planes, padded, uniform random pixels
+    refs = []
+    for _ in range(2):
+        rp = []
+        for (pw, ph) in planes:
+            stride = (pw + 2 * REF_PAD + 63) // 64 * 64
+            rp.append(rng.integers(0, bdmax + 1, size=(ph + 2 * REF_PAD, stride),
+                                   dtype=cfg.pixel_dtype))
+        refs.append(rp)
+
+    lx, ly, ls = _partition(rng, W, H)
+    nb = len(lx)
+    r = rng.random(nb)
+    if cfg.kind == "mc":
+        kind = np.where(rng.random(nb) < cfg.compound_frac, abi.PRED_INTER_AVG, abi.PRED_INTER)
+    else:
+        kind = np.where(r < cfg.intra_frac, abi.PRED_INTRA,
+                        np.where(rng.random(nb) < cfg.compound_frac, abi.PRED_INTER_AVG,
+                                 abi.PRED_INTER))
+    filt = rng.integers(0, 9, nb)
+    mv = rng.integers(-64 * 16, 64 * 16 + 1, size=(nb, 2, 2))   # [block][ref][x|y], 1/16 px
+    mode = rng.integers(0, 14, nb)
+    zang = Z_ANGLES[rng.integers(0, 27, nb)]
+    zflags = rng.integers(0, 4, nb) << 9
+    fidx = rng.integers(0, 5, nb)
+    z2mw = rng.integers(1, 65, nb)
+    z2mh = rng.integers(1, 65, nb)
+
+    rows = []   # per-unit python tuples assembled below (vectorised per block)
+    unit_fields = {k: [] for k in ("plane", "x", "y", "tw", "th", "blk", "bs")}
+    for plane in range(3):
+        sub = 0 if plane == 0 else 1
+        bx, by, bs = lx >> sub, ly >> sub, ls >> sub
+        for b in range(nb):
+            s = int(bs[b])
+            if cfg.kind == "mc":
+                tw = th = s
+            else:
+                cands = _tx_candidates(s)
+                tw, th = cands[(b * 7 + plane * 3 + int(rng.integers(0, 1 << 20))) % len(cands)]
+            for oy in range(0, s, th):
+                for ox in range(0, s, tw):
+                    unit_fields["plane"].append(plane)
+                    unit_fields["x"].append(int(bx[b]) + ox)
+                    unit_fields["y"].append(int(by[b]) + oy)
+                    unit_fields["tw"].append(tw)
+                    unit_fields["th"].append(th)
+                    unit_fields["blk"].append(b)
+                    unit_fields["bs"].append(s)
+    del rows
+    plane_u = np.array(unit_fields["plane"], np.int32)
+    ux = np.array(unit_fields["x"], np.int32)
+    uy = np.array(unit_fields["y"], np.int32)
+    tw = np.array(unit_fields["tw"], np.int32)
+    th = np.array(unit_fields["th"], np.int32)
+    blk = np.array(unit_fields["blk"], np.int32)
+    bsz = np.array(unit_fields["bs"], np.int32)
+    n = len(ux)
+    tx = np.array([abi.TX_INDEX[(a, b)] for a, b in zip(tw, th)], np.int32)
+
+    units = np.zeros(n, abi.UNIT_DTYPE)
+    pw = np.array([planes[p][0] for p in range(3)])
+    units["dst_off"] = uy * pw[plane_u] + ux
+    units["tx"] = tx
+    units["plane"] = plane_u
+    pk = kind[blk]
+    units["pred"] = pk
+    units["bw4"] = bsz // 4
+    units["bh4"] = bsz // 4
+
+    # inter parameters
+    inter = pk != abi.PRED_INTRA
+    ref_stride = np.array([refs[0][p].shape[1] for p in range(3)])
+    for k in range(2):
+        mvx = mv[blk, k, 0]
+        mvy = mv[blk, k, 1]
+        chroma = plane_u > 0
+        mvx = np.where(chroma, mvx >> 1, mvx)
+        mvy = np.where(chroma, mvy >> 1, mvy)
+        sx = ux + (mvx >> 4)
+        sy = uy + (mvy >> 4)
+        units[f"src_off{k}"] = np.where(inter, sy * ref_stride[plane_u] + sx, 0)
+        units[f"mx{k}"] = np.where(inter, mvx & 15, 0)
+        units[f"my{k}"] = np.where(inter, mvy & 15, 0)
+        units[f"ref{k}"] = k
+    units["filter2d"] = np.where(inter, filt[blk], 0)
+
+    # intra parameters
+    intra = ~inter
+    m = mode[blk]
+    ang = np.where((m >= abi.Z1_PRED) & (m <= abi.Z3_PRED),
+                   (90 * (m - abi.Z1_PRED) + zang[blk]) | zflags[blk],
+                   np.where(m == abi.FILTER_PRED, fidx[blk], 0))
+    # the intra fields share bytes with the inter ones (a C union): write
+    # them only where the unit is intra
+    edge_len = np.where(intra, 2 * th + 2 * tw + 1, 0)
+    edge_start = np.concatenate([[0], np.cumsum(edge_len)[:-1]])
+    iu = units[intra]
+    iu["src_off1"] = 0
+    iu["filter2d"] = 0
+    iu["ref0"] = 0
+    iu["ref1"] = 0
+    iu["edge_off"] = (edge_start + 2 * th)[intra]
+    iu["mode"] = m[intra]
+    iu["angle"] = ang[intra]
+    z2 = m[intra] == abi.Z2_PRED
+    iu["max_w"] = np.where(z2, z2mw[blk][intra], 0)
+    iu["max_h"] = np.where(z2, z2mh[blk][intra], 0)
+    units[intra] = iu
+    sort_minor = np.where(inter, filt[blk], 16 + m)
+    edges = rng.integers(0, bdmax + 1, size=max(int(edge_len.sum()), 1), dtype=cfg.pixel_dtype)
+
+    # transform types, coefficient regions and coefficients
+    if cfg.kind == "mc":
+        units["txtp"] = abi.NO_RESIDUAL
+        coefs = np.zeros(1, cfg.coef_dtype)
+    else:
+        txtp = np.zeros(n, np.int32)
+        for t in range(abi.N_TX):
+            sel = np.nonzero(tx == t)[0]
+            if not len(sel):
+                continue
+            ok = [tp for tp in range(16) if abi.itx_supported(t, tp)]
+            txtp[sel] = np.array(ok)[rng.integers(0, len(ok), len(sel))]
+        units["txtp"] = txtp
+        eclass = rng.random(n)          # <.25 DC-only, <.75 partial, else full
+        sw = np.minimum(tw, 32)
+        sh = np.minimum(th, 32)
+        nzw = np.where(eclass < 0.25, np.where(txtp == abi.DCT_DCT, 0, 1),
+                       np.where(eclass < 0.75, 1 + (rng.random(n) * sw).astype(np.int32), sw))
+        nzh = np.where(eclass < 0.25, np.where(txtp == abi.DCT_DCT, 0, 1),
+                       np.where(eclass < 0.75, 1 + (rng.random(n) * sh).astype(np.int32), sh))
+        units["nzw"] = nzw
+        units["nzh"] = nzh
+        ncoef = np.where(nzw == 0, 1, nzw * nzh)
+        coef_off = np.concatenate([[0], np.cumsum(ncoef)[:-1]])
+        units["coef_off"] = coef_off
+        coefs = np.zeros(int(ncoef.sum()), cfg.coef_dtype)
+        lim = np.iinfo(np.int16)
+        for t in range(abi.N_TX):
+            w_, h_ = abi.TX_WH[t]
+            for tp in range(16):
+                sel = np.nonzero((tx == t) & (txtp == tp))[0]
+                if not len(sel):
+                    continue
+                res = rng.integers(-bdmax, bdmax + 1, size=(len(sel), h_, w_)).astype(np.float64)
+                mh = _fwd_mat(_KH[tp], w_)
+                mvv = _fwd_mat(_KV[tp], h_)
+                sc = _SCALE[int(np.log2(w_ * h_)) - 4]
+                c = np.einsum("yk,nkx->nyx", mvv, np.einsum("nyk,xk->nyx", res, mh)) * sc
+                c = np.floor(c + 0.5)
+                c = np.clip(c, lim.min, lim.max).astype(np.int64)
+                for j, i in enumerate(sel):
+                    a, b, o = int(nzw[i]), int(nzh[i]), int(coef_off[i])
+                    if a == 0:
+                        coefs[o] = c[j, 0, 0]
+                    else:
+                        coefs[o:o + a * b] = c[j, :b, :a].T.ravel()
+
+    # sort by (class, pred kind, filter / mode) so waves are uniform
+    order = np.lexsort((sort_minor, units["pred"], units["tx"]))
+    units = units[order]
+    counts = np.bincount(units["tx"], minlength=abi.N_TX)
+    class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+
+    fd = FrameData(cfg=cfg, units=units, class_start=class_start, coefs=coefs, edges=edges,
+                   refs=refs, plane_wh=planes, blk=(blk * 3 + plane_u)[order])
+    fd.stats = algorithmic_bytes(fd)
+    return fd
+
+
+def algorithmic_bytes(fd: FrameData):
+    """Bytes the reconstruction must move per frame: the
+    reference footprint each mc call reads, edge arrays, stored
+    coefficients, one write of every output pixel, and the 32-B unit
+    descriptors."""
+    u = fd.units
+    bpp = 1 if fd.cfg.bpc == 8 else 2
+    cb = 2 if fd.cfg.bpc == 8 else 4
+    w = np.array([abi.TX_WH[t][0] for t in u["tx"]])
+    h = np.array([abi.TX_WH[t][1] for t in u["tx"]])
+    bw, bh = u["bw4"].astype(np.int64) * 4, u["bh4"].astype(np.int64) * 4
+    # the reference reads each prediction block's footprint once per mc call
+    # (src/recon_tmpl.c:957-1059): count it per block, not per transform unit
+    inter = (u["pred"] == abi.PRED_INTER) | (u["pred"] == abi.PRED_INTER_AVG)
+    _, first = np.unique(np.where(inter, fd.blk, -1), return_index=True)
+    first = first[inter[first]]
+    src = np.zeros(len(u), np.int64)
+    for k in range(2):
+        use = (u["pred"] == abi.PRED_INTER) if k == 0 else np.zeros(len(u), bool)
+        use = use | (u["pred"] == abi.PRED_INTER_AVG)
+        mx, my = u[f"mx{k}"], u[f"my{k}"]
+        fh = np.where(mx > 0, np.where(bw > 4, 7, 3), 0)
+        fv = np.where(my > 0, np.where(bh > 4, 7, 3), 0)
+        src[first] += np.where(use, (bw + fh) * (bh + fv), 0)[first]
+    intra = u["pred"] == abi.PRED_INTRA
+    edge = np.where(intra, 2 * w + 2 * h + 1, 0)
+    ncoef = np.where(u["txtp"] == abi.NO_RESIDUAL, 0, np.where(u["nzw"] == 0, 1,
+                     u["nzw"].astype(np.int64) * u["nzh"]))
+    out_px = int((w * h).sum())
+    return {
+        "units": int(len(u)),
+        "ref_bytes": int(src.sum()) * bpp,
+        "edge_bytes": int(edge.sum()) * bpp,
+        "coef_bytes": int(ncoef.sum()) * cb,
+        "dst_bytes": out_px * bpp,
+        "desc_bytes": int(len(u)) * 32,
+        "pixels": out_px,
+        "total_bytes": int(src.sum()) * bpp + int(edge.sum()) * bpp + int(ncoef.sum()) * cb
+                       + out_px * bpp + int(len(u)) * 32,
+        "n_intra": int(intra.sum()),
+        "n_inter": int((~intra).sum()),
+    }

@@ -205,6 +205,9 @@ enum Dav1dGpuPredKind {
     DGPU_PRED_INTRA = 3,     /* intra_pred from the unit's edge array        */
 };
 
+/* txtp value of a prediction-only unit (no inv_txfm_add): mc-only batches */
+#define DGPU_NO_RESIDUAL 0xff
+
 /* 32 bytes, device-resident, one per transform block.
  *
  * Coefficients are stored compactly: the nzw x nzh top-left region that can

@@ -81,11 +81,11 @@ static inline int rshift_rnd(int v, int sh) { return (v + ((1 << sh) >> 1)) >> s
 /* put_8tap_c, src/mc_tmpl.c:113-171 (copy path put_c :52-61) */
 static void put_8tap(pixel *dst, ptrdiff_t dst_stride, const pixel *src,
                      ptrdiff_t src_stride, int w, int h, int mx, int my,
-                     int ftype, int bdmax)
+                     int ftype, int bw, int bh, int bdmax)
 {
     const int ib = IBITS(bdmax);
     const ptrdiff_t ds = PX(dst_stride), ss = PX(src_stride);
-    const int8_t *fh = kern8(ftype & 3, mx, w), *fv = kern8(ftype >> 2, my, h);
+    const int8_t *fh = kern8(ftype & 3, mx, bw), *fv = kern8(ftype >> 2, my, bh);
     if (fh && fv) {
         int16_t mid[(128 + 7) * 128];
         for (int r = 0; r < h + 7; r++)
@@ -111,11 +111,11 @@ static void put_8tap(pixel *dst, ptrdiff_t dst_stride, const pixel *src,
 
 /* prep_8tap_c, src/mc_tmpl.c:223-282 (prep_c :64-75) */
 static void prep_8tap(int16_t *tmp, const pixel *src, ptrdiff_t src_stride,
-                      int w, int h, int mx, int my, int ftype, int bdmax)
+                      int w, int h, int mx, int my, int ftype, int bw, int bh, int bdmax)
 {
     const int ib = IBITS(bdmax);
     const ptrdiff_t ss = PX(src_stride);
-    const int8_t *fh = kern8(ftype & 3, mx, w), *fv = kern8(ftype >> 2, my, h);
+    const int8_t *fh = kern8(ftype & 3, mx, bw), *fv = kern8(ftype >> 2, my, bh);
     if (fh && fv) {
         int16_t mid[(128 + 7) * 128];
         for (int r = 0; r < h + 7; r++)
@@ -728,10 +728,10 @@ static void pal_pred(pixel *d, ptrdiff_t s, const pixel *pal, const uint8_t *idx
 #define MC_WRAPPERS(name, ft)                                                   \
 static void put_##name(pixel *d, ptrdiff_t ds, const pixel *s, ptrdiff_t ss,    \
                        int w, int h, int mx, int my BDPARAM)                    \
-{ BD_DECL put_8tap(d, ds, s, ss, w, h, mx, my, ft, bdmax_); }                   \
+{ BD_DECL put_8tap(d, ds, s, ss, w, h, mx, my, ft, w, h, bdmax_); }                   \
 static void prep_##name(int16_t *t, const pixel *s, ptrdiff_t ss,               \
                         int w, int h, int mx, int my BDPARAM)                   \
-{ BD_DECL prep_8tap(t, s, ss, w, h, mx, my, ft, bdmax_); }                      \
+{ BD_DECL prep_8tap(t, s, ss, w, h, mx, my, ft, w, h, bdmax_); }                      \
 static void put_scaled_##name(pixel *d, ptrdiff_t ds, const pixel *s,           \
                               ptrdiff_t ss, int w, int h, int mx, int my,       \
                               int dx, int dy BDPARAM)                           \
@@ -1406,4 +1406,92 @@ void SFX(oracle_itx_dsp_init)(ITCTX *c, int bpc)
             if (SFX(oracle_itx_supported)(tx, tp))
                 c->itxfm_add[tx][tp] = (void *)itx_all[tx][tp];
     c->itxfm_add[DGPU_TX_4X4][DGPU_WHT_WHT] = itx_wht_wht_4x4;
+}
+
+/* ========================================================== batch oracle */
+
+/* CPU reconstruction of a Dav1dGpuFrameBatch whose pointers are HOST
+ * pointers: for each unit the same DSP calls the decoder makes
+ * (recon_b_inter: mc put or mct x2 + avg, src/recon_tmpl.c:957-1059, :1845;
+ * recon_b_intra: intra_pred per transform block, :1294), then
+ * inv_txfm_add (:816 / :1347) on the dense coefficient block rebuilt from the
+ * compact region.  The mc filter bank follows the prediction block size
+ * (bw4/bh4), as the decoder's call over the whole block would.  Units are
+ * independent; [u0, u1) lets callers split the work. */
+static const int ftype_of[9] = { 0, 4, 8, 2, 6, 10, 1, 5, 9 };
+
+int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
+{
+    const int bdmax = BITDEPTH == 8 ? 255 : b->bitdepth_max;
+    IPCTX ipc;
+    SFX(oracle_intra_pred_dsp_init)(&ipc);
+    const Dav1dGpuUnit *units = b->units;
+    coef *pool = (coef *)b->coef;
+    const pixel *edges = (const pixel *)b->edges;
+    int16_t t1[64 * 64], t2[64 * 64];
+    coef cf[32 * 32];
+    for (int i = u0; i < u1; i++) {
+        const Dav1dGpuUnit *u = &units[i];
+        const int w = txdim[u->tx].w, h = txdim[u->tx].h;
+        const int pl = u->plane;
+        const ptrdiff_t ds = b->dst[pl].stride;
+        pixel *dst = (pixel *)b->dst[pl].data + u->dst_off;
+        if (u->pred == DGPU_PRED_INTER || u->pred == DGPU_PRED_INTER_AVG) {
+            const int f2d = u->p.inter.filter2d;
+            const int comp = u->pred == DGPU_PRED_INTER_AVG;
+            for (int k = 0; k <= comp; k++) {
+                const int r = u->p.inter.ref[k];
+                const pixel *src = (const pixel *)b->ref[r][pl].data + u->p.inter.src_off[k];
+                const ptrdiff_t ss = b->ref[r][pl].stride;
+                const int mx = u->p.inter.mx[k], my = u->p.inter.my[k];
+                if (!comp) {
+                    if (f2d == DGPU_FILTER_2D_BILINEAR) bilin_mc(dst, ds, NULL, src, ss, w, h, mx, my, bdmax);
+                    else put_8tap(dst, ds, src, ss, w, h, mx, my, ftype_of[f2d], u->bw4 * 4, u->bh4 * 4, bdmax);
+                } else {
+                    int16_t *t = k ? t2 : t1;
+                    if (f2d == DGPU_FILTER_2D_BILINEAR) bilin_mc(NULL, 0, t, src, ss, w, h, mx, my, bdmax);
+                    else prep_8tap(t, src, ss, w, h, mx, my, ftype_of[f2d], u->bw4 * 4, u->bh4 * 4, bdmax);
+                }
+            }
+            if (comp) avg_blend(dst, ds, t1, t2, w, h, 0, 0, NULL, bdmax);
+        } else if (u->pred == DGPU_PRED_INTRA) {
+            const pixel *tl = edges + u->p.intra.edge_off;
+            ipc.intra_pred[u->p.intra.mode](dst, ds, tl, w, h, u->p.intra.angle,
+                                            u->p.intra.max_w, u->p.intra.max_h
+#if BITDEPTH == 16
+                                            , bdmax
+#endif
+                                            );
+        }
+        if (u->txtp == DGPU_NO_RESIDUAL) continue;
+        /* inv_txfm_add on the dense block */
+        const int sw = mini(w, 32), sh = mini(h, 32);
+        memset(cf, 0, sizeof(cf));
+        coef *src = pool + u->coef_off;
+        int eob;
+        if (u->nzw == 0) {
+            cf[0] = src[0];
+            eob = 0;
+            if (b->zero_coefs) src[0] = 0;
+        } else {
+            for (int x = 0; x < u->nzw; x++)
+                for (int y = 0; y < u->nzh; y++) {
+                    cf[y + x * sh] = src[y + x * u->nzh];
+                    if (b->zero_coefs) src[y + x * u->nzh] = 0;
+                }
+            eob = 1;
+        }
+        (void)sw;
+        if (u->txtp == DGPU_WHT_WHT) itx_wht_wht_4x4(dst, ds, cf, eob
+#if BITDEPTH == 16
+                                                     , bdmax
+#endif
+                                                     );
+        else itx_all[u->tx][u->txtp](dst, ds, cf, eob
+#if BITDEPTH == 16
+                                     , bdmax
+#endif
+                                     );
+    }
+    return 0;
 }

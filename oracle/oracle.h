@@ -10,4 +10,6 @@ void oracle_intra_pred_dsp_init_16bpc(Dav1dIntraPredDSPContext_16bpc *c);
 void oracle_itx_dsp_init_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int bpc);
 void oracle_itx_dsp_init_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc);
 int oracle_itx_supported_8bpc(int tx, int tp);
+int oracle_recon_units_8bpc(const Dav1dGpuFrameBatch *b, int u0, int u1);
+int oracle_recon_units_16bpc(const Dav1dGpuFrameBatch *b, int u0, int u1);
 #endif
