@@ -85,10 +85,11 @@ def main():
     pkg = ge.load_package()
     import dav1d_mirror_amd.workload as wl
     import dav1d_mirror_amd.batch as bt
+    import dav1d_mirror_amd.shard as sh
 
     c = dict(CONFIGS[args.config])
     label = c.pop("label")
-    cfg = wl.FrameConfig(seed=0x5EED0001 + 7919 * rank, **c)
+    cfg = sh.rank_config(wl.FrameConfig(**c), rank)
     t0 = time.perf_counter()
     fd = wl.make_frame(cfg)
     log(f"[rank {rank}] frame: {fd.n_units} units, {fd.stats['pixels']} px, "
@@ -112,11 +113,7 @@ def main():
         frame.launch(stream)
     torch.cuda.synchronize(dev)
     barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = sh.max_over_ranks(time.perf_counter() - t0, dist, dev)
 
     # per-launch kernel duration with HIP events on the launch stream
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -139,8 +136,7 @@ def main():
         log(f"[rank 0] bit-exact vs oracle: {check}")
 
     if rank == 0:
-        px_total = fd.stats["pixels"] * args.steps * world
-        value = px_total / el / 1e9
+        value = sh.aggregate_gpix_per_s(fd.stats["pixels"], args.steps, world, el)
         bytes_launch = fd.stats["total_bytes"]
         achieved = bytes_launch / kern_s / 1e9
         out = {

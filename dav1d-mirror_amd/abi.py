@@ -43,18 +43,19 @@ def itx_supported(tx, tp):
     return True
 
 
-# Dav1dGpuUnit, 32 bytes, with the inter / intra union as overlapping fields.
+# Dav1dGpuUnit, 32 bytes, with the inter / intra union as overlapping fields;
+# every byte belongs to a field so copies never carry uninitialised padding.
 UNIT_DTYPE = np.dtype({
     "names": ["dst_off", "coef_off", "tx", "txtp", "plane", "pred", "nzw", "nzh",
               "bw4", "bh4",
               "src_off0", "src_off1", "mx0", "mx1", "my0", "my1", "filter2d", "ref0", "ref1",
-              "edge_off", "angle", "mode", "max_w", "max_h"],
+              "pad_inter", "edge_off", "angle", "mode", "pad_intra", "max_w", "max_h"],
     "formats": ["<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
-                "<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
-                "<i4", "<u2", "u1", "<u2", "<u2"],
+                "<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
+                "<i4", "<u2", "u1", "u1", "<u2", "<u2"],
     "offsets": [0, 4, 8, 9, 10, 11, 12, 13, 14, 15,
-                16, 20, 24, 25, 26, 27, 28, 29, 30,
-                16, 20, 22, 24, 26],
+                16, 20, 24, 25, 26, 27, 28, 29, 30, 31,
+                16, 20, 22, 23, 24, 26],
     "itemsize": 32,
 })
 
@@ -113,5 +114,5 @@ EXPORTED_SYMBOLS = [
     "dav1d_intra_pred_dsp_init_gpu_8bpc", "dav1d_intra_pred_dsp_init_gpu_16bpc",
     "dav1d_itx_dsp_init_gpu_8bpc", "dav1d_itx_dsp_init_gpu_16bpc",
     "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version",
-    "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc",
+    "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc", "dav1d_gpu_recon_lds_bytes",
 ]

@@ -8,6 +8,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <utility>
@@ -98,6 +99,10 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     memcpy(a.class_start, b->class_start, sizeof(a.class_start));
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;
+    {   // debug-only phase ablation for profiling (never set in production)
+        const char *ev = getenv("DAV1D_GPU_ABLATE");
+        a.ablate = ev ? atoi(ev) : 0;
+    }
 
     for (int big = 0; big < 2; big++) {
         int acc = 0;

@@ -42,6 +42,7 @@ template <int BPC> struct ReconArgs {
     int wave_start[DGPU_N_RECT_TX_SIZES + 1];   // cumulative waves per class
     int bdmax;
     int zero_coefs;
+    int ablate;   // debug-only phase mask (DAV1D_GPU_ABLATE); 0 in production
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -153,19 +154,22 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
     // ---------------- phase A: stage sources ----------------
     const int nref = u.pred == DGPU_PRED_INTER_AVG ? 2 : u.pred == DGPU_PRED_INTER ? 1 : 0;
     int skew0 = 0, skew1 = 0;
-    for (int k = 0; k < nref; k++) {
-        const int r = u.p.inter.ref[k];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (k >= nref || (a.ablate & 1)) break;
+        const int r = k ? u.p.inter.ref[1] : u.p.inter.ref[0];
         const int rs = a.ref_stride[r][plane];
-        const P *org = a.ref[r][plane] + u.p.inter.src_off[k] - 3 * rs - 3;
+        const P *org = a.ref[r][plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
         const uintptr_t ad = reinterpret_cast<uintptr_t>(org);
         const uintptr_t a0 = ad & ~(uintptr_t)3;
         const int sk = (int)(ad - a0) / B;
         if (k) skew1 = sk; else skew0 = sk;
         const int ndw = ((int)(ad - a0) + (W + 7) * B + 3) >> 2;
+        const float inv = 1.0f / (float)ndw;
         uint32_t *dstl = reinterpret_cast<uint32_t *>(srcl + k * SL::FP);
         const int total = (H + 7) * ndw;
         for (int i = l; i < total; i += G) {
-            const int row = i / ndw, d = i - row * ndw;
+            const int row = (int)(((float)i + 0.5f) * inv), d = i - row * ndw;
             const uint32_t *s = reinterpret_cast<const uint32_t *>(a0 + (intptr_t)row * rs * B);
             dstl[row * (SL::FPB / 4) + d] = s[d];
         }
@@ -304,7 +308,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
 
     // intra prediction of the whole unit into the LDS tile, all G lanes
     // (src/ipred_tmpl.c:93-599); FILTER_PRED already filled it above
-    if (u.pred == DGPU_PRED_INTRA && ip.mode != DGPU_FILTER_PRED) {
+    if (u.pred == DGPU_PRED_INTRA && ip.mode != DGPU_FILTER_PRED && !(a.ablate & 4)) {
         const int mode = ip.mode;
         for (int i = l; i < W * H; i += G) {
             const int x = i % W, y = i / W;
@@ -381,7 +385,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
     const bool dconly = !nores && u.nzw == 0;
     const Clip rc = ItxClip<BPC>::row(bdmax), cc = ItxClip<BPC>::col(bdmax);
     typename Px<BPC>::coef *cf = a.coef + u.coef_off;
-    if (!nores && !dconly && l < SH) {
+    if (!nores && !dconly && l < SH && !(a.ablate & 8)) {
         const int nzw = u.nzw, nzh = u.nzh;
         int c[W];
 #pragma unroll
@@ -401,9 +405,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
     // ---------------- phase C: column transform + prediction + store -------
     if (l >= W) return;
     int res[H];
-    if (nores) {
+    if (nores || (a.ablate & 8)) {
 #pragma unroll
-        for (int y = 0; y < H; y++) res[y] = 0;
+        for (int y = 0; y < H; y++) res[y] = (a.ablate & 8) ? (int)tmp[y] : 0;
     } else if (dconly) {  // src/itx_tmpl.c:53-65
         int dc = cf[0];
         if (a.zero_coefs) {
@@ -437,8 +441,11 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
         const bool comp = u.pred == DGPU_PRED_INTER_AVG;
         const int PB = Px<BPC>::PBIAS;
         int p0[H];
-        for (int k = 0; k < (comp ? 2 : 1); k++) {
-            const int mx = u.p.inter.mx[k], my = u.p.inter.my[k];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (k == 1 && !comp) break;
+            const int mx = k ? u.p.inter.mx[1] : u.p.inter.mx[0];
+            const int my = k ? u.p.inter.my[1] : u.p.inter.my[0];
             const signed char *fh = subpel_kernel(ftype & 3, mx, bw);
             const signed char *fv = subpel_kernel(ftype >> 2, my, bh);
             const P *F = reinterpret_cast<const P *>(srcl + k * SL::FP) + (k ? skew1 : skew0) + x;
@@ -456,7 +463,10 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
                 return s;
             };
             int out[H];
-            if (bil) {        // put_bilin_c / prep_bilin_c, src/mc_tmpl.c:395-546
+            if (a.ablate & 2) {
+#pragma unroll
+                for (int y = 0; y < H; y++) out[y] = F[y * FPP];
+            } else if (bil) {        // put_bilin_c / prep_bilin_c, src/mc_tmpl.c:395-546
                 auto bl = [&](int r, int c0, int c1, int m) {
                     const int p = F[r * FPP + c0], q = F[r * FPP + c1];
                     return 16 * p + m * (q - p);

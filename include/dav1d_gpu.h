@@ -274,6 +274,10 @@ typedef struct Dav1dGpuFrameBatch {
 int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream);
 int dav1d_gpu_recon_16bpc(const Dav1dGpuFrameBatch *b, void *stream);
 
+/* LDS bytes per 256-thread workgroup of the batch kernel (bpc 8/16; big=1:
+ * the launch over transform sizes with a 64-point side).  Diagnostics. */
+int dav1d_gpu_recon_lds_bytes(int bpc, int big);
+
 #ifdef __cplusplus
 }
 #endif

@@ -90,3 +90,72 @@ class HostFrame:
             t.start()
         for t in ts:
             t.join()
+
+
+# ---------------------------------------------------------------------------
+# Direct access to the oracle's DSP tables (same layouts as dav1d_gpu.h) for
+# property tests.
+class _MC(ctypes.Structure):
+    _fields_ = [("mc", ctypes.c_void_p * 10), ("mc_scaled", ctypes.c_void_p * 10),
+                ("mct", ctypes.c_void_p * 10), ("mct_scaled", ctypes.c_void_p * 10),
+                ("avg", ctypes.c_void_p), ("w_avg", ctypes.c_void_p), ("mask", ctypes.c_void_p),
+                ("w_mask", ctypes.c_void_p * 3), ("blend", ctypes.c_void_p),
+                ("blend_v", ctypes.c_void_p), ("blend_h", ctypes.c_void_p),
+                ("warp8x8", ctypes.c_void_p), ("warp8x8t", ctypes.c_void_p),
+                ("emu_edge", ctypes.c_void_p), ("resize", ctypes.c_void_p)]
+
+
+class _ITX(ctypes.Structure):
+    _fields_ = [("itxfm_add", (ctypes.c_void_p * 17) * 19)]
+
+
+def mc_table(bpc):
+    L = load()
+    t = _MC()
+    getattr(L, f"oracle_mc_dsp_init_{bpc}bpc")(ctypes.byref(t))
+    return t
+
+
+def itx_table(bpc, bits=None):
+    L = load()
+    t = _ITX()
+    getattr(L, f"oracle_itx_dsp_init_{bpc}bpc")(ctypes.byref(t), bits or (8 if bpc == 8 else 10))
+    return t
+
+
+def call_put(tbl, f, dst, src, src_off, w, h, mx, my, bdmax=None):
+    """mc[f](dst, dst_stride, src + src_off, src_stride, w, h, mx, my[, bdmax])."""
+    hbd = dst.dtype == np.uint16
+    args = [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p, ctypes.c_ssize_t] + [ctypes.c_int] * 4
+    if hbd:
+        args.append(ctypes.c_int)
+    fn = ctypes.CFUNCTYPE(None, *args)(tbl.mc[f])
+    a = [dst.ctypes.data, dst.strides[0], src.ctypes.data + src_off * src.itemsize, src.strides[0],
+         w, h, mx, my]
+    if hbd:
+        a.append(bdmax)
+    fn(*a)
+
+
+def call_prep(tbl, f, tmp, src, src_off, w, h, mx, my, bdmax=None):
+    hbd = src.dtype == np.uint16
+    args = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ssize_t] + [ctypes.c_int] * 4
+    if hbd:
+        args.append(ctypes.c_int)
+    fn = ctypes.CFUNCTYPE(None, *args)(tbl.mct[f])
+    a = [tmp.ctypes.data, src.ctypes.data + src_off * src.itemsize, src.strides[0], w, h, mx, my]
+    if hbd:
+        a.append(bdmax)
+    fn(*a)
+
+
+def call_itx(tbl, tx, tp, dst, coef, eob, bdmax=None):
+    hbd = dst.dtype == np.uint16
+    args = [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p, ctypes.c_int]
+    if hbd:
+        args.append(ctypes.c_int)
+    fn = ctypes.CFUNCTYPE(None, *args)(tbl.itxfm_add[tx][tp])
+    a = [dst.ctypes.data, dst.strides[0], coef.ctypes.data, eob]
+    if hbd:
+        a.append(bdmax)
+    fn(*a)

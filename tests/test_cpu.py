@@ -1,0 +1,161 @@
+"""CPU-side tests (no GPU): the C-ABI library loads and exports what
+include/dav1d_gpu.h declares, the oracle against its golden fixtures and
+against properties the reference's algorithms guarantee, and the host-side
+batch builder.  Fixtures are oracle-generated (parity unpinned vs the
+reference binary, which cannot be built here)."""
+import ctypes
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ------------------------------------------------------------------ C ABI --
+
+def test_header_symbols_exported(pkg):
+    hdr = open(os.path.join(ROOT, "include", "dav1d_gpu.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    declared = set(re.findall(r"^\s*(?:int|void|const char \*)\s*(dav1d_\w+)\s*\(", hdr, flags=re.M))
+    assert len(declared) >= 17
+    assert declared == set(pkg.abi.EXPORTED_SYMBOLS)
+    lib = ctypes.CDLL(pkg.abi.lib_path())   # loads without touching a device
+    for name in sorted(declared):
+        assert hasattr(lib, name), name
+
+
+def test_abi_struct_sizes(pkg):
+    assert pkg.abi.UNIT_DTYPE.itemsize == 32
+    fb = pkg.abi.FrameBatch
+    # 3 + 8*3 planes of 24 bytes, then pointers / ints as in dav1d_gpu.h
+    assert ctypes.sizeof(pkg.abi.Plane) == 24
+    assert fb.units.offset == 27 * 24
+
+
+def test_itx_table_matches_reference_count(pkg, oracle):
+    L = oracle.load()
+    for bpc in (8, 16):
+        t = oracle.itx_table(bpc)
+        n = sum(1 for tx in range(19) for tp in range(17) if t.itxfm_add[tx][tp])
+        assert n == 156, (bpc, n)        # tests/checkasm/itx.c:313-314 table density
+        ours = sum(1 for tx in range(19) for tp in range(17) if pkg.abi.itx_supported(tx, tp))
+        assert ours == 156
+    assert L.oracle_itx_supported_8bpc(4, 0) == 1
+
+
+# ---------------------------------------------------------------- oracle ---
+
+def test_oracle_golden(pkg, oracle):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_golden
+    g = np.load(os.path.join(ROOT, "tests", "golden", "recon_golden.npz"))
+    for name, kw in gen_golden.CASES:
+        fd, planes = gen_golden.run_case(kw)
+        assert int(g[f"{name}_units"][0]) == fd.n_units, name
+        for p, a in enumerate(planes):
+            h = np.frombuffer(hashlib.sha256(a.tobytes()).digest(), np.uint8)
+            assert np.array_equal(h, g[f"{name}_p{p}_sha256"]), (name, p)
+            if name == "full8_s1":
+                assert np.array_equal(a, g[f"{name}_p{p}"])
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023), (16, 4095)])
+def test_mc_constant_image_is_preserved(oracle, bpc, bdmax):
+    """Every 8-tap / bilinear kernel has unit DC gain (taps sum to 64), so a
+    flat picture stays flat through put for all sub-pel positions
+    (src/mc_tmpl.c:113-171, :395-450)."""
+    tbl = oracle.mc_table(bpc)
+    pdt = np.uint8 if bpc == 8 else np.uint16
+    rng = np.random.default_rng(bpc + bdmax)
+    for f in range(10):
+        for w, h in ((4, 4), (8, 8), (16, 32), (2, 8)):
+            c = int(rng.integers(0, bdmax + 1))
+            src = np.full((h + 8, w + 8), c, pdt)
+            dst = np.zeros((h, w), pdt)
+            mx, my = int(rng.integers(0, 16)), int(rng.integers(0, 16))
+            oracle.call_put(tbl, f, dst, src, 3 * (w + 8) + 3, w, h, mx, my, bdmax)
+            assert (dst == c).all(), (f, w, h, mx, my)
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+def test_prep_copy_then_avg_equals_put(oracle, bpc, bdmax):
+    """Integer-position compound: avg(prep(x), prep(x)) == put(x) (the
+    intermediate scaling/bias of src/mc_tmpl.c:39-49 cancels exactly)."""
+    tbl = oracle.mc_table(bpc)
+    pdt = np.uint8 if bpc == 8 else np.uint16
+    rng = np.random.default_rng(3)
+    w = h = 16
+    src = rng.integers(0, bdmax + 1, (h + 8, w + 8)).astype(pdt)
+    tmp = np.zeros(w * h, np.int16)
+    oracle.call_prep(tbl, 0, tmp, src, 3 * (w + 8) + 3, w, h, 0, 0, bdmax)
+    ib = 4 if bpc == 8 else 14 - int(np.log2(bdmax + 1))
+    pb = 0 if bpc == 8 else 8192
+    avg = np.clip((2 * tmp.astype(np.int32) + (1 << ib) + 2 * pb) >> (ib + 1), 0, bdmax)
+    assert np.array_equal(avg.reshape(h, w), src[3:3 + h, 3:3 + w])
+
+
+@pytest.mark.parametrize("bpc", [8, 16])
+def test_itx_dc_only_shortcut_matches_full_path(oracle, pkg, bpc):
+    """The eob==0 DC-only shortcut of dct_dct (src/itx_tmpl.c:53-65) equals
+    the full separable path on a DC-only block for in-range DC values."""
+    tbl = oracle.itx_table(bpc)
+    pdt = np.uint8 if bpc == 8 else np.uint16
+    cdt = np.int16 if bpc == 8 else np.int32
+    bdmax = 255 if bpc == 8 else 1023
+    rng = np.random.default_rng(bpc)
+    for tx, (w, h) in enumerate(pkg.abi.TX_WH):
+        for _ in range(4):
+            dc = int(rng.integers(-2000, 2000))
+            base = rng.integers(0, bdmax + 1, (h, w)).astype(pdt)
+            d0, d1 = base.copy(), base.copy()
+            c0 = np.zeros(32 * 32, cdt)
+            c1 = np.zeros(32 * 32, cdt)
+            c0[0] = c1[0] = dc
+            oracle.call_itx(tbl, tx, 0, d0, c0, 0, bdmax)
+            oracle.call_itx(tbl, tx, 0, d1, c1, 1, bdmax)
+            assert np.array_equal(d0, d1), (w, h, dc)
+            assert not c0.any() and not c1.any()       # coefficient zeroing contract
+
+
+# ------------------------------------------------------------- workload ---
+
+def test_workload_covers_every_pixel_once(pkg):
+    import dav1d_mirror_amd.workload as wl
+    for kind in ("full", "mc"):
+        fd = wl.make_frame(wl.FrameConfig(width=512, height=256, kind=kind, seed=3))
+        u = fd.units
+        assert np.array_equal(fd.class_start, np.concatenate(
+            [[0], np.cumsum(np.bincount(u["tx"], minlength=19))]))
+        assert (np.diff(u["tx"].astype(int)) >= 0).all()        # sorted by class
+        for p, (w, h) in enumerate(fd.plane_wh):
+            cover = np.zeros(h * w, np.int32)
+            for t in range(19):
+                sel = u[(u["plane"] == p) & (u["tx"] == t)]
+                tw, th = pkg.abi.TX_WH[t]
+                for off in sel["dst_off"]:
+                    y, x = divmod(int(off), w)
+                    cover.reshape(h, w)[y:y + th, x:x + tw] += 1
+            assert (cover == 1).all(), (kind, p)
+
+
+def test_workload_deterministic(pkg):
+    import dav1d_mirror_amd.workload as wl
+    a = wl.make_frame(wl.FrameConfig(width=256, height=128, seed=42))
+    b = wl.make_frame(wl.FrameConfig(width=256, height=128, seed=42))
+    assert a.units.tobytes() == b.units.tobytes()
+    assert np.array_equal(a.coefs, b.coefs) and np.array_equal(a.edges, b.edges)
+
+
+def test_workload_types_valid(pkg):
+    import dav1d_mirror_amd.workload as wl
+    fd = wl.make_frame(wl.FrameConfig(width=512, height=256, seed=8))
+    u = fd.units
+    for tx, tp in zip(u["tx"], u["txtp"]):
+        assert pkg.abi.itx_supported(int(tx), int(tp))
+    inter = u["pred"] != pkg.abi.PRED_INTRA
+    assert (u["filter2d"][inter] < 9).all()
+    assert ((u["mode"][~inter]) < 14).all()

@@ -1,0 +1,59 @@
+"""The N>1 path on CPU: world_size-2 gloo, each rank reconstructs its own
+frame (oracle on the host, standing in for the GPU kernel), timings reduce
+with MAX and pixel counts with SUM exactly as bench.py does over RCCL."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import __graft_entry__ as ge
+    ge.load_package()
+    import dav1d_mirror_amd.workload as wl
+    import dav1d_mirror_amd.shard as sh
+    orc = ge.load_oracle()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    cfg = sh.rank_config(wl.FrameConfig(width=256, height=128), rank)
+    fd = wl.make_frame(cfg)
+    hf = orc.HostFrame(fd)
+    hf.run()
+    digest = int(np.bitwise_xor.reduce(hf.dst[0].view(np.uint8).ravel().astype(np.int64)
+                                       * np.arange(hf.dst[0].size, dtype=np.int64)))
+    el = sh.max_over_ranks(0.01 * (rank + 1), dist, "cpu")
+    px = sh.sum_over_ranks(fd.stats["pixels"], dist, "cpu")
+    q.put((rank, cfg.seed, digest, el, px, fd.stats["pixels"]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_frame_sharding_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seeds = {r[1] for r in res}
+    assert len(seeds) == world                      # distinct frame per rank
+    assert res[0][2] != res[1][2]                   # different content
+    assert all(abs(r[3] - 0.02) < 1e-12 for r in res)   # MAX over ranks
+    assert all(r[4] == res[0][5] + res[1][5] for r in res)  # SUM of pixels
