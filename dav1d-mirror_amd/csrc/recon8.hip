@@ -5,8 +5,12 @@ extern "C" int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream) {
     return dgpu::launch<8>(b, (hipStream_t)stream);
 }
 
-// LDS bytes per 256-thread workgroup of each launch (roofline notes)
-extern "C" int dav1d_gpu_recon_lds_bytes(int bpc, int big) {
-    if (bpc == 8) return 4 * (big ? dgpu::ClassSet<true>::wave_lds<8>() : dgpu::ClassSet<false>::wave_lds<8>());
-    return 4 * (big ? dgpu::ClassSet<true>::wave_lds<16>() : dgpu::ClassSet<false>::wave_lds<16>());
+// LDS bytes per workgroup of one kernel (group 0 small, 1 large
+// -- up to 32x32 --, 2 huge -- a 64-point side); `big` != 0 selects group 2
+// for compatibility.  Diagnostics only.
+extern "C" int dav1d_gpu_recon_lds_bytes(int bpc, int group) {
+    using namespace dgpu;
+    if (bpc == 8)
+        return group == 0 ? 4 * wave_lds<8, 0>() : group == 1 ? 4 * wave_lds<8, 1>() : wave_lds<8, 2>();
+    return group == 0 ? 4 * wave_lds<16, 0>() : group == 1 ? 2 * wave_lds<16, 1>() : wave_lds<16, 2>();
 }

@@ -1,76 +1,118 @@
 // recon_impl.hpp -- batch-tier launch logic (instantiated per bitdepth in
 // recon8.hip / recon16.hip so the two heavy TUs compile in parallel).
 //
-// Two launches at most per frame batch: one over the transform classes with
-// both sides <= 32 (the only ones in 4:2:0 content up to 32x32 transforms),
-// one over the classes with a 64-point side (their 64-entry register arrays
-// would otherwise set the VGPR budget, and hence occupancy, of every wave).
+// Three kernels per frame batch, one per class group (small: w*h <= 128,
+// large: up to 32x32, huge: a 64-point side), each with its own register and
+// LDS budget.  Within a kernel the waves are scheduled (segment, class):
+// every class's unit range (units are sorted by class and, within a class,
+// by position) is cut into kSegments equal parts, so waves that run at the
+// same time touch the same band of the picture.  Blocks are mapped so each
+// XCD works through a contiguous run of bands: a picture line is then
+// written by one XCD's L2 instead of partially by several.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <utility>
 
 #include "recon_kernel.hpp"
 
 namespace dgpu {
 
-template <bool BIG> struct ClassSet;
-template <> struct ClassSet<false> {
-    template <int BPC> static constexpr int wave_lds() {
-        return MaxWave<BPC, DGPU_TX_4X4, DGPU_TX_8X8, DGPU_TX_16X16, DGPU_TX_32X32, DGPU_RTX_4X8,
-                       DGPU_RTX_8X4, DGPU_RTX_8X16, DGPU_RTX_16X8, DGPU_RTX_16X32, DGPU_RTX_32X16,
-                       DGPU_RTX_4X16, DGPU_RTX_16X4, DGPU_RTX_8X32, DGPU_RTX_32X8>::v;
-    }
-};
-template <> struct ClassSet<true> {
-    template <int BPC> static constexpr int wave_lds() {
-        return MaxWave<BPC, DGPU_TX_64X64, DGPU_RTX_32X64, DGPU_RTX_64X32, DGPU_RTX_16X64,
-                       DGPU_RTX_64X16>::v;
-    }
-};
+template <int BPC, int GRP, int... TX>
+__host__ __device__ constexpr int group_wave_lds(std::integer_sequence<int, TX...>) {
+    int m = 0;
+    ((m = (class_group(TX) == GRP && Slot<BPC, TX>::WAVE > m) ? Slot<BPC, TX>::WAVE : m), ...);
+    return m;
+}
+template <int BPC, int GRP> __host__ __device__ constexpr int wave_lds() {
+    return group_wave_lds<BPC, GRP>(std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
+}
 
-template <int BPC, int TX, bool BIG>
-__device__ __forceinline__ void dispatch_one(const ReconArgs<BPC> &a, int cls, int wic, uint8_t *lds) {
-    if constexpr (Cls<TX>::BIG == BIG) {
-        if (cls == TX) {
-            constexpr int U = Cls<TX>::U;
-            const int first = a.class_start[TX] + wic * U;
-            const int count = min(U, a.class_start[TX + 1] - first);
-            recon_units<BPC, TX>(a, first, count, lds);
-        }
+// waves per workgroup: one 64-lane wave for the 64-point classes (their LDS
+// slot alone is 37-47 KB), 4 otherwise (2 for 16bpc large units)
+template <int BPC, int GRP> __host__ __device__ constexpr int waves_per_block() {
+    return GRP == GROUP_HUGE ? 1 : (BPC == 16 && GRP == GROUP_LARGE) ? 2 : 4;
+}
+
+template <int BPC, int TX, int GRP>
+__device__ __forceinline__ void dispatch_one(const ReconArgs<BPC> &a, int cls, int first, int count,
+                                             uint8_t *lds) {
+    if constexpr (class_group(TX) == GRP) {
+        if (cls == TX) recon_units<BPC, TX>(a, first, count, lds);
     }
 }
 
-template <int BPC, bool BIG, int... TX>
-__device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, int cls, int wic, uint8_t *lds,
+template <int BPC, int GRP, int... TX>
+__device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, int cls, int first, int count, uint8_t *lds,
                                          std::integer_sequence<int, TX...>) {
-    (dispatch_one<BPC, TX, BIG>(a, cls, wic, lds), ...);
+    (dispatch_one<BPC, TX, GRP>(a, cls, first, count, lds), ...);
 }
 
-template <int BPC, bool BIG>
-__global__ __launch_bounds__(256) void k_recon(ReconArgs<BPC> a) {
+template <int BPC, int GRP>
+__global__ __launch_bounds__((64 * waves_per_block<BPC, GRP>())) void k_recon(ReconArgs<BPC> a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int WL = ClassSet<BIG>::template wave_lds<BPC>();
+    constexpr int WL = wave_lds<BPC, GRP>();
+    constexpr int NC = DGPU_N_RECT_TX_SIZES;
+    // XCD-contiguous block order: hardware deals blocks round-robin over the
+    // 8 XCDs, so logical block (b % 8) * (nb / 8) + b / 8 gives XCD x the
+    // x-th contiguous eighth of the schedule (gridDim.x is a multiple of 8)
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int lb = (b & 7) * (nb >> 3) + (b >> 3);
     const int wave = threadIdx.x >> 6;
-    const int gw = blockIdx.x * 4 + wave;
-    int cls = -1;
-#pragma unroll
-    for (int c = 0; c < DGPU_N_RECT_TX_SIZES; c++)
-        if (gw >= a.wave_start[c] && gw < a.wave_start[c + 1]) cls = c;
-    if (cls < 0) return;
-    dispatch<BPC, BIG>(a, cls, gw - a.wave_start[cls], lds + wave * WL,
+    const int gw = lb * waves_per_block<BPC, GRP>() + wave;
+    if (gw >= a.nwaves) return;
+    // locate (segment, class) of this wave: last entry with seg_wave <= gw
+    int lo = 0, hi = kSegments * NC;   // seg_wave[hi] == nwaves > gw
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.seg_wave[mid] <= gw) lo = mid; else hi = mid;
+    }
+    const int s = lo / NC, cls = lo % NC;
+    const int cs = a.class_start[cls], n = a.class_start[cls + 1] - cs;
+    const int seg_lo = cs + (int)((long)n * s / kSegments);
+    const int seg_hi = cs + (int)((long)n * (s + 1) / kSegments);
+    const int U = 64 / lanes_per_unit(cls);
+    const int first = seg_lo + (gw - a.seg_wave[lo]) * U;
+    const int count = min(U, seg_hi - first);
+    dispatch<BPC, GRP>(a, cls, first, count, lds + wave * WL,
                        std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 
-static constexpr int units_per_wave(int tx) {
-    const int w = tx_info(tx).w, h = tx_info(tx).h;
-    const int sh = h < 32 ? h : 32;
-    return 64 / (w > sh ? w : sh);
+template <int BPC, int GRP>
+static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned classmask, hipStream_t stream) {
+    constexpr int NC = DGPU_N_RECT_TX_SIZES;
+    int acc = 0;
+    for (int s = 0; s < kSegments; s++)
+        for (int c = 0; c < NC; c++) {
+            a.seg_wave[s * NC + c] = acc;
+            if (class_group(c) != GRP || !((classmask >> c) & 1)) continue;
+            const int n = b->class_start[c + 1] - b->class_start[c];
+            const int nseg = (int)((long)n * (s + 1) / kSegments) - (int)((long)n * s / kSegments);
+            const int U = 64 / lanes_per_unit(c);
+            acc += (nseg + U - 1) / U;
+        }
+    a.seg_wave[kSegments * NC] = acc;
+    a.nwaves = acc;
+    if (!acc) return 0;
+    constexpr int WPB = waves_per_block<BPC, GRP>();
+    const int nblk = ((acc + WPB - 1) / WPB + 7) & ~7;
+    constexpr int lds = WPB * wave_lds<BPC, GRP>();
+    static std::once_flag once;
+    std::call_once(once, [] {
+        hipFuncSetAttribute((const void *)k_recon<BPC, GRP>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    });
+    k_recon<BPC, GRP><<<dim3(nblk), 64 * WPB, lds, stream>>>(a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        fprintf(stderr, "dav1d-gpu: recon launch failed: %s\n", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
 }
-static constexpr bool is_big(int tx) { return tx_info(tx).w == 64 || tx_info(tx).h == 64; }
 
 template <int BPC>
 static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
@@ -81,6 +123,8 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     for (int c = 0; c < DGPU_N_RECT_TX_SIZES; c++)
         if (b->class_start[c + 1] < b->class_start[c]) return -2;
     if (b->class_start[0] != 0 || b->class_start[DGPU_N_RECT_TX_SIZES] != b->n_units) return -2;
+    for (int p = 0; p < 3; p++)   // output rows are stored with aligned 4..16-byte stores
+        if (((uintptr_t)b->dst[p].data & 15) || (b->dst[p].stride & 15)) return -4;
     if (b->n_units == 0) return 0;
 
     ReconArgs<BPC> a;
@@ -99,50 +143,18 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     memcpy(a.class_start, b->class_start, sizeof(a.class_start));
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;
-    {   // debug-only phase ablation for profiling (never set in production)
-        const char *ev = getenv("DAV1D_GPU_ABLATE");
-        a.ablate = ev ? atoi(ev) : 0;
-    }
+    // debug-only knobs for profiling (never set in production):
+    //   DAV1D_GPU_ABLATE    phase mask (outputs wrong)
+    //   DAV1D_GPU_CLASSMASK restrict to some size classes (others stale)
+    const char *ev = getenv("DAV1D_GPU_ABLATE");
+    a.ablate = ev ? atoi(ev) : 0;
+    const char *cm = getenv("DAV1D_GPU_CLASSMASK");
+    const unsigned classmask = cm ? (unsigned)strtoul(cm, nullptr, 0) : ~0u;
 
-    for (int big = 0; big < 2; big++) {
-        int acc = 0;
-        for (int c = 0; c < DGPU_N_RECT_TX_SIZES; c++) {
-            a.wave_start[c] = acc;
-            if (is_big(c) == (bool)big) {
-                const int n = b->class_start[c + 1] - b->class_start[c];
-                acc += (n + units_per_wave(c) - 1) / units_per_wave(c);
-            }
-        }
-        a.wave_start[DGPU_N_RECT_TX_SIZES] = acc;
-        if (!acc) continue;
-        const dim3 grid((acc + 3) / 4);
-        if (big) {
-            constexpr int lds = 4 * ClassSet<true>::wave_lds<BPC>();
-            static bool attr = false;
-            if (!attr) {
-                hipFuncSetAttribute((const void *)k_recon<BPC, true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-                attr = true;
-            }
-            k_recon<BPC, true><<<grid, 256, lds, stream>>>(a);
-        } else {
-            constexpr int lds = 4 * ClassSet<false>::wave_lds<BPC>();
-            static bool attr = false;
-            if (!attr) {
-                hipFuncSetAttribute((const void *)k_recon<BPC, false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-                attr = true;
-            }
-            k_recon<BPC, false><<<grid, 256, lds, stream>>>(a);
-        }
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) {
-            fprintf(stderr, "dav1d-gpu: recon launch failed: %s\n", hipGetErrorString(e));
-            return -3;
-        }
-    }
-    return 0;
+    int rc = launch_group<BPC, GROUP_SMALL>(a, b, classmask, stream);
+    if (!rc) rc = launch_group<BPC, GROUP_LARGE>(a, b, classmask, stream);
+    if (!rc) rc = launch_group<BPC, GROUP_HUGE>(a, b, classmask, stream);
+    return rc;
 }
 
 }  // namespace dgpu
-

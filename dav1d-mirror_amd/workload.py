@@ -300,8 +300,12 @@ def make_frame(cfg: FrameConfig) -> FrameData:
                     else:
                         coefs[o:o + a * b] = c[j, :b, :a].T.ravel()
 
-    # sort by (class, pred kind, filter / mode) so waves are uniform
-    order = np.lexsort((sort_minor, units["pred"], units["tx"]))
+    # sort by (class, picture band, pred kind, filter / mode): the kernel cuts
+    # each class into 16 equal segments scheduled together (spatial locality
+    # of the writes), and inside a band waves see uniform prediction kinds
+    ph = np.array([planes[p][1] for p in range(3)])
+    band = (uy * 16) // ph[plane_u]
+    order = np.lexsort((sort_minor, units["pred"], band, units["tx"]))
     units = units[order]
     counts = np.bincount(units["tx"], minlength=abi.N_TX)
     class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)

@@ -248,7 +248,8 @@ typedef struct Dav1dGpuUnit {
 } Dav1dGpuUnit;
 
 typedef struct Dav1dGpuPlane {
-    void    *data;        /* device pointer to pixel (0,0)                   */
+    void    *data;        /* device pointer to pixel (0,0); dst planes must be
+                             16-byte aligned with a 16-byte multiple stride */
     int64_t  stride;      /* bytes                                           */
     int32_t  w, h;        /* visible size (reference reads are clamped)      */
 } Dav1dGpuPlane;
@@ -274,9 +275,10 @@ typedef struct Dav1dGpuFrameBatch {
 int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream);
 int dav1d_gpu_recon_16bpc(const Dav1dGpuFrameBatch *b, void *stream);
 
-/* LDS bytes per 256-thread workgroup of the batch kernel (bpc 8/16; big=1:
- * the launch over transform sizes with a 64-point side).  Diagnostics. */
-int dav1d_gpu_recon_lds_bytes(int bpc, int big);
+/* LDS bytes per 256-thread workgroup of a batch kernel (bpc 8/16; group 0:
+ * transform sizes with w*h <= 128, 1: larger up to 32x32, 2: a 64-point
+ * side).  Diagnostics. */
+int dav1d_gpu_recon_lds_bytes(int bpc, int group);
 
 #ifdef __cplusplus
 }
