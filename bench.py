@@ -169,7 +169,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None,
-                "kernel": "k_recon<8,false>",
+                "kernel": f"k_recon<{cfg.bpc},0..2> (one launch per class group; events bracket the step's launches)",
                 "kernel_us": round(kern_s * 1e6, 2),
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "bytes_breakdown": {k: fd.stats[k] for k in

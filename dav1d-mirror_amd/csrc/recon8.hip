@@ -11,6 +11,10 @@ extern "C" int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream) {
 extern "C" int dav1d_gpu_recon_lds_bytes(int bpc, int group) {
     using namespace dgpu;
     if (bpc == 8)
-        return group == 0 ? 4 * wave_lds<8, 0>() : group == 1 ? 4 * wave_lds<8, 1>() : wave_lds<8, 2>();
-    return group == 0 ? 4 * wave_lds<16, 0>() : group == 1 ? 2 * wave_lds<16, 1>() : wave_lds<16, 2>();
+        return group == 0 ? waves_per_block<8, 0>() * wave_lds<8, 0>()
+             : group == 1 ? waves_per_block<8, 1>() * wave_lds<8, 1>()
+                          : waves_per_block<8, 2>() * wave_lds<8, 2>();
+    return group == 0 ? waves_per_block<16, 0>() * wave_lds<16, 0>()
+         : group == 1 ? waves_per_block<16, 1>() * wave_lds<16, 1>()
+                      : waves_per_block<16, 2>() * wave_lds<16, 2>();
 }

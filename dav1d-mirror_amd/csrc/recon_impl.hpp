@@ -32,10 +32,10 @@ template <int BPC, int GRP> __host__ __device__ constexpr int wave_lds() {
     return group_wave_lds<BPC, GRP>(std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 
-// waves per workgroup: one 64-lane wave for the 64-point classes (their LDS
-// slot alone is 37-47 KB), 4 otherwise (2 for 16bpc large units)
+// waves per workgroup: waves never share LDS, so small workgroups only
+// serve to pack the CU's LDS tightly (one wave for the 64-point classes)
 template <int BPC, int GRP> __host__ __device__ constexpr int waves_per_block() {
-    return GRP == GROUP_HUGE ? 1 : (BPC == 16 && GRP == GROUP_LARGE) ? 2 : 4;
+    return GRP == GROUP_HUGE ? 1 : 2;
 }
 
 template <int BPC, int TX, int GRP>
@@ -123,8 +123,11 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     for (int c = 0; c < DGPU_N_RECT_TX_SIZES; c++)
         if (b->class_start[c + 1] < b->class_start[c]) return -2;
     if (b->class_start[0] != 0 || b->class_start[DGPU_N_RECT_TX_SIZES] != b->n_units) return -2;
-    for (int p = 0; p < 3; p++)   // output rows are stored with aligned 4..16-byte stores
+    for (int p = 0; p < 3; p++) {   // output rows are stored with aligned 4/8-byte stores
         if (((uintptr_t)b->dst[p].data & 15) || (b->dst[p].stride & 15)) return -4;
+        for (int r = 0; r < DGPU_MAX_REFS; r++)   // footprint rows are read as aligned dwords
+            if (b->ref[r][p].data && (b->ref[r][p].stride & 3)) return -4;
+    }
     if (b->n_units == 0) return 0;
 
     ReconArgs<BPC> a;
@@ -143,11 +146,8 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     memcpy(a.class_start, b->class_start, sizeof(a.class_start));
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;
-    // debug-only knobs for profiling (never set in production):
-    //   DAV1D_GPU_ABLATE    phase mask (outputs wrong)
+    // debug-only profiling knob (never set in production):
     //   DAV1D_GPU_CLASSMASK restrict to some size classes (others stale)
-    const char *ev = getenv("DAV1D_GPU_ABLATE");
-    a.ablate = ev ? atoi(ev) : 0;
     const char *cm = getenv("DAV1D_GPU_CLASSMASK");
     const unsigned classmask = cm ? (unsigned)strtoul(cm, nullptr, 0) : ~0u;
 

@@ -7,22 +7,25 @@
 // :1294) then inv_txfm_add (:816 / :1347), fused so the prediction never
 // round-trips through HBM.
 //
-// Mapping (wave64, v2).  Units are sorted by transform size class.  A wave
-// owns U = 64 / G units of one class, G lanes each (G grows with the unit so
-// each lane has a handful of pixels).  Every phase is element-parallel over
-// the unit's G lanes -- no lane walks a whole column serially:
-//   P1  reference footprint(s): a fixed, unrolled count of dword loads per
-//       lane (all issued before any is consumed), kept at their byte skew
-//       in LDS; intra edges likewise; coefficient rows for P3 are loaded too
-//   P2  intra: directional / filter-intra edge preparation, then the
-//       prediction of every pixel into an LDS tile
-//   P3  row transforms (lane y < min(h,32)), transposed into LDS
-//   P4  column transforms (lane x < w) -> residual tile in LDS
-//   P5  mc horizontal pass: one 8-tap sum per (row, x) -- packed-byte
-//       v_dot4 on 8bpc -- into an int16 intermediate tile
-//   P6  mc vertical pass / compound average / intra tile, + residual, clip,
-//       into the output tile
-//   P7  output rows stored with aligned 4..16-byte stores
+// Mapping (wave64, v3).  Units are sorted by transform size class.  A unit
+// is cut into 4x2-pixel output tasks; a class gives each unit G = W*H/8
+// lanes (2..64), i.e. one task per lane, and a wave owns 64/G units.
+//   P1  global loads: descriptor, the compact coefficient region and intra
+//       edge array (16-B chunks into LDS), the mc footprint rows (dwordx4
+//       per row and 4-px quad, straight into registers)
+//   P2  mc horizontal pass, both refs: one task = 2 footprint rows x 4
+//       outputs; 8bpc uses v_alignbyte + v_dot4 on bias-shifted bytes, 16bpc
+//       v_dot2 on pixel pairs.  Intermediates are stored as (row 2p, row
+//       2p+1) int16 pairs so the vertical pass is v_dot2 as well.
+//   P3  row transforms (rows >= nzh are zero and skip the math)
+//   P4  column transforms -> residual, column-major
+//   P5  intra edge preparation / filter-intra wavefront
+//   P6  per task: vertical pass (+ compound average) or intra formula, add
+//       the residual, clip, and store 4-px rows straight to the picture.
+// Every 8-tap and bilinear case runs the same h+v pipeline: m == 0 is the
+// identity tap and bilinear is the (64 - 4m, 4m) bank, which give the
+// reference's h-only / v-only / copy / bilinear results exactly (the
+// rounding identities are spelled out in DESIGN.md section 4).
 // Every LDS hand-off stays inside one wave (no workgroup barrier).
 #pragma once
 #include "dav1d_gpu.h"
@@ -49,7 +52,6 @@ template <int BPC> struct ReconArgs {
     int nwaves;
     int bdmax;
     int zero_coefs;
-    int ablate;   // debug-only phase mask (DAV1D_GPU_ABLATE); 0 in production
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -62,11 +64,9 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 
-// size-class shape: lanes per unit G = clamp(w*h/4, 8, 64), at least
-// max(w, min(h,32)) so the 1-D transforms have a lane per line
+// lanes per unit: one 4x2 output task per lane, 2..64
 __host__ __device__ constexpr int lanes_per_unit(int tx) {
-    const int w = tx_info(tx).w, h = tx_info(tx).h, sh = cmin(h, 32);
-    return cmax(cmax(cmin(cmax(w * h / 4, 8), 64), w), sh);
+    return cmin(cmax(tx_info(tx).w * tx_info(tx).h / 8, 2), 64);
 }
 // class groups, each its own kernel (own register / LDS budget)
 enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2 };
@@ -78,31 +78,77 @@ __host__ __device__ constexpr int class_group(int tx) {
 template <int TX> struct Cls {
     static constexpr int W = tx_info(TX).w, H = tx_info(TX).h, SHIFT = tx_info(TX).shift;
     static constexpr int SW = cmin(W, 32), SH = cmin(H, 32);
-    static constexpr int G = lanes_per_unit(TX);
-    static constexpr int U = 64 / G;
+    static constexpr int G = lanes_per_unit(TX), U = 64 / G;
     static constexpr bool RECT2 = W * 2 == H || H * 2 == W;
+    static constexpr int QW = W / 4;            // 4-px quads per row
+    static constexpr int NT = H / 2 * QW;       // 4x2 output tasks
+    static constexpr int RP = (H + 8) / 2;      // mc intermediate row pairs (rows 0..H+7)
+    static constexpr int NH = RP * QW;          // h-pass tasks
 };
 
 template <int BPC> struct Tmp { using T = int32_t; };
-template <> struct Tmp<8> { using T = int16_t; };  // 8-bit column range is int16
+template <> struct Tmp<8> { using T = int16_t; };   // 8-bit row output / residual fit int16
 
-// LDS slot of one unit (bytes).  TMP holds the transposed row results, then
-// (aliased, consumed in program order) the residual tile and the output tile.
+// LDS slot of one unit (bytes): [coefs | residual] [row-pass tmp] [mc | intra]
 template <int BPC, int TX> struct Slot {
     using CL = Cls<TX>;
     static constexpr int W = CL::W, H = CL::H, B = BPC / 8;
-    static constexpr int TP = CL::SH + 1;
-    static constexpr int TMP = a16(cmax(W * TP * (int)sizeof(typename Tmp<BPC>::T), W * H * 2));
-    static constexpr int NDW = (3 + (W + 7) * B + 3) / 4;           // dwords per footprint row
-    static constexpr int FPB = NDW * 4;
-    static constexpr int FP = a16((H + 7) * FPB);
-    static constexpr int MID = a16((H + 7) * W * 2);
-    static constexpr int EDGE = 2 * H + 2 * W + 1;                   // topleft[-2h..2w]
-    static constexpr int INTRA = a16(2 * EDGE * 2 + W * H * 2);
-    static constexpr int SRC = cmax(2 * FP + 2 * MID, INTRA);
-    static constexpr int BYTES = TMP + SRC;
+    static constexpr int CB = sizeof(typename Px<BPC>::coef);
+    static constexpr int TB = sizeof(typename Tmp<BPC>::T);
+    static constexpr int CF = a16(CL::SW * CL::SH * CB + 16);   // compact coefs at their 16-B skew
+    static constexpr int RES = W * H * TB;                       // residual, column-major [x][y]
+    static constexpr int CFR = a16(cmax(CF, RES));
+    static constexpr int TMP = a16(CL::SH * W * TB);             // row-pass output [y][x]
+    static constexpr int MID = CL::RP * W * 4;                   // one ref: [row pair][x] int16 x2
+    static constexpr int EDGE = 2 * H + 2 * W + 1;               // topleft[-2h..2w]
+    static constexpr int EB = a16(EDGE * B + 16);                // raw edge pixels at their skew
+    static constexpr int FE = a16(EDGE * 2);                     // prepared edge, int16
+    static constexpr int PT = a16(W * H * 2);                    // filter-intra tile, int16
+    static constexpr int SRC = cmax(2 * MID, EB + FE + PT);
+    static constexpr int BYTES = CFR + TMP + SRC;
     static constexpr int WAVE = CL::U * BYTES;
 };
+
+// ------------------------------------------------------------ primitives ---
+
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, a), __builtin_bit_cast(v2i16, b), c, false);
+}
+__device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+// ({hi, lo} >> 8s)[31:0]
+__device__ __forceinline__ uint32_t alb(uint32_t hi, uint32_t lo, int s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+// (lo16(lo), lo16(hi)) -- int16 truncation, as the reference's int16_t stores
+__device__ __forceinline__ uint32_t pack16(int lo, int hi) {
+    return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+
+// Copies bytes [src, src + n) into 16-B aligned LDS at their own 16-B skew
+// (returned) with 16-byte loads.  Reads stay inside the 16-B blocks holding
+// the first and last byte.
+template <int MAXN, int G>
+__device__ __forceinline__ int stage16(uint8_t *dst, const void *src, int n, int l) {
+    const int sk = (int)(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint4 *s = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(src) - sk);
+    const int nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
+    constexpr int IT = ((MAXN + 30) / 16 + G - 1) / G;
+    uint4 v[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) v[k] = s[min(l + k * G, nch - 1)];   // clamped: always a valid block
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const int i = l + k * G;
+        if (i < nch) reinterpret_cast<uint4 *>(dst)[i] = v[k];
+    }
+    return sk;
+}
 
 // ---------------------------------------------------------------- intra ---
 
@@ -123,8 +169,8 @@ __device__ __forceinline__ int ip_upsample(int wh, int angle, int is_sm) {
     return angle < 40 && wh <= (16 >> is_sm);
 }
 // filter_edge element (src/ipred_tmpl.c:362-385), `in` indexed from 0
-__device__ __forceinline__ int ip_smooth(const int16_t *in, int i, int lim_from, int lim_to, int from,
-                                         int to, int st) {
+template <typename T>
+__device__ __forceinline__ int ip_smooth(const T *in, int i, int lim_from, int lim_to, int from, int to, int st) {
     if (i < lim_from || i >= lim_to) return in[clampi(i, from, to - 1)];
     const int k0 = st == 3 ? 2 : 0, k1 = st == 2 ? 5 : 4, k2 = st == 1 ? 8 : st == 2 ? 6 : 4;
     const int s = k0 * (in[clampi(i - 2, from, to - 1)] + in[clampi(i + 2, from, to - 1)]) +
@@ -133,7 +179,8 @@ __device__ __forceinline__ int ip_smooth(const int16_t *in, int i, int lim_from,
     return (s + 8) >> 4;
 }
 // upsample_edge element (src/ipred_tmpl.c:391-406)
-__device__ __forceinline__ int ip_up(const int16_t *in, int o, int hsz, int from, int to, int bdmax) {
+template <typename T>
+__device__ __forceinline__ int ip_up(const T *in, int o, int hsz, int from, int to, int bdmax) {
     const int i = o >> 1;
     if (!(o & 1) || i >= hsz - 1) return in[clampi(i, from, to - 1)];
     const int s = -in[clampi(i - 1, from, to - 1)] + 9 * in[clampi(i, from, to - 1)] +
@@ -141,63 +188,66 @@ __device__ __forceinline__ int ip_up(const int16_t *in, int o, int hsz, int from
     return clampi((s + 8) >> 4, 0, bdmax);
 }
 
-// intra prediction of one unit into `ptile` (int16, W x H), all G lanes.
-// e: topleft[-2h..2w] staged as int16; fe: scratch edge.
-template <int BPC, int TX>
-__device__ __forceinline__ void intra_unit(const Dav1dGpuUnit &u, int16_t *e, int16_t *fe, int16_t *ptile,
-                                           int l, int bdmax) {
+// Per-unit intra state after edge preparation.
+struct IntraState {
+    int mode, up, upl, d1, d2, maxb, dc;
+};
+
+// Edge preparation for the directional modes (into fe) and the DC-family
+// value; all G lanes of the unit.  tl = topleft pixel in the staged edge.
+template <int BPC, int TX, typename P>
+__device__ __forceinline__ IntraState intra_prep(const Dav1dGpuUnit &u, const P *tl, int16_t *fe, int l,
+                                                 int bdmax) {
     using CL = Cls<TX>;
     constexpr int W = CL::W, H = CL::H, G = CL::G;
-    const int16_t *tl = e + 2 * H;   // topleft[0]
-    const int mode = u.p.intra.mode;
+    IntraState s{u.p.intra.mode, 0, 0, 0, 0, 0, 0};
     const int ang = u.p.intra.angle & 511, is_sm = (u.p.intra.angle >> 9) & 1, filt = u.p.intra.angle >> 10;
-    int up = 0, upl = 0, d1 = 0, d2 = 0, maxb = 0, dc = 0;
-    if (mode == DGPU_Z1_PRED) {   // src/ipred_tmpl.c:408-443
-        d1 = dspt_dr_deriv[ang >> 1];
-        up = filt ? ip_upsample(W + H, 90 - ang, is_sm) : 0;
-        const int st = (!up && filt) ? ip_strength(W + H, 90 - ang, is_sm) : 0;
-        if (up) {
+    if (s.mode == DGPU_Z1_PRED) {   // src/ipred_tmpl.c:408-443
+        s.d1 = dspt_dr_deriv[ang >> 1];
+        s.up = filt ? ip_upsample(W + H, 90 - ang, is_sm) : 0;
+        const int st = (!s.up && filt) ? ip_strength(W + H, 90 - ang, is_sm) : 0;
+        if (s.up) {
             for (int o = l; o < 2 * (W + H) - 1; o += G) fe[o] = ip_up(tl + 1, o, W + H, -1, W + cmin(W, H), bdmax);
-            maxb = 2 * (W + H) - 2;
-            d1 <<= 1;
+            s.maxb = 2 * (W + H) - 2;
+            s.d1 <<= 1;
         } else if (st) {
             for (int i = l; i < W + H; i += G) fe[i] = ip_smooth(tl + 1, i, 0, W + H, -1, W + cmin(W, H), st);
-            maxb = W + H - 1;
+            s.maxb = W + H - 1;
         } else {
             for (int i = l; i < W + cmin(W, H); i += G) fe[i] = tl[1 + i];
-            maxb = W + cmin(W, H) - 1;
+            s.maxb = W + cmin(W, H) - 1;
         }
-    } else if (mode == DGPU_Z3_PRED) {   // src/ipred_tmpl.c:542-581; fe[maxb - i] == left[-i]
-        d1 = dspt_dr_deriv[(270 - ang) >> 1];
-        up = filt ? ip_upsample(W + H, ang - 180, is_sm) : 0;
-        const int st = (!up && filt) ? ip_strength(W + H, ang - 180, is_sm) : 0;
-        if (up) {
+    } else if (s.mode == DGPU_Z3_PRED) {   // src/ipred_tmpl.c:542-581; fe[maxb - i] == left[-i]
+        s.d1 = dspt_dr_deriv[(270 - ang) >> 1];
+        s.up = filt ? ip_upsample(W + H, ang - 180, is_sm) : 0;
+        const int st = (!s.up && filt) ? ip_strength(W + H, ang - 180, is_sm) : 0;
+        if (s.up) {
             for (int o = l; o < 2 * (W + H) - 1; o += G)
                 fe[o] = ip_up(tl - (W + H), o, W + H, cmax(W - H, 0), W + H + 1, bdmax);
-            maxb = 2 * (W + H) - 2;
-            d1 <<= 1;
+            s.maxb = 2 * (W + H) - 2;
+            s.d1 <<= 1;
         } else if (st) {
             for (int i = l; i < W + H; i += G)
                 fe[i] = ip_smooth(tl - (W + H), i, 0, W + H, cmax(W - H, 0), W + H + 1, st);
-            maxb = W + H - 1;
+            s.maxb = W + H - 1;
         } else {
-            maxb = H + cmin(W, H) - 1;
-            for (int i = l; i <= maxb; i += G) fe[i] = tl[-1 - maxb + i];
+            s.maxb = H + cmin(W, H) - 1;
+            for (int i = l; i <= s.maxb; i += G) fe[i] = tl[-1 - s.maxb + i];
         }
-    } else if (mode == DGPU_Z2_PRED) {   // src/ipred_tmpl.c:462-513
-        d2 = dspt_dr_deriv[(ang - 90) >> 1];   // dy
-        d1 = dspt_dr_deriv[(180 - ang) >> 1];  // dx
-        upl = filt ? ip_upsample(W + H, 180 - ang, is_sm) : 0;
-        up = filt ? ip_upsample(W + H, ang - 90, is_sm) : 0;
+    } else if (s.mode == DGPU_Z2_PRED) {   // src/ipred_tmpl.c:462-513
+        s.d2 = dspt_dr_deriv[(ang - 90) >> 1];   // dy
+        s.d1 = dspt_dr_deriv[(180 - ang) >> 1];  // dx
+        s.upl = filt ? ip_upsample(W + H, 180 - ang, is_sm) : 0;
+        s.up = filt ? ip_upsample(W + H, ang - 90, is_sm) : 0;
         int16_t *c = fe + 2 * H;   // corner
-        if (up) {
+        if (s.up) {
             for (int o = l; o < 2 * W + 1; o += G) c[o] = ip_up(tl, o, W + 1, 0, W + 1, bdmax);
         } else {
             const int st = filt ? ip_strength(W + H, ang - 90, is_sm) : 0;
             for (int i = l; i < W; i += G)
                 c[1 + i] = st ? ip_smooth(tl + 1, i, 0, u.p.intra.max_w, -1, W, st) : tl[1 + i];
         }
-        if (upl) {
+        if (s.upl) {
             for (int o = l; o < 2 * H + 1; o += G) c[-2 * H + o] = ip_up(tl - H, o, H + 1, 0, H + 1, bdmax);
         } else {
             const int st = filt ? ip_strength(W + H, 180 - ang, is_sm) : 0;
@@ -206,41 +256,9 @@ __device__ __forceinline__ void intra_unit(const Dav1dGpuUnit &u, int16_t *e, in
         }
         wave_sync();
         if (l == 0) c[0] = tl[0];
-        if (up) d1 <<= 1;
-        if (upl) d2 <<= 1;
-    } else if (mode == DGPU_FILTER_PRED) {   // src/ipred_tmpl.c:617-655, cells in anti-diagonal waves
-        if constexpr (W <= 32 && H <= 32) {
-            const signed char *taps = &dspt_filter_intra[(u.p.intra.angle & 511) * 56];
-            constexpr int cw = W / 4, ch = H / 2;
-            for (int step = 0; step < cw + ch - 1; step++) {
-                for (int cidx = l; cidx < cw * ch; cidx += G) {
-                    const int cx = cidx % cw, cy = cidx / cw;
-                    if (cx + cy != step) continue;
-                    const int x = cx * 4, y = cy * 2;
-                    int p0, p1, p2, p3, p4, p5, p6;
-                    if (y == 0) {
-                        p0 = x == 0 ? tl[0] : tl[x];
-                        p1 = tl[1 + x]; p2 = tl[2 + x]; p3 = tl[3 + x]; p4 = tl[4 + x];
-                    } else {
-                        const int16_t *upr = ptile + (y - 1) * W + x;
-                        p0 = x == 0 ? tl[-y] : upr[-1];
-                        p1 = upr[0]; p2 = upr[1]; p3 = upr[2]; p4 = upr[3];
-                    }
-                    p5 = x == 0 ? tl[-(y + 1)] : ptile[y * W + x - 1];
-                    p6 = x == 0 ? tl[-(y + 2)] : ptile[(y + 1) * W + x - 1];
-#pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        const signed char *tk = taps + k * 7;
-                        const int acc = tk[0] * p0 + tk[1] * p1 + tk[2] * p2 + tk[3] * p3 + tk[4] * p4 +
-                                        tk[5] * p5 + tk[6] * p6;
-                        ptile[(y + (k >> 2)) * W + x + (k & 3)] = clampi((acc + 8) >> 4, 0, bdmax);
-                    }
-                }
-                wave_sync();
-            }
-        }
-        return;
-    } else if (mode != DGPU_VERT_PRED && mode != DGPU_HOR_PRED && mode <= DGPU_DC_128_PRED) {
+        if (s.up) s.d1 <<= 1;
+        if (s.upl) s.d2 <<= 1;
+    } else if (s.mode != DGPU_VERT_PRED && s.mode != DGPU_HOR_PRED && s.mode <= DGPU_DC_128_PRED) {
         // DC family: group reduction of the edge sums (src/ipred_tmpl.c:86-166)
         unsigned st = 0, sl = 0;
         for (int i = l; i < W; i += G) st += tl[1 + i];
@@ -250,117 +268,292 @@ __device__ __forceinline__ void intra_unit(const Dav1dGpuUnit &u, int16_t *e, in
             st += __shfl_xor(st, off, 64);
             sl += __shfl_xor(sl, off, 64);
         }
-        unsigned s;
-        if (mode == DGPU_DC_128_PRED) s = (bdmax + 1) >> 1;
-        else if (mode == DGPU_TOP_DC_PRED) s = (st + (W >> 1)) >> __builtin_ctz(W);
-        else if (mode == DGPU_LEFT_DC_PRED) s = (sl + (H >> 1)) >> __builtin_ctz(H);
+        unsigned v;
+        if (s.mode == DGPU_DC_128_PRED) v = (bdmax + 1) >> 1;
+        else if (s.mode == DGPU_TOP_DC_PRED) v = (st + (W >> 1)) >> __builtin_ctz(W);
+        else if (s.mode == DGPU_LEFT_DC_PRED) v = (sl + (H >> 1)) >> __builtin_ctz(H);
         else {
-            s = (st + sl + ((W + H) >> 1)) >> __builtin_ctz(W + H);
+            v = (st + sl + ((W + H) >> 1)) >> __builtin_ctz(W + H);
             if (W != H) {
                 const bool r4 = W > 2 * H || H > 2 * W;
-                if (BPC == 8) s = (s * (r4 ? 0x3334u : 0x5556u)) >> 16;
-                else s = (s * (r4 ? 0x6667u : 0xAAABu)) >> 17;
+                if (BPC == 8) v = (v * (r4 ? 0x3334u : 0x5556u)) >> 16;
+                else v = (v * (r4 ? 0x6667u : 0xAAABu)) >> 17;
             }
         }
-        dc = (int)s;
+        s.dc = (int)v;
     }
-    wave_sync();
-    for (int i = l; i < W * H; i += G) {
-        const int x = i % W, y = i / W;
-        const int top = tl[1 + x], left = tl[-(1 + y)];
-        int v;
-        switch (mode) {
-        case DGPU_VERT_PRED: v = top; break;
-        case DGPU_HOR_PRED: v = left; break;
-        case DGPU_PAETH_PRED: {   // src/ipred_tmpl.c:244-265
-            const int c0 = tl[0], base = left + top - c0;
+    return s;
+}
+
+// Intra prediction of one 4x2 task (x0 = 4q, rows y0, y0 + 1) into pv[8]
+// (row-major), for every mode but FILTER_PRED.
+template <int TX, typename P>
+__device__ __forceinline__ void intra_task(const IntraState &s, const P *tl, const int16_t *fe, int x0, int y0,
+                                           int *pv) {
+    using CL = Cls<TX>;
+    constexpr int W = CL::W, H = CL::H;
+    switch (s.mode) {
+    case DGPU_VERT_PRED:
+#pragma unroll
+        for (int i = 0; i < 8; i++) pv[i] = tl[1 + x0 + (i & 3)];
+        break;
+    case DGPU_HOR_PRED:
+#pragma unroll
+        for (int i = 0; i < 8; i++) pv[i] = tl[-(1 + y0 + (i >> 2))];
+        break;
+    case DGPU_PAETH_PRED: {   // src/ipred_tmpl.c:244-265
+        const int c0 = tl[0];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int top = tl[1 + x0 + (i & 3)], left = tl[-(1 + y0 + (i >> 2))];
+            const int base = left + top - c0;
             const int dl = abs(left - base), dt = abs(top - base), dd = abs(c0 - base);
-            v = (dl <= dt && dl <= dd) ? left : dt <= dd ? top : c0;
-            break;
+            pv[i] = (dl <= dt && dl <= dd) ? left : dt <= dd ? top : c0;
         }
-        case DGPU_SMOOTH_PRED: {   // src/ipred_tmpl.c:267-325
+        break;
+    }
+    case DGPU_SMOOTH_PRED: {   // src/ipred_tmpl.c:267-325
+        const int bl = tl[-H], tr = tl[W];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int x = x0 + (i & 3), y = y0 + (i >> 2);
             const int wv = dspt_sm_weights[H + y], wh = dspt_sm_weights[W + x];
-            v = (wv * top + (256 - wv) * tl[-H] + wh * left + (256 - wh) * tl[W] + 256) >> 9;
-            break;
+            pv[i] = (wv * tl[1 + x] + (256 - wv) * bl + wh * tl[-(1 + y)] + (256 - wh) * tr + 256) >> 9;
         }
-        case DGPU_SMOOTH_V_PRED: {
-            const int wv = dspt_sm_weights[H + y];
-            v = (wv * top + (256 - wv) * tl[-H] + 128) >> 8;
-            break;
+        break;
+    }
+    case DGPU_SMOOTH_V_PRED: {
+        const int bl = tl[-H];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int wv = dspt_sm_weights[H + y0 + (i >> 2)];
+            pv[i] = (wv * tl[1 + x0 + (i & 3)] + (256 - wv) * bl + 128) >> 8;
         }
-        case DGPU_SMOOTH_H_PRED: {
-            const int wh = dspt_sm_weights[W + x];
-            v = (wh * left + (256 - wh) * tl[W] + 128) >> 8;
-            break;
+        break;
+    }
+    case DGPU_SMOOTH_H_PRED: {
+        const int tr = tl[W];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int wh = dspt_sm_weights[W + x0 + (i & 3)];
+            pv[i] = (wh * tl[-(1 + y0 + (i >> 2))] + (256 - wh) * tr + 128) >> 8;
         }
-        case DGPU_Z1_PRED: {
-            const int xpos = (y + 1) * d1, frac = xpos & 0x3e;
-            const int base = (xpos >> 6) + x * (1 + up);
-            v = base < maxb ? (fe[base] * (64 - frac) + fe[base + 1] * frac + 32) >> 6 : fe[maxb];
-            break;
+        break;
+    }
+    case DGPU_Z1_PRED:
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int x = x0 + (i & 3), y = y0 + (i >> 2);
+            const int xpos = (y + 1) * s.d1, frac = xpos & 0x3e;
+            const int base = (xpos >> 6) + x * (1 + s.up);
+            pv[i] = base < s.maxb ? (fe[base] * (64 - frac) + fe[base + 1] * frac + 32) >> 6 : fe[s.maxb];
         }
-        case DGPU_Z3_PRED: {
-            const int ypos = (x + 1) * d1, frac = ypos & 0x3e;
-            const int base = (ypos >> 6) + y * (1 + up);
-            v = base < maxb ? (fe[maxb - base] * (64 - frac) + fe[maxb - base - 1] * frac + 32) >> 6 : fe[0];
-            break;
+        break;
+    case DGPU_Z3_PRED:
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int x = x0 + (i & 3), y = y0 + (i >> 2);
+            const int ypos = (x + 1) * s.d1, frac = ypos & 0x3e;
+            const int base = (ypos >> 6) + y * (1 + s.up);
+            pv[i] = base < s.maxb ? (fe[s.maxb - base] * (64 - frac) + fe[s.maxb - base - 1] * frac + 32) >> 6
+                                  : fe[0];
         }
-        case DGPU_Z2_PRED: {
-            const int16_t *c = fe + 2 * H;
-            const int xpos = ((1 + up) << 6) - (y + 1) * d1;
-            const int bx = (xpos >> 6) + x * (1 + up);
+        break;
+    case DGPU_Z2_PRED: {
+        const int16_t *c = fe + 2 * H;
+        const int16_t *lft = c - (1 + s.upl);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int x = x0 + (i & 3), y = y0 + (i >> 2);
+            const int xpos = ((1 + s.up) << 6) - (y + 1) * s.d1;
+            const int bx = (xpos >> 6) + x * (1 + s.up);
             int t;
             if (bx >= 0) {
                 const int fx = xpos & 0x3e;
                 t = c[bx] * (64 - fx) + c[bx + 1] * fx;
             } else {
-                const int ypos = (y << (6 + upl)) - (x + 1) * d2;
+                const int ypos = (y << (6 + s.upl)) - (x + 1) * s.d2;
                 const int by = ypos >> 6, fy = ypos & 0x3e;
-                const int16_t *lft = c - (1 + upl);
                 t = lft[-by] * (64 - fy) + lft[-(by + 1)] * fy;
             }
-            v = (t + 32) >> 6;
-            break;
+            pv[i] = (t + 32) >> 6;
         }
-        default: v = dc; break;   // DC family
+        break;
+    }
+    default:   // DC family
+#pragma unroll
+        for (int i = 0; i < 8; i++) pv[i] = s.dc;
+        break;
+    }
+}
+
+// Filter intra (src/ipred_tmpl.c:617-655): 4x2 cells == output tasks, run in
+// anti-diagonal waves, into ptile.
+template <int TX, typename P>
+__device__ __forceinline__ void filter_intra(const Dav1dGpuUnit &u, const P *tl, int16_t *ptile, int l, int bdmax) {
+    using CL = Cls<TX>;
+    constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NT = CL::NT;
+    constexpr int TPL = (NT + G - 1) / G;
+    const signed char *taps = &dspt_filter_intra[(u.p.intra.angle & 511) * 56];
+    for (int step = 0; step < QW + H / 2 - 1; step++) {
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            const int cy = t / QW, cx = t % QW;
+            if (t < NT && cx + cy == step) {
+                const int x = cx * 4, y = cy * 2;
+                int p0, p1, p2, p3, p4, p5, p6;
+                if (y == 0) {
+                    p0 = tl[x];
+                    p1 = tl[1 + x]; p2 = tl[2 + x]; p3 = tl[3 + x]; p4 = tl[4 + x];
+                } else {
+                    const int16_t *upr = ptile + (y - 1) * W + x;
+                    p0 = x == 0 ? (int)tl[-y] : upr[-1];
+                    p1 = upr[0]; p2 = upr[1]; p3 = upr[2]; p4 = upr[3];
+                }
+                p5 = x == 0 ? (int)tl[-(y + 1)] : ptile[y * W + x - 1];
+                p6 = x == 0 ? (int)tl[-(y + 2)] : ptile[(y + 1) * W + x - 1];
+#pragma unroll
+                for (int o = 0; o < 8; o++) {
+                    const signed char *tk = taps + o * 7;
+                    const int acc = tk[0] * p0 + tk[1] * p1 + tk[2] * p2 + tk[3] * p3 + tk[4] * p4 +
+                                    tk[5] * p5 + tk[6] * p6;
+                    ptile[(y + (o >> 2)) * W + x + (o & 3)] = (int16_t)clampi((acc + 8) >> 4, 0, bdmax);
+                }
+            }
         }
-        ptile[i] = (int16_t)v;
+        wave_sync();
     }
 }
 
 // ------------------------------------------------------------------ mc -----
 
-// 8-tap kernel as two packed dwords (signed bytes), or {0,0} for m == 0
-struct Taps { uint32_t lo, hi; const signed char *k; };
-__device__ __forceinline__ Taps get_taps(int t, int m, int len) {
-    Taps r{0, 0, nullptr};
-    const signed char *k = subpel_kernel(t, m, len);
-    r.k = k;
-    if (k) {
-        r.lo = (uint8_t)k[0] | (uint32_t)(uint8_t)k[1] << 8 | (uint32_t)(uint8_t)k[2] << 16 | (uint32_t)(uint8_t)k[3] << 24;
-        r.hi = (uint8_t)k[4] | (uint32_t)(uint8_t)k[5] << 8 | (uint32_t)(uint8_t)k[6] << 16 | (uint32_t)(uint8_t)k[7] << 24;
-    }
-    return r;
+// filter bank for one direction: bilinear (x4), 8-tap, or the 4-tap bank
+// for a block extent <= 4 (src/mc_tmpl.c:99-107); m == 0 is the identity
+__device__ __forceinline__ int mc_bank(int type, bool bil, int len) {
+    return bil ? 5 : len > 4 ? type : 3 + (type & 1);
 }
 
-// Horizontal 8-tap sum over footprint bytes [boff, boff+8) of an 8bpc row
-// (dword-aligned row start): v_alignbyte to the window, then two v_dot4 on
-// bias-shifted bytes (p ^ 0x80 == p - 128; taps sum to 64 -> + 128 * 64).
-__device__ __forceinline__ int hsum8(const uint8_t *row, int boff, const Taps &t) {
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(row) + (boff >> 2);
-    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
-    const int s = boff & 3;
-    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, s) ^ 0x80808080u;
-    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, s) ^ 0x80808080u;
-    int acc = __builtin_amdgcn_sdot4((int)w0, (int)t.lo, 0, false);
-    acc = __builtin_amdgcn_sdot4((int)w1, (int)t.hi, acc, false);
-    return acc + 128 * 64;
-}
-__device__ __forceinline__ int hsum16(const uint16_t *row, const Taps &t) {
-    int s = 0;
+// Horizontal pass of one reference: NH tasks of (row pair p, quad q) ->
+// mid[p * W + 4q .. +3] = (row 2p, row 2p+1) int16 pairs.  `org` is the
+// footprint origin (block position - 3 rows - 3 columns).
+template <int BPC, int TX>
+__device__ __forceinline__ void mc_hpass(const typename Px<BPC>::pixel *org, int stride_px, uint32_t *mid,
+                                         int bank, int m, int ib, int l) {
+    using CL = Cls<TX>;
+    constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NH = CL::NH;
+    constexpr int IT = (NH + G - 1) / G;
+    const int sk = (int)(reinterpret_cast<uintptr_t>(org) & 3);
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(org) - sk;
+    const int sb = stride_px * (BPC / 8);
+    if constexpr (BPC == 8) {
+        const uint2 th = reinterpret_cast<const uint2 *>(dspt_mc8)[bank * 16 + m];
+        u32x4a4 raw[IT][2];
 #pragma unroll
-    for (int i = 0; i < 8; i++) s += t.k[i] * (int)row[i];
-    return s;
+        for (int k = 0; k < IT; k++) {   // clamped task: the loads are always in the footprint
+            const int t = min(l + k * G, NH - 1);
+            const int p = t / QW, q = t % QW;
+            const int r0 = 2 * p, r1 = min(2 * p + 1, H + 6);   // row H+7 is never used
+            raw[k][0] = *reinterpret_cast<const u32x4a4 *>(base + r0 * sb + 4 * q);
+            raw[k][1] = *reinterpret_cast<const u32x4a4 *>(base + r1 * sb + 4 * q);
+        }
+        // taps sum to 64 and p ^ 0x80 == p - 128 as int8: s = acc + 128 * 64;
+        // mid = (s + 2) >> 2 (intermediate_bits 4)
+        constexpr int C = 128 * 64 + 2;
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int t = l + k * G;
+            if (t < NH) {
+                const int p = t / QW, q = t % QW;
+                int mm[2][4];
+#pragma unroll
+                for (int rr = 0; rr < 2; rr++) {
+                    const u32x4a4 d = raw[k][rr];
+                    const uint32_t w0 = alb(d.y, d.x, sk) ^ 0x80808080u;
+                    const uint32_t w1 = alb(d.z, d.y, sk) ^ 0x80808080u;
+                    const uint32_t w2 = alb(d.w, d.z, sk) ^ 0x80808080u;
+                    mm[rr][0] = dot4(w1, th.y, dot4(w0, th.x, C)) >> 2;
+                    mm[rr][1] = dot4(alb(w2, w1, 1), th.y, dot4(alb(w1, w0, 1), th.x, C)) >> 2;
+                    mm[rr][2] = dot4(alb(w2, w1, 2), th.y, dot4(alb(w1, w0, 2), th.x, C)) >> 2;
+                    mm[rr][3] = dot4(alb(w2, w1, 3), th.y, dot4(alb(w1, w0, 3), th.x, C)) >> 2;
+                }
+                uint4 o;
+                o.x = pack16(mm[0][0], mm[1][0]);
+                o.y = pack16(mm[0][1], mm[1][1]);
+                o.z = pack16(mm[0][2], mm[1][2]);
+                o.w = pack16(mm[0][3], mm[1][3]);
+                *reinterpret_cast<uint4 *>(mid + p * W + 4 * q) = o;
+            }
+        }
+    } else {
+        const uint4 th = reinterpret_cast<const uint4 *>(dspt_mc16)[bank * 16 + m];
+        const int sh = 6 - ib, rnd = (1 << sh) >> 1;
+        u32x4a4 ra[IT][2];
+        u32x2a4 rb[IT][2];
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int t = min(l + k * G, NH - 1);
+            const int p = t / QW, q = t % QW;
+            const int r0 = 2 * p, r1 = min(2 * p + 1, H + 6);
+            const uint8_t *a0 = base + r0 * sb + 8 * q, *a1 = base + r1 * sb + 8 * q;
+            ra[k][0] = *reinterpret_cast<const u32x4a4 *>(a0);
+            rb[k][0] = *reinterpret_cast<const u32x2a4 *>(a0 + 16);
+            ra[k][1] = *reinterpret_cast<const u32x4a4 *>(a1);
+            rb[k][1] = *reinterpret_cast<const u32x2a4 *>(a1 + 16);
+        }
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int t = l + k * G;
+            if (t < NH) {
+                const int p = t / QW, q = t % QW;
+                int mm[2][4];
+#pragma unroll
+                for (int rr = 0; rr < 2; rr++) {
+                    const uint32_t d[6] = {ra[k][rr].x, ra[k][rr].y, ra[k][rr].z, ra[k][rr].w,
+                                           rb[k][rr].x, rb[k][rr].y};
+                    uint32_t e[6], o[5];   // e: pixel pairs (2i, 2i+1), o: (2i+1, 2i+2)
+#pragma unroll
+                    for (int i = 0; i < 5; i++) e[i] = alb(d[i + 1], d[i], sk);
+                    e[5] = alb(d[5], d[5], sk);   // only its low half (pixel 10) is used
+#pragma unroll
+                    for (int i = 0; i < 5; i++) o[i] = alb(e[i + 1], e[i], 2);
+                    const int s0 = dot2(e[3], th.w, dot2(e[2], th.z, dot2(e[1], th.y, dot2(e[0], th.x, 0))));
+                    const int s1 = dot2(o[3], th.w, dot2(o[2], th.z, dot2(o[1], th.y, dot2(o[0], th.x, 0))));
+                    const int s2 = dot2(e[4], th.w, dot2(e[3], th.z, dot2(e[2], th.y, dot2(e[1], th.x, 0))));
+                    const int s3 = dot2(o[4], th.w, dot2(o[3], th.z, dot2(o[2], th.y, dot2(o[1], th.x, 0))));
+                    mm[rr][0] = (s0 + rnd) >> sh;
+                    mm[rr][1] = (s1 + rnd) >> sh;
+                    mm[rr][2] = (s2 + rnd) >> sh;
+                    mm[rr][3] = (s3 + rnd) >> sh;
+                }
+                uint4 o;
+                o.x = pack16(mm[0][0], mm[1][0]);
+                o.y = pack16(mm[0][1], mm[1][1]);
+                o.z = pack16(mm[0][2], mm[1][2]);
+                o.w = pack16(mm[0][3], mm[1][3]);
+                *reinterpret_cast<uint4 *>(mid + p * W + 4 * q) = o;
+            }
+        }
+    }
+}
+
+// Vertical pass of one reference for a 4x2 task: t[i] = the 8-tap sum over
+// intermediates, rows j*2 (i < 4) and j*2+1 (i >= 4), columns 4q + (i & 3).
+template <int W>
+__device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, const uint4 tv, int *t) {
+    uint32_t P[5][4];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(mid + (j + k) * W + 4 * q);
+        P[k][0] = v.x; P[k][1] = v.y; P[k][2] = v.z; P[k][3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        t[i] = dot2(P[3][i], tv.w, dot2(P[2][i], tv.z, dot2(P[1][i], tv.y, dot2(P[0][i], tv.x, 0))));
+        t[4 + i] = dot2(alb(P[4][i], P[3][i], 2), tv.w,
+                        dot2(alb(P[3][i], P[2][i], 2), tv.z,
+                             dot2(alb(P[2][i], P[1][i], 2), tv.y, dot2(alb(P[1][i], P[0][i], 2), tv.x, 0))));
+    }
 }
 
 // ---------------------------------------------------------------- kernel --
@@ -370,269 +563,235 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
     using CL = Cls<TX>;
     using SL = Slot<BPC, TX>;
     using P = typename Px<BPC>::pixel;
+    using C = typename Px<BPC>::coef;
     using TT = typename Tmp<BPC>::T;
-    constexpr int W = CL::W, H = CL::H, SH = CL::SH, G = CL::G, B = BPC / 8;
+    constexpr int W = CL::W, H = CL::H, SW = CL::SW, SH = CL::SH, G = CL::G, QW = CL::QW, NT = CL::NT;
+    constexpr int TPL = (NT + G - 1) / G;
     const int lane = threadIdx.x & 63;
     const int g = lane / G, l = lane % G;
     if (g >= count) return;
 
     const Dav1dGpuUnit u = a.units[first + g];
     uint8_t *slot = wave_lds + g * SL::BYTES;
-    TT *tmp = reinterpret_cast<TT *>(slot);
-    int16_t *restile = reinterpret_cast<int16_t *>(slot);     // aliases tmp (read before written)
-    P *otile = reinterpret_cast<P *>(slot);                    // aliases restile, same index order
-    uint8_t *srcl = slot + SL::TMP;
+    uint8_t *cfl = slot;                                           // staged coefs, then residual
+    TT *res = reinterpret_cast<TT *>(slot);
+    TT *tmp = reinterpret_cast<TT *>(slot + SL::CFR);
+    uint8_t *src = slot + SL::CFR + SL::TMP;
+    uint32_t *mid0 = reinterpret_cast<uint32_t *>(src);
+    uint32_t *mid1 = reinterpret_cast<uint32_t *>(src + SL::MID);
+    int16_t *fe = reinterpret_cast<int16_t *>(src + SL::EB);
+    int16_t *ptile = reinterpret_cast<int16_t *>(src + SL::EB + SL::FE);
+
     const int plane = u.plane;
     const int bdmax = a.bdmax;
     const int ib = Px<BPC>::ibits(bdmax);
-    const int PB = Px<BPC>::PBIAS;
     const int pred = u.pred;
     const bool inter = pred == DGPU_PRED_INTER || pred == DGPU_PRED_INTER_AVG;
     const bool comp = pred == DGPU_PRED_INTER_AVG;
     const int txtp = u.txtp;
     const bool nores = txtp == DGPU_NO_RESIDUAL;
-    const bool dconly = !nores && u.nzw == 0;
+    const int nzw = u.nzw, nzh = u.nzh;
+    const bool dconly = !nores && nzw == 0;
+    const bool haveres = !nores && !dconly;
+    P *dstp = a.dst[plane] + u.dst_off;
+    const int ds = a.dst_stride[plane];
 
-    // ---------------- P1: issue every global load of the unit ----------------
-    int sk0 = 0, sk1 = 0;   // byte skew of each footprint in its LDS rows
-    if (inter && !(a.ablate & 1)) {
-        constexpr int TOT = (H + 7) * SL::NDW;
-        constexpr int NIT = (TOT + G - 1) / G;
-        uint32_t v0[NIT], v1[NIT];
-        uintptr_t base[2];
-        int rsb[2];
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int r = k ? u.p.inter.ref[1] : u.p.inter.ref[0];
-            const int rs = a.ref_stride[r][plane];
-            const P *org = a.ref[r][plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
-            const uintptr_t ad = reinterpret_cast<uintptr_t>(org);
-            base[k] = ad & ~(uintptr_t)3;
-            rsb[k] = rs * B;
-            if (k) sk1 = (int)(ad & 3); else sk0 = (int)(ad & 3);
-        }
-#pragma unroll
-        for (int it = 0; it < NIT; it++) {
-            const int i = l + it * G;
-            const int row = i / SL::NDW, d = i - row * SL::NDW;
-            if (i < TOT) {
-                v0[it] = reinterpret_cast<const uint32_t *>(base[0] + (intptr_t)row * rsb[0])[d];
-                if (comp) v1[it] = reinterpret_cast<const uint32_t *>(base[1] + (intptr_t)row * rsb[1])[d];
-            }
-        }
-        uint32_t *f0 = reinterpret_cast<uint32_t *>(srcl);
-        uint32_t *f1 = reinterpret_cast<uint32_t *>(srcl + SL::FP);
-#pragma unroll
-        for (int it = 0; it < NIT; it++) {
-            const int i = l + it * G;
-            if (i < TOT) {
-                f0[i] = v0[it];
-                if (comp) f1[i] = v1[it];
-            }
-        }
-    }
-    int16_t *e = reinterpret_cast<int16_t *>(srcl);            // intra: topleft[-2h..2w]
-    int16_t *fe = e + SL::EDGE;                                  // prepared edge
-    int16_t *ptile = fe + SL::EDGE;                              // intra prediction W x H
+    // ---------------- P1: coefficient region and intra edges into LDS ----------------
+    C *cf = a.coef + u.coef_off;
+    const int ncoef = nores ? 0 : dconly ? 1 : nzw * nzh;
+    int cfsk = 0;
+    if (ncoef) cfsk = stage16<CL::SW * CL::SH * (int)sizeof(C), G>(cfl, cf, ncoef * (int)sizeof(C), l);
+    const P *tl = nullptr;
     if (pred == DGPU_PRED_INTRA) {
         const P *es = a.edges + u.p.intra.edge_off - 2 * H;
-        for (int i = l; i < SL::EDGE; i += G) e[i] = es[i];
-    }
-    // coefficient row for P3 (lane y owns row y), compact column-major region
-    typename Px<BPC>::coef *cf = a.coef + u.coef_off;
-    int c[W];
-    const bool rowlane = !nores && !dconly && l < SH && !(a.ablate & 8);
-    if (rowlane) {
-        const int nzw = u.nzw, nzh = u.nzh;
-#pragma unroll
-        for (int x = 0; x < W; x++) {
-            int v = (x < nzw && l < nzh) ? (int)cf[l + x * nzh] : 0;
-            c[x] = CL::RECT2 ? r8s(v) : v;
-        }
-        if (a.zero_coefs && l < nzh)
-            for (int x = 0; x < nzw; x++) cf[l + x * nzh] = 0;
-    }
-    int dcres = 0;
-    if (dconly) {  // src/itx_tmpl.c:53-65
-        int dc = cf[0];
-        if (CL::RECT2) dc = r8s(dc);
-        dc = r8s(dc);
-        dc = (dc + ((1 << CL::SHIFT) >> 1)) >> CL::SHIFT;
-        dcres = (dc * 181 + 128 + 2048) >> 12;
-    }
-    wave_sync();
-    if (dconly && a.zero_coefs && l == 0) cf[0] = 0;
-
-    // ---------------- P2: intra prediction into ptile ----------------
-    if (pred == DGPU_PRED_INTRA && !(a.ablate & 4)) {
-        intra_unit<BPC, TX>(u, e, fe, ptile, l, bdmax);
-        wave_sync();
+        const int esk = stage16<SL::EDGE * (int)sizeof(P), G>(src, es, SL::EDGE * (int)sizeof(P), l);
+        tl = reinterpret_cast<const P *>(src + esk) + 2 * H;
     }
 
-    // ---------------- P3 / P4: inverse transform -> residual tile --------------
-    const Clip rc = ItxClip<BPC>::row(bdmax), cc = ItxClip<BPC>::col(bdmax);
-    if (rowlane) {
-        tx1d<W, 1>(kind_h(txtp), c, rc);
-        constexpr int RND = (1 << CL::SHIFT) >> 1;
-#pragma unroll
-        for (int x = 0; x < W; x++) tmp[x * SL::TP + l] = (TT)cc((c[x] + RND) >> CL::SHIFT);
-    }
-    wave_sync();
-    const bool haveres = !nores && !dconly && !(a.ablate & 8);
-    if (haveres && l < W) {
-        int col[H];
-#pragma unroll
-        for (int y = 0; y < H; y++) col[y] = y < SH ? (int)tmp[l * SL::TP + y] : 0;
-        tx1d<H, 1>(kind_v(txtp), col, cc);
-#pragma unroll
-        for (int y = 0; y < H; y++) restile[y * W + l] = (int16_t)((col[y] + 8) >> 4);
-    }
-    wave_sync();
-
-    // ---------------- P5: mc horizontal pass -> int16 intermediate tiles ----------
+    // ---------------- P2: mc horizontal pass(es) ----------------
     const int f2d = inter ? u.p.inter.filter2d : 0;
     const bool bil = f2d == DGPU_FILTER_2D_BILINEAR;
     // filter_type = type_h | type_v << 2 per Filter2d (src/mc_tmpl.c:376-384)
     const int ftype = bil ? 0 : (int)((0x951a62840ull >> (4 * f2d)) & 15);
     const int bw = u.bw4 * 4, bh = u.bh4 * 4;
-    constexpr int FPP = SL::FPB / B;   // footprint pitch in pixels
-    int16_t *mid0 = reinterpret_cast<int16_t *>(srcl + 2 * SL::FP);
-    int16_t *mid1 = reinterpret_cast<int16_t *>(srcl + 2 * SL::FP + SL::MID);
-    Taps th0{}, tv0{}, th1{}, tv1{};
-    int mx0 = 0, my0 = 0, mx1 = 0, my1 = 0;
+    const int bank_h = mc_bank(ftype & 3, bil, bw), bank_v = mc_bank(ftype >> 2, bil, bh);
     if (inter) {
-        mx0 = u.p.inter.mx[0]; my0 = u.p.inter.my[0];
-        mx1 = u.p.inter.mx[1]; my1 = u.p.inter.my[1];
-        if (!bil) {
-            th0 = get_taps(ftype & 3, mx0, bw); tv0 = get_taps(ftype >> 2, my0, bh);
-            th1 = get_taps(ftype & 3, mx1, bw); tv1 = get_taps(ftype >> 2, my1, bh);
-        }
-    }
-    if (inter && !bil && !(a.ablate & 2)) {
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             if (k == 1 && !comp) break;
-            const Taps &th = k ? th1 : th0;
-            const Taps &tv = k ? tv1 : tv0;
-            if (!th.k) continue;
-            const uint8_t *F = srcl + k * SL::FP;
-            const int skp = (k ? sk1 : sk0);
-            int16_t *M = k ? mid1 : mid0;
-            // rows needed: all H+7 for hv, rows 3..H+2 for h-only
-            const int r0 = tv.k ? 0 : 3;
-            const int nrows = tv.k ? H + 7 : H;
-            constexpr int NE = ((H + 7) * W + G - 1) / G;
-#pragma unroll
-            for (int it = 0; it < NE; it++) {
-                const int i = l + it * G;
-                if (i < nrows * W) {
-                    const int r = r0 + i / W, x = i % W;
-                    int s;
-                    if constexpr (BPC == 8) s = hsum8(F + r * SL::FPB, skp + x, th);
-                    else s = hsum16(reinterpret_cast<const uint16_t *>(F + r * SL::FPB) + (skp >> 1) + x, th);
-                    int m;
-                    if (tv.k) m = rnd_sh(s, 6 - ib);                                   // hv intermediate
-                    else if (comp) m = rnd_sh(s, 6 - ib) - PB;                         // prep h-only
-                    else m = clampi((s + 32 + ((1 << (6 - ib)) >> 1)) >> 6, 0, bdmax); // put h-only
-                    M[r * W + x] = (int16_t)m;
-                }
-            }
-        }
-        wave_sync();
-    }
-
-    // ---------------- P6: vertical pass / blend / add residual -> output tile -------
-    {
-        constexpr int NO = (W * H + G - 1) / G;
-        P *dstp = a.dst[plane] + u.dst_off;
-        const int ds = a.dst_stride[plane];
-#pragma unroll
-        for (int it = 0; it < NO; it++) {
-            const int i = l + it * G;
-            if (i >= W * H) break;
-            const int y = i / W, x = i % W;
-            int p;
-            if (inter) {
-                int o[2];
-#pragma unroll
-                for (int k = 0; k < 2; k++) {
-                    if (k == 1 && !comp) { o[1] = 0; break; }
-                    const int mx = k ? mx1 : mx0, my = k ? my1 : my0;
-                    const Taps &th = k ? th1 : th0;
-                    const Taps &tv = k ? tv1 : tv0;
-                    const P *F = reinterpret_cast<const P *>(srcl + k * SL::FP) + ((k ? sk1 : sk0) / B);
-                    const int16_t *M = k ? mid1 : mid0;
-                    int v;
-                    if (a.ablate & 2) {
-                        v = F[(y + 3) * FPP + x + 3];
-                    } else if (bil) {   // put_bilin_c / prep_bilin_c, src/mc_tmpl.c:395-546
-                        const P *s0 = F + (y + 3) * FPP + x + 3;
-                        if (mx && my) {
-                            const int m0 = (int16_t)rnd_sh(16 * s0[0] + mx * (s0[1] - s0[0]), 4 - ib);
-                            const int m1 = (int16_t)rnd_sh(16 * s0[FPP] + mx * (s0[FPP + 1] - s0[FPP]), 4 - ib);
-                            const int t = 16 * m0 + my * (m1 - m0);
-                            v = comp ? rnd_sh(t, 4) - PB : clampi(rnd_sh(t, 4 + ib), 0, bdmax);
-                        } else if (mx) {
-                            const int px = rnd_sh(16 * s0[0] + mx * (s0[1] - s0[0]), 4 - ib);
-                            v = comp ? px - PB : clampi(rnd_sh(px, ib), 0, bdmax);
-                        } else if (my) {
-                            const int t = 16 * s0[0] + my * (s0[FPP] - s0[0]);
-                            v = comp ? rnd_sh(t, 4 - ib) - PB : clampi(rnd_sh(t, 4), 0, bdmax);
-                        } else {
-                            v = comp ? ((int)s0[0] << ib) - PB : (int)s0[0];
-                        }
-                    } else if (th.k && tv.k) {   // put/prep_8tap_c hv, src/mc_tmpl.c:126-150, :232-258
-                        const int16_t *mc = M + y * W + x;
-                        int t = 0;
-#pragma unroll
-                        for (int q = 0; q < 8; q++) t += tv.k[q] * mc[q * W];
-                        v = comp ? rnd_sh(t, 6) - PB : clampi(rnd_sh(t, 6 + ib), 0, bdmax);
-                    } else if (th.k) {           // h-only, already final in M
-                        v = M[(y + 3) * W + x];
-                    } else if (tv.k) {           // v-only, src/mc_tmpl.c:161-168, :270-279
-                        const P *s0 = F + y * FPP + x + 3;
-                        int t = 0;
-#pragma unroll
-                        for (int q = 0; q < 8; q++) t += tv.k[q] * (int)s0[q * FPP];
-                        v = comp ? rnd_sh(t, 6 - ib) - PB : clampi(rnd_sh(t, 6), 0, bdmax);
-                    } else {                     // integer position
-                        const int s0 = F[(y + 3) * FPP + x + 3];
-                        v = comp ? (s0 << ib) - PB : s0;
-                    }
-                    o[k] = v;
-                }
-                // avg_c, src/mc_tmpl.c:587-602
-                p = comp ? clampi((o[0] + o[1] + (1 << ib) + 2 * PB) >> (ib + 1), 0, bdmax) : o[0];
-            } else if (pred == DGPU_PRED_INTRA) {
-                p = ptile[i];
-            } else {
-                p = dstp[y * ds + x];   // PRED_NONE: residual onto the picture
-            }
-            const int r = haveres ? restile[i] : dcres;
-            otile[i] = (P)clampi(p + r, 0, bdmax);
+            const int r = k ? u.p.inter.ref[1] : u.p.inter.ref[0];
+            const int rs = a.ref_stride[r][plane];
+            const P *org = a.ref[r][plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
+            mc_hpass<BPC, TX>(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], ib, l);
         }
     }
     wave_sync();
 
-    // ---------------- P7: store the finished unit rows ----------------
-    {
-        constexpr int RB = W * B;                       // bytes per row
-        constexpr int CB = RB >= 16 ? 16 : RB;          // bytes per store
-        constexpr int NC = RB / CB;                     // stores per row
-        constexpr int NS = (H * NC + G - 1) / G;
-        uint8_t *dbase = reinterpret_cast<uint8_t *>(a.dst[plane] + u.dst_off);
-        const int dsb = a.dst_stride[plane] * B;
-        const uint8_t *ob = reinterpret_cast<const uint8_t *>(otile);
+    // coefficient zeroing (the reference's itx zeroes what it consumed,
+    // src/itx_tmpl.c:55/89); loads above completed before the LDS writes
+    if (a.zero_coefs && ncoef)
+        for (int i = l; i < ncoef; i += G) cf[i] = 0;
+
+    // ---------------- P3: row transforms -> tmp [SH][W] ----------------
+    int dcres = 0;
+    if (dconly) {   // src/itx_tmpl.c:53-65
+        int dc = reinterpret_cast<const C *>(cfl + cfsk)[0];
+        if (CL::RECT2) dc = r8s(dc);
+        dc = r8s(dc);
+        dc = (dc + ((1 << CL::SHIFT) >> 1)) >> CL::SHIFT;
+        dcres = (dc * 181 + 128 + 2048) >> 12;
+    }
+    const Clip rc = ItxClip<BPC>::row(bdmax), cc = ItxClip<BPC>::col(bdmax);
+    if (haveres) {
+        const C *cs = reinterpret_cast<const C *>(cfl + cfsk);
 #pragma unroll
-        for (int it = 0; it < NS; it++) {
-            const int i = l + it * G;
-            if (i >= H * NC) break;
-            const int y = i / NC, cx = i % NC;
-            uint8_t *dp = dbase + (intptr_t)y * dsb + cx * CB;
-            const uint8_t *sp = ob + y * RB + cx * CB;
-            if constexpr (CB == 16) *reinterpret_cast<uint4 *>(dp) = *reinterpret_cast<const uint4 *>(sp);
-            else if constexpr (CB == 8) *reinterpret_cast<uint2 *>(dp) = *reinterpret_cast<const uint2 *>(sp);
-            else *reinterpret_cast<uint32_t *>(dp) = *reinterpret_cast<const uint32_t *>(sp);
+        for (int k = 0; k < (SH + G - 1) / G; k++) {
+            const int r = l + k * G;
+            if (r < SH) {
+                TT *trow = tmp + r * W;
+                if (r < nzh) {
+                    int c[W];
+#pragma unroll
+                    for (int x = 0; x < W; x++) {
+                        int v = 0;
+                        if (x < SW) {
+                            v = cs[x * nzh + r];
+                            v = x < nzw ? v : 0;
+                        }
+                        c[x] = CL::RECT2 ? r8s(v) : v;
+                    }
+                    tx1d<W, 1>(kind_h(txtp), c, rc);
+                    constexpr int RND = (1 << CL::SHIFT) >> 1;
+#pragma unroll
+                    for (int x = 0; x < W; x++) c[x] = cc((c[x] + RND) >> CL::SHIFT);
+                    if constexpr (BPC == 8) {
+#pragma unroll
+                        for (int x = 0; x < W; x += 4) {
+                            uint2 o;
+                            o.x = pack16(c[x], c[x + 1]);
+                            o.y = pack16(c[x + 2], c[x + 3]);
+                            *reinterpret_cast<uint2 *>(trow + x) = o;
+                        }
+                    } else {
+#pragma unroll
+                        for (int x = 0; x < W; x += 4)
+                            *reinterpret_cast<int4 *>(trow + x) = make_int4(c[x], c[x + 1], c[x + 2], c[x + 3]);
+                    }
+                } else {
+#pragma unroll
+                    for (int x = 0; x < W * (int)sizeof(TT); x += 8)
+                        *reinterpret_cast<uint2 *>(reinterpret_cast<uint8_t *>(trow) + x) = make_uint2(0, 0);
+                }
+            }
+        }
+    }
+    wave_sync();
+
+    // ---------------- P4: column transforms -> residual [W][H] ----------------
+    if (haveres) {
+#pragma unroll
+        for (int k = 0; k < (W + G - 1) / G; k++) {
+            const int x = l + k * G;
+            if (x < W) {
+                int col[H];
+#pragma unroll
+                for (int y = 0; y < H; y++) col[y] = y < SH ? (int)tmp[y * W + x] : 0;
+                tx1d<H, 1>(kind_v(txtp), col, cc);
+                TT *rcol = res + x * H;
+                if constexpr (BPC == 8) {
+#pragma unroll
+                    for (int y = 0; y < H; y += 4) {
+                        uint2 o;
+                        o.x = pack16((col[y] + 8) >> 4, (col[y + 1] + 8) >> 4);
+                        o.y = pack16((col[y + 2] + 8) >> 4, (col[y + 3] + 8) >> 4);
+                        *reinterpret_cast<uint2 *>(rcol + y) = o;
+                    }
+                } else {
+#pragma unroll
+                    for (int y = 0; y < H; y += 4)
+                        *reinterpret_cast<int4 *>(rcol + y) =
+                            make_int4((col[y] + 8) >> 4, (col[y + 1] + 8) >> 4, (col[y + 2] + 8) >> 4,
+                                      (col[y + 3] + 8) >> 4);
+                }
+            }
+        }
+    }
+
+    // ---------------- P5: intra edge preparation ----------------
+    IntraState is{};
+    if (pred == DGPU_PRED_INTRA) {
+        is = intra_prep<BPC, TX>(u, tl, fe, l, bdmax);
+        wave_sync();
+        if (is.mode == DGPU_FILTER_PRED) filter_intra<TX>(u, tl, ptile, l, bdmax);
+    }
+    wave_sync();
+
+    // ---------------- P6: prediction + residual -> picture ----------------
+    const uint4 tv0 = inter ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[0]]
+                            : make_uint4(0, 0, 0, 0);
+    const uint4 tv1 = comp ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[1]]
+                           : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < TPL; k++) {
+        const int t = l + k * G;
+        if (t >= NT) break;
+        const int j = t / QW, q = t % QW;   // rows 2j, 2j+1; columns 4q..4q+3
+        int pv[8];
+        if (inter) {
+            int t0[8];
+            mc_vtask<W>(mid0, j, q, tv0, t0);
+            if (comp) {   // prep x2 (rnd_sh(t, 6) - PB) then avg_c, src/mc_tmpl.c:587-602
+                int t1[8];
+                mc_vtask<W>(mid1, j, q, tv1, t1);
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+                    pv[i] = clampi((((t0[i] + 32) >> 6) + ((t1[i] + 32) >> 6) + (1 << ib)) >> (ib + 1), 0, bdmax);
+            } else {      // put: rnd_sh(t, 6 + ib)
+                const int sh = 6 + ib;
+#pragma unroll
+                for (int i = 0; i < 8; i++) pv[i] = clampi((t0[i] + (1 << (sh - 1))) >> sh, 0, bdmax);
+            }
+        } else if (pred == DGPU_PRED_INTRA) {
+            if (is.mode == DGPU_FILTER_PRED) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) pv[i] = ptile[(2 * j + (i >> 2)) * W + 4 * q + (i & 3)];
+            } else {
+                intra_task<TX>(is, tl, fe, 4 * q, 2 * j, pv);
+            }
+        } else {   // PRED_NONE: the residual goes onto the picture
+#pragma unroll
+            for (int i = 0; i < 8; i++) pv[i] = dstp[(2 * j + (i >> 2)) * ds + 4 * q + (i & 3)];
+        }
+        int rv[8];
+        if (haveres) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const TT *rp = res + (4 * q + i) * H + 2 * j;
+                if constexpr (BPC == 8) {
+                    const uint32_t v = *reinterpret_cast<const uint32_t *>(rp);
+                    rv[i] = (int)(int16_t)(v & 0xffff);
+                    rv[4 + i] = (int)v >> 16;
+                } else {
+                    const int2 v = *reinterpret_cast<const int2 *>(rp);
+                    rv[i] = v.x;
+                    rv[4 + i] = v.y;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) rv[i] = dcres;
+        }
+#pragma unroll
+        for (int rr = 0; rr < 2; rr++) {
+            P *row = dstp + (2 * j + rr) * ds + 4 * q;
+            const int o0 = clampi(pv[4 * rr + 0] + rv[4 * rr + 0], 0, bdmax);
+            const int o1 = clampi(pv[4 * rr + 1] + rv[4 * rr + 1], 0, bdmax);
+            const int o2 = clampi(pv[4 * rr + 2] + rv[4 * rr + 2], 0, bdmax);
+            const int o3 = clampi(pv[4 * rr + 3] + rv[4 * rr + 3], 0, bdmax);
+            if constexpr (BPC == 8)
+                *reinterpret_cast<uint32_t *>(row) = (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24;
+            else
+                *reinterpret_cast<uint2 *>(row) = make_uint2((uint32_t)o0 | o1 << 16, (uint32_t)o2 | (uint32_t)o3 << 16);
         }
     }
 }
