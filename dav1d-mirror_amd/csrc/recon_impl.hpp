@@ -2,8 +2,8 @@
 // recon8.hip / recon16.hip so the two heavy TUs compile in parallel).
 //
 // Three kernels per frame batch, one per class group (small: w*h <= 128,
-// large: up to 32x32, huge: a 64-point side), each with its own register and
-// LDS budget.  Within a kernel the waves are scheduled (segment, class):
+// large: up to 32x32, huge: the 64-point sides), each with its own
+// register and LDS budget.  Within a kernel the waves are scheduled (segment, class):
 // every class's unit range (units are sorted by class and, within a class,
 // by position) is cut into kSegments equal parts, so waves that run at the
 // same time touch the same band of the picture.  Blocks are mapped so each
@@ -39,17 +39,20 @@ template <int BPC, int GRP> __host__ __device__ constexpr int waves_per_block() 
 }
 
 template <int BPC, int TX, int GRP>
-__device__ __forceinline__ void dispatch_one(const ReconArgs<BPC> &a, int cls, int first, int count,
-                                             uint8_t *lds) {
-    if constexpr (class_group(TX) == GRP) {
-        if (cls == TX) recon_units<BPC, TX>(a, first, count, lds);
+__device__ __forceinline__ void dispatch_one(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int cls, int first,
+                                             int count, uint8_t *lds) {
+#ifndef DGPU_ONLY_CLASS
+#define DGPU_ONLY_CLASS -1   // build-time probe: compile a single class (resource studies)
+#endif
+    if constexpr (class_group(TX) == GRP && (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS)) {
+        if (cls == TX) recon_units<BPC, TX>(a, pt, first, count, lds);
     }
 }
 
 template <int BPC, int GRP, int... TX>
-__device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, int cls, int first, int count, uint8_t *lds,
-                                         std::integer_sequence<int, TX...>) {
-    (dispatch_one<BPC, TX, GRP>(a, cls, first, count, lds), ...);
+__device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int cls, int first,
+                                         int count, uint8_t *lds, std::integer_sequence<int, TX...>) {
+    (dispatch_one<BPC, TX, GRP>(a, pt, cls, first, count, lds), ...);
 }
 
 template <int BPC, int GRP>
@@ -60,6 +63,19 @@ __global__ __launch_bounds__((64 * waves_per_block<BPC, GRP>())) void k_recon(Re
     // XCD-contiguous block order: hardware deals blocks round-robin over the
     // 8 XCDs, so logical block (b % 8) * (nb / 8) + b / 8 gives XCD x the
     // x-th contiguous eighth of the schedule (gridDim.x is a multiple of 8)
+    __shared__ PlaneTab<BPC> pt;
+    {
+        const int t = threadIdx.x;
+        if (t < DGPU_MAX_REFS * 3) {
+            pt.ref[t] = (&a.ref[0][0])[t];
+            pt.ref_stride[t] = (&a.ref_stride[0][0])[t];
+        }
+        if (t < 3) {
+            pt.dst[t] = a.dst[t];
+            pt.dst_stride[t] = a.dst_stride[t];
+        }
+        __syncthreads();
+    }
     const int nb = gridDim.x, b = blockIdx.x;
     const int lb = (b & 7) * (nb >> 3) + (b >> 3);
     const int wave = threadIdx.x >> 6;
@@ -78,7 +94,7 @@ __global__ __launch_bounds__((64 * waves_per_block<BPC, GRP>())) void k_recon(Re
     const int U = 64 / lanes_per_unit(cls);
     const int first = seg_lo + (gw - a.seg_wave[lo]) * U;
     const int count = min(U, seg_hi - first);
-    dispatch<BPC, GRP>(a, cls, first, count, lds + wave * WL,
+    dispatch<BPC, GRP>(a, pt, cls, first, count, lds + wave * WL,
                        std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 
@@ -151,9 +167,11 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     const char *cm = getenv("DAV1D_GPU_CLASSMASK");
     const unsigned classmask = cm ? (unsigned)strtoul(cm, nullptr, 0) : ~0u;
 
-    int rc = launch_group<BPC, GROUP_SMALL>(a, b, classmask, stream);
+    // Group kernels in order on the caller's stream (cross-stream fork/join
+    // measured ~25 us of event overhead per frame on MI355X: slower).
+    int rc = launch_group<BPC, GROUP_HUGE>(a, b, classmask, stream);
     if (!rc) rc = launch_group<BPC, GROUP_LARGE>(a, b, classmask, stream);
-    if (!rc) rc = launch_group<BPC, GROUP_HUGE>(a, b, classmask, stream);
+    if (!rc) rc = launch_group<BPC, GROUP_SMALL>(a, b, classmask, stream);
     return rc;
 }
 

@@ -8,8 +8,9 @@
 // round-trips through HBM.
 //
 // Mapping (wave64, v3).  Units are sorted by transform size class.  A unit
-// is cut into 4x2-pixel output tasks; a class gives each unit G = W*H/8
-// lanes (2..64), i.e. one task per lane, and a wave owns 64/G units.
+// is cut into 4x2-pixel output tasks; a class gives each unit G lanes (one
+// task per lane up to the width of the 1-D transform passes, see
+// lanes_per_unit) and a wave owns 64/G units.
 //   P1  global loads: descriptor, the compact coefficient region and intra
 //       edge array (16-B chunks into LDS), the mc footprint rows (dwordx4
 //       per row and 4-px quad, straight into registers)
@@ -54,6 +55,17 @@ template <int BPC> struct ReconArgs {
     int zero_coefs;
 };
 
+// Plane pointers and strides, copied once per workgroup into LDS so the
+// per-unit (ref, plane) lookup is an LDS read, not a dependent load from
+// the kernel-argument segment.
+template <int BPC> struct PlaneTab {
+    using P = typename Px<BPC>::pixel;
+    const P *ref[DGPU_MAX_REFS * 3];
+    P *dst[3];
+    int ref_stride[DGPU_MAX_REFS * 3];   // pixels
+    int dst_stride[3];
+};
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -64,12 +76,18 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 
-// lanes per unit: one 4x2 output task per lane, 2..64
+// lanes per unit: one 4x2 output task per lane (W*H/8), but no more lanes
+// than the 1-D transform passes can use (max(W, min(H, 32)) lines), 2..64;
+// 32x32 takes a whole wave so its LDS slot (9 KB) does not set the budget
+// of the large group
 __host__ __device__ constexpr int lanes_per_unit(int tx) {
-    return cmin(cmax(tx_info(tx).w * tx_info(tx).h / 8, 2), 64);
+    const int w = tx_info(tx).w, h = tx_info(tx).h;
+    if (w * h >= 1024) return 64;
+    return cmin(cmax(cmin(w * h / 8, cmax(w, cmin(h, 32))), 2), 64);
 }
-// class groups, each its own kernel (own register / LDS budget)
-enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2 };
+// class groups, each its own kernel with its own register / LDS budget:
+// small (w*h <= 128), large (up to 32x32), huge (the 64-point sides)
+enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2, N_GROUPS = 3 };
 __host__ __device__ constexpr int class_group(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
     return (w == 64 || h == 64) ? GROUP_HUGE : (w * h <= 128 ? GROUP_SMALL : GROUP_LARGE);
@@ -84,12 +102,17 @@ template <int TX> struct Cls {
     static constexpr int NT = H / 2 * QW;       // 4x2 output tasks
     static constexpr int RP = (H + 8) / 2;      // mc intermediate row pairs (rows 0..H+7)
     static constexpr int NH = RP * QW;          // h-pass tasks
+    static constexpr int TPL = (NT + G - 1) / G;  // output tasks per lane
+    // compound refs run one after the other through one intermediate tile,
+    // the first ref's predictions held in registers across the second
+    static constexpr bool SEQREF = TPL <= 2;
 };
 
 template <int BPC> struct Tmp { using T = int32_t; };
 template <> struct Tmp<8> { using T = int16_t; };   // 8-bit row output / residual fit int16
 
 // LDS slot of one unit (bytes): [coefs | residual] [row-pass tmp] [mc | intra]
+// (FE serves the directional modes, PT filter intra: never both)
 template <int BPC, int TX> struct Slot {
     using CL = Cls<TX>;
     static constexpr int W = CL::W, H = CL::H, B = BPC / 8;
@@ -103,8 +126,8 @@ template <int BPC, int TX> struct Slot {
     static constexpr int EDGE = 2 * H + 2 * W + 1;               // topleft[-2h..2w]
     static constexpr int EB = a16(EDGE * B + 16);                // raw edge pixels at their skew
     static constexpr int FE = a16(EDGE * 2);                     // prepared edge, int16
-    static constexpr int PT = a16(W * H * 2);                    // filter-intra tile, int16
-    static constexpr int SRC = cmax(2 * MID, EB + FE + PT);
+    static constexpr int PT = a16(W * H * 2);                    // filter-intra tile, int16 (aliases FE)
+    static constexpr int SRC = cmax((CL::SEQREF ? 1 : 2) * MID, EB + cmax(FE, PT));
     static constexpr int BYTES = CFR + TMP + SRC;
     static constexpr int WAVE = CL::U * BYTES;
 };
@@ -115,11 +138,28 @@ typedef short v2i16 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3a1 __attribute__((ext_vector_type(3), aligned(1)));
+typedef uint32_t u32x4a2 __attribute__((ext_vector_type(4), aligned(2)));
+typedef uint32_t u32x2a2 __attribute__((ext_vector_type(2), aligned(2)));
+
+// Packed dot products.  Chains start from an inline constant (0 .. 64) so
+// the compiler keeps the three-operand form for the first step and the
+// accumulating two-operand form after it (no accumulator copies).
 __device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, a), __builtin_bit_cast(v2i16, b), c, false);
 }
 __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+// Global-memory access through pointers that came from LDS (the plane
+// table): tell the compiler the address space so it emits global_*
+// instead of flat_* instructions.
+template <typename T> __device__ __forceinline__ T gld(const void *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
+template <typename T> __device__ __forceinline__ void gst(void *p, T v) {
+    *(__attribute__((address_space(1))) T *)p = v;
 }
 // ({hi, lo} >> 8s)[31:0]
 __device__ __forceinline__ uint32_t alb(uint32_t hi, uint32_t lo, int s) {
@@ -436,109 +476,121 @@ __device__ __forceinline__ int mc_bank(int type, bool bil, int len) {
 
 // Horizontal pass of one reference: NH tasks of (row pair p, quad q) ->
 // mid[p * W + 4q .. +3] = (row 2p, row 2p+1) int16 pairs.  `org` is the
-// footprint origin (block position - 3 rows - 3 columns).
+// footprint origin (block position - 3 rows - 3 columns).  Rows are read
+// with unaligned 12-byte (8bpc) / 24-byte (16bpc) loads, one per row and
+// quad.  G is a multiple of QW for every class, so a lane's quad is fixed
+// and its row pairs advance by G / QW.
 template <int BPC, int TX>
 __device__ __forceinline__ void mc_hpass(const typename Px<BPC>::pixel *org, int stride_px, uint32_t *mid,
                                          int bank, int m, int ib, int l) {
     using CL = Cls<TX>;
-    constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NH = CL::NH;
+    constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NH = CL::NH, RP = CL::RP;
     constexpr int IT = (NH + G - 1) / G;
-    const int sk = (int)(reinterpret_cast<uintptr_t>(org) & 3);
-    const uint8_t *base = reinterpret_cast<const uint8_t *>(org) - sk;
-    const int sb = stride_px * (BPC / 8);
+    constexpr int PS = G / QW;   // row-pair step per task
+    static_assert(G % QW == 0, "lane quads must be fixed");
+    constexpr int B = BPC / 8;
+    const unsigned sb = (unsigned)stride_px * B;
+    const int q = l % QW, p0 = l / QW;
+    const uint8_t *rp = reinterpret_cast<const uint8_t *>(org) + (size_t)(2u * p0 * sb) + 4 * B * q;
+    uint32_t *mp = mid + p0 * W + 4 * q;
     if constexpr (BPC == 8) {
         const uint2 th = reinterpret_cast<const uint2 *>(dspt_mc8)[bank * 16 + m];
-        u32x4a4 raw[IT][2];
+        // taps sum to 64 and p ^ 0x80 == p - 128 as int8: s = acc + 128 * 64,
+        // and the reference's mid = (s + 2) >> 2 (intermediate_bits 4) is
+        // stored here as mid - 2048 = (acc + 2) >> 2; the vertical pass adds
+        // back 64 * 2048 (kMidBias8).  Both forms fit int16 for 8-bit input.
+        constexpr int CH = cmin(IT, 3);   // tasks whose loads are in flight together
 #pragma unroll
-        for (int k = 0; k < IT; k++) {   // clamped task: the loads are always in the footprint
-            const int t = min(l + k * G, NH - 1);
-            const int p = t / QW, q = t % QW;
-            const int r0 = 2 * p, r1 = min(2 * p + 1, H + 6);   // row H+7 is never used
-            raw[k][0] = *reinterpret_cast<const u32x4a4 *>(base + r0 * sb + 4 * q);
-            raw[k][1] = *reinterpret_cast<const u32x4a4 *>(base + r1 * sb + 4 * q);
-        }
-        // taps sum to 64 and p ^ 0x80 == p - 128 as int8: s = acc + 128 * 64;
-        // mid = (s + 2) >> 2 (intermediate_bits 4)
-        constexpr int C = 128 * 64 + 2;
+        for (int k0 = 0; k0 < IT; k0 += CH) {
+            u32x3a1 raw[CH][2];
 #pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const int t = l + k * G;
-            if (t < NH) {
-                const int p = t / QW, q = t % QW;
-                int mm[2][4];
+            for (int c = 0; c < CH; c++) {   // clamped: the loads stay inside the footprint
+                const int p = cmin(p0 + (k0 + c) * PS, RP - 1);
+                const uint8_t *r0 = rp + (size_t)((unsigned)(p - p0) * 2u * sb);
+                raw[c][0] = gld<u32x3a1>(r0);
+                // row 2p+1 == H+7 (last pair) is never used: re-read row 2p
+                raw[c][1] = gld<u32x3a1>(2 * p + 1 < H + 7 ? r0 + sb : r0);
+            }
 #pragma unroll
-                for (int rr = 0; rr < 2; rr++) {
-                    const u32x4a4 d = raw[k][rr];
-                    const uint32_t w0 = alb(d.y, d.x, sk) ^ 0x80808080u;
-                    const uint32_t w1 = alb(d.z, d.y, sk) ^ 0x80808080u;
-                    const uint32_t w2 = alb(d.w, d.z, sk) ^ 0x80808080u;
-                    mm[rr][0] = dot4(w1, th.y, dot4(w0, th.x, C)) >> 2;
-                    mm[rr][1] = dot4(alb(w2, w1, 1), th.y, dot4(alb(w1, w0, 1), th.x, C)) >> 2;
-                    mm[rr][2] = dot4(alb(w2, w1, 2), th.y, dot4(alb(w1, w0, 2), th.x, C)) >> 2;
-                    mm[rr][3] = dot4(alb(w2, w1, 3), th.y, dot4(alb(w1, w0, 3), th.x, C)) >> 2;
+            for (int c = 0; c < CH; c++) {
+                const int p = p0 + (k0 + c) * PS;
+                if (k0 + c < IT && p < RP) {
+                    int mm[2][4];
+#pragma unroll
+                    for (int rr = 0; rr < 2; rr++) {
+                        const uint32_t w0 = raw[c][rr].x ^ 0x80808080u;
+                        const uint32_t w1 = raw[c][rr].y ^ 0x80808080u;
+                        const uint32_t w2 = raw[c][rr].z ^ 0x80808080u;
+                        mm[rr][0] = dot4(w1, th.y, dot4(w0, th.x, 2)) >> 2;
+                        mm[rr][1] = dot4(alb(w2, w1, 1), th.y, dot4(alb(w1, w0, 1), th.x, 2)) >> 2;
+                        mm[rr][2] = dot4(alb(w2, w1, 2), th.y, dot4(alb(w1, w0, 2), th.x, 2)) >> 2;
+                        mm[rr][3] = dot4(alb(w2, w1, 3), th.y, dot4(alb(w1, w0, 3), th.x, 2)) >> 2;
+                    }
+                    uint4 o;
+                    o.x = pack16(mm[0][0], mm[1][0]);
+                    o.y = pack16(mm[0][1], mm[1][1]);
+                    o.z = pack16(mm[0][2], mm[1][2]);
+                    o.w = pack16(mm[0][3], mm[1][3]);
+                    *reinterpret_cast<uint4 *>(mp + (k0 + c) * PS * W) = o;
                 }
-                uint4 o;
-                o.x = pack16(mm[0][0], mm[1][0]);
-                o.y = pack16(mm[0][1], mm[1][1]);
-                o.z = pack16(mm[0][2], mm[1][2]);
-                o.w = pack16(mm[0][3], mm[1][3]);
-                *reinterpret_cast<uint4 *>(mid + p * W + 4 * q) = o;
             }
         }
     } else {
         const uint4 th = reinterpret_cast<const uint4 *>(dspt_mc16)[bank * 16 + m];
         const int sh = 6 - ib, rnd = (1 << sh) >> 1;
-        u32x4a4 ra[IT][2];
-        u32x2a4 rb[IT][2];
+        constexpr int CH = cmin(IT, 2);
 #pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const int t = min(l + k * G, NH - 1);
-            const int p = t / QW, q = t % QW;
-            const int r0 = 2 * p, r1 = min(2 * p + 1, H + 6);
-            const uint8_t *a0 = base + r0 * sb + 8 * q, *a1 = base + r1 * sb + 8 * q;
-            ra[k][0] = *reinterpret_cast<const u32x4a4 *>(a0);
-            rb[k][0] = *reinterpret_cast<const u32x2a4 *>(a0 + 16);
-            ra[k][1] = *reinterpret_cast<const u32x4a4 *>(a1);
-            rb[k][1] = *reinterpret_cast<const u32x2a4 *>(a1 + 16);
-        }
+        for (int k0 = 0; k0 < IT; k0 += CH) {
+            u32x4a2 ra[CH][2];
+            u32x2a2 rb[CH][2];
 #pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const int t = l + k * G;
-            if (t < NH) {
-                const int p = t / QW, q = t % QW;
-                int mm[2][4];
+            for (int c = 0; c < CH; c++) {
+                const int p = cmin(p0 + (k0 + c) * PS, RP - 1);
+                const uint8_t *a0 = rp + (size_t)((unsigned)(p - p0) * 2u * sb);
+                const uint8_t *a1 = 2 * p + 1 < H + 7 ? a0 + sb : a0;
+                ra[c][0] = gld<u32x4a2>(a0);
+                rb[c][0] = gld<u32x2a2>(a0 + 16);
+                ra[c][1] = gld<u32x4a2>(a1);
+                rb[c][1] = gld<u32x2a2>(a1 + 16);
+            }
 #pragma unroll
-                for (int rr = 0; rr < 2; rr++) {
-                    const uint32_t d[6] = {ra[k][rr].x, ra[k][rr].y, ra[k][rr].z, ra[k][rr].w,
-                                           rb[k][rr].x, rb[k][rr].y};
-                    uint32_t e[6], o[5];   // e: pixel pairs (2i, 2i+1), o: (2i+1, 2i+2)
+            for (int c = 0; c < CH; c++) {
+                const int p = p0 + (k0 + c) * PS;
+                if (k0 + c < IT && p < RP) {
+                    int mm[2][4];
 #pragma unroll
-                    for (int i = 0; i < 5; i++) e[i] = alb(d[i + 1], d[i], sk);
-                    e[5] = alb(d[5], d[5], sk);   // only its low half (pixel 10) is used
+                    for (int rr = 0; rr < 2; rr++) {
+                        // e: pixel pairs (2i, 2i+1), o: (2i+1, 2i+2)
+                        const uint32_t e[6] = {ra[c][rr].x, ra[c][rr].y, ra[c][rr].z, ra[c][rr].w,
+                                               rb[c][rr].x, rb[c][rr].y};
+                        uint32_t o[5];
 #pragma unroll
-                    for (int i = 0; i < 5; i++) o[i] = alb(e[i + 1], e[i], 2);
-                    const int s0 = dot2(e[3], th.w, dot2(e[2], th.z, dot2(e[1], th.y, dot2(e[0], th.x, 0))));
-                    const int s1 = dot2(o[3], th.w, dot2(o[2], th.z, dot2(o[1], th.y, dot2(o[0], th.x, 0))));
-                    const int s2 = dot2(e[4], th.w, dot2(e[3], th.z, dot2(e[2], th.y, dot2(e[1], th.x, 0))));
-                    const int s3 = dot2(o[4], th.w, dot2(o[3], th.z, dot2(o[2], th.y, dot2(o[1], th.x, 0))));
-                    mm[rr][0] = (s0 + rnd) >> sh;
-                    mm[rr][1] = (s1 + rnd) >> sh;
-                    mm[rr][2] = (s2 + rnd) >> sh;
-                    mm[rr][3] = (s3 + rnd) >> sh;
+                        for (int i = 0; i < 5; i++) o[i] = alb(e[i + 1], e[i], 2);
+                        const int s0 = dot2(e[3], th.w, dot2(e[2], th.z, dot2(e[1], th.y, dot2(e[0], th.x, 0))));
+                        const int s1 = dot2(o[3], th.w, dot2(o[2], th.z, dot2(o[1], th.y, dot2(o[0], th.x, 0))));
+                        const int s2 = dot2(e[4], th.w, dot2(e[3], th.z, dot2(e[2], th.y, dot2(e[1], th.x, 0))));
+                        const int s3 = dot2(o[4], th.w, dot2(o[3], th.z, dot2(o[2], th.y, dot2(o[1], th.x, 0))));
+                        mm[rr][0] = (s0 + rnd) >> sh;
+                        mm[rr][1] = (s1 + rnd) >> sh;
+                        mm[rr][2] = (s2 + rnd) >> sh;
+                        mm[rr][3] = (s3 + rnd) >> sh;
+                    }
+                    uint4 o;
+                    o.x = pack16(mm[0][0], mm[1][0]);
+                    o.y = pack16(mm[0][1], mm[1][1]);
+                    o.z = pack16(mm[0][2], mm[1][2]);
+                    o.w = pack16(mm[0][3], mm[1][3]);
+                    *reinterpret_cast<uint4 *>(mp + (k0 + c) * PS * W) = o;
                 }
-                uint4 o;
-                o.x = pack16(mm[0][0], mm[1][0]);
-                o.y = pack16(mm[0][1], mm[1][1]);
-                o.z = pack16(mm[0][2], mm[1][2]);
-                o.w = pack16(mm[0][3], mm[1][3]);
-                *reinterpret_cast<uint4 *>(mid + p * W + 4 * q) = o;
             }
         }
     }
 }
 
 // Vertical pass of one reference for a 4x2 task: t[i] = the 8-tap sum over
-// intermediates, rows j*2 (i < 4) and j*2+1 (i >= 4), columns 4q + (i & 3).
+// stored intermediates, rows j*2 (i < 4) and j*2+1 (i >= 4), columns
+// 4q + (i & 3).  Add kMidBias<BPC> for the reference's sum.
+template <int BPC> inline constexpr int kMidBias = BPC == 8 ? 64 * 2048 : 0;
 template <int W>
 __device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, const uint4 tv, int *t) {
     uint32_t P[5][4];
@@ -559,14 +611,15 @@ __device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, cons
 // ---------------------------------------------------------------- kernel --
 
 template <int BPC, int TX>
-__device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, int count, uint8_t *wave_lds) {
+__device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int first, int count,
+                                            uint8_t *wave_lds) {
     using CL = Cls<TX>;
     using SL = Slot<BPC, TX>;
     using P = typename Px<BPC>::pixel;
     using C = typename Px<BPC>::coef;
     using TT = typename Tmp<BPC>::T;
     constexpr int W = CL::W, H = CL::H, SW = CL::SW, SH = CL::SH, G = CL::G, QW = CL::QW, NT = CL::NT;
-    constexpr int TPL = (NT + G - 1) / G;
+    constexpr int TPL = CL::TPL;
     const int lane = threadIdx.x & 63;
     const int g = lane / G, l = lane % G;
     if (g >= count) return;
@@ -578,9 +631,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
     TT *tmp = reinterpret_cast<TT *>(slot + SL::CFR);
     uint8_t *src = slot + SL::CFR + SL::TMP;
     uint32_t *mid0 = reinterpret_cast<uint32_t *>(src);
-    uint32_t *mid1 = reinterpret_cast<uint32_t *>(src + SL::MID);
+    uint32_t *mid1 = reinterpret_cast<uint32_t *>(src + (CL::SEQREF ? 0 : SL::MID));
     int16_t *fe = reinterpret_cast<int16_t *>(src + SL::EB);
-    int16_t *ptile = reinterpret_cast<int16_t *>(src + SL::EB + SL::FE);
+    int16_t *ptile = reinterpret_cast<int16_t *>(src + SL::EB);
 
     const int plane = u.plane;
     const int bdmax = a.bdmax;
@@ -593,8 +646,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
     const int nzw = u.nzw, nzh = u.nzh;
     const bool dconly = !nores && nzw == 0;
     const bool haveres = !nores && !dconly;
-    P *dstp = a.dst[plane] + u.dst_off;
-    const int ds = a.dst_stride[plane];
+    P *dstp = pt.dst[plane] + u.dst_off;
+    const int ds = pt.dst_stride[plane];
 
     // ---------------- P1: coefficient region and intra edges into LDS ----------------
     C *cf = a.coef + u.coef_off;
@@ -615,15 +668,20 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
     const int ftype = bil ? 0 : (int)((0x951a62840ull >> (4 * f2d)) & 15);
     const int bw = u.bw4 * 4, bh = u.bh4 * 4;
     const int bank_h = mc_bank(ftype & 3, bil, bw), bank_v = mc_bank(ftype >> 2, bil, bh);
+    // vertical taps are loaded here so their latency overlaps the h-pass
+    const uint4 tv0 = inter ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[0]]
+                            : make_uint4(0, 0, 0, 0);
+    const uint4 tv1 = comp ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[1]]
+                           : make_uint4(0, 0, 0, 0);
+    auto hpass = [&](int k) {
+        const int r = k ? u.p.inter.ref[1] : u.p.inter.ref[0];
+        const int rs = pt.ref_stride[r * 3 + plane];
+        const P *org = pt.ref[r * 3 + plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
+        mc_hpass<BPC, TX>(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], ib, l);
+    };
     if (inter) {
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            if (k == 1 && !comp) break;
-            const int r = k ? u.p.inter.ref[1] : u.p.inter.ref[0];
-            const int rs = a.ref_stride[r][plane];
-            const P *org = a.ref[r][plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
-            mc_hpass<BPC, TX>(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], ib, l);
-        }
+        hpass(0);
+        if (!CL::SEQREF && comp) hpass(1);
     }
     wave_sync();
 
@@ -726,11 +784,27 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
     }
     wave_sync();
 
+    // ---------------- P6a: first ref of a compound unit (SEQREF) ----------------
+    // prep values rnd_sh(t, 6) (the reference's mct output + PREP_BIAS), kept
+    // in registers while the second ref's h-pass reuses the tile
+    int q0[CL::SEQREF ? TPL : 1][8];
+    if (CL::SEQREF && comp) {
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t < NT) {
+                int t0[8];
+                mc_vtask<W>(mid0, t / QW, t % QW, tv0, t0);
+#pragma unroll
+                for (int i = 0; i < 8; i++) q0[k][i] = (t0[i] + (kMidBias<BPC> + 32)) >> 6;
+            }
+        }
+        wave_sync();
+        hpass(1);
+        wave_sync();
+    }
+
     // ---------------- P6: prediction + residual -> picture ----------------
-    const uint4 tv0 = inter ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[0]]
-                            : make_uint4(0, 0, 0, 0);
-    const uint4 tv1 = comp ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[1]]
-                           : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int k = 0; k < TPL; k++) {
         const int t = l + k * G;
@@ -738,18 +812,27 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
         const int j = t / QW, q = t % QW;   // rows 2j, 2j+1; columns 4q..4q+3
         int pv[8];
         if (inter) {
-            int t0[8];
-            mc_vtask<W>(mid0, j, q, tv0, t0);
             if (comp) {   // prep x2 (rnd_sh(t, 6) - PB) then avg_c, src/mc_tmpl.c:587-602
-                int t1[8];
+                int p0[8], t1[8];
+                if constexpr (CL::SEQREF) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) p0[i] = q0[k][i];
+                } else {
+                    int t0[8];
+                    mc_vtask<W>(mid0, j, q, tv0, t0);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) p0[i] = (t0[i] + (kMidBias<BPC> + 32)) >> 6;
+                }
                 mc_vtask<W>(mid1, j, q, tv1, t1);
 #pragma unroll
                 for (int i = 0; i < 8; i++)
-                    pv[i] = clampi((((t0[i] + 32) >> 6) + ((t1[i] + 32) >> 6) + (1 << ib)) >> (ib + 1), 0, bdmax);
-            } else {      // put: rnd_sh(t, 6 + ib)
-                const int sh = 6 + ib;
+                    pv[i] = clampi((p0[i] + ((t1[i] + (kMidBias<BPC> + 32)) >> 6) + (1 << ib)) >> (ib + 1), 0, bdmax);
+            } else {
+                int t0[8];
+                const int sh = 6 + ib;   // put: rnd_sh(t, 6 + ib)
+                mc_vtask<W>(mid0, j, q, tv0, t0);
 #pragma unroll
-                for (int i = 0; i < 8; i++) pv[i] = clampi((t0[i] + (1 << (sh - 1))) >> sh, 0, bdmax);
+                for (int i = 0; i < 8; i++) pv[i] = clampi((t0[i] + (kMidBias<BPC> + (1 << (sh - 1)))) >> sh, 0, bdmax);
             }
         } else if (pred == DGPU_PRED_INTRA) {
             if (is.mode == DGPU_FILTER_PRED) {
@@ -760,7 +843,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
             }
         } else {   // PRED_NONE: the residual goes onto the picture
 #pragma unroll
-            for (int i = 0; i < 8; i++) pv[i] = dstp[(2 * j + (i >> 2)) * ds + 4 * q + (i & 3)];
+            for (int i = 0; i < 8; i++) pv[i] = gld<P>(dstp + (2 * j + (i >> 2)) * ds + 4 * q + (i & 3));
         }
         int rv[8];
         if (haveres) {
@@ -789,9 +872,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, int first, 
             const int o2 = clampi(pv[4 * rr + 2] + rv[4 * rr + 2], 0, bdmax);
             const int o3 = clampi(pv[4 * rr + 3] + rv[4 * rr + 3], 0, bdmax);
             if constexpr (BPC == 8)
-                *reinterpret_cast<uint32_t *>(row) = (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24;
+                gst<uint32_t>(row, (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24);
             else
-                *reinterpret_cast<uint2 *>(row) = make_uint2((uint32_t)o0 | o1 << 16, (uint32_t)o2 | (uint32_t)o3 << 16);
+                gst<u32x2>(row, u32x2{(uint32_t)o0 | o1 << 16, (uint32_t)o2 | (uint32_t)o3 << 16});
         }
     }
 }

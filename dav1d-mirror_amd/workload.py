@@ -300,12 +300,17 @@ def make_frame(cfg: FrameConfig) -> FrameData:
                     else:
                         coefs[o:o + a * b] = c[j, :b, :a].T.ravel()
 
-    # sort by (class, picture band, pred kind, filter / mode): the kernel cuts
-    # each class into 16 equal segments scheduled together (spatial locality
-    # of the writes), and inside a band waves see uniform prediction kinds
+    # sort by (class, picture band, pred kind, then transform type / filter
+    # for inter and mode / transform type for intra).  The kernel cuts each
+    # class into 16 equal segments scheduled together (spatial locality of
+    # the writes); inside a band, waves then see one prediction kind and one
+    # transform type, so the per-unit branches (1-D transform kind, intra
+    # mode) do not diverge.  Order inside a class is free for correctness.
     ph = np.array([planes[p][1] for p in range(3)])
     band = (uy * 16) // ph[plane_u]
-    order = np.lexsort((sort_minor, units["pred"], band, units["tx"]))
+    tt = units["txtp"].astype(np.int64)
+    minor = np.where(inter, tt * 16 + sort_minor, sort_minor * 256 + tt)
+    order = np.lexsort((minor, units["pred"], band, units["tx"]))
     units = units[order]
     counts = np.bincount(units["tx"], minlength=abi.N_TX)
     class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
