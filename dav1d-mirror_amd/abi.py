@@ -81,7 +81,11 @@ _LIB = None
 
 
 def lib_path():
-    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdav1d_gpu.so")
+    # DAV1D_GPU_LIB_VARIANT=<name> loads libdav1d_gpu.<name>.so: profiling
+    # builds from tools/build_variants.sh (phase ablations), never a fallback
+    v = os.environ.get("DAV1D_GPU_LIB_VARIANT")
+    name = f"libdav1d_gpu.{v}.so" if v else "libdav1d_gpu.so"
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), name)
 
 
 def load_lib():

@@ -32,9 +32,27 @@
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
 
+// Profiling-only phase ablations (tools/build_variants.sh); all 0 in the
+// product build.  Outputs are wrong when any is set.
+#ifndef DGPU_ABL_MC
+#define DGPU_ABL_MC 0      // skip the mc h/v passes
+#endif
+#ifndef DGPU_ABL_ITX
+#define DGPU_ABL_ITX 0     // skip the row/column transforms
+#endif
+#ifndef DGPU_ABL_INTRA
+#define DGPU_ABL_INTRA 0   // skip intra edge preparation and prediction
+#endif
+
 namespace dgpu {
 
-constexpr int kSegments = 16;   // spatial segments per class (task ordering)
+#ifndef DGPU_SEGMENTS
+#define DGPU_SEGMENTS 16
+#endif
+#ifndef DGPU_SEQREF_MAX_TPL
+#define DGPU_SEQREF_MAX_TPL 2
+#endif
+constexpr int kSegments = DGPU_SEGMENTS;   // spatial segments per class (task ordering)
 
 template <int BPC> struct ReconArgs {
     using P = typename Px<BPC>::pixel;
@@ -105,7 +123,7 @@ template <int TX> struct Cls {
     static constexpr int TPL = (NT + G - 1) / G;  // output tasks per lane
     // compound refs run one after the other through one intermediate tile,
     // the first ref's predictions held in registers across the second
-    static constexpr bool SEQREF = TPL <= 2;
+    static constexpr bool SEQREF = TPL <= DGPU_SEQREF_MAX_TPL;
 };
 
 template <int BPC> struct Tmp { using T = int32_t; };
@@ -645,7 +663,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     const bool nores = txtp == DGPU_NO_RESIDUAL;
     const int nzw = u.nzw, nzh = u.nzh;
     const bool dconly = !nores && nzw == 0;
-    const bool haveres = !nores && !dconly;
+    const bool haveres = !nores && !dconly && !DGPU_ABL_ITX;
     P *dstp = pt.dst[plane] + u.dst_off;
     const int ds = pt.dst_stride[plane];
 
@@ -679,7 +697,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         const P *org = pt.ref[r * 3 + plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
         mc_hpass<BPC, TX>(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], ib, l);
     };
-    if (inter) {
+    if (inter && !DGPU_ABL_MC) {
         hpass(0);
         if (!CL::SEQREF && comp) hpass(1);
     }
@@ -777,7 +795,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 
     // ---------------- P5: intra edge preparation ----------------
     IntraState is{};
-    if (pred == DGPU_PRED_INTRA) {
+    if (pred == DGPU_PRED_INTRA && !DGPU_ABL_INTRA) {
         is = intra_prep<BPC, TX>(u, tl, fe, l, bdmax);
         wave_sync();
         if (is.mode == DGPU_FILTER_PRED) filter_intra<TX>(u, tl, ptile, l, bdmax);
@@ -788,7 +806,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     // prep values rnd_sh(t, 6) (the reference's mct output + PREP_BIAS), kept
     // in registers while the second ref's h-pass reuses the tile
     int q0[CL::SEQREF ? TPL : 1][8];
-    if (CL::SEQREF && comp) {
+    if (CL::SEQREF && comp && !DGPU_ABL_MC) {
 #pragma unroll
         for (int k = 0; k < TPL; k++) {
             const int t = l + k * G;
@@ -811,7 +829,10 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         if (t >= NT) break;
         const int j = t / QW, q = t % QW;   // rows 2j, 2j+1; columns 4q..4q+3
         int pv[8];
-        if (inter) {
+        if (inter && DGPU_ABL_MC) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) pv[i] = 0;
+        } else if (inter) {
             if (comp) {   // prep x2 (rnd_sh(t, 6) - PB) then avg_c, src/mc_tmpl.c:587-602
                 int p0[8], t1[8];
                 if constexpr (CL::SEQREF) {
@@ -834,6 +855,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #pragma unroll
                 for (int i = 0; i < 8; i++) pv[i] = clampi((t0[i] + (kMidBias<BPC> + (1 << (sh - 1)))) >> sh, 0, bdmax);
             }
+        } else if (pred == DGPU_PRED_INTRA && DGPU_ABL_INTRA) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) pv[i] = 0;
         } else if (pred == DGPU_PRED_INTRA) {
             if (is.mode == DGPU_FILTER_PRED) {
 #pragma unroll

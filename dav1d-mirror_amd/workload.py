@@ -46,6 +46,7 @@ class FrameConfig:
     intra_frac: float = 0.30
     compound_frac: float = 0.50   # of inter blocks
     seed: int = 0x5EED0001
+    tx64: bool = False            # allow 64-point transforms (64x64 luma blocks)
 
     @property
     def pixel_dtype(self):
@@ -127,11 +128,12 @@ _KV = [0, 1, 0, 1, 2, 0, 2, 1, 2, 3, 0, 3, 1, 3, 2, 3]
 _KH = [0, 0, 1, 1, 0, 2, 2, 2, 1, 3, 3, 0, 3, 1, 3, 2]
 
 
-def _tx_candidates(s):
+def _tx_candidates(s, tx64=False):
     """(tw, th) transform sizes tiling an s x s block: sides in {s, s/2, s/4}
-    within [4, 32], aspect ratio at most 4 (all such pairs are reference
-    transform sizes)."""
-    sides = [v for v in (s, s // 2, s // 4) if 4 <= v <= 32]
+    within [4, 32] (or [4, 64] with tx64), aspect ratio at most 4 (all such
+    pairs are reference transform sizes)."""
+    top = 64 if tx64 else 32
+    sides = [v for v in (s, s // 2, s // 4) if 4 <= v <= top]
     return [(a, b) for a in sides for b in sides if max(a, b) <= 4 * min(a, b)]
 
 
@@ -179,7 +181,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
             if cfg.kind == "mc":
                 tw = th = s
             else:
-                cands = _tx_candidates(s)
+                cands = _tx_candidates(s, cfg.tx64)
                 tw, th = cands[(b * 7 + plane * 3 + int(rng.integers(0, 1 << 20))) % len(cands)]
             for oy in range(0, s, th):
                 for ox in range(0, s, tw):

@@ -40,6 +40,17 @@ def test_batch_small_16bpc(pkg, oracle, bdmax):
     _check(_frame(pkg, width=512, height=256, bpc=16, bitdepth_max=bdmax, seed=11), oracle)
 
 
+@pytest.mark.parametrize("seed,bpc,bdmax", [(3, 8, 255), (4, 8, 255), (5, 16, 4095), (6, 16, 1023)])
+def test_batch_tx64(pkg, oracle, seed, bpc, bdmax):
+    """64-point transforms (64x64 / 64x32 / 32x64 / 64x16 / 16x64 units,
+    the huge class group) next to every smaller class."""
+    fd = _frame(pkg, width=1024, height=512, bpc=bpc, bitdepth_max=bdmax, seed=seed, tx64=True)
+    import numpy as np
+    big = np.diff(fd.class_start)[[4, 11, 12, 17, 18]]
+    assert big.sum() > 0
+    _check(fd, oracle)
+
+
 def test_batch_4k_full_bitexact(pkg, oracle):
     """BASELINE config 3 at its full size (12.44 Mpx, ~290k units)."""
     _check(_frame(pkg), oracle, threads=8)

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Profiling builds: libdav1d_gpu.<name>.so with one phase of the batch
+# kernel ablated (DGPU_ABL_* in csrc/recon_kernel.hpp), or a tunable changed.  Select one with
+# DAV1D_GPU_LIB_VARIANT=<name>.  Outputs of these builds are wrong by design.
+set -e
+cd "$(dirname "$0")/../dav1d-mirror_amd"
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include -Icsrc"
+mkdir -p build/var
+build() {
+    local name=$1; shift
+    for s in runtime mc ipred itx recon8 recon16; do
+        $HIPCC $F "$@" -c csrc/$s.hip -o build/var/$name.$s.o &
+    done
+    wait
+    $HIPCC $F -shared -o libdav1d_gpu.$name.so build/var/$name.*.o
+}
+for v in ${VARIANTS:-nomc noitx nointra}; do
+    case $v in
+        nomc) build nomc -DDGPU_ABL_MC=1 ;;
+        noitx) build noitx -DDGPU_ABL_ITX=1 ;;
+        nointra) build nointra -DDGPU_ABL_INTRA=1 ;;
+        none) build none -DDGPU_ABL_MC=1 -DDGPU_ABL_ITX=1 -DDGPU_ABL_INTRA=1 ;;
+        noseq) build noseq -DDGPU_SEQREF_MAX_TPL=0 ;;
+        seg4) build seg4 -DDGPU_SEGMENTS=4 ;;
+        seg64) build seg64 -DDGPU_SEGMENTS=64 ;;
+        seg1) build seg1 -DDGPU_SEGMENTS=1 ;;
+    esac
+done
