@@ -5,8 +5,8 @@
 // large: up to 32x32, huge: the 64-point sides), each with its own
 // register and LDS budget.  Within a kernel the waves are scheduled (segment, class):
 // every class's unit range (units are sorted by class and, within a class,
-// by position) is cut into kSegments equal parts, so waves that run at the
-// same time touch the same band of the picture.  Blocks are mapped so each
+// by position) is cut into kSegments runs of equal wave count, so waves
+// that run at the same time touch the same band of the picture.  Blocks are mapped so each
 // XCD works through a contiguous run of bands: a picture line is then
 // written by one XCD's L2 instead of partially by several.
 #pragma once
@@ -38,26 +38,48 @@ template <int BPC, int GRP> __host__ __device__ constexpr int waves_per_block() 
     return GRP == GROUP_HUGE ? 1 : 2;
 }
 
+// log2(lanes_per_unit) of every class packed 3 bits each into a constant
+__host__ __device__ constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
+template <int... TX> constexpr uint64_t pack_log2_lanes(std::integer_sequence<int, TX...>) {
+    uint64_t v = 0;
+    ((v |= (uint64_t)ilog2c(lanes_per_unit(TX)) << (3 * TX)), ...);
+    return v;
+}
+constexpr uint64_t kLog2Lanes = pack_log2_lanes(std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
+
 template <int BPC, int TX, int GRP>
 __device__ __forceinline__ void dispatch_one(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int cls, int first,
-                                             int count, uint8_t *lds) {
+                                             int count, uint8_t *lds, int gw) {
 #ifndef DGPU_ONLY_CLASS
 #define DGPU_ONLY_CLASS -1   // build-time probe: compile a single class (resource studies)
 #endif
     if constexpr (class_group(TX) == GRP && (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS)) {
-        if (cls == TX) recon_units<BPC, TX>(a, pt, first, count, lds);
+        if (cls == TX) recon_units<BPC, TX>(a, pt, first, count, lds, gw, GRP);
     }
 }
 
 template <int BPC, int GRP, int... TX>
 __device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int cls, int first,
-                                         int count, uint8_t *lds, std::integer_sequence<int, TX...>) {
-    (dispatch_one<BPC, TX, GRP>(a, pt, cls, first, count, lds), ...);
+                                         int count, uint8_t *lds, int gw, std::integer_sequence<int, TX...>) {
+    (dispatch_one<BPC, TX, GRP>(a, pt, cls, first, count, lds, gw), ...);
+}
+
+// Minimum waves per SIMD the register allocator must allow, per bitdepth
+// and group: 6 for the 8-bit small group fits in 80 VGPRs without spills
+// (the union of its classes otherwise takes 91); the others are left to the
+// compiler (forcing them spills).
+#ifndef DGPU_WPE_SMALL8
+#define DGPU_WPE_SMALL8 6
+#endif
+template <int BPC, int GRP> constexpr int min_waves_per_eu() {
+    return (BPC == 8 && GRP == GROUP_SMALL) ? DGPU_WPE_SMALL8 : 1;
 }
 
 template <int BPC, int GRP>
-__global__ __launch_bounds__((64 * waves_per_block<BPC, GRP>())) void k_recon(ReconArgs<BPC> a) {
+__global__ __launch_bounds__((64 * waves_per_block<BPC, GRP>()))
+__attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(ReconArgs<BPC> a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const unsigned long long t_entry = DGPU_TRACE ? __builtin_amdgcn_s_memtime() : 0;
     constexpr int WL = wave_lds<BPC, GRP>();
     constexpr int NC = DGPU_N_RECT_TX_SIZES;
     // XCD-contiguous block order: hardware deals blocks round-robin over the
@@ -78,23 +100,23 @@ __global__ __launch_bounds__((64 * waves_per_block<BPC, GRP>())) void k_recon(Re
     }
     const int nb = gridDim.x, b = blockIdx.x;
     const int lb = (b & 7) * (nb >> 3) + (b >> 3);
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int gw = lb * waves_per_block<BPC, GRP>() + wave;
     if (gw >= a.nwaves) return;
-    // locate (segment, class) of this wave: last entry with seg_wave <= gw
-    int lo = 0, hi = kSegments * NC;   // seg_wave[hi] == nwaves > gw
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.seg_wave[mid] <= gw) lo = mid; else hi = mid;
+    // (segment, class) of this wave from the per-segment wave prefix
+    const int wseg = a.wpre[NC];
+    const int s = gw / wseg, r = gw - s * wseg;
+    int cls = 0;
+#pragma unroll
+    for (int c = 1; c < NC; c++) cls += r >= a.wpre[c];
+    const int U = 64 >> (int)((kLog2Lanes >> (3 * cls)) & 7);   // no table load
+    const int first = a.class_start[cls] + (s * a.wps[cls] + r - a.wpre[cls]) * U;
+    const int count = min(U, a.class_start[cls + 1] - first);
+    if (count <= 0) return;
+    if constexpr (DGPU_TRACE) {   // kernel-entry time of this wave
+        if ((threadIdx.x & 63) == 0) a.trace[((size_t)GRP << 20) + (size_t)gw * 16 + 15] = t_entry;
     }
-    const int s = lo / NC, cls = lo % NC;
-    const int cs = a.class_start[cls], n = a.class_start[cls + 1] - cs;
-    const int seg_lo = cs + (int)((long)n * s / kSegments);
-    const int seg_hi = cs + (int)((long)n * (s + 1) / kSegments);
-    const int U = 64 / lanes_per_unit(cls);
-    const int first = seg_lo + (gw - a.seg_wave[lo]) * U;
-    const int count = min(U, seg_hi - first);
-    dispatch<BPC, GRP>(a, pt, cls, first, count, lds + wave * WL,
+    dispatch<BPC, GRP>(a, pt, cls, first, count, lds + wave * WL, gw,
                        std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 
@@ -102,16 +124,17 @@ template <int BPC, int GRP>
 static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned classmask, hipStream_t stream) {
     constexpr int NC = DGPU_N_RECT_TX_SIZES;
     int acc = 0;
-    for (int s = 0; s < kSegments; s++)
-        for (int c = 0; c < NC; c++) {
-            a.seg_wave[s * NC + c] = acc;
-            if (class_group(c) != GRP || !((classmask >> c) & 1)) continue;
-            const int n = b->class_start[c + 1] - b->class_start[c];
-            const int nseg = (int)((long)n * (s + 1) / kSegments) - (int)((long)n * s / kSegments);
-            const int U = 64 / lanes_per_unit(c);
-            acc += (nseg + U - 1) / U;
-        }
-    a.seg_wave[kSegments * NC] = acc;
+    for (int c = 0; c < NC; c++) {
+        a.wpre[c] = acc;
+        a.wps[c] = 0;
+        if (class_group(c) != GRP || !((classmask >> c) & 1)) continue;
+        const int n = b->class_start[c + 1] - b->class_start[c];
+        const int U = 64 / lanes_per_unit(c);
+        a.wps[c] = ((n + U - 1) / U + kSegments - 1) / kSegments;
+        acc += a.wps[c];
+    }
+    a.wpre[NC] = acc;
+    acc *= kSegments;
     a.nwaves = acc;
     if (!acc) return 0;
     constexpr int WPB = waves_per_block<BPC, GRP>();
@@ -169,9 +192,34 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
 
     // Group kernels in order on the caller's stream (cross-stream fork/join
     // measured ~25 us of event overhead per frame on MI355X: slower).
+    static unsigned long long *trace_buf = nullptr;   // DGPU_TRACE builds only
+    if (DGPU_TRACE && !trace_buf && hipMalloc(&trace_buf, (size_t)3 << 23) != hipSuccess) return -3;
+    a.trace = trace_buf;
+    int nw[3] = {0, 0, 0};
     int rc = launch_group<BPC, GROUP_HUGE>(a, b, classmask, stream);
+    nw[2] = a.nwaves;
     if (!rc) rc = launch_group<BPC, GROUP_LARGE>(a, b, classmask, stream);
+    nw[1] = a.nwaves;
     if (!rc) rc = launch_group<BPC, GROUP_SMALL>(a, b, classmask, stream);
+    nw[0] = a.nwaves;
+    if (DGPU_TRACE && !rc) {   // debug: synchronous dump of the phase timestamps
+        const char *f = getenv("DAV1D_GPU_TRACE_FILE");
+        if (f && hipStreamSynchronize(stream) == hipSuccess) {
+            FILE *fp = fopen(f, "ab");
+            for (int g = 0; g < 3 && fp; g++) {
+                const size_t n = (size_t)nw[g] * 16;
+                unsigned long long *h = (unsigned long long *)malloc(n * 8 + 8);
+                if (n && h && hipMemcpy(h, trace_buf + ((size_t)g << 20), n * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                    const int hdr[2] = {g, nw[g]};
+                    fwrite(hdr, sizeof(hdr), 1, fp);
+                    fwrite(h, 8, n, fp);
+                }
+                free(h);
+            }
+            if (fp) fclose(fp);
+            hipMemset(trace_buf, 0, (size_t)3 << 23);
+        }
+    }
     return rc;
 }
 

@@ -43,6 +43,9 @@
 #ifndef DGPU_ABL_INTRA
 #define DGPU_ABL_INTRA 0   // skip intra edge preparation and prediction
 #endif
+#ifndef DGPU_TRACE
+#define DGPU_TRACE 0       // per-wave phase timestamps (tools/wave_trace.py)
+#endif
 
 namespace dgpu {
 
@@ -65,10 +68,14 @@ template <int BPC> struct ReconArgs {
     C *coef;
     const P *edges;
     int class_start[DGPU_N_RECT_TX_SIZES + 1];
-    // wave schedule: waves are ordered (segment, class); seg_wave[s * NC + c]
-    // is the first wave of (segment s, class c), a running prefix.
-    int seg_wave[kSegments * DGPU_N_RECT_TX_SIZES + 1];
+    // wave schedule, ordered (segment, class): every one of the kSegments
+    // segments gives class c wps[c] waves (the class's unit range cut into
+    // kSegments runs of wps[c] * U units); wpre is the prefix of wps, so a
+    // wave's (segment, class, first unit) is arithmetic, no search.
+    int wps[DGPU_N_RECT_TX_SIZES];
+    int wpre[DGPU_N_RECT_TX_SIZES + 1];
     int nwaves;
+    unsigned long long *trace;   // DGPU_TRACE builds only: [group][wave][16] s_memtime
     int bdmax;
     int zero_coefs;
 };
@@ -157,6 +164,7 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x3a1 __attribute__((ext_vector_type(3), aligned(1)));
 typedef uint32_t u32x4a2 __attribute__((ext_vector_type(4), aligned(2)));
 typedef uint32_t u32x2a2 __attribute__((ext_vector_type(2), aligned(2)));
@@ -189,24 +197,29 @@ __device__ __forceinline__ uint32_t pack16(int lo, int hi) {
 }
 
 // Copies bytes [src, src + n) into 16-B aligned LDS at their own 16-B skew
-// (returned) with 16-byte loads.  Reads stay inside the 16-B blocks holding
-// the first and last byte.
-template <int MAXN, int G>
-__device__ __forceinline__ int stage16(uint8_t *dst, const void *src, int n, int l) {
-    const int sk = (int)(reinterpret_cast<uintptr_t>(src) & 15);
-    const uint4 *s = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(src) - sk);
-    const int nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
-    constexpr int IT = ((MAXN + 30) / 16 + G - 1) / G;
-    uint4 v[IT];
+// with 16-byte loads, in two steps so other loads can be issued in between:
+// load() issues the global loads, commit() writes LDS and returns the skew.
+// Reads stay inside the 16-B blocks holding the first and last byte.
+template <int MAXN, int G> struct Stage {
+    static constexpr int IT = ((MAXN + 30) / 16 + G - 1) / G;
+    u32x4 v[IT];
+    int sk, nch;
+    __device__ __forceinline__ void load(const void *src, int n, int l) {
+        sk = (int)(reinterpret_cast<uintptr_t>(src) & 15);
+        const uint8_t *s = reinterpret_cast<const uint8_t *>(src) - sk;
+        nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
 #pragma unroll
-    for (int k = 0; k < IT; k++) v[k] = s[min(l + k * G, nch - 1)];   // clamped: always a valid block
-#pragma unroll
-    for (int k = 0; k < IT; k++) {
-        const int i = l + k * G;
-        if (i < nch) reinterpret_cast<uint4 *>(dst)[i] = v[k];
+        for (int k = 0; k < IT; k++) v[k] = gld<u32x4>(s + 16 * min(l + k * G, nch - 1));   // clamped
     }
-    return sk;
-}
+    __device__ __forceinline__ int commit(uint8_t *dst, int l) const {
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int i = l + k * G;
+            if (i < nch) reinterpret_cast<u32x4 *>(dst)[i] = v[k];
+        }
+        return sk;
+    }
+};
 
 // ---------------------------------------------------------------- intra ---
 
@@ -497,113 +510,106 @@ __device__ __forceinline__ int mc_bank(int type, bool bil, int len) {
 // footprint origin (block position - 3 rows - 3 columns).  Rows are read
 // with unaligned 12-byte (8bpc) / 24-byte (16bpc) loads, one per row and
 // quad.  G is a multiple of QW for every class, so a lane's quad is fixed
-// and its row pairs advance by G / QW.
-template <int BPC, int TX>
-__device__ __forceinline__ void mc_hpass(const typename Px<BPC>::pixel *org, int stride_px, uint32_t *mid,
-                                         int bank, int m, int ib, int l) {
+// and its row pairs advance by G / QW.  Split in steps so the loads of the
+// first chunk (all of them below the 64-point classes) are issued together
+// with the unit's other loads: init + load(0) ... compute(0) + rest().
+template <int BPC, int TX> struct HPass {
     using CL = Cls<TX>;
-    constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NH = CL::NH, RP = CL::RP;
-    constexpr int IT = (NH + G - 1) / G;
-    constexpr int PS = G / QW;   // row-pair step per task
+    static constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NH = CL::NH, RP = CL::RP;
+    static constexpr int IT = (NH + G - 1) / G;
+    static constexpr int PS = G / QW;   // row-pair step per task
     static_assert(G % QW == 0, "lane quads must be fixed");
-    constexpr int B = BPC / 8;
-    const unsigned sb = (unsigned)stride_px * B;
-    const int q = l % QW, p0 = l / QW;
-    const uint8_t *rp = reinterpret_cast<const uint8_t *>(org) + (size_t)(2u * p0 * sb) + 4 * B * q;
-    uint32_t *mp = mid + p0 * W + 4 * q;
-    if constexpr (BPC == 8) {
-        const uint2 th = reinterpret_cast<const uint2 *>(dspt_mc8)[bank * 16 + m];
-        // taps sum to 64 and p ^ 0x80 == p - 128 as int8: s = acc + 128 * 64,
-        // and the reference's mid = (s + 2) >> 2 (intermediate_bits 4) is
-        // stored here as mid - 2048 = (acc + 2) >> 2; the vertical pass adds
-        // back 64 * 2048 (kMidBias8).  Both forms fit int16 for 8-bit input.
-        constexpr int CH = cmin(IT, 3);   // tasks whose loads are in flight together
+    static constexpr int B = BPC / 8;
+    static constexpr int CH = cmin(IT, BPC == 8 ? 3 : 2);   // tasks whose loads are in flight together
+    using Raw = typename std::conditional<BPC == 8, u32x3a1, u32x4a2>::type;
+    Raw ra[CH][2];
+    u32x2a2 rb[CH][2];   // 16bpc: pixels 8..11 of each row
+    const uint8_t *rp;
+    uint32_t *mp;
+    unsigned sb;
+    int p0;
+    uint4 th;            // taps: 8bpc .x/.y int8 x4, 16bpc int16 pairs
+
+    __device__ __forceinline__ void init(const typename Px<BPC>::pixel *org, int stride_px, uint32_t *mid, int bank,
+                                         int m, int l) {
+        sb = (unsigned)stride_px * B;
+        const int q = l % QW;
+        p0 = l / QW;
+        rp = reinterpret_cast<const uint8_t *>(org) + (size_t)(2u * p0 * sb) + 4 * B * q;
+        mp = mid + p0 * W + 4 * q;
+        if constexpr (BPC == 8) {
+            const uint2 t = reinterpret_cast<const uint2 *>(dspt_mc8)[bank * 16 + m];
+            th = make_uint4(t.x, t.y, 0, 0);
+        } else {
+            th = reinterpret_cast<const uint4 *>(dspt_mc16)[bank * 16 + m];
+        }
+    }
+    __device__ __forceinline__ void load(int k0) {
 #pragma unroll
-        for (int k0 = 0; k0 < IT; k0 += CH) {
-            u32x3a1 raw[CH][2];
-#pragma unroll
-            for (int c = 0; c < CH; c++) {   // clamped: the loads stay inside the footprint
-                const int p = cmin(p0 + (k0 + c) * PS, RP - 1);
-                const uint8_t *r0 = rp + (size_t)((unsigned)(p - p0) * 2u * sb);
-                raw[c][0] = gld<u32x3a1>(r0);
-                // row 2p+1 == H+7 (last pair) is never used: re-read row 2p
-                raw[c][1] = gld<u32x3a1>(2 * p + 1 < H + 7 ? r0 + sb : r0);
+        for (int c = 0; c < CH; c++) {   // clamped: the loads stay inside the footprint
+            const int p = cmin(p0 + (k0 + c) * PS, RP - 1);
+            const uint8_t *a0 = rp + (size_t)((unsigned)(p - p0) * 2u * sb);
+            // row 2p+1 == H+7 (last pair) is never used: re-read row 2p
+            const uint8_t *a1 = 2 * p + 1 < H + 7 ? a0 + sb : a0;
+            ra[c][0] = gld<Raw>(a0);
+            ra[c][1] = gld<Raw>(a1);
+            if constexpr (BPC == 16) {
+                rb[c][0] = gld<u32x2a2>(a0 + 16);
+                rb[c][1] = gld<u32x2a2>(a1 + 16);
             }
+        }
+    }
+    __device__ __forceinline__ void compute(int k0, int ib) {
 #pragma unroll
-            for (int c = 0; c < CH; c++) {
-                const int p = p0 + (k0 + c) * PS;
-                if (k0 + c < IT && p < RP) {
-                    int mm[2][4];
+        for (int c = 0; c < CH; c++) {
+            const int p = p0 + (k0 + c) * PS;
+            if (k0 + c < IT && p < RP) {
+                int mm[2][4];
 #pragma unroll
-                    for (int rr = 0; rr < 2; rr++) {
-                        const uint32_t w0 = raw[c][rr].x ^ 0x80808080u;
-                        const uint32_t w1 = raw[c][rr].y ^ 0x80808080u;
-                        const uint32_t w2 = raw[c][rr].z ^ 0x80808080u;
+                for (int rr = 0; rr < 2; rr++) {
+                    if constexpr (BPC == 8) {
+                        // taps sum to 64 and p ^ 0x80 == p - 128 as int8: s = acc + 128 * 64,
+                        // and the reference's mid = (s + 2) >> 2 (intermediate_bits 4) is
+                        // stored as mid - 2048 = (acc + 2) >> 2; the vertical pass adds back
+                        // 64 * 2048 (kMidBias).  Both forms fit int16 for 8-bit input.
+                        const uint32_t w0 = ra[c][rr].x ^ 0x80808080u;
+                        const uint32_t w1 = ra[c][rr].y ^ 0x80808080u;
+                        const uint32_t w2 = ra[c][rr].z ^ 0x80808080u;
                         mm[rr][0] = dot4(w1, th.y, dot4(w0, th.x, 2)) >> 2;
                         mm[rr][1] = dot4(alb(w2, w1, 1), th.y, dot4(alb(w1, w0, 1), th.x, 2)) >> 2;
                         mm[rr][2] = dot4(alb(w2, w1, 2), th.y, dot4(alb(w1, w0, 2), th.x, 2)) >> 2;
                         mm[rr][3] = dot4(alb(w2, w1, 3), th.y, dot4(alb(w1, w0, 3), th.x, 2)) >> 2;
-                    }
-                    uint4 o;
-                    o.x = pack16(mm[0][0], mm[1][0]);
-                    o.y = pack16(mm[0][1], mm[1][1]);
-                    o.z = pack16(mm[0][2], mm[1][2]);
-                    o.w = pack16(mm[0][3], mm[1][3]);
-                    *reinterpret_cast<uint4 *>(mp + (k0 + c) * PS * W) = o;
-                }
-            }
-        }
-    } else {
-        const uint4 th = reinterpret_cast<const uint4 *>(dspt_mc16)[bank * 16 + m];
-        const int sh = 6 - ib, rnd = (1 << sh) >> 1;
-        constexpr int CH = cmin(IT, 2);
-#pragma unroll
-        for (int k0 = 0; k0 < IT; k0 += CH) {
-            u32x4a2 ra[CH][2];
-            u32x2a2 rb[CH][2];
-#pragma unroll
-            for (int c = 0; c < CH; c++) {
-                const int p = cmin(p0 + (k0 + c) * PS, RP - 1);
-                const uint8_t *a0 = rp + (size_t)((unsigned)(p - p0) * 2u * sb);
-                const uint8_t *a1 = 2 * p + 1 < H + 7 ? a0 + sb : a0;
-                ra[c][0] = gld<u32x4a2>(a0);
-                rb[c][0] = gld<u32x2a2>(a0 + 16);
-                ra[c][1] = gld<u32x4a2>(a1);
-                rb[c][1] = gld<u32x2a2>(a1 + 16);
-            }
-#pragma unroll
-            for (int c = 0; c < CH; c++) {
-                const int p = p0 + (k0 + c) * PS;
-                if (k0 + c < IT && p < RP) {
-                    int mm[2][4];
-#pragma unroll
-                    for (int rr = 0; rr < 2; rr++) {
+                    } else {
+                        const int sh = 6 - ib, rnd = (1 << sh) >> 1;
                         // e: pixel pairs (2i, 2i+1), o: (2i+1, 2i+2)
                         const uint32_t e[6] = {ra[c][rr].x, ra[c][rr].y, ra[c][rr].z, ra[c][rr].w,
                                                rb[c][rr].x, rb[c][rr].y};
                         uint32_t o[5];
 #pragma unroll
                         for (int i = 0; i < 5; i++) o[i] = alb(e[i + 1], e[i], 2);
-                        const int s0 = dot2(e[3], th.w, dot2(e[2], th.z, dot2(e[1], th.y, dot2(e[0], th.x, 0))));
-                        const int s1 = dot2(o[3], th.w, dot2(o[2], th.z, dot2(o[1], th.y, dot2(o[0], th.x, 0))));
-                        const int s2 = dot2(e[4], th.w, dot2(e[3], th.z, dot2(e[2], th.y, dot2(e[1], th.x, 0))));
-                        const int s3 = dot2(o[4], th.w, dot2(o[3], th.z, dot2(o[2], th.y, dot2(o[1], th.x, 0))));
-                        mm[rr][0] = (s0 + rnd) >> sh;
-                        mm[rr][1] = (s1 + rnd) >> sh;
-                        mm[rr][2] = (s2 + rnd) >> sh;
-                        mm[rr][3] = (s3 + rnd) >> sh;
+                        mm[rr][0] = (dot2(e[3], th.w, dot2(e[2], th.z, dot2(e[1], th.y, dot2(e[0], th.x, 0)))) + rnd) >> sh;
+                        mm[rr][1] = (dot2(o[3], th.w, dot2(o[2], th.z, dot2(o[1], th.y, dot2(o[0], th.x, 0)))) + rnd) >> sh;
+                        mm[rr][2] = (dot2(e[4], th.w, dot2(e[3], th.z, dot2(e[2], th.y, dot2(e[1], th.x, 0)))) + rnd) >> sh;
+                        mm[rr][3] = (dot2(o[4], th.w, dot2(o[3], th.z, dot2(o[2], th.y, dot2(o[1], th.x, 0)))) + rnd) >> sh;
                     }
-                    uint4 o;
-                    o.x = pack16(mm[0][0], mm[1][0]);
-                    o.y = pack16(mm[0][1], mm[1][1]);
-                    o.z = pack16(mm[0][2], mm[1][2]);
-                    o.w = pack16(mm[0][3], mm[1][3]);
-                    *reinterpret_cast<uint4 *>(mp + (k0 + c) * PS * W) = o;
                 }
+                uint4 o;
+                o.x = pack16(mm[0][0], mm[1][0]);
+                o.y = pack16(mm[0][1], mm[1][1]);
+                o.z = pack16(mm[0][2], mm[1][2]);
+                o.w = pack16(mm[0][3], mm[1][3]);
+                *reinterpret_cast<uint4 *>(mp + (k0 + c) * PS * W) = o;
             }
         }
     }
-}
+    __device__ __forceinline__ void rest(int ib) {   // chunks after the first (64-point classes)
+#pragma unroll
+        for (int k0 = CH; k0 < IT; k0 += CH) {
+            load(k0);
+            compute(k0, ib);
+        }
+    }
+};
 
 // Vertical pass of one reference for a 4x2 task: t[i] = the 8-tap sum over
 // stored intermediates, rows j*2 (i < 4) and j*2+1 (i >= 4), columns
@@ -630,7 +636,7 @@ __device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, cons
 
 template <int BPC, int TX>
 __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int first, int count,
-                                            uint8_t *wave_lds) {
+                                            uint8_t *wave_lds, int gw, int grp) {
     using CL = Cls<TX>;
     using SL = Slot<BPC, TX>;
     using P = typename Px<BPC>::pixel;
@@ -641,8 +647,18 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     const int lane = threadIdx.x & 63;
     const int g = lane / G, l = lane % G;
     if (g >= count) return;
+    // DGPU_TRACE: timestamp phase i after draining this wave's memory ops
+    auto mark = [&](int i) {
+        if constexpr (DGPU_TRACE) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (lane == 0) a.trace[((size_t)grp << 20) + (size_t)gw * 16 + i] = t;
+        }
+    };
+    mark(0);
 
     const Dav1dGpuUnit u = a.units[first + g];
+    mark(1);
     uint8_t *slot = wave_lds + g * SL::BYTES;
     uint8_t *cfl = slot;                                           // staged coefs, then residual
     TT *res = reinterpret_cast<TT *>(slot);
@@ -667,41 +683,59 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     P *dstp = pt.dst[plane] + u.dst_off;
     const int ds = pt.dst_stride[plane];
 
-    // ---------------- P1: coefficient region and intra edges into LDS ----------------
+    // ---------------- P1: every global load of the unit, then the LDS commits --------------
+    // (coefficients, intra edges and the first ref's footprint rows are in
+    // flight together: one memory round trip after the descriptor)
     C *cf = a.coef + u.coef_off;
     const int ncoef = nores ? 0 : dconly ? 1 : nzw * nzh;
-    int cfsk = 0;
-    if (ncoef) cfsk = stage16<CL::SW * CL::SH * (int)sizeof(C), G>(cfl, cf, ncoef * (int)sizeof(C), l);
-    const P *tl = nullptr;
-    if (pred == DGPU_PRED_INTRA) {
-        const P *es = a.edges + u.p.intra.edge_off - 2 * H;
-        const int esk = stage16<SL::EDGE * (int)sizeof(P), G>(src, es, SL::EDGE * (int)sizeof(P), l);
-        tl = reinterpret_cast<const P *>(src + esk) + 2 * H;
-    }
+    Stage<CL::SW * CL::SH * (int)sizeof(C), G> cst;
+    if (ncoef) cst.load(cf, ncoef * (int)sizeof(C), l);
+    Stage<SL::EDGE * (int)sizeof(P), G> est;
+    if (pred == DGPU_PRED_INTRA) est.load(a.edges + u.p.intra.edge_off - 2 * H, SL::EDGE * (int)sizeof(P), l);
 
-    // ---------------- P2: mc horizontal pass(es) ----------------
     const int f2d = inter ? u.p.inter.filter2d : 0;
     const bool bil = f2d == DGPU_FILTER_2D_BILINEAR;
     // filter_type = type_h | type_v << 2 per Filter2d (src/mc_tmpl.c:376-384)
     const int ftype = bil ? 0 : (int)((0x951a62840ull >> (4 * f2d)) & 15);
     const int bw = u.bw4 * 4, bh = u.bh4 * 4;
     const int bank_h = mc_bank(ftype & 3, bil, bw), bank_v = mc_bank(ftype >> 2, bil, bh);
-    // vertical taps are loaded here so their latency overlaps the h-pass
     const uint4 tv0 = inter ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[0]]
                             : make_uint4(0, 0, 0, 0);
     const uint4 tv1 = comp ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[1]]
                            : make_uint4(0, 0, 0, 0);
-    auto hpass = [&](int k) {
+    auto hinit = [&](HPass<BPC, TX> &hp, int k) {
         const int r = k ? u.p.inter.ref[1] : u.p.inter.ref[0];
         const int rs = pt.ref_stride[r * 3 + plane];
         const P *org = pt.ref[r * 3 + plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
-        mc_hpass<BPC, TX>(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], ib, l);
+        hp.init(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], l);
     };
-    if (inter && !DGPU_ABL_MC) {
-        hpass(0);
+    auto hpass = [&](int k) {   // the whole h-pass of ref k
+        HPass<BPC, TX> hp;
+        hinit(hp, k);
+        hp.load(0);
+        hp.compute(0, ib);
+        hp.rest(ib);
+    };
+    const bool do_mc = inter && !DGPU_ABL_MC;
+    HPass<BPC, TX> hp0;
+    if (do_mc) {
+        hinit(hp0, 0);
+        hp0.load(0);
+    }
+    int cfsk = 0;
+    if (ncoef) cfsk = cst.commit(cfl, l);
+    const P *tl = nullptr;
+    if (pred == DGPU_PRED_INTRA) tl = reinterpret_cast<const P *>(src + est.commit(src, l)) + 2 * H;
+    mark(2);
+
+    // ---------------- P2: mc horizontal pass(es) ----------------
+    if (do_mc) {
+        hp0.compute(0, ib);
+        hp0.rest(ib);
         if (!CL::SEQREF && comp) hpass(1);
     }
     wave_sync();
+    mark(3);
 
     // coefficient zeroing (the reference's itx zeroes what it consumed,
     // src/itx_tmpl.c:55/89); loads above completed before the LDS writes
@@ -763,6 +797,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     }
     wave_sync();
 
+    mark(4);
     // ---------------- P4: column transforms -> residual [W][H] ----------------
     if (haveres) {
 #pragma unroll
@@ -793,82 +828,13 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
     }
 
-    // ---------------- P5: intra edge preparation ----------------
-    IntraState is{};
-    if (pred == DGPU_PRED_INTRA && !DGPU_ABL_INTRA) {
-        is = intra_prep<BPC, TX>(u, tl, fe, l, bdmax);
-        wave_sync();
-        if (is.mode == DGPU_FILTER_PRED) filter_intra<TX>(u, tl, ptile, l, bdmax);
-    }
     wave_sync();
+    mark(5);
 
-    // ---------------- P6a: first ref of a compound unit (SEQREF) ----------------
-    // prep values rnd_sh(t, 6) (the reference's mct output + PREP_BIAS), kept
-    // in registers while the second ref's h-pass reuses the tile
-    int q0[CL::SEQREF ? TPL : 1][8];
-    if (CL::SEQREF && comp && !DGPU_ABL_MC) {
-#pragma unroll
-        for (int k = 0; k < TPL; k++) {
-            const int t = l + k * G;
-            if (t < NT) {
-                int t0[8];
-                mc_vtask<W>(mid0, t / QW, t % QW, tv0, t0);
-#pragma unroll
-                for (int i = 0; i < 8; i++) q0[k][i] = (t0[i] + (kMidBias<BPC> + 32)) >> 6;
-            }
-        }
-        wave_sync();
-        hpass(1);
-        wave_sync();
-    }
-
-    // ---------------- P6: prediction + residual -> picture ----------------
-#pragma unroll
-    for (int k = 0; k < TPL; k++) {
-        const int t = l + k * G;
-        if (t >= NT) break;
-        const int j = t / QW, q = t % QW;   // rows 2j, 2j+1; columns 4q..4q+3
-        int pv[8];
-        if (inter && DGPU_ABL_MC) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) pv[i] = 0;
-        } else if (inter) {
-            if (comp) {   // prep x2 (rnd_sh(t, 6) - PB) then avg_c, src/mc_tmpl.c:587-602
-                int p0[8], t1[8];
-                if constexpr (CL::SEQREF) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) p0[i] = q0[k][i];
-                } else {
-                    int t0[8];
-                    mc_vtask<W>(mid0, j, q, tv0, t0);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) p0[i] = (t0[i] + (kMidBias<BPC> + 32)) >> 6;
-                }
-                mc_vtask<W>(mid1, j, q, tv1, t1);
-#pragma unroll
-                for (int i = 0; i < 8; i++)
-                    pv[i] = clampi((p0[i] + ((t1[i] + (kMidBias<BPC> + 32)) >> 6) + (1 << ib)) >> (ib + 1), 0, bdmax);
-            } else {
-                int t0[8];
-                const int sh = 6 + ib;   // put: rnd_sh(t, 6 + ib)
-                mc_vtask<W>(mid0, j, q, tv0, t0);
-#pragma unroll
-                for (int i = 0; i < 8; i++) pv[i] = clampi((t0[i] + (kMidBias<BPC> + (1 << (sh - 1)))) >> sh, 0, bdmax);
-            }
-        } else if (pred == DGPU_PRED_INTRA && DGPU_ABL_INTRA) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) pv[i] = 0;
-        } else if (pred == DGPU_PRED_INTRA) {
-            if (is.mode == DGPU_FILTER_PRED) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) pv[i] = ptile[(2 * j + (i >> 2)) * W + 4 * q + (i & 3)];
-            } else {
-                intra_task<TX>(is, tl, fe, 4 * q, 2 * j, pv);
-            }
-        } else {   // PRED_NONE: the residual goes onto the picture
-#pragma unroll
-            for (int i = 0; i < 8; i++) pv[i] = gld<P>(dstp + (2 * j + (i >> 2)) * ds + 4 * q + (i & 3));
-        }
+    // ---------------- P5/P6: prediction + residual -> picture ----------------
+    // One loop per prediction kind, so values of one kind's path are not
+    // live (register pressure) in another's.
+    auto emit = [&](int j, int q, const int *pv) {   // + residual, clip, store 2 rows of 4
         int rv[8];
         if (haveres) {
 #pragma unroll
@@ -900,7 +866,111 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             else
                 gst<u32x2>(row, u32x2{(uint32_t)o0 | o1 << 16, (uint32_t)o2 | (uint32_t)o3 << 16});
         }
+    };
+
+    if (inter) {
+        if (DGPU_ABL_MC) {
+            int pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < TPL; k++) {
+                const int t = l + k * G;
+                if (t < NT) emit(t / QW, t % QW, pv);
+            }
+        } else if (comp) {   // prep x2 (rnd_sh(t, 6) - PB) then avg_c, src/mc_tmpl.c:587-602
+            constexpr int KP = kMidBias<BPC> + 32;
+            int q0[CL::SEQREF ? TPL : 1][8];
+            if constexpr (CL::SEQREF) {
+                // first ref's prep values in registers while the second
+                // ref's h-pass reuses the intermediate tile
+#pragma unroll
+                for (int k = 0; k < TPL; k++) {
+                    const int t = l + k * G;
+                    if (t < NT) {
+                        int t0[8];
+                        mc_vtask<W>(mid0, t / QW, t % QW, tv0, t0);
+#pragma unroll
+                        for (int i = 0; i < 8; i++) q0[k][i] = (t0[i] + KP) >> 6;
+                    }
+                }
+                wave_sync();
+                mark(6);
+                hpass(1);
+                wave_sync();
+                mark(7);
+            }
+#pragma unroll
+            for (int k = 0; k < TPL; k++) {
+                const int t = l + k * G;
+                if (t >= NT) break;
+                const int j = t / QW, q = t % QW;
+                int p0[8], t1[8], pv[8];
+                if constexpr (CL::SEQREF) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) p0[i] = q0[k][i];
+                } else {
+                    int t0[8];
+                    mc_vtask<W>(mid0, j, q, tv0, t0);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) p0[i] = (t0[i] + KP) >> 6;
+                }
+                mc_vtask<W>(mid1, j, q, tv1, t1);
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+                    pv[i] = clampi((p0[i] + ((t1[i] + KP) >> 6) + (1 << ib)) >> (ib + 1), 0, bdmax);
+                emit(j, q, pv);
+            }
+        } else {   // put: rnd_sh(t, 6 + ib)
+            const int sh = 6 + ib, kp = kMidBias<BPC> + (1 << (sh - 1));
+#pragma unroll
+            for (int k = 0; k < TPL; k++) {
+                const int t = l + k * G;
+                if (t >= NT) break;
+                const int j = t / QW, q = t % QW;
+                int t0[8], pv[8];
+                mc_vtask<W>(mid0, j, q, tv0, t0);
+#pragma unroll
+                for (int i = 0; i < 8; i++) pv[i] = clampi((t0[i] + kp) >> sh, 0, bdmax);
+                emit(j, q, pv);
+            }
+        }
+    } else if (pred == DGPU_PRED_INTRA) {
+        IntraState is{};
+        if (!DGPU_ABL_INTRA) {
+            is = intra_prep<BPC, TX>(u, tl, fe, l, bdmax);
+            wave_sync();
+            if (is.mode == DGPU_FILTER_PRED) filter_intra<TX>(u, tl, ptile, l, bdmax);
+            wave_sync();
+        }
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t >= NT) break;
+            const int j = t / QW, q = t % QW;
+            int pv[8];
+            if (DGPU_ABL_INTRA) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) pv[i] = 0;
+            } else if (is.mode == DGPU_FILTER_PRED) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) pv[i] = ptile[(2 * j + (i >> 2)) * W + 4 * q + (i & 3)];
+            } else {
+                intra_task<TX>(is, tl, fe, 4 * q, 2 * j, pv);
+            }
+            emit(j, q, pv);
+        }
+    } else {   // PRED_NONE: the residual goes onto the picture
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t >= NT) break;
+            const int j = t / QW, q = t % QW;
+            int pv[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) pv[i] = gld<P>(dstp + (2 * j + (i >> 2)) * ds + 4 * q + (i & 3));
+            emit(j, q, pv);
+        }
     }
+    mark(8);
 }
 
 }  // namespace dgpu

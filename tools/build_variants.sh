@@ -25,5 +25,6 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         seg4) build seg4 -DDGPU_SEGMENTS=4 ;;
         seg64) build seg64 -DDGPU_SEGMENTS=64 ;;
         seg1) build seg1 -DDGPU_SEGMENTS=1 ;;
+        trace) build trace -DDGPU_TRACE=1 ;;
     esac
 done

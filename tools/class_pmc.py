@@ -66,11 +66,29 @@ def summarise(path):
         print(f"{w:2d}x{h:<2d} {cnt[t]:7d}  " + "  ".join(f"{m[n]:14.0f}" for n in names) + extra)
 
 
+def durations(path):
+    """Kernel-trace durations per class (rocprofv3 --kernel-trace run of this script)."""
+    pkg, fd, cls, cnt = classes_with_units()
+    rows = []
+    for r in csv.DictReader(open(path)):
+        if "k_recon" in r["Kernel_Name"]:
+            rows.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3))
+    rows.sort()
+    assert len(rows) == REPS * len(cls)
+    for i, t in enumerate(cls):
+        d = sorted(x[1] for x in rows[i * REPS:(i + 1) * REPS])
+        w, h = pkg.abi.TX_WH[t]
+        print(f"{w:2d}x{h:<2d} {cnt[t]:7d} units  kernel {d[len(d) // 2]:7.1f} us")
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--summarise")
+    ap.add_argument("--durations")
     a = ap.parse_args()
-    if a.summarise:
+    if a.durations:
+        durations(a.durations)
+    elif a.summarise:
         summarise(a.summarise)
     else:
         run()
