@@ -61,6 +61,29 @@ def cpu_baseline(fd, budget_s=12.0):
                       f"{el:.1f} s single-thread, oracle/dsp_ref.c -O2 (restatement of dav1d C, not dav1d)"}
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "v3i_pmc_summary.json")
+
+
+def pmc_traffic(bpc):
+    """HBM bytes per launch of the same kernels from the committed rocprofv3
+    PMC summary (FETCH_SIZE and WRITE_SIZE, separate --pmc passes, KB as
+    rocprofv3 reports them).  PMC needs rocprofv3 around the process, so a
+    plain bench run cannot re-measure it; the source file is named."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None, None
+    tot = 0.0
+    for k, v in d.items():
+        if k.startswith(f"k_recon<{bpc},") and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            tot += (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
+    if not tot:
+        return None, None
+    return int(tot), (f"FETCH_SIZE+WRITE_SIZE per frame from {os.path.relpath(PMC_SUMMARY, ROOT)} "
+                      "(uncorrected: the gfx950 x2 FETCH factor holds for wide coalesced reads, "
+                      "not these scattered row loads)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -136,6 +159,7 @@ def main():
         log(f"[rank 0] bit-exact vs oracle: {check}")
 
     if rank == 0:
+        traffic, traffic_note = pmc_traffic(cfg.bpc) if args.config == "4k" else (None, None)
         value = sh.aggregate_gpix_per_s(fd.stats["pixels"], args.steps, world, el)
         bytes_launch = fd.stats["total_bytes"]
         achieved = bytes_launch / kern_s / 1e9
@@ -168,8 +192,10 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
-                "kernel": f"k_recon<{cfg.bpc},0..2> (one launch per class group; events bracket the step's launches)",
+                "traffic": traffic,
+                "traffic_note": traffic_note,
+                "kernel": f"k_recon<{cfg.bpc},*> (main group: all classes up to 32x32 in one launch; "
+                          "the 64-point group launches only when such units exist; events bracket the step)",
                 "kernel_us": round(kern_s * 1e6, 2),
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "bytes_breakdown": {k: fd.stats[k] for k in

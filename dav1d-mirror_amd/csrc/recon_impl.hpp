@@ -65,11 +65,11 @@ __device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, const PlaneTab
 }
 
 // Minimum waves per SIMD the register allocator must allow, per bitdepth
-// and group: 6 for the 8-bit small group fits in 80 VGPRs without spills
-// (the union of its classes otherwise takes 91); the others are left to the
-// compiler (forcing them spills).
+// and group: 5 for the 8-bit main group (small + large classes) fits in 96
+// VGPRs without spills (left alone it takes ~102, 4 waves: measured 2 us
+// slower); the others are left to the compiler (forcing them spills).
 #ifndef DGPU_WPE_SMALL8
-#define DGPU_WPE_SMALL8 6
+#define DGPU_WPE_SMALL8 5
 #endif
 template <int BPC, int GRP> constexpr int min_waves_per_eu() {
     return (BPC == 8 && GRP == GROUP_SMALL) ? DGPU_WPE_SMALL8 : 1;
@@ -106,11 +106,12 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     // (segment, class) of this wave from the per-segment wave prefix
     const int wseg = a.wpre[NC];
     const int s = gw / wseg, r = gw - s * wseg;
-    int cls = 0;
+    int pos = 0;   // schedule position inside the segment (kOrder)
 #pragma unroll
-    for (int c = 1; c < NC; c++) cls += r >= a.wpre[c];
+    for (int c = 1; c < NC; c++) pos += r >= a.wpre[c];
+    const int cls = order_class(pos);
     const int U = 64 >> (int)((kLog2Lanes >> (3 * cls)) & 7);   // no table load
-    const int first = a.class_start[cls] + (s * a.wps[cls] + r - a.wpre[cls]) * U;
+    const int first = a.class_start[cls] + (s * a.wps[pos] + r - a.wpre[pos]) * U;
     const int count = min(U, a.class_start[cls + 1] - first);
     if (count <= 0) return;
     if constexpr (DGPU_TRACE) {   // kernel-entry time of this wave
@@ -124,14 +125,15 @@ template <int BPC, int GRP>
 static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned classmask, hipStream_t stream) {
     constexpr int NC = DGPU_N_RECT_TX_SIZES;
     int acc = 0;
-    for (int c = 0; c < NC; c++) {
-        a.wpre[c] = acc;
-        a.wps[c] = 0;
+    for (int k = 0; k < NC; k++) {   // wps / wpre indexed by schedule position
+        const int c = kOrder[k];
+        a.wpre[k] = acc;
+        a.wps[k] = 0;
         if (class_group(c) != GRP || !((classmask >> c) & 1)) continue;
         const int n = b->class_start[c + 1] - b->class_start[c];
         const int U = 64 / lanes_per_unit(c);
-        a.wps[c] = ((n + U - 1) / U + kSegments - 1) / kSegments;
-        acc += a.wps[c];
+        a.wps[k] = ((n + U - 1) / U + kSegments - 1) / kSegments;
+        acc += a.wps[k];
     }
     a.wpre[NC] = acc;
     acc *= kSegments;

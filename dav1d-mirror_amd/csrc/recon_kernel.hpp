@@ -68,10 +68,11 @@ template <int BPC> struct ReconArgs {
     C *coef;
     const P *edges;
     int class_start[DGPU_N_RECT_TX_SIZES + 1];
-    // wave schedule, ordered (segment, class): every one of the kSegments
-    // segments gives class c wps[c] waves (the class's unit range cut into
-    // kSegments runs of wps[c] * U units); wpre is the prefix of wps, so a
-    // wave's (segment, class, first unit) is arithmetic, no search.
+    // wave schedule, ordered (segment, class position): every one of the
+    // kSegments segments gives the class at position k (kOrder) wps[k]
+    // waves (its unit range cut into kSegments runs of wps[k] * U units);
+    // wpre is the prefix of wps, so a wave's (segment, class, first unit)
+    // is arithmetic, no search.
     int wps[DGPU_N_RECT_TX_SIZES];
     int wpre[DGPU_N_RECT_TX_SIZES + 1];
     int nwaves;
@@ -111,11 +112,33 @@ __host__ __device__ constexpr int lanes_per_unit(int tx) {
     return cmin(cmax(cmin(w * h / 8, cmax(w, cmin(h, 32))), 2), 64);
 }
 // class groups, each its own kernel with its own register / LDS budget:
-// small (w*h <= 128), large (up to 32x32), huge (the 64-point sides)
+// small (w*h <= 128), large (up to 32x32), huge (the 64-point sides).
+// By default (DGPU_MERGE_GROUPS) small and large are one launch: the large
+// classes' long-latency waves then overlap the small classes' work
+// (measured 76 -> 64 us per 4K frame against two launches back to back).
+#ifndef DGPU_MERGE_GROUPS
+#define DGPU_MERGE_GROUPS 1
+#endif
 enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2, N_GROUPS = 3 };
 __host__ __device__ constexpr int class_group(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
-    return (w == 64 || h == 64) ? GROUP_HUGE : (w * h <= 128 ? GROUP_SMALL : GROUP_LARGE);
+    return (w == 64 || h == 64) ? GROUP_HUGE
+         : (w * h <= 128 || DGPU_MERGE_GROUPS) ? GROUP_SMALL : GROUP_LARGE;
+}
+// Order of the classes inside one schedule segment: largest first, so
+// their long-latency waves start early.  kOrder[position] = class.
+constexpr int kOrder[DGPU_N_RECT_TX_SIZES] = {3, 9, 10, 2, 15, 16, 7, 8, 1, 13, 14, 5, 6, 0, 4, 11, 12, 17, 18};
+__host__ __device__ constexpr uint64_t pack_order(int half) {
+    uint64_t v = 0;
+    for (int i = 0; i < 12; i++) {
+        const int k = half * 12 + i;
+        if (k < DGPU_N_RECT_TX_SIZES) v |= (uint64_t)kOrder[k] << (5 * i);
+    }
+    return v;
+}
+__device__ __forceinline__ int order_class(int k) {   // kOrder[k] without a memory load
+    constexpr uint64_t lo = pack_order(0), hi = pack_order(1);
+    return (int)(((k < 12 ? lo : hi) >> (5 * (k < 12 ? k : k - 12))) & 31);
 }
 
 template <int TX> struct Cls {

@@ -26,5 +26,11 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         seg64) build seg64 -DDGPU_SEGMENTS=64 ;;
         seg1) build seg1 -DDGPU_SEGMENTS=1 ;;
         trace) build trace -DDGPU_TRACE=1 ;;
+        merge) build merge -DDGPU_MERGE_GROUPS=1 ;;
+        merge5) build merge5 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=5 ;;
+        merge4) build merge4 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=1 ;;
+        merge6) build merge6 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=6 ;;
+        m5seg8) build m5seg8 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=5 -DDGPU_SEGMENTS=8 ;;
+        m5seg32) build m5seg32 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=5 -DDGPU_SEGMENTS=32 ;;
     esac
 done
