@@ -18,7 +18,7 @@ N_TX = len(TX_WH)
 DCT_DCT, IDTX, H_DCT, WHT_WHT = 0, 9, 11, 16
 NO_RESIDUAL = 0xFF          # txtp value: prediction only (no inv_txfm_add)
 
-PRED_NONE, PRED_INTER, PRED_INTER_AVG, PRED_INTRA = 0, 1, 2, 3
+PRED_NONE, PRED_INTER, PRED_INTER_AVG, PRED_INTRA, PRED_CFL = 0, 1, 2, 3, 4
 FILTER_2D_BILINEAR = 9
 
 (DC_PRED, VERT_PRED, HOR_PRED, LEFT_DC_PRED, TOP_DC_PRED, DC_128_PRED, Z1_PRED,
@@ -49,13 +49,16 @@ UNIT_DTYPE = np.dtype({
     "names": ["dst_off", "coef_off", "tx", "txtp", "plane", "pred", "nzw", "nzh",
               "bw4", "bh4",
               "src_off0", "src_off1", "mx0", "mx1", "my0", "my1", "filter2d", "ref0", "ref1",
-              "pad_inter", "edge_off", "angle", "mode", "pad_intra", "max_w", "max_h"],
+              "pad_inter", "edge_off", "angle", "mode", "pad_intra", "max_w", "max_h",
+              "cfl_alpha", "cfl_pad_wh", "cfl_luma_off"],
     "formats": ["<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
                 "<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
-                "<i4", "<u2", "u1", "u1", "<u2", "<u2"],
+                "<i4", "<u2", "u1", "u1", "<u2", "<u2",
+                "i1", "u1", "<i4"],
     "offsets": [0, 4, 8, 9, 10, 11, 12, 13, 14, 15,
                 16, 20, 24, 25, 26, 27, 28, 29, 30, 31,
-                16, 20, 22, 23, 24, 26],
+                16, 20, 22, 23, 24, 26,
+                20, 21, 28],
     "itemsize": 32,
 })
 
@@ -74,7 +77,9 @@ class FrameBatch(ctypes.Structure):
                 ("coef", ctypes.c_void_p),
                 ("edges", ctypes.c_void_p),
                 ("bitdepth_max", ctypes.c_int32),
-                ("zero_coefs", ctypes.c_int32)]
+                ("zero_coefs", ctypes.c_int32),
+                ("cfl_luma", Plane),
+                ("cfl_ss", ctypes.c_int32)]
 
 
 _LIB = None

@@ -37,6 +37,8 @@ class DeviceFrame:
                 src = a if fd.cfg.bpc == 8 else a.view(np.int16)
                 planes.append(torch.from_numpy(src.copy()).to(dev))
             self.refs.append(planes)
+        cl = fd.cfl_luma if fd.cfg.bpc == 8 else fd.cfl_luma.view(np.int16)
+        self.cfl_luma = torch.from_numpy(cl.copy()).to(dev)
         self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fd.plane_wh]
         self.zero_coefs = zero_coefs
         self.batch = self._make_batch()
@@ -65,6 +67,10 @@ class DeviceFrame:
         b.edges = self.edges.data_ptr()
         b.bitdepth_max = fd.cfg.bitdepth_max if fd.cfg.bpc == 16 else 255
         b.zero_coefs = 1 if self.zero_coefs else 0
+        b.cfl_luma.data = self.cfl_luma.data_ptr()
+        b.cfl_luma.stride = self.cfl_luma.shape[1] * bpp
+        b.cfl_luma.w, b.cfl_luma.h = fd.plane_wh[0]
+        b.cfl_ss = 3   # 4:2:0
         return b
 
     def launch(self, stream=None):

@@ -510,12 +510,19 @@ __device__ __forceinline__ void tx1d(int kind, int *c, Clip cl) {
     } else if (kind == K_IDENTITY) {
         if constexpr (N <= 32) identity<N, S>(c);
     } else {
-        if constexpr (N == 4) {
-            if (kind == K_ADST) adst4<S, false>(c); else adst4<S, true>(c);
-        } else if constexpr (N == 8) {
-            if (kind == K_ADST) adst8<S, false>(c, cl); else adst8<S, true>(c, cl);
-        } else if constexpr (N == 16) {
-            if (kind == K_ADST) adst16<S, false>(c, cl); else adst16<S, true>(c, cl);
+        // ADST and FLIPADST share one body (lanes of a wave may mix them);
+        // the flip is an in-register reversal by selects
+        if constexpr (N == 4) adst4<S, false>(c);
+        else if constexpr (N == 8) adst8<S, false>(c, cl);
+        else if constexpr (N == 16) adst16<S, false>(c, cl);
+        if constexpr (N <= 16) {
+            const bool f = kind == K_FLIPADST;
+#pragma unroll
+            for (int i = 0; i < N / 2; i++) {
+                const int lo = c[i * S], hi = c[(N - 1 - i) * S];
+                c[i * S] = f ? hi : lo;
+                c[(N - 1 - i) * S] = f ? lo : hi;
+            }
         }
     }
 }

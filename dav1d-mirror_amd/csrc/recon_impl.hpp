@@ -184,6 +184,9 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     a.units = b->units;
     a.coef = (C *)b->coef;
     a.edges = (const P *)b->edges;
+    a.cfl_luma = (const P *)b->cfl_luma.data;
+    a.cfl_luma_stride = (int)(b->cfl_luma.stride / B);
+    a.cfl_ss = b->cfl_ss;
     memcpy(a.class_start, b->class_start, sizeof(a.class_start));
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;

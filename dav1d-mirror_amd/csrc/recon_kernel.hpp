@@ -67,6 +67,9 @@ template <int BPC> struct ReconArgs {
     const Dav1dGpuUnit *units;
     C *coef;
     const P *edges;
+    const P *cfl_luma;    // luma read by CFL units
+    int cfl_luma_stride;  // pixels
+    int cfl_ss;           // ss_hor | ss_ver << 1
     int class_start[DGPU_N_RECT_TX_SIZES + 1];
     // wave schedule, ordered (segment, class position): every one of the
     // kSegments segments gives the class at position k (kOrder) wps[k]
@@ -189,6 +192,7 @@ typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x3a1 __attribute__((ext_vector_type(3), aligned(1)));
+typedef uint32_t u32x2a1 __attribute__((ext_vector_type(2), aligned(1)));
 typedef uint32_t u32x4a2 __attribute__((ext_vector_type(4), aligned(2)));
 typedef uint32_t u32x2a2 __attribute__((ext_vector_type(2), aligned(2)));
 
@@ -655,6 +659,88 @@ __device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, cons
     }
 }
 
+// ------------------------------------------------------------------ cfl ---
+
+// Chroma-from-luma for one unit (the whole chroma block, square <= 32):
+// cfl_ac on the co-located luma (src/ipred_tmpl.c:657-703), then cfl_pred
+// with the DC of the edge array (:71-84, :103-218), task by task through
+// `emit`.  The 4:2:0 no-padding case sums luma pairs with packed dots.
+template <int BPC, int TX, typename P, typename Emit>
+__device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGpuUnit &u, const P *tl, int16_t *fe,
+                                          int l, int bdmax, Emit &emit) {
+    using CL = Cls<TX>;
+    constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NT = CL::NT, TPL = CL::TPL;
+    const IntraState dcs = intra_prep<BPC, TX>(u, tl, fe, l, bdmax);   // DC family only reads tl
+    const int ssh = a.cfl_ss & 1, ssv = (a.cfl_ss >> 1) & 1;
+    const int wpad = u.p.cfl.pad_wh & 15, hpad = u.p.cfl.pad_wh >> 4;
+    const int vw = W - 4 * wpad, vh = H - 4 * hpad;
+    const int ys = a.cfl_luma_stride;
+    const P *yp = a.cfl_luma + u.p.cfl.luma_off;
+    const bool fast = ssh && ssv && !wpad && !hpad;
+    const int acsh = 1 + !ssv + !ssh;
+    int ac[TPL][8];
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < TPL; k++) {
+        const int t = l + k * G;
+        if (t >= NT) break;
+        const int j = t / QW, q = t % QW;
+        if (fast) {   // luma rows 4j..4j+3, columns 8q..8q+7
+#pragma unroll
+            for (int rr = 0; rr < 2; rr++) {
+                const P *r0 = yp + (4 * j + 2 * rr) * ys + 8 * q;
+                if constexpr (BPC == 8) {
+                    const u32x2 v0 = gld<u32x2a1>(r0), v1 = gld<u32x2a1>(r0 + ys);
+                    // byte pairs summed over both rows: dot4 with 1-masks
+                    ac[k][4 * rr + 0] = (int)__builtin_amdgcn_udot4(v1.x, 0x00000101u, __builtin_amdgcn_udot4(v0.x, 0x00000101u, 0, false), false) << 1;
+                    ac[k][4 * rr + 1] = (int)__builtin_amdgcn_udot4(v1.x, 0x01010000u, __builtin_amdgcn_udot4(v0.x, 0x01010000u, 0, false), false) << 1;
+                    ac[k][4 * rr + 2] = (int)__builtin_amdgcn_udot4(v1.y, 0x00000101u, __builtin_amdgcn_udot4(v0.y, 0x00000101u, 0, false), false) << 1;
+                    ac[k][4 * rr + 3] = (int)__builtin_amdgcn_udot4(v1.y, 0x01010000u, __builtin_amdgcn_udot4(v0.y, 0x01010000u, 0, false), false) << 1;
+                } else {
+                    const u32x4a2 v0 = gld<u32x4a2>(r0), v1 = gld<u32x4a2>(r0 + ys);
+                    const uint32_t d0[4] = {v0.x, v0.y, v0.z, v0.w}, d1[4] = {v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        ac[k][4 * rr + i] = (int)((d0[i] & 0xffff) + (d0[i] >> 16) + (d1[i] & 0xffff) + (d1[i] >> 16)) << 1;
+                }
+            }
+        } else {   // general: clamp to the visible part, any subsampling
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int sx = min(4 * q + (i & 3), vw - 1), sy = min(2 * j + (i >> 2), vh - 1);
+                const P *p = yp + (sy << ssv) * ys + (sx << ssh);
+                int v = gld<P>(p);
+                if (ssh) v += gld<P>(p + 1);
+                if (ssv) {
+                    v += gld<P>(p + ys);
+                    if (ssh) v += gld<P>(p + ys + 1);
+                }
+                ac[k][i] = v << acsh;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) sum += ac[k][i];
+    }
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) sum += __shfl_xor(sum, off, 64);
+    constexpr int LG = __builtin_ctz(W) + __builtin_ctz(H);
+    const int avg = (sum + ((1 << LG) >> 1)) >> LG;
+    const int alpha = u.p.cfl.alpha;
+#pragma unroll
+    for (int k = 0; k < TPL; k++) {
+        const int t = l + k * G;
+        if (t >= NT) break;
+        int pv[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int d = alpha * (int)(int16_t)(ac[k][i] - avg);   // ac is int16 in the reference
+            const int mag = (abs(d) + 32) >> 6;
+            pv[i] = clampi(dcs.dc + (d < 0 ? -mag : mag), 0, bdmax);
+        }
+        emit(t / QW, t % QW, pv);
+    }
+}
+
 // ---------------------------------------------------------------- kernel --
 
 template <int BPC, int TX>
@@ -714,7 +800,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     Stage<CL::SW * CL::SH * (int)sizeof(C), G> cst;
     if (ncoef) cst.load(cf, ncoef * (int)sizeof(C), l);
     Stage<SL::EDGE * (int)sizeof(P), G> est;
-    if (pred == DGPU_PRED_INTRA) est.load(a.edges + u.p.intra.edge_off - 2 * H, SL::EDGE * (int)sizeof(P), l);
+    const bool edged = pred == DGPU_PRED_INTRA || pred == DGPU_PRED_CFL;   // same edge_off in both views
+    if (edged) est.load(a.edges + u.p.intra.edge_off - 2 * H, SL::EDGE * (int)sizeof(P), l);
 
     const int f2d = inter ? u.p.inter.filter2d : 0;
     const bool bil = f2d == DGPU_FILTER_2D_BILINEAR;
@@ -748,7 +835,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     int cfsk = 0;
     if (ncoef) cfsk = cst.commit(cfl, l);
     const P *tl = nullptr;
-    if (pred == DGPU_PRED_INTRA) tl = reinterpret_cast<const P *>(src + est.commit(src, l)) + 2 * H;
+    if (edged) tl = reinterpret_cast<const P *>(src + est.commit(src, l)) + 2 * H;
     mark(2);
 
     // ---------------- P2: mc horizontal pass(es) ----------------
@@ -981,6 +1068,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             }
             emit(j, q, pv);
         }
+    } else if (pred == DGPU_PRED_CFL) {
+        if constexpr (W == H && W <= 32) cfl_units<BPC, TX>(a, u, tl, fe, l, bdmax, emit);
     } else {   // PRED_NONE: the residual goes onto the picture
 #pragma unroll
         for (int k = 0; k < TPL; k++) {

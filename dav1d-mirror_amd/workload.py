@@ -18,6 +18,7 @@ config 2: inter only, prediction-only units (one per block, no residual).
 
 Everything here is host-side numpy; nothing is timed.
 """
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -31,6 +32,9 @@ Z_ANGLES = np.array([3, 6, 9, 14, 17, 20, 23, 26, 29, 32, 36, 39, 42, 45, 48, 51
 _LEVELS = [(64, 0.15), (32, 0.25 / 0.85), (16, 0.35 / 0.60), (8, 1.0)]
 
 REF_PAD = 96   # reference planes carry this many padding pixels on every side
+
+# picture bands of the unit sort (see make_frame); DAV1D_GPU_SORT_BANDS overrides (tuning)
+SORT_BANDS = int(os.environ.get("DAV1D_GPU_SORT_BANDS", "16"))
 
 _SCALE = [4.0, 4.0 * 2 ** -0.5, 2.0, 2.0 * 2 ** -0.5, 1.0, 0.5 * 2 ** -0.5, 0.25,
           0.125 * 2 ** -0.5, 0.0625]
@@ -47,6 +51,7 @@ class FrameConfig:
     compound_frac: float = 0.50   # of inter blocks
     seed: int = 0x5EED0001
     tx64: bool = False            # allow 64-point transforms (64x64 luma blocks)
+    cfl_frac: float = 0.50        # of intra blocks: chroma predicted with CfL (config 3)
 
     @property
     def pixel_dtype(self):
@@ -67,6 +72,7 @@ class FrameData:
     refs: list                    # [ref][plane] padded 2-D arrays
     plane_wh: list                # [(w, h)] per plane
     blk: np.ndarray = None        # prediction-block id of each unit (stats only)
+    cfl_luma: np.ndarray = None   # luma plane CFL units read (synthetic "reconstructed" luma)
     stats: dict = field(default_factory=dict)
 
     @property
@@ -170,6 +176,11 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     fidx = rng.integers(0, 5, nb)
     z2mw = rng.integers(1, 65, nb)
     z2mh = rng.integers(1, 65, nb)
+    # CfL (own stream): chroma of these intra blocks is one CFL unit per block
+    crng = np.random.default_rng(cfg.seed ^ 0xCF1C)
+    cfl_blk = (kind == abi.PRED_INTRA) & (crng.random(nb) < (cfg.cfl_frac if cfg.kind != "mc" else 0.0))
+    cfl_alpha = crng.integers(1, 17, size=(nb, 2)) * np.where(crng.random((nb, 2)) < 0.5, -1, 1)
+    cfl_dc = np.array([abi.DC_PRED, abi.LEFT_DC_PRED, abi.TOP_DC_PRED, abi.DC_128_PRED])[crng.integers(0, 4, nb)]
 
     rows = []   # per-unit python tuples assembled below (vectorised per block)
     unit_fields = {k: [] for k in ("plane", "x", "y", "tw", "th", "blk", "bs")}
@@ -183,6 +194,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
             else:
                 cands = _tx_candidates(s, cfg.tx64)
                 tw, th = cands[(b * 7 + plane * 3 + int(rng.integers(0, 1 << 20))) % len(cands)]
+                if plane > 0 and cfl_blk[b]:
+                    tw = th = s   # CfL predicts the whole chroma block (<= 32x32)
             for oy in range(0, s, th):
                 for ox in range(0, s, tw):
                     unit_fields["plane"].append(plane)
@@ -208,13 +221,15 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     units["dst_off"] = uy * pw[plane_u] + ux
     units["tx"] = tx
     units["plane"] = plane_u
-    pk = kind[blk]
+    pk = kind[blk].copy()
+    cfl = (plane_u > 0) & cfl_blk[blk]
+    pk[cfl] = abi.PRED_CFL
     units["pred"] = pk
     units["bw4"] = bsz // 4
     units["bh4"] = bsz // 4
 
     # inter parameters
-    inter = pk != abi.PRED_INTRA
+    inter = (pk == abi.PRED_INTER) | (pk == abi.PRED_INTER_AVG)
     ref_stride = np.array([refs[0][p].shape[1] for p in range(3)])
     for k in range(2):
         mvx = mv[blk, k, 0]
@@ -231,14 +246,14 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     units["filter2d"] = np.where(inter, filt[blk], 0)
 
     # intra parameters
-    intra = ~inter
+    intra = pk == abi.PRED_INTRA
     m = mode[blk]
     ang = np.where((m >= abi.Z1_PRED) & (m <= abi.Z3_PRED),
                    (90 * (m - abi.Z1_PRED) + zang[blk]) | zflags[blk],
                    np.where(m == abi.FILTER_PRED, fidx[blk], 0))
     # the intra fields share bytes with the inter ones (a C union): write
     # them only where the unit is intra
-    edge_len = np.where(intra, 2 * th + 2 * tw + 1, 0)
+    edge_len = np.where(intra | cfl, 2 * th + 2 * tw + 1, 0)
     edge_start = np.concatenate([[0], np.cumsum(edge_len)[:-1]])
     iu = units[intra]
     iu["src_off1"] = 0
@@ -252,6 +267,24 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     iu["max_w"] = np.where(z2, z2mw[blk][intra], 0)
     iu["max_h"] = np.where(z2, z2mh[blk][intra], 0)
     units[intra] = iu
+    # CfL parameters (union view "cfl"): DC source, alpha per chroma plane,
+    # co-located luma offset in the cfl_luma plane (4:2:0, no edge padding)
+    cu = units[cfl]
+    cu["src_off1"] = 0
+    cu["filter2d"] = 0
+    cu["ref0"] = 0
+    cu["ref1"] = 0
+    cu["max_w"] = 0
+    cu["max_h"] = 0
+    cu["edge_off"] = (edge_start + 2 * th)[cfl]
+    cu["mode"] = cfl_dc[blk][cfl]
+    cu["cfl_alpha"] = cfl_alpha[blk[cfl], plane_u[cfl] - 1]
+    cu["cfl_pad_wh"] = 0
+    luma_stride = (W + 63) // 64 * 64
+    cu["cfl_luma_off"] = (2 * uy[cfl]) * luma_stride + 2 * ux[cfl]
+    units[cfl] = cu
+    cfl_luma = crng.integers(0, bdmax + 1, size=(H, luma_stride), dtype=cfg.pixel_dtype)
+    m = np.where(cfl, cfl_dc[blk], m)
     sort_minor = np.where(inter, filt[blk], 16 + m)
     edges = rng.integers(0, bdmax + 1, size=max(int(edge_len.sum()), 1), dtype=cfg.pixel_dtype)
 
@@ -309,7 +342,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     # transform type, so the per-unit branches (1-D transform kind, intra
     # mode) do not diverge.  Order inside a class is free for correctness.
     ph = np.array([planes[p][1] for p in range(3)])
-    band = (uy * 16) // ph[plane_u]
+    band = (uy * SORT_BANDS) // ph[plane_u]
     tt = units["txtp"].astype(np.int64)
     minor = np.where(inter, tt * 16 + sort_minor, sort_minor * 256 + tt)
     order = np.lexsort((minor, units["pred"], band, units["tx"]))
@@ -318,7 +351,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
 
     fd = FrameData(cfg=cfg, units=units, class_start=class_start, coefs=coefs, edges=edges,
-                   refs=refs, plane_wh=planes, blk=(blk * 3 + plane_u)[order])
+                   refs=refs, plane_wh=planes, blk=(blk * 3 + plane_u)[order], cfl_luma=cfl_luma)
     fd.stats = algorithmic_bytes(fd)
     return fd
 
@@ -348,7 +381,9 @@ def algorithmic_bytes(fd: FrameData):
         fv = np.where(my > 0, np.where(bh > 4, 7, 3), 0)
         src[first] += np.where(use, (bw + fh) * (bh + fv), 0)[first]
     intra = u["pred"] == abi.PRED_INTRA
-    edge = np.where(intra, 2 * w + 2 * h + 1, 0)
+    cfl = u["pred"] == abi.PRED_CFL
+    edge = np.where(intra | cfl, 2 * w + 2 * h + 1, 0)
+    src = src + np.where(cfl, 4 * w * h, 0)   # co-located 4:2:0 luma the cfl_ac reads
     ncoef = np.where(u["txtp"] == abi.NO_RESIDUAL, 0, np.where(u["nzw"] == 0, 1,
                      u["nzw"].astype(np.int64) * u["nzh"]))
     out_px = int((w * h).sum())
@@ -363,5 +398,6 @@ def algorithmic_bytes(fd: FrameData):
         "total_bytes": int(src.sum()) * bpp + int(edge.sum()) * bpp + int(ncoef.sum()) * cb
                        + out_px * bpp + int(len(u)) * 32,
         "n_intra": int(intra.sum()),
-        "n_inter": int((~intra).sum()),
+        "n_cfl": int(cfl.sum()),
+        "n_inter": int((~intra & ~cfl).sum()),
     }

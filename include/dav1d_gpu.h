@@ -203,6 +203,10 @@ enum Dav1dGpuPredKind {
     DGPU_PRED_INTER = 1,     /* mc put from ref0                             */
     DGPU_PRED_INTER_AVG = 2, /* mct(ref0) + mct(ref1) -> avg                 */
     DGPU_PRED_INTRA = 3,     /* intra_pred from the unit's edge array        */
+    DGPU_PRED_CFL = 4,       /* chroma-from-luma: cfl_ac on the co-located
+                                luma (batch cfl_luma plane) + cfl_pred with
+                                the DC of the unit's edge array
+                                (src/recon_tmpl.c:1380-1420)                 */
 };
 
 /* txtp value of a prediction-only unit (no inv_txfm_add): mc-only batches */
@@ -244,6 +248,17 @@ typedef struct Dav1dGpuUnit {
             uint8_t  pad_;
             uint16_t max_w, max_h;   /* Z2 edge-filter limits                */
         } intra;
+        struct {          /* CFL: the unit is the whole chroma block (<= 32x32) */
+            int32_t  edge_off;       /* topleft[0] in the edge pool (DC)     */
+            int8_t   alpha;          /* cfl_alpha[plane], -16..16            */
+            uint8_t  pad_wh;         /* w_pad | h_pad << 4 (4-px units)      */
+            uint8_t  mode;           /* DC source: DC / LEFT_DC / TOP_DC /
+                                        DC_128 (Dav1dGpuIntraMode)           */
+            uint8_t  pad_;
+            int32_t  reserved_;
+            int32_t  luma_off;       /* pixel offset of the co-located luma
+                                        top-left in cfl_luma                  */
+        } cfl;
     } p;
 } Dav1dGpuUnit;
 
@@ -268,6 +283,11 @@ typedef struct Dav1dGpuFrameBatch {
     int32_t  zero_coefs;  /* 1: honour the coefficient-zeroing contract on
                              device (src/itx_tmpl.c:55/89): consumed
                              coefficients are written back as zeros          */
+    Dav1dGpuPlane cfl_luma; /* luma that CFL units read (the reconstructed
+                             luma of the same blocks); must not be a plane
+                             this batch writes: units run unordered          */
+    int32_t  cfl_ss;      /* chroma subsampling of CFL units: ss_hor |
+                             ss_ver << 1 (3 = 4:2:0, 1 = 4:2:2, 0 = 4:4:4)  */
 } Dav1dGpuFrameBatch;
 
 /* Launch one frame batch on `stream` (a hipStream_t, NULL = default).

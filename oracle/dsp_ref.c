@@ -1454,6 +1454,18 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
                 }
             }
             if (comp) avg_blend(dst, ds, t1, t2, w, h, 0, 0, NULL, bdmax);
+        } else if (u->pred == DGPU_PRED_CFL) {
+            /* recon_b_intra's CfL: cfl_ac on the co-located luma, then
+             * cfl_pred with the DC of the edge array (src/recon_tmpl.c:1380-1420) */
+            const pixel *tl = edges + u->p.cfl.edge_off;
+            const pixel *ypx = (const pixel *)b->cfl_luma.data + u->p.cfl.luma_off;
+            const int ssh = b->cfl_ss & 1, ssv = (b->cfl_ss >> 1) & 1;
+            cfl_ac(t1, ypx, b->cfl_luma.stride, u->p.cfl.pad_wh & 15, u->p.cfl.pad_wh >> 4, w, h, ssh, ssv);
+            ipc.cfl_pred[u->p.cfl.mode](dst, ds, tl, w, h, t1, u->p.cfl.alpha
+#if BITDEPTH == 16
+                                        , bdmax
+#endif
+                                        );
         } else if (u->pred == DGPU_PRED_INTRA) {
             const pixel *tl = edges + u->p.intra.edge_off;
             ipc.intra_pred[u->p.intra.mode](dst, ds, tl, w, h, u->p.intra.angle,

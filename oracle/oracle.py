@@ -71,6 +71,11 @@ class HostFrame:
         b.edges = self.edges.ctypes.data
         b.bitdepth_max = fd.cfg.bitdepth_max if fd.cfg.bpc == 16 else 255
         b.zero_coefs = 0
+        self.cfl_luma = np.ascontiguousarray(fd.cfl_luma)
+        b.cfl_luma.data = self.cfl_luma.ctypes.data
+        b.cfl_luma.stride = self.cfl_luma.shape[1] * bpp
+        b.cfl_luma.w, b.cfl_luma.h = fd.plane_wh[0]
+        b.cfl_ss = 3
         self.batch = b
 
     def run(self, u0=0, u1=None, threads=1):

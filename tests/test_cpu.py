@@ -156,6 +156,41 @@ def test_workload_types_valid(pkg):
     u = fd.units
     for tx, tp in zip(u["tx"], u["txtp"]):
         assert pkg.abi.itx_supported(int(tx), int(tp))
-    inter = u["pred"] != pkg.abi.PRED_INTRA
+    abi = pkg.abi
+    inter = (u["pred"] == abi.PRED_INTER) | (u["pred"] == abi.PRED_INTER_AVG)
+    intra = u["pred"] == abi.PRED_INTRA
+    cfl = u["pred"] == abi.PRED_CFL
     assert (u["filter2d"][inter] < 9).all()
-    assert ((u["mode"][~inter]) < 14).all()
+    assert (u["mode"][intra] < 14).all()
+    # CfL: chroma only, whole square block <= 32, DC-family source, |alpha| 1..16
+    assert cfl.any() and (u["plane"][cfl] > 0).all()
+    assert np.isin(u["tx"][cfl], [0, 1, 2, 3]).all()
+    assert np.isin(u["mode"][cfl], [abi.DC_PRED, abi.LEFT_DC_PRED, abi.TOP_DC_PRED, abi.DC_128_PRED]).all()
+    al = np.abs(u["cfl_alpha"][cfl].astype(int))
+    assert ((al >= 1) & (al <= 16)).all()
+
+
+def test_oracle_cfl_flat_luma_is_dc(pkg, oracle):
+    """cfl_ac of a flat luma block is all zero (mean removed), so CfL must
+    reproduce the DC-family prediction of the same edges
+    (src/ipred_tmpl.c:71-84, :657-703)."""
+    import dav1d_mirror_amd.workload as wl
+    abi = pkg.abi
+    fd = wl.make_frame(wl.FrameConfig(width=256, height=128, seed=21))
+    fd.cfl_luma[:] = 77
+    a = oracle.HostFrame(fd)
+    a.run()
+    cfl = fd.units["pred"] == abi.PRED_CFL
+    assert cfl.any()
+    u2 = fd.units.copy()
+    v = u2[cfl]
+    v["pred"] = abi.PRED_INTRA
+    v["angle"] = 0        # overwrites alpha / pad_wh (the union's intra view)
+    v["max_w"] = 0
+    v["max_h"] = 0
+    u2[cfl] = v
+    fd.units = u2
+    b = oracle.HostFrame(fd)
+    b.run()
+    for p in range(3):
+        assert np.array_equal(a.dst[p], b.dst[p])

@@ -51,6 +51,22 @@ def test_batch_tx64(pkg, oracle, seed, bpc, bdmax):
     _check(fd, oracle)
 
 
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+def test_batch_cfl_padded(pkg, oracle, bpc, bdmax):
+    """CfL units whose luma is partly outside the picture (cfl_ac w_pad /
+    h_pad > 0: the general, clamped path of the kernel)."""
+    fd = _frame(pkg, width=512, height=256, bpc=bpc, bitdepth_max=bdmax, seed=12)
+    u = fd.units.copy()
+    cfl = np.nonzero(u["pred"] == pkg.abi.PRED_CFL)[0]
+    assert len(cfl)
+    rng = np.random.default_rng(5)
+    for i in cfl:
+        w = pkg.abi.TX_WH[int(u["tx"][i])][0]
+        u["cfl_pad_wh"][i] = int(rng.integers(0, w // 4)) | int(rng.integers(0, w // 4)) << 4
+    fd.units = u
+    _check(fd, oracle)
+
+
 def test_batch_4k_full_bitexact(pkg, oracle):
     """BASELINE config 3 at its full size (12.44 Mpx, ~290k units)."""
     _check(_frame(pkg), oracle, threads=8)

@@ -24,6 +24,7 @@ CASES = [
     ("mc8", dict(width=256, height=128, kind="mc", seed=3)),
     ("full10", dict(width=128, height=64, bpc=16, bitdepth_max=1023, seed=4)),
     ("full12", dict(width=128, height=64, bpc=16, bitdepth_max=4095, seed=5)),
+    ("full8_tx64", dict(width=256, height=128, seed=6, tx64=True)),
 ]
 
 
