@@ -104,14 +104,20 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     const int gw = lb * waves_per_block<BPC, GRP>() + wave;
     if (gw >= a.nwaves) return;
     // (segment, class) of this wave from the per-segment wave prefix
-    const int wseg = a.wpre[NC];
-    const int s = gw / wseg, r = gw - s * wseg;
-    int pos = 0;   // schedule position inside the segment (kOrder)
+    // schedule: (segment group, class position, segment in group); a group
+    // of kSegInner segments runs its classes largest first as a whole
+    constexpr int SL = kSegInner;
+    const int wgrp = a.wpre[NC] * SL;
+    const int sg = gw / wgrp, r = gw - sg * wgrp;
+    int pos = 0;   // schedule position inside the group (kOrder)
 #pragma unroll
-    for (int c = 1; c < NC; c++) pos += r >= a.wpre[c];
+    for (int c = 1; c < NC; c++) pos += r >= a.wpre[c] * SL;
     const int cls = order_class(pos);
     const int U = 64 >> (int)((kLog2Lanes >> (3 * cls)) & 7);   // no table load
-    const int first = a.class_start[cls] + (s * a.wps[pos] + r - a.wpre[pos]) * U;
+    const int r2 = r - a.wpre[pos] * SL, wp = a.wps[pos];
+    const int sl = SL == 1 ? 0 : r2 / wp;
+    const int s = sg * SL + sl;
+    const int first = a.class_start[cls] + (s * wp + r2 - sl * wp) * U;
     const int count = min(U, a.class_start[cls + 1] - first);
     if (count <= 0) return;
     if constexpr (DGPU_TRACE) {   // kernel-entry time of this wave

@@ -43,6 +43,9 @@
 #ifndef DGPU_ABL_INTRA
 #define DGPU_ABL_INTRA 0   // skip intra edge preparation and prediction
 #endif
+#ifndef DGPU_EARLY_REF1
+#define DGPU_EARLY_REF1 0  // issue the second ref's footprint loads up front
+#endif
 #ifndef DGPU_TRACE
 #define DGPU_TRACE 0       // per-wave phase timestamps (tools/wave_trace.py)
 #endif
@@ -55,7 +58,11 @@ namespace dgpu {
 #ifndef DGPU_SEQREF_MAX_TPL
 #define DGPU_SEQREF_MAX_TPL 2
 #endif
+#ifndef DGPU_SEG_INNER
+#define DGPU_SEG_INNER 1
+#endif
 constexpr int kSegments = DGPU_SEGMENTS;   // spatial segments per class (task ordering)
+constexpr int kSegInner = DGPU_SEG_INNER;  // segments whose classes are scheduled as one group
 
 template <int BPC> struct ReconArgs {
     using P = typename Px<BPC>::pixel;
@@ -205,6 +212,65 @@ __device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
 __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
 }
+// Dot-product blocks in inline assembly, four independent chains per
+// block.  The compiler's own selection always starts a chain with a copy
+// of the start value into the accumulator (two-operand v_dot*c forms); the
+// three-operand forms here take it as an inline constant or SGPR.  The
+// compiler cannot see a hazard inside asm, so each block keeps it itself:
+// a DOT result is read by another VALU op only >= 3 instructions later
+// (gfx950 DOT-write -> VALU-read wait states); chains are interleaved and
+// every block ends in plain VALU ops.
+//
+// m[i] = (dot4(hi[i], ty, dot4(lo[i], tx, 2))) >> 2
+__device__ __forceinline__ void hdot4x4(const uint32_t *lo, const uint32_t *hi, uint32_t tx, uint32_t ty, int *m) {
+    asm("v_dot4_i32_i8 %0, %4, %12, 2\n\t"
+        "v_dot4_i32_i8 %1, %5, %12, 2\n\t"
+        "v_dot4_i32_i8 %2, %6, %12, 2\n\t"
+        "v_dot4_i32_i8 %3, %7, %12, 2\n\t"
+        "v_dot4_i32_i8 %0, %8, %13, %0\n\t"
+        "v_dot4_i32_i8 %1, %9, %13, %1\n\t"
+        "v_dot4_i32_i8 %2, %10, %13, %2\n\t"
+        "v_dot4_i32_i8 %3, %11, %13, %3\n\t"
+        "v_ashrrev_i32 %0, 2, %0\n\t"
+        "v_ashrrev_i32 %1, 2, %1\n\t"
+        "v_ashrrev_i32 %2, 2, %2\n\t"
+        "v_ashrrev_i32 %3, 2, %3"
+        : "=&v"(m[0]), "=&v"(m[1]), "=&v"(m[2]), "=&v"(m[3])
+        : "v"(lo[0]), "v"(lo[1]), "v"(lo[2]), "v"(lo[3]), "v"(hi[0]), "v"(hi[1]), "v"(hi[2]), "v"(hi[3]),
+          "v"(tx), "v"(ty));
+}
+// t[i] = (sum_k dot2(a[k][i], tap pair k) + kk) >> sh, k = 0..3
+__device__ __forceinline__ void vdot4x4(const uint32_t (*a)[4], const uint4 &tv, int kk, int sh, int *t) {
+    asm("v_dot2_i32_i16 %0, %4, %20, 0\n\t"
+        "v_dot2_i32_i16 %1, %5, %20, 0\n\t"
+        "v_dot2_i32_i16 %2, %6, %20, 0\n\t"
+        "v_dot2_i32_i16 %3, %7, %20, 0\n\t"
+        "v_dot2_i32_i16 %0, %8, %21, %0\n\t"
+        "v_dot2_i32_i16 %1, %9, %21, %1\n\t"
+        "v_dot2_i32_i16 %2, %10, %21, %2\n\t"
+        "v_dot2_i32_i16 %3, %11, %21, %3\n\t"
+        "v_dot2_i32_i16 %0, %12, %22, %0\n\t"
+        "v_dot2_i32_i16 %1, %13, %22, %1\n\t"
+        "v_dot2_i32_i16 %2, %14, %22, %2\n\t"
+        "v_dot2_i32_i16 %3, %15, %22, %3\n\t"
+        "v_dot2_i32_i16 %0, %16, %23, %0\n\t"
+        "v_dot2_i32_i16 %1, %17, %23, %1\n\t"
+        "v_dot2_i32_i16 %2, %18, %23, %2\n\t"
+        "v_dot2_i32_i16 %3, %19, %23, %3\n\t"
+        "v_add_u32 %0, %24, %0\n\t"
+        "v_add_u32 %1, %24, %1\n\t"
+        "v_add_u32 %2, %24, %2\n\t"
+        "v_add_u32 %3, %24, %3\n\t"
+        "v_ashrrev_i32 %0, %25, %0\n\t"
+        "v_ashrrev_i32 %1, %25, %1\n\t"
+        "v_ashrrev_i32 %2, %25, %2\n\t"
+        "v_ashrrev_i32 %3, %25, %3"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
+        : "v"(a[0][0]), "v"(a[0][1]), "v"(a[0][2]), "v"(a[0][3]), "v"(a[1][0]), "v"(a[1][1]), "v"(a[1][2]),
+          "v"(a[1][3]), "v"(a[2][0]), "v"(a[2][1]), "v"(a[2][2]), "v"(a[2][3]), "v"(a[3][0]), "v"(a[3][1]),
+          "v"(a[3][2]), "v"(a[3][3]), "v"(tv.x), "v"(tv.y), "v"(tv.z), "v"(tv.w), "s"(kk), "s"(sh));
+}
+
 // Global-memory access through pointers that came from LDS (the plane
 // table): tell the compiler the address space so it emits global_*
 // instead of flat_* instructions.
@@ -602,10 +668,9 @@ template <int BPC, int TX> struct HPass {
                         const uint32_t w0 = ra[c][rr].x ^ 0x80808080u;
                         const uint32_t w1 = ra[c][rr].y ^ 0x80808080u;
                         const uint32_t w2 = ra[c][rr].z ^ 0x80808080u;
-                        mm[rr][0] = dot4(w1, th.y, dot4(w0, th.x, 2)) >> 2;
-                        mm[rr][1] = dot4(alb(w2, w1, 1), th.y, dot4(alb(w1, w0, 1), th.x, 2)) >> 2;
-                        mm[rr][2] = dot4(alb(w2, w1, 2), th.y, dot4(alb(w1, w0, 2), th.x, 2)) >> 2;
-                        mm[rr][3] = dot4(alb(w2, w1, 3), th.y, dot4(alb(w1, w0, 3), th.x, 2)) >> 2;
+                        const uint32_t lo[4] = {w0, alb(w1, w0, 1), alb(w1, w0, 2), alb(w1, w0, 3)};
+                        const uint32_t hi[4] = {w1, alb(w2, w1, 1), alb(w2, w1, 2), alb(w2, w1, 3)};
+                        hdot4x4(lo, hi, th.x, th.y, mm[rr]);
                     } else {
                         const int sh = 6 - ib, rnd = (1 << sh) >> 1;
                         // e: pixel pairs (2i, 2i+1), o: (2i+1, 2i+2)
@@ -638,25 +703,26 @@ template <int BPC, int TX> struct HPass {
     }
 };
 
-// Vertical pass of one reference for a 4x2 task: t[i] = the 8-tap sum over
-// stored intermediates, rows j*2 (i < 4) and j*2+1 (i >= 4), columns
-// 4q + (i & 3).  Add kMidBias<BPC> for the reference's sum.
+// Vertical pass of one reference for a 4x2 task: t[i] = (the 8-tap sum over
+// stored intermediates + kk) >> sh, rows j*2 (i < 4) and j*2+1 (i >= 4),
+// columns 4q + (i & 3).  kk includes kMidBias<BPC> (the reference's sum is
+// the stored one + kMidBias).
 template <int BPC> inline constexpr int kMidBias = BPC == 8 ? 64 * 2048 : 0;
 template <int W>
-__device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, const uint4 tv, int *t) {
+__device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, const uint4 tv, int kk, int sh, int *t) {
     uint32_t P[5][4];
 #pragma unroll
     for (int k = 0; k < 5; k++) {
         const uint4 v = *reinterpret_cast<const uint4 *>(mid + (j + k) * W + 4 * q);
         P[k][0] = v.x; P[k][1] = v.y; P[k][2] = v.z; P[k][3] = v.w;
     }
+    uint32_t O[4][4];   // odd rows: (row 2j+1+2k, row 2j+2+2k) pairs
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        t[i] = dot2(P[3][i], tv.w, dot2(P[2][i], tv.z, dot2(P[1][i], tv.y, dot2(P[0][i], tv.x, 0))));
-        t[4 + i] = dot2(alb(P[4][i], P[3][i], 2), tv.w,
-                        dot2(alb(P[3][i], P[2][i], 2), tv.z,
-                             dot2(alb(P[2][i], P[1][i], 2), tv.y, dot2(alb(P[1][i], P[0][i], 2), tv.x, 0))));
-    }
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) O[k][i] = alb(P[k + 1][i], P[k][i], 2);
+    vdot4x4(P, tv, kk, sh, t);
+    vdot4x4(O, tv, kk, sh, t + 4);
 }
 
 // ------------------------------------------------------------------ cfl ---
@@ -832,6 +898,14 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         hinit(hp0, 0);
         hp0.load(0);
     }
+    // DGPU_EARLY_REF1: the second ref's first load chunk goes out with the
+    // first's (held in registers until its h-pass after the first ref's
+    // vertical pass); otherwise it is issued when needed
+    HPass<BPC, TX> hp1;
+    if (DGPU_EARLY_REF1 && CL::SEQREF && do_mc && comp) {
+        hinit(hp1, 1);
+        hp1.load(0);
+    }
     int cfsk = 0;
     if (ncoef) cfsk = cst.commit(cfl, l);
     const P *tl = nullptr;
@@ -996,15 +1070,17 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                 for (int k = 0; k < TPL; k++) {
                     const int t = l + k * G;
                     if (t < NT) {
-                        int t0[8];
-                        mc_vtask<W>(mid0, t / QW, t % QW, tv0, t0);
-#pragma unroll
-                        for (int i = 0; i < 8; i++) q0[k][i] = (t0[i] + KP) >> 6;
+                        mc_vtask<W>(mid0, t / QW, t % QW, tv0, KP, 6, q0[k]);
                     }
                 }
                 wave_sync();
                 mark(6);
-                hpass(1);
+                if (DGPU_EARLY_REF1) {
+                    hp1.compute(0, ib);
+                    hp1.rest(ib);
+                } else {
+                    hpass(1);
+                }
                 wave_sync();
                 mark(7);
             }
@@ -1018,15 +1094,12 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #pragma unroll
                     for (int i = 0; i < 8; i++) p0[i] = q0[k][i];
                 } else {
-                    int t0[8];
-                    mc_vtask<W>(mid0, j, q, tv0, t0);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) p0[i] = (t0[i] + KP) >> 6;
+                    mc_vtask<W>(mid0, j, q, tv0, KP, 6, p0);
                 }
-                mc_vtask<W>(mid1, j, q, tv1, t1);
+                mc_vtask<W>(mid1, j, q, tv1, KP, 6, t1);
 #pragma unroll
                 for (int i = 0; i < 8; i++)
-                    pv[i] = clampi((p0[i] + ((t1[i] + KP) >> 6) + (1 << ib)) >> (ib + 1), 0, bdmax);
+                    pv[i] = clampi((p0[i] + t1[i] + (1 << ib)) >> (ib + 1), 0, bdmax);
                 emit(j, q, pv);
             }
         } else {   // put: rnd_sh(t, 6 + ib)
@@ -1037,9 +1110,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                 if (t >= NT) break;
                 const int j = t / QW, q = t % QW;
                 int t0[8], pv[8];
-                mc_vtask<W>(mid0, j, q, tv0, t0);
+                mc_vtask<W>(mid0, j, q, tv0, kp, sh, t0);
 #pragma unroll
-                for (int i = 0; i < 8; i++) pv[i] = clampi((t0[i] + kp) >> sh, 0, bdmax);
+                for (int i = 0; i < 8; i++) pv[i] = clampi(t0[i], 0, bdmax);
                 emit(j, q, pv);
             }
         }

@@ -27,6 +27,11 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         seg1) build seg1 -DDGPU_SEGMENTS=1 ;;
         trace) build trace -DDGPU_TRACE=1 ;;
         merge) build merge -DDGPU_MERGE_GROUPS=1 ;;
+        sl2) build sl2 -DDGPU_SEG_INNER=2 ;;
+        early1) build early1 -DDGPU_EARLY_REF1=1 ;;
+        early1w4) build early1w4 -DDGPU_EARLY_REF1=1 -DDGPU_WPE_SMALL8=4 ;;
+        sl4) build sl4 -DDGPU_SEG_INNER=4 ;;
+        sl2s32) build sl2s32 -DDGPU_SEG_INNER=2 -DDGPU_SEGMENTS=32 ;;
         merge5) build merge5 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=5 ;;
         merge4) build merge4 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=1 ;;
         merge6) build merge6 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=6 ;;
