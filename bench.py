@@ -8,10 +8,18 @@ kernel.  N GPUs = N independent frames, one per rank (frame sharding, no
 collective on the data path; weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4k|1080p-mc|4k-10bit]
+                    [--feed local|rccl] [--no-families] [--no-cpu]
+
+--feed rccl: rank 0 generates every rank's frame and scatters them over RCCL
+point-to-point before the timed region (config 5's coded-block feed over
+xGMI); the feed's time and bytes are reported on their own ("feed").
+At N=1 the line also carries a per-family breakdown ("families": mc-only,
+intra-only and itx-only 4K frames of the same bitdepth, one launch each).
 
 Rank 0 prints one JSON line.  See DESIGN.md for the roofline accounting.
 """
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -61,7 +69,9 @@ def cpu_baseline(fd, budget_s=12.0):
                       f"{el:.1f} s single-thread, oracle/dsp_ref.c -O2 (restatement of dav1d C, not dav1d)"}
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1", "v3i_pmc_summary.json")
+# rocprofv3 PMC summaries of the current kernels (tools/prof.sh + tools/pmc_summary.py)
+PMC_SUMMARY = {8: os.path.join(ROOT, "profiles", "r1", "r1b_pmc_summary.json"),
+               16: os.path.join(ROOT, "profiles", "r1", "r1b_10bit_pmc_summary.json")}
 
 
 def pmc_traffic(bpc):
@@ -69,8 +79,9 @@ def pmc_traffic(bpc):
     PMC summary (FETCH_SIZE and WRITE_SIZE, separate --pmc passes, KB as
     rocprofv3 reports them).  PMC needs rocprofv3 around the process, so a
     plain bench run cannot re-measure it; the source file is named."""
+    path = PMC_SUMMARY[bpc]
     try:
-        d = json.load(open(PMC_SUMMARY))
+        d = json.load(open(path))
     except (OSError, ValueError):
         return None, None
     tot = 0.0
@@ -79,9 +90,48 @@ def pmc_traffic(bpc):
             tot += (v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024
     if not tot:
         return None, None
-    return int(tot), (f"FETCH_SIZE+WRITE_SIZE per frame from {os.path.relpath(PMC_SUMMARY, ROOT)} "
+    return int(tot), (f"FETCH_SIZE+WRITE_SIZE per frame from {os.path.relpath(path, ROOT)} "
                       "(uncorrected: the gfx950 x2 FETCH factor holds for wide coalesced reads, "
                       "not these scattered row loads)")
+
+
+FAMILIES = {
+    # per-family frames ("also report per-family Gpix/s")
+    "mc": "inter only: mc put / mct x2 + avg per block, no residual",
+    "ipred": "intra only: the 14 intra_pred modes + CfL per transform block, no residual",
+    "itx": "inv_txfm_add only: residual 4x4..32x32 onto an existing picture (dst read + write)",
+}
+
+
+def kernel_seconds(frame, stream, n):
+    """Mean launch duration over n launches, HIP events on the launch stream."""
+    import torch
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in evs:
+        a.record(stream)
+        frame.launch(stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in evs])) * 1e-3
+
+
+def family_breakdown(base_cfg, dev, stream, steps):
+    import dav1d_mirror_amd.workload as wl
+    import dav1d_mirror_amd.batch as bt
+    out = {}
+    for kind, what in FAMILIES.items():
+        fd = wl.make_frame(dataclasses.replace(base_cfg, kind=kind))
+        frame = bt.DeviceFrame(fd, dev)
+        for _ in range(3):
+            frame.launch(stream)
+        ks = kernel_seconds(frame, stream, max(steps, 10))
+        out[kind] = {"workload": what, "units": fd.n_units, "pixels": fd.stats["pixels"],
+                     "kernel_us": round(ks * 1e6, 2), "gpix_s": round(fd.stats["pixels"] / ks / 1e9, 2),
+                     "algorithmic_bytes": fd.stats["total_bytes"],
+                     "achieved_gbs": round(fd.stats["total_bytes"] / ks / 1e9, 1),
+                     "frac": round(fd.stats["total_bytes"] / ks / 1e9 / HBM_PEAK_GBS, 4)}
+        del frame
+    return out
 
 
 def main():
@@ -92,6 +142,9 @@ def main():
     ap.add_argument("--config", default="4k", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--check", action="store_true", help="verify rank 0's frame against the oracle")
+    ap.add_argument("--feed", default="local", choices=["local", "rccl"],
+                    help="local: each rank generates its frame; rccl: rank 0 generates all and scatters")
+    ap.add_argument("--no-families", action="store_true", help="skip the per-family breakdown (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -112,9 +165,20 @@ def main():
 
     c = dict(CONFIGS[args.config])
     label = c.pop("label")
-    cfg = sh.rank_config(wl.FrameConfig(**c), rank)
+    base = wl.FrameConfig(**c)
+    cfg = sh.rank_config(base, rank)
     t0 = time.perf_counter()
-    fd = wl.make_frame(cfg)
+    feed = None
+    if args.feed == "rccl" and world > 1:
+        fd, feed_s, feed_bytes = sh.feed_frame(lambda r: sh.rank_config(base, r), rank, world, dist, dev)
+        feed_s = sh.max_over_ranks(feed_s, dist, dev)
+        feed_bytes = sh.sum_over_ranks(feed_bytes if rank else 0, dist, dev)
+        feed = {"kind": "rccl send/recv from rank 0 (scatter of independent frames)",
+                "bytes": feed_bytes, "ms": round(feed_s * 1e3, 3),
+                "gbs": round(feed_bytes / feed_s / 1e9, 2) if feed_s > 0 else None,
+                "note": "outside the timed region; kernel-phase scaling excludes it (SURVEY 8(e))"}
+    else:
+        fd = wl.make_frame(cfg)
     log(f"[rank {rank}] frame: {fd.n_units} units, {fd.stats['pixels']} px, "
         f"{fd.stats['total_bytes'] / 1e6:.1f} MB algorithmic, generated in {time.perf_counter() - t0:.1f}s")
     frame = bt.DeviceFrame(fd, dev)
@@ -139,15 +203,7 @@ def main():
     el = sh.max_over_ranks(time.perf_counter() - t0, dist, dev)
 
     # per-launch kernel duration with HIP events on the launch stream
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    for a, b in evs:
-        a.record(stream)
-        frame.launch(stream)
-        b.record(stream)
-    torch.cuda.synchronize(dev)
-    durs = np.array([a.elapsed_time(b) for a, b in evs]) * 1e-3   # s
-    kern_s = float(np.mean(durs))
+    kern_s = kernel_seconds(frame, stream, args.steps)
 
     check = None
     if args.check and rank == 0:
@@ -159,7 +215,7 @@ def main():
         log(f"[rank 0] bit-exact vs oracle: {check}")
 
     if rank == 0:
-        traffic, traffic_note = pmc_traffic(cfg.bpc) if args.config == "4k" else (None, None)
+        traffic, traffic_note = pmc_traffic(cfg.bpc) if args.config in ("4k", "4k-10bit") else (None, None)
         value = sh.aggregate_gpix_per_s(fd.stats["pixels"], args.steps, world, el)
         bytes_launch = fd.stats["total_bytes"]
         achieved = bytes_launch / kern_s / 1e9
@@ -204,6 +260,10 @@ def main():
         }
         if check is not None:
             out["config"]["bit_exact_vs_oracle"] = check
+        if feed is not None:
+            out["feed"] = feed
+        if not args.no_families and world == 1 and c.get("kind") == "full":
+            out["families"] = family_breakdown(cfg, dev, stream, args.steps)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
         print(json.dumps(out), flush=True)

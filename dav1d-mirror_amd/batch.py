@@ -39,7 +39,11 @@ class DeviceFrame:
             self.refs.append(planes)
         cl = fd.cfl_luma if fd.cfg.bpc == 8 else fd.cfl_luma.view(np.int16)
         self.cfl_luma = torch.from_numpy(cl.copy()).to(dev)
-        self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fd.plane_wh]
+        if fd.dst_init is not None:
+            self.dst = [torch.from_numpy((a if fd.cfg.bpc == 8 else a.view(np.int16)).copy()).to(dev)
+                        for a in fd.dst_init]
+        else:
+            self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fd.plane_wh]
         self.zero_coefs = zero_coefs
         self.batch = self._make_batch()
         self.lib = abi.load_lib()

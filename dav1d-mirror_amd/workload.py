@@ -46,7 +46,11 @@ class FrameConfig:
     height: int = 2160
     bpc: int = 8                  # 8 or 16 (ABI); 16 uses bitdepth_max
     bitdepth_max: int = 255
-    kind: str = "full"            # "full" (mc + ipred + itx) or "mc" (put/avg only)
+    # "full" (mc + ipred + itx, config 3), "mc" (put/avg only, one unit per
+    # block, config 2), or a per-family frame for the bench breakdown:
+    # "ipred" (every block intra / CfL, no residual) or "itx" (no prediction:
+    # inv_txfm_add onto the picture, the reference's dst read + write)
+    kind: str = "full"
     intra_frac: float = 0.30
     compound_frac: float = 0.50   # of inter blocks
     seed: int = 0x5EED0001
@@ -73,6 +77,7 @@ class FrameData:
     plane_wh: list                # [(w, h)] per plane
     blk: np.ndarray = None        # prediction-block id of each unit (stats only)
     cfl_luma: np.ndarray = None   # luma plane CFL units read (synthetic "reconstructed" luma)
+    dst_init: list = None         # starting picture planes ("itx" frames add onto them)
     stats: dict = field(default_factory=dict)
 
     @property
@@ -164,6 +169,9 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     r = rng.random(nb)
     if cfg.kind == "mc":
         kind = np.where(rng.random(nb) < cfg.compound_frac, abi.PRED_INTER_AVG, abi.PRED_INTER)
+    elif cfg.kind in ("ipred", "itx"):
+        rng.random(nb)   # keep the later draws aligned with "full"
+        kind = np.full(nb, abi.PRED_INTRA if cfg.kind == "ipred" else abi.PRED_NONE)
     else:
         kind = np.where(r < cfg.intra_frac, abi.PRED_INTRA,
                         np.where(rng.random(nb) < cfg.compound_frac, abi.PRED_INTER_AVG,
@@ -289,7 +297,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     edges = rng.integers(0, bdmax + 1, size=max(int(edge_len.sum()), 1), dtype=cfg.pixel_dtype)
 
     # transform types, coefficient regions and coefficients
-    if cfg.kind == "mc":
+    if cfg.kind in ("mc", "ipred"):
         units["txtp"] = abi.NO_RESIDUAL
         coefs = np.zeros(1, cfg.coef_dtype)
     else:
@@ -350,8 +358,13 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     counts = np.bincount(units["tx"], minlength=abi.N_TX)
     class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
 
+    dst_init = None
+    if cfg.kind == "itx":   # a picture for the residual to land on (own stream)
+        drng = np.random.default_rng(cfg.seed ^ 0x1D57)
+        dst_init = [drng.integers(0, bdmax + 1, size=(ph_, pw_), dtype=cfg.pixel_dtype) for (pw_, ph_) in planes]
     fd = FrameData(cfg=cfg, units=units, class_start=class_start, coefs=coefs, edges=edges,
-                   refs=refs, plane_wh=planes, blk=(blk * 3 + plane_u)[order], cfl_luma=cfl_luma)
+                   refs=refs, plane_wh=planes, blk=(blk * 3 + plane_u)[order], cfl_luma=cfl_luma,
+                   dst_init=dst_init)
     fd.stats = algorithmic_bytes(fd)
     return fd
 
@@ -382,22 +395,27 @@ def algorithmic_bytes(fd: FrameData):
         src[first] += np.where(use, (bw + fh) * (bh + fv), 0)[first]
     intra = u["pred"] == abi.PRED_INTRA
     cfl = u["pred"] == abi.PRED_CFL
+    nopred = u["pred"] == abi.PRED_NONE
     edge = np.where(intra | cfl, 2 * w + 2 * h + 1, 0)
     src = src + np.where(cfl, 4 * w * h, 0)   # co-located 4:2:0 luma the cfl_ac reads
     ncoef = np.where(u["txtp"] == abi.NO_RESIDUAL, 0, np.where(u["nzw"] == 0, 1,
                      u["nzw"].astype(np.int64) * u["nzh"]))
     out_px = int((w * h).sum())
+    # PRED_NONE: inv_txfm_add reads the picture it adds to (dst read + write)
+    dst_read = int((w * h)[nopred].sum()) * bpp
     return {
         "units": int(len(u)),
         "ref_bytes": int(src.sum()) * bpp,
         "edge_bytes": int(edge.sum()) * bpp,
         "coef_bytes": int(ncoef.sum()) * cb,
         "dst_bytes": out_px * bpp,
+        "dst_read_bytes": dst_read,
         "desc_bytes": int(len(u)) * 32,
         "pixels": out_px,
         "total_bytes": int(src.sum()) * bpp + int(edge.sum()) * bpp + int(ncoef.sum()) * cb
-                       + out_px * bpp + int(len(u)) * 32,
+                       + out_px * bpp + dst_read + int(len(u)) * 32,
         "n_intra": int(intra.sum()),
         "n_cfl": int(cfl.sum()),
-        "n_inter": int((~intra & ~cfl).sum()),
+        "n_inter": int((~intra & ~cfl & ~nopred).sum()),
+        "n_nopred": int(nopred.sum()),
     }

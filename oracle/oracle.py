@@ -46,7 +46,10 @@ class HostFrame:
         abi = _abi()
         self.fd = fd
         pdt = fd.cfg.pixel_dtype
-        self.dst = [np.zeros((h, w), pdt) for (w, h) in fd.plane_wh]
+        if getattr(fd, "dst_init", None) is not None:
+            self.dst = [a.copy() for a in fd.dst_init]
+        else:
+            self.dst = [np.zeros((h, w), pdt) for (w, h) in fd.plane_wh]
         self.units = np.ascontiguousarray(fd.units)
         self.coefs = fd.coefs.copy()
         self.edges = np.ascontiguousarray(fd.edges)

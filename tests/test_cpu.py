@@ -125,7 +125,7 @@ def test_itx_dc_only_shortcut_matches_full_path(oracle, pkg, bpc):
 
 def test_workload_covers_every_pixel_once(pkg):
     import dav1d_mirror_amd.workload as wl
-    for kind in ("full", "mc"):
+    for kind in ("full", "mc", "ipred", "itx"):
         fd = wl.make_frame(wl.FrameConfig(width=512, height=256, kind=kind, seed=3))
         u = fd.units
         assert np.array_equal(fd.class_start, np.concatenate(
@@ -140,6 +140,23 @@ def test_workload_covers_every_pixel_once(pkg):
                     y, x = divmod(int(off), w)
                     cover.reshape(h, w)[y:y + th, x:x + tw] += 1
             assert (cover == 1).all(), (kind, p)
+
+
+def test_workload_family_kinds(pkg, oracle):
+    """Bench breakdown frames: every unit of an "ipred" frame is intra / CfL
+    without residual, every unit of an "itx" frame is PRED_NONE with one,
+    and the oracle adds the residual onto the starting picture."""
+    import dav1d_mirror_amd.workload as wl
+    abi = pkg.abi
+    fi = wl.make_frame(wl.FrameConfig(width=256, height=128, kind="ipred", seed=8))
+    assert np.isin(fi.units["pred"], [abi.PRED_INTRA, abi.PRED_CFL]).all()
+    assert (fi.units["txtp"] == abi.NO_RESIDUAL).all()
+    fx = wl.make_frame(wl.FrameConfig(width=256, height=128, kind="itx", seed=8))
+    assert (fx.units["pred"] == abi.PRED_NONE).all() and (fx.units["txtp"] != abi.NO_RESIDUAL).all()
+    assert fx.stats["dst_read_bytes"] == fx.stats["dst_bytes"]
+    hf = oracle.HostFrame(fx)
+    hf.run()
+    assert any(not np.array_equal(hf.dst[p], fx.dst_init[p]) for p in range(3))
 
 
 def test_workload_deterministic(pkg):

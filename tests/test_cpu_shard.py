@@ -57,3 +57,43 @@ def test_two_rank_frame_sharding_gloo():
     assert res[0][2] != res[1][2]                   # different content
     assert all(abs(r[3] - 0.02) < 1e-12 for r in res)   # MAX over ranks
     assert all(r[4] == res[0][5] + res[1][5] for r in res)  # SUM of pixels
+
+
+def _feed_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import __graft_entry__ as ge
+    ge.load_package()
+    import dav1d_mirror_amd.workload as wl
+    import dav1d_mirror_amd.shard as sh
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    base = wl.FrameConfig(width=256, height=128, kind="itx" if world == 3 else "full")
+    fd, secs, nbytes = sh.feed_frame(lambda r: sh.rank_config(base, r), rank, world, dist, "cpu")
+    ref = wl.make_frame(sh.rank_config(base, rank))   # what this rank must have received
+    same = (fd.units.tobytes() == ref.units.tobytes() and np.array_equal(fd.class_start, ref.class_start)
+            and np.array_equal(fd.coefs, ref.coefs) and np.array_equal(fd.edges, ref.edges)
+            and np.array_equal(fd.cfl_luma, ref.cfl_luma)
+            and all(np.array_equal(fd.refs[k][p], ref.refs[k][p]) for k in range(2) for p in range(3))
+            and (ref.dst_init is None or all(np.array_equal(fd.dst_init[p], ref.dst_init[p]) for p in range(3)))
+            and fd.stats == ref.stats)
+    q.put((rank, same, nbytes))
+    dist.destroy_process_group()
+
+
+def test_rccl_feed_scatter_gloo():
+    """bench.py --feed rccl: rank 0 generates every frame and sends frame r
+    to rank r (send/recv, the same calls RCCL runs over xGMI); each rank
+    ends up with exactly the frame it would have generated itself."""
+    for world in (2, 3):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        ps = [ctx.Process(target=_feed_worker, args=(r, world, port, q)) for r in range(world)]
+        for p in ps:
+            p.start()
+        res = sorted(q.get(timeout=240) for _ in range(world))
+        for p in ps:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        assert all(r[1] for r in res), res
+        assert res[0][2] > 0 and all(r[2] > 0 for r in res[1:])

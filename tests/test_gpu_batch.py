@@ -115,3 +115,12 @@ def test_zero_coefs_contract(pkg, oracle):
 def test_smoke_entry():
     import __graft_entry__ as ge
     ge.smoke()
+
+
+@pytest.mark.parametrize("kind,bpc,bdmax", [("ipred", 8, 255), ("itx", 8, 255), ("ipred", 16, 1023),
+                                            ("itx", 16, 4095)])
+def test_batch_family(pkg, oracle, kind, bpc, bdmax):
+    """The per-family frames of the bench breakdown: intra/CfL prediction
+    only, and inv_txfm_add onto an existing picture (PRED_NONE: the
+    kernel's picture-read path)."""
+    _check(_frame(pkg, width=512, height=256, bpc=bpc, bitdepth_max=bdmax, kind=kind, seed=21), oracle)

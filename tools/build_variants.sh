@@ -9,11 +9,16 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include -Icsrc"
 mkdir -p build/var
 build() {
     local name=$1; shift
-    for s in runtime mc ipred itx recon8 recon16; do
+    # only the batch TUs differ; the per-call TUs come from the product build
+    for s in ${TUS:-recon8 recon16}; do
         $HIPCC $F "$@" -c csrc/$s.hip -o build/var/$name.$s.o &
     done
     wait
-    $HIPCC $F -shared -o libdav1d_gpu.$name.so build/var/$name.*.o
+    local objs=""
+    for s in runtime mc ipred itx recon8 recon16; do
+        if [ -f build/var/$name.$s.o ] && [[ " ${TUS:-recon8 recon16} " == *" $s "* ]]; then objs="$objs build/var/$name.$s.o"; else objs="$objs build/$s.o"; fi
+    done
+    $HIPCC $F -shared -o libdav1d_gpu.$name.so $objs
 }
 for v in ${VARIANTS:-nomc noitx nointra}; do
     case $v in
