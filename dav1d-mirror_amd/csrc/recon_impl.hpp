@@ -47,22 +47,34 @@ template <int... TX> constexpr uint64_t pack_log2_lanes(std::integer_sequence<in
 }
 constexpr uint64_t kLog2Lanes = pack_log2_lanes(std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 
-template <int BPC, int TX, int GRP>
-__device__ __forceinline__ void dispatch_one(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int cls, int first,
-                                             int count, uint8_t *lds, int gw) {
 #ifndef DGPU_ONLY_CLASS
 #define DGPU_ONLY_CLASS -1   // build-time probe: compile a single class (resource studies)
 #endif
-    if constexpr (class_group(TX) == GRP && (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS)) {
-        if (cls == TX) recon_units<BPC, TX>(a, pt, first, count, lds, gw, GRP);
-    }
+template <int BPC, int TX, int GRP>
+__device__ __forceinline__ void run_class(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
+                                          int first, int count, uint8_t *lds, int gw) {
+    if constexpr (TX < DGPU_N_RECT_TX_SIZES && class_group(TX) == GRP &&
+                  (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS))
+        recon_units<BPC, TX>(a, pt, u, first, count, lds, gw, GRP);
 }
 
-template <int BPC, int GRP, int... TX>
-__device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int cls, int first,
-                                         int count, uint8_t *lds, int gw, std::integer_sequence<int, TX...>) {
-    (dispatch_one<BPC, TX, GRP>(a, pt, cls, first, count, lds, gw), ...);
+// One switch (a compact compare tree) instead of a chain of class tests
+// spread between the inlined class bodies: the chain's targets were cold
+// instruction-cache lines on every wave's way to its class.
+template <int BPC, int GRP>
+__device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
+                                         int cls, int first, int count, uint8_t *lds, int gw) {
+#define DGPU_CASE(T) \
+    case T: run_class<BPC, T, GRP>(a, pt, u, first, count, lds, gw); break;
+    switch (cls) {
+        DGPU_CASE(0) DGPU_CASE(1) DGPU_CASE(2) DGPU_CASE(3) DGPU_CASE(4) DGPU_CASE(5) DGPU_CASE(6)
+        DGPU_CASE(7) DGPU_CASE(8) DGPU_CASE(9) DGPU_CASE(10) DGPU_CASE(11) DGPU_CASE(12) DGPU_CASE(13)
+        DGPU_CASE(14) DGPU_CASE(15) DGPU_CASE(16) DGPU_CASE(17) DGPU_CASE(18)
+        default: break;
+    }
+#undef DGPU_CASE
 }
+static_assert(DGPU_N_RECT_TX_SIZES == 19, "dispatch switch lists 19 classes");
 
 // Minimum waves per SIMD the register allocator must allow, per bitdepth
 // and group: 5 for the 8-bit main group (small + large classes) fits in 96
@@ -85,46 +97,99 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     // XCD-contiguous block order: hardware deals blocks round-robin over the
     // 8 XCDs, so logical block (b % 8) * (nb / 8) + b / 8 gives XCD x the
     // x-th contiguous eighth of the schedule (gridDim.x is a multiple of 8)
-    __shared__ PlaneTab<BPC> pt;
-    {
-        const int t = threadIdx.x;
-        if (t < DGPU_MAX_REFS * 3) {
-            pt.ref[t] = (&a.ref[0][0])[t];
-            pt.ref_stride[t] = (&a.ref_stride[0][0])[t];
-        }
-        if (t < 3) {
-            pt.dst[t] = a.dst[t];
-            pt.dst_stride[t] = a.dst_stride[t];
-        }
-        __syncthreads();
-    }
+    // Prologue, one memory round trip deep: every kernel argument the wave
+    // needs is a scalar load issued here; the schedule is arithmetic on them;
+    // the unit descriptors are loaded before the plane table is written and
+    // the class code is entered.
     const int nb = gridDim.x, b = blockIdx.x;
     const int lb = (b & 7) * (nb >> 3) + (b >> 3);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int gw = lb * waves_per_block<BPC, GRP>() + wave;
-    if (gw >= a.nwaves) return;
+    // Every kernel argument of the prologue by constant index, pinned in
+    // SGPRs at the top (the empty asm uses them), so the scalar loads go out
+    // as one batch with one wait instead of a chain of dependent waits.
+    int wpre[NC + 1], wps[NC], cs[NC + 1];
+#pragma unroll
+    for (int c = 0; c <= NC; c++) {
+        wpre[c] = a.wpre[c];
+        cs[c] = a.class_start[c];
+        if (c < NC) wps[c] = a.wps[c];
+    }
+    using P = typename Px<BPC>::pixel;
+    const int nwaves = a.nwaves;
+    const Dav1dGpuUnit *units = a.units;
+    asm volatile("" ::"s"(nwaves), "s"(units));
+#pragma unroll
+    for (int c = 0; c <= NC; c += 4)
+        asm volatile("" ::"s"(wpre[c]), "s"(cs[c]), "s"(wps[c < NC ? c : 0]), "s"(wpre[cmin(c + 1, NC)]),
+                     "s"(cs[cmin(c + 1, NC)]), "s"(wps[cmin(c + 1, NC - 1)]), "s"(wpre[cmin(c + 2, NC)]),
+                     "s"(cs[cmin(c + 2, NC)]), "s"(wps[cmin(c + 2, NC - 1)]), "s"(wpre[cmin(c + 3, NC)]),
+                     "s"(cs[cmin(c + 3, NC)]), "s"(wps[cmin(c + 3, NC - 1)]));
+    if (gw >= nwaves) return;
     // (segment, class) of this wave from the per-segment wave prefix
     // schedule: (segment group, class position, segment in group); a group
     // of kSegInner segments runs its classes largest first as a whole
     constexpr int SL = kSegInner;
-    const int wgrp = a.wpre[NC] * SL;
+    const int wgrp = wpre[NC] * SL;
     const int sg = gw / wgrp, r = gw - sg * wgrp;
-    int pos = 0;   // schedule position inside the group (kOrder)
+    int pos = 0, wpre_p = 0, wp = wps[0];   // schedule position inside the group (kOrder)
 #pragma unroll
-    for (int c = 1; c < NC; c++) pos += r >= a.wpre[c] * SL;
+    for (int c = 1; c < NC; c++) {
+        const bool ge = r >= wpre[c] * SL;
+        pos = ge ? c : pos;
+        wpre_p = ge ? wpre[c] : wpre_p;
+        wp = ge ? wps[c] : wp;
+    }
     const int cls = order_class(pos);
-    const int U = 64 >> (int)((kLog2Lanes >> (3 * cls)) & 7);   // no table load
-    const int r2 = r - a.wpre[pos] * SL, wp = a.wps[pos];
+    int cs0 = cs[0], cs1 = cs[1];   // class_start[cls], class_start[cls + 1] by selects
+#pragma unroll
+    for (int c = 1; c < NC; c++) {
+        cs0 = cls == c ? cs[c] : cs0;
+        cs1 = cls == c ? cs[c + 1] : cs1;
+    }
+    const int lg = (int)((kLog2Lanes >> (3 * cls)) & 7);   // log2 lanes per unit, no table load
+    const int U = 64 >> lg;
+    const int r2 = r - wpre_p * SL;
     const int sl = SL == 1 ? 0 : r2 / wp;
     const int s = sg * SL + sl;
-    const int first = a.class_start[cls] + (s * wp + r2 - sl * wp) * U;
-    const int count = min(U, a.class_start[cls + 1] - first);
+    const int first = cs0 + (s * wp + r2 - sl * wp) * U;
+    const int count = min(U, cs1 - first);
     if (count <= 0) return;
-    if constexpr (DGPU_TRACE) {   // kernel-entry time of this wave
-        if ((threadIdx.x & 63) == 0) a.trace[((size_t)GRP << 20) + (size_t)gw * 16 + 15] = t_entry;
+    // this lane's unit descriptor (lanes past the last unit re-read it)
+    const Dav1dGpuUnit u = units[first + min((int)(threadIdx.x & 63) >> lg, count - 1)];
+    // per-wave copy of the plane table: lane-indexed vector loads of the
+    // argument segment, in flight together with the descriptor loads (no
+    // workgroup barrier: the waves do not wait for each other)
+    __shared__ PlaneTab<BPC> ptab[waves_per_block<BPC, GRP>()];
+    PlaneTab<BPC> &pt = ptab[wave];
+    {
+        const int t = threadIdx.x & 63;
+        const int tr = min(t, DGPU_MAX_REFS * 3 - 1), td = min(t, 2);   // clamped: loads need no branch
+        const P *rp = (&a.ref[0][0])[tr];
+        const int rs = (&a.ref_stride[0][0])[tr];
+        P *dp = a.dst[td];
+        const int dsd = a.dst_stride[td];
+        if (t < DGPU_MAX_REFS * 3) {
+            pt.ref[t] = rp;
+            pt.ref_stride[t] = rs;
+        }
+        if (t < 3) {
+            pt.dst[t] = dp;
+            pt.dst_stride[t] = dsd;
+        }
     }
-    dispatch<BPC, GRP>(a, pt, cls, first, count, lds + wave * WL, gw,
-                       std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
+    wave_sync();
+    if constexpr (DGPU_TRACE) {   // kernel-entry and post-prologue times of this wave
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long t_sched = __builtin_amdgcn_s_memtime();
+        if ((threadIdx.x & 63) == 0) {
+            unsigned long long *tr = a.trace + ((size_t)GRP << 20) + (size_t)gw * 16;
+            tr[15] = t_entry;
+            tr[13] = t_entry;
+            tr[14] = t_sched;
+        }
+    }
+    dispatch<BPC, GRP>(a, pt, u, cls, first, count, lds + wave * WL, gw);
 }
 
 template <int BPC, int GRP>

@@ -810,8 +810,8 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
 // ---------------------------------------------------------------- kernel --
 
 template <int BPC, int TX>
-__device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, int first, int count,
-                                            uint8_t *wave_lds, int gw, int grp) {
+__device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
+                                            int first, int count, uint8_t *wave_lds, int gw, int grp) {
     using CL = Cls<TX>;
     using SL = Slot<BPC, TX>;
     using P = typename Px<BPC>::pixel;
@@ -832,8 +832,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     };
     mark(0);
 
-    const Dav1dGpuUnit u = a.units[first + g];
-    mark(1);
+    mark(1);   // the descriptor was loaded by the kernel prologue (lane's unit = first + g)
     uint8_t *slot = wave_lds + g * SL::BYTES;
     uint8_t *cfl = slot;                                           // staged coefs, then residual
     TT *res = reinterpret_cast<TT *>(slot);

@@ -35,6 +35,10 @@ REF_PAD = 96   # reference planes carry this many padding pixels on every side
 
 # picture bands of the unit sort (see make_frame); DAV1D_GPU_SORT_BANDS overrides (tuning)
 SORT_BANDS = int(os.environ.get("DAV1D_GPU_SORT_BANDS", "16"))
+# order inside (class, band, pred kind): "txtp" (transform type, then filter /
+# mode), "block" (prediction block, so a block's units share a wave),
+# "raster" (picture position), "txblk" (txtp, then block); tuning knob
+SORT_MODE = os.environ.get("DAV1D_GPU_SORT_MODE", "txtp")
 
 _SCALE = [4.0, 4.0 * 2 ** -0.5, 2.0, 2.0 * 2 ** -0.5, 1.0, 0.5 * 2 ** -0.5, 0.25,
           0.125 * 2 ** -0.5, 0.0625]
@@ -353,7 +357,16 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     band = (uy * SORT_BANDS) // ph[plane_u]
     tt = units["txtp"].astype(np.int64)
     minor = np.where(inter, tt * 16 + sort_minor, sort_minor * 256 + tt)
-    order = np.lexsort((minor, units["pred"], band, units["tx"]))
+    pos = uy.astype(np.int64) * W + ux
+    if SORT_MODE == "block":
+        keys = (pos, blk, units["pred"], band, units["tx"])
+    elif SORT_MODE == "raster":
+        keys = (ux, uy, units["pred"], band, units["tx"])
+    elif SORT_MODE == "txblk":
+        keys = (pos, blk, minor, units["pred"], band, units["tx"])
+    else:
+        keys = (minor, units["pred"], band, units["tx"])
+    order = np.lexsort(keys)
     units = units[order]
     counts = np.bincount(units["tx"], minlength=abi.N_TX)
     class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
