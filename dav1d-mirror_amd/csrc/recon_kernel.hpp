@@ -49,6 +49,12 @@
 #ifndef DGPU_TRACE
 #define DGPU_TRACE 0       // per-wave phase timestamps (tools/wave_trace.py)
 #endif
+#ifndef DGPU_ALIGNED_ROWS8
+#define DGPU_ALIGNED_ROWS8 1    // 8bpc footprint rows by aligned loads + v_alignbyte (see HPass)
+#endif
+#ifndef DGPU_ALIGNED_ROWS16
+#define DGPU_ALIGNED_ROWS16 0   // 16bpc: register pressure spills with it (measured), off
+#endif
 
 namespace dgpu {
 
@@ -614,9 +620,17 @@ template <int BPC, int TX> struct HPass {
     static_assert(G % QW == 0, "lane quads must be fixed");
     static constexpr int B = BPC / 8;
     static constexpr int CH = cmin(IT, BPC == 8 ? 3 : 2);   // tasks whose loads are in flight together
-    using Raw = typename std::conditional<BPC == 8, u32x3a1, u32x4a2>::type;
+    // 8bpc rows are read with dword-aligned loads from the row's dword and
+    // realigned in registers (v_alignbyte by the byte skew): the texture
+    // path splits an unaligned multi-dword load, measured 2.4-3.3x the cost
+    // of an aligned one (tools/probe/ta_rate.hip)
+    static constexpr bool AL = BPC == 8 ? DGPU_ALIGNED_ROWS8 : DGPU_ALIGNED_ROWS16;
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+    using Raw = typename std::conditional<AL, u32x4, typename std::conditional<BPC == 8, u32x3a1, u32x4a2>::type>::type;
+    using RawB = typename std::conditional<AL, u32x3, u32x2a2>::type;   // 16bpc: the row's tail
     Raw ra[CH][2];
-    u32x2a2 rb[CH][2];   // 16bpc: pixels 8..11 of each row
+    RawB rb[CH][2];
+    unsigned sh;         // byte skew of the footprint rows (all rows share it; AL only)
     const uint8_t *rp;
     uint32_t *mp;
     unsigned sb;
@@ -629,6 +643,11 @@ template <int BPC, int TX> struct HPass {
         const int q = l % QW;
         p0 = l / QW;
         rp = reinterpret_cast<const uint8_t *>(org) + (size_t)(2u * p0 * sb) + 4 * B * q;
+        sh = 0;
+        if constexpr (AL) {
+            sh = (unsigned)reinterpret_cast<uintptr_t>(rp) & 3u;   // strides are dword multiples (launch check)
+            rp -= sh;
+        }
         mp = mid + p0 * W + 4 * q;
         if constexpr (BPC == 8) {
             const uint2 t = reinterpret_cast<const uint2 *>(dspt_mc8)[bank * 16 + m];
@@ -644,11 +663,23 @@ template <int BPC, int TX> struct HPass {
             const uint8_t *a0 = rp + (size_t)((unsigned)(p - p0) * 2u * sb);
             // row 2p+1 == H+7 (last pair) is never used: re-read row 2p
             const uint8_t *a1 = 2 * p + 1 < H + 7 ? a0 + sb : a0;
+#ifdef DGPU_FAKE_COALESCE
+            (void)a1;
+#endif
+#ifdef DGPU_FAKE_COALESCE   // cost-model probe: every lane reads lane 0's rows (wrong output)
+            {
+                const uint64_t av = reinterpret_cast<uint64_t>(a0);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)av);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(av >> 32));
+                a0 = reinterpret_cast<const uint8_t *>(((uint64_t)hi << 32) | (uint64_t)lo);
+            }
+            a1 = a0;
+#endif
             ra[c][0] = gld<Raw>(a0);
             ra[c][1] = gld<Raw>(a1);
             if constexpr (BPC == 16) {
-                rb[c][0] = gld<u32x2a2>(a0 + 16);
-                rb[c][1] = gld<u32x2a2>(a1 + 16);
+                rb[c][0] = gld<RawB>(a0 + 16);
+                rb[c][1] = gld<RawB>(a1 + 16);
             }
         }
     }
@@ -665,17 +696,29 @@ template <int BPC, int TX> struct HPass {
                         // and the reference's mid = (s + 2) >> 2 (intermediate_bits 4) is
                         // stored as mid - 2048 = (acc + 2) >> 2; the vertical pass adds back
                         // 64 * 2048 (kMidBias).  Both forms fit int16 for 8-bit input.
-                        const uint32_t w0 = ra[c][rr].x ^ 0x80808080u;
-                        const uint32_t w1 = ra[c][rr].y ^ 0x80808080u;
-                        const uint32_t w2 = ra[c][rr].z ^ 0x80808080u;
+                        uint32_t w0 = ra[c][rr].x, w1 = ra[c][rr].y, w2 = ra[c][rr].z;
+                        if constexpr (AL) {
+                            w0 = alb(ra[c][rr].y, ra[c][rr].x, sh);
+                            w1 = alb(ra[c][rr].z, ra[c][rr].y, sh);
+                            w2 = alb(ra[c][rr][3], ra[c][rr].z, sh);
+                        }
+                        w0 ^= 0x80808080u;
+                        w1 ^= 0x80808080u;
+                        w2 ^= 0x80808080u;
                         const uint32_t lo[4] = {w0, alb(w1, w0, 1), alb(w1, w0, 2), alb(w1, w0, 3)};
                         const uint32_t hi[4] = {w1, alb(w2, w1, 1), alb(w2, w1, 2), alb(w2, w1, 3)};
                         hdot4x4(lo, hi, th.x, th.y, mm[rr]);
                     } else {
                         const int sh = 6 - ib, rnd = (1 << sh) >> 1;
                         // e: pixel pairs (2i, 2i+1), o: (2i+1, 2i+2)
-                        const uint32_t e[6] = {ra[c][rr].x, ra[c][rr].y, ra[c][rr].z, ra[c][rr].w,
-                                               rb[c][rr].x, rb[c][rr].y};
+                        uint32_t e[6] = {ra[c][rr][0], ra[c][rr][1], ra[c][rr][2], ra[c][rr][3],
+                                         rb[c][rr][0], rb[c][rr][1]};
+                        if constexpr (AL) {
+                            const uint32_t d[7] = {ra[c][rr][0], ra[c][rr][1], ra[c][rr][2], ra[c][rr][3],
+                                                   rb[c][rr][0], rb[c][rr][1], rb[c][rr][2]};
+#pragma unroll
+                            for (int i = 0; i < 6; i++) e[i] = alb(d[i + 1], d[i], sh);
+                        }
                         uint32_t o[5];
 #pragma unroll
                         for (int i = 0; i < 5; i++) o[i] = alb(e[i + 1], e[i], 2);
@@ -824,6 +867,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     if (g >= count) return;
     // DGPU_TRACE: timestamp phase i after draining this wave's memory ops
     auto mark = [&](int i) {
+#ifdef DGPU_ASM_MARKS   // static per-phase instruction counts (tools/phase_isa.py)
+        asm volatile(";DGPU_MARK %0" ::"n"(i));
+#endif
         if constexpr (DGPU_TRACE) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -1155,6 +1201,30 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
     }
     mark(8);
+#if defined(DGPU_PAD_SALU) || defined(DGPU_PAD_VALU) || defined(DGPU_PAD_VMEM)   // cost-model probes (tools/build_variants.sh)
+    {
+        int p0 = first, p1 = count, p2 = gw, p3 = grp;
+#ifdef DGPU_PAD_SALU
+#pragma unroll
+        for (int i = 0; i < DGPU_PAD_SALU / 4; i++)
+            asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1"
+                         : "+s"(p0), "+s"(p1), "+s"(p2), "+s"(p3));
+#endif
+        int v0 = lane, v1 = lane + 1, v2 = lane + 2, v3 = lane + 3;
+#ifdef DGPU_PAD_VALU
+#pragma unroll
+        for (int i = 0; i < DGPU_PAD_VALU / 4; i++)
+            asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1"
+                         : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+#endif
+#ifdef DGPU_PAD_VMEM
+#pragma unroll
+        for (int i = 0; i < DGPU_PAD_VMEM; i++)
+            v0 += gld<int>(pt.ref[0] + ((uint32_t)(u.dst_off * 7 + lane * 4099 + i * 131) % (1u << 22)));
+#endif
+        asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(p3), "v"(v0), "v"(v1), "v"(v2), "v"(v3));
+    }
+#endif
 }
 
 }  // namespace dgpu

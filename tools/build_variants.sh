@@ -22,6 +22,10 @@ build() {
 }
 for v in ${VARIANTS:-nomc noitx nointra}; do
     case $v in
+        salu200) build salu200 -DDGPU_PAD_SALU=200 ;;
+        vmem8) build vmem8 -DDGPU_PAD_VMEM=8 ;;
+        fakecoal) build fakecoal -DDGPU_FAKE_COALESCE=1 ;;
+        valu200) build valu200 -DDGPU_PAD_VALU=200 ;;
         nomc) build nomc -DDGPU_ABL_MC=1 ;;
         noitx) build noitx -DDGPU_ABL_ITX=1 ;;
         nointra) build nointra -DDGPU_ABL_INTRA=1 ;;
