@@ -619,7 +619,10 @@ template <int BPC, int TX> struct HPass {
     static constexpr int PS = G / QW;   // row-pair step per task
     static_assert(G % QW == 0, "lane quads must be fixed");
     static constexpr int B = BPC / 8;
-    static constexpr int CH = cmin(IT, BPC == 8 ? 3 : 2);   // tasks whose loads are in flight together
+#ifndef DGPU_CH16
+#define DGPU_CH16 2
+#endif
+    static constexpr int CH = cmin(IT, BPC == 8 ? 3 : DGPU_CH16);   // tasks whose loads are in flight together
     // 8bpc rows are read with dword-aligned loads from the row's dword and
     // realigned in registers (v_alignbyte by the byte skew): the texture
     // path splits an unaligned multi-dword load, measured 2.4-3.3x the cost

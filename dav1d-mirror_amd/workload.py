@@ -60,6 +60,11 @@ class FrameConfig:
     seed: int = 0x5EED0001
     tx64: bool = False            # allow 64-point transforms (64x64 luma blocks)
     cfl_frac: float = 0.50        # of intra blocks: chroma predicted with CfL (config 3)
+    # "mc" frames: prediction-only blocks wider than this are cut into units of
+    # this size (the prediction of a piece is the block's prediction there:
+    # mc is pointwise and the filter bank follows the block size, bw4/bh4), so
+    # a 64x64 block does not need the 64-point class group's long waves
+    mc_split: int = int(os.environ.get("DAV1D_GPU_MC_SPLIT", "32"))   # env: tuning knob
 
     @property
     def pixel_dtype(self):
@@ -202,7 +207,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         for b in range(nb):
             s = int(bs[b])
             if cfg.kind == "mc":
-                tw = th = s
+                tw = th = min(s, cfg.mc_split)
             else:
                 cands = _tx_candidates(s, cfg.tx64)
                 tw, th = cands[(b * 7 + plane * 3 + int(rng.integers(0, 1 << 20))) % len(cands)]

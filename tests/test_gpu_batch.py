@@ -31,8 +31,9 @@ def test_batch_small_8bpc(pkg, oracle, seed):
     _check(_frame(pkg, width=512, height=256, seed=seed), oracle)
 
 
-def test_batch_small_mc_only(pkg, oracle):
-    _check(_frame(pkg, width=512, height=256, kind="mc", seed=5), oracle)
+@pytest.mark.parametrize("split", [16, 32, 64])
+def test_batch_small_mc_only(pkg, oracle, split):
+    _check(_frame(pkg, width=512, height=256, kind="mc", seed=5, mc_split=split), oracle)
 
 
 @pytest.mark.parametrize("bdmax", [1023, 4095])

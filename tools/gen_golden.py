@@ -21,7 +21,7 @@ import __graft_entry__ as ge  # noqa: E402
 CASES = [
     ("full8_s1", dict(width=128, height=64, seed=1)),
     ("full8_s2", dict(width=256, height=128, seed=2)),
-    ("mc8", dict(width=256, height=128, kind="mc", seed=3)),
+    ("mc8", dict(width=256, height=128, kind="mc", seed=3, mc_split=64)),
     ("full10", dict(width=128, height=64, bpc=16, bitdepth_max=1023, seed=4)),
     ("full12", dict(width=128, height=64, bpc=16, bitdepth_max=4095, seed=5)),
     ("full8_tx64", dict(width=256, height=128, seed=6, tx64=True)),
