@@ -100,6 +100,7 @@ FAMILIES = {
     "mc": "inter only: mc put / mct x2 + avg per block, no residual",
     "ipred": "intra only: the 14 intra_pred modes + CfL per transform block, no residual",
     "itx": "inv_txfm_add only: residual 4x4..32x32 onto an existing picture (dst read + write)",
+    "ext": "the other batch kinds with residual: mc put / avg / w_avg / mask compound and pal_pred blocks",
 }
 
 

@@ -19,6 +19,9 @@ DCT_DCT, IDTX, H_DCT, WHT_WHT = 0, 9, 11, 16
 NO_RESIDUAL = 0xFF          # txtp value: prediction only (no inv_txfm_add)
 
 PRED_NONE, PRED_INTER, PRED_INTER_AVG, PRED_INTRA, PRED_CFL = 0, 1, 2, 3, 4
+PRED_INTER_WAVG, PRED_INTER_MASK, PRED_PAL = 5, 6, 7
+INTER_KINDS = (PRED_INTER, PRED_INTER_AVG, PRED_INTER_WAVG, PRED_INTER_MASK)
+COMPOUND_KINDS = (PRED_INTER_AVG, PRED_INTER_WAVG, PRED_INTER_MASK)
 FILTER_2D_BILINEAR = 9
 
 (DC_PRED, VERT_PRED, HOR_PRED, LEFT_DC_PRED, TOP_DC_PRED, DC_128_PRED, Z1_PRED,
@@ -49,7 +52,7 @@ UNIT_DTYPE = np.dtype({
     "names": ["dst_off", "coef_off", "tx", "txtp", "plane", "pred", "nzw", "nzh",
               "bw4", "bh4",
               "src_off0", "src_off1", "mx0", "mx1", "my0", "my1", "filter2d", "ref0", "ref1",
-              "pad_inter", "edge_off", "angle", "mode", "pad_intra", "max_w", "max_h",
+              "weight", "edge_off", "angle", "mode", "pad_intra", "max_w", "max_h",
               "cfl_alpha", "cfl_pad_wh", "cfl_luma_off"],
     "formats": ["<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
                 "<i4", "<i4", "u1", "u1", "u1", "u1", "u1", "u1", "u1", "u1",
@@ -79,7 +82,9 @@ class FrameBatch(ctypes.Structure):
                 ("bitdepth_max", ctypes.c_int32),
                 ("zero_coefs", ctypes.c_int32),
                 ("cfl_luma", Plane),
-                ("cfl_ss", ctypes.c_int32)]
+                ("cfl_ss", ctypes.c_int32),
+                ("aux", ctypes.c_void_p),
+                ("aux_pool", ctypes.c_void_p)]
 
 
 _LIB = None

@@ -44,6 +44,10 @@ class DeviceFrame:
                         for a in fd.dst_init]
         else:
             self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fd.plane_wh]
+        self.aux = self.aux_pool = None
+        if fd.aux is not None:   # INTER_MASK masks / PAL palette records
+            self.aux = torch.from_numpy(np.ascontiguousarray(fd.aux, dtype=np.int32)).to(dev)
+            self.aux_pool = torch.from_numpy(np.ascontiguousarray(fd.aux_pool, dtype=np.uint8)).to(dev)
         self.zero_coefs = zero_coefs
         self.batch = self._make_batch()
         self.lib = abi.load_lib()
@@ -75,6 +79,9 @@ class DeviceFrame:
         b.cfl_luma.stride = self.cfl_luma.shape[1] * bpp
         b.cfl_luma.w, b.cfl_luma.h = fd.plane_wh[0]
         b.cfl_ss = 3   # 4:2:0
+        if self.aux is not None:
+            b.aux = self.aux.data_ptr()
+            b.aux_pool = self.aux_pool.data_ptr()
         return b
 
     def launch(self, stream=None):

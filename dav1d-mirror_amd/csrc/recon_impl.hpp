@@ -258,6 +258,8 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     a.cfl_luma = (const P *)b->cfl_luma.data;
     a.cfl_luma_stride = (int)(b->cfl_luma.stride / B);
     a.cfl_ss = b->cfl_ss;
+    a.aux = b->aux;
+    a.aux_pool = (const uint8_t *)b->aux_pool;
     memcpy(a.class_start, b->class_start, sizeof(a.class_start));
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;

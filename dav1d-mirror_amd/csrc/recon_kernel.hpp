@@ -83,6 +83,8 @@ template <int BPC> struct ReconArgs {
     const P *cfl_luma;    // luma read by CFL units
     int cfl_luma_stride;  // pixels
     int cfl_ss;           // ss_hor | ss_ver << 1
+    const int32_t *aux;       // per unit: aux_pool offset (INTER_MASK mask, PAL record)
+    const uint8_t *aux_pool;
     int class_start[DGPU_N_RECT_TX_SIZES + 1];
     // wave schedule, ordered (segment, class position): every one of the
     // kSegments segments gives the class at position k (kOrder) wps[k]
@@ -896,8 +898,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     const int bdmax = a.bdmax;
     const int ib = Px<BPC>::ibits(bdmax);
     const int pred = u.pred;
-    const bool inter = pred == DGPU_PRED_INTER || pred == DGPU_PRED_INTER_AVG;
-    const bool comp = pred == DGPU_PRED_INTER_AVG;
+    const bool comp = pred == DGPU_PRED_INTER_AVG || pred == DGPU_PRED_INTER_WAVG || pred == DGPU_PRED_INTER_MASK;
+    const bool inter = pred == DGPU_PRED_INTER || comp;
     const int txtp = u.txtp;
     const bool nores = txtp == DGPU_NO_RESIDUAL;
     const int nzw = u.nzw, nzh = u.nzh;
@@ -954,6 +956,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         hinit(hp1, 1);
         hp1.load(0);
     }
+    // INTER_MASK / PAL: the unit's aux_pool offset (mask / palette record)
+    const bool auxed = pred == DGPU_PRED_INTER_MASK || pred == DGPU_PRED_PAL;
+    const int auxo = auxed ? a.aux[first + g] : 0;
     int cfsk = 0;
     if (ncoef) cfsk = cst.commit(cfl, l);
     const P *tl = nullptr;
@@ -1145,9 +1150,26 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                     mc_vtask<W>(mid0, j, q, tv0, KP, 6, p0);
                 }
                 mc_vtask<W>(mid1, j, q, tv1, KP, 6, t1);
+                // p = prep + PREP_BIAS, so the reference's bias terms cancel:
+                // avg_c / w_avg_c / mask_c (src/mc_tmpl.c:587-639)
+                if (pred == DGPU_PRED_INTER_AVG) {
 #pragma unroll
-                for (int i = 0; i < 8; i++)
-                    pv[i] = clampi((p0[i] + t1[i] + (1 << ib)) >> (ib + 1), 0, bdmax);
+                    for (int i = 0; i < 8; i++)
+                        pv[i] = clampi((p0[i] + t1[i] + (1 << ib)) >> (ib + 1), 0, bdmax);
+                } else if (pred == DGPU_PRED_INTER_WAVG) {
+                    const int wt = u.p.inter.weight;
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+                        pv[i] = clampi((p0[i] * wt + t1[i] * (16 - wt) + (8 << ib)) >> (ib + 4), 0, bdmax);
+                } else {   // INTER_MASK: mask rows of the block (stride bw), 4 bytes per task row
+                    const uint8_t *mk = a.aux_pool + auxo + (2 * j) * bw + 4 * q;
+                    const uint32_t m0 = gld<uint32_t>(mk), m1 = gld<uint32_t>(mk + bw);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const int m = (int)(((i < 4 ? m0 : m1) >> (8 * (i & 3))) & 0xff);
+                        pv[i] = clampi((p0[i] * m + t1[i] * (64 - m) + (32 << ib)) >> (ib + 6), 0, bdmax);
+                    }
+                }
                 emit(j, q, pv);
             }
         } else {   // put: rnd_sh(t, 6 + ib)
@@ -1186,6 +1208,30 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                 for (int i = 0; i < 8; i++) pv[i] = ptile[(2 * j + (i >> 2)) * W + 4 * q + (i & 3)];
             } else {
                 intra_task<TX>(is, tl, fe, 4 * q, 2 * j, pv);
+            }
+            emit(j, q, pv);
+        }
+    } else if (pred == DGPU_PRED_PAL) {   // pal_pred (src/ipred_tmpl.c:717-730)
+        const uint8_t *rec = a.aux_pool + auxo;
+        const u32x4 pal = gld<u32x4>(rec);   // 8 entries (u8 x 8 or u16 x 8)
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t >= NT) break;
+            const int j = t / QW, q = t % QW;
+            int pv[8];
+#pragma unroll
+            for (int rr = 0; rr < 2; rr++) {
+                const uint32_t ix = gld<uint16_t>(rec + 16 + (2 * j + rr) * (W / 2) + 2 * q);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int e = (int)((ix >> (4 * i)) & 7);
+                    if constexpr (BPC == 8)
+                        pv[4 * rr + i] = (int)(((e < 4 ? pal[0] : pal[1]) >> (8 * (e & 3))) & 0xff);
+                    else
+                        pv[4 * rr + i] = (int)(((e < 2 ? pal[0] : e < 4 ? pal[1] : e < 6 ? pal[2] : pal[3]) >>
+                                                (16 * (e & 1))) & 0xffff);
+                }
             }
             emit(j, q, pv);
         }

@@ -87,6 +87,8 @@ class FrameData:
     blk: np.ndarray = None        # prediction-block id of each unit (stats only)
     cfl_luma: np.ndarray = None   # luma plane CFL units read (synthetic "reconstructed" luma)
     dst_init: list = None         # starting picture planes ("itx" frames add onto them)
+    aux: np.ndarray = None        # per-unit int32: aux_pool offset (INTER_MASK / PAL units)
+    aux_pool: np.ndarray = None   # u8 pool: block masks, palette records
     stats: dict = field(default_factory=dict)
 
     @property
@@ -178,6 +180,14 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     r = rng.random(nb)
     if cfg.kind == "mc":
         kind = np.where(rng.random(nb) < cfg.compound_frac, abi.PRED_INTER_AVG, abi.PRED_INTER)
+    elif cfg.kind == "ext":
+        # the batch tier's other prediction kinds, with residual as in
+        # "full": put / avg / w_avg / mask compound and palette blocks
+        rng.random(nb)   # keep the later draws aligned with "full"
+        e = np.random.default_rng(cfg.seed ^ 0xE7E7).random(nb)
+        kind = np.select([e < 0.25, e < 0.40, e < 0.60, e < 0.80],
+                         [abi.PRED_INTER, abi.PRED_INTER_AVG, abi.PRED_INTER_WAVG, abi.PRED_INTER_MASK],
+                         abi.PRED_PAL)
     elif cfg.kind in ("ipred", "itx"):
         rng.random(nb)   # keep the later draws aligned with "full"
         kind = np.full(nb, abi.PRED_INTRA if cfg.kind == "ipred" else abi.PRED_NONE)
@@ -246,7 +256,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     units["bh4"] = bsz // 4
 
     # inter parameters
-    inter = (pk == abi.PRED_INTER) | (pk == abi.PRED_INTER_AVG)
+    inter = np.isin(pk, abi.INTER_KINDS)
     ref_stride = np.array([refs[0][p].shape[1] for p in range(3)])
     for k in range(2):
         mvx = mv[blk, k, 0]
@@ -261,6 +271,42 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         units[f"my{k}"] = np.where(inter, mvy & 15, 0)
         units[f"ref{k}"] = k
     units["filter2d"] = np.where(inter, filt[blk], 0)
+    aux = aux_pool = None
+    if cfg.kind == "ext":
+        xr = np.random.default_rng(cfg.seed ^ 0xA0A0)
+        units["weight"] = np.where(pk == abi.PRED_INTER_WAVG, xr.integers(1, 16, n), 0)
+        aux = np.zeros(n, np.int32)
+        chunks, off = [], 0
+        # INTER_MASK: one mask 0..64 per prediction block (per plane), row
+        # stride = the block width; a unit points at its top-left inside it
+        mb = np.nonzero(pk == abi.PRED_INTER_MASK)[0]
+        bkey = blk * 3 + plane_u
+        first_of = {}
+        for i in mb:
+            k = int(bkey[i])
+            if k not in first_of:
+                s_ = int(bsz[i])
+                first_of[k] = off
+                chunks.append(xr.integers(0, 65, s_ * s_, dtype=np.uint8))
+                off += (s_ * s_ + 15) // 16 * 16
+                chunks.append(np.zeros((s_ * s_ + 15) // 16 * 16 - s_ * s_, np.uint8))
+            bx0 = (int(ux[i]) // int(bsz[i])) * int(bsz[i])   # blocks are aligned to their size
+            by0 = (int(uy[i]) // int(bsz[i])) * int(bsz[i])
+            aux[i] = first_of[k] + (int(uy[i]) - by0) * int(bsz[i]) + (int(ux[i]) - bx0)
+        # PAL: per unit a 16-B record of 8 entries, then the packed index map
+        pb = np.nonzero(pk == abi.PRED_PAL)[0]
+        bpp_ = 1 if cfg.bpc == 8 else 2
+        for i in pb:
+            w_, h_ = int(tw[i]), int(th[i])
+            pal = xr.integers(0, bdmax + 1, 8).astype(cfg.pixel_dtype).view(np.uint8)
+            rec = np.zeros(16 + (w_ * h_ // 2 + 15) // 16 * 16, np.uint8)
+            rec[:8 * bpp_] = pal
+            idx = xr.integers(0, 8, size=(h_, w_))
+            rec[16:16 + w_ * h_ // 2] = (idx[:, 0::2] | (idx[:, 1::2] << 4)).astype(np.uint8).ravel()
+            aux[i] = off
+            chunks.append(rec)
+            off += len(rec)
+        aux_pool = np.concatenate(chunks) if chunks else np.zeros(16, np.uint8)
 
     # intra parameters
     intra = pk == abi.PRED_INTRA
@@ -302,7 +348,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     units[cfl] = cu
     cfl_luma = crng.integers(0, bdmax + 1, size=(H, luma_stride), dtype=cfg.pixel_dtype)
     m = np.where(cfl, cfl_dc[blk], m)
-    sort_minor = np.where(inter, filt[blk], 16 + m)
+    sort_minor = np.where(inter, filt[blk], 16 + np.where(pk == abi.PRED_PAL, 0, m))
     edges = rng.integers(0, bdmax + 1, size=max(int(edge_len.sum()), 1), dtype=cfg.pixel_dtype)
 
     # transform types, coefficient regions and coefficients
@@ -382,7 +428,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         dst_init = [drng.integers(0, bdmax + 1, size=(ph_, pw_), dtype=cfg.pixel_dtype) for (pw_, ph_) in planes]
     fd = FrameData(cfg=cfg, units=units, class_start=class_start, coefs=coefs, edges=edges,
                    refs=refs, plane_wh=planes, blk=(blk * 3 + plane_u)[order], cfl_luma=cfl_luma,
-                   dst_init=dst_init)
+                   dst_init=dst_init, aux=None if aux is None else aux[order], aux_pool=aux_pool)
     fd.stats = algorithmic_bytes(fd)
     return fd
 
@@ -400,13 +446,13 @@ def algorithmic_bytes(fd: FrameData):
     bw, bh = u["bw4"].astype(np.int64) * 4, u["bh4"].astype(np.int64) * 4
     # the reference reads each prediction block's footprint once per mc call
     # (src/recon_tmpl.c:957-1059): count it per block, not per transform unit
-    inter = (u["pred"] == abi.PRED_INTER) | (u["pred"] == abi.PRED_INTER_AVG)
+    inter = np.isin(u["pred"], abi.INTER_KINDS)
     _, first = np.unique(np.where(inter, fd.blk, -1), return_index=True)
     first = first[inter[first]]
     src = np.zeros(len(u), np.int64)
     for k in range(2):
         use = (u["pred"] == abi.PRED_INTER) if k == 0 else np.zeros(len(u), bool)
-        use = use | (u["pred"] == abi.PRED_INTER_AVG)
+        use = use | np.isin(u["pred"], abi.COMPOUND_KINDS)
         mx, my = u[f"mx{k}"], u[f"my{k}"]
         fh = np.where(mx > 0, np.where(bw > 4, 7, 3), 0)
         fv = np.where(my > 0, np.where(bh > 4, 7, 3), 0)
@@ -416,6 +462,11 @@ def algorithmic_bytes(fd: FrameData):
     nopred = u["pred"] == abi.PRED_NONE
     edge = np.where(intra | cfl, 2 * w + 2 * h + 1, 0)
     src = src + np.where(cfl, 4 * w * h, 0)   # co-located 4:2:0 luma the cfl_ac reads
+    # mask compound reads its mask (u8 per pixel); palette units their
+    # entries and packed index map
+    aux_bytes = int((w * h)[u["pred"] == abi.PRED_INTER_MASK].sum())
+    pal = u["pred"] == abi.PRED_PAL
+    aux_bytes += int((w * h // 2)[pal].sum()) + int(pal.sum()) * 8 * bpp
     ncoef = np.where(u["txtp"] == abi.NO_RESIDUAL, 0, np.where(u["nzw"] == 0, 1,
                      u["nzw"].astype(np.int64) * u["nzh"]))
     out_px = int((w * h).sum())
@@ -428,12 +479,14 @@ def algorithmic_bytes(fd: FrameData):
         "coef_bytes": int(ncoef.sum()) * cb,
         "dst_bytes": out_px * bpp,
         "dst_read_bytes": dst_read,
+        "aux_bytes": aux_bytes,
         "desc_bytes": int(len(u)) * 32,
         "pixels": out_px,
         "total_bytes": int(src.sum()) * bpp + int(edge.sum()) * bpp + int(ncoef.sum()) * cb
-                       + out_px * bpp + dst_read + int(len(u)) * 32,
+                       + out_px * bpp + dst_read + aux_bytes + int(len(u)) * 32,
         "n_intra": int(intra.sum()),
         "n_cfl": int(cfl.sum()),
-        "n_inter": int((~intra & ~cfl & ~nopred).sum()),
+        "n_inter": int(inter.sum()),
+        "n_pal": int(pal.sum()),
         "n_nopred": int(nopred.sum()),
     }

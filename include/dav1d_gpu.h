@@ -207,6 +207,22 @@ enum Dav1dGpuPredKind {
                                 luma (batch cfl_luma plane) + cfl_pred with
                                 the DC of the unit's edge array
                                 (src/recon_tmpl.c:1380-1420)                 */
+    DGPU_PRED_INTER_WAVG = 5,/* mct x2 -> w_avg with p.inter.weight (the
+                                jnt_comp weight of ref0, 1..15;
+                                src/mc_tmpl.c:604-620, recon_tmpl.c:1873)    */
+    DGPU_PRED_INTER_MASK = 6,/* mct x2 -> mask_c with a per-pixel mask
+                                0..64 from aux_pool (wedge / inter-intra
+                                style compound; src/mc_tmpl.c:622-639,
+                                recon_tmpl.c:1880-1900).  aux[unit] = byte
+                                offset of the unit's top-left mask value,
+                                row stride = the block width (bw4 * 4)     */
+    DGPU_PRED_PAL = 7,       /* pal_pred (src/ipred_tmpl.c:717-730,
+                                recon_tmpl.c:1233-1250): aux[unit] = byte
+                                offset of a 16-byte aligned record of the
+                                8 palette entries (pixels, padded to 16 B),
+                                followed by the unit's packed index map
+                                (two 4-bit indices per byte, low nibble
+                                first, row stride w / 2)                     */
 };
 
 /* txtp value of a prediction-only unit (no inv_txfm_add): mc-only batches */
@@ -238,7 +254,7 @@ typedef struct Dav1dGpuUnit {
             uint8_t mx[2], my[2];    /* 1/16-pel fraction 0..15              */
             uint8_t filter2d;        /* Dav1dGpuFilter2d                     */
             uint8_t ref[2];          /* reference picture slot               */
-            uint8_t pad_;
+            uint8_t weight;          /* INTER_WAVG: ref0's weight 1..15      */
         } inter;
         struct {          /* INTRA                                           */
             int32_t  edge_off;       /* offset of topleft[0] in the edge pool */
@@ -288,6 +304,11 @@ typedef struct Dav1dGpuFrameBatch {
                              this batch writes: units run unordered          */
     int32_t  cfl_ss;      /* chroma subsampling of CFL units: ss_hor |
                              ss_ver << 1 (3 = 4:2:0, 1 = 4:2:2, 0 = 4:4:4)  */
+    const int32_t *aux;   /* device, one int32 per unit (by unit index): the
+                             aux_pool byte offset of an INTER_MASK unit's
+                             mask or a PAL unit's palette record; only those
+                             kinds read it (may be NULL without them)      */
+    const void *aux_pool; /* device pool of masks (u8) / palette records   */
 } Dav1dGpuFrameBatch;
 
 /* Launch one frame batch on `stream` (a hipStream_t, NULL = default).

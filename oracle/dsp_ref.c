@@ -1436,9 +1436,10 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
         const int pl = u->plane;
         const ptrdiff_t ds = b->dst[pl].stride;
         pixel *dst = (pixel *)b->dst[pl].data + u->dst_off;
-        if (u->pred == DGPU_PRED_INTER || u->pred == DGPU_PRED_INTER_AVG) {
+        if (u->pred == DGPU_PRED_INTER || u->pred == DGPU_PRED_INTER_AVG ||
+            u->pred == DGPU_PRED_INTER_WAVG || u->pred == DGPU_PRED_INTER_MASK) {
             const int f2d = u->p.inter.filter2d;
-            const int comp = u->pred == DGPU_PRED_INTER_AVG;
+            const int comp = u->pred != DGPU_PRED_INTER;
             for (int k = 0; k <= comp; k++) {
                 const int r = u->p.inter.ref[k];
                 const pixel *src = (const pixel *)b->ref[r][pl].data + u->p.inter.src_off[k];
@@ -1453,7 +1454,22 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
                     else prep_8tap(t, src, ss, w, h, mx, my, ftype_of[f2d], u->bw4 * 4, u->bh4 * 4, bdmax);
                 }
             }
-            if (comp) avg_blend(dst, ds, t1, t2, w, h, 0, 0, NULL, bdmax);
+            if (u->pred == DGPU_PRED_INTER_AVG) avg_blend(dst, ds, t1, t2, w, h, 0, 0, NULL, bdmax);
+            else if (u->pred == DGPU_PRED_INTER_WAVG)   /* w_avg_c: jnt weight of ref0 */
+                avg_blend(dst, ds, t1, t2, w, h, 1, u->p.inter.weight, NULL, bdmax);
+            else if (u->pred == DGPU_PRED_INTER_MASK) { /* mask_c on the unit's part of the block mask */
+                uint8_t m[64 * 64];
+                const uint8_t *ms = (const uint8_t *)b->aux_pool + b->aux[i];
+                for (int y = 0; y < h; y++)
+                    for (int x = 0; x < w; x++) m[y * w + x] = ms[y * (u->bw4 * 4) + x];
+                avg_blend(dst, ds, t1, t2, w, h, 2, 0, m, bdmax);
+            }
+        } else if (u->pred == DGPU_PRED_PAL) {
+            /* pal_pred on the unit (pointwise, so the unit's part of the
+             * block's call): 8 entries at the record start, then the packed
+             * index map with stride w / 2 */
+            const uint8_t *rec = (const uint8_t *)b->aux_pool + b->aux[i];
+            pal_pred(dst, ds, (const pixel *)rec, rec + 16, w, h);
         } else if (u->pred == DGPU_PRED_CFL) {
             /* recon_b_intra's CfL: cfl_ac on the co-located luma, then
              * cfl_pred with the DC of the edge array (src/recon_tmpl.c:1380-1420) */

@@ -79,6 +79,12 @@ class HostFrame:
         b.cfl_luma.stride = self.cfl_luma.shape[1] * bpp
         b.cfl_luma.w, b.cfl_luma.h = fd.plane_wh[0]
         b.cfl_ss = 3
+        self.aux = self.aux_pool = None
+        if getattr(fd, "aux", None) is not None:
+            self.aux = np.ascontiguousarray(fd.aux, dtype=np.int32)
+            self.aux_pool = np.ascontiguousarray(fd.aux_pool, dtype=np.uint8)
+            b.aux = self.aux.ctypes.data
+            b.aux_pool = self.aux_pool.ctypes.data
         self.batch = b
 
     def run(self, u0=0, u1=None, threads=1):

@@ -125,7 +125,7 @@ def test_itx_dc_only_shortcut_matches_full_path(oracle, pkg, bpc):
 
 def test_workload_covers_every_pixel_once(pkg):
     import dav1d_mirror_amd.workload as wl
-    for kind in ("full", "mc", "ipred", "itx"):
+    for kind in ("full", "mc", "ipred", "itx", "ext"):
         fd = wl.make_frame(wl.FrameConfig(width=512, height=256, kind=kind, seed=3))
         u = fd.units
         assert np.array_equal(fd.class_start, np.concatenate(
@@ -172,6 +172,37 @@ def test_mc_split_prediction_is_exact(pkg, oracle):
     hb.run()
     assert all(np.array_equal(ha.dst[p], hb.dst[p]) for p in range(3))
     assert a.stats["ref_bytes"] == b.stats["ref_bytes"]
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+def test_oracle_wavg8_and_mask32_equal_avg(pkg, oracle, bpc, bdmax):
+    """w_avg with weight 8 and mask_c with a flat 32 mask are avg_c exactly
+    (src/mc_tmpl.c:587-639): the batch's extra compound kinds reduce to the
+    plain compound average."""
+    import dav1d_mirror_amd.workload as wl
+    abi = pkg.abi
+    fd = wl.make_frame(wl.FrameConfig(width=256, height=128, kind="ext", bpc=bpc, bitdepth_max=bdmax, seed=9))
+    u = fd.units.copy()
+    wv, mk = u["pred"] == abi.PRED_INTER_WAVG, u["pred"] == abi.PRED_INTER_MASK
+    assert wv.any() and mk.any()
+    u["weight"][wv] = 8
+    fd.units = u
+    pool = fd.aux_pool.copy()
+    for i in np.nonzero(mk)[0]:
+        bw = int(u["bw4"][i]) * 4
+        w, h = abi.TX_WH[int(u["tx"][i])]
+        for y in range(h):
+            o = int(fd.aux[i]) + y * bw
+            pool[o:o + w] = 32
+    fd.aux_pool = pool
+    a = oracle.HostFrame(fd)
+    a.run()
+    u2 = u.copy()
+    u2["pred"][wv | mk] = abi.PRED_INTER_AVG
+    fd.units = u2
+    b = oracle.HostFrame(fd)
+    b.run()
+    assert all(np.array_equal(a.dst[p], b.dst[p]) for p in range(3))
 
 
 def test_workload_deterministic(pkg):

@@ -119,9 +119,16 @@ def test_smoke_entry():
 
 
 @pytest.mark.parametrize("kind,bpc,bdmax", [("ipred", 8, 255), ("itx", 8, 255), ("ipred", 16, 1023),
-                                            ("itx", 16, 4095)])
+                                            ("itx", 16, 4095), ("ext", 8, 255), ("ext", 16, 1023),
+                                            ("ext", 16, 4095)])
 def test_batch_family(pkg, oracle, kind, bpc, bdmax):
     """The per-family frames of the bench breakdown: intra/CfL prediction
-    only, and inv_txfm_add onto an existing picture (PRED_NONE: the
-    kernel's picture-read path)."""
+    only, inv_txfm_add onto an existing picture (PRED_NONE: the kernel's
+    picture-read path), and the other inter / palette kinds (w_avg and
+    mask compound, pal_pred), each with residual."""
     _check(_frame(pkg, width=512, height=256, bpc=bpc, bitdepth_max=bdmax, kind=kind, seed=21), oracle)
+
+
+def test_batch_ext_tx64(pkg, oracle):
+    """w_avg / mask / palette units in the 64-point class group too."""
+    _check(_frame(pkg, width=512, height=256, kind="ext", tx64=True, seed=22), oracle)
