@@ -19,7 +19,7 @@ DCT_DCT, IDTX, H_DCT, WHT_WHT = 0, 9, 11, 16
 NO_RESIDUAL = 0xFF          # txtp value: prediction only (no inv_txfm_add)
 
 PRED_NONE, PRED_INTER, PRED_INTER_AVG, PRED_INTRA, PRED_CFL = 0, 1, 2, 3, 4
-PRED_INTER_WAVG, PRED_INTER_MASK, PRED_PAL = 5, 6, 7
+PRED_INTER_WAVG, PRED_INTER_MASK, PRED_PAL, PRED_WARP = 5, 6, 7, 8
 INTER_KINDS = (PRED_INTER, PRED_INTER_AVG, PRED_INTER_WAVG, PRED_INTER_MASK)
 COMPOUND_KINDS = (PRED_INTER_AVG, PRED_INTER_WAVG, PRED_INTER_MASK)
 FILTER_2D_BILINEAR = 9
@@ -84,7 +84,8 @@ class FrameBatch(ctypes.Structure):
                 ("cfl_luma", Plane),
                 ("cfl_ss", ctypes.c_int32),
                 ("aux", ctypes.c_void_p),
-                ("aux_pool", ctypes.c_void_p)]
+                ("aux_pool", ctypes.c_void_p),
+                ("class_warp", ctypes.c_int32 * N_TX)]
 
 
 _LIB = None

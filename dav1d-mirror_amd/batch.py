@@ -82,6 +82,9 @@ class DeviceFrame:
         if self.aux is not None:
             b.aux = self.aux.data_ptr()
             b.aux_pool = self.aux_pool.data_ptr()
+        if fd.class_warp is not None:
+            for i in range(abi.N_TX):
+                b.class_warp[i] = int(fd.class_warp[i])
         return b
 
     def launch(self, stream=None):

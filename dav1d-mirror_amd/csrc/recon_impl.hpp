@@ -25,7 +25,7 @@ namespace dgpu {
 template <int BPC, int GRP, int... TX>
 __host__ __device__ constexpr int group_wave_lds(std::integer_sequence<int, TX...>) {
     int m = 0;
-    ((m = (class_group(TX) == GRP && Slot<BPC, TX>::WAVE > m) ? Slot<BPC, TX>::WAVE : m), ...);
+    ((m = (in_group(TX, GRP) && Slot<BPC, TX>::WAVE > m) ? Slot<BPC, TX>::WAVE : m), ...);
     return m;
 }
 template <int BPC, int GRP> __host__ __device__ constexpr int wave_lds() {
@@ -53,9 +53,9 @@ constexpr uint64_t kLog2Lanes = pack_log2_lanes(std::make_integer_sequence<int, 
 template <int BPC, int TX, int GRP>
 __device__ __forceinline__ void run_class(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
                                           int first, int count, uint8_t *lds, int gw) {
-    if constexpr (TX < DGPU_N_RECT_TX_SIZES && class_group(TX) == GRP &&
+    if constexpr (TX < DGPU_N_RECT_TX_SIZES && in_group(TX, GRP) &&
                   (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS))
-        recon_units<BPC, TX>(a, pt, u, first, count, lds, gw, GRP);
+        recon_units<BPC, TX, GRP == GROUP_WARP>(a, pt, u, first, count, lds, gw, GRP);
 }
 
 // One switch (a compact compare tree) instead of a chain of class tests
@@ -141,12 +141,10 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
         wp = ge ? wps[c] : wp;
     }
     const int cls = order_class(pos);
-    int cs0 = cs[0], cs1 = cs[1];   // class_start[cls], class_start[cls + 1] by selects
+    int cs0 = cs[0];   // the class's range start by selects; its end by one scalar load
 #pragma unroll
-    for (int c = 1; c < NC; c++) {
-        cs0 = cls == c ? cs[c] : cs0;
-        cs1 = cls == c ? cs[c + 1] : cs1;
-    }
+    for (int c = 1; c < NC; c++) cs0 = cls == c ? cs[c] : cs0;
+    const int cs1 = a.class_end[cls];
     const int lg = (int)((kLog2Lanes >> (3 * cls)) & 7);   // log2 lanes per unit, no table load
     const int U = 64 >> lg;
     const int r2 = r - wpre_p * SL;
@@ -200,8 +198,13 @@ static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned
         const int c = kOrder[k];
         a.wpre[k] = acc;
         a.wps[k] = 0;
-        if (class_group(c) != GRP || !((classmask >> c) & 1)) continue;
-        const int n = b->class_start[c + 1] - b->class_start[c];
+        // this launch's range of class c: the WARP units at the end of the
+        // class for the warp launch, the rest for the class's own group
+        const int nw = b->class_warp[c];
+        a.class_start[c] = GRP == GROUP_WARP ? b->class_start[c + 1] - nw : b->class_start[c];
+        a.class_end[c] = GRP == GROUP_WARP ? b->class_start[c + 1] : b->class_start[c + 1] - nw;
+        if (!in_group(c, GRP) || !((classmask >> c) & 1)) continue;
+        const int n = a.class_end[c] - a.class_start[c];
         const int U = 64 / lanes_per_unit(c);
         a.wps[k] = ((n + U - 1) / U + kSegments - 1) / kSegments;
         acc += a.wps[k];
@@ -260,7 +263,10 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     a.cfl_ss = b->cfl_ss;
     a.aux = b->aux;
     a.aux_pool = (const uint8_t *)b->aux_pool;
-    memcpy(a.class_start, b->class_start, sizeof(a.class_start));
+    for (int c = 0; c < DGPU_N_RECT_TX_SIZES; c++) {   // WARP sub-ranges: classes with both sides >= 8
+        const int nw = b->class_warp[c];
+        if (nw < 0 || nw > b->class_start[c + 1] - b->class_start[c] || (nw && !in_group(c, GROUP_WARP))) return -2;
+    }
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;
     // debug-only profiling knob (never set in production):
@@ -274,7 +280,8 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     if (DGPU_TRACE && !trace_buf && hipMalloc(&trace_buf, (size_t)3 << 23) != hipSuccess) return -3;
     a.trace = trace_buf;
     int nw[3] = {0, 0, 0};
-    int rc = launch_group<BPC, GROUP_HUGE>(a, b, classmask, stream);
+    int rc = launch_group<BPC, GROUP_WARP>(a, b, classmask, stream);
+    if (!rc) rc = launch_group<BPC, GROUP_HUGE>(a, b, classmask, stream);
     nw[2] = a.nwaves;
     if (!rc) rc = launch_group<BPC, GROUP_LARGE>(a, b, classmask, stream);
     nw[1] = a.nwaves;

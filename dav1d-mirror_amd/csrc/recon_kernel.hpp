@@ -85,7 +85,8 @@ template <int BPC> struct ReconArgs {
     int cfl_ss;           // ss_hor | ss_ver << 1
     const int32_t *aux;       // per unit: aux_pool offset (INTER_MASK mask, PAL record)
     const uint8_t *aux_pool;
-    int class_start[DGPU_N_RECT_TX_SIZES + 1];
+    int class_start[DGPU_N_RECT_TX_SIZES + 1];   // this launch's unit range per class: [start, end)
+    int class_end[DGPU_N_RECT_TX_SIZES];
     // wave schedule, ordered (segment, class position): every one of the
     // kSegments segments gives the class at position k (kOrder) wps[k]
     // waves (its unit range cut into kSegments runs of wps[k] * U units);
@@ -137,7 +138,7 @@ __host__ __device__ constexpr int lanes_per_unit(int tx) {
 #ifndef DGPU_MERGE_GROUPS
 #define DGPU_MERGE_GROUPS 1
 #endif
-enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2, N_GROUPS = 3 };
+enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2, GROUP_WARP = 3, N_GROUPS = 4 };
 __host__ __device__ constexpr int class_group(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
     return (w == 64 || h == 64) ? GROUP_HUGE
@@ -157,6 +158,12 @@ __host__ __device__ constexpr uint64_t pack_order(int half) {
 __device__ __forceinline__ int order_class(int k) {   // kOrder[k] without a memory load
     constexpr uint64_t lo = pack_order(0), hi = pack_order(1);
     return (int)(((k < 12 ? lo : hi) >> (5 * (k < 12 ? k : k - 12))) & 31);
+}
+
+// classes a launch of group GRP runs: the warp launch takes every class with
+// both sides >= 8 (its units are the WARP sub-ranges), the others by size
+__host__ __device__ constexpr bool in_group(int tx, int grp) {
+    return grp == GROUP_WARP ? (tx_info(tx).w >= 8 && tx_info(tx).h >= 8) : class_group(tx) == grp;
 }
 
 template <int TX> struct Cls {
@@ -855,9 +862,131 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
     }
 }
 
+// ----------------------------------------------------------------- warp ---
+
+// One WARP unit (w, h multiples of 8): warp_affine_8x8_c (src/mc_tmpl.c:
+// 758-791) for each of its 8x8s, 8 rows at a time.  Per strip the 15 x W
+// horizontal intermediates (each column with its own filter) go to the
+// unit's LDS mid area; then each 4x2 task takes its 8 vertical taps per
+// output from it and is emitted (+ residual) like every other prediction.
+template <int BPC, int TX, typename P, typename Emit>
+__device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
+                                          int auxo, int16_t *mid, int l, int bdmax, Emit &emit) {
+    using CL = Cls<TX>;
+    constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NBX = W / 8;
+    const uint8_t *rec = a.aux_pool + auxo;
+    const u32x2 abcd = gld<u32x2>(rec);
+    const int a0 = (int16_t)(abcd[0] & 0xffff), a1 = (int)abcd[0] >> 16;
+    const int a2 = (int16_t)(abcd[1] & 0xffff), a3 = (int)abcd[1] >> 16;
+    const int ri = u.p.inter.ref[0] * 3 + u.plane;
+    const P *ref = pt.ref[ri];
+    const int rs = pt.ref_stride[ri];
+    const int ib = Px<BPC>::ibits(bdmax);
+    const int hsh = 7 - ib, hrnd = (1 << hsh) >> 1;
+    constexpr int NHT = 15 * QW, NVT = 4 * QW;
+#pragma unroll 1
+    for (int sy = 0; sy < H / 8; sy++) {
+#pragma unroll 1
+        for (int k = 0; k < (NHT + G - 1) / G; k++) {   // horizontal: (row, quad) tasks
+            const int t = l + k * G;
+            if (t < NHT) {
+                const int row = t / QW, q = t % QW, x0 = (q & 1) * 4;
+                const u32x2 sb = gld<u32x2>(rec + 16 + 8 * (sy * NBX + (q >> 1)));
+                const int mx = (int)(int16_t)(sb[1] & 0xffff) * 64;
+                const P *s = ref + (int)sb[0] + (row - 3) * rs + x0 - 3;   // columns x0-3 .. x0+7
+                int m4[4];
+                if constexpr (BPC == 8) {
+                    const unsigned sh = (unsigned)reinterpret_cast<uintptr_t>(s) & 3u;
+                    const u32x4 d = gld<u32x4>(reinterpret_cast<const uint8_t *>(s) - sh);
+                    const uint32_t w0 = alb(d[1], d[0], sh) ^ 0x80808080u, w1 = alb(d[2], d[1], sh) ^ 0x80808080u,
+                                   w2 = alb(d[3], d[2], sh) ^ 0x80808080u;
+                    const uint32_t lo[4] = {w0, alb(w1, w0, 1), alb(w1, w0, 2), alb(w1, w0, 3)};
+                    const uint32_t hi[4] = {w1, alb(w2, w1, 1), alb(w2, w1, 2), alb(w2, w1, 3)};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int pos = mx + row * a1 + (x0 + i) * a0;
+                        const uint2 kt = reinterpret_cast<const uint2 *>(dspt_warp)[64 + ((pos + 512) >> 10)];
+                        // taps sum to 128 and p ^ 0x80 == p - 128: sum = acc + 128 * 128
+                        m4[i] = (dot4(hi[i], kt.y, dot4(lo[i], kt.x, 16384 + hrnd))) >> hsh;
+                    }
+                } else {
+                    const u32x4a2 v0 = gld<u32x4a2>(s);
+                    const u32x2a2 v1 = gld<u32x2a2>(s + 8);
+                    const uint32_t e[6] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y};   // pixel pairs (2m, 2m+1)
+                    uint32_t o[5];
+#pragma unroll
+                    for (int i = 0; i < 5; i++) o[i] = alb(e[i + 1], e[i], 2);   // pairs (2m+1, 2m+2)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int pos = mx + row * a1 + (x0 + i) * a0;
+                        const uint2 kt = reinterpret_cast<const uint2 *>(dspt_warp)[64 + ((pos + 512) >> 10)];
+                        uint32_t tp[4];   // int8 taps -> int16 pairs
+#pragma unroll
+                        for (int m = 0; m < 4; m++) {
+                            const uint32_t src = m < 2 ? kt.x : kt.y;
+                            const int b0 = __builtin_amdgcn_sbfe((int)src, 16 * (m & 1), 8);
+                            const int b1 = __builtin_amdgcn_sbfe((int)src, 16 * (m & 1) + 8, 8);
+                            tp[m] = pack16(b0, b1);
+                        }
+                        const uint32_t *pp = (i & 1) ? o + (i >> 1) : e + (i >> 1);
+                        const int acc = dot2(pp[3], tp[3], dot2(pp[2], tp[2], dot2(pp[1], tp[1], dot2(pp[0], tp[0], 0))));
+                        m4[i] = (acc + hrnd) >> hsh;
+                    }
+                }
+                uint2 ov;
+                ov.x = pack16(m4[0], m4[1]);
+                ov.y = pack16(m4[2], m4[3]);
+                *reinterpret_cast<uint2 *>(mid + row * W + 4 * q) = ov;
+            }
+        }
+        wave_sync();
+#pragma unroll 1
+        for (int k = 0; k < (NVT + G - 1) / G; k++) {   // vertical + emit: 4x2 tasks of the strip
+            const int t = l + k * G;
+            if (t < NVT) {
+                const int j = t / QW, q = t % QW, x0 = (q & 1) * 4;
+                const u32x2 sb = gld<u32x2>(rec + 16 + 8 * (sy * NBX + (q >> 1)));
+                const int my = ((int)sb[1] >> 16) * 64;
+                // the 8 outputs' vertical taps, then the 9 mid rows streamed
+                // through the 8 accumulators (few live registers)
+                u32x2 kv[2][4];
+#pragma unroll
+                for (int rr = 0; rr < 2; rr++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int pos = my + (2 * j + rr) * a3 + (x0 + i) * a2;
+                        kv[rr][i] = reinterpret_cast<const u32x2 *>(dspt_warp)[64 + ((pos + 512) >> 10)];
+                    }
+                int sum[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+                for (int r = 0; r < 9; r++) {
+                    const uint2 v = *reinterpret_cast<const uint2 *>(mid + (2 * j + r) * W + 4 * q);
+                    const int m[4] = {(int16_t)(v.x & 0xffff), (int)v.x >> 16, (int16_t)(v.y & 0xffff), (int)v.y >> 16};
+#pragma unroll
+                    for (int rr = 0; rr < 2; rr++) {
+                        const int kk = r - rr;
+                        if (kk < 0 || kk > 7) continue;
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            sum[rr][i] += __builtin_amdgcn_sbfe((int)kv[rr][i][kk >> 2], 8 * (kk & 3), 8) * m[i];
+                    }
+                }
+                int pv[8];
+#pragma unroll
+                for (int rr = 0; rr < 2; rr++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        pv[4 * rr + i] = clampi((sum[rr][i] + ((1 << (7 + ib)) >> 1)) >> (7 + ib), 0, bdmax);
+                emit(4 * sy + j, q, pv);
+            }
+        }
+        wave_sync();
+    }
+}
+
 // ---------------------------------------------------------------- kernel --
 
-template <int BPC, int TX>
+template <int BPC, int TX, bool WARPK>
 __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
                                             int first, int count, uint8_t *wave_lds, int gw, int grp) {
     using CL = Cls<TX>;
@@ -916,7 +1045,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     Stage<CL::SW * CL::SH * (int)sizeof(C), G> cst;
     if (ncoef) cst.load(cf, ncoef * (int)sizeof(C), l);
     Stage<SL::EDGE * (int)sizeof(P), G> est;
-    const bool edged = pred == DGPU_PRED_INTRA || pred == DGPU_PRED_CFL;   // same edge_off in both views
+    constexpr bool NW = !WARPK;   // the warp launch compiles only the WARP prediction
+    const bool edged = NW && (pred == DGPU_PRED_INTRA || pred == DGPU_PRED_CFL);   // same edge_off in both views
     if (edged) est.load(a.edges + u.p.intra.edge_off - 2 * H, SL::EDGE * (int)sizeof(P), l);
 
     const int f2d = inter ? u.p.inter.filter2d : 0;
@@ -942,7 +1072,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         hp.compute(0, ib);
         hp.rest(ib);
     };
-    const bool do_mc = inter && !DGPU_ABL_MC;
+    const bool do_mc = NW && inter && !DGPU_ABL_MC;
     HPass<BPC, TX> hp0;
     if (do_mc) {
         hinit(hp0, 0);
@@ -957,7 +1087,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         hp1.load(0);
     }
     // INTER_MASK / PAL: the unit's aux_pool offset (mask / palette record)
-    const bool auxed = pred == DGPU_PRED_INTER_MASK || pred == DGPU_PRED_PAL;
+    const bool auxed = pred == DGPU_PRED_INTER_MASK || pred == DGPU_PRED_PAL || pred == DGPU_PRED_WARP;
     const int auxo = auxed ? a.aux[first + g] : 0;
     int cfsk = 0;
     if (ncoef) cfsk = cst.commit(cfl, l);
@@ -1105,7 +1235,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
     };
 
-    if (inter) {
+    if (NW && inter) {
         if (DGPU_ABL_MC) {
             int pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -1186,7 +1316,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                 emit(j, q, pv);
             }
         }
-    } else if (pred == DGPU_PRED_INTRA) {
+    } else if (NW && pred == DGPU_PRED_INTRA) {
         IntraState is{};
         if (!DGPU_ABL_INTRA) {
             is = intra_prep<BPC, TX>(u, tl, fe, l, bdmax);
@@ -1211,7 +1341,10 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             }
             emit(j, q, pv);
         }
-    } else if (pred == DGPU_PRED_PAL) {   // pal_pred (src/ipred_tmpl.c:717-730)
+    } else if (pred == DGPU_PRED_WARP) {   // only in the warp launch (its own register budget)
+        if constexpr (WARPK && W >= 8 && H >= 8)
+            warp_unit<BPC, TX, P>(a, pt, u, auxo, reinterpret_cast<int16_t *>(mid0), l, bdmax, emit);
+    } else if (NW && pred == DGPU_PRED_PAL) {   // pal_pred (src/ipred_tmpl.c:717-730)
         const uint8_t *rec = a.aux_pool + auxo;
         const u32x4 pal = gld<u32x4>(rec);   // 8 entries (u8 x 8 or u16 x 8)
 #pragma unroll
@@ -1235,9 +1368,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             }
             emit(j, q, pv);
         }
-    } else if (pred == DGPU_PRED_CFL) {
+    } else if (NW && pred == DGPU_PRED_CFL) {
         if constexpr (W == H && W <= 32) cfl_units<BPC, TX>(a, u, tl, fe, l, bdmax, emit);
-    } else {   // PRED_NONE: the residual goes onto the picture
+    } else if (NW) {   // PRED_NONE: the residual goes onto the picture
 #pragma unroll
         for (int k = 0; k < TPL; k++) {
             const int t = l + k * G;

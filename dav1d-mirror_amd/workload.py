@@ -89,6 +89,7 @@ class FrameData:
     dst_init: list = None         # starting picture planes ("itx" frames add onto them)
     aux: np.ndarray = None        # per-unit int32: aux_pool offset (INTER_MASK / PAL units)
     aux_pool: np.ndarray = None   # u8 pool: block masks, palette records
+    class_warp: np.ndarray = None # WARP units at the end of each class range
     stats: dict = field(default_factory=dict)
 
     @property
@@ -185,9 +186,9 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         # "full": put / avg / w_avg / mask compound and palette blocks
         rng.random(nb)   # keep the later draws aligned with "full"
         e = np.random.default_rng(cfg.seed ^ 0xE7E7).random(nb)
-        kind = np.select([e < 0.25, e < 0.40, e < 0.60, e < 0.80],
-                         [abi.PRED_INTER, abi.PRED_INTER_AVG, abi.PRED_INTER_WAVG, abi.PRED_INTER_MASK],
-                         abi.PRED_PAL)
+        kind = np.select([e < 0.20, e < 0.32, e < 0.48, e < 0.64, e < 0.82],
+                         [abi.PRED_INTER, abi.PRED_INTER_AVG, abi.PRED_INTER_WAVG, abi.PRED_INTER_MASK,
+                          abi.PRED_PAL], abi.PRED_WARP)
     elif cfg.kind in ("ipred", "itx"):
         rng.random(nb)   # keep the later draws aligned with "full"
         kind = np.full(nb, abi.PRED_INTRA if cfg.kind == "ipred" else abi.PRED_NONE)
@@ -220,6 +221,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
                 tw = th = min(s, cfg.mc_split)
             else:
                 cands = _tx_candidates(s, cfg.tx64)
+                if kind[b] == abi.PRED_WARP and plane == 0:   # warp units are whole 8x8s
+                    cands = [c for c in cands if min(c) >= 8]
                 tw, th = cands[(b * 7 + plane * 3 + int(rng.integers(0, 1 << 20))) % len(cands)]
                 if plane > 0 and cfl_blk[b]:
                     tw = th = s   # CfL predicts the whole chroma block (<= 32x32)
@@ -249,6 +252,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     units["tx"] = tx
     units["plane"] = plane_u
     pk = kind[blk].copy()
+    pk[(pk == abi.PRED_WARP) & (plane_u > 0)] = abi.PRED_INTER   # chroma of warped blocks: translation
     cfl = (plane_u > 0) & cfl_blk[blk]
     pk[cfl] = abi.PRED_CFL
     units["pred"] = pk
@@ -306,6 +310,33 @@ def make_frame(cfg: FrameConfig) -> FrameData:
             aux[i] = off
             chunks.append(rec)
             off += len(rec)
+        # WARP: per unit abcd[4] (int16), 8 pad bytes, then per 8x8 of the
+        # unit int32 src_off, int16 mx >> 6, int16 my >> 6 (warp_affine,
+        # src/recon_tmpl.c:1063-1100, with shear parameters within +-1024)
+        wb = np.nonzero(pk == abi.PRED_WARP)[0]
+        babcd = xr.integers(-1024, 1025, size=(nb, 4)).astype(np.int16)
+        for i in wb:
+            w_, h_ = int(tw[i]), int(th[i])
+            a_ = babcd[blk[i]]
+            rec = np.zeros(16 + 8 * (w_ // 8) * (h_ // 8), np.uint8)
+            rec[:8] = a_.view(np.uint8)
+            mvx, mvy = int(mv[blk[i], 0, 0]) >> 4, int(mv[blk[i], 0, 1]) >> 4
+            sub = np.zeros((h_ // 8) * (w_ // 8), dtype=[("off", "<i4"), ("mx", "<i2"), ("my", "<i2")])
+            k_ = 0
+            for sy in range(h_ // 8):
+                for sx in range(w_ // 8):
+                    x_ = int(ux[i]) + 8 * sx + mvx + int(xr.integers(-2, 3))
+                    y_ = int(uy[i]) + 8 * sy + mvy + int(xr.integers(-2, 3))
+                    sub["off"][k_] = y_ * int(ref_stride[0]) + x_
+                    mx_ = (int(xr.integers(0, 65536)) - 4 * int(a_[0]) - 7 * int(a_[1])) & ~63
+                    my_ = (int(xr.integers(0, 65536)) - 4 * int(a_[2]) - 4 * int(a_[3])) & ~63
+                    sub["mx"][k_], sub["my"][k_] = mx_ >> 6, my_ >> 6
+                    k_ += 1
+            rec[16:] = sub.view(np.uint8)
+            aux[i] = off
+            chunks.append(rec)
+            off += len(rec) + (-len(rec)) % 16
+            chunks.append(np.zeros((-len(rec)) % 16, np.uint8))
         aux_pool = np.concatenate(chunks) if chunks else np.zeros(16, np.uint8)
 
     # intra parameters
@@ -417,10 +448,14 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         keys = (pos, blk, minor, units["pred"], band, units["tx"])
     else:
         keys = (minor, units["pred"], band, units["tx"])
-    order = np.lexsort(keys)
+    # WARP units go last inside their class (the batch's class_warp ranges,
+    # run by the warp launch)
+    is_warp = units["pred"] == abi.PRED_WARP
+    order = np.lexsort(keys[:-1] + (is_warp, units["tx"]))
     units = units[order]
     counts = np.bincount(units["tx"], minlength=abi.N_TX)
     class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    class_warp = np.bincount(units["tx"][units["pred"] == abi.PRED_WARP], minlength=abi.N_TX).astype(np.int32)
 
     dst_init = None
     if cfg.kind == "itx":   # a picture for the residual to land on (own stream)
@@ -428,7 +463,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         dst_init = [drng.integers(0, bdmax + 1, size=(ph_, pw_), dtype=cfg.pixel_dtype) for (pw_, ph_) in planes]
     fd = FrameData(cfg=cfg, units=units, class_start=class_start, coefs=coefs, edges=edges,
                    refs=refs, plane_wh=planes, blk=(blk * 3 + plane_u)[order], cfl_luma=cfl_luma,
-                   dst_init=dst_init, aux=None if aux is None else aux[order], aux_pool=aux_pool)
+                   dst_init=dst_init, aux=None if aux is None else aux[order], aux_pool=aux_pool,
+                   class_warp=class_warp)
     fd.stats = algorithmic_bytes(fd)
     return fd
 
@@ -467,6 +503,9 @@ def algorithmic_bytes(fd: FrameData):
     aux_bytes = int((w * h)[u["pred"] == abi.PRED_INTER_MASK].sum())
     pal = u["pred"] == abi.PRED_PAL
     aux_bytes += int((w * h // 2)[pal].sum()) + int(pal.sum()) * 8 * bpp
+    warp = u["pred"] == abi.PRED_WARP   # warp8x8: a 15x15 footprint per 8x8 + its parameters
+    src = src + np.where(warp, (w // 8) * (h // 8) * 225, 0)
+    aux_bytes += int(((w // 8) * (h // 8) * 8 + 16)[warp].sum())
     ncoef = np.where(u["txtp"] == abi.NO_RESIDUAL, 0, np.where(u["nzw"] == 0, 1,
                      u["nzw"].astype(np.int64) * u["nzh"]))
     out_px = int((w * h).sum())
@@ -488,5 +527,6 @@ def algorithmic_bytes(fd: FrameData):
         "n_cfl": int(cfl.sum()),
         "n_inter": int(inter.sum()),
         "n_pal": int(pal.sum()),
+        "n_warp": int(warp.sum()),
         "n_nopred": int(nopred.sum()),
     }

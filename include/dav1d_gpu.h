@@ -223,6 +223,15 @@ enum Dav1dGpuPredKind {
                                 followed by the unit's packed index map
                                 (two 4-bit indices per byte, low nibble
                                 first, row stride w / 2)                     */
+    DGPU_PRED_WARP = 8,      /* warp8x8 from p.inter.ref[0] for every 8x8 of
+                                the unit (unit w, h multiples of 8;
+                                src/mc_tmpl.c:758-791, recon_tmpl.c:1063-1100
+                                warp_affine).  aux[unit] = byte offset of a
+                                16-byte aligned record: int16 abcd[4], 8 pad
+                                bytes, then per 8x8 (row-major) int32 src_off
+                                (the warp source position in the ref plane),
+                                int16 mx >> 6, int16 my >> 6 (warp_affine
+                                clears their low 6 bits, :1085-1090)         */
 };
 
 /* txtp value of a prediction-only unit (no inv_txfm_add): mc-only batches */
@@ -309,6 +318,11 @@ typedef struct Dav1dGpuFrameBatch {
                              mask or a PAL unit's palette record; only those
                              kinds read it (may be NULL without them)      */
     const void *aux_pool; /* device pool of masks (u8) / palette records   */
+    int32_t  class_warp[DGPU_N_RECT_TX_SIZES]; /* WARP units at the end of
+                             each class range (units sorted so); they run in
+                             their own launch with the warp kernel, which
+                             keeps warp's registers out of the main kernel.
+                             Classes with a side < 8 must have none         */
 } Dav1dGpuFrameBatch;
 
 /* Launch one frame batch on `stream` (a hipStream_t, NULL = default).

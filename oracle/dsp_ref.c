@@ -1464,6 +1464,25 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
                     for (int x = 0; x < w; x++) m[y * w + x] = ms[y * (u->bw4 * 4) + x];
                 avg_blend(dst, ds, t1, t2, w, h, 2, 0, m, bdmax);
             }
+        } else if (u->pred == DGPU_PRED_WARP) {
+            /* recon_tmpl.c warp_affine (:1063-1100): warp8x8 for each 8x8 of
+             * the unit with its own source position and mx / my */
+            const uint8_t *rec = (const uint8_t *)b->aux_pool + b->aux[i];
+            int16_t abcd[4];
+            memcpy(abcd, rec, 8);
+            const int r = u->p.inter.ref[0];
+            const ptrdiff_t ss = b->ref[r][pl].stride;
+            for (int sy = 0; sy < h / 8; sy++)
+                for (int sx = 0; sx < w / 8; sx++) {
+                    const uint8_t *sb = rec + 16 + 8 * (sy * (w / 8) + sx);
+                    int32_t soff;
+                    int16_t mxy[2];
+                    memcpy(&soff, sb, 4);
+                    memcpy(mxy, sb + 4, 4);
+                    const pixel *src = (const pixel *)b->ref[r][pl].data + soff;
+                    warp8x8(dst + 8 * sy * PX(ds) + 8 * sx, ds, NULL, 0, src, ss, abcd, mxy[0] * 64, mxy[1] * 64,
+                            bdmax);
+                }
         } else if (u->pred == DGPU_PRED_PAL) {
             /* pal_pred on the unit (pointwise, so the unit's part of the
              * block's call): 8 entries at the record start, then the packed

@@ -85,6 +85,9 @@ class HostFrame:
             self.aux_pool = np.ascontiguousarray(fd.aux_pool, dtype=np.uint8)
             b.aux = self.aux.ctypes.data
             b.aux_pool = self.aux_pool.ctypes.data
+        if getattr(fd, "class_warp", None) is not None:
+            for i in range(abi.N_TX):
+                b.class_warp[i] = int(fd.class_warp[i])
         self.batch = b
 
     def run(self, u0=0, u1=None, threads=1):
