@@ -108,23 +108,17 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     // Every kernel argument of the prologue by constant index, pinned in
     // SGPRs at the top (the empty asm uses them), so the scalar loads go out
     // as one batch with one wait instead of a chain of dependent waits.
-    int wpre[NC + 1], wps[NC], cs[NC + 1];
+    int wpre[NC + 1];
 #pragma unroll
-    for (int c = 0; c <= NC; c++) {
-        wpre[c] = a.wpre[c];
-        cs[c] = a.class_start[c];
-        if (c < NC) wps[c] = a.wps[c];
-    }
+    for (int c = 0; c <= NC; c++) wpre[c] = a.wpre[c];
     using P = typename Px<BPC>::pixel;
     const int nwaves = a.nwaves;
     const Dav1dGpuUnit *units = a.units;
     asm volatile("" ::"s"(nwaves), "s"(units));
 #pragma unroll
     for (int c = 0; c <= NC; c += 4)
-        asm volatile("" ::"s"(wpre[c]), "s"(cs[c]), "s"(wps[c < NC ? c : 0]), "s"(wpre[cmin(c + 1, NC)]),
-                     "s"(cs[cmin(c + 1, NC)]), "s"(wps[cmin(c + 1, NC - 1)]), "s"(wpre[cmin(c + 2, NC)]),
-                     "s"(cs[cmin(c + 2, NC)]), "s"(wps[cmin(c + 2, NC - 1)]), "s"(wpre[cmin(c + 3, NC)]),
-                     "s"(cs[cmin(c + 3, NC)]), "s"(wps[cmin(c + 3, NC - 1)]));
+        asm volatile("" ::"s"(wpre[c]), "s"(wpre[cmin(c + 1, NC)]), "s"(wpre[cmin(c + 2, NC)]),
+                     "s"(wpre[cmin(c + 3, NC)]));
     if (gw >= nwaves) return;
     // (segment, class) of this wave from the per-segment wave prefix
     // schedule: (segment group, class position, segment in group); a group
@@ -132,19 +126,18 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     constexpr int SL = kSegInner;
     const int wgrp = wpre[NC] * SL;
     const int sg = gw / wgrp, r = gw - sg * wgrp;
-    int pos = 0, wpre_p = 0, wp = wps[0];   // schedule position inside the group (kOrder)
+    int pos = 0, wpre_p = 0;   // schedule position inside the group (kOrder)
 #pragma unroll
     for (int c = 1; c < NC; c++) {
         const bool ge = r >= wpre[c] * SL;
         pos = ge ? c : pos;
         wpre_p = ge ? wpre[c] : wpre_p;
-        wp = ge ? wps[c] : wp;
     }
     const int cls = order_class(pos);
-    int cs0 = cs[0];   // the class's range start by selects; its end by one scalar load
-#pragma unroll
-    for (int c = 1; c < NC; c++) cs0 = cls == c ? cs[c] : cs0;
-    const int cs1 = a.class_end[cls];
+    // the position's wave count and the class's unit range: three scalar
+    // loads in one round trip (holding every class's values in SGPRs made
+    // the compiler re-load them, measured slower)
+    const int wp = a.wps[pos], cs0 = a.class_start[cls], cs1 = a.class_end[cls];
     const int lg = (int)((kLog2Lanes >> (3 * cls)) & 7);   // log2 lanes per unit, no table load
     const int U = 64 >> lg;
     const int r2 = r - wpre_p * SL;
