@@ -22,15 +22,6 @@
 
 namespace dgpu {
 
-template <int BPC, int GRP, int... TX>
-__host__ __device__ constexpr int group_wave_lds(std::integer_sequence<int, TX...>) {
-    int m = 0;
-    ((m = (in_group(TX, GRP) && Slot<BPC, TX>::WAVE > m) ? Slot<BPC, TX>::WAVE : m), ...);
-    return m;
-}
-template <int BPC, int GRP> __host__ __device__ constexpr int wave_lds() {
-    return group_wave_lds<BPC, GRP>(std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
-}
 
 // waves per workgroup: waves never share LDS, so small workgroups only
 // serve to pack the CU's LDS tightly (one wave for the 64-point classes)
@@ -179,6 +170,11 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
             tr[13] = t_entry;
             tr[14] = t_sched;
         }
+    }
+    if constexpr (GRP == GROUP_WARP) {   // the warp filter table in this wave's LDS (after its slots)
+        uint2 *wt = reinterpret_cast<uint2 *>(lds + wave * WL + kWarpTabOff<BPC>);
+        for (int i = threadIdx.x & 63; i < 193; i += 64) wt[i] = reinterpret_cast<const uint2 *>(dspt_warp)[i];
+        wave_sync();
     }
     dispatch<BPC, GRP>(a, pt, u, cls, first, count, lds + wave * WL, gw);
 }

@@ -32,6 +32,8 @@
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
 
+#include <utility>
+
 // Profiling-only phase ablations (tools/build_variants.sh); all 0 in the
 // product build.  Outputs are wrong when any is set.
 #ifndef DGPU_ABL_MC
@@ -204,6 +206,21 @@ template <int BPC, int TX> struct Slot {
     static constexpr int BYTES = CFR + TMP + SRC;
     static constexpr int WAVE = CL::U * BYTES;
 };
+
+// LDS bytes per wave of a launch group: its largest class slot set; the warp
+// launch adds its copy of the warp filter table (193 x 8 int8) after that
+template <int BPC, int GRP, int... TX>
+__host__ __device__ constexpr int group_wave_lds(std::integer_sequence<int, TX...>) {
+    int m = 0;
+    ((m = (in_group(TX, GRP) && Slot<BPC, TX>::WAVE > m) ? Slot<BPC, TX>::WAVE : m), ...);
+    return m;
+}
+template <int BPC> inline constexpr int kWarpTabOff =
+    group_wave_lds<BPC, GROUP_WARP>(std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
+template <int BPC, int GRP> __host__ __device__ constexpr int wave_lds() {
+    return group_wave_lds<BPC, GRP>(std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>()) +
+           (GRP == GROUP_WARP ? 193 * 8 + 8 : 0);
+}
 
 // ------------------------------------------------------------ primitives ---
 
@@ -871,7 +888,7 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
 // output from it and is emitted (+ residual) like every other prediction.
 template <int BPC, int TX, typename P, typename Emit>
 __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
-                                          int auxo, int16_t *mid, int l, int bdmax, Emit &emit) {
+                                          int auxo, int16_t *mid, const uint2 *wtab, int l, int bdmax, Emit &emit) {
     using CL = Cls<TX>;
     constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NBX = W / 8;
     const uint8_t *rec = a.aux_pool + auxo;
@@ -886,18 +903,40 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
     constexpr int NHT = 15 * QW, NVT = 4 * QW;
 #pragma unroll 1
     for (int sy = 0; sy < H / 8; sy++) {
-#pragma unroll 1
-        for (int k = 0; k < (NHT + G - 1) / G; k++) {   // horizontal: (row, quad) tasks
+        // horizontal: (row, quad) tasks; every task's source row and
+        // parameters are loaded first (all in flight together), then computed
+        constexpr int KH = (NHT + G - 1) / G;
+        using Raw = typename std::conditional<BPC == 8, u32x4, u32x4a2>::type;
+        Raw raw[KH];
+        u32x2a2 raw2[KH];   // 16bpc: pixels 8..11
+        int mxs[KH];
+        unsigned shs[KH];
+#pragma unroll
+        for (int k = 0; k < KH; k++) {
+            const int t = cmin(l + k * G, NHT - 1);   // clamped: loads stay inside the footprint
+            const int row = t / QW, q = t % QW, x0 = (q & 1) * 4;
+            const u32x2 sb = gld<u32x2>(rec + 16 + 8 * (sy * NBX + (q >> 1)));
+            mxs[k] = (int)(int16_t)(sb[1] & 0xffff) * 64;
+            const P *s = ref + (int)sb[0] + (row - 3) * rs + x0 - 3;   // columns x0-3 .. x0+7
+            if constexpr (BPC == 8) {
+                shs[k] = (unsigned)reinterpret_cast<uintptr_t>(s) & 3u;
+                raw[k] = gld<u32x4>(reinterpret_cast<const uint8_t *>(s) - shs[k]);
+            } else {
+                shs[k] = 0;
+                raw[k] = gld<u32x4a2>(s);
+                raw2[k] = gld<u32x2a2>(s + 8);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KH; k++) {
             const int t = l + k * G;
             if (t < NHT) {
                 const int row = t / QW, q = t % QW, x0 = (q & 1) * 4;
-                const u32x2 sb = gld<u32x2>(rec + 16 + 8 * (sy * NBX + (q >> 1)));
-                const int mx = (int)(int16_t)(sb[1] & 0xffff) * 64;
-                const P *s = ref + (int)sb[0] + (row - 3) * rs + x0 - 3;   // columns x0-3 .. x0+7
+                const int mx = mxs[k];
                 int m4[4];
                 if constexpr (BPC == 8) {
-                    const unsigned sh = (unsigned)reinterpret_cast<uintptr_t>(s) & 3u;
-                    const u32x4 d = gld<u32x4>(reinterpret_cast<const uint8_t *>(s) - sh);
+                    const u32x4 d = raw[k];
+                    const unsigned sh = shs[k];
                     const uint32_t w0 = alb(d[1], d[0], sh) ^ 0x80808080u, w1 = alb(d[2], d[1], sh) ^ 0x80808080u,
                                    w2 = alb(d[3], d[2], sh) ^ 0x80808080u;
                     const uint32_t lo[4] = {w0, alb(w1, w0, 1), alb(w1, w0, 2), alb(w1, w0, 3)};
@@ -905,21 +944,19 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         const int pos = mx + row * a1 + (x0 + i) * a0;
-                        const uint2 kt = reinterpret_cast<const uint2 *>(dspt_warp)[64 + ((pos + 512) >> 10)];
+                        const uint2 kt = wtab[64 + ((pos + 512) >> 10)];
                         // taps sum to 128 and p ^ 0x80 == p - 128: sum = acc + 128 * 128
                         m4[i] = (dot4(hi[i], kt.y, dot4(lo[i], kt.x, 16384 + hrnd))) >> hsh;
                     }
                 } else {
-                    const u32x4a2 v0 = gld<u32x4a2>(s);
-                    const u32x2a2 v1 = gld<u32x2a2>(s + 8);
-                    const uint32_t e[6] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y};   // pixel pairs (2m, 2m+1)
+                    const uint32_t e[6] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w, raw2[k].x, raw2[k].y};
                     uint32_t o[5];
 #pragma unroll
                     for (int i = 0; i < 5; i++) o[i] = alb(e[i + 1], e[i], 2);   // pairs (2m+1, 2m+2)
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         const int pos = mx + row * a1 + (x0 + i) * a0;
-                        const uint2 kt = reinterpret_cast<const uint2 *>(dspt_warp)[64 + ((pos + 512) >> 10)];
+                        const uint2 kt = wtab[64 + ((pos + 512) >> 10)];
                         uint32_t tp[4];   // int8 taps -> int16 pairs
 #pragma unroll
                         for (int m = 0; m < 4; m++) {
@@ -955,7 +992,8 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         const int pos = my + (2 * j + rr) * a3 + (x0 + i) * a2;
-                        kv[rr][i] = reinterpret_cast<const u32x2 *>(dspt_warp)[64 + ((pos + 512) >> 10)];
+                        const uint2 t2 = wtab[64 + ((pos + 512) >> 10)];
+                        kv[rr][i] = u32x2{t2.x, t2.y};
                     }
                 int sum[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
@@ -1343,7 +1381,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
     } else if (pred == DGPU_PRED_WARP) {   // only in the warp launch (its own register budget)
         if constexpr (WARPK && W >= 8 && H >= 8)
-            warp_unit<BPC, TX, P>(a, pt, u, auxo, reinterpret_cast<int16_t *>(mid0), l, bdmax, emit);
+            warp_unit<BPC, TX, P>(a, pt, u, auxo, reinterpret_cast<int16_t *>(mid0),
+                                  reinterpret_cast<const uint2 *>(wave_lds + kWarpTabOff<BPC>), l, bdmax, emit);
     } else if (NW && pred == DGPU_PRED_PAL) {   // pal_pred (src/ipred_tmpl.c:717-730)
         const uint8_t *rec = a.aux_pool + auxo;
         const u32x4 pal = gld<u32x4>(rec);   // 8 entries (u8 x 8 or u16 x 8)
@@ -1383,7 +1422,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
     }
     mark(8);
-#if defined(DGPU_PAD_SALU) || defined(DGPU_PAD_VALU) || defined(DGPU_PAD_VMEM)   // cost-model probes (tools/build_variants.sh)
+#if defined(DGPU_PAD_SALU) || defined(DGPU_PAD_VALU) || defined(DGPU_PAD_VMEM) || defined(DGPU_PAD_VMEM1)   // cost-model probes (tools/build_variants.sh)
     {
         int p0 = first, p1 = count, p2 = gw, p3 = grp;
 #ifdef DGPU_PAD_SALU
@@ -1403,6 +1442,11 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #pragma unroll
         for (int i = 0; i < DGPU_PAD_VMEM; i++)
             v0 += gld<int>(pt.ref[0] + ((uint32_t)(u.dst_off * 7 + lane * 4099 + i * 131) % (1u << 22)));
+#endif
+#ifdef DGPU_PAD_VMEM1   // the same line for every lane: the per-instruction floor
+#pragma unroll
+        for (int i = 0; i < DGPU_PAD_VMEM1; i++)
+            v0 += gld<int>(pt.ref[0] + 4 * (lane & 15) + 64 * i);
 #endif
         asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(p3), "v"(v0), "v"(v1), "v"(v2), "v"(v3));
     }

@@ -23,7 +23,10 @@ build() {
 for v in ${VARIANTS:-nomc noitx nointra}; do
     case $v in
         salu200) build salu200 -DDGPU_PAD_SALU=200 ;;
+        al16) build al16 -DDGPU_ALIGNED_ROWS16=1 ;;
+        ch16) build ch16 -DDGPU_CH16=1 ;;
         vmem8) build vmem8 -DDGPU_PAD_VMEM=8 ;;
+        vmem1x8) build vmem1x8 -DDGPU_PAD_VMEM1=8 ;;
         fakecoal) build fakecoal -DDGPU_FAKE_COALESCE=1 ;;
         valu200) build valu200 -DDGPU_PAD_VALU=200 ;;
         nomc) build nomc -DDGPU_ABL_MC=1 ;;
