@@ -330,9 +330,11 @@ typedef struct Dav1dGpuFrameBatch {
 int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream);
 int dav1d_gpu_recon_16bpc(const Dav1dGpuFrameBatch *b, void *stream);
 
-/* LDS bytes per 256-thread workgroup of a batch kernel (bpc 8/16; group 0:
- * transform sizes with w*h <= 128, 1: larger up to 32x32, 2: a 64-point
- * side).  Diagnostics. */
+/* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
+ * kernel, every size up to 32x32; 1: the large sizes when built with split
+ * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).
+ * Diagnostics.  Errors of dav1d_gpu_recon_*: -1 NULL batch / units, -2 bad
+ * class_start / class_warp ranges, -3 launch failure, -4 misaligned planes. */
 int dav1d_gpu_recon_lds_bytes(int bpc, int group);
 
 #ifdef __cplusplus

@@ -35,6 +35,44 @@ def test_abi_struct_sizes(pkg):
     assert fb.units.offset == 27 * 24
 
 
+def test_recon_batch_validation(pkg):
+    """dav1d_gpu_recon_* reject malformed batches before touching a device
+    (no GPU needed): NULL, non-monotonic class ranges, WARP ranges in classes
+    narrower than 8 or longer than the class, misaligned output planes; an
+    empty batch is a no-op."""
+    abi = pkg.abi
+    L = abi.load_lib()
+    assert L.dav1d_gpu_recon_8bpc(None, None) == -1
+
+    def batch(n):
+        b = abi.FrameBatch()
+        b.units = 64          # never dereferenced on these paths
+        b.n_units = n
+        for i in range(abi.N_TX + 1):
+            b.class_start[i] = 0 if i <= 1 else n   # all units in class 1 (8x8)
+        return b
+
+    for fn in (L.dav1d_gpu_recon_8bpc, L.dav1d_gpu_recon_16bpc):
+        assert fn(ctypes.byref(batch(0)), None) == 0
+        b = batch(5)
+        b.class_start[3] = 2   # not monotonic
+        assert fn(ctypes.byref(b), None) == -2
+        b = batch(5)
+        b.class_start[abi.N_TX] = 4   # last bound != n_units
+        assert fn(ctypes.byref(b), None) == -2
+        b = batch(5)
+        b.class_warp[0] = 1   # 4x4 cannot hold WARP units
+        assert fn(ctypes.byref(b), None) == -2
+        b = batch(5)
+        b.class_warp[1] = 6   # more WARP units than the class has
+        assert fn(ctypes.byref(b), None) == -2
+        b = batch(5)
+        b.dst[0].data = 8     # not 16-byte aligned
+        assert fn(ctypes.byref(b), None) == -4
+    assert L.dav1d_gpu_recon_lds_bytes(8, 3) > L.dav1d_gpu_recon_lds_bytes(8, 2) - 65536
+    assert L.dav1d_gpu_recon_lds_bytes(8, 9) == -1
+
+
 def test_itx_table_matches_reference_count(pkg, oracle):
     L = oracle.load()
     for bpc in (8, 16):

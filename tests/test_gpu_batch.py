@@ -132,3 +132,30 @@ def test_batch_family(pkg, oracle, kind, bpc, bdmax):
 def test_batch_ext_tx64(pkg, oracle):
     """w_avg / mask / palette units in the 64-point class group too."""
     _check(_frame(pkg, width=512, height=256, kind="ext", tx64=True, seed=22), oracle)
+
+
+@pytest.mark.parametrize("kind", ["full", "ext"])
+def test_batch_ragged_subsets(pkg, oracle, kind):
+    """Ragged batches: random subsets of a frame's units (untouched pixels
+    stay as they were), one unit per class, and classes left empty."""
+    import dav1d_mirror_amd.workload as wl
+    fd = _frame(pkg, width=512, height=256, kind=kind, seed=31)
+    rng = np.random.default_rng(7)
+    for keep_p in (0.5, 0.03, None):
+        u = fd.units
+        if keep_p is None:   # the first unit of every class only
+            keep = np.zeros(len(u), bool)
+            keep[fd.class_start[:-1][np.diff(fd.class_start) > 0]] = True
+        else:
+            keep = rng.random(len(u)) < keep_p
+        sub = wl.FrameData(**{k: getattr(fd, k) for k in fd.__dataclass_fields__})
+        sub.units = u[keep]
+        if fd.aux is not None:
+            sub.aux = fd.aux[keep]
+        sub.class_start = np.concatenate([[0], np.cumsum(np.bincount(sub.units["tx"], minlength=19))]).astype(np.int32)
+        if fd.class_warp is not None:
+            sub.class_warp = np.bincount(sub.units["tx"][sub.units["pred"] == pkg.abi.PRED_WARP],
+                                         minlength=19).astype(np.int32)
+        sub.blk = fd.blk[keep]
+        sub.stats = wl.algorithmic_bytes(sub)
+        _check(sub, oracle)
