@@ -51,6 +51,12 @@
 #ifndef DGPU_TRACE
 #define DGPU_TRACE 0       // per-wave phase timestamps (tools/wave_trace.py)
 #endif
+#ifndef DGPU_ROWSKIP
+// skip footprint rows no vertical tap reads (HPass::load): measured slower
+// at both bitdepths (60 -> 63 us 8-bit with a 20 B/lane spill, 83.5 -> 86
+// us 10-bit), so off; kept as a knob
+#define DGPU_ROWSKIP 0
+#endif
 #ifndef DGPU_ALIGNED_ROWS8
 #define DGPU_ALIGNED_ROWS8 1    // 8bpc footprint rows by aligned loads + v_alignbyte (see HPass)
 #endif
@@ -666,8 +672,11 @@ template <int BPC, int TX> struct HPass {
     int p0;
     uint4 th;            // taps: 8bpc .x/.y int8 x4, 16bpc int16 pairs
 
+    int rlo, rhi;        // footprint rows the vertical taps read (others are not loaded)
     __device__ __forceinline__ void init(const typename Px<BPC>::pixel *org, int stride_px, uint32_t *mid, int bank,
-                                         int m, int l) {
+                                         int m, int l, int rlo_, int rhi_) {
+        rlo = rlo_;
+        rhi = rhi_;
         sb = (unsigned)stride_px * B;
         const int q = l % QW;
         p0 = l / QW;
@@ -688,7 +697,14 @@ template <int BPC, int TX> struct HPass {
     __device__ __forceinline__ void load(int k0) {
 #pragma unroll
         for (int c = 0; c < CH; c++) {   // clamped: the loads stay inside the footprint
-            const int p = cmin(p0 + (k0 + c) * PS, RP - 1);
+            const int pu = p0 + (k0 + c) * PS;
+            const int p = cmin(pu, RP - 1);
+            // a row is loaded only when its task exists and a vertical tap
+            // reads it (4-tap and bilinear banks, m == 0, the unused row
+            // H+7): skipped rows are zero, and meet zero taps
+            const bool task = k0 + c < IT && pu < RP;
+            const bool n0 = !DGPU_ROWSKIP || (task && 2 * p >= rlo && 2 * p <= rhi);
+            const bool n1 = !DGPU_ROWSKIP || (task && 2 * p + 1 >= rlo && 2 * p + 1 <= rhi);
             const uint8_t *a0 = rp + (size_t)((unsigned)(p - p0) * 2u * sb);
             // row 2p+1 == H+7 (last pair) is never used: re-read row 2p
             const uint8_t *a1 = 2 * p + 1 < H + 7 ? a0 + sb : a0;
@@ -704,12 +720,28 @@ template <int BPC, int TX> struct HPass {
             }
             a1 = a0;
 #endif
+#ifndef DGPU_FAKE_COALESCE
+            // zero first, then an exec-masked load into the same registers
+            ra[c][0] = Raw{};
+            ra[c][1] = Raw{};
+            if (n0) ra[c][0] = gld<Raw>(a0);
+            if (n1) ra[c][1] = gld<Raw>(a1);
+            if constexpr (BPC == 16) {
+                rb[c][0] = RawB{};
+                rb[c][1] = RawB{};
+                if (n0) rb[c][0] = gld<RawB>(a0 + 16);
+                if (n1) rb[c][1] = gld<RawB>(a1 + 16);
+            }
+#else
+            (void)n0;
+            (void)n1;
             ra[c][0] = gld<Raw>(a0);
             ra[c][1] = gld<Raw>(a1);
             if constexpr (BPC == 16) {
                 rb[c][0] = gld<RawB>(a0 + 16);
                 rb[c][1] = gld<RawB>(a1 + 16);
             }
+#endif
         }
     }
     __device__ __forceinline__ void compute(int k0, int ib) {
@@ -1101,7 +1133,12 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         const int r = k ? u.p.inter.ref[1] : u.p.inter.ref[0];
         const int rs = pt.ref_stride[r * 3 + plane];
         const P *org = pt.ref[r * 3 + plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
-        hp.init(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], l);
+        // footprint rows the vertical taps read: m == 0 is the identity (tap
+        // 3), bilinear taps 3..4, the 4-tap banks 2..5, 8-tap 0..7
+        const int my = k ? u.p.inter.my[1] : u.p.inter.my[0];
+        const int tf = my == 0 ? 3 : bil ? 3 : bank_v >= 3 ? 2 : 0;
+        const int tl = my == 0 ? 3 : bil ? 4 : bank_v >= 3 ? 5 : 7;
+        hp.init(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], l, tf, H - 1 + tl);
     };
     auto hpass = [&](int k) {   // the whole h-pass of ref k
         HPass<BPC, TX> hp;

@@ -47,6 +47,9 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         merge5) build merge5 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=5 ;;
         merge4) build merge4 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=1 ;;
         merge6) build merge6 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=6 ;;
+        seg8) build seg8 -DDGPU_SEGMENTS=8 ;;
+        noskip) build noskip -DDGPU_ROWSKIP=0 ;;
+        seg32) build seg32 -DDGPU_SEGMENTS=32 ;;
         m5seg8) build m5seg8 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=5 -DDGPU_SEGMENTS=8 ;;
         m5seg32) build m5seg32 -DDGPU_MERGE_GROUPS=1 -DDGPU_WPE_SMALL8=5 -DDGPU_SEGMENTS=32 ;;
     esac
