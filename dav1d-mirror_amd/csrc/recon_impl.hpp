@@ -254,7 +254,7 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     a.aux_pool = (const uint8_t *)b->aux_pool;
     for (int c = 0; c < DGPU_N_RECT_TX_SIZES; c++) {   // WARP sub-ranges: classes with both sides >= 8
         const int nw = b->class_warp[c];
-        if (nw < 0 || nw > b->class_start[c + 1] - b->class_start[c] || (nw && !in_group(c, GROUP_WARP))) return -2;
+        if (nw < 0 || nw > b->class_start[c + 1] - b->class_start[c] || (nw && !in_group(c, GROUP_WARP))) return -2;   // no 64-point class
     }
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;

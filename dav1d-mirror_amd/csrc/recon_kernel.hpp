@@ -171,7 +171,7 @@ __device__ __forceinline__ int order_class(int k) {   // kOrder[k] without a mem
 // classes a launch of group GRP runs: the warp launch takes every class with
 // both sides >= 8 (its units are the WARP sub-ranges), the others by size
 __host__ __device__ constexpr bool in_group(int tx, int grp) {
-    return grp == GROUP_WARP ? (tx_info(tx).w >= 8 && tx_info(tx).h >= 8) : class_group(tx) == grp;
+    return grp == GROUP_WARP ? class_group(tx) != GROUP_HUGE : class_group(tx) == grp;
 }
 
 template <int TX> struct Cls {
@@ -1098,7 +1098,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     const int ib = Px<BPC>::ibits(bdmax);
     const int pred = u.pred;
     const bool comp = pred == DGPU_PRED_INTER_AVG || pred == DGPU_PRED_INTER_WAVG || pred == DGPU_PRED_INTER_MASK;
-    const bool inter = pred == DGPU_PRED_INTER || comp;
+    const bool ii = WARPK && pred == DGPU_PRED_INTER_INTRA;   // second launch only
+    const bool inter = pred == DGPU_PRED_INTER || comp || ii;
     const int txtp = u.txtp;
     const bool nores = txtp == DGPU_NO_RESIDUAL;
     const int nzw = u.nzw, nzh = u.nzh;
@@ -1119,7 +1120,11 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     const bool edged = NW && (pred == DGPU_PRED_INTRA || pred == DGPU_PRED_CFL);   // same edge_off in both views
     if (edged) est.load(a.edges + u.p.intra.edge_off - 2 * H, SL::EDGE * (int)sizeof(P), l);
 
-    const int f2d = inter ? u.p.inter.filter2d : 0;
+    // read for every unit (only inter kinds use it; the bank math below stays
+    // in range for any byte).  Selecting it on `inter` gave inter-intra units
+    // Filter2d 0 in the second launch's kernel (measured on MI355X, cause
+    // not isolated), so no select.
+    const int f2d = u.p.inter.filter2d;
     const bool bil = f2d == DGPU_FILTER_2D_BILINEAR;
     // filter_type = type_h | type_v << 2 per Filter2d (src/mc_tmpl.c:376-384)
     const int ftype = bil ? 0 : (int)((0x951a62840ull >> (4 * f2d)) & 15);
@@ -1147,7 +1152,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         hp.compute(0, ib);
         hp.rest(ib);
     };
-    const bool do_mc = NW && inter && !DGPU_ABL_MC;
+    const bool do_mc = (NW ? inter : ii) && !DGPU_ABL_MC;
     HPass<BPC, TX> hp0;
     if (do_mc) {
         hinit(hp0, 0);
@@ -1162,7 +1167,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         hp1.load(0);
     }
     // INTER_MASK / PAL: the unit's aux_pool offset (mask / palette record)
-    const bool auxed = pred == DGPU_PRED_INTER_MASK || pred == DGPU_PRED_PAL || pred == DGPU_PRED_WARP;
+    const bool auxed = pred == DGPU_PRED_INTER_MASK || pred == DGPU_PRED_PAL || pred == DGPU_PRED_WARP || ii;
     const int auxo = auxed ? a.aux[first + g] : 0;
     int cfsk = 0;
     if (ncoef) cfsk = cst.commit(cfl, l);
@@ -1413,6 +1418,59 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                 for (int i = 0; i < 8; i++) pv[i] = ptile[(2 * j + (i >> 2)) * W + 4 * q + (i & 3)];
             } else {
                 intra_task<TX>(is, tl, fe, 4 * q, 2 * j, pv);
+            }
+            emit(j, q, pv);
+        }
+    } else if (ii) {   // inter-intra, second launch: put, intra_pred, blend_c (src/mc_tmpl.c:641-653)
+        // 1. the inter (put) prediction of every task into registers
+        const int sh = 6 + ib, kp = kMidBias<BPC> + (1 << (sh - 1));
+        int ipv[TPL][8];
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t < NT) {
+                int t0[8];
+                mc_vtask<W>(mid0, t / QW, t % QW, tv0, kp, sh, t0);
+#pragma unroll
+                for (int i = 0; i < 8; i++) ipv[k][i] = clampi(t0[i], 0, bdmax);
+            }
+        }
+        wave_sync();   // the intermediate tile is free: the edges go there
+        // 2. the intra record, its edge array and the edge preparation
+        const u32x4 rec = gld<u32x4>(a.aux_pool + auxo);
+        Dav1dGpuUnit ui = u;
+        ui.p.intra.edge_off = (int32_t)rec[0];
+        ui.p.intra.mode = (uint8_t)(rec[1] & 0xff);
+        ui.p.intra.angle = (uint16_t)(rec[1] >> 16);
+        ui.p.intra.max_w = ui.p.intra.max_h = 0;
+        Stage<SL::EDGE * (int)sizeof(P), G> est2;
+        est2.load(a.edges + (int)rec[0] - 2 * H, SL::EDGE * (int)sizeof(P), l);
+        const P *tl2 = reinterpret_cast<const P *>(src + est2.commit(src, l)) + 2 * H;
+        wave_sync();
+        const IntraState is = intra_prep<BPC, TX>(ui, tl2, fe, l, bdmax);
+        wave_sync();
+        if (is.mode == DGPU_FILTER_PRED) filter_intra<TX>(ui, tl2, ptile, l, bdmax);
+        wave_sync();
+        const uint8_t *mkb = a.aux_pool + rec[2];
+        // 3. per task: intra prediction, the mask, blend, residual
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t >= NT) break;
+            const int j = t / QW, q = t % QW;
+            int pvi[8], pv[8];
+            if (is.mode == DGPU_FILTER_PRED) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) pvi[i] = ptile[(2 * j + (i >> 2)) * W + 4 * q + (i & 3)];
+            } else {
+                intra_task<TX>(is, tl2, fe, 4 * q, 2 * j, pvi);
+            }
+            const uint8_t *mk = mkb + (2 * j) * bw + 4 * q;
+            const uint32_t m0 = gld<uint32_t>(mk), m1 = gld<uint32_t>(mk + bw);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int m = (int)(((i < 4 ? m0 : m1) >> (8 * (i & 3))) & 0xff);
+                pv[i] = (ipv[k][i] * (64 - m) + pvi[i] * m + 32) >> 6;
             }
             emit(j, q, pv);
         }

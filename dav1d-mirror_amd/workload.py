@@ -186,9 +186,9 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         # "full": put / avg / w_avg / mask compound and palette blocks
         rng.random(nb)   # keep the later draws aligned with "full"
         e = np.random.default_rng(cfg.seed ^ 0xE7E7).random(nb)
-        kind = np.select([e < 0.20, e < 0.32, e < 0.48, e < 0.64, e < 0.82],
+        kind = np.select([e < 0.18, e < 0.30, e < 0.44, e < 0.58, e < 0.74, e < 0.88],
                          [abi.PRED_INTER, abi.PRED_INTER_AVG, abi.PRED_INTER_WAVG, abi.PRED_INTER_MASK,
-                          abi.PRED_PAL], abi.PRED_WARP)
+                          abi.PRED_PAL, abi.PRED_WARP], abi.PRED_INTER_INTRA)
     elif cfg.kind in ("ipred", "itx"):
         rng.random(nb)   # keep the later draws aligned with "full"
         kind = np.full(nb, abi.PRED_INTRA if cfg.kind == "ipred" else abi.PRED_NONE)
@@ -223,6 +223,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
                 cands = _tx_candidates(s, cfg.tx64)
                 if kind[b] == abi.PRED_WARP and plane == 0:   # warp units are whole 8x8s
                     cands = [c for c in cands if min(c) >= 8]
+                if kind[b] == abi.PRED_INTER_INTRA:   # second launch: no 64-point class
+                    cands = [c for c in cands if max(c) <= 32]
                 tw, th = cands[(b * 7 + plane * 3 + int(rng.integers(0, 1 << 20))) % len(cands)]
                 if plane > 0 and cfl_blk[b]:
                     tw = th = s   # CfL predicts the whole chroma block (<= 32x32)
@@ -260,7 +262,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     units["bh4"] = bsz // 4
 
     # inter parameters
-    inter = np.isin(pk, abi.INTER_KINDS)
+    inter = np.isin(pk, abi.INTER_KINDS + (abi.PRED_INTER_INTRA,))
     ref_stride = np.array([refs[0][p].shape[1] for p in range(3)])
     for k in range(2):
         mvx = mv[blk, k, 0]
@@ -283,7 +285,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         chunks, off = [], 0
         # INTER_MASK: one mask 0..64 per prediction block (per plane), row
         # stride = the block width; a unit points at its top-left inside it
-        mb = np.nonzero(pk == abi.PRED_INTER_MASK)[0]
+        mb = np.nonzero((pk == abi.PRED_INTER_MASK) | (pk == abi.PRED_INTER_INTRA))[0]
+        mask_at = np.zeros(n, np.int64)   # INTER_INTRA: the mask offset goes into its record
         bkey = blk * 3 + plane_u
         first_of = {}
         for i in mb:
@@ -296,7 +299,9 @@ def make_frame(cfg: FrameConfig) -> FrameData:
                 chunks.append(np.zeros((s_ * s_ + 15) // 16 * 16 - s_ * s_, np.uint8))
             bx0 = (int(ux[i]) // int(bsz[i])) * int(bsz[i])   # blocks are aligned to their size
             by0 = (int(uy[i]) // int(bsz[i])) * int(bsz[i])
-            aux[i] = first_of[k] + (int(uy[i]) - by0) * int(bsz[i]) + (int(ux[i]) - bx0)
+            mask_at[i] = first_of[k] + (int(uy[i]) - by0) * int(bsz[i]) + (int(ux[i]) - bx0)
+            if pk[i] == abi.PRED_INTER_MASK:
+                aux[i] = mask_at[i]
         # PAL: per unit a 16-B record of 8 entries, then the packed index map
         pb = np.nonzero(pk == abi.PRED_PAL)[0]
         bpp_ = 1 if cfg.bpc == 8 else 2
@@ -337,7 +342,6 @@ def make_frame(cfg: FrameConfig) -> FrameData:
             chunks.append(rec)
             off += len(rec) + (-len(rec)) % 16
             chunks.append(np.zeros((-len(rec)) % 16, np.uint8))
-        aux_pool = np.concatenate(chunks) if chunks else np.zeros(16, np.uint8)
 
     # intra parameters
     intra = pk == abi.PRED_INTRA
@@ -347,8 +351,23 @@ def make_frame(cfg: FrameConfig) -> FrameData:
                    np.where(m == abi.FILTER_PRED, fidx[blk], 0))
     # the intra fields share bytes with the inter ones (a C union): write
     # them only where the unit is intra
-    edge_len = np.where(intra | cfl, 2 * th + 2 * tw + 1, 0)
+    iiu = pk == abi.PRED_INTER_INTRA
+    edge_len = np.where(intra | cfl | iiu, 2 * th + 2 * tw + 1, 0)
     edge_start = np.concatenate([[0], np.cumsum(edge_len)[:-1]])
+    if cfg.kind == "ext":
+        # INTER_INTRA records: edge_off, mode (the inter-intra modes DC / V /
+        # H / SMOOTH, src/recon_tmpl.c:1550), angle 0, mask offset
+        ii_modes = np.array([abi.DC_PRED, abi.VERT_PRED, abi.HOR_PRED, abi.SMOOTH_PRED])
+        bmode = ii_modes[xr.integers(0, 4, nb)]
+        for i in np.nonzero(iiu)[0]:
+            rec = np.zeros(16, np.uint8)
+            rec[0:4] = np.array([edge_start[i] + 2 * th[i]], "<i4").view(np.uint8)
+            rec[4] = bmode[blk[i]]
+            rec[8:12] = np.array([mask_at[i]], "<i4").view(np.uint8)
+            aux[i] = off
+            chunks.append(rec)
+            off += 16
+        aux_pool = np.concatenate(chunks) if chunks else np.zeros(16, np.uint8)
     iu = units[intra]
     iu["src_off1"] = 0
     iu["filter2d"] = 0
@@ -450,12 +469,13 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         keys = (minor, units["pred"], band, units["tx"])
     # WARP units go last inside their class (the batch's class_warp ranges,
     # run by the warp launch)
-    is_warp = units["pred"] == abi.PRED_WARP
+    is_warp = np.isin(units["pred"], abi.SECOND_LAUNCH_KINDS)
     order = np.lexsort(keys[:-1] + (is_warp, units["tx"]))
     units = units[order]
     counts = np.bincount(units["tx"], minlength=abi.N_TX)
     class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
-    class_warp = np.bincount(units["tx"][units["pred"] == abi.PRED_WARP], minlength=abi.N_TX).astype(np.int32)
+    class_warp = np.bincount(units["tx"][np.isin(units["pred"], abi.SECOND_LAUNCH_KINDS)],
+                             minlength=abi.N_TX).astype(np.int32)
 
     dst_init = None
     if cfg.kind == "itx":   # a picture for the residual to land on (own stream)
@@ -482,12 +502,12 @@ def algorithmic_bytes(fd: FrameData):
     bw, bh = u["bw4"].astype(np.int64) * 4, u["bh4"].astype(np.int64) * 4
     # the reference reads each prediction block's footprint once per mc call
     # (src/recon_tmpl.c:957-1059): count it per block, not per transform unit
-    inter = np.isin(u["pred"], abi.INTER_KINDS)
+    inter = np.isin(u["pred"], abi.INTER_KINDS + (abi.PRED_INTER_INTRA,))
     _, first = np.unique(np.where(inter, fd.blk, -1), return_index=True)
     first = first[inter[first]]
     src = np.zeros(len(u), np.int64)
     for k in range(2):
-        use = (u["pred"] == abi.PRED_INTER) if k == 0 else np.zeros(len(u), bool)
+        use = np.isin(u["pred"], (abi.PRED_INTER, abi.PRED_INTER_INTRA)) if k == 0 else np.zeros(len(u), bool)
         use = use | np.isin(u["pred"], abi.COMPOUND_KINDS)
         mx, my = u[f"mx{k}"], u[f"my{k}"]
         fh = np.where(mx > 0, np.where(bw > 4, 7, 3), 0)
@@ -503,6 +523,9 @@ def algorithmic_bytes(fd: FrameData):
     aux_bytes = int((w * h)[u["pred"] == abi.PRED_INTER_MASK].sum())
     pal = u["pred"] == abi.PRED_PAL
     aux_bytes += int((w * h // 2)[pal].sum()) + int(pal.sum()) * 8 * bpp
+    ii = u["pred"] == abi.PRED_INTER_INTRA   # + its edge array, mask and 16-B record
+    edge = edge + np.where(ii, 2 * w + 2 * h + 1, 0)
+    aux_bytes += int((w * h + 16)[ii].sum())
     warp = u["pred"] == abi.PRED_WARP   # warp8x8: a 15x15 footprint per 8x8 + its parameters
     src = src + np.where(warp, (w // 8) * (h // 8) * 225, 0)
     aux_bytes += int(((w // 8) * (h // 8) * 8 + 16)[warp].sum())
@@ -528,5 +551,6 @@ def algorithmic_bytes(fd: FrameData):
         "n_inter": int(inter.sum()),
         "n_pal": int(pal.sum()),
         "n_warp": int(warp.sum()),
+        "n_inter_intra": int(ii.sum()),
         "n_nopred": int(nopred.sum()),
     }

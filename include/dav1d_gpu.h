@@ -232,6 +232,14 @@ enum Dav1dGpuPredKind {
                                 (the warp source position in the ref plane),
                                 int16 mx >> 6, int16 my >> 6 (warp_affine
                                 clears their low 6 bits, :1085-1090)         */
+    DGPU_PRED_INTER_INTRA = 9,/* inter-intra: mc put from ref 0, intra_pred
+                                into a tile, then blend (src/mc_tmpl.c:
+                                641-653, recon_tmpl.c:1540-1580).  aux[unit]
+                                = byte offset of a 16-byte record: int32
+                                edge_off (topleft[0] in the edge pool),
+                                uint8 mode, uint8 0, uint16 angle, int32
+                                mask_off (aux_pool offset of the unit's
+                                top-left mask value, stride bw4 * 4)         */
 };
 
 /* txtp value of a prediction-only unit (no inv_txfm_add): mc-only batches */
@@ -318,11 +326,12 @@ typedef struct Dav1dGpuFrameBatch {
                              mask or a PAL unit's palette record; only those
                              kinds read it (may be NULL without them)      */
     const void *aux_pool; /* device pool of masks (u8) / palette records   */
-    int32_t  class_warp[DGPU_N_RECT_TX_SIZES]; /* WARP units at the end of
-                             each class range (units sorted so); they run in
-                             their own launch with the warp kernel, which
-                             keeps warp's registers out of the main kernel.
-                             Classes with a side < 8 must have none         */
+    int32_t  class_warp[DGPU_N_RECT_TX_SIZES]; /* WARP and INTER_INTRA units
+                             at the end of each class range (units sorted
+                             so); they run in a second launch whose kernel
+                             keeps their registers out of the main kernel.
+                             64-point classes must have none; WARP units
+                             need both sides >= 8                           */
 } Dav1dGpuFrameBatch;
 
 /* Launch one frame batch on `stream` (a hipStream_t, NULL = default).

@@ -1464,6 +1464,36 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
                     for (int x = 0; x < w; x++) m[y * w + x] = ms[y * (u->bw4 * 4) + x];
                 avg_blend(dst, ds, t1, t2, w, h, 2, 0, m, bdmax);
             }
+        } else if (u->pred == DGPU_PRED_INTER_INTRA) {
+            /* recon_b_inter's inter-intra (src/recon_tmpl.c:1540-1580): the
+             * put prediction, intra_pred into a tile, then blend_c
+             * (src/mc_tmpl.c:641-653) with the unit's part of the mask */
+            const int f2d = u->p.inter.filter2d;
+            const int r = u->p.inter.ref[0];
+            const pixel *src = (const pixel *)b->ref[r][pl].data + u->p.inter.src_off[0];
+            const ptrdiff_t ss = b->ref[r][pl].stride;
+            const int mx = u->p.inter.mx[0], my = u->p.inter.my[0];
+            if (f2d == DGPU_FILTER_2D_BILINEAR) bilin_mc(dst, ds, NULL, src, ss, w, h, mx, my, bdmax);
+            else put_8tap(dst, ds, src, ss, w, h, mx, my, ftype_of[f2d], u->bw4 * 4, u->bh4 * 4, bdmax);
+            const uint8_t *rec = (const uint8_t *)b->aux_pool + b->aux[i];
+            int32_t eoff, moff;
+            uint16_t ang;
+            memcpy(&eoff, rec, 4);
+            memcpy(&ang, rec + 6, 2);
+            memcpy(&moff, rec + 8, 4);
+            pixel tile[64 * 64];
+            ipc.intra_pred[rec[4]](tile, w * sizeof(pixel), edges + eoff, w, h, ang, 0, 0
+#if BITDEPTH == 16
+                                   , bdmax
+#endif
+                                   );
+            const uint8_t *mk = (const uint8_t *)b->aux_pool + moff;
+            for (int y = 0; y < h; y++)
+                for (int x = 0; x < w; x++) {
+                    pixel *d = &dst[y * PX(ds) + x];
+                    const int m = mk[y * (u->bw4 * 4) + x];
+                    *d = (pixel)((*d * (64 - m) + tile[y * w + x] * m + 32) >> 6);
+                }
         } else if (u->pred == DGPU_PRED_WARP) {
             /* recon_tmpl.c warp_affine (:1063-1100): warp8x8 for each 8x8 of
              * the unit with its own source position and mx / my */

@@ -61,7 +61,9 @@ def test_recon_batch_validation(pkg):
         b.class_start[abi.N_TX] = 4   # last bound != n_units
         assert fn(ctypes.byref(b), None) == -2
         b = batch(5)
-        b.class_warp[0] = 1   # 4x4 cannot hold WARP units
+        for i in range(abi.N_TX + 1):
+            b.class_start[i] = 0 if i <= 4 else 5   # all units in class 4 (64x64)
+        b.class_warp[4] = 1   # 64-point classes have no second launch
         assert fn(ctypes.byref(b), None) == -2
         b = batch(5)
         b.class_warp[1] = 6   # more WARP units than the class has

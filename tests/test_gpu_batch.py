@@ -124,8 +124,8 @@ def test_smoke_entry():
 def test_batch_family(pkg, oracle, kind, bpc, bdmax):
     """The per-family frames of the bench breakdown: intra/CfL prediction
     only, inv_txfm_add onto an existing picture (PRED_NONE: the kernel's
-    picture-read path), and the other inter / palette kinds (w_avg and
-    mask compound, pal_pred), each with residual."""
+    picture-read path), and the other kinds (w_avg and mask compound,
+    pal_pred, warp, inter-intra blend), each with residual."""
     _check(_frame(pkg, width=512, height=256, bpc=bpc, bitdepth_max=bdmax, kind=kind, seed=21), oracle)
 
 
@@ -154,7 +154,7 @@ def test_batch_ragged_subsets(pkg, oracle, kind):
             sub.aux = fd.aux[keep]
         sub.class_start = np.concatenate([[0], np.cumsum(np.bincount(sub.units["tx"], minlength=19))]).astype(np.int32)
         if fd.class_warp is not None:
-            sub.class_warp = np.bincount(sub.units["tx"][sub.units["pred"] == pkg.abi.PRED_WARP],
+            sub.class_warp = np.bincount(sub.units["tx"][np.isin(sub.units["pred"], pkg.abi.SECOND_LAUNCH_KINDS)],
                                          minlength=19).astype(np.int32)
         sub.blk = fd.blk[keep]
         sub.stats = wl.algorithmic_bytes(sub)

@@ -18,8 +18,10 @@ def main():
     import dav1d_mirror_amd.workload as wl
     import dav1d_mirror_amd.batch as bt
     kw = dict(width=512, height=256, seed=int(sys.argv[1]) if len(sys.argv) > 1 else 1)
-    if len(sys.argv) > 2:
+    if len(sys.argv) > 2 and int(sys.argv[2]) > 255:
         kw.update(bpc=16, bitdepth_max=int(sys.argv[2]))
+    if len(sys.argv) > 3:
+        kw.update(kind=sys.argv[3])
     fd = wl.make_frame(wl.FrameConfig(**kw))
     dev = bt.DeviceFrame(fd, "cuda:0")
     dev.launch()
@@ -40,7 +42,7 @@ def main():
         b = hf.dst[p][y0:y0 + h, x0:x0 + w]
         pred = int(u["pred"])
         key = [f"pred{pred}", f"{w}x{h}"]
-        if pred in (1, 2):
+        if pred in (1, 2, 9):
             key += [f"f{int(u['filter2d'])}", f"mx0={int(u['mx0']) > 0}", f"my0={int(u['my0']) > 0}",
                     f"bw{int(u['bw4']) * 4}"]
         elif pred == 3:
@@ -51,7 +53,7 @@ def main():
             tot[k] += 1
             if bad:
                 stats[k] += 1
-        if bad and shown < 6:
+        if bad and shown < 3:
             shown += 1
             print("unit", {n: int(u[n]) for n in u.dtype.names if not n.startswith("pad")})
             print(" got\n", a.astype(int))
