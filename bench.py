@@ -70,8 +70,8 @@ def cpu_baseline(fd, budget_s=12.0):
 
 
 # rocprofv3 PMC summaries of the current kernels (tools/prof.sh + tools/pmc_summary.py)
-PMC_SUMMARY = {8: os.path.join(ROOT, "profiles", "r1", "r1c_pmc_summary.json"),
-               16: os.path.join(ROOT, "profiles", "r1", "r1c_10bit_pmc_summary.json")}
+PMC_SUMMARY = {8: os.path.join(ROOT, "profiles", "r1", "r1d_pmc_summary.json"),
+               16: os.path.join(ROOT, "profiles", "r1", "r1d_10bit_pmc_summary.json")}
 
 
 def pmc_traffic(bpc):
