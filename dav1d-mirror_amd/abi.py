@@ -89,6 +89,23 @@ class FrameBatch(ctypes.Structure):
                 ("class_warp", ctypes.c_int32 * N_TX)]
 
 
+class TileBatch(ctypes.Structure):
+    _fields_ = [("dst", Plane * 3),
+                ("ref", (Plane * 3) * MAX_REFS),
+                ("tiles", ctypes.c_void_p),
+                ("n_tiles", ctypes.c_int32),
+                ("n_tiles_huge", ctypes.c_int32),
+                ("bitdepth_max", ctypes.c_int32),
+                ("preds", ctypes.c_void_p),
+                ("txs", ctypes.c_void_p),
+                ("coef", ctypes.c_void_p),
+                ("edges", ctypes.c_void_p),
+                ("aux_pool", ctypes.c_void_p),
+                ("cfl_luma", Plane),
+                ("cfl_ss", ctypes.c_int32),
+                ("zero_coefs", ctypes.c_int32)]
+
+
 _LIB = None
 
 
@@ -115,6 +132,10 @@ def load_lib():
         L.dav1d_gpu_recon_16bpc.restype = ctypes.c_int
         L.dav1d_gpu_device_count.restype = ctypes.c_int
         L.dav1d_gpu_version.restype = ctypes.c_char_p
+        for bpc in (8, 16):
+            f = getattr(L, f"dav1d_gpu_recon_tiles_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(TileBatch), ctypes.c_void_p]
+            f.restype = ctypes.c_int
         L.dav1d_gpu_recon_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         L.dav1d_gpu_recon_lds_bytes.restype = ctypes.c_int
         _LIB = L
@@ -131,4 +152,5 @@ EXPORTED_SYMBOLS = [
     "dav1d_itx_dsp_init_gpu_8bpc", "dav1d_itx_dsp_init_gpu_16bpc",
     "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version",
     "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc", "dav1d_gpu_recon_lds_bytes",
+    "dav1d_gpu_recon_tiles_8bpc", "dav1d_gpu_recon_tiles_16bpc",
 ]

@@ -104,3 +104,80 @@ class DeviceFrame:
             a = t.cpu().numpy()
             out.append(a if self.fd.cfg.bpc == 8 else a.view(np.uint16))
         return out
+
+
+class DeviceTiles:
+    """A TileData (tiles.build_tiles) uploaded to one GPU, plus its output
+    planes: the superblock-tile batch (dav1d_gpu_recon_tiles_{8,16}bpc)."""
+
+    def __init__(self, fd, td, device="cuda:0", zero_coefs=False):
+        import torch
+        self.torch = torch
+        self.fd, self.td = fd, td
+        self.device = torch.device(device)
+        dev = self.device
+        hbd = fd.cfg.bpc != 8
+        pdt = torch.uint8 if not hbd else torch.int16   # int16 storage for uint16 bits
+        up = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).to(dev)   # noqa: E731
+        self.tiles = up(td.tiles.view(np.uint8))
+        self.preds = up(td.preds.view(np.uint8))
+        self.txs = up(td.txs.view(np.uint8))
+        self.coefs = up(td.coefs.view(np.int16 if not hbd else np.int32))
+        self.edges = up(td.edges if not hbd else td.edges.view(np.int16))
+        self.aux_pool = up(td.aux_pool) if td.aux_pool is not None else None
+        self.refs = [[up(a if not hbd else a.view(np.int16)) for a in rp] for rp in fd.refs]
+        self.cfl_luma = up(fd.cfl_luma if not hbd else fd.cfl_luma.view(np.int16))
+        if fd.dst_init is not None:
+            self.dst = [up(a if not hbd else a.view(np.int16)) for a in fd.dst_init]
+        else:
+            self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fd.plane_wh]
+        self.zero_coefs = zero_coefs
+        self.batch = self._make_batch()
+        self.lib = abi.load_lib()
+
+    def _make_batch(self):
+        fd, td = self.fd, self.td
+        bpp = 1 if fd.cfg.bpc == 8 else 2
+        b = abi.TileBatch()
+        for p in range(3):
+            w, h = fd.plane_wh[p]
+            b.dst[p].data = self.dst[p].data_ptr()
+            b.dst[p].stride = w * bpp
+            b.dst[p].w, b.dst[p].h = w, h
+            for r in range(len(self.refs)):
+                t = self.refs[r][p]
+                b.ref[r][p].data = t.data_ptr() + fd.ref_origin_offset(p) * bpp
+                b.ref[r][p].stride = t.shape[1] * bpp
+                b.ref[r][p].w, b.ref[r][p].h = w, h   # the clamp bounds (emu_edge)
+        b.tiles = self.tiles.data_ptr()
+        b.n_tiles = len(td.tiles)
+        b.n_tiles_huge = td.n_tiles_huge
+        b.bitdepth_max = fd.cfg.bitdepth_max if fd.cfg.bpc == 16 else 255
+        b.preds = self.preds.data_ptr()
+        b.txs = self.txs.data_ptr()
+        b.coef = self.coefs.data_ptr()
+        b.edges = self.edges.data_ptr()
+        b.aux_pool = self.aux_pool.data_ptr() if self.aux_pool is not None else None
+        b.cfl_luma.data = self.cfl_luma.data_ptr()
+        b.cfl_luma.stride = self.cfl_luma.shape[1] * bpp
+        b.cfl_luma.w, b.cfl_luma.h = fd.plane_wh[0]
+        b.cfl_ss = 3   # 4:2:0
+        b.zero_coefs = 1 if self.zero_coefs else 0
+        return b
+
+    def launch(self, stream=None):
+        """Enqueue one reconstruction of every tile on `stream` (a
+        torch.cuda.Stream; default: the current stream)."""
+        torch = self.torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        fn = self.lib.dav1d_gpu_recon_tiles_8bpc if self.fd.cfg.bpc == 8 else self.lib.dav1d_gpu_recon_tiles_16bpc
+        rc = fn(ctypes.byref(self.batch), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"dav1d_gpu_recon_tiles failed: {rc}")
+
+    def planes_host(self):
+        out = []
+        for t in self.dst:
+            a = t.cpu().numpy()
+            out.append(a if self.fd.cfg.bpc == 8 else a.view(np.uint16))
+        return out

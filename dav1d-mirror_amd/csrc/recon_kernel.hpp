@@ -949,7 +949,8 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
             const int row = t / QW, q = t % QW, x0 = (q & 1) * 4;
             const u32x2 sb = gld<u32x2>(rec + 16 + 8 * (sy * NBX + (q >> 1)));
             mxs[k] = (int)(int16_t)(sb[1] & 0xffff) * 64;
-            const P *s = ref + (int)sb[0] + (row - 3) * rs + x0 - 3;   // columns x0-3 .. x0+7
+            const int wx = (int16_t)(sb[0] & 0xffff), wy = (int)sb[0] >> 16;   // the 8x8's source position
+            const P *s = ref + (wy + row - 3) * rs + wx + x0 - 3;   // columns x0-3 .. x0+7
             if constexpr (BPC == 8) {
                 shs[k] = (unsigned)reinterpret_cast<uintptr_t>(s) & 3u;
                 raw[k] = gld<u32x4>(reinterpret_cast<const uint8_t *>(s) - shs[k]);

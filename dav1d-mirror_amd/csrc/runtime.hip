@@ -29,6 +29,18 @@ void ThreadCtx::reserve(size_t bytes) {
     cap = n;
 }
 
+ThreadCtx::~ThreadCtx() {
+    // errors ignored: at process exit the HIP runtime may already be gone
+    if (device < 0 && !host && !dev) return;
+    if (device >= 0) (void)hipSetDevice(device);
+    if (stream) (void)hipStreamDestroy(stream);
+    if (host) (void)hipHostFree(host);
+    if (dev) (void)hipFree(dev);
+    stream = nullptr;
+    host = dev = nullptr;
+    cap = 0;
+}
+
 ThreadCtx &thread_ctx() {
     ThreadCtx &c = tls_ctx;
     if (c.device != tls_device_req || !c.stream) {

@@ -27,6 +27,10 @@ struct ThreadCtx {
     uint8_t *dev = nullptr;
     size_t cap = 0;
     void reserve(size_t bytes);
+    // A worker thread's stream and staging buffers die with the thread
+    // (dav1d starts and joins its n_tc workers per decoder instance, so a
+    // long-running process would otherwise leak them on every instance).
+    ~ThreadCtx();
 };
 ThreadCtx &thread_ctx();
 

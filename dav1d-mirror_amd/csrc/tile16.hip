@@ -1,0 +1,6 @@
+// tile16.hip -- 16bpc superblock-tile batch entry point (include/dav1d_gpu.h)
+#include "tile_impl.hpp"
+
+extern "C" int dav1d_gpu_recon_tiles_16bpc(const Dav1dGpuTileBatch *b, void *stream) {
+    return dgpu::launch_tiles<16>(b, (hipStream_t)stream);
+}

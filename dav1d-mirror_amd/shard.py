@@ -47,27 +47,37 @@ def aggregate_gpix_per_s(pixels_per_frame, steps, world, elapsed_max_s):
 # stays outside the reconstruction's timed region.
 
 _DTYPES = [np.uint8, np.int16, np.int32, np.uint16, np.int64]
-_HDR = 4   # per array: dtype code, rows, cols, nbytes
+_HDR = 5   # per array: name code, dtype code, rows, cols, nbytes
+# every FrameData array the batch can read, by name; optional ones (None in
+# the frame) are simply not sent, and the receiver leaves them None
+_NAMES = (["units", "class_start", "coefs", "edges", "blk", "cfl_luma", "aux", "aux_pool", "class_warp", "src_xy"]
+          + [f"ref{r}_{p}" for r in range(2) for p in range(3)] + [f"dst_init{p}" for p in range(3)])
 
 
 def _frame_arrays(fd):
-    arrs = [fd.units.view(np.uint8), fd.class_start.astype(np.int32), fd.coefs, fd.edges,
-            fd.blk.astype(np.int32), fd.cfl_luma]
-    arrs += [a for rp in fd.refs for a in rp]
+    """(name, array) of every array of the frame that is present."""
+    out = [("units", fd.units.view(np.uint8)), ("class_start", fd.class_start.astype(np.int32)),
+           ("coefs", fd.coefs), ("edges", fd.edges), ("blk", fd.blk.astype(np.int32)), ("cfl_luma", fd.cfl_luma)]
+    for name in ("aux", "aux_pool", "class_warp", "src_xy"):
+        a = getattr(fd, name)
+        if a is not None:
+            out.append((name, np.asarray(a)))
+    assert len(fd.refs) <= 2, "feed ships at most 2 reference pictures"
+    out += [(f"ref{r}_{p}", a) for r, rp in enumerate(fd.refs) for p, a in enumerate(rp)]
     if fd.dst_init is not None:
-        arrs += list(fd.dst_init)
-    return arrs
+        out += [(f"dst_init{p}", a) for p, a in enumerate(fd.dst_init)]
+    return out
 
 
-def _header(arrs):
-    h = [len(arrs)]
-    for a in arrs:
+def _header(named):
+    h = [len(named)]
+    for name, a in named:
         a2 = a.reshape(a.shape[0], -1) if a.ndim > 1 else a.reshape(1, -1)
-        h += [_DTYPES.index(a.dtype.type), a2.shape[0], a2.shape[1], a.nbytes]
+        h += [_NAMES.index(name), _DTYPES.index(a.dtype.type), a2.shape[0], a2.shape[1], a.nbytes]
     return h
 
 
-def feed_frame(cfg_of_rank, rank, world, dist, device, max_arrays=32):
+def feed_frame(cfg_of_rank, rank, world, dist, device, max_arrays=len(_NAMES)):
     """Rank 0 builds world frames (cfg_of_rank(r)) and sends frame r to rank r;
     returns (FrameData of this rank, feed seconds, bytes received).  Works on
     any backend with send/recv (nccl = RCCL on device tensors, gloo on CPU)."""
@@ -83,8 +93,9 @@ def feed_frame(cfg_of_rank, rank, world, dist, device, max_arrays=32):
             if r == 0:
                 mine = fd
                 continue
-            arrs = _frame_arrays(fd)
-            h = _header(arrs)
+            named = _frame_arrays(fd)
+            arrs = [a for _, a in named]
+            h = _header(named)
             hdr = torch.zeros(hlen, dtype=torch.int64)
             hdr[:len(h)] = torch.tensor(h, dtype=torch.int64)
             bufs = [torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).to(device)
@@ -104,25 +115,28 @@ def feed_frame(cfg_of_rank, rank, world, dist, device, max_arrays=32):
     t0 = time.perf_counter()
     dist.recv(hdr, src=0)
     h = hdr.cpu().tolist()
-    arrs = []
+    got = {}
     for i in range(int(h[0])):
-        code, rows, cols, nb = h[1 + _HDR * i: 1 + _HDR * (i + 1)]
+        name, code, rows, cols, nb = h[1 + _HDR * i: 1 + _HDR * (i + 1)]
         b = torch.empty(int(nb), dtype=torch.uint8, device=device)
         dist.recv(b, src=0)
         a = b.cpu().numpy().view(_DTYPES[int(code)])
-        arrs.append(a.reshape(int(rows), int(cols)) if rows > 1 else a.reshape(-1))
+        got[_NAMES[int(name)]] = a.reshape(int(rows), int(cols)) if rows > 1 else a.reshape(-1)
         nbytes += int(nb)
     if str(device) != "cpu":
         torch.cuda.synchronize(device)
     t_total = time.perf_counter() - t0
     cfg = cfg_of_rank(rank)
     from . import abi
-    units = arrs[0].reshape(-1).view(abi.UNIT_DTYPE)
-    refs = [arrs[6:9], arrs[9:12]]
-    dst_init = arrs[12:15] if len(arrs) > 12 else None
+    flat = lambda k: None if k not in got else got[k].reshape(-1)   # noqa: E731
+    refs = [[got[f"ref{r}_{p}"] for p in range(3)] for r in range(2) if f"ref{r}_0" in got]
+    dst_init = [got[f"dst_init{p}"] for p in range(3)] if "dst_init0" in got else None
     W, H = cfg.width, cfg.height
-    fd = wl.FrameData(cfg=cfg, units=units, class_start=arrs[1].reshape(-1), coefs=arrs[2].reshape(-1),
-                      edges=arrs[3].reshape(-1), refs=refs, plane_wh=[(W, H), (W // 2, H // 2), (W // 2, H // 2)],
-                      blk=arrs[4].reshape(-1), cfl_luma=arrs[5], dst_init=dst_init)
+    fd = wl.FrameData(cfg=cfg, units=got["units"].reshape(-1).view(abi.UNIT_DTYPE),
+                      class_start=flat("class_start"), coefs=flat("coefs"), edges=flat("edges"), refs=refs,
+                      plane_wh=[(W, H), (W // 2, H // 2), (W // 2, H // 2)], blk=flat("blk"),
+                      cfl_luma=got["cfl_luma"], dst_init=dst_init, aux=flat("aux"), aux_pool=flat("aux_pool"),
+                      class_warp=flat("class_warp"),
+                      src_xy=None if "src_xy" not in got else got["src_xy"].reshape(-1, 2, 2))
     fd.stats = wl.algorithmic_bytes(fd)
     return fd, t_total, nbytes

@@ -65,6 +65,18 @@ class FrameConfig:
     # mc is pointwise and the filter bank follows the block size, bw4/bh4), so
     # a 64x64 block does not need the 64-point class group's long waves
     mc_split: int = int(os.environ.get("DAV1D_GPU_MC_SPLIT", "32"))   # env: tuning knob
+    # integer MV range in luma pixels (+-); beyond REF_PAD - 8 the footprints
+    # leave the padded reference planes: only the tile batch (which clamps,
+    # emu_edge semantics) may then run the frame
+    mv_range: int = 64
+    # reference planes padded by replicating their edge pixels (what
+    # emu_edge would read) instead of random pixels: then every footprint,
+    # clamped or read from the padding, sees the same values
+    edge_pad: bool = True
+
+    @property
+    def ref_pad(self):
+        return max(REF_PAD, self.mv_range + 32)
 
     @property
     def pixel_dtype(self):
@@ -90,6 +102,8 @@ class FrameData:
     aux: np.ndarray = None        # per-unit int32: aux_pool offset (INTER_MASK / PAL units)
     aux_pool: np.ndarray = None   # u8 pool: block masks, palette records
     class_warp: np.ndarray = None # WARP units at the end of each class range
+    src_xy: np.ndarray = None     # [unit][ref][x|y]: integer source position of the unit's
+                                  # top-left in the reference plane (visible coordinates)
     stats: dict = field(default_factory=dict)
 
     @property
@@ -98,7 +112,7 @@ class FrameData:
 
     def ref_origin_offset(self, plane):
         stride = self.refs[0][plane].shape[1]
-        return REF_PAD * stride + REF_PAD
+        return self.cfg.ref_pad * stride + self.cfg.ref_pad
 
 
 def _partition(rng, W, H):
@@ -168,12 +182,15 @@ def make_frame(cfg: FrameConfig) -> FrameData:
 
     # reference pictures: 2 x 3 planes, padded, uniform random pixels
     refs = []
+    pad = cfg.ref_pad
     for _ in range(2):
         rp = []
         for (pw, ph) in planes:
-            stride = (pw + 2 * REF_PAD + 63) // 64 * 64
-            rp.append(rng.integers(0, bdmax + 1, size=(ph + 2 * REF_PAD, stride),
-                                   dtype=cfg.pixel_dtype))
+            stride = (pw + 2 * pad + 63) // 64 * 64
+            a = rng.integers(0, bdmax + 1, size=(ph + 2 * pad, stride), dtype=cfg.pixel_dtype)
+            if cfg.edge_pad:
+                a[:, :] = np.pad(a[pad:pad + ph, pad:pad + pw], ((pad, pad), (pad, stride - pw - pad)), mode="edge")
+            rp.append(a)
         refs.append(rp)
 
     lx, ly, ls = _partition(rng, W, H)
@@ -197,7 +214,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
                         np.where(rng.random(nb) < cfg.compound_frac, abi.PRED_INTER_AVG,
                                  abi.PRED_INTER))
     filt = rng.integers(0, 9, nb)
-    mv = rng.integers(-64 * 16, 64 * 16 + 1, size=(nb, 2, 2))   # [block][ref][x|y], 1/16 px
+    mv = rng.integers(-cfg.mv_range * 16, cfg.mv_range * 16 + 1, size=(nb, 2, 2))   # [block][ref][x|y], 1/16 px
     mode = rng.integers(0, 14, nb)
     zang = Z_ANGLES[rng.integers(0, 27, nb)]
     zflags = rng.integers(0, 4, nb) << 9
@@ -264,6 +281,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     # inter parameters
     inter = np.isin(pk, abi.INTER_KINDS + (abi.PRED_INTER_INTRA,))
     ref_stride = np.array([refs[0][p].shape[1] for p in range(3)])
+    src_xy = np.zeros((n, 2, 2), np.int32)
     for k in range(2):
         mvx = mv[blk, k, 0]
         mvy = mv[blk, k, 1]
@@ -273,6 +291,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         sx = ux + (mvx >> 4)
         sy = uy + (mvy >> 4)
         units[f"src_off{k}"] = np.where(inter, sy * ref_stride[plane_u] + sx, 0)
+        src_xy[:, k, 0] = np.where(inter, sx, 0)
+        src_xy[:, k, 1] = np.where(inter, sy, 0)
         units[f"mx{k}"] = np.where(inter, mvx & 15, 0)
         units[f"my{k}"] = np.where(inter, mvy & 15, 0)
         units[f"ref{k}"] = k
@@ -280,7 +300,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     aux = aux_pool = None
     if cfg.kind == "ext":
         xr = np.random.default_rng(cfg.seed ^ 0xA0A0)
-        units["weight"] = np.where(pk == abi.PRED_INTER_WAVG, xr.integers(1, 16, n), 0)
+        # jnt_comp weight per prediction block (f->jnt_weights, src/recon_tmpl.c:1873)
+        units["weight"] = np.where(pk == abi.PRED_INTER_WAVG, xr.integers(1, 16, nb)[blk], 0)
         aux = np.zeros(n, np.int32)
         chunks, off = [], 0
         # INTER_MASK: one mask 0..64 per prediction block (per plane), row
@@ -316,8 +337,9 @@ def make_frame(cfg: FrameConfig) -> FrameData:
             chunks.append(rec)
             off += len(rec)
         # WARP: per unit abcd[4] (int16), 8 pad bytes, then per 8x8 of the
-        # unit int32 src_off, int16 mx >> 6, int16 my >> 6 (warp_affine,
-        # src/recon_tmpl.c:1063-1100, with shear parameters within +-1024)
+        # unit int16 x, y (its source position), int16 mx >> 6, int16 my >> 6
+        # (warp_affine, src/recon_tmpl.c:1134-1193, with shear parameters
+        # within +-1024)
         wb = np.nonzero(pk == abi.PRED_WARP)[0]
         babcd = xr.integers(-1024, 1025, size=(nb, 4)).astype(np.int16)
         for i in wb:
@@ -326,13 +348,13 @@ def make_frame(cfg: FrameConfig) -> FrameData:
             rec = np.zeros(16 + 8 * (w_ // 8) * (h_ // 8), np.uint8)
             rec[:8] = a_.view(np.uint8)
             mvx, mvy = int(mv[blk[i], 0, 0]) >> 4, int(mv[blk[i], 0, 1]) >> 4
-            sub = np.zeros((h_ // 8) * (w_ // 8), dtype=[("off", "<i4"), ("mx", "<i2"), ("my", "<i2")])
+            sub = np.zeros((h_ // 8) * (w_ // 8), dtype=[("x", "<i2"), ("y", "<i2"), ("mx", "<i2"), ("my", "<i2")])
             k_ = 0
             for sy in range(h_ // 8):
                 for sx in range(w_ // 8):
                     x_ = int(ux[i]) + 8 * sx + mvx + int(xr.integers(-2, 3))
                     y_ = int(uy[i]) + 8 * sy + mvy + int(xr.integers(-2, 3))
-                    sub["off"][k_] = y_ * int(ref_stride[0]) + x_
+                    sub["x"][k_], sub["y"][k_] = x_, y_
                     mx_ = (int(xr.integers(0, 65536)) - 4 * int(a_[0]) - 7 * int(a_[1])) & ~63
                     my_ = (int(xr.integers(0, 65536)) - 4 * int(a_[2]) - 4 * int(a_[3])) & ~63
                     sub["mx"][k_], sub["my"][k_] = mx_ >> 6, my_ >> 6
@@ -484,7 +506,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     fd = FrameData(cfg=cfg, units=units, class_start=class_start, coefs=coefs, edges=edges,
                    refs=refs, plane_wh=planes, blk=(blk * 3 + plane_u)[order], cfl_luma=cfl_luma,
                    dst_init=dst_init, aux=None if aux is None else aux[order], aux_pool=aux_pool,
-                   class_warp=class_warp)
+                   class_warp=class_warp, src_xy=src_xy[order])
     fd.stats = algorithmic_bytes(fd)
     return fd
 

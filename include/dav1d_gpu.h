@@ -228,10 +228,11 @@ enum Dav1dGpuPredKind {
                                 src/mc_tmpl.c:758-791, recon_tmpl.c:1063-1100
                                 warp_affine).  aux[unit] = byte offset of a
                                 16-byte aligned record: int16 abcd[4], 8 pad
-                                bytes, then per 8x8 (row-major) int32 src_off
-                                (the warp source position in the ref plane),
-                                int16 mx >> 6, int16 my >> 6 (warp_affine
-                                clears their low 6 bits, :1085-1090)         */
+                                bytes, then per 8x8 (row-major) int16 x, y
+                                (the warp source position in the ref plane:
+                                dx, dy of recon_tmpl.c:1162-1167), int16
+                                mx >> 6, int16 my >> 6 (warp_affine clears
+                                their low 6 bits, :1163-1167)                */
     DGPU_PRED_INTER_INTRA = 9,/* inter-intra: mc put from ref 0, intra_pred
                                 into a tile, then blend (src/mc_tmpl.c:
                                 641-653, recon_tmpl.c:1540-1580).  aux[unit]
@@ -335,9 +336,149 @@ typedef struct Dav1dGpuFrameBatch {
 } Dav1dGpuFrameBatch;
 
 /* Launch one frame batch on `stream` (a hipStream_t, NULL = default).
- * Returns 0 or a negative error.  Asynchronous w.r.t. the host. */
+ * Returns 0 or a negative error.  Asynchronous w.r.t. the host.
+ * Reference footprints are read straight from the reference planes: the
+ * unit batch does NOT emulate edges, so every footprint (the unit's
+ * rectangle -3 / +4 pixels) must lie inside readable, edge-replicated
+ * memory (e.g. planes padded by >= 80 px with dav1d's own border
+ * extension).  Blocks whose footprint leaves the picture belong in the
+ * tile batch below, which clamps (emu_edge semantics). */
 int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream);
 int dav1d_gpu_recon_16bpc(const Dav1dGpuFrameBatch *b, void *stream);
+
+/* ---- batch tier, superblock tiles ----------------------------------------
+ * The throughput path.  A tile is one plane's rectangle of at most 64x64
+ * pixels -- a superblock's luma, or its chroma -- and one workgroup
+ * reconstructs it entirely, the way recon_b_inter / recon_b_intra do for
+ * the blocks of one superblock (src/recon_tmpl.c:1598, :1195):
+ *   1. the residual of every transform block (inv_txfm_add's two 1-D
+ *      passes, src/itx_tmpl.c:40-100) into an on-chip tile,
+ *   2. the prediction of every prediction block (mc once per block and
+ *      reference, as recon_tmpl.c's mc() call; intra_pred / cfl / pal per
+ *      block) added to it, clipped,
+ *   3. one store of the finished rectangle (whole rows).
+ * Every pixel of a tile must be covered by exactly one Dav1dGpuPred; tx
+ * blocks need not cover the tile (no residual there).
+ *
+ * Records are grouped per tile (contiguous ranges), and the per-tile lane
+ * bases (`lane0`) are the producer's prefix sums -- see the comments. */
+
+typedef struct Dav1dGpuTile {   /* 48 bytes */
+    int16_t  x, y;        /* top-left in the plane, pixels                   */
+    uint8_t  plane;       /* 0 = Y, 1 = U, 2 = V                             */
+    uint8_t  w4, h4;      /* size in 4-px units, 1..16                       */
+    uint8_t  flags;       /* bit 0: the tile has WARP preds                  */
+    int32_t  pred0;       /* first Dav1dGpuPred of the tile                  */
+    int32_t  tx0;         /* first Dav1dGpuTx                                */
+    int32_t  coef0;       /* first coefficient (element) of the tile         */
+    int32_t  edge0;       /* first intra edge pixel of the tile              */
+    uint16_t n_pred, n_tx;
+    uint16_t n_coef;      /* coefficients of the tile (<= 4096 + n_tx)       */
+    uint16_t n_edge;      /* edge pixels of the tile (<= DGPU_TILE_MAX_EDGE) */
+    uint16_t lanes_tx;    /* sum of the tx records' lane counts              */
+    uint16_t lanes_coop;  /* lanes of the cooperative preds, multiple of 64  */
+    uint16_t lanes_task;  /* lanes of the independent-task preds             */
+    uint16_t lanes_coop_used; /* cooperative lanes actually assigned (the
+                             rest of lanes_coop is padding)                 */
+    int32_t  reserved2_[2];
+} Dav1dGpuTile;
+
+#define DGPU_TILE_MAX_EDGE 4608   /* edge pixels staged per tile              */
+
+/* A prediction block (or the part of one inside the tile), 32 bytes.
+ *
+ * Cooperative kinds (INTRA, CFL) run as a group of 2^lanes_log2 lanes
+ * (edge preparation, DC sums); they come first in the tile's pred range,
+ * sorted by group size, largest first, and lane0 is the group's base in
+ * the cooperative section (a multiple of its size).
+ *
+ * Every other kind runs as independent tasks of 4 columns x R rows,
+ * R = min(8, h): (w / 4) * (h / R) tasks, one per lane; lane0 is the first
+ * task's lane in the task section.  WARP needs w, h multiples of 8. */
+typedef struct Dav1dGpuPred {
+    uint8_t  kind;        /* Dav1dGpuPredKind (NONE: residual onto the
+                             existing picture)                              */
+    uint8_t  x4, y4;      /* position in the tile, 4-px units                */
+    uint8_t  w4, h4;      /* size, 4-px units                                */
+    uint8_t  bw4, bh4;    /* size of the whole block: the mc filter bank
+                             (src/mc_tmpl.c:99-107) and mask / warp record
+                             strides follow it                              */
+    uint8_t  lanes_log2;  /* cooperative kinds: log2 of the group size      */
+    uint16_t lane0;       /* see above                                       */
+    uint16_t pad_;
+    union {
+        struct {          /* INTER, INTER_AVG / WAVG / MASK, INTER_INTRA,
+                             WARP (ref 0 only)                               */
+            int16_t src_x[2], src_y[2];  /* integer position in the reference
+                             plane of the pred's top-left (the block position
+                             + the mv's integer part); footprints outside the
+                             plane are clamped to it (emu_edge_c,
+                             src/mc_tmpl.c:827-875, as recon_tmpl.c:986-999
+                             applies it)                                     */
+            uint8_t mx[2], my[2];        /* 1/16-pel fractions 0..15         */
+            uint8_t filter2d;            /* Dav1dGpuFilter2d                 */
+            uint8_t ref[2];              /* reference picture slots          */
+            uint8_t weight;              /* INTER_WAVG: ref0's weight 1..15  */
+            int32_t aux;      /* aux_pool byte offset: INTER_MASK the mask
+                                 value of the pred's top-left (row stride
+                                 bw4 * 4); WARP / INTER_INTRA their records
+                                 (as in the unit batch, the pred being the
+                                 unit)                                        */
+        } inter;
+        struct {          /* INTRA, CFL, PAL                                 */
+            int32_t  edge_off;   /* topleft[0], relative to the tile's edge0  */
+            uint16_t angle;      /* angle | is_sm<<9 | filt<<10, filter_idx   */
+            uint8_t  mode;       /* Dav1dGpuIntraMode (CFL: its DC source)    */
+            int8_t   alpha;      /* CFL: cfl_alpha, -16..16                   */
+            uint16_t max_w, max_h;   /* Z2 edge-filter limits                 */
+            uint8_t  cfl_pad_wh; /* CFL: w_pad | h_pad << 4                   */
+            uint8_t  pad2_[3];
+            int32_t  aux;        /* CFL: luma offset in cfl_luma; PAL: the
+                                    aux_pool offset of its record             */
+        } intra;
+    } p;
+} Dav1dGpuPred;
+
+/* A transform block, 8 bytes, bit-packed:
+ *   w0 = x4 | y4 << 4 | tx << 8 | txtp << 13 | nzw << 18 | nzh << 24
+ *   w1 = coef_off | lane0 << 16
+ * x4, y4: position in the tile (4-px units); nzw x nzh: the stored
+ * coefficient region, column-major with stride nzh (0 x 0: the reference's
+ * DC-only call, one coefficient); coef_off: relative to the tile's coef0;
+ * lane0: base of its max(w, min(h, 32)) lanes in the tile's tx section
+ * (records sorted by that lane count, largest first).  Transform blocks
+ * with no residual are simply absent. */
+typedef struct Dav1dGpuTx {
+    uint32_t w0, w1;
+} Dav1dGpuTx;
+
+typedef struct Dav1dGpuTileBatch {
+    Dav1dGpuPlane dst[3];
+    Dav1dGpuPlane ref[DGPU_MAX_REFS][3];   /* w / h: the clamp bounds        */
+    const Dav1dGpuTile *tiles;             /* device                         */
+    int32_t  n_tiles;
+    int32_t  n_tiles_huge;  /* the LAST n_tiles_huge tiles hold transform
+                               blocks with a 64-point side; they run in a
+                               second kernel whose registers fit the 64-point
+                               transforms (the first kernel has none)       */
+    int32_t  bitdepth_max;
+    const Dav1dGpuPred *preds;             /* device                         */
+    const Dav1dGpuTx *txs;                 /* device                         */
+    void    *coef;        /* int16 (8bpc) / int32 (16bpc), tile order; zeroed
+                             after use when zero_coefs (src/itx_tmpl.c:55/89) */
+    const void *edges;    /* intra edge pixels, tile order                    */
+    const void *aux_pool; /* masks, palette / warp / inter-intra records      */
+    Dav1dGpuPlane cfl_luma;
+    int32_t  cfl_ss;      /* ss_hor | ss_ver << 1                             */
+    int32_t  zero_coefs;
+} Dav1dGpuTileBatch;
+
+/* Launch one tile batch: one workgroup per tile.  Reference planes need 16
+ * readable bytes past the end of each row (the last one included): rows are
+ * fetched with aligned 16-byte loads.  Returns 0, -1 (NULL / bad counts),
+ * -3 (launch failure) or -4 (misaligned planes). */
+int dav1d_gpu_recon_tiles_8bpc(const Dav1dGpuTileBatch *b, void *stream);
+int dav1d_gpu_recon_tiles_16bpc(const Dav1dGpuTileBatch *b, void *stream);
 
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split

@@ -1505,11 +1505,10 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
             for (int sy = 0; sy < h / 8; sy++)
                 for (int sx = 0; sx < w / 8; sx++) {
                     const uint8_t *sb = rec + 16 + 8 * (sy * (w / 8) + sx);
-                    int32_t soff;
-                    int16_t mxy[2];
-                    memcpy(&soff, sb, 4);
+                    int16_t xy[2], mxy[2];   /* the 8x8's source position, mx >> 6, my >> 6 */
+                    memcpy(xy, sb, 4);
                     memcpy(mxy, sb + 4, 4);
-                    const pixel *src = (const pixel *)b->ref[r][pl].data + soff;
+                    const pixel *src = (const pixel *)b->ref[r][pl].data + xy[1] * PX(ss) + xy[0];
                     warp8x8(dst + 8 * sy * PX(ds) + 8 * sx, ds, NULL, 0, src, ss, abcd, mxy[0] * 64, mxy[1] * 64,
                             bdmax);
                 }
@@ -1569,6 +1568,192 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
                                      , bdmax
 #endif
                                      );
+    }
+    return 0;
+}
+
+/* ===================================================== tile batch oracle */
+
+/* recon_tmpl.c mc() for one prediction block and reference, without
+ * scaling (src/recon_tmpl.c:957-1009): the block at integer source position
+ * (dx, dy) with fractions mx / my; when the filter footprint leaves the
+ * iw x ih reference, emu_edge copies it into a 192-stride scratch first
+ * (:986-996), exactly the reference's condition and offsets. */
+static void tile_mc(pixel *dst, ptrdiff_t ds, int16_t *tmp, const Dav1dGpuPlane *rp, int dx, int dy,
+                    int w, int h, int mx, int my, int f2d, int bw, int bh, int bdmax)
+{
+    static __thread pixel emu[(128 + 7) * 192];
+    const pixel *ref;
+    ptrdiff_t rs = rp->stride;
+    const int iw = rp->w, ih = rp->h;
+    if (dx < !!mx * 3 || dy < !!my * 3 || dx + w + !!mx * 4 > iw || dy + h + !!my * 4 > ih) {
+        emu_edge(w + !!mx * 7, h + !!my * 7, iw, ih, dx - !!mx * 3, dy - !!my * 3, emu, 192 * sizeof(pixel),
+                 (const pixel *)rp->data, rp->stride);
+        ref = &emu[192 * !!my * 3 + !!mx * 3];
+        rs = 192 * sizeof(pixel);
+    } else {
+        ref = (const pixel *)rp->data + (ptrdiff_t)dy * PX(rs) + dx;
+    }
+    if (f2d == DGPU_FILTER_2D_BILINEAR) bilin_mc(tmp ? NULL : dst, ds, tmp, ref, rs, w, h, mx, my, bdmax);
+    else if (tmp) prep_8tap(tmp, ref, rs, w, h, mx, my, ftype_of[f2d], bw, bh, bdmax);
+    else put_8tap(dst, ds, ref, rs, w, h, mx, my, ftype_of[f2d], bw, bh, bdmax);
+}
+
+/* CPU reconstruction of a Dav1dGpuTileBatch with HOST pointers, tile by
+ * tile as recon_b_inter / recon_b_intra would for the superblock's blocks:
+ * every pred (mc per block and reference via tile_mc; intra_pred / CfL /
+ * pal_pred; warp_affine with its emu_edge, src/recon_tmpl.c:1134-1193;
+ * inter-intra), then inv_txfm_add per transform block. */
+int SFX(oracle_recon_tiles)(const Dav1dGpuTileBatch *b, int t0, int t1)
+{
+    const int bdmax = BITDEPTH == 8 ? 255 : b->bitdepth_max;
+    IPCTX ipc;
+    SFX(oracle_intra_pred_dsp_init)(&ipc);
+    const pixel *edges = (const pixel *)b->edges;
+    const uint8_t *aux = (const uint8_t *)b->aux_pool;
+    static __thread int16_t tt1[128 * 128], tt2[128 * 128];
+    coef cf[32 * 32];
+    for (int ti = t0; ti < t1; ti++) {
+        const Dav1dGpuTile *T = &b->tiles[ti];
+        const int pl = T->plane;
+        const ptrdiff_t ds = b->dst[pl].stride;
+        pixel *tdst = (pixel *)b->dst[pl].data + (ptrdiff_t)T->y * PX(ds) + T->x;
+        for (int i = 0; i < T->n_pred; i++) {
+            const Dav1dGpuPred *p = &b->preds[T->pred0 + i];
+            const int w = p->w4 * 4, h = p->h4 * 4, bw = p->bw4 * 4, bh = p->bh4 * 4;
+            pixel *dst = tdst + (ptrdiff_t)(p->y4 * 4) * PX(ds) + p->x4 * 4;
+            const int f2d = p->p.inter.filter2d;
+            switch (p->kind) {
+            case DGPU_PRED_INTER:
+            case DGPU_PRED_INTER_INTRA: {
+                const Dav1dGpuPlane *rp = &b->ref[p->p.inter.ref[0]][pl];
+                tile_mc(dst, ds, NULL, rp, p->p.inter.src_x[0], p->p.inter.src_y[0], w, h, p->p.inter.mx[0],
+                        p->p.inter.my[0], f2d, bw, bh, bdmax);
+                if (p->kind == DGPU_PRED_INTER_INTRA) {   /* src/recon_tmpl.c:1540-1580, blend_c :641-653 */
+                    const uint8_t *rec = aux + p->p.inter.aux;
+                    int32_t eoff, moff;
+                    uint16_t ang;
+                    memcpy(&eoff, rec, 4);
+                    memcpy(&ang, rec + 6, 2);
+                    memcpy(&moff, rec + 8, 4);
+                    pixel it[64 * 64];
+                    ipc.intra_pred[rec[4]](it, w * sizeof(pixel), edges + eoff, w, h, ang, 0, 0
+#if BITDEPTH == 16
+                                           , bdmax
+#endif
+                                           );
+                    const uint8_t *mk = aux + moff;
+                    for (int y = 0; y < h; y++)
+                        for (int x = 0; x < w; x++) {
+                            pixel *d = &dst[y * PX(ds) + x];
+                            *d = (pixel)((*d * (64 - mk[y * bw + x]) + it[y * w + x] * mk[y * bw + x] + 32) >> 6);
+                        }
+                }
+                break;
+            }
+            case DGPU_PRED_INTER_AVG:
+            case DGPU_PRED_INTER_WAVG:
+            case DGPU_PRED_INTER_MASK: {
+                for (int k = 0; k < 2; k++)
+                    tile_mc(NULL, 0, k ? tt2 : tt1, &b->ref[p->p.inter.ref[k]][pl], p->p.inter.src_x[k],
+                            p->p.inter.src_y[k], w, h, p->p.inter.mx[k], p->p.inter.my[k], f2d, bw, bh, bdmax);
+                if (p->kind == DGPU_PRED_INTER_AVG) avg_blend(dst, ds, tt1, tt2, w, h, 0, 0, NULL, bdmax);
+                else if (p->kind == DGPU_PRED_INTER_WAVG) avg_blend(dst, ds, tt1, tt2, w, h, 1, p->p.inter.weight, NULL, bdmax);
+                else {
+                    static __thread uint8_t m[128 * 128];
+                    for (int y = 0; y < h; y++)
+                        for (int x = 0; x < w; x++) m[y * w + x] = aux[p->p.inter.aux + y * bw + x];
+                    avg_blend(dst, ds, tt1, tt2, w, h, 2, 0, m, bdmax);
+                }
+                break;
+            }
+            case DGPU_PRED_WARP: {   /* warp_affine, src/recon_tmpl.c:1134-1193 */
+                const uint8_t *rec = aux + p->p.inter.aux;
+                int16_t abcd[4];
+                memcpy(abcd, rec, 8);
+                const Dav1dGpuPlane *rp = &b->ref[p->p.inter.ref[0]][pl];
+                pixel emu[15 * 32];
+                for (int sy = 0; sy < h / 8; sy++)
+                    for (int sx = 0; sx < w / 8; sx++) {
+                        int16_t xy[2], mxy[2];
+                        memcpy(xy, rec + 16 + 8 * (sy * (w / 8) + sx), 4);
+                        memcpy(mxy, rec + 16 + 8 * (sy * (w / 8) + sx) + 4, 4);
+                        const int dx = xy[0], dy = xy[1];
+                        const pixel *src;
+                        ptrdiff_t ss = rp->stride;
+                        if (dx < 3 || dx + 8 + 4 > rp->w || dy < 3 || dy + 8 + 4 > rp->h) {
+                            emu_edge(15, 15, rp->w, rp->h, dx - 3, dy - 3, emu, 32 * sizeof(pixel),
+                                     (const pixel *)rp->data, rp->stride);
+                            src = &emu[32 * 3 + 3];
+                            ss = 32 * sizeof(pixel);
+                        } else {
+                            src = (const pixel *)rp->data + (ptrdiff_t)dy * PX(ss) + dx;
+                        }
+                        warp8x8(dst + 8 * sy * PX(ds) + 8 * sx, ds, NULL, 0, src, ss, abcd, mxy[0] * 64, mxy[1] * 64,
+                                bdmax);
+                    }
+                break;
+            }
+            case DGPU_PRED_PAL: {
+                const uint8_t *rec = aux + p->p.intra.aux;
+                pal_pred(dst, ds, (const pixel *)rec, rec + 16, w, h);
+                break;
+            }
+            case DGPU_PRED_CFL: {
+                const pixel *tl = edges + T->edge0 + p->p.intra.edge_off;
+                const pixel *ypx = (const pixel *)b->cfl_luma.data + p->p.intra.aux;
+                const int ssh = b->cfl_ss & 1, ssv = (b->cfl_ss >> 1) & 1;
+                cfl_ac(tt1, ypx, b->cfl_luma.stride, p->p.intra.cfl_pad_wh & 15, p->p.intra.cfl_pad_wh >> 4, w, h,
+                       ssh, ssv);
+                ipc.cfl_pred[p->p.intra.mode](dst, ds, tl, w, h, tt1, p->p.intra.alpha
+#if BITDEPTH == 16
+                                              , bdmax
+#endif
+                                              );
+                break;
+            }
+            case DGPU_PRED_INTRA: {
+                const pixel *tl = edges + T->edge0 + p->p.intra.edge_off;
+                ipc.intra_pred[p->p.intra.mode](dst, ds, tl, w, h, p->p.intra.angle, p->p.intra.max_w,
+                                                p->p.intra.max_h
+#if BITDEPTH == 16
+                                                , bdmax
+#endif
+                                                );
+                break;
+            }
+            default:   /* NONE: the residual goes onto the picture as it is */
+                break;
+            }
+        }
+        coef *pool = (coef *)b->coef + T->coef0;
+        for (int i = 0; i < T->n_tx; i++) {
+            const Dav1dGpuTx *x = &b->txs[T->tx0 + i];
+            const int x4 = x->w0 & 15, y4 = (x->w0 >> 4) & 15, tx = (x->w0 >> 8) & 31, tp = (x->w0 >> 13) & 31;
+            const int nzw = (x->w0 >> 18) & 63, nzh = (x->w0 >> 24) & 63;
+            const int h = txdim[tx].h;
+            const int sh = mini(h, 32);
+            coef *src = pool + (x->w1 & 0xffff);
+            memset(cf, 0, sizeof(cf));
+            int eob;
+            if (nzw == 0) {
+                cf[0] = src[0];
+                eob = 0;
+                if (b->zero_coefs) src[0] = 0;
+            } else {
+                for (int xx = 0; xx < nzw; xx++)
+                    for (int yy = 0; yy < nzh; yy++) {
+                        cf[yy + xx * sh] = src[yy + xx * nzh];
+                        if (b->zero_coefs) src[yy + xx * nzh] = 0;
+                    }
+                eob = 1;
+            }
+            itx_all[tx][tp](tdst + (ptrdiff_t)(y4 * 4) * PX(ds) + x4 * 4, ds, cf, eob
+#if BITDEPTH == 16
+                            , bdmax
+#endif
+                            );
+        }
     }
     return 0;
 }

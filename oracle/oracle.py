@@ -35,6 +35,9 @@ def load():
             f = getattr(L, f"oracle_recon_units_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(abi.FrameBatch), ctypes.c_int, ctypes.c_int]
             f.restype = ctypes.c_int
+            f = getattr(L, f"oracle_recon_tiles_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(abi.TileBatch), ctypes.c_int, ctypes.c_int]
+            f.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -103,6 +106,72 @@ class HostFrame:
         bounds = np.linspace(u0, u1, threads + 1).astype(int)
         ts = [threading.Thread(target=fn, args=(ctypes.byref(self.batch), int(bounds[i]),
                                                 int(bounds[i + 1]))) for i in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+
+
+class HostTiles:
+    """A TileData (dav1d_mirror_amd.tiles.build_tiles) reconstructed on the
+    CPU by the oracle's tile walker: per tile, the reference's DSP calls for
+    each pred (mc with recon_tmpl.c's emu_edge condition, intra, CfL, pal,
+    warp, inter-intra) and each transform block."""
+
+    def __init__(self, fd, td, zero_coefs=False):
+        abi = _abi()
+        self.fd, self.td = fd, td
+        pdt = fd.cfg.pixel_dtype
+        if getattr(fd, "dst_init", None) is not None:
+            self.dst = [a.copy() for a in fd.dst_init]
+        else:
+            self.dst = [np.zeros((h, w), pdt) for (w, h) in fd.plane_wh]
+        self.tiles = np.ascontiguousarray(td.tiles)
+        self.preds = np.ascontiguousarray(td.preds)
+        self.txs = np.ascontiguousarray(td.txs)
+        self.coefs = td.coefs.copy()
+        self.edges = np.ascontiguousarray(td.edges)
+        self.aux_pool = None if td.aux_pool is None else np.ascontiguousarray(td.aux_pool)
+        self.refs = fd.refs
+        self.cfl_luma = np.ascontiguousarray(fd.cfl_luma)
+        bpp = 1 if fd.cfg.bpc == 8 else 2
+        b = abi.TileBatch()
+        for p in range(3):
+            w, h = fd.plane_wh[p]
+            b.dst[p].data = self.dst[p].ctypes.data
+            b.dst[p].stride = w * bpp
+            b.dst[p].w, b.dst[p].h = w, h
+            for r in range(len(self.refs)):
+                a = self.refs[r][p]
+                b.ref[r][p].data = a.ctypes.data + fd.ref_origin_offset(p) * bpp
+                b.ref[r][p].stride = a.shape[1] * bpp
+                b.ref[r][p].w, b.ref[r][p].h = w, h
+        b.tiles = self.tiles.ctypes.data
+        b.n_tiles = len(self.tiles)
+        b.n_tiles_huge = td.n_tiles_huge
+        b.bitdepth_max = fd.cfg.bitdepth_max if fd.cfg.bpc == 16 else 255
+        b.preds = self.preds.ctypes.data
+        b.txs = self.txs.ctypes.data
+        b.coef = self.coefs.ctypes.data
+        b.edges = self.edges.ctypes.data
+        b.aux_pool = None if self.aux_pool is None else self.aux_pool.ctypes.data
+        b.cfl_luma.data = self.cfl_luma.ctypes.data
+        b.cfl_luma.stride = self.cfl_luma.shape[1] * bpp
+        b.cfl_luma.w, b.cfl_luma.h = fd.plane_wh[0]
+        b.cfl_ss = 3
+        b.zero_coefs = 1 if zero_coefs else 0
+        self.batch = b
+
+    def run(self, threads=1):
+        L = load()
+        fn = L.oracle_recon_tiles_8bpc if self.fd.cfg.bpc == 8 else L.oracle_recon_tiles_16bpc
+        n = len(self.tiles)
+        if threads <= 1:
+            fn(ctypes.byref(self.batch), 0, n)
+            return
+        bounds = np.linspace(0, n, threads + 1).astype(int)
+        ts = [threading.Thread(target=fn, args=(ctypes.byref(self.batch), int(bounds[i]), int(bounds[i + 1])))
+              for i in range(threads)]
         for t in ts:
             t.start()
         for t in ts:

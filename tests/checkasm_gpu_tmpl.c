@@ -67,8 +67,10 @@ static void BD(check_mc)(void) {
         for (int w = 2; w <= 128; w <<= 1)
             for (int mxy = 0; mxy < 4; mxy++) {
                 const int h_min = w <= 32 ? 2 : w / 4, h_max = imax(imin(w * 4, 128), 32);
-                for (int h = h_min; h <= h_max; h = mc_h_next(h)) {
-                    if (g_quick && (rnd() & 3)) continue;
+                int hi = 0;
+                for (int h = h_min; h <= h_max; h = mc_h_next(h), hi++) {
+                    /* quick: every (filter, w, h) cell once, the sub-pel case rotating */
+                    if (g_quick && ((f + hi + w) & 3) != mxy) continue;
                     const int mx = (mxy & 1) ? rnd() % 15 + 1 : 0, my = (mxy & 2) ? rnd() % 15 + 1 : 0;
                     const int bdmax = BDMAX_RAND();
                     for (int i = 0; i < 135 * 135; i++) src_buf[i] = rnd() & bdmax;
@@ -83,8 +85,8 @@ static void BD(check_mc)(void) {
     for (int f = 0; f < DGPU_N_2D_FILTERS; f++)
         for (int w = 4; w <= 128; w <<= 1)
             for (int mxy = 0; mxy < 4; mxy++)
-                for (int h = imax(w / 4, 4); h <= imin(w * 4, 128); h <<= 1) {
-                    if (g_quick && (rnd() & 3)) continue;
+                for (int h = imax(w / 4, 4), hi = 0; h <= imin(w * 4, 128); h <<= 1, hi++) {
+                    if (g_quick && ((f + hi + w) & 3) != mxy) continue;
                     const int mx = (mxy & 1) ? rnd() % 15 + 1 : 0, my = (mxy & 2) ? rnd() % 15 + 1 : 0;
                     const int bdmax = BDMAX_RAND();
                     static const int8_t pat[8] = { -1, 0, -1, 0, 0, -1, 0, -1 };
@@ -103,8 +105,10 @@ static void BD(check_mc)(void) {
         for (int w = 2; w <= 128; w <<= 1)
             for (int p = 0; p < 3; p++) {
                 const int h_min = w <= 32 ? 2 : w / 4, h_max = imax(imin(w * 4, 128), 32);
-                for (int h = h_min; h <= h_max; h = mc_h_next(h)) {
-                    if (g_quick && (rnd() & 7)) continue;
+                int hi = 0;
+                for (int h = h_min; h <= h_max; h = mc_h_next(h), hi++) {
+                    /* quick: every (filter, w, h) cell once, the dy kind rotating */
+                    if (g_quick && (f + hi + w) % 3 != p) continue;
                     const int mx = rnd() % 1024, my = rnd() % 1024, dx = rnd() % 2048 + 1;
                     const int dy = !p ? (int)(rnd() % 2048 + 1) : p << 10;
                     const int bdmax = BDMAX_RAND();
@@ -126,7 +130,6 @@ static void BD(check_mc)(void) {
     for (int kind = 0; kind < 6; kind++)
         for (int w = 4; w <= 128; w <<= 1)
             for (int h = imax(w / 4, 4); h <= imin(w * 4, 128); h <<= 1) {
-                if (g_quick && (rnd() & 1)) continue;
                 const int bdmax = BDMAX_RAND();
                 for (int i = 0; i < 2; i++) {
                     for (int k = 0; k < 135 * 135; k++) src_buf[k] = rnd() & bdmax;

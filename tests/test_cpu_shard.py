@@ -67,7 +67,9 @@ def _feed_worker(rank, world, port, q):
     import dav1d_mirror_amd.workload as wl
     import dav1d_mirror_amd.shard as sh
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    base = wl.FrameConfig(width=256, height=128, kind="itx" if world == 3 else "full")
+    # world 2: a full frame; 3: an itx frame (dst_init); 4: an ext frame (aux,
+    # aux_pool and class_warp: mask / palette / warp / inter-intra units)
+    base = wl.FrameConfig(width=256, height=128, kind={2: "full", 3: "itx", 4: "ext"}[world])
     fd, secs, nbytes = sh.feed_frame(lambda r: sh.rank_config(base, r), rank, world, dist, "cpu")
     ref = wl.make_frame(sh.rank_config(base, rank))   # what this rank must have received
     same = (fd.units.tobytes() == ref.units.tobytes() and np.array_equal(fd.class_start, ref.class_start)
@@ -75,6 +77,8 @@ def _feed_worker(rank, world, port, q):
             and np.array_equal(fd.cfl_luma, ref.cfl_luma)
             and all(np.array_equal(fd.refs[k][p], ref.refs[k][p]) for k in range(2) for p in range(3))
             and (ref.dst_init is None or all(np.array_equal(fd.dst_init[p], ref.dst_init[p]) for p in range(3)))
+            and all((getattr(ref, k) is None and getattr(fd, k) is None)
+                    or np.array_equal(getattr(fd, k), getattr(ref, k)) for k in ("aux", "aux_pool", "class_warp", "src_xy"))
             and fd.stats == ref.stats)
     q.put((rank, same, nbytes))
     dist.destroy_process_group()
@@ -84,7 +88,7 @@ def test_rccl_feed_scatter_gloo():
     """bench.py --feed rccl: rank 0 generates every frame and sends frame r
     to rank r (send/recv, the same calls RCCL runs over xGMI); each rank
     ends up with exactly the frame it would have generated itself."""
-    for world in (2, 3):
+    for world in (2, 3, 4):
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         port = _free_port()

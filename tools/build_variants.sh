@@ -15,7 +15,7 @@ build() {
     done
     wait
     local objs=""
-    for s in runtime mc ipred itx recon8 recon16; do
+    for s in runtime mc ipred itx recon8 recon16 tile8 tile16; do
         if [ -f build/var/$name.$s.o ] && [[ " ${TUS:-recon8 recon16} " == *" $s "* ]]; then objs="$objs build/var/$name.$s.o"; else objs="$objs build/$s.o"; fi
     done
     $HIPCC $F -shared -o libdav1d_gpu.$name.so $objs
@@ -29,6 +29,9 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         vmem1x8) build vmem1x8 -DDGPU_PAD_VMEM1=8 ;;
         fakecoal) build fakecoal -DDGPU_FAKE_COALESCE=1 ;;
         valu200) build valu200 -DDGPU_PAD_VALU=200 ;;
+        t1|t2|t4|t8|t16|t3|t6|t7|t15|t31) TUS=tile8 build $v -DDGPU_TILE_ABL=${v#t} ;;
+        ttrace) TUS=tile8 build ttrace -DDGPU_TILE_TRACE=1 ;;
+        twpe2|twpe4|twpe5) TUS=tile8 build $v -DDGPU_TILE_WPE=${v#twpe} ;;
         nomc) build nomc -DDGPU_ABL_MC=1 ;;
         noitx) build noitx -DDGPU_ABL_ITX=1 ;;
         nointra) build nointra -DDGPU_ABL_INTRA=1 ;;

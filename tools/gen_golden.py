@@ -25,6 +25,11 @@ CASES = [
     ("full10", dict(width=128, height=64, bpc=16, bitdepth_max=1023, seed=4)),
     ("full12", dict(width=128, height=64, bpc=16, bitdepth_max=4095, seed=5)),
     ("full8_tx64", dict(width=256, height=128, seed=6, tx64=True)),
+    ("ext8", dict(width=256, height=128, seed=7, kind="ext")),
+    ("ext12", dict(width=256, height=128, seed=8, kind="ext", bpc=16, bitdepth_max=4095)),
+    # MVs far past the picture on edge-replicated references: the unit walker
+    # reads the replicated padding, the tile walker clamps (emu_edge)
+    ("edge8", dict(width=256, height=128, seed=9, kind="ext", mv_range=200)),
 ]
 
 
