@@ -70,8 +70,8 @@ def cpu_baseline(fd, budget_s=12.0):
 
 
 # rocprofv3 PMC summaries of the current kernels (tools/prof.sh + tools/pmc_summary.py)
-PMC_SUMMARY = {8: os.path.join(ROOT, "profiles", "r1", "r1d_pmc_summary.json"),
-               16: os.path.join(ROOT, "profiles", "r1", "r1d_10bit_pmc_summary.json")}
+PMC_SUMMARY = {8: os.path.join(ROOT, "profiles", "r2", "r2a_pmc_summary.json"),
+               16: os.path.join(ROOT, "profiles", "r2", "r2a_10bit_pmc_summary.json")}
 
 
 def pmc_traffic(bpc):
@@ -135,6 +135,26 @@ def family_breakdown(base_cfg, dev, stream, steps):
     return out
 
 
+def tile_breakdown(fd, dev, stream, steps):
+    """The same frame through the superblock-tile batch (dav1d_gpu_recon_tiles_*):
+    block-level mc with clamped (emu_edge) footprints, one workgroup per
+    64x64 luma / 32x32 chroma tile.  Reported beside the headline unit batch."""
+    import dav1d_mirror_amd.tiles as tl
+    import dav1d_mirror_amd.batch as bt
+    td = tl.build_tiles(fd)
+    frame = bt.DeviceTiles(fd, td, dev)
+    for _ in range(3):
+        frame.launch(stream)
+    ks = kernel_seconds(frame, stream, max(steps, 10))
+    b = td.stats["total_bytes"]
+    out = {"kernel": "k_tiles<bpc, huge=false/true>", "tiles": int(len(td.tiles)), "preds": int(len(td.preds)),
+           "txs": int(len(td.txs)), "kernel_us": round(ks * 1e6, 2),
+           "gpix_s": round(fd.stats["pixels"] / ks / 1e9, 2), "algorithmic_bytes": b,
+           "achieved_gbs": round(b / ks / 1e9, 1), "frac": round(b / ks / 1e9 / HBM_PEAK_GBS, 4)}
+    del frame
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,6 +166,7 @@ def main():
     ap.add_argument("--feed", default="local", choices=["local", "rccl"],
                     help="local: each rank generates its frame; rccl: rank 0 generates all and scatters")
     ap.add_argument("--no-families", action="store_true", help="skip the per-family breakdown (N=1)")
+    ap.add_argument("--no-tiles", action="store_true", help="skip the tile-batch measurement (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -265,6 +286,8 @@ def main():
             out["feed"] = feed
         if not args.no_families and world == 1 and c.get("kind") == "full":
             out["families"] = family_breakdown(cfg, dev, stream, args.steps)
+        if not args.no_tiles and world == 1:
+            out["tile_batch"] = tile_breakdown(fd, dev, stream, args.steps)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
         print(json.dumps(out), flush=True)

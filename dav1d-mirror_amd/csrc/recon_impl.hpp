@@ -207,7 +207,7 @@ static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned
     constexpr int lds = WPB * wave_lds<BPC, GRP>();
     static std::once_flag once;
     std::call_once(once, [] {
-        hipFuncSetAttribute((const void *)k_recon<BPC, GRP>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void *)k_recon<BPC, GRP>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     });
     k_recon<BPC, GRP><<<dim3(nblk), 64 * WPB, lds, stream>>>(a);
     const hipError_t e = hipGetLastError();
@@ -291,7 +291,7 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
                 free(h);
             }
             if (fp) fclose(fp);
-            hipMemset(trace_buf, 0, (size_t)3 << 23);
+            (void)hipMemset(trace_buf, 0, (size_t)3 << 23);
         }
     }
     return rc;

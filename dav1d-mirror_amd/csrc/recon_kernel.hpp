@@ -45,6 +45,9 @@
 #ifndef DGPU_ABL_INTRA
 #define DGPU_ABL_INTRA 0   // skip intra edge preparation and prediction
 #endif
+#ifndef DGPU_ABL_STORE
+#define DGPU_ABL_STORE 0   // skip the picture stores (probe)
+#endif
 #ifndef DGPU_EARLY_REF1
 #define DGPU_EARLY_REF1 0  // issue the second ref's footprint loads up front
 #endif
@@ -1309,10 +1312,14 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             const int o1 = clampi(pv[4 * rr + 1] + rv[4 * rr + 1], 0, bdmax);
             const int o2 = clampi(pv[4 * rr + 2] + rv[4 * rr + 2], 0, bdmax);
             const int o3 = clampi(pv[4 * rr + 3] + rv[4 * rr + 3], 0, bdmax);
+#if DGPU_ABL_STORE   // cost-model probe: no picture stores (values kept alive)
+            asm volatile("" ::"v"((uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24), "v"(row));
+#else
             if constexpr (BPC == 8)
                 gst<uint32_t>(row, (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24);
             else
                 gst<u32x2>(row, u32x2{(uint32_t)o0 | o1 << 16, (uint32_t)o2 | (uint32_t)o3 << 16});
+#endif
         }
     };
 

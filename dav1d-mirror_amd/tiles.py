@@ -250,7 +250,13 @@ def build_tiles(fd):
     assert np.all(u["txtp"][xu] < abi.WHT_WHT), "WHT_WHT (lossless) is not in the tile batch"
     xl = tx_lanes(tw[xu], th[xu])
     xtile = tid[xu]
-    xorder = np.lexsort((u["tx"][xu], u["txtp"][xu], -xl, xtile))
+    # inside a lane-count group: by width, height, then the 1-D kinds (ADST
+    # and FLIPADST share a body), so a wave's lanes mostly run one row path
+    # and one column path
+    kc = np.array([0, 1, 1, 2])   # DCT, ADST, FLIPADST, IDENTITY -> body
+    kh = kc[(0xb73da850 >> (2 * u["txtp"][xu].astype(np.int64))) & 3]
+    kv = kc[(0xedce6244 >> (2 * u["txtp"][xu].astype(np.int64))) & 3]
+    xorder = np.lexsort((u["txtp"][xu], kv, kh, th[xu], tw[xu], -xl, xtile))
     xu, xl, xtile = xu[xorder], xl[xorder], xtile[xorder]
     tile_tx_count = np.bincount(xtile, minlength=n_tiles_all)
     tx0 = np.cumsum(tile_tx_count) - tile_tx_count

@@ -92,3 +92,22 @@ def test_tiles_idempotent(oracle):
     torch.cuda.synchronize()
     for a, b in zip(first, dev.planes_host()):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("kind,bpc,bdmax", [("full", 8, 255), ("ext", 8, 255), ("full", 16, 1023)])
+def test_tiles_equal_unit_batch(oracle, kind, bpc, bdmax):
+    """Both batch tiers on one frame whose MVs reach 200 px past the picture:
+    the unit batch reads the edge-replicated reference padding (the caller's
+    emu_edge, as dav1d's DSP functions expect), the tile batch clamps
+    (recon_tmpl.c's mc() emu_edge); the pictures are identical."""
+    import torch
+    import dav1d_mirror_amd.batch as bt
+    import dav1d_mirror_amd.tiles as tl
+    fd = _frame(width=512, height=256, seed=33, kind=kind, mv_range=200, bpc=bpc, bitdepth_max=bdmax)
+    du = bt.DeviceFrame(fd, "cuda:0")
+    du.launch()
+    dt = bt.DeviceTiles(fd, tl.build_tiles(fd), "cuda:0")
+    dt.launch()
+    torch.cuda.synchronize()
+    for a, b in zip(du.planes_host(), dt.planes_host()):
+        assert np.array_equal(a, b)

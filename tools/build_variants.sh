@@ -33,6 +33,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         ttrace) TUS=tile8 build ttrace -DDGPU_TILE_TRACE=1 ;;
         twpe2|twpe4|twpe5) TUS=tile8 build $v -DDGPU_TILE_WPE=${v#twpe} ;;
         nomc) build nomc -DDGPU_ABL_MC=1 ;;
+        nostore) build nostore -DDGPU_ABL_STORE=1 ;;
         noitx) build noitx -DDGPU_ABL_ITX=1 ;;
         nointra) build nointra -DDGPU_ABL_INTRA=1 ;;
         none) build none -DDGPU_ABL_MC=1 -DDGPU_ABL_ITX=1 -DDGPU_ABL_INTRA=1 ;;

@@ -16,8 +16,9 @@ import os
 
 
 def short(name):
-    if "k_recon" in name:
-        return name[name.index("k_recon"):].split("(")[0]
+    for k in ("k_recon", "k_tiles"):
+        if k in name:
+            return name[name.index(k):].split("(")[0]
     return None
 
 
