@@ -106,6 +106,24 @@ class TileBatch(ctypes.Structure):
                 ("zero_coefs", ctypes.c_int32)]
 
 
+# Dav1dGpuIntraEdge (16 bytes) and its batch: device dav1d_prepare_intra_edges
+INTRA_EDGE_DTYPE = np.dtype([("unit", "<i4"), ("x4", "<i2"), ("y4", "<i2"), ("w4", "<i2"), ("h4", "<i2"),
+                             ("mode", "u1"), ("angle", "i1"), ("flags", "u1"), ("pad", "u1")])
+IE_HAVE_LEFT, IE_HAVE_TOP, IE_TOP_HAS_RIGHT, IE_LEFT_HAS_BOTTOM = 1, 2, 4, 8
+IE_FILTER_EDGE, IE_SMOOTH, IE_TOP_SB_EDGE = 16, 32, 64
+
+
+class IntraEdgeBatch(ctypes.Structure):
+    _fields_ = [("pic", Plane * 3),
+                ("top_edge", Plane * 3),
+                ("sb_log2", ctypes.c_int32 * 3),
+                ("units", ctypes.c_void_p),
+                ("edges", ctypes.c_void_p),
+                ("recs", ctypes.c_void_p),
+                ("n_recs", ctypes.c_int32),
+                ("bitdepth_max", ctypes.c_int32)]
+
+
 _LIB = None
 
 
@@ -136,6 +154,10 @@ def load_lib():
             f = getattr(L, f"dav1d_gpu_recon_tiles_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(TileBatch), ctypes.c_void_p]
             f.restype = ctypes.c_int
+        for bpc in (8, 16):
+            f = getattr(L, f"dav1d_gpu_prepare_intra_edges_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(IntraEdgeBatch), ctypes.c_void_p]
+            f.restype = ctypes.c_int
         L.dav1d_gpu_recon_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         L.dav1d_gpu_recon_lds_bytes.restype = ctypes.c_int
         _LIB = L
@@ -153,4 +175,5 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version",
     "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc", "dav1d_gpu_recon_lds_bytes",
     "dav1d_gpu_recon_tiles_8bpc", "dav1d_gpu_recon_tiles_16bpc",
+    "dav1d_gpu_prepare_intra_edges_8bpc", "dav1d_gpu_prepare_intra_edges_16bpc",
 ]

@@ -480,6 +480,57 @@ typedef struct Dav1dGpuTileBatch {
 int dav1d_gpu_recon_tiles_8bpc(const Dav1dGpuTileBatch *b, void *stream);
 int dav1d_gpu_recon_tiles_16bpc(const Dav1dGpuTileBatch *b, void *stream);
 
+/* ---- intra edge preparation ---------------------------
+ * Device form of bytefn(dav1d_prepare_intra_edges) (src/ipred_prepare_tmpl.c:
+ * 76-204, declared src/ipred_prepare.h:78-86) for a batch of intra transform
+ * blocks: each record gathers its block's edge array (top-left, top,
+ * top-right, left, bottom-left, extended as the function does when edges are
+ * missing) from the reconstructed picture into the unit batch's edge pool
+ * and rewrites its unit's mode (the implementation index the function
+ * returns) and angle (the absolute angle | the smooth / edge-filter flags of
+ * recon_tmpl.c:1238-1294).  With it, dependent intra blocks chain on the
+ * device: prepare the edges of one dependency level, reconstruct it with
+ * dav1d_gpu_recon_*, then the next level, all on one stream. */
+typedef struct Dav1dGpuIntraEdge {   /* 16 bytes */
+    int32_t unit;        /* the Dav1dGpuUnit it serves: its plane, tx size
+                            (tw, th), dst_off (block position) and edge_off
+                            (where topleft[0] goes) are read, its
+                            p.intra.mode / angle written                    */
+    int16_t x4, y4;      /* block position in the plane, 4-px units          */
+    int16_t w4, h4;      /* the dependent tile's end (col_end, row_end)      */
+    uint8_t mode;        /* IntraPredMode as coded: DC, V, H, the six
+                            directional modes, SMOOTH*, PAETH, FILTER (13)   */
+    int8_t  angle;       /* angle_delta -3..3 (FILTER: the filter index)      */
+    uint8_t flags;       /* DGPU_IE_* below                                   */
+    uint8_t pad_;
+} Dav1dGpuIntraEdge;
+
+#define DGPU_IE_HAVE_LEFT      1   /* x4 > tile col_start                   */
+#define DGPU_IE_HAVE_TOP       2   /* y4 > tile row_start                   */
+#define DGPU_IE_TOP_HAS_RIGHT  4   /* EDGE_I444_TOP_HAS_RIGHT of edge_flags  */
+#define DGPU_IE_LEFT_HAS_BOTTOM 8  /* EDGE_I444_LEFT_HAS_BOTTOM              */
+#define DGPU_IE_FILTER_EDGE   16   /* seq_hdr->intra_edge_filter             */
+#define DGPU_IE_SMOOTH        32   /* a neighbour is SMOOTH* (sm_flag)        */
+#define DGPU_IE_TOP_SB_EDGE   64   /* top row from top_edge[] (the block is at
+                                      a superblock's top: prefilter_toplevel_
+                                      sb_edge, recon_tmpl.c:1270-1275)       */
+
+typedef struct Dav1dGpuIntraEdgeBatch {
+    Dav1dGpuPlane pic[3];       /* reconstructed picture (read)               */
+    Dav1dGpuPlane top_edge[3];  /* row r = the pre-filter row above superblock
+                                   row r + 1 (f->ipred_edge); may be NULL when
+                                   no record sets DGPU_IE_TOP_SB_EDGE        */
+    int32_t  sb_log2[3];        /* superblock height in the plane, log2 px    */
+    Dav1dGpuUnit *units;        /* device, read / written                      */
+    void    *edges;             /* device edge pool (written)                  */
+    const Dav1dGpuIntraEdge *recs;
+    int32_t  n_recs;
+    int32_t  bitdepth_max;
+} Dav1dGpuIntraEdgeBatch;
+
+int dav1d_gpu_prepare_intra_edges_8bpc(const Dav1dGpuIntraEdgeBatch *b, void *stream);
+int dav1d_gpu_prepare_intra_edges_16bpc(const Dav1dGpuIntraEdgeBatch *b, void *stream);
+
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split
  * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).

@@ -1757,3 +1757,107 @@ int SFX(oracle_recon_tiles)(const Dav1dGpuTileBatch *b, int t0, int t1)
     }
     return 0;
 }
+
+/* ================================================ intra edge preparation */
+
+/* bytefn(dav1d_prepare_intra_edges), src/ipred_prepare_tmpl.c:76-204, for
+ * one record of a Dav1dGpuIntraEdgeBatch (host pointers): the mode remap
+ * (:83-104, tables :38-75), then each edge the remapped mode needs, copied
+ * from the picture or extended as the reference does when it is missing.
+ * Edges the mode does not need are left untouched. */
+static const uint8_t ie_needs[14] = {   /* bit0 left, 1 top, 2 topleft, 3 topright, 4 bottomleft */
+    /* DC */ 3, /* V */ 2, /* H */ 1, /* LEFT_DC */ 1, /* TOP_DC */ 2, /* DC_128 */ 0,
+    /* Z1 */ 2 | 4 | 8, /* Z2 */ 1 | 2 | 4, /* Z3 */ 1 | 4 | 16, /* SMOOTH* */ 3, 3, 3,
+    /* PAETH */ 7, /* FILTER */ 7 };
+
+static int ie_remap(int mode, int have_left, int have_top, int *angle)
+{
+    static const uint8_t dir_angle[8] = { 90, 180, 45, 135, 113, 157, 203, 67 };
+    if (mode >= 1 && mode <= 8) {   /* VERT .. VERT_LEFT */
+        *angle = dir_angle[mode - 1] + 3 * *angle;
+        if (*angle <= 90) return *angle < 90 && have_top ? DGPU_Z1_PRED : DGPU_VERT_PRED;
+        if (*angle < 180) return DGPU_Z2_PRED;
+        return *angle > 180 && have_left ? DGPU_Z3_PRED : DGPU_HOR_PRED;
+    }
+    if (mode == 0)   /* DC: DC_128 / TOP_DC / LEFT_DC / DC by (have_left, have_top) */
+        return have_left ? (have_top ? DGPU_DC_PRED : DGPU_LEFT_DC_PRED)
+                         : (have_top ? DGPU_TOP_DC_PRED : DGPU_DC_128_PRED);
+    if (mode == 12)  /* PAETH: DC_128 / V / H / PAETH */
+        return have_left ? (have_top ? DGPU_PAETH_PRED : DGPU_HOR_PRED)
+                         : (have_top ? DGPU_VERT_PRED : DGPU_DC_128_PRED);
+    return mode;     /* SMOOTH*, FILTER keep their index */
+}
+
+int SFX(oracle_prepare_intra_edges)(const Dav1dGpuIntraEdgeBatch *b)
+{
+    const int bdmax = BITDEPTH == 8 ? 255 : b->bitdepth_max;
+    const int half = (bdmax + 1) >> 1;
+    pixel *pool = (pixel *)b->edges;
+    for (int i = 0; i < b->n_recs; i++) {
+        const Dav1dGpuIntraEdge *r = &b->recs[i];
+        Dav1dGpuUnit *u = &b->units[r->unit];
+        const int pl = u->plane;
+        const ptrdiff_t ps = PX(b->pic[pl].stride);
+        const pixel *dst = (const pixel *)b->pic[pl].data + (ptrdiff_t)r->y4 * 4 * ps + r->x4 * 4;
+        const int tw = txdim[u->tx].w >> 2, th = txdim[u->tx].h >> 2;
+        const int have_left = r->flags & DGPU_IE_HAVE_LEFT, have_top = r->flags & DGPU_IE_HAVE_TOP;
+        int angle = r->angle;
+        const int mode = ie_remap(r->mode, !!have_left, !!have_top, &angle);
+        const int nd = ie_needs[mode];
+        pixel *tl = pool + u->p.intra.edge_off;
+        const pixel *top = NULL;
+        if (have_top && ((nd & 2) || (nd & 4) || ((nd & 1) && !have_left))) {
+            if (r->flags & DGPU_IE_TOP_SB_EDGE)
+                top = (const pixel *)b->top_edge[pl].data +
+                      (ptrdiff_t)(((r->y4 * 4) >> b->sb_log2[pl]) - 1) * PX(b->top_edge[pl].stride) + r->x4 * 4;
+            else
+                top = dst - ps;
+        }
+        if (nd & 1) {   /* left, then bottom-left (:124-154) */
+            const int sz = th * 4;
+            if (have_left) {
+                const int n = mini(sz, (r->h4 - r->y4) * 4);
+                for (int k = 0; k < sz; k++) tl[-1 - k] = dst[(ptrdiff_t)mini(k, n - 1) * ps - 1];
+            } else {
+                for (int k = 0; k < sz; k++) tl[-1 - k] = have_top ? top[0] : half + 1;
+            }
+            if (nd & 16) {
+                const int hbl = have_left && r->y4 + th < r->h4 && (r->flags & DGPU_IE_LEFT_HAS_BOTTOM);
+                if (hbl) {
+                    const int n = mini(sz, (r->h4 - r->y4 - th) * 4);
+                    for (int k = 0; k < sz; k++) tl[-1 - sz - k] = dst[(ptrdiff_t)(sz + mini(k, n - 1)) * ps - 1];
+                } else {
+                    for (int k = 0; k < sz; k++) tl[-1 - sz - k] = tl[-sz];
+                }
+            }
+        }
+        if (nd & 2) {   /* top, then top-right (:156-185) */
+            const int sz = tw * 4;
+            if (have_top) {
+                const int n = mini(sz, (r->w4 - r->x4) * 4);
+                for (int k = 0; k < sz; k++) tl[1 + k] = top[mini(k, n - 1)];
+            } else {
+                for (int k = 0; k < sz; k++) tl[1 + k] = have_left ? dst[-1] : half - 1;
+            }
+            if (nd & 8) {
+                const int htr = have_top && r->x4 + tw < r->w4 && (r->flags & DGPU_IE_TOP_HAS_RIGHT);
+                if (htr) {
+                    const int n = mini(sz, (r->w4 - r->x4 - tw) * 4);
+                    for (int k = 0; k < sz; k++) tl[1 + sz + k] = top[sz + mini(k, n - 1)];
+                } else {
+                    for (int k = 0; k < sz; k++) tl[1 + sz + k] = tl[sz];
+                }
+            }
+        }
+        if (nd & 4) {   /* top-left (:187-201) */
+            if (have_left) tl[0] = have_top ? top[-1] : dst[-1];
+            else tl[0] = have_top ? top[0] : half;
+            if (mode == DGPU_Z2_PRED && tw + th >= 6 && (r->flags & DGPU_IE_FILTER_EDGE))
+                tl[0] = (pixel)(((tl[-1] + tl[1]) * 5 + tl[0] * 6 + 8) >> 4);
+        }
+        u->p.intra.mode = (uint8_t)mode;
+        u->p.intra.angle = (uint16_t)((angle & 511) | ((r->flags & DGPU_IE_SMOOTH) ? 512 : 0) |
+                                      ((r->flags & DGPU_IE_FILTER_EDGE) ? 1024 : 0));
+    }
+    return 0;
+}

@@ -12,4 +12,8 @@ void oracle_itx_dsp_init_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc);
 int oracle_itx_supported_8bpc(int tx, int tp);
 int oracle_recon_units_8bpc(const Dav1dGpuFrameBatch *b, int u0, int u1);
 int oracle_recon_units_16bpc(const Dav1dGpuFrameBatch *b, int u0, int u1);
+int oracle_recon_tiles_8bpc(const Dav1dGpuTileBatch *b, int t0, int t1);
+int oracle_recon_tiles_16bpc(const Dav1dGpuTileBatch *b, int t0, int t1);
+int oracle_prepare_intra_edges_8bpc(const Dav1dGpuIntraEdgeBatch *b);
+int oracle_prepare_intra_edges_16bpc(const Dav1dGpuIntraEdgeBatch *b);
 #endif

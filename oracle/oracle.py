@@ -38,6 +38,9 @@ def load():
             f = getattr(L, f"oracle_recon_tiles_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(abi.TileBatch), ctypes.c_int, ctypes.c_int]
             f.restype = ctypes.c_int
+            f = getattr(L, f"oracle_prepare_intra_edges_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(abi.IntraEdgeBatch)]
+            f.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -245,3 +248,23 @@ def call_itx(tbl, tx, tp, dst, coef, eob, bdmax=None):
     if hbd:
         a.append(bdmax)
     fn(*a)
+
+
+def prepare_intra_edges(case):
+    """An intra.EdgeCase through the oracle's dav1d_prepare_intra_edges
+    restatement; returns the (units, edge pool) it leaves."""
+    import dav1d_mirror_amd.intra as intra
+    abi = _abi()
+    L = load()
+    pics = [np.ascontiguousarray(a) for a in case.pics]
+    tops = [np.ascontiguousarray(a) for a in case.top_edge]
+    units = case.units.copy()
+    edges = case.edges.copy()
+    recs = np.ascontiguousarray(case.recs)
+    b = intra.fill_batch(abi.IntraEdgeBatch(), case, [a.ctypes.data for a in pics],
+                         [a.ctypes.data for a in tops], units.ctypes.data, edges.ctypes.data,
+                         recs.ctypes.data)
+    fn = getattr(L, f"oracle_prepare_intra_edges_{8 if case.bpc == 8 else 16}bpc")
+    rc = fn(ctypes.byref(b))
+    assert rc == 0
+    return units, edges
