@@ -124,6 +124,18 @@ class IntraEdgeBatch(ctypes.Structure):
                 ("bitdepth_max", ctypes.c_int32)]
 
 
+EDGE_BACKUP_DTYPE = np.dtype([("plane", "<i4"), ("sby", "<i4"), ("x0", "<i4"), ("w", "<i4")])
+
+
+class IntraSchedule(ctypes.Structure):
+    _fields_ = [("n_levels", ctypes.c_int32),
+                ("unit_start", ctypes.c_void_p),
+                ("class_start", ctypes.c_void_p),
+                ("rec_start", ctypes.c_void_p),
+                ("run_start", ctypes.c_void_p),
+                ("runs", ctypes.c_void_p)]
+
+
 _LIB = None
 
 
@@ -158,6 +170,13 @@ def load_lib():
             f = getattr(L, f"dav1d_gpu_prepare_intra_edges_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(IntraEdgeBatch), ctypes.c_void_p]
             f.restype = ctypes.c_int
+            f = getattr(L, f"dav1d_gpu_backup_ipred_edge_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(IntraEdgeBatch), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+            f.restype = ctypes.c_int
+            f = getattr(L, f"dav1d_gpu_recon_intra_frame_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(FrameBatch), ctypes.POINTER(IntraEdgeBatch),
+                          ctypes.POINTER(IntraSchedule), ctypes.c_void_p]
+            f.restype = ctypes.c_int
         L.dav1d_gpu_recon_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         L.dav1d_gpu_recon_lds_bytes.restype = ctypes.c_int
         _LIB = L
@@ -176,4 +195,6 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc", "dav1d_gpu_recon_lds_bytes",
     "dav1d_gpu_recon_tiles_8bpc", "dav1d_gpu_recon_tiles_16bpc",
     "dav1d_gpu_prepare_intra_edges_8bpc", "dav1d_gpu_prepare_intra_edges_16bpc",
+    "dav1d_gpu_backup_ipred_edge_8bpc", "dav1d_gpu_backup_ipred_edge_16bpc",
+    "dav1d_gpu_recon_intra_frame_8bpc", "dav1d_gpu_recon_intra_frame_16bpc",
 ]

@@ -12,6 +12,7 @@
 // edge pixels read (strided for the left column) and written.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
@@ -112,8 +113,9 @@ __global__ __launch_bounds__(256) void k_intra_edges(EdgeArgs<BPC> a) {
         tl[i] = (P)v;
     }
     if (l == 0) {
-        u->p.intra.mode = (uint8_t)mode;
-        u->p.intra.angle = (uint16_t)((angle & 511) | ((r.flags & DGPU_IE_SMOOTH) ? 512 : 0) |
+        u->p.intra.mode = (uint8_t)mode;   // CFL: its DC source (the same byte)
+        if (u->pred != DGPU_PRED_CFL)
+            u->p.intra.angle = (uint16_t)((angle & 511) | ((r.flags & DGPU_IE_SMOOTH) ? 512 : 0) |
                                       ((r.flags & DGPU_IE_FILTER_EDGE) ? 1024 : 0));
     }
 }
@@ -147,6 +149,88 @@ static int launch_edges(const Dav1dGpuIntraEdgeBatch *b, hipStream_t stream) {
     return 0;
 }
 
+// bytefn(dav1d_backup_ipred_edge) for runs of columns: one 64-lane
+// workgroup per run.
+template <int BPC> struct BackupArgs {
+    using P = typename Px<BPC>::pixel;
+    const P *pic[3];
+    int ps[3];
+    P *top[3];
+    int ts[3];
+    int sb_log2[3];
+    const Dav1dGpuEdgeBackup *runs;
+};
+
+template <int BPC>
+__global__ __launch_bounds__(64) void k_backup_edge(BackupArgs<BPC> a) {
+    const Dav1dGpuEdgeBackup r = a.runs[blockIdx.x];
+    const int y = ((r.sby + 1) << a.sb_log2[r.plane]) - 1;
+    const auto *src = a.pic[r.plane] + (size_t)y * a.ps[r.plane] + r.x0;
+    auto *dst = a.top[r.plane] + (size_t)r.sby * a.ts[r.plane] + r.x0;
+    for (int i = threadIdx.x; i < r.w; i += 64) dst[i] = src[i];
+}
+
+template <int BPC>
+static int launch_backup(const Dav1dGpuIntraEdgeBatch *b, const Dav1dGpuEdgeBackup *runs, int n,
+                         hipStream_t stream) {
+    using P = typename Px<BPC>::pixel;
+    constexpr int B = BPC / 8;
+    if (!b || n < 0 || (n && !runs)) return -1;
+    if (!n) return 0;
+    BackupArgs<BPC> a;
+    for (int p = 0; p < 3; p++) {
+        a.pic[p] = (const P *)b->pic[p].data;
+        a.ps[p] = (int)(b->pic[p].stride / B);
+        a.top[p] = (P *)b->top_edge[p].data;
+        a.ts[p] = (int)(b->top_edge[p].stride / B);
+        a.sb_log2[p] = b->sb_log2[p];
+    }
+    a.runs = runs;
+    k_backup_edge<BPC><<<dim3(n), 64, 0, stream>>>(a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        fprintf(stderr, "dav1d-gpu: edge backup launch failed: %s\n", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
+}
+
+// The level loop of the intra wavefront: edges -> recon -> backups per level.
+template <int BPC>
+static int launch_intra_frame(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraEdgeBatch *eb,
+                              const Dav1dGpuIntraSchedule *s, hipStream_t stream) {
+    constexpr int NC = DGPU_N_RECT_TX_SIZES;
+    if (!rb || !eb || !s || s->n_levels < 0) return -1;
+    if (s->n_levels && (!s->unit_start || !s->class_start || !s->rec_start || !s->run_start)) return -1;
+    for (int l = 0; l < s->n_levels; l++) {
+        if (s->unit_start[l + 1] < s->unit_start[l] || s->rec_start[l + 1] < s->rec_start[l] ||
+            s->run_start[l + 1] < s->run_start[l])
+            return -2;
+        const int32_t *cs = s->class_start + (size_t)l * (NC + 1);
+        if (cs[0] != 0 || cs[NC] != s->unit_start[l + 1] - s->unit_start[l]) return -2;
+    }
+    if (s->n_levels && (s->unit_start[0] < 0 || s->unit_start[s->n_levels] > rb->n_units ||
+                        s->rec_start[0] < 0 || s->rec_start[s->n_levels] > eb->n_recs || s->run_start[0] < 0))
+        return -2;
+    Dav1dGpuFrameBatch lb = *rb;
+    memset(lb.class_warp, 0, sizeof(lb.class_warp));
+    Dav1dGpuIntraEdgeBatch le = *eb;
+    for (int l = 0; l < s->n_levels; l++) {
+        le.recs = eb->recs + s->rec_start[l];
+        le.n_recs = s->rec_start[l + 1] - s->rec_start[l];
+        int rc = le.n_recs ? launch_edges<BPC>(&le, stream) : 0;
+        if (rc) return rc;
+        lb.units = rb->units + s->unit_start[l];
+        lb.n_units = s->unit_start[l + 1] - s->unit_start[l];
+        memcpy(lb.class_start, s->class_start + (size_t)l * (NC + 1), sizeof(lb.class_start));
+        rc = BPC == 8 ? dav1d_gpu_recon_8bpc(&lb, stream) : dav1d_gpu_recon_16bpc(&lb, stream);
+        if (rc) return rc;
+        rc = launch_backup<BPC>(eb, s->runs + s->run_start[l], s->run_start[l + 1] - s->run_start[l], stream);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
 }  // namespace dgpu
 
 extern "C" int dav1d_gpu_prepare_intra_edges_8bpc(const Dav1dGpuIntraEdgeBatch *b, void *stream) {
@@ -154,4 +238,20 @@ extern "C" int dav1d_gpu_prepare_intra_edges_8bpc(const Dav1dGpuIntraEdgeBatch *
 }
 extern "C" int dav1d_gpu_prepare_intra_edges_16bpc(const Dav1dGpuIntraEdgeBatch *b, void *stream) {
     return dgpu::launch_edges<16>(b, (hipStream_t)stream);
+}
+extern "C" int dav1d_gpu_backup_ipred_edge_8bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav1dGpuEdgeBackup *runs,
+                                                int n_runs, void *stream) {
+    return dgpu::launch_backup<8>(b, runs, n_runs, (hipStream_t)stream);
+}
+extern "C" int dav1d_gpu_backup_ipred_edge_16bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav1dGpuEdgeBackup *runs,
+                                                 int n_runs, void *stream) {
+    return dgpu::launch_backup<16>(b, runs, n_runs, (hipStream_t)stream);
+}
+extern "C" int dav1d_gpu_recon_intra_frame_8bpc(const Dav1dGpuFrameBatch *recon, const Dav1dGpuIntraEdgeBatch *edges,
+                                                const Dav1dGpuIntraSchedule *s, void *stream) {
+    return dgpu::launch_intra_frame<8>(recon, edges, s, (hipStream_t)stream);
+}
+extern "C" int dav1d_gpu_recon_intra_frame_16bpc(const Dav1dGpuFrameBatch *recon, const Dav1dGpuIntraEdgeBatch *edges,
+                                                 const Dav1dGpuIntraSchedule *s, void *stream) {
+    return dgpu::launch_intra_frame<16>(recon, edges, s, (hipStream_t)stream);
 }

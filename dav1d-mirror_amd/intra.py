@@ -72,10 +72,17 @@ def make_edge_case(seed=1, bpc=8, bitdepth_max=255, n=2000, width=256, height=12
             if rng.random() < 0.6:
                 fl |= bit
         u = int(order[i])
-        units[u]["plane"], units[u]["tx"], units[u]["pred"] = pl, tx, abi.PRED_INTRA
+        cfl = pl > 0 and max(tw, th) <= 8 and rng.random() < 0.3   # CfL: DC source only
+        if cfl:
+            mode, angle, fl = abi.DC_PRED, 0, fl & (abi.IE_HAVE_LEFT | abi.IE_HAVE_TOP | abi.IE_TOP_SB_EDGE)
+            units[u]["cfl_alpha"] = int(rng.integers(1, 17))
+            units[u]["cfl_pad_wh"] = 0x21
+        units[u]["plane"], units[u]["tx"] = pl, tx
+        units[u]["pred"] = abi.PRED_CFL if cfl else abi.PRED_INTRA
         units[u]["txtp"] = abi.NO_RESIDUAL
         units[u]["edge_off"] = off + 8 * th
-        units[u]["max_w"], units[u]["max_h"] = tw * 4, th * 4
+        if not cfl:
+            units[u]["max_w"], units[u]["max_h"] = tw * 4, th * 4
         off += 8 * th + 8 * tw + 1
         recs[i] = (u, x4, y4, w4, h4, mode, angle, fl, 0)
     edges = rng.integers(0, bdmax + 1, off).astype(pdt)
@@ -128,3 +135,385 @@ class DeviceEdges:
         units = self.units.cpu().numpy().view(abi.UNIT_DTYPE)
         e = self.edges.cpu().numpy()
         return units, (e if self.case.bpc == 8 else e.view(np.uint16))
+
+
+# ---------------------------------------------------------------- wavefront
+# Host mirror of the function's mode remap and edge needs (the scheduler must
+# know which neighbours a record reads): av1_mode_to_angle_map,
+# av1_mode_conv and av1_intra_prediction_edges, src/ipred_prepare_tmpl.c:38-75.
+_DIR_ANGLE = (90, 180, 45, 135, 113, 157, 203, 67)
+_NEED_L, _NEED_T, _NEED_TL, _NEED_TR, _NEED_BL = 1, 2, 4, 8, 16
+_NEEDS = (3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7)
+
+
+def remap_mode(mode, angle, have_left, have_top):
+    """(implementation mode, angle) as dav1d_prepare_intra_edges returns them."""
+    if 1 <= mode <= 8:
+        angle = _DIR_ANGLE[mode - 1] + 3 * angle
+        if angle <= 90:
+            return (abi.Z1_PRED if angle < 90 and have_top else abi.VERT_PRED), angle
+        if angle < 180:
+            return abi.Z2_PRED, angle
+        return (abi.Z3_PRED if angle > 180 and have_left else abi.HOR_PRED), angle
+    if mode == abi.DC_PRED:
+        return ((abi.DC_PRED if have_top else abi.LEFT_DC_PRED) if have_left else
+                (abi.TOP_DC_PRED if have_top else abi.DC_128_PRED)), angle
+    if mode == abi.PAETH_PRED:
+        return ((abi.PAETH_PRED if have_top else abi.HOR_PRED) if have_left else
+                (abi.VERT_PRED if have_top else abi.DC_128_PRED)), angle
+    return mode, angle
+
+
+@dataclass
+class IntraConfig:
+    width: int = 512
+    height: int = 256
+    bpc: int = 8
+    bitdepth_max: int = 255
+    seed: int = 1
+    cfl_frac: float = 0.4
+    filter_edge: bool = True
+    tx64: bool = True
+    sb_log2: int = 6          # 64x64 superblocks
+
+    @property
+    def pixel_dtype(self):
+        return np.uint8 if self.bpc == 8 else np.uint16
+
+    @property
+    def coef_dtype(self):
+        return np.int16 if self.bpc == 8 else np.int32
+
+
+@dataclass
+class IntraFrame:
+    cfg: IntraConfig
+    plane_wh: list
+    units: np.ndarray        # abi.UNIT_DTYPE, level order (size classes inside a level)
+    coefs: np.ndarray
+    edges: np.ndarray        # edge pool (written by the edge stage)
+    recs: np.ndarray         # INTRA_EDGE_DTYPE, level order
+    runs: np.ndarray         # abi.EDGE_BACKUP_DTYPE, level order (per column run)
+    unit_start: np.ndarray   # int32 [n_levels + 1]
+    class_start: np.ndarray  # int32 [n_levels, N_TX + 1]
+    rec_start: np.ndarray
+    run_start: np.ndarray
+    steps: np.ndarray        # int32 [n, 2]: the decoder's own order (0 unit / 1 oracle run)
+    unit_rec: np.ndarray     # int32 per unit: its record or -1
+    oracle_runs: np.ndarray  # whole-row backups at superblock-row ends
+    top_rows: list           # top_edge shapes (rows, w) per plane
+    sb_log2: tuple
+
+    @property
+    def n_levels(self):
+        return len(self.unit_start) - 1
+
+
+def _morton(x, y):
+    r = 0
+    for b in range(4):
+        r |= ((x >> b) & 1) << (2 * b) | ((y >> b) & 1) << (2 * b + 1)
+    return r
+
+
+def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
+    """A seeded all-intra 4:2:0 frame coded the way recon_b_intra walks it
+    (src/recon_tmpl.c:1195-1596): quadtree blocks in superblock raster and
+    Z order, luma transform blocks in raster order, then U and V; luma modes
+    over all 13 coded modes + filter intra (blocks <= 32x32), angle deltas
+    -3..3, chroma modes or CfL (whole chroma block); block edge flags from
+    decode order (what intra_edge.c's tree encodes), transform-level flags
+    as recon_b_intra derives them (:1252-1266), smooth flags from the above
+    / left neighbours, superblock-top rows read through top_edge.  Then the
+    dependency levels: a unit's level is one more than the highest level of
+    any pixel its edges (after the mode remap) or its CfL luma read."""
+    from .workload import _partition, _tx_candidates, make_residuals
+    assert cfg.width % 32 == 0 and cfg.height % 8 == 0
+    rng = np.random.default_rng(cfg.seed)
+    W, H = cfg.width, cfg.height
+    bdmax = 255 if cfg.bpc == 8 else cfg.bitdepth_max
+    planes = [(W, H), (W // 2, H // 2), (W // 2, H // 2)]
+    sbl = (cfg.sb_log2, cfg.sb_log2 - 1, cfg.sb_log2 - 1)
+    sb = 1 << cfg.sb_log2
+    lx, ly, ls = _partition(rng, W, H)
+    order = np.lexsort((np.array([_morton((x % sb) >> 3, (y % sb) >> 3) for x, y in zip(lx, ly)]),
+                        lx // sb, ly // sb))
+    lx, ly, ls = lx[order], ly[order], ls[order]
+    nb = len(lx)
+    ymode = rng.integers(0, 14, nb)
+    ymode[(ymode == abi.FILTER_PRED) & (ls > 32)] = abi.DC_PRED
+    yang = np.where((ymode >= 1) & (ymode <= 8), rng.integers(-3, 4, nb),
+                    np.where(ymode == abi.FILTER_PRED, rng.integers(0, 5, nb), 0))
+    is_cfl = rng.random(nb) < cfg.cfl_frac
+    uvmode = rng.integers(0, 13, nb)
+    uvang = np.where((uvmode >= 1) & (uvmode <= 8), rng.integers(-3, 4, nb), 0)
+    alpha = rng.integers(1, 17, (nb, 2)) * np.where(rng.random((nb, 2)) < 0.5, -1, 1)
+    # decode index of the block covering each luma 4x4
+    bmap = np.full((H // 4, W // 4), -1, np.int64)
+    for b in range(nb):
+        bmap[ly[b] // 4:(ly[b] + ls[b]) // 4, lx[b] // 4:(lx[b] + ls[b]) // 4] = b
+    assert bmap.min() >= 0
+    smooth = lambda m: 9 <= m <= 11   # noqa: E731
+
+    U = {k: [] for k in ("plane", "x", "y", "tw", "th", "blk", "cfl", "mode", "angle", "flags")}
+    for b in range(nb):
+        x, y, s = int(lx[b]), int(ly[b]), int(ls[b])
+        tr = y > 0 and x + s < W and bmap[(y - 1) // 4, (x + s) // 4] < b
+        bl = x > 0 and y + s < H and bmap[(y + s) // 4, (x - 1) // 4] < b
+        above = bmap[(y - 1) // 4, x // 4] if y > 0 else -1
+        left = bmap[y // 4, (x - 1) // 4] if x > 0 else -1
+        ysm = (above >= 0 and smooth(ymode[above])) or (left >= 0 and smooth(ymode[left]))
+        uvsm = ((above >= 0 and not is_cfl[above] and smooth(uvmode[above])) or
+                (left >= 0 and not is_cfl[left] and smooth(uvmode[left])))
+        cands = _tx_candidates(s, cfg.tx64)
+        luma_tx = cands[int(rng.integers(0, len(cands)))]
+        for pl in range(3):
+            ss = 0 if pl == 0 else 1
+            px_, py_, ps_ = x >> ss, y >> ss, s >> ss
+            tw, th = luma_tx if pl == 0 else (ps_, ps_)
+            cfl = pl > 0 and bool(is_cfl[b])
+            bw4 = ps_ // 4
+            for oy in range(0, ps_, th):
+                for ox in range(0, ps_, tw):
+                    x4, y4 = ox // 4, oy // 4
+                    fl = 0
+                    if not cfl:
+                        if (y4 == 0 and tr) or x4 + tw // 4 < bw4:
+                            fl |= abi.IE_TOP_HAS_RIGHT
+                        if x4 == 0 and (bl or y4 + th // 4 < bw4):
+                            fl |= abi.IE_LEFT_HAS_BOTTOM
+                        if cfg.filter_edge:
+                            fl |= abi.IE_FILTER_EDGE
+                        if (ysm if pl == 0 else uvsm):
+                            fl |= abi.IE_SMOOTH
+                    U["plane"].append(pl)
+                    U["x"].append(px_ + ox)
+                    U["y"].append(py_ + oy)
+                    U["tw"].append(tw)
+                    U["th"].append(th)
+                    U["blk"].append(b)
+                    U["cfl"].append(cfl)
+                    U["mode"].append(abi.DC_PRED if cfl else int(ymode[b] if pl == 0 else uvmode[b]))
+                    U["angle"].append(0 if cfl else int(yang[b] if pl == 0 else uvang[b]))
+                    U["flags"].append(fl)
+    plane_u = np.array(U["plane"], np.int32)
+    ux, uy = np.array(U["x"], np.int32), np.array(U["y"], np.int32)
+    tw, th = np.array(U["tw"], np.int32), np.array(U["th"], np.int32)
+    blk = np.array(U["blk"], np.int32)
+    cflu = np.array(U["cfl"], bool)
+    n = len(ux)
+    tx = np.array([abi.TX_INDEX[(a, b_)] for a, b_ in zip(tw, th)], np.int32)
+    pw = np.array([p[0] for p in planes])
+    ph = np.array([p[1] for p in planes])
+    flags = np.array(U["flags"], np.int32)
+    flags |= np.where(ux > 0, abi.IE_HAVE_LEFT, 0)
+    flags |= np.where(uy > 0, abi.IE_HAVE_TOP, 0)
+    sbh = np.array([1 << s_ for s_ in sbl])[plane_u]
+    flags |= np.where((uy > 0) & (uy % sbh == 0), abi.IE_TOP_SB_EDGE, 0)
+
+    units = np.zeros(n, abi.UNIT_DTYPE)   # decode order for now
+    units["dst_off"] = uy * pw[plane_u] + ux
+    units["tx"] = tx
+    units["plane"] = plane_u
+    units["pred"] = np.where(cflu, abi.PRED_CFL, abi.PRED_INTRA)
+    units["bw4"] = units["bh4"] = 0
+    txtp, nzw, nzh, coef_off, coefs = make_residuals(rng, tx, tw, th, bdmax, cfg.coef_dtype)
+    units["txtp"], units["nzw"], units["nzh"], units["coef_off"] = txtp, nzw, nzh, coef_off
+    edge_len = 2 * th + 2 * tw + 1
+    edge_start = np.concatenate([[0], np.cumsum(edge_len)[:-1]])
+    units["edge_off"] = edge_start + 2 * th
+    iu = ~cflu
+    units["max_w"] = np.where(iu, pw[plane_u] - ux, 0)
+    units["max_h"] = np.where(iu, ph[plane_u] - uy, 0)
+    cu = units[cflu]
+    cu["cfl_alpha"] = alpha[blk[cflu], plane_u[cflu] - 1]
+    cu["cfl_pad_wh"] = 0
+    cu["cfl_luma_off"] = (2 * uy[cflu]) * W + 2 * ux[cflu]
+    units[cflu] = cu
+
+    # dependency levels, at 4x4 granularity per plane
+    lv = [np.full((h // 4, w // 4), -1, np.int64) for (w, h) in planes]
+    level = np.zeros(n, np.int64)
+    modes, angles = U["mode"], U["angle"]
+    for i in range(n):
+        p, x4, y4 = int(plane_u[i]), int(ux[i]) // 4, int(uy[i]) // 4
+        t4w, t4h = int(tw[i]) // 4, int(th[i]) // 4
+        w4, h4 = int(pw[p]) // 4, int(ph[p]) // 4
+        f = int(flags[i])
+        hl, ht = bool(f & abi.IE_HAVE_LEFT), bool(f & abi.IE_HAVE_TOP)
+        m, _ = remap_mode(modes[i], angles[i], hl, ht)
+        nd = _NEEDS[m]
+        L = lv[p]
+        deps = [-1]
+        if nd & _NEED_L:
+            if hl:
+                deps.append(L[y4:min(y4 + t4h, h4), x4 - 1].max())
+                if nd & _NEED_BL and y4 + t4h < h4 and (f & abi.IE_LEFT_HAS_BOTTOM):
+                    deps.append(L[y4 + t4h:min(y4 + 2 * t4h, h4), x4 - 1].max())
+            elif ht:
+                deps.append(L[y4 - 1, x4])
+        if nd & _NEED_T:
+            if ht:
+                deps.append(L[y4 - 1, x4:min(x4 + t4w, w4)].max())
+                if nd & _NEED_TR and x4 + t4w < w4 and (f & abi.IE_TOP_HAS_RIGHT):
+                    deps.append(L[y4 - 1, x4 + t4w:min(x4 + 2 * t4w, w4)].max())
+            elif hl:
+                deps.append(L[y4, x4 - 1])
+        if nd & _NEED_TL:
+            deps.append(L[y4 - 1, x4 - 1] if hl and ht else L[y4, x4 - 1] if hl else L[y4 - 1, x4] if ht else -1)
+        if cflu[i]:
+            luma = lv[0][2 * y4:2 * (y4 + t4h), 2 * x4:2 * (x4 + t4w)]
+            assert luma.min() >= 0          # the block's luma precedes its chroma
+            deps.append(luma.max())
+        d = max(int(v) for v in deps)
+        level[i] = d + 1
+        L[y4:y4 + t4h, x4:x4 + t4w] = d + 1
+    for L in lv:
+        assert L.min() >= 0
+
+    # backup runs: each superblock row's last pixel row, per run of 4x4
+    # columns written at one level, backed up right after that level
+    runs, run_lv = [], []
+    for p, (w, h) in enumerate(planes):
+        nsb = (h + (1 << sbl[p]) - 1) >> sbl[p]
+        for r in range(nsb - 1):
+            row = lv[p][(((r + 1) << sbl[p]) - 1) // 4]
+            c0 = 0
+            for c in range(1, len(row) + 1):
+                if c == len(row) or row[c] != row[c0]:
+                    runs.append((p, r, c0 * 4, (c - c0) * 4))
+                    run_lv.append(int(row[c0]))
+                    c0 = c
+    runs = np.array(runs, abi.EDGE_BACKUP_DTYPE) if runs else np.zeros(0, abi.EDGE_BACKUP_DTYPE)
+    run_lv = np.array(run_lv, np.int64)
+
+    # the decoder's order with whole-row backups at superblock-row ends
+    steps, oracle_runs = [], []
+    cur_sbrow = 0
+    for i in range(n):
+        r = int(ly[blk[i]]) >> cfg.sb_log2
+        while r > cur_sbrow:
+            for p, (w, h) in enumerate(planes):
+                oracle_runs.append((p, cur_sbrow, 0, w))
+                steps.append((1, len(oracle_runs) - 1))
+            cur_sbrow += 1
+        steps.append((0, i))
+
+    # level order, size classes inside a level, then pred / mode / type
+    perm = np.lexsort((units["txtp"], np.array(modes), units["pred"], units["tx"], level))
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    units = units[perm]
+    lvl_sorted = level[perm]
+    n_levels = int(level.max()) + 1
+    unit_start = np.searchsorted(lvl_sorted, np.arange(n_levels + 1)).astype(np.int32)
+    class_start = np.zeros((n_levels, abi.N_TX + 1), np.int32)
+    for l_ in range(n_levels):
+        t = units["tx"][unit_start[l_]:unit_start[l_ + 1]]
+        class_start[l_, 1:] = np.cumsum(np.bincount(t, minlength=abi.N_TX))
+    recs = np.zeros(n, abi.INTRA_EDGE_DTYPE)
+    recs["unit"] = inv
+    recs["x4"], recs["y4"] = ux // 4, uy // 4
+    recs["w4"], recs["h4"] = pw[plane_u] // 4, ph[plane_u] // 4
+    recs["mode"], recs["angle"], recs["flags"] = modes, angles, flags
+    rperm = np.argsort(level, kind="stable")
+    recs = recs[rperm]
+    rec_start = np.searchsorted(level[rperm], np.arange(n_levels + 1)).astype(np.int32)
+    unit_rec = np.full(n, -1, np.int32)
+    unit_rec[recs["unit"]] = np.arange(n)
+    rp = np.argsort(run_lv, kind="stable")
+    runs = runs[rp]
+    run_start = np.searchsorted(run_lv[rp], np.arange(n_levels + 1)).astype(np.int32)
+    steps = np.array(steps, np.int32)
+    unit_steps = steps[:, 0] == 0
+    steps[unit_steps, 1] = inv[steps[unit_steps, 1]]
+    top_rows = [(max(1, h >> s_), w) for (w, h), s_ in zip(planes, sbl)]
+    edges = np.zeros(int(edge_len.sum()), cfg.pixel_dtype)
+    return IntraFrame(cfg, planes, units, coefs, edges, recs, runs, unit_start, class_start, rec_start,
+                      run_start, steps, unit_rec, np.array(oracle_runs, abi.EDGE_BACKUP_DTYPE), top_rows, sbl)
+
+
+def frame_batch(fr, dst_ptrs, units, coefs, edges):
+    """abi.FrameBatch of an IntraFrame (cfl_luma = the reconstructed luma)."""
+    bpp = 1 if fr.cfg.bpc == 8 else 2
+    b = abi.FrameBatch()
+    for p, (w, h) in enumerate(fr.plane_wh):
+        b.dst[p].data, b.dst[p].stride, b.dst[p].w, b.dst[p].h = dst_ptrs[p], w * bpp, w, h
+    b.units, b.n_units = units, len(fr.units)
+    b.class_start[abi.N_TX] = len(fr.units)   # unused: the driver passes per-level ranges
+    b.coef, b.edges = coefs, edges
+    b.bitdepth_max = fr.cfg.bitdepth_max if fr.cfg.bpc == 16 else 255
+    W, H = fr.plane_wh[0]
+    b.cfl_luma.data, b.cfl_luma.stride, b.cfl_luma.w, b.cfl_luma.h = dst_ptrs[0], W * bpp, W, H
+    b.cfl_ss = 3
+    return b
+
+
+def edge_batch(fr, dst_ptrs, top_ptrs, units, edges, recs):
+    bpp = 1 if fr.cfg.bpc == 8 else 2
+    b = abi.IntraEdgeBatch()
+    for p, (w, h) in enumerate(fr.plane_wh):
+        b.pic[p].data, b.pic[p].stride, b.pic[p].w, b.pic[p].h = dst_ptrs[p], w * bpp, w, h
+        rows, tw_ = fr.top_rows[p]
+        b.top_edge[p].data, b.top_edge[p].stride = top_ptrs[p], tw_ * bpp
+        b.top_edge[p].w, b.top_edge[p].h = tw_, rows
+        b.sb_log2[p] = fr.sb_log2[p]
+    b.units, b.edges, b.recs = units, edges, recs
+    b.n_recs = len(fr.recs)
+    b.bitdepth_max = fr.cfg.bitdepth_max if fr.cfg.bpc == 16 else 255
+    return b
+
+
+class DeviceIntraFrame:
+    """An IntraFrame on one GPU; launch() runs the whole wavefront
+    (dav1d_gpu_recon_intra_frame_*) on a stream."""
+
+    def __init__(self, fr, device="cuda:0", top_fill=0x5A):
+        import torch
+        self.torch, self.fr = torch, fr
+        dev = torch.device(device)
+        hbd = fr.cfg.bpc != 8
+        pdt = torch.int16 if hbd else torch.uint8
+        up = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).to(dev)   # noqa: E731
+        self.units0 = fr.units.copy()
+        self.units = up(fr.units.view(np.uint8))
+        self.coefs = up(fr.coefs.view(np.int16 if not hbd else np.int32))
+        self.edges = up(fr.edges.view(np.int16) if hbd else fr.edges)
+        self.recs = up(fr.recs.view(np.uint8))
+        self.runs = up(fr.runs.view(np.uint8)) if len(fr.runs) else torch.zeros(16, dtype=torch.uint8, device=dev)
+        self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fr.plane_wh]
+        self.top = [torch.full(s, top_fill, dtype=pdt, device=dev) for s in fr.top_rows]
+        d = [t.data_ptr() for t in self.dst]
+        self.rb = frame_batch(fr, d, self.units.data_ptr(), self.coefs.data_ptr(), self.edges.data_ptr())
+        self.eb = edge_batch(fr, d, [t.data_ptr() for t in self.top], self.units.data_ptr(),
+                             self.edges.data_ptr(), self.recs.data_ptr())
+        self._host = [np.ascontiguousarray(a, dtype=np.int32) for a in
+                      (fr.unit_start, fr.class_start, fr.rec_start, fr.run_start)]
+        s = abi.IntraSchedule()
+        s.n_levels = fr.n_levels
+        s.unit_start, s.class_start, s.rec_start, s.run_start = (a.ctypes.data for a in self._host)
+        s.runs = self.runs.data_ptr()
+        self.sched = s
+        self.lib = abi.load_lib()
+
+    def reset(self):
+        """Restore the inputs the wavefront consumes (unit modes / angles are
+        rewritten, coefficients kept: zero_coefs is off)."""
+        self.units.copy_(self.torch.from_numpy(self.units0.view(np.uint8)))
+        for t in self.dst:
+            t.zero_()
+
+    def launch(self, stream=None):
+        s = stream if stream is not None else self.torch.cuda.current_stream()
+        fn = getattr(self.lib, f"dav1d_gpu_recon_intra_frame_{8 if self.fr.cfg.bpc == 8 else 16}bpc")
+        rc = fn(ctypes.byref(self.rb), ctypes.byref(self.eb), ctypes.byref(self.sched),
+                ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"dav1d_gpu_recon_intra_frame failed: {rc}")
+
+    def planes_host(self):
+        out = []
+        for t in self.dst:
+            a = t.cpu().numpy()
+            out.append(a if self.fr.cfg.bpc == 8 else a.view(np.uint16))
+        return out

@@ -174,6 +174,52 @@ def _tx_candidates(s, tx64=False):
     return [(a, b) for a in sides for b in sides if max(a, b) <= 4 * min(a, b)]
 
 
+def make_residuals(rng, tx, tw, th, bdmax, coef_dtype):
+    """Transform types (uniform over the reference's valid ones per size),
+    stored coefficient regions (25% DC-only, 50% partial, 25% full) and
+    coefficients from a seeded forward transform of uniform residuals
+    (SURVEY 8(d) config 3).  Returns (txtp, nzw, nzh, coef_off, coefs)."""
+    n = len(tx)
+    txtp = np.zeros(n, np.int32)
+    for t in range(abi.N_TX):
+        sel = np.nonzero(tx == t)[0]
+        if not len(sel):
+            continue
+        ok = [tp for tp in range(16) if abi.itx_supported(t, tp)]
+        txtp[sel] = np.array(ok)[rng.integers(0, len(ok), len(sel))]
+    eclass = rng.random(n)          # <.25 DC-only, <.75 partial, else full
+    sw = np.minimum(tw, 32)
+    sh = np.minimum(th, 32)
+    nzw = np.where(eclass < 0.25, np.where(txtp == abi.DCT_DCT, 0, 1),
+                   np.where(eclass < 0.75, 1 + (rng.random(n) * sw).astype(np.int32), sw))
+    nzh = np.where(eclass < 0.25, np.where(txtp == abi.DCT_DCT, 0, 1),
+                   np.where(eclass < 0.75, 1 + (rng.random(n) * sh).astype(np.int32), sh))
+    ncoef = np.where(nzw == 0, 1, nzw * nzh)
+    coef_off = np.concatenate([[0], np.cumsum(ncoef)[:-1]])
+    coefs = np.zeros(int(ncoef.sum()), coef_dtype)
+    lim = np.iinfo(np.int16)
+    for t in range(abi.N_TX):
+        w_, h_ = abi.TX_WH[t]
+        for tp in range(16):
+            sel = np.nonzero((tx == t) & (txtp == tp))[0]
+            if not len(sel):
+                continue
+            res = rng.integers(-bdmax, bdmax + 1, size=(len(sel), h_, w_)).astype(np.float64)
+            mh = _fwd_mat(_KH[tp], w_)
+            mvv = _fwd_mat(_KV[tp], h_)
+            sc = _SCALE[int(np.log2(w_ * h_)) - 4]
+            c = np.einsum("yk,nkx->nyx", mvv, np.einsum("nyk,xk->nyx", res, mh)) * sc
+            c = np.floor(c + 0.5)
+            c = np.clip(c, lim.min, lim.max).astype(np.int64)
+            for j, i in enumerate(sel):
+                a, b, o = int(nzw[i]), int(nzh[i]), int(coef_off[i])
+                if a == 0:
+                    coefs[o] = c[j, 0, 0]
+                else:
+                    coefs[o:o + a * b] = c[j, :b, :a].T.ravel()
+    return txtp, nzw, nzh, coef_off, coefs
+
+
 def make_frame(cfg: FrameConfig) -> FrameData:
     rng = np.random.default_rng(cfg.seed)
     W, H = cfg.width, cfg.height
@@ -428,47 +474,11 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         units["txtp"] = abi.NO_RESIDUAL
         coefs = np.zeros(1, cfg.coef_dtype)
     else:
-        txtp = np.zeros(n, np.int32)
-        for t in range(abi.N_TX):
-            sel = np.nonzero(tx == t)[0]
-            if not len(sel):
-                continue
-            ok = [tp for tp in range(16) if abi.itx_supported(t, tp)]
-            txtp[sel] = np.array(ok)[rng.integers(0, len(ok), len(sel))]
+        txtp, nzw, nzh, coef_off, coefs = make_residuals(rng, tx, tw, th, bdmax, cfg.coef_dtype)
         units["txtp"] = txtp
-        eclass = rng.random(n)          # <.25 DC-only, <.75 partial, else full
-        sw = np.minimum(tw, 32)
-        sh = np.minimum(th, 32)
-        nzw = np.where(eclass < 0.25, np.where(txtp == abi.DCT_DCT, 0, 1),
-                       np.where(eclass < 0.75, 1 + (rng.random(n) * sw).astype(np.int32), sw))
-        nzh = np.where(eclass < 0.25, np.where(txtp == abi.DCT_DCT, 0, 1),
-                       np.where(eclass < 0.75, 1 + (rng.random(n) * sh).astype(np.int32), sh))
         units["nzw"] = nzw
         units["nzh"] = nzh
-        ncoef = np.where(nzw == 0, 1, nzw * nzh)
-        coef_off = np.concatenate([[0], np.cumsum(ncoef)[:-1]])
         units["coef_off"] = coef_off
-        coefs = np.zeros(int(ncoef.sum()), cfg.coef_dtype)
-        lim = np.iinfo(np.int16)
-        for t in range(abi.N_TX):
-            w_, h_ = abi.TX_WH[t]
-            for tp in range(16):
-                sel = np.nonzero((tx == t) & (txtp == tp))[0]
-                if not len(sel):
-                    continue
-                res = rng.integers(-bdmax, bdmax + 1, size=(len(sel), h_, w_)).astype(np.float64)
-                mh = _fwd_mat(_KH[tp], w_)
-                mvv = _fwd_mat(_KV[tp], h_)
-                sc = _SCALE[int(np.log2(w_ * h_)) - 4]
-                c = np.einsum("yk,nkx->nyx", mvv, np.einsum("nyk,xk->nyx", res, mh)) * sc
-                c = np.floor(c + 0.5)
-                c = np.clip(c, lim.min, lim.max).astype(np.int64)
-                for j, i in enumerate(sel):
-                    a, b, o = int(nzw[i]), int(nzh[i]), int(coef_off[i])
-                    if a == 0:
-                        coefs[o] = c[j, 0, 0]
-                    else:
-                        coefs[o:o + a * b] = c[j, :b, :a].T.ravel()
 
     # sort by (class, picture band, pred kind, then transform type / filter
     # for inter and mode / transform type for intra).  The kernel cuts each

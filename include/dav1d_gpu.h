@@ -528,8 +528,58 @@ typedef struct Dav1dGpuIntraEdgeBatch {
     int32_t  bitdepth_max;
 } Dav1dGpuIntraEdgeBatch;
 
+/* A CFL unit's record carries mode DC_PRED, angle 0, flags without the
+ * filter / smooth bits (recon_tmpl.c:1393-1410); only its DC source
+ * (p.cfl.mode) is written, alpha and padding stay.  Errors: -1 NULL batch or
+ * buffers / negative count, -3 launch failure. */
 int dav1d_gpu_prepare_intra_edges_8bpc(const Dav1dGpuIntraEdgeBatch *b, void *stream);
 int dav1d_gpu_prepare_intra_edges_16bpc(const Dav1dGpuIntraEdgeBatch *b, void *stream);
+
+/* bytefn(dav1d_backup_ipred_edge) (src/recon_tmpl.c:2162-2186): copy the last
+ * pre-filter pixel row of superblock row `sby` into top_edge row `sby`, over
+ * columns [x0, x0 + w) of one plane.  A run of columns rather than the whole
+ * tile row, so a wavefront can back up each column as soon as the block
+ * writing it is done. */
+typedef struct Dav1dGpuEdgeBackup {   /* 16 bytes */
+    int32_t plane, sby;
+    int32_t x0, w;
+} Dav1dGpuEdgeBackup;
+
+int dav1d_gpu_backup_ipred_edge_8bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav1dGpuEdgeBackup *runs,
+                                     int n_runs, void *stream);
+int dav1d_gpu_backup_ipred_edge_16bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav1dGpuEdgeBackup *runs,
+                                      int n_runs, void *stream);
+
+/* ---- intra wavefront ----------------------------------
+ * Dependent intra reconstruction on the device.  The caller orders the
+ * units, edge records and backup runs by dependency level (a level only
+ * reads pixels written by earlier levels: the left, top, top-right,
+ * bottom-left and top-left edges its records read, the co-located luma of a
+ * CFL unit, the top_edge columns its runs backed up); per level the driver
+ * enqueues edge preparation, reconstruction (dav1d_gpu_recon_*, the level's
+ * units sorted by size class) and the level's backup runs, in that order, on
+ * one stream.  This replaces recon_b_intra's per-transform-block sequence
+ * prepare_intra_edges -> intra_pred / cfl_pred -> itxfm_add
+ * (src/recon_tmpl.c:1195-1596) for a whole frame without host round trips. */
+typedef struct Dav1dGpuIntraSchedule {
+    int32_t n_levels;
+    const int32_t *unit_start;   /* host, n_levels + 1: the level's units in
+                                    recon->units (contiguous)                 */
+    const int32_t *class_start;  /* host, n_levels x (DGPU_N_RECT_TX_SIZES+1):
+                                    size-class ranges within the level        */
+    const int32_t *rec_start;    /* host, n_levels + 1: its edge records       */
+    const int32_t *run_start;    /* host, n_levels + 1: its backup runs        */
+    const Dav1dGpuEdgeBackup *runs;   /* device                                */
+} Dav1dGpuIntraSchedule;
+
+/* recon: the frame's unit batch (units in level order, class_start and
+ * class_warp ignored; cfl_luma normally the reconstructed luma plane);
+ * edges: pic = the same planes, units = recon->units, every record.
+ * Errors: those of the three stages, -2 inconsistent schedule. */
+int dav1d_gpu_recon_intra_frame_8bpc(const Dav1dGpuFrameBatch *recon, const Dav1dGpuIntraEdgeBatch *edges,
+                                     const Dav1dGpuIntraSchedule *s, void *stream);
+int dav1d_gpu_recon_intra_frame_16bpc(const Dav1dGpuFrameBatch *recon, const Dav1dGpuIntraEdgeBatch *edges,
+                                      const Dav1dGpuIntraSchedule *s, void *stream);
 
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split

@@ -1855,9 +1855,49 @@ int SFX(oracle_prepare_intra_edges)(const Dav1dGpuIntraEdgeBatch *b)
             if (mode == DGPU_Z2_PRED && tw + th >= 6 && (r->flags & DGPU_IE_FILTER_EDGE))
                 tl[0] = (pixel)(((tl[-1] + tl[1]) * 5 + tl[0] * 6 + 8) >> 4);
         }
-        u->p.intra.mode = (uint8_t)mode;
-        u->p.intra.angle = (uint16_t)((angle & 511) | ((r->flags & DGPU_IE_SMOOTH) ? 512 : 0) |
-                                      ((r->flags & DGPU_IE_FILTER_EDGE) ? 1024 : 0));
+        u->p.intra.mode = (uint8_t)mode;   /* CFL: the DC source (same byte), alpha kept */
+        if (u->pred != DGPU_PRED_CFL)
+            u->p.intra.angle = (uint16_t)((angle & 511) | ((r->flags & DGPU_IE_SMOOTH) ? 512 : 0) |
+                                          ((r->flags & DGPU_IE_FILTER_EDGE) ? 1024 : 0));
+    }
+    return 0;
+}
+
+/* bytefn(dav1d_backup_ipred_edge), src/recon_tmpl.c:2162-2186, per run of
+ * columns: the last row of superblock row sby into top_edge row sby. */
+int SFX(oracle_backup_ipred_edge)(const Dav1dGpuIntraEdgeBatch *b, const Dav1dGpuEdgeBackup *runs, int n)
+{
+    for (int i = 0; i < n; i++) {
+        const Dav1dGpuEdgeBackup *r = &runs[i];
+        const int y = ((r->sby + 1) << b->sb_log2[r->plane]) - 1;
+        const pixel *src = (const pixel *)b->pic[r->plane].data + (ptrdiff_t)y * PX(b->pic[r->plane].stride) + r->x0;
+        pixel *dst = (pixel *)b->top_edge[r->plane].data + (ptrdiff_t)r->sby * PX(b->top_edge[r->plane].stride) + r->x0;
+        memcpy(dst, src, (size_t)r->w * sizeof(pixel));
+    }
+    return 0;
+}
+
+/* The decoder's own sequence for an intra frame (recon_b_intra,
+ * src/recon_tmpl.c:1195-1596, and the per-sbrow backup, decode.c:2677):
+ * steps[2i] = 0: unit steps[2i+1] -- prepare its edges (its record
+ * unit_rec[u], if any) and reconstruct it; 1: backup run steps[2i+1]. */
+int SFX(oracle_recon_intra_frame)(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraEdgeBatch *eb,
+                                  const int32_t *steps, int n_steps, const int32_t *unit_rec,
+                                  const Dav1dGpuEdgeBackup *runs)
+{
+    Dav1dGpuIntraEdgeBatch one = *eb;
+    one.n_recs = 1;
+    for (int i = 0; i < n_steps; i++) {
+        const int op = steps[2 * i], a = steps[2 * i + 1];
+        if (op == 0) {
+            if (unit_rec[a] >= 0) {
+                one.recs = eb->recs + unit_rec[a];
+                SFX(oracle_prepare_intra_edges)(&one);
+            }
+            SFX(oracle_recon_units)(rb, a, a + 1);
+        } else {
+            SFX(oracle_backup_ipred_edge)(eb, runs + a, 1);
+        }
     }
     return 0;
 }

@@ -16,4 +16,12 @@ int oracle_recon_tiles_8bpc(const Dav1dGpuTileBatch *b, int t0, int t1);
 int oracle_recon_tiles_16bpc(const Dav1dGpuTileBatch *b, int t0, int t1);
 int oracle_prepare_intra_edges_8bpc(const Dav1dGpuIntraEdgeBatch *b);
 int oracle_prepare_intra_edges_16bpc(const Dav1dGpuIntraEdgeBatch *b);
+int oracle_backup_ipred_edge_8bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav1dGpuEdgeBackup *runs, int n);
+int oracle_backup_ipred_edge_16bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav1dGpuEdgeBackup *runs, int n);
+int oracle_recon_intra_frame_8bpc(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraEdgeBatch *eb,
+                                  const int32_t *steps, int n_steps, const int32_t *unit_rec,
+                                  const Dav1dGpuEdgeBackup *runs);
+int oracle_recon_intra_frame_16bpc(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraEdgeBatch *eb,
+                                   const int32_t *steps, int n_steps, const int32_t *unit_rec,
+                                   const Dav1dGpuEdgeBackup *runs);
 #endif

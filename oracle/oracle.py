@@ -41,6 +41,13 @@ def load():
             f = getattr(L, f"oracle_prepare_intra_edges_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(abi.IntraEdgeBatch)]
             f.restype = ctypes.c_int
+            f = getattr(L, f"oracle_backup_ipred_edge_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(abi.IntraEdgeBatch), ctypes.c_void_p, ctypes.c_int]
+            f.restype = ctypes.c_int
+            f = getattr(L, f"oracle_recon_intra_frame_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(abi.FrameBatch), ctypes.POINTER(abi.IntraEdgeBatch), ctypes.c_void_p,
+                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+            f.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -268,3 +275,57 @@ def prepare_intra_edges(case):
     rc = fn(ctypes.byref(b))
     assert rc == 0
     return units, edges
+
+
+class HostIntraFrame:
+    """An intra.IntraFrame reconstructed by the oracle in the decoder's own
+    order: per transform block prepare_intra_edges then the DSP calls, the
+    top_edge backup at each superblock-row end (oracle_recon_intra_frame)."""
+
+    def __init__(self, fr, top_fill=0x5A):
+        import dav1d_mirror_amd.intra as intra
+        abi = _abi()
+        self.fr = fr
+        pdt = fr.cfg.pixel_dtype
+        self.dst = [np.zeros((h, w), pdt) for (w, h) in fr.plane_wh]
+        self.top = [np.full(s, top_fill, pdt) for s in fr.top_rows]
+        self.units = fr.units.copy()
+        self.coefs = fr.coefs.copy()
+        self.edges = fr.edges.copy()
+        self.recs = np.ascontiguousarray(fr.recs)
+        self.steps = np.ascontiguousarray(fr.steps, dtype=np.int32)
+        self.unit_rec = np.ascontiguousarray(fr.unit_rec, dtype=np.int32)
+        self.oruns = np.ascontiguousarray(fr.oracle_runs) if len(fr.oracle_runs) else np.zeros(1, abi.EDGE_BACKUP_DTYPE)
+        d = [a.ctypes.data for a in self.dst]
+        self.rb = intra.frame_batch(fr, d, self.units.ctypes.data, self.coefs.ctypes.data, self.edges.ctypes.data)
+        self.eb = intra.edge_batch(fr, d, [a.ctypes.data for a in self.top], self.units.ctypes.data,
+                                   self.edges.ctypes.data, self.recs.ctypes.data)
+
+    def run(self):
+        fn = getattr(load(), f"oracle_recon_intra_frame_{8 if self.fr.cfg.bpc == 8 else 16}bpc")
+        rc = fn(ctypes.byref(self.rb), ctypes.byref(self.eb), self.steps.ctypes.data, len(self.steps),
+                self.unit_rec.ctypes.data, self.oruns.ctypes.data)
+        assert rc == 0
+
+    def run_levels(self):
+        """The same frame in the wavefront's level order (edges, units, then
+        backup runs per level), on the CPU: checks the schedule itself."""
+        abi = _abi()
+        fr = self.fr
+        L = load()
+        sfx = 8 if fr.cfg.bpc == 8 else 16
+        prep = getattr(L, f"oracle_prepare_intra_edges_{sfx}bpc")
+        recon = getattr(L, f"oracle_recon_units_{sfx}bpc")
+        backup = getattr(L, f"oracle_backup_ipred_edge_{sfx}bpc")
+        runs = np.ascontiguousarray(fr.runs) if len(fr.runs) else np.zeros(1, abi.EDGE_BACKUP_DTYPE)
+        rec_sz = fr.recs.dtype.itemsize
+        run_sz = runs.dtype.itemsize
+        e = abi.IntraEdgeBatch.from_buffer_copy(self.eb)
+        for lv in range(fr.n_levels):
+            r0, r1 = int(fr.rec_start[lv]), int(fr.rec_start[lv + 1])
+            e.recs = self.recs.ctypes.data + r0 * rec_sz
+            e.n_recs = r1 - r0
+            prep(ctypes.byref(e))
+            recon(ctypes.byref(self.rb), int(fr.unit_start[lv]), int(fr.unit_start[lv + 1]))
+            b0, b1 = int(fr.run_start[lv]), int(fr.run_start[lv + 1])
+            backup(ctypes.byref(self.eb), runs.ctypes.data + b0 * run_sz, b1 - b0)

@@ -155,7 +155,8 @@ def _py_prepare(case, rec, units, edges):
     for k, v in E.items():
         edges[o + k] = v
     units[rec["unit"]]["mode"] = mode
-    units[rec["unit"]]["angle"] = (angle & 511) | (512 if fl & 32 else 0) | (1024 if fl & 16 else 0)
+    if u["pred"] != 4:   # PRED_CFL: the DC source only, alpha / padding kept
+        units[rec["unit"]]["angle"] = (angle & 511) | (512 if fl & 32 else 0) | (1024 if fl & 16 else 0)
 
 
 @pytest.mark.parametrize("bpc,bdmax,seed", [(8, 255, 5), (16, 1023, 6), (16, 4095, 7)])
@@ -172,6 +173,8 @@ def test_oracle_matches_python_restatement(pkg, oracle, bpc, bdmax, seed):
     assert set(np.unique(units["mode"][case.recs["unit"]])) == set(range(14))
     for bit in (1, 2, 4, 8, 16, 32, 64):
         assert np.any(case.recs["flags"] & bit)
+    cfl = units["pred"] == pkg.abi.PRED_CFL
+    assert cfl.any() and np.array_equal(units["cfl_alpha"][cfl], case.units["cfl_alpha"][cfl])
 
 
 def _one(pkg, pic, rec, tx, bpc=8, bdmax=255, top_edge=None):

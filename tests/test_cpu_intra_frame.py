@@ -1,0 +1,79 @@
+"""CPU tests of the intra wavefront: the scheduler's
+dependency levels replayed by the oracle in level order must give the
+pixels of the decoder's own order (per transform block: prepare edges,
+predict, add the residual; top_edge backed up at superblock-row ends,
+src/recon_tmpl.c:1195-1596, :2162, src/decode.c:2677), plus the schedule's
+structural invariants."""
+import numpy as np
+import pytest
+
+
+def _frame(**kw):
+    import dav1d_mirror_amd.intra as intra
+    return intra.make_intra_frame(intra.IntraConfig(**kw))
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(seed=2, cfl_frac=1.0), dict(seed=3, filter_edge=False, tx64=False),
+                                dict(seed=4, bpc=16, bitdepth_max=1023), dict(seed=5, bpc=16, bitdepth_max=4095),
+                                dict(seed=6, width=480, height=264)])
+def test_level_order_equals_decode_order(pkg, oracle, kw):
+    fr = _frame(**kw)
+    a = oracle.HostIntraFrame(fr)
+    a.run()
+    b = oracle.HostIntraFrame(fr)
+    b.run_levels()
+    for p in range(3):
+        assert np.array_equal(a.dst[p], b.dst[p]), p
+        assert np.array_equal(a.top[p][:-1], b.top[p][:-1]), p   # (the last sb row is never backed up)
+    assert np.array_equal(a.units, b.units)
+
+
+def test_schedule_invariants(pkg):
+    abi = pkg.abi
+    fr = _frame(seed=7)
+    n = len(fr.units)
+    assert fr.unit_start[0] == 0 and fr.unit_start[-1] == n
+    assert fr.rec_start[-1] == len(fr.recs) == n          # every unit is intra or CfL here
+    assert fr.run_start[-1] == len(fr.runs)
+    assert np.array_equal(np.sort(fr.recs["unit"]), np.arange(n))
+    for lv in range(fr.n_levels):
+        u0, u1 = fr.unit_start[lv], fr.unit_start[lv + 1]
+        assert u1 > u0                                      # no empty level
+        t = fr.units["tx"][u0:u1]
+        assert np.all(np.diff(t.astype(int)) >= 0)          # size classes contiguous
+        assert np.array_equal(fr.class_start[lv], np.concatenate([[0], np.cumsum(np.bincount(t, minlength=abi.N_TX))]))
+        r = fr.recs["unit"][fr.rec_start[lv]:fr.rec_start[lv + 1]]
+        assert np.all((r >= u0) & (r < u1))                 # a level's records serve its units
+    # every pixel of every plane is written by exactly one unit
+    for p, (w, h) in enumerate(fr.plane_wh):
+        cov = np.zeros((h, w), np.int32)
+        for u in fr.units[fr.units["plane"] == p]:
+            tw, th = abi.TX_WH[u["tx"]]
+            y, x = divmod(int(u["dst_off"]), w)
+            cov[y:y + th, x:x + tw] += 1
+        assert np.all(cov == 1)
+    # the wavefront is much shorter than the unit count
+    assert fr.n_levels < n / 8
+
+
+def test_intra_frame_launch_validation(pkg):
+    import ctypes
+    L = pkg.abi.load_lib()
+    for bpc in (8, 16):
+        fn = getattr(L, f"dav1d_gpu_recon_intra_frame_{bpc}bpc")
+        rb, eb, s = pkg.abi.FrameBatch(), pkg.abi.IntraEdgeBatch(), pkg.abi.IntraSchedule()
+        assert fn(None, None, None, None) == -1
+        s.n_levels = 1
+        assert fn(ctypes.byref(rb), ctypes.byref(eb), ctypes.byref(s), None) == -1   # NULL tables
+        us = (ctypes.c_int32 * 2)(0, 5)
+        cs = (ctypes.c_int32 * (pkg.abi.N_TX + 1))()
+        z = (ctypes.c_int32 * 2)(0, 0)
+        s.unit_start, s.class_start, s.rec_start, s.run_start = (ctypes.addressof(us), ctypes.addressof(cs),
+                                                                  ctypes.addressof(z), ctypes.addressof(z))
+        assert fn(ctypes.byref(rb), ctypes.byref(eb), ctypes.byref(s), None) == -2   # class_start != level size
+        s.n_levels = 0
+        assert fn(ctypes.byref(rb), ctypes.byref(eb), ctypes.byref(s), None) == 0
+        bk = getattr(L, f"dav1d_gpu_backup_ipred_edge_{bpc}bpc")
+        assert bk(None, None, 0, None) == -1
+        assert bk(ctypes.byref(eb), None, 3, None) == -1
+        assert bk(ctypes.byref(eb), None, 0, None) == 0
