@@ -155,6 +155,37 @@ def tile_breakdown(fd, dev, stream, steps):
     return out
 
 
+def intra_breakdown(cfg, dev, stream, steps):
+    """an all-intra frame of the config's size and
+    bitdepth reconstructed on the device by the intra wavefront
+    (dav1d_gpu_recon_intra_frame_*, fused: one launch per dependency level),
+    one tile and 2x2 tiles; beside it the oracle in the decoder's own order
+    on one host core.  Reported beside the headline, not part of it."""
+    import dav1d_mirror_amd.intra as intra
+    out = {}
+    orc = ge.load_oracle()
+    for name, tiles in (("1_tile", (1, 1)), ("2x2_tiles", (2, 2))):
+        fr = intra.make_intra_frame(intra.IntraConfig(width=cfg.width, height=cfg.height, bpc=cfg.bpc,
+                                                      bitdepth_max=cfg.bitdepth_max, tile_cols=tiles[0],
+                                                      tile_rows=tiles[1]))
+        frame = intra.DeviceIntraFrame(fr, dev)
+        for _ in range(2):
+            frame.launch(stream)
+        ks = kernel_seconds(frame, stream, max(3, min(steps, 5)))
+        ho = orc.HostIntraFrame(fr)
+        t0 = time.perf_counter()
+        ho.run()
+        cpu_s = time.perf_counter() - t0
+        got = frame.planes_host()
+        px = sum(w * h for w, h in fr.plane_wh)
+        out[name] = {"units": int(len(fr.units)), "levels": int(fr.n_levels), "ms_per_frame": round(ks * 1e3, 3),
+                     "gpix_s": round(px / ks / 1e9, 4), "us_per_level": round(ks * 1e6 / fr.n_levels, 2),
+                     "oracle_1core_ms": round(cpu_s * 1e3, 2),
+                     "bit_exact_vs_oracle": all(bool(np.array_equal(g, o)) for g, o in zip(got, ho.dst))}
+        del frame
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,6 +198,7 @@ def main():
                     help="local: each rank generates its frame; rccl: rank 0 generates all and scatters")
     ap.add_argument("--no-families", action="store_true", help="skip the per-family breakdown (N=1)")
     ap.add_argument("--no-tiles", action="store_true", help="skip the tile-batch measurement (N=1)")
+    ap.add_argument("--no-intra", action="store_true", help="skip the intra-wavefront measurement (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -288,6 +320,8 @@ def main():
             out["families"] = family_breakdown(cfg, dev, stream, args.steps)
         if not args.no_tiles and world == 1:
             out["tile_batch"] = tile_breakdown(fd, dev, stream, args.steps)
+        if not args.no_intra and world == 1 and c.get("kind") == "full":
+            out["intra_wavefront"] = intra_breakdown(cfg, dev, stream, args.steps)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
         print(json.dumps(out), flush=True)

@@ -124,11 +124,13 @@ class IntraEdgeBatch(ctypes.Structure):
                 ("bitdepth_max", ctypes.c_int32)]
 
 
+IS_FUSED = 1
 EDGE_BACKUP_DTYPE = np.dtype([("plane", "<i4"), ("sby", "<i4"), ("x0", "<i4"), ("w", "<i4")])
 
 
 class IntraSchedule(ctypes.Structure):
     _fields_ = [("n_levels", ctypes.c_int32),
+                ("flags", ctypes.c_int32),
                 ("unit_start", ctypes.c_void_p),
                 ("class_start", ctypes.c_void_p),
                 ("rec_start", ctypes.c_void_p),

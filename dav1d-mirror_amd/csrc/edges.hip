@@ -16,6 +16,11 @@
 
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
+#include "intra_edge_dev.hpp"
+
+// the fused reconstruction launch (recon_ie.hpp, recon_ie8/16.hip)
+int dgpu_recon_ie_8bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, void *stream);
+int dgpu_recon_ie_16bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, void *stream);
 
 namespace dgpu {
 
@@ -35,15 +40,6 @@ template <int BPC> struct EdgeArgs {
     int bdmax;
 };
 
-// needs per implementation mode: bit0 left, 1 top, 2 top-left, 3 top-right,
-// 4 bottom-left (av1_intra_prediction_edges, src/ipred_prepare_tmpl.c:50-75)
-__device__ __forceinline__ int ie_needs(int m) {
-    constexpr uint64_t t = (3ull << 0) | (2ull << 5) | (1ull << 10) | (1ull << 15) | (2ull << 20) | (0ull << 25) |
-                           (14ull << 30) | (7ull << 35) | (21ull << 40) | (3ull << 45) | (3ull << 50) |
-                           (3ull << 55) | (7ull << 60);
-    return m == DGPU_FILTER_PRED ? 7 : (int)((t >> (5 * m)) & 31);
-}
-
 template <int BPC>
 __global__ __launch_bounds__(256) void k_intra_edges(EdgeArgs<BPC> a) {
     using P = typename Px<BPC>::pixel;
@@ -53,70 +49,17 @@ __global__ __launch_bounds__(256) void k_intra_edges(EdgeArgs<BPC> a) {
     const Dav1dGpuIntraEdge r = a.recs[ri];
     Dav1dGpuUnit *u = a.units + r.unit;
     const int pl = u->plane, txs = u->tx;
-    const int tw = tx_info(txs).w >> 2, th = tx_info(txs).h >> 2;
-    const int ps = a.ps[pl];
-    const P *dst = a.pic[pl] + (size_t)(r.y4 * 4) * ps + r.x4 * 4;
-    const int hl = r.flags & DGPU_IE_HAVE_LEFT, ht = r.flags & DGPU_IE_HAVE_TOP;
-    // mode remap (:83-104)
-    int angle = r.angle, mode = r.mode;
-    if (mode >= 1 && mode <= 8) {
-        // base angles of modes 1..8: 90 180 45 135 113 157 203 67
-        angle = (int)((0x43cb9d71872db45aull >> (8 * (mode - 1))) & 0xff) + 3 * angle;
-        mode = angle <= 90 ? (angle < 90 && ht ? DGPU_Z1_PRED : DGPU_VERT_PRED)
-             : angle < 180 ? DGPU_Z2_PRED
-                           : (angle > 180 && hl ? DGPU_Z3_PRED : DGPU_HOR_PRED);
-    } else if (mode == 0) {
-        mode = hl ? (ht ? DGPU_DC_PRED : DGPU_LEFT_DC_PRED) : (ht ? DGPU_TOP_DC_PRED : DGPU_DC_128_PRED);
-    } else if (mode == 12) {
-        mode = hl ? (ht ? DGPU_PAETH_PRED : DGPU_HOR_PRED) : (ht ? DGPU_VERT_PRED : DGPU_DC_128_PRED);
-    }
-    const int nd = ie_needs(mode);
-    const int half = (a.bdmax + 1) >> 1;
-    const P *top = dst - ps;
-    if (r.flags & DGPU_IE_TOP_SB_EDGE)
-        top = a.top[pl] + (size_t)(((r.y4 * 4) >> a.sb_log2[pl]) - 1) * a.ts[pl] + r.x4 * 4;
-    const int szl = th * 4, szt = tw * 4;
-    const int nl = min(szl, (r.h4 - r.y4) * 4), nt = min(szt, (r.w4 - r.x4) * 4);
-    const bool hbl = hl && r.y4 + th < r.h4 && (r.flags & DGPU_IE_LEFT_HAS_BOTTOM);
-    const bool htr = ht && r.x4 + tw < r.w4 && (r.flags & DGPU_IE_TOP_HAS_RIGHT);
-    const int nbl = hbl ? min(szl, (r.h4 - r.y4 - th) * 4) : 1;
-    const int ntr = htr ? min(szt, (r.w4 - r.x4 - tw) * 4) : 1;
-    auto leftv = [&](int k) -> int {
-        return hl ? (int)dst[(size_t)min(k, nl - 1) * ps - 1] : ht ? (int)top[0] : half + 1;
-    };
-    auto topv = [&](int k) -> int {
-        return ht ? (int)top[min(k, nt - 1)] : hl ? (int)dst[-1] : half - 1;
-    };
+    const IeCtx<P> c = ie_setup<P>(r, a.pic[pl], a.ps[pl], a.top[pl], a.ts[pl], a.sb_log2[pl], tx_info(txs).w >> 2,
+                                   tx_info(txs).h >> 2, a.bdmax);
     P *tl = a.edges + u->p.intra.edge_off;
-    for (int i = -2 * szl + l; i <= 2 * szt; i += kEdgeLanes) {
-        int v;
-        if (i < -szl) {           // bottom-left (:135-154)
-            if (!(nd & 16)) continue;
-            const int k = -i - szl - 1;
-            v = hbl ? (int)dst[(size_t)(szl + min(k, nbl - 1)) * ps - 1] : leftv(szl - 1);
-        } else if (i < 0) {       // left (:124-133)
-            if (!(nd & 1)) continue;
-            v = leftv(-i - 1);
-        } else if (i == 0) {      // top-left (:187-201)
-            if (!(nd & 4)) continue;
-            v = hl ? (ht ? (int)top[-1] : (int)dst[-1]) : (ht ? (int)top[0] : half);
-            if (mode == DGPU_Z2_PRED && tw + th >= 6 && (r.flags & DGPU_IE_FILTER_EDGE))
-                v = ((leftv(0) + topv(0)) * 5 + v * 6 + 8) >> 4;
-        } else if (i <= szt) {    // top (:156-166)
-            if (!(nd & 2)) continue;
-            v = topv(i - 1);
-        } else {                  // top-right (:168-185)
-            if (!(nd & 8)) continue;
-            const int k = i - szt - 1;
-            v = htr ? (int)top[szt + min(k, ntr - 1)] : topv(szt - 1);
-        }
-        tl[i] = (P)v;
+    for (int i = -2 * c.szl + l; i <= 2 * c.szt; i += kEdgeLanes) {
+        bool need;
+        const int v = ie_value(c, i, need);
+        if (need) tl[i] = (P)v;
     }
     if (l == 0) {
-        u->p.intra.mode = (uint8_t)mode;   // CFL: its DC source (the same byte)
-        if (u->pred != DGPU_PRED_CFL)
-            u->p.intra.angle = (uint16_t)((angle & 511) | ((r.flags & DGPU_IE_SMOOTH) ? 512 : 0) |
-                                      ((r.flags & DGPU_IE_FILTER_EDGE) ? 1024 : 0));
+        u->p.intra.mode = (uint8_t)c.mode;   // CFL: its DC source (the same byte)
+        if (u->pred != DGPU_PRED_CFL) u->p.intra.angle = ie_angle_field(r, c.angle);
     }
 }
 
@@ -212,10 +155,25 @@ static int launch_intra_frame(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraE
     if (s->n_levels && (s->unit_start[0] < 0 || s->unit_start[s->n_levels] > rb->n_units ||
                         s->rec_start[0] < 0 || s->rec_start[s->n_levels] > eb->n_recs || s->run_start[0] < 0))
         return -2;
+    const bool fused = s->flags & DGPU_IS_FUSED;
+    if (fused)
+        for (int l = 0; l <= s->n_levels; l++)
+            if (s->rec_start[l] != s->unit_start[l]) return -2;
     Dav1dGpuFrameBatch lb = *rb;
     memset(lb.class_warp, 0, sizeof(lb.class_warp));
     Dav1dGpuIntraEdgeBatch le = *eb;
     for (int l = 0; l < s->n_levels; l++) {
+        if (fused) {   // edges, prediction, residual and backups in one launch per level
+            lb.units = rb->units + s->unit_start[l];
+            lb.n_units = s->unit_start[l + 1] - s->unit_start[l];
+            memcpy(lb.class_start, s->class_start + (size_t)l * (NC + 1), sizeof(lb.class_start));
+            le.units = eb->units + s->unit_start[l];
+            le.recs = eb->recs + s->unit_start[l];
+            le.n_recs = lb.n_units;
+            const int rc = BPC == 8 ? dgpu_recon_ie_8bpc(&lb, &le, stream) : dgpu_recon_ie_16bpc(&lb, &le, stream);
+            if (rc) return rc;
+            continue;
+        }
         le.recs = eb->recs + s->rec_start[l];
         le.n_recs = s->rec_start[l + 1] - s->rec_start[l];
         int rc = le.n_recs ? launch_edges<BPC>(&le, stream) : 0;

@@ -1,0 +1,8 @@
+// recon_ie16.hip -- 16bpc instantiation of the intra wavefront's fused
+// reconstruction launch (recon_ie.hpp); its own TU so it compiles in
+// parallel with the unit batch and leaves that code unchanged.
+#include "recon_ie.hpp"
+
+int dgpu_recon_ie_16bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, void *stream) {
+    return dgpu::launch_ie<16>(b, e, (hipStream_t)stream);
+}

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "recon_kernel.hpp"
@@ -26,7 +27,7 @@ namespace dgpu {
 // waves per workgroup: waves never share LDS, so small workgroups only
 // serve to pack the CU's LDS tightly (one wave for the 64-point classes)
 template <int BPC, int GRP> __host__ __device__ constexpr int waves_per_block() {
-    return GRP == GROUP_HUGE ? 1 : 2;
+    return base_group(GRP) == GROUP_HUGE ? 1 : 2;
 }
 
 // log2(lanes_per_unit) of every class packed 3 bits each into a constant
@@ -43,10 +44,10 @@ constexpr uint64_t kLog2Lanes = pack_log2_lanes(std::make_integer_sequence<int, 
 #endif
 template <int BPC, int TX, int GRP>
 __device__ __forceinline__ void run_class(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
-                                          int first, int count, uint8_t *lds, int gw) {
+                                          const Dav1dGpuIntraEdge &rec, int first, int count, uint8_t *lds, int gw) {
     if constexpr (TX < DGPU_N_RECT_TX_SIZES && in_group(TX, GRP) &&
                   (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS))
-        recon_units<BPC, TX, GRP == GROUP_WARP>(a, pt, u, first, count, lds, gw, GRP);
+        recon_units<BPC, TX, GRP == GROUP_WARP, gathers(GRP)>(a, pt, u, rec, first, count, lds, gw, GRP);
 }
 
 // One switch (a compact compare tree) instead of a chain of class tests
@@ -54,9 +55,10 @@ __device__ __forceinline__ void run_class(const ReconArgs<BPC> &a, const PlaneTa
 // instruction-cache lines on every wave's way to its class.
 template <int BPC, int GRP>
 __device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
-                                         int cls, int first, int count, uint8_t *lds, int gw) {
+                                         const Dav1dGpuIntraEdge &rec, int cls, int first, int count, uint8_t *lds,
+                                         int gw) {
 #define DGPU_CASE(T) \
-    case T: run_class<BPC, T, GRP>(a, pt, u, first, count, lds, gw); break;
+    case T: run_class<BPC, T, GRP>(a, pt, u, rec, first, count, lds, gw); break;
     switch (cls) {
         DGPU_CASE(0) DGPU_CASE(1) DGPU_CASE(2) DGPU_CASE(3) DGPU_CASE(4) DGPU_CASE(5) DGPU_CASE(6)
         DGPU_CASE(7) DGPU_CASE(8) DGPU_CASE(9) DGPU_CASE(10) DGPU_CASE(11) DGPU_CASE(12) DGPU_CASE(13)
@@ -138,12 +140,16 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     const int count = min(U, cs1 - first);
     if (count <= 0) return;
     // this lane's unit descriptor (lanes past the last unit re-read it)
-    const Dav1dGpuUnit u = units[first + min((int)(threadIdx.x & 63) >> lg, count - 1)];
+    const int ui_ = first + min((int)(threadIdx.x & 63) >> lg, count - 1);
+    const Dav1dGpuUnit u = units[ui_];
+    Dav1dGpuIntraEdge rec{};
+    if constexpr (gathers(GRP)) rec = a.recs[ui_];   // its edge record, in the same round trip
     // per-wave copy of the plane table: lane-indexed vector loads of the
     // argument segment, in flight together with the descriptor loads (no
     // workgroup barrier: the waves do not wait for each other)
-    __shared__ PlaneTab<BPC> ptab[waves_per_block<BPC, GRP>()];
-    PlaneTab<BPC> &pt = ptab[wave];
+    using PT = std::conditional_t<gathers(GRP), PlaneTabIE<BPC>, PlaneTab<BPC>>;
+    __shared__ PT ptab[waves_per_block<BPC, GRP>()];
+    PT &pt = ptab[wave];
     {
         const int t = threadIdx.x & 63;
         const int tr = min(t, DGPU_MAX_REFS * 3 - 1), td = min(t, 2);   // clamped: loads need no branch
@@ -158,6 +164,16 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
         if (t < 3) {
             pt.dst[t] = dp;
             pt.dst_stride[t] = dsd;
+        }
+        if constexpr (gathers(GRP)) {
+            P *tp = a.top[td];
+            const int ts = a.top_stride[td], tr_ = a.top_rows[td], sl = a.sb_log2[td];
+            if (t < 3) {
+                pt.top[t] = tp;
+                pt.top_stride[t] = ts;
+                pt.top_rows[t] = tr_;
+                pt.sb_log2[t] = sl;
+            }
         }
     }
     wave_sync();
@@ -176,7 +192,7 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
         for (int i = threadIdx.x & 63; i < 193; i += 64) wt[i] = reinterpret_cast<const uint2 *>(dspt_warp)[i];
         wave_sync();
     }
-    dispatch<BPC, GRP>(a, pt, u, cls, first, count, lds + wave * WL, gw);
+    dispatch<BPC, GRP>(a, pt, u, rec, cls, first, count, lds + wave * WL, gw);
 }
 
 template <int BPC, int GRP>

@@ -31,6 +31,7 @@
 #pragma once
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
+#include "intra_edge_dev.hpp"
 
 #include <utility>
 
@@ -109,6 +110,16 @@ template <int BPC> struct ReconArgs {
     unsigned long long *trace;   // DGPU_TRACE builds only: [group][wave][16] s_memtime
     int bdmax;
     int zero_coefs;
+    // intra wavefront launches only (GROUP_*_IE): recs[i] is units[i]'s
+    // edge record; the edges are gathered from the picture in the kernel,
+    // the rewritten mode / angle go back to units_rw, and superblock-bottom
+    // rows are also stored to top[] (dav1d_backup_ipred_edge) when set
+    const Dav1dGpuIntraEdge *recs;
+    Dav1dGpuUnit *units_rw;
+    P *top[3];
+    int top_stride[3];   // pixels
+    int top_rows[3];
+    int sb_log2[3];
 };
 
 // Plane pointers and strides, copied once per workgroup into LDS so the
@@ -120,6 +131,14 @@ template <int BPC> struct PlaneTab {
     P *dst[3];
     int ref_stride[DGPU_MAX_REFS * 3];   // pixels
     int dst_stride[3];
+};
+
+template <int BPC> struct PlaneTabIE : PlaneTab<BPC> {
+    using P = typename Px<BPC>::pixel;
+    P *top[3];
+    int top_stride[3];   // pixels
+    int top_rows[3];
+    int sb_log2[3];
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -149,7 +168,15 @@ __host__ __device__ constexpr int lanes_per_unit(int tx) {
 #ifndef DGPU_MERGE_GROUPS
 #define DGPU_MERGE_GROUPS 1
 #endif
-enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2, GROUP_WARP = 3, N_GROUPS = 4 };
+#ifndef DGPU_IE_NOGATHER
+#define DGPU_IE_NOGATHER 0   // probe only: no edge gather in the intra wavefront kernels
+#endif
+enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2, GROUP_WARP = 3, N_GROUPS = 4,
+       // the intra wavefront's variants of SMALL / HUGE: edges gathered in
+       // the kernel (intra_edge_dev.hpp) instead of read from the edge pool
+       GROUP_SMALL_IE = 4, GROUP_HUGE_IE = 6 };
+__host__ __device__ constexpr int base_group(int grp) { return grp >= N_GROUPS ? grp - N_GROUPS : grp; }
+__host__ __device__ constexpr bool gathers(int grp) { return grp >= N_GROUPS; }
 __host__ __device__ constexpr int class_group(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
     return (w == 64 || h == 64) ? GROUP_HUGE
@@ -173,7 +200,8 @@ __device__ __forceinline__ int order_class(int k) {   // kOrder[k] without a mem
 
 // classes a launch of group GRP runs: the warp launch takes every class with
 // both sides >= 8 (its units are the WARP sub-ranges), the others by size
-__host__ __device__ constexpr bool in_group(int tx, int grp) {
+__host__ __device__ constexpr bool in_group(int tx, int grp_) {
+    const int grp = base_group(grp_);
     return grp == GROUP_WARP ? class_group(tx) != GROUP_HUGE : class_group(tx) == grp;
 }
 
@@ -1060,9 +1088,10 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
 
 // ---------------------------------------------------------------- kernel --
 
-template <int BPC, int TX, bool WARPK>
-__device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
-                                            int first, int count, uint8_t *wave_lds, int gw, int grp) {
+template <int BPC, int TX, bool WARPK, bool GATHER = false>
+__device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt,
+                                            const Dav1dGpuUnit &u_in, const Dav1dGpuIntraEdge &rec, int first,
+                                            int count, uint8_t *wave_lds, int gw, int grp) {
     using CL = Cls<TX>;
     using SL = Slot<BPC, TX>;
     using P = typename Px<BPC>::pixel;
@@ -1086,6 +1115,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     };
     mark(0);
 
+    Dav1dGpuUnit ug = u_in;   // GATHER: the edge stage rewrites its mode / angle
+    const Dav1dGpuUnit &u = GATHER ? ug : u_in;
     mark(1);   // the descriptor was loaded by the kernel prologue (lane's unit = first + g)
     uint8_t *slot = wave_lds + g * SL::BYTES;
     uint8_t *cfl = slot;                                           // staged coefs, then residual
@@ -1122,7 +1153,26 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     Stage<SL::EDGE * (int)sizeof(P), G> est;
     constexpr bool NW = !WARPK;   // the warp launch compiles only the WARP prediction
     const bool edged = NW && (pred == DGPU_PRED_INTRA || pred == DGPU_PRED_CFL);   // same edge_off in both views
-    if (edged) est.load(a.edges + u.p.intra.edge_off - 2 * H, SL::EDGE * (int)sizeof(P), l);
+    if (edged && !GATHER) est.load(a.edges + u.p.intra.edge_off - 2 * H, SL::EDGE * (int)sizeof(P), l);
+    IeCtx<P> iec;
+    if constexpr (GATHER && !DGPU_IE_NOGATHER) {   // dav1d_prepare_intra_edges, every entry straight into LDS
+        if (edged) {
+            const PlaneTabIE<BPC> &pti = static_cast<const PlaneTabIE<BPC> &>(pt);
+            iec = ie_setup<P>(rec, pt.dst[plane], ds, pti.top[plane], pti.top_stride[plane], pti.sb_log2[plane],
+                              W / 4, H / 4, bdmax);
+            P *tw_ = reinterpret_cast<P *>(src) + 2 * H;
+            for (int i = -2 * H + l; i <= 2 * W; i += G) {
+                bool need;
+                if (ie_need(iec, i)) tw_[i] = (P)ie_value(iec, i, need);
+            }
+            ug.p.intra.mode = (uint8_t)iec.mode;   // CFL: its DC source, the same byte
+            if (pred != DGPU_PRED_CFL) ug.p.intra.angle = ie_angle_field(rec, iec.angle);
+            if (l == 0) {
+                a.units_rw[first + g].p.intra.mode = ug.p.intra.mode;
+                if (pred != DGPU_PRED_CFL) a.units_rw[first + g].p.intra.angle = ug.p.intra.angle;
+            }
+        }
+    }
 
     // read for every unit (only inter kinds use it; the bank math below stays
     // in range for any byte).  Selecting it on `inter` gave inter-intra units
@@ -1176,7 +1226,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     int cfsk = 0;
     if (ncoef) cfsk = cst.commit(cfl, l);
     const P *tl = nullptr;
-    if (edged) tl = reinterpret_cast<const P *>(src + est.commit(src, l)) + 2 * H;
+    if (edged) tl = GATHER ? reinterpret_cast<const P *>(src) + 2 * H
+                           : reinterpret_cast<const P *>(src + est.commit(src, l)) + 2 * H;
     mark(2);
 
     // ---------------- P2: mc horizontal pass(es) ----------------
@@ -1285,6 +1336,15 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     // ---------------- P5/P6: prediction + residual -> picture ----------------
     // One loop per prediction kind, so values of one kind's path are not
     // live (register pressure) in another's.
+    // GATHER: a unit whose bottom row ends a superblock row also copies it
+    // to top_edge once stored (units never straddle superblock rows)
+    P *bkrow = nullptr;
+    if constexpr (GATHER) {
+        const PlaneTabIE<BPC> &pti = static_cast<const PlaneTabIE<BPC> &>(pt);
+        const int y1 = rec.y4 * 4 + H, sbl = pti.sb_log2[plane], sby = (y1 >> sbl) - 1;
+        if (pti.top[plane] && (y1 & ((1 << sbl) - 1)) == 0 && sby < pti.top_rows[plane])
+            bkrow = pti.top[plane] + (size_t)sby * pti.top_stride[plane] + rec.x4 * 4;
+    }
     auto emit = [&](int j, int q, const int *pv) {   // + residual, clip, store 2 rows of 4
         int rv[8];
         if (haveres) {
@@ -1522,6 +1582,13 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #pragma unroll
             for (int i = 0; i < 8; i++) pv[i] = gld<P>(dstp + (2 * j + (i >> 2)) * ds + 4 * q + (i & 3));
             emit(j, q, pv);
+        }
+    }
+    if constexpr (GATHER) {   // dav1d_backup_ipred_edge for this unit's columns
+        if (bkrow) {
+            wave_sync();   // this wave's picture stores are visible to its own loads
+            const P *last = dstp + (size_t)(H - 1) * ds;
+            for (int x = l; x < W; x += G) bkrow[x] = last[x];
         }
     }
     mark(8);

@@ -175,6 +175,9 @@ class IntraConfig:
     filter_edge: bool = True
     tx64: bool = True
     sb_log2: int = 6          # 64x64 superblocks
+    tile_cols: int = 1        # uniform tiling (in superblocks); tiles cut the
+    tile_rows: int = 1        # edge dependencies (have_left / have_top, w4 / h4)
+    sb_edge_backup: bool = True   # superblock-top rows read through top_edge
 
     @property
     def pixel_dtype(self):
@@ -236,9 +239,14 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     sbl = (cfg.sb_log2, cfg.sb_log2 - 1, cfg.sb_log2 - 1)
     sb = 1 << cfg.sb_log2
     lx, ly, ls = _partition(rng, W, H)
+    # uniform tiles of tsw x tsh superblocks, decoded in raster order
+    tsw = -(-(-(-W // sb)) // cfg.tile_cols) * sb
+    tsh = -(-(-(-H // sb)) // cfg.tile_rows) * sb
     order = np.lexsort((np.array([_morton((x % sb) >> 3, (y % sb) >> 3) for x, y in zip(lx, ly)]),
-                        lx // sb, ly // sb))
+                        lx // sb, ly // sb, lx // tsw, ly // tsh))
     lx, ly, ls = lx[order], ly[order], ls[order]
+    tile_x0, tile_y0 = (lx // tsw) * tsw, (ly // tsh) * tsh          # luma px
+    tile_x1, tile_y1 = np.minimum(tile_x0 + tsw, W), np.minimum(tile_y0 + tsh, H)
     nb = len(lx)
     ymode = rng.integers(0, 14, nb)
     ymode[(ymode == abi.FILTER_PRED) & (ls > 32)] = abi.DC_PRED
@@ -258,10 +266,12 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     U = {k: [] for k in ("plane", "x", "y", "tw", "th", "blk", "cfl", "mode", "angle", "flags")}
     for b in range(nb):
         x, y, s = int(lx[b]), int(ly[b]), int(ls[b])
-        tr = y > 0 and x + s < W and bmap[(y - 1) // 4, (x + s) // 4] < b
-        bl = x > 0 and y + s < H and bmap[(y + s) // 4, (x - 1) // 4] < b
-        above = bmap[(y - 1) // 4, x // 4] if y > 0 else -1
-        left = bmap[y // 4, (x - 1) // 4] if x > 0 else -1
+        x0, y0, x1, y1 = int(tile_x0[b]), int(tile_y0[b]), int(tile_x1[b]), int(tile_y1[b])
+        tr = y > y0 and x + s < x1 and bmap[(y - 1) // 4, (x + s) // 4] < b
+        bl = x > x0 and y + s < y1 and bmap[(y + s) // 4, (x - 1) // 4] < b
+        # mode contexts are reset at tile starts (dav1d_reset_context)
+        above = bmap[(y - 1) // 4, x // 4] if y > y0 else -1
+        left = bmap[y // 4, (x - 1) // 4] if x > x0 else -1
         ysm = (above >= 0 and smooth(ymode[above])) or (left >= 0 and smooth(ymode[left]))
         uvsm = ((above >= 0 and not is_cfl[above] and smooth(uvmode[above])) or
                 (left >= 0 and not is_cfl[left] and smooth(uvmode[left])))
@@ -306,10 +316,14 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     pw = np.array([p[0] for p in planes])
     ph = np.array([p[1] for p in planes])
     flags = np.array(U["flags"], np.int32)
-    flags |= np.where(ux > 0, abi.IE_HAVE_LEFT, 0)
-    flags |= np.where(uy > 0, abi.IE_HAVE_TOP, 0)
+    ssu = np.where(plane_u > 0, 1, 0)
+    tx0, ty0 = tile_x0[blk] >> ssu, tile_y0[blk] >> ssu         # the unit's tile, plane px
+    tx1, ty1 = tile_x1[blk] >> ssu, tile_y1[blk] >> ssu
+    flags |= np.where(ux > tx0, abi.IE_HAVE_LEFT, 0)
+    flags |= np.where(uy > ty0, abi.IE_HAVE_TOP, 0)
     sbh = np.array([1 << s_ for s_ in sbl])[plane_u]
-    flags |= np.where((uy > 0) & (uy % sbh == 0), abi.IE_TOP_SB_EDGE, 0)
+    if cfg.sb_edge_backup:
+        flags |= np.where((uy > ty0) & (uy % sbh == 0), abi.IE_TOP_SB_EDGE, 0)
 
     units = np.zeros(n, abi.UNIT_DTYPE)   # decode order for now
     units["dst_off"] = uy * pw[plane_u] + ux
@@ -338,7 +352,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     for i in range(n):
         p, x4, y4 = int(plane_u[i]), int(ux[i]) // 4, int(uy[i]) // 4
         t4w, t4h = int(tw[i]) // 4, int(th[i]) // 4
-        w4, h4 = int(pw[p]) // 4, int(ph[p]) // 4
+        w4, h4 = int(tx1[i]) // 4, int(ty1[i]) // 4
         f = int(flags[i])
         hl, ht = bool(f & abi.IE_HAVE_LEFT), bool(f & abi.IE_HAVE_TOP)
         m, _ = remap_mode(modes[i], angles[i], hl, ht)
@@ -374,7 +388,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     # backup runs: each superblock row's last pixel row, per run of 4x4
     # columns written at one level, backed up right after that level
     runs, run_lv = [], []
-    for p, (w, h) in enumerate(planes):
+    for p, (w, h) in enumerate(planes if cfg.sb_edge_backup else []):
         nsb = (h + (1 << sbl[p]) - 1) >> sbl[p]
         for r in range(nsb - 1):
             row = lv[p][(((r + 1) << sbl[p]) - 1) // 4]
@@ -388,16 +402,22 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     run_lv = np.array(run_lv, np.int64)
 
     # the decoder's order with whole-row backups at superblock-row ends
+    # (per tile superblock row, dav1d_backup_ipred_edge at its end)
     steps, oracle_runs = [], []
-    cur_sbrow = 0
-    for i in range(n):
-        r = int(ly[blk[i]]) >> cfg.sb_log2
-        while r > cur_sbrow:
+    cur = None
+    for i in range(n + 1):
+        key = None if i == n else (int(tile_y0[blk[i]]), int(tile_x0[blk[i]]), int(ly[blk[i]]) >> cfg.sb_log2)
+        if cur is not None and key != cur and cfg.sb_edge_backup:
+            _, cx0, r = cur
+            cx1 = min(cx0 + tsw, W)
             for p, (w, h) in enumerate(planes):
-                oracle_runs.append((p, cur_sbrow, 0, w))
-                steps.append((1, len(oracle_runs) - 1))
-            cur_sbrow += 1
-        steps.append((0, i))
+                ss_ = 0 if p == 0 else 1
+                if ((r + 1) << sbl[p]) <= h:
+                    oracle_runs.append((p, r, cx0 >> ss_, (cx1 - cx0) >> ss_))
+                    steps.append((1, len(oracle_runs) - 1))
+        cur = key
+        if i < n:
+            steps.append((0, i))
 
     # level order, size classes inside a level, then pred / mode / type
     perm = np.lexsort((units["txtp"], np.array(modes), units["pred"], units["tx"], level))
@@ -411,16 +431,16 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     for l_ in range(n_levels):
         t = units["tx"][unit_start[l_]:unit_start[l_ + 1]]
         class_start[l_, 1:] = np.cumsum(np.bincount(t, minlength=abi.N_TX))
+    # one record per unit (every unit is INTRA or CFL), in unit order:
+    # record i serves unit i, as the fused launch requires
     recs = np.zeros(n, abi.INTRA_EDGE_DTYPE)
     recs["unit"] = inv
     recs["x4"], recs["y4"] = ux // 4, uy // 4
-    recs["w4"], recs["h4"] = pw[plane_u] // 4, ph[plane_u] // 4
+    recs["w4"], recs["h4"] = tx1 // 4, ty1 // 4
     recs["mode"], recs["angle"], recs["flags"] = modes, angles, flags
-    rperm = np.argsort(level, kind="stable")
-    recs = recs[rperm]
-    rec_start = np.searchsorted(level[rperm], np.arange(n_levels + 1)).astype(np.int32)
-    unit_rec = np.full(n, -1, np.int32)
-    unit_rec[recs["unit"]] = np.arange(n)
+    recs = recs[perm]
+    rec_start = unit_start.copy()
+    unit_rec = np.arange(n, dtype=np.int32)
     rp = np.argsort(run_lv, kind="stable")
     runs = runs[rp]
     run_start = np.searchsorted(run_lv[rp], np.arange(n_levels + 1)).astype(np.int32)
@@ -455,7 +475,10 @@ def edge_batch(fr, dst_ptrs, top_ptrs, units, edges, recs):
     for p, (w, h) in enumerate(fr.plane_wh):
         b.pic[p].data, b.pic[p].stride, b.pic[p].w, b.pic[p].h = dst_ptrs[p], w * bpp, w, h
         rows, tw_ = fr.top_rows[p]
-        b.top_edge[p].data, b.top_edge[p].stride = top_ptrs[p], tw_ * bpp
+        # no top_edge when the frame does not back up superblock rows (the
+        # fused launch stores superblock-bottom rows whenever it has one)
+        b.top_edge[p].data = top_ptrs[p] if fr.cfg.sb_edge_backup else None
+        b.top_edge[p].stride = tw_ * bpp
         b.top_edge[p].w, b.top_edge[p].h = tw_, rows
         b.sb_log2[p] = fr.sb_log2[p]
     b.units, b.edges, b.recs = units, edges, recs
@@ -468,7 +491,7 @@ class DeviceIntraFrame:
     """An IntraFrame on one GPU; launch() runs the whole wavefront
     (dav1d_gpu_recon_intra_frame_*) on a stream."""
 
-    def __init__(self, fr, device="cuda:0", top_fill=0x5A):
+    def __init__(self, fr, device="cuda:0", top_fill=0x5A, fused=True):
         import torch
         self.torch, self.fr = torch, fr
         dev = torch.device(device)
@@ -491,6 +514,7 @@ class DeviceIntraFrame:
                       (fr.unit_start, fr.class_start, fr.rec_start, fr.run_start)]
         s = abi.IntraSchedule()
         s.n_levels = fr.n_levels
+        s.flags = abi.IS_FUSED if fused else 0
         s.unit_start, s.class_start, s.rec_start, s.run_start = (a.ctypes.data for a in self._host)
         s.runs = self.runs.data_ptr()
         self.sched = s

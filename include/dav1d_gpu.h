@@ -561,8 +561,15 @@ int dav1d_gpu_backup_ipred_edge_16bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav
  * one stream.  This replaces recon_b_intra's per-transform-block sequence
  * prepare_intra_edges -> intra_pred / cfl_pred -> itxfm_add
  * (src/recon_tmpl.c:1195-1596) for a whole frame without host round trips. */
+#define DGPU_IS_FUSED 1   /* one launch per level: the reconstruction kernel
+                             gathers each unit's edges itself (record i serves
+                             unit i: rec_start == unit_start) and stores
+                             superblock-bottom rows to top_edge as it writes
+                             them; run_start / runs are then unused */
+
 typedef struct Dav1dGpuIntraSchedule {
     int32_t n_levels;
+    int32_t flags;               /* DGPU_IS_*                                   */
     const int32_t *unit_start;   /* host, n_levels + 1: the level's units in
                                     recon->units (contiguous)                 */
     const int32_t *class_start;  /* host, n_levels x (DGPU_N_RECT_TX_SIZES+1):

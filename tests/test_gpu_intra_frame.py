@@ -9,10 +9,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _check(oracle, fr):
+def _check(oracle, fr, fused=True):
     import torch
     import dav1d_mirror_amd.intra as intra
-    dev = intra.DeviceIntraFrame(fr)
+    dev = intra.DeviceIntraFrame(fr, fused=fused)
     dev.launch()
     torch.cuda.synchronize()
     got = dev.planes_host()
@@ -34,13 +34,19 @@ def _frame(**kw):
     return intra.make_intra_frame(intra.IntraConfig(**kw))
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023), (16, 4095)])
-def test_intra_frame(oracle, bpc, bdmax):
-    _check(oracle, _frame(seed=31, bpc=bpc, bitdepth_max=bdmax))
+def test_intra_frame(oracle, bpc, bdmax, fused):
+    """fused: one launch per level (edges gathered in the reconstruction
+    kernel, backups with the stores); else edge stage, unit batch and
+    backup runs as three launches per level."""
+    _check(oracle, _frame(seed=31, bpc=bpc, bitdepth_max=bdmax), fused=fused)
 
 
 @pytest.mark.parametrize("kw", [dict(seed=32, cfl_frac=1.0), dict(seed=33, filter_edge=False, tx64=False),
-                                dict(seed=34, width=480, height=264), dict(seed=35, sb_log2=7, width=512, height=384)])
+                                dict(seed=34, width=480, height=264), dict(seed=35, sb_log2=7, width=512, height=384),
+                                dict(seed=38, width=640, height=384, tile_cols=3, tile_rows=2),
+                                dict(seed=39, tile_cols=2, sb_edge_backup=False)])
 def test_intra_frame_variants(oracle, kw):
     _check(oracle, _frame(**kw))
 
@@ -57,6 +63,7 @@ def test_intra_frame_relaunch(oracle):
         assert np.array_equal(a, b)
 
 
-def test_intra_frame_1080p(oracle):
+@pytest.mark.parametrize("fused", [True, False])
+def test_intra_frame_1080p(oracle, fused):
     """A 1080p intra frame (partial superblock row at the bottom)."""
-    _check(oracle, _frame(seed=37, width=1920, height=1080))
+    _check(oracle, _frame(seed=37, width=1920, height=1080), fused=fused)
