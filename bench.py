@@ -158,9 +158,10 @@ def tile_breakdown(fd, dev, stream, steps):
 def intra_breakdown(cfg, dev, stream, steps):
     """an all-intra frame of the config's size and
     bitdepth reconstructed on the device by the intra wavefront
-    (dav1d_gpu_recon_intra_frame_*, fused: one launch per dependency level),
-    one tile and 2x2 tiles; beside it the oracle in the decoder's own order
-    on one host core.  Reported beside the headline, not part of it."""
+    (dav1d_gpu_recon_intra_frame_*: persistent, one launch per frame whose
+    waves wait on per-level counters; and fused, one launch per level), one
+    tile and 2x2 tiles; beside it the oracle in the decoder's own order on
+    one host core.  Reported beside the headline, not part of it."""
     import dav1d_mirror_amd.intra as intra
     out = {}
     orc = ge.load_oracle()
@@ -168,21 +169,27 @@ def intra_breakdown(cfg, dev, stream, steps):
         fr = intra.make_intra_frame(intra.IntraConfig(width=cfg.width, height=cfg.height, bpc=cfg.bpc,
                                                       bitdepth_max=cfg.bitdepth_max, tile_cols=tiles[0],
                                                       tile_rows=tiles[1]))
-        frame = intra.DeviceIntraFrame(fr, dev)
-        for _ in range(2):
-            frame.launch(stream)
-        ks = kernel_seconds(frame, stream, max(3, min(steps, 5)))
+        ms = {}
+        for mode in ("persistent", "fused"):
+            frame = intra.DeviceIntraFrame(fr, dev, mode=mode)
+            for _ in range(2):
+                frame.launch(stream)
+            ms[mode] = kernel_seconds(frame, stream, max(3, min(steps, 5)))
+            if mode == "persistent":
+                flow_error = frame.flow_error()
+                got = frame.planes_host()
+            del frame
+        ks = ms["persistent"]
         ho = orc.HostIntraFrame(fr)
         t0 = time.perf_counter()
         ho.run()
         cpu_s = time.perf_counter() - t0
-        got = frame.planes_host()
         px = sum(w * h for w, h in fr.plane_wh)
         out[name] = {"units": int(len(fr.units)), "levels": int(fr.n_levels), "ms_per_frame": round(ks * 1e3, 3),
                      "gpix_s": round(px / ks / 1e9, 4), "us_per_level": round(ks * 1e6 / fr.n_levels, 2),
-                     "oracle_1core_ms": round(cpu_s * 1e3, 2),
+                     "fused_ms_per_frame": round(ms["fused"] * 1e3, 3),
+                     "oracle_1core_ms": round(cpu_s * 1e3, 2), "flow_error": flow_error,
                      "bit_exact_vs_oracle": all(bool(np.array_equal(g, o)) for g, o in zip(got, ho.dst))}
-        del frame
     return out
 
 

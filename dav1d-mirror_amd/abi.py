@@ -124,7 +124,7 @@ class IntraEdgeBatch(ctypes.Structure):
                 ("bitdepth_max", ctypes.c_int32)]
 
 
-IS_FUSED = 1
+IS_FUSED, IS_PERSISTENT = 1, 2
 EDGE_BACKUP_DTYPE = np.dtype([("plane", "<i4"), ("sby", "<i4"), ("x0", "<i4"), ("w", "<i4")])
 
 
@@ -135,7 +135,9 @@ class IntraSchedule(ctypes.Structure):
                 ("class_start", ctypes.c_void_p),
                 ("rec_start", ctypes.c_void_p),
                 ("run_start", ctypes.c_void_p),
-                ("runs", ctypes.c_void_p)]
+                ("runs", ctypes.c_void_p),
+                ("workspace", ctypes.c_void_p),
+                ("workspace_bytes", ctypes.c_int64)]
 
 
 _LIB = None
@@ -179,6 +181,8 @@ def load_lib():
             f.argtypes = [ctypes.POINTER(FrameBatch), ctypes.POINTER(IntraEdgeBatch),
                           ctypes.POINTER(IntraSchedule), ctypes.c_void_p]
             f.restype = ctypes.c_int
+        L.dav1d_gpu_intra_workspace_bytes.argtypes = [ctypes.POINTER(IntraSchedule), ctypes.c_int]
+        L.dav1d_gpu_intra_workspace_bytes.restype = ctypes.c_int64
         L.dav1d_gpu_recon_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         L.dav1d_gpu_recon_lds_bytes.restype = ctypes.c_int
         _LIB = L
@@ -199,4 +203,5 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_prepare_intra_edges_8bpc", "dav1d_gpu_prepare_intra_edges_16bpc",
     "dav1d_gpu_backup_ipred_edge_8bpc", "dav1d_gpu_backup_ipred_edge_16bpc",
     "dav1d_gpu_recon_intra_frame_8bpc", "dav1d_gpu_recon_intra_frame_16bpc",
+    "dav1d_gpu_intra_workspace_bytes",
 ]

@@ -21,6 +21,11 @@
 // the fused reconstruction launch (recon_ie.hpp, recon_ie8/16.hip)
 int dgpu_recon_ie_8bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, void *stream);
 int dgpu_recon_ie_16bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, void *stream);
+int dgpu_recon_flow_8bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, const Dav1dGpuIntraSchedule *s,
+                         void *stream);
+int dgpu_recon_flow_16bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, const Dav1dGpuIntraSchedule *s,
+                          void *stream);
+int64_t dgpu_flow_workspace_bytes_8bpc(const Dav1dGpuIntraSchedule *s, int n_units);
 
 namespace dgpu {
 
@@ -155,6 +160,12 @@ static int launch_intra_frame(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraE
     if (s->n_levels && (s->unit_start[0] < 0 || s->unit_start[s->n_levels] > rb->n_units ||
                         s->rec_start[0] < 0 || s->rec_start[s->n_levels] > eb->n_recs || s->run_start[0] < 0))
         return -2;
+    if (s->flags & DGPU_IS_PERSISTENT) {   // one launch: the level loop runs on the device
+        if (s->n_levels && s->rec_start[0] != s->unit_start[0]) return -2;
+        for (int l = 0; l <= s->n_levels; l++)
+            if (s->rec_start[l] != s->unit_start[l]) return -2;
+        return BPC == 8 ? dgpu_recon_flow_8bpc(rb, eb, s, stream) : dgpu_recon_flow_16bpc(rb, eb, s, stream);
+    }
     const bool fused = s->flags & DGPU_IS_FUSED;
     if (fused)
         for (int l = 0; l <= s->n_levels; l++)
@@ -212,4 +223,8 @@ extern "C" int dav1d_gpu_recon_intra_frame_8bpc(const Dav1dGpuFrameBatch *recon,
 extern "C" int dav1d_gpu_recon_intra_frame_16bpc(const Dav1dGpuFrameBatch *recon, const Dav1dGpuIntraEdgeBatch *edges,
                                                  const Dav1dGpuIntraSchedule *s, void *stream) {
     return dgpu::launch_intra_frame<16>(recon, edges, s, (hipStream_t)stream);
+}
+extern "C" int64_t dav1d_gpu_intra_workspace_bytes(const Dav1dGpuIntraSchedule *s, int n_units) {
+    if (!s || s->n_levels < 0 || (s->n_levels && (!s->unit_start || !s->class_start))) return -2;
+    return dgpu_flow_workspace_bytes_8bpc(s, n_units);
 }

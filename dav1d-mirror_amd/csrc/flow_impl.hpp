@@ -1,0 +1,248 @@
+// flow_impl.hpp -- the persistent intra wavefront kernel (DGPU_IS_PERSISTENT).
+//
+// One launch per frame instead of one per dependency level.  The host cuts
+// every level into wave tasks (one size class, up to 64/G units, the
+// unit batch's own grouping), in level order; the grid has one wave per
+// task.  A wave takes a task by ticket (one atomic counter), waits until
+// every task of the previous level has been counted done (a per-level
+// counter, polled by one lane with s_sleep between polls), runs the task
+// through the same class code as the unit batch (GATHER: edges from the
+// picture, backups of superblock-bottom rows), then releases its stores at
+// agent scope and counts itself done.
+//
+// Progress: tickets go out in level order to waves that already run, and a
+// wave waits only for tasks with smaller tickets, so every awaited task is
+// held by a resident wave that itself waits only on earlier ones.  A poll
+// bound (DGPU_FLOW_SPIN_LIMIT) turns any unexpected stall into an error
+// flag; a wave that gives up still counts itself done, so the grid drains.
+#pragma once
+#include <vector>
+
+#include "recon_impl.hpp"
+
+#ifndef DGPU_FLOW_SPIN_LIMIT
+#define DGPU_FLOW_SPIN_LIMIT (1 << 21)   // polls of ~0.25 us: ~0.5 s
+#endif
+
+#ifndef DGPU_FLOW_NOFENCE
+#define DGPU_FLOW_NOFENCE 0   // probe only: no agent-scope fences (unsafe)
+#endif
+#ifndef DGPU_FLOW_TRACE
+#define DGPU_FLOW_TRACE 0     // probe only: per-task s_memrealtime stamps after the task list
+#endif
+#ifndef DGPU_FLOW_SLEEP
+#define DGPU_FLOW_SLEEP 8     // s_sleep between polls (x64 cycles)
+#endif
+
+namespace dgpu {
+
+struct FlowTask {   // 16 B
+    int32_t level, cls, first, count;
+};
+
+// workspace: counters, then tasks, then per-level task counts
+constexpr int kFlowCtrHead = 32;                 // ints: [0] ticket, [1] error
+constexpr int kFlowCtrStride = 16;               // ints per level counter (64 B apart)
+__host__ __device__ constexpr size_t flow_ctr_ints(int n_levels) {
+    return kFlowCtrHead + (size_t)kFlowCtrStride * (size_t)(n_levels > 0 ? n_levels : 1);
+}
+
+struct FlowArgs {
+    const FlowTask *tasks;
+    int n_tasks;
+    const int32_t *level_tasks;   // tasks per level
+    int *ctr;
+    unsigned long long *trace;    // DGPU_FLOW_TRACE: [ticket][4] start, ready, computed, released
+};
+
+template <int BPC>
+__global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    using P = typename Px<BPC>::pixel;
+    __shared__ PlaneTabIE<BPC> pt;
+    const int lane = threadIdx.x & 63;
+    {   // plane and top_edge tables, as in k_recon's prologue
+        const int td = min(lane, 2);
+        P *dp = a.dst[td];
+        const int dsd = a.dst_stride[td];
+        P *tp = a.top[td];
+        const int ts = a.top_stride[td], tr = a.top_rows[td], sl = a.sb_log2[td];
+        if (lane < 3) {
+            pt.dst[lane] = dp;
+            pt.dst_stride[lane] = dsd;
+            pt.top[lane] = tp;
+            pt.top_stride[lane] = ts;
+            pt.top_rows[lane] = tr;
+            pt.sb_log2[lane] = sl;
+        }
+    }
+    wave_sync();
+    // one task per wave, taken by ticket: tickets go out in the order waves
+    // start, so every task a wave waits for is held by a wave that already
+    // runs (a loop over tasks would hoist the argument loads out of the
+    // whole class code and spill)
+    int t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(&f.ctr[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t >= f.n_tasks) return;
+    unsigned long long tr0 = 0, tr1 = 0, tr2 = 0;
+    if constexpr (DGPU_FLOW_TRACE) tr0 = __builtin_amdgcn_s_memrealtime();
+    const FlowTask task = f.tasks[t];
+    const int level = __builtin_amdgcn_readfirstlane(task.level);
+    const int cls = __builtin_amdgcn_readfirstlane(task.cls);
+    const int first = __builtin_amdgcn_readfirstlane(task.first);
+    const int count = __builtin_amdgcn_readfirstlane(task.count);
+    if (level > 0) {
+        int ok = 1;
+        if (lane == 0) {
+            const int need = f.level_tasks[level - 1];
+            int *done = &f.ctr[kFlowCtrHead + kFlowCtrStride * (level - 1)];
+            for (int it = 0;; it++) {
+                if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+                if (it >= DGPU_FLOW_SPIN_LIMIT ||
+                    __hip_atomic_load(&f.ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(DGPU_FLOW_SLEEP);
+            }
+            if (!ok) __hip_atomic_store(&f.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // a wave that gave up still counts itself done, so no later wave
+        // waits on it longer than its own bound
+        if (!__builtin_amdgcn_readfirstlane(ok)) {
+            if (lane == 0)
+                __hip_atomic_fetch_add(&f.ctr[kFlowCtrHead + kFlowCtrStride * level], 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        // the previous levels' picture / top_edge stores are visible from here
+        if (!DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    if constexpr (DGPU_FLOW_TRACE) tr1 = __builtin_amdgcn_s_memrealtime();
+    const int lg = (int)((kLog2Lanes >> (3 * cls)) & 7);
+    const int ui = first + min(lane >> lg, count - 1);
+    const Dav1dGpuUnit u = a.units[ui];
+    const Dav1dGpuIntraEdge rec = a.recs[ui];
+    dispatch<BPC, GROUP_ALL_IE>(a, pt, u, rec, cls, first, count, lds, 0);
+    if constexpr (DGPU_FLOW_TRACE) {
+        __builtin_amdgcn_s_waitcnt(0);
+        tr2 = __builtin_amdgcn_s_memrealtime();
+    }
+    // this task's stores reach agent scope before it is counted
+    if (!DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    else __builtin_amdgcn_s_waitcnt(0);
+    if (lane == 0)
+        __hip_atomic_fetch_add(&f.ctr[kFlowCtrHead + kFlowCtrStride * level], 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (DGPU_FLOW_TRACE) {
+        const unsigned long long tr3 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            f.trace[4 * (size_t)t + 0] = tr0;
+            f.trace[4 * (size_t)t + 1] = tr1;
+            f.trace[4 * (size_t)t + 2] = tr2;
+            f.trace[4 * (size_t)t + 3] = tr3;
+        }
+    }
+}
+
+// host: the wave tasks of a schedule (level order, classes largest first)
+static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<FlowTask> &tasks,
+                      std::vector<int32_t> &level_tasks) {
+    constexpr int NC = DGPU_N_RECT_TX_SIZES;
+    tasks.clear();
+    level_tasks.assign(s->n_levels > 0 ? s->n_levels : 1, 0);
+    for (int l = 0; l < s->n_levels; l++) {
+        const int u0 = s->unit_start[l];
+        const int32_t *cs = s->class_start + (size_t)l * (NC + 1);
+        if (u0 < 0 || s->unit_start[l + 1] < u0 || s->unit_start[l + 1] > n_units) return -2;
+        if (cs[0] != 0 || cs[NC] != s->unit_start[l + 1] - u0) return -2;
+        for (int k = 0; k < NC; k++) {
+            const int c = kOrder[k];
+            if (cs[c + 1] < cs[c]) return -2;
+            const int U = 64 >> (int)((kLog2Lanes >> (3 * c)) & 7);
+            for (int i = cs[c]; i < cs[c + 1]; i += U) {
+                tasks.push_back(FlowTask{l, c, u0 + i, std::min(U, cs[c + 1] - i)});
+                level_tasks[l]++;
+            }
+        }
+    }
+    return 0;
+}
+
+template <int BPC>
+static int64_t flow_workspace_bytes(const Dav1dGpuIntraSchedule *s, int n_units) {
+    std::vector<FlowTask> t;
+    std::vector<int32_t> lt;
+    if (flow_tasks(s, n_units, t, lt)) return -2;
+    const size_t base = flow_ctr_ints(s->n_levels) * 4 + t.size() * sizeof(FlowTask) + lt.size() * 4;
+    return (int64_t)(DGPU_FLOW_TRACE ? ((base + 15) & ~(size_t)15) + t.size() * 32 : base);
+}
+
+template <int BPC>
+static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, const Dav1dGpuIntraSchedule *s,
+                       hipStream_t stream) {
+    using P = typename Px<BPC>::pixel;
+    using C = typename Px<BPC>::coef;
+    constexpr int B = BPC / 8;
+    if (!b || !e || !s || !b->units || !e->recs || !s->workspace) return -1;
+    for (int p = 0; p < 3; p++)
+        if (((uintptr_t)b->dst[p].data & 15) || (b->dst[p].stride & 15)) return -4;
+    std::vector<FlowTask> tasks;
+    std::vector<int32_t> level_tasks;
+    int rc = flow_tasks(s, b->n_units, tasks, level_tasks);
+    if (rc) return rc;
+    if (tasks.empty()) return 0;
+    const size_t ctr_bytes = flow_ctr_ints(s->n_levels) * 4;
+    const size_t base = ctr_bytes + tasks.size() * sizeof(FlowTask) + level_tasks.size() * 4;
+    const size_t need = DGPU_FLOW_TRACE ? ((base + 15) & ~(size_t)15) + tasks.size() * 32 : base;
+    if ((size_t)s->workspace_bytes < need || ((uintptr_t)s->workspace & 15)) return -5;
+    uint8_t *ws = (uint8_t *)s->workspace;
+    FlowArgs f;
+    f.ctr = (int *)ws;
+    f.tasks = (const FlowTask *)(ws + ctr_bytes);
+    f.n_tasks = (int)tasks.size();
+    f.level_tasks = (const int32_t *)(ws + ctr_bytes + tasks.size() * sizeof(FlowTask));
+    f.trace = (unsigned long long *)(ws + ((base + 15) & ~(size_t)15));
+    // (pageable sources: the copies are staged before these calls return)
+    if (hipMemsetAsync(ws, 0, ctr_bytes, stream) != hipSuccess ||
+        hipMemcpyAsync(ws + ctr_bytes, tasks.data(), tasks.size() * sizeof(FlowTask), hipMemcpyHostToDevice,
+                       stream) != hipSuccess ||
+        hipMemcpyAsync(ws + ctr_bytes + tasks.size() * sizeof(FlowTask), level_tasks.data(),
+                       level_tasks.size() * 4, hipMemcpyHostToDevice, stream) != hipSuccess)
+        return -3;
+    ReconArgs<BPC> a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) {
+        a.dst[p] = (P *)b->dst[p].data;
+        a.dst_stride[p] = (int)(b->dst[p].stride / B);
+        a.top[p] = (P *)e->top_edge[p].data;
+        a.top_stride[p] = (int)(e->top_edge[p].stride / B);
+        a.top_rows[p] = e->top_edge[p].h;
+        a.sb_log2[p] = e->sb_log2[p];
+    }
+    a.units = b->units;
+    a.units_rw = e->units;
+    a.recs = e->recs;
+    a.coef = (C *)b->coef;
+    a.edges = (const P *)b->edges;
+    a.cfl_luma = (const P *)b->cfl_luma.data;
+    a.cfl_luma_stride = (int)(b->cfl_luma.stride / B);
+    a.cfl_ss = b->cfl_ss;
+    a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
+    a.zero_coefs = b->zero_coefs;
+    constexpr int lds = wave_lds<BPC, GROUP_ALL_IE>();
+    static std::once_flag once;
+    std::call_once(once, [] {
+        (void)hipFuncSetAttribute((const void *)k_flow<BPC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    });
+    k_flow<BPC><<<dim3((unsigned)tasks.size()), 64, lds, stream>>>(a, f);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fprintf(stderr, "dav1d-gpu: intra flow launch failed: %s\n", hipGetErrorString(err));
+        return -3;
+    }
+    return 0;
+}
+
+}  // namespace dgpu

@@ -5,6 +5,7 @@
 // of superblock-bottom rows.  Instantiated in recon_ie8.hip / recon_ie16.hip.
 #pragma once
 #include "recon_impl.hpp"
+#include "flow_impl.hpp"
 
 namespace dgpu {
 

@@ -174,8 +174,12 @@ __host__ __device__ constexpr int lanes_per_unit(int tx) {
 enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2, GROUP_WARP = 3, N_GROUPS = 4,
        // the intra wavefront's variants of SMALL / HUGE: edges gathered in
        // the kernel (intra_edge_dev.hpp) instead of read from the edge pool
-       GROUP_SMALL_IE = 4, GROUP_HUGE_IE = 6 };
-__host__ __device__ constexpr int base_group(int grp) { return grp >= N_GROUPS ? grp - N_GROUPS : grp; }
+       GROUP_SMALL_IE = 4, GROUP_HUGE_IE = 6,
+       // the persistent intra wavefront kernel (flow_impl.hpp): every class
+       GROUP_ALL_IE = 8 };
+__host__ __device__ constexpr int base_group(int grp) {
+    return grp == GROUP_ALL_IE ? GROUP_HUGE : grp >= N_GROUPS ? grp - N_GROUPS : grp;
+}
 __host__ __device__ constexpr bool gathers(int grp) { return grp >= N_GROUPS; }
 __host__ __device__ constexpr int class_group(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
@@ -201,6 +205,7 @@ __device__ __forceinline__ int order_class(int k) {   // kOrder[k] without a mem
 // classes a launch of group GRP runs: the warp launch takes every class with
 // both sides >= 8 (its units are the WARP sub-ranges), the others by size
 __host__ __device__ constexpr bool in_group(int tx, int grp_) {
+    if (grp_ == GROUP_ALL_IE) return true;
     const int grp = base_group(grp_);
     return grp == GROUP_WARP ? class_group(tx) != GROUP_HUGE : class_group(tx) == grp;
 }
@@ -1160,11 +1165,20 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             const PlaneTabIE<BPC> &pti = static_cast<const PlaneTabIE<BPC> &>(pt);
             iec = ie_setup<P>(rec, pt.dst[plane], ds, pti.top[plane], pti.top_stride[plane], pti.sb_log2[plane],
                               W / 4, H / 4, bdmax);
+            // every entry's load first (a fixed, unrolled count per lane, so
+            // the loads go out together), then the LDS writes
+            constexpr int NE = 2 * W + 2 * H + 1, EPL = (NE + G - 1) / G;
             P *tw_ = reinterpret_cast<P *>(src) + 2 * H;
-            for (int i = -2 * H + l; i <= 2 * W; i += G) {
+            int ev[EPL];
+#pragma unroll
+            for (int k = 0; k < EPL; k++) {
+                const int i = -2 * H + l + k * G;
                 bool need;
-                if (ie_need(iec, i)) tw_[i] = (P)ie_value(iec, i, need);
+                ev[k] = (i <= 2 * W && ie_need(iec, i)) ? ie_value(iec, i, need) : -1;
             }
+#pragma unroll
+            for (int k = 0; k < EPL; k++)
+                if (ev[k] >= 0) tw_[-2 * H + l + k * G] = (P)ev[k];
             ug.p.intra.mode = (uint8_t)iec.mode;   // CFL: its DC source, the same byte
             if (pred != DGPU_PRED_CFL) ug.p.intra.angle = ie_angle_field(rec, iec.angle);
             if (l == 0) {

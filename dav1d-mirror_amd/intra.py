@@ -491,7 +491,13 @@ class DeviceIntraFrame:
     """An IntraFrame on one GPU; launch() runs the whole wavefront
     (dav1d_gpu_recon_intra_frame_*) on a stream."""
 
-    def __init__(self, fr, device="cuda:0", top_fill=0x5A, fused=True):
+    MODES = ("persistent", "fused", "staged")
+
+    def __init__(self, fr, device="cuda:0", top_fill=0x5A, mode="persistent"):
+        """mode: persistent -- one launch per frame (DGPU_IS_PERSISTENT);
+        fused -- one launch per level (DGPU_IS_FUSED); staged -- edge stage,
+        unit batch and backup runs per level."""
+        assert mode in self.MODES
         import torch
         self.torch, self.fr = torch, fr
         dev = torch.device(device)
@@ -514,11 +520,24 @@ class DeviceIntraFrame:
                       (fr.unit_start, fr.class_start, fr.rec_start, fr.run_start)]
         s = abi.IntraSchedule()
         s.n_levels = fr.n_levels
-        s.flags = abi.IS_FUSED if fused else 0
+        s.flags = {"persistent": abi.IS_FUSED | abi.IS_PERSISTENT, "fused": abi.IS_FUSED, "staged": 0}[mode]
         s.unit_start, s.class_start, s.rec_start, s.run_start = (a.ctypes.data for a in self._host)
         s.runs = self.runs.data_ptr()
         self.sched = s
         self.lib = abi.load_lib()
+        self.workspace = None
+        if mode == "persistent":
+            nb = self.lib.dav1d_gpu_intra_workspace_bytes(ctypes.byref(s), len(fr.units))
+            if nb < 0:
+                raise RuntimeError(f"dav1d_gpu_intra_workspace_bytes failed: {nb}")
+            self.workspace = torch.zeros(max(int(nb), 16), dtype=torch.uint8, device=dev)
+            s.workspace, s.workspace_bytes = self.workspace.data_ptr(), int(nb)
+
+    def flow_error(self):
+        """The persistent kernel's give-up flag (int32 [1] of the workspace)."""
+        if self.workspace is None:
+            return 0
+        return int(self.workspace[4:8].cpu().numpy().view(np.int32)[0])
 
     def reset(self):
         """Restore the inputs the wavefront consumes (unit modes / angles are

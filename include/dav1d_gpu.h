@@ -567,6 +567,12 @@ int dav1d_gpu_backup_ipred_edge_16bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav
                              superblock-bottom rows to top_edge as it writes
                              them; run_start / runs are then unused */
 
+#define DGPU_IS_PERSISTENT 2   /* one launch per frame (implies FUSED): a
+                                  persistent kernel whose waves take the
+                                  levels' tasks in order and wait on per-level
+                                  counters in `workspace` instead of launch
+                                  boundaries */
+
 typedef struct Dav1dGpuIntraSchedule {
     int32_t n_levels;
     int32_t flags;               /* DGPU_IS_*                                   */
@@ -577,12 +583,22 @@ typedef struct Dav1dGpuIntraSchedule {
     const int32_t *rec_start;    /* host, n_levels + 1: its edge records       */
     const int32_t *run_start;    /* host, n_levels + 1: its backup runs        */
     const Dav1dGpuEdgeBackup *runs;   /* device                                */
+    void    *workspace;          /* device, 16-B aligned (DGPU_IS_PERSISTENT):
+                                    counters + the task list                  */
+    int64_t  workspace_bytes;    /* >= dav1d_gpu_intra_workspace_bytes()       */
 } Dav1dGpuIntraSchedule;
+
+/* Workspace a DGPU_IS_PERSISTENT schedule needs (bytes), or -2 if the
+ * schedule is inconsistent.  After the launch, int32 [1] of the workspace is
+ * non-zero if a wave gave up waiting (never expected; the frame is then
+ * incomplete and the call is to be treated as failed). */
+int64_t dav1d_gpu_intra_workspace_bytes(const Dav1dGpuIntraSchedule *s, int n_units);
 
 /* recon: the frame's unit batch (units in level order, class_start and
  * class_warp ignored; cfl_luma normally the reconstructed luma plane);
  * edges: pic = the same planes, units = recon->units, every record.
- * Errors: those of the three stages, -2 inconsistent schedule. */
+ * Errors: those of the three stages, -2 inconsistent schedule, -5 workspace
+ * too small or misaligned. */
 int dav1d_gpu_recon_intra_frame_8bpc(const Dav1dGpuFrameBatch *recon, const Dav1dGpuIntraEdgeBatch *edges,
                                      const Dav1dGpuIntraSchedule *s, void *stream);
 int dav1d_gpu_recon_intra_frame_16bpc(const Dav1dGpuFrameBatch *recon, const Dav1dGpuIntraEdgeBatch *edges,

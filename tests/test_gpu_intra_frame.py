@@ -9,12 +9,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _check(oracle, fr, fused=True):
+def _check(oracle, fr, mode="persistent"):
     import torch
     import dav1d_mirror_amd.intra as intra
-    dev = intra.DeviceIntraFrame(fr, fused=fused)
+    dev = intra.DeviceIntraFrame(fr, mode=mode)
     dev.launch()
     torch.cuda.synchronize()
+    assert dev.flow_error() == 0
     got = dev.planes_host()
     ho = oracle.HostIntraFrame(fr)
     ho.run()
@@ -34,13 +35,14 @@ def _frame(**kw):
     return intra.make_intra_frame(intra.IntraConfig(**kw))
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("mode", ["persistent", "fused", "staged"])
 @pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023), (16, 4095)])
-def test_intra_frame(oracle, bpc, bdmax, fused):
-    """fused: one launch per level (edges gathered in the reconstruction
-    kernel, backups with the stores); else edge stage, unit batch and
+def test_intra_frame(oracle, bpc, bdmax, mode):
+    """persistent: one launch per frame, waves wait on per-level counters;
+    fused: one launch per level (edges gathered in the reconstruction
+    kernel, backups with the stores); staged: edge stage, unit batch and
     backup runs as three launches per level."""
-    _check(oracle, _frame(seed=31, bpc=bpc, bitdepth_max=bdmax), fused=fused)
+    _check(oracle, _frame(seed=31, bpc=bpc, bitdepth_max=bdmax), mode=mode)
 
 
 @pytest.mark.parametrize("kw", [dict(seed=32, cfl_frac=1.0), dict(seed=33, filter_edge=False, tx64=False),
@@ -63,7 +65,19 @@ def test_intra_frame_relaunch(oracle):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_intra_frame_1080p(oracle, fused):
+@pytest.mark.parametrize("mode", ["persistent", "fused", "staged"])
+def test_intra_frame_1080p(oracle, mode):
     """A 1080p intra frame (partial superblock row at the bottom)."""
-    _check(oracle, _frame(seed=37, width=1920, height=1080), fused=fused)
+    _check(oracle, _frame(seed=37, width=1920, height=1080), mode=mode)
+
+
+def test_intra_frame_4k_persistent(oracle):
+    """A 4K intra frame (1603 levels) through the persistent kernel, twice."""
+    import torch
+    dev, ho = _check(oracle, _frame(seed=40, width=3840, height=2160))
+    dev.reset()
+    dev.launch()
+    torch.cuda.synchronize()
+    assert dev.flow_error() == 0
+    for a, b in zip(dev.planes_host(), ho.dst):
+        assert np.array_equal(a, b)

@@ -32,6 +32,12 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         t1|t2|t4|t8|t16|t3|t6|t7|t15|t31) TUS=tile8 build $v -DDGPU_TILE_ABL=${v#t} ;;
         ttrace) TUS=tile8 build ttrace -DDGPU_TILE_TRACE=1 ;;
         twpe2|twpe4|twpe5) TUS=tile8 build $v -DDGPU_TILE_WPE=${v#twpe} ;;
+        fnofence) TUS="recon_ie8" build fnofence -DDGPU_FLOW_NOFENCE=1 ;;
+        fsleep1) TUS="recon_ie8" build fsleep1 -DDGPU_FLOW_SLEEP=1 ;;
+        ftrace) TUS="recon_ie8" build ftrace -DDGPU_FLOW_TRACE=1 ;;
+        ftrace127) TUS="recon_ie8" build ftrace127 -DDGPU_FLOW_TRACE=1 -DDGPU_FLOW_SLEEP=127 ;;
+        fsleep32) TUS="recon_ie8" build fsleep32 -DDGPU_FLOW_SLEEP=32 ;;
+        fsleep127) TUS="recon_ie8" build fsleep127 -DDGPU_FLOW_SLEEP=127 ;;
         nomc) build nomc -DDGPU_ABL_MC=1 ;;
         nostore) build nostore -DDGPU_ABL_STORE=1 ;;
         noitx) build noitx -DDGPU_ABL_ITX=1 ;;

@@ -1,0 +1,65 @@
+"""Per-task timeline of the persistent intra wavefront (DGPU_FLOW_TRACE
+build: DAV1D_GPU_LIB_VARIANT=ftrace).  Prints, per level, the wake latency
+(first task ready after the previous level's last release), the slowest
+task's compute time and the release time, averaged over levels."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import numpy as np
+    import torch
+    import __graft_entry__ as ge
+    ge.load_package()
+    import dav1d_mirror_amd.intra as intra
+    import dav1d_mirror_amd.abi as abi
+    w, h = (int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "3840x2160").split("x"))
+    fr = intra.make_intra_frame(intra.IntraConfig(width=w, height=h))
+    dev = intra.DeviceIntraFrame(fr, mode="persistent")
+    for _ in range(3):
+        dev.launch()
+    torch.cuda.synchronize()
+    # the task list as the library builds it (levels, classes largest first)
+    order = [3, 9, 10, 2, 15, 16, 7, 8, 1, 13, 14, 5, 6, 0, 4, 11, 12, 17, 18]
+    lanes = {}
+    for t, (tw, th) in enumerate(abi.TX_WH):
+        # lanes_per_unit, csrc/recon_kernel.hpp
+        lanes[t] = 64 if tw * th >= 1024 else min(max(min(tw * th // 8, max(tw, min(th, 32))), 2), 64)
+    levels = []
+    for l in range(fr.n_levels):
+        cs = fr.class_start[l]
+        for c in order:
+            n = int(cs[c + 1] - cs[c])
+            U = 64 // lanes[c]
+            levels += [l] * ((n + U - 1) // U)
+    nt = len(levels)
+    ws = dev.workspace.cpu().numpy()
+    base = (32 + 16 * fr.n_levels) * 4 + nt * 16 + fr.n_levels * 4
+    base = (base + 15) & ~15
+    assert base + nt * 32 == len(ws), (base + nt * 32, len(ws))   # same task list as the library
+    tr = ws[base:base + nt * 32].view(np.uint64).reshape(nt, 4).astype(np.int64)
+    lv = np.array(levels)
+    ready_first = np.full(fr.n_levels, np.iinfo(np.int64).max)
+    rel_last = np.zeros(fr.n_levels, np.int64)
+    comp_max = np.zeros(fr.n_levels, np.int64)
+    np.minimum.at(ready_first, lv, tr[:, 1])
+    np.maximum.at(rel_last, lv, tr[:, 3])
+    np.maximum.at(comp_max, lv, tr[:, 2] - tr[:, 1])
+    wake = ready_first[1:] - rel_last[:-1]
+    rel = tr[:, 3] - tr[:, 2]
+    span = (rel_last[-1] - tr[:, 0].min())
+    out = {"levels": int(fr.n_levels), "tasks": int(nt), "frame_us": span / 100.0,
+           "per_level_us": span / 100.0 / fr.n_levels,
+           "wake_us_mean": float(wake.mean()) / 100.0, "wake_us_p50": float(np.median(wake)) / 100.0,
+           "slowest_task_compute_us_mean": float(comp_max.mean()) / 100.0,
+           "task_compute_us_p50": float(np.median(tr[:, 2] - tr[:, 1])) / 100.0,
+           "release_us_p50": float(np.median(rel)) / 100.0,
+           "ticket_to_ready_us_p50": float(np.median(tr[:, 1] - tr[:, 0])) / 100.0}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

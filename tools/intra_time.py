@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture one frame in a HIP graph, time replays")
+    ap.add_argument("--mode", default="persistent", choices=["persistent", "fused", "staged"])
+    ap.add_argument("--tiles", default="1x1", help="tile columns x rows")
     a = ap.parse_args()
     import __graft_entry__ as ge
     ge.load_package()
@@ -27,10 +29,11 @@ def main():
     import torch
     import dav1d_mirror_amd.intra as intra
     t0 = time.time()
+    tc, tr = (int(v) for v in a.tiles.split("x"))
     fr = intra.make_intra_frame(intra.IntraConfig(width=a.width, height=a.height, bpc=a.bpc,
-                                                  bitdepth_max=a.bdmax))
+                                                  bitdepth_max=a.bdmax, tile_cols=tc, tile_rows=tr))
     gen_s = time.time() - t0
-    dev = intra.DeviceIntraFrame(fr)
+    dev = intra.DeviceIntraFrame(fr, mode=a.mode)
     s = torch.cuda.current_stream()
     for _ in range(2):
         dev.launch(s)
@@ -60,7 +63,7 @@ def main():
     px = sum(w * h for w, h in fr.plane_wh)
     out = {"frame": f"{a.width}x{a.height}", "bpc": a.bpc, "units": len(fr.units), "levels": fr.n_levels,
            "ms_per_frame": ms, "gpix_s": px / ms / 1e6, "host_enqueue_ms": host_enqueue * 1e3,
-           "gen_s": gen_s, "graph": a.graph}
+           "gen_s": gen_s, "graph": a.graph, "mode": a.mode, "tiles": a.tiles}
     oracle = ge.load_oracle()
     ho = oracle.HostIntraFrame(fr)
     t0 = time.perf_counter()
@@ -69,6 +72,7 @@ def main():
     if a.check:
         got = dev.planes_host()
         out["bit_exact"] = all(bool(np.array_equal(g, o)) for g, o in zip(got, ho.dst))
+        out["flow_error"] = dev.flow_error()
     print(json.dumps(out), flush=True)
 
 
