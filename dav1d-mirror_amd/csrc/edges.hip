@@ -53,6 +53,7 @@ __global__ __launch_bounds__(256) void k_intra_edges(EdgeArgs<BPC> a) {
     if (ri >= a.n) return;
     const Dav1dGpuIntraEdge r = a.recs[ri];
     Dav1dGpuUnit *u = a.units + r.unit;
+    if (u->pred != DGPU_PRED_INTRA && u->pred != DGPU_PRED_CFL) return;   // not an edge consumer
     const int pl = u->plane, txs = u->tx;
     const IeCtx<P> c = ie_setup<P>(r, a.pic[pl], a.ps[pl], a.top[pl], a.ts[pl], a.sb_log2[pl], tx_info(txs).w >> 2,
                                    tx_info(txs).h >> 2, a.bdmax);

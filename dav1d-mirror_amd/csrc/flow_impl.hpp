@@ -61,7 +61,14 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
     using P = typename Px<BPC>::pixel;
     __shared__ PlaneTabIE<BPC> pt;
     const int lane = threadIdx.x & 63;
-    {   // plane and top_edge tables, as in k_recon's prologue
+    {   // plane, reference and top_edge tables, as in k_recon's prologue
+        const int tr_ = min(lane, DGPU_MAX_REFS * 3 - 1);
+        const P *rp = (&a.ref[0][0])[tr_];
+        const int rs = (&a.ref_stride[0][0])[tr_];
+        if (lane < DGPU_MAX_REFS * 3) {
+            pt.ref[lane] = rp;
+            pt.ref_stride[lane] = rs;
+        }
         const int td = min(lane, 2);
         P *dp = a.dst[td];
         const int dsd = a.dst_stride[td];
@@ -216,6 +223,10 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     for (int p = 0; p < 3; p++) {
         a.dst[p] = (P *)b->dst[p].data;
         a.dst_stride[p] = (int)(b->dst[p].stride / B);
+        for (int r = 0; r < DGPU_MAX_REFS; r++) {   // inter units of a mixed frame
+            a.ref[r][p] = (const P *)b->ref[r][p].data;
+            a.ref_stride[r][p] = (int)(b->ref[r][p].stride / B);
+        }
         a.top[p] = (P *)e->top_edge[p].data;
         a.top_stride[p] = (int)(e->top_edge[p].stride / B);
         a.top_rows[p] = e->top_edge[p].h;

@@ -26,6 +26,10 @@ static int launch_ie(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *
     for (int p = 0; p < 3; p++) {
         a.dst[p] = (P *)b->dst[p].data;
         a.dst_stride[p] = (int)(b->dst[p].stride / B);
+        for (int r = 0; r < DGPU_MAX_REFS; r++) {   // inter units of a mixed frame
+            a.ref[r][p] = (const P *)b->ref[r][p].data;
+            a.ref_stride[r][p] = (int)(b->ref[r][p].stride / B);
+        }
         a.top[p] = (P *)e->top_edge[p].data;
         a.top_stride[p] = (int)(e->top_edge[p].stride / B);
         a.top_rows[p] = e->top_edge[p].h;

@@ -178,6 +178,12 @@ class IntraConfig:
     tile_cols: int = 1        # uniform tiling (in superblocks); tiles cut the
     tile_rows: int = 1        # edge dependencies (have_left / have_top, w4 / h4)
     sb_edge_backup: bool = True   # superblock-top rows read through top_edge
+    # mixed frames: this fraction of blocks is inter (put or compound avg from
+    # two edge-replicated random references, MVs within +-mv_range px); intra
+    # blocks next to them read their reconstructed pixels
+    inter_frac: float = 0.0
+    mv_range: int = 32
+    ref_pad: int = 64
 
     @property
     def pixel_dtype(self):
@@ -206,6 +212,10 @@ class IntraFrame:
     oracle_runs: np.ndarray  # whole-row backups at superblock-row ends
     top_rows: list           # top_edge shapes (rows, w) per plane
     sb_log2: tuple
+    refs: list = None        # [ref][plane] padded reference planes (mixed frames)
+
+    def ref_origin_offset(self, plane):
+        return self.cfg.ref_pad * self.refs[0][plane].shape[1] + self.cfg.ref_pad
 
     @property
     def n_levels(self):
@@ -256,6 +266,24 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     uvmode = rng.integers(0, 13, nb)
     uvang = np.where((uvmode >= 1) & (uvmode <= 8), rng.integers(-3, 4, nb), 0)
     alpha = rng.integers(1, 17, (nb, 2)) * np.where(rng.random((nb, 2)) < 0.5, -1, 1)
+    # inter blocks (own stream, so frames without them keep their draws)
+    irng = np.random.default_rng(cfg.seed ^ 0x1A7E)
+    bkind = np.where(irng.random(nb) < cfg.inter_frac,
+                     np.where(irng.random(nb) < 0.5, abi.PRED_INTER_AVG, abi.PRED_INTER), abi.PRED_INTRA)
+    bmv = irng.integers(-cfg.mv_range * 16, cfg.mv_range * 16 + 1, size=(nb, 2, 2))
+    bfilt = irng.integers(0, 9, nb)
+    refs = None
+    if cfg.inter_frac > 0:
+        refs = []
+        pad = cfg.ref_pad
+        for _ in range(2):
+            rp = []
+            for (pw_, ph_) in planes:
+                stride = (pw_ + 2 * pad + 63) // 64 * 64
+                a_ = irng.integers(0, bdmax + 1, size=(ph_, pw_)).astype(cfg.pixel_dtype)
+                rp.append(np.ascontiguousarray(np.pad(a_, ((pad, pad), (pad, stride - pw_ - pad)), mode="edge")))
+            refs.append(rp)
+    is_inter = bkind != abi.PRED_INTRA
     # decode index of the block covering each luma 4x4
     bmap = np.full((H // 4, W // 4), -1, np.int64)
     for b in range(nb):
@@ -272,16 +300,18 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
         # mode contexts are reset at tile starts (dav1d_reset_context)
         above = bmap[(y - 1) // 4, x // 4] if y > y0 else -1
         left = bmap[y // 4, (x - 1) // 4] if x > x0 else -1
-        ysm = (above >= 0 and smooth(ymode[above])) or (left >= 0 and smooth(ymode[left]))
-        uvsm = ((above >= 0 and not is_cfl[above] and smooth(uvmode[above])) or
-                (left >= 0 and not is_cfl[left] and smooth(uvmode[left])))
+        # (inter neighbours carry no smooth mode)
+        ysm = ((above >= 0 and not is_inter[above] and smooth(ymode[above])) or
+               (left >= 0 and not is_inter[left] and smooth(ymode[left])))
+        uvsm = ((above >= 0 and not is_inter[above] and not is_cfl[above] and smooth(uvmode[above])) or
+                (left >= 0 and not is_inter[left] and not is_cfl[left] and smooth(uvmode[left])))
         cands = _tx_candidates(s, cfg.tx64)
         luma_tx = cands[int(rng.integers(0, len(cands)))]
         for pl in range(3):
             ss = 0 if pl == 0 else 1
             px_, py_, ps_ = x >> ss, y >> ss, s >> ss
             tw, th = luma_tx if pl == 0 else (ps_, ps_)
-            cfl = pl > 0 and bool(is_cfl[b])
+            cfl = pl > 0 and bool(is_cfl[b]) and not is_inter[b]
             bw4 = ps_ // 4
             for oy in range(0, ps_, th):
                 for ox in range(0, ps_, tw):
@@ -329,16 +359,34 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     units["dst_off"] = uy * pw[plane_u] + ux
     units["tx"] = tx
     units["plane"] = plane_u
-    units["pred"] = np.where(cflu, abi.PRED_CFL, abi.PRED_INTRA)
-    units["bw4"] = units["bh4"] = 0
+    interu = is_inter[blk]
+    units["pred"] = np.where(interu, bkind[blk], np.where(cflu, abi.PRED_CFL, abi.PRED_INTRA))
+    bsz = ls[blk] >> np.where(plane_u > 0, 1, 0)
+    units["bw4"] = units["bh4"] = np.where(interu, bsz // 4, 0)
     txtp, nzw, nzh, coef_off, coefs = make_residuals(rng, tx, tw, th, bdmax, cfg.coef_dtype)
     units["txtp"], units["nzw"], units["nzh"], units["coef_off"] = txtp, nzw, nzh, coef_off
-    edge_len = 2 * th + 2 * tw + 1
+    edge_len = np.where(interu, 0, 2 * th + 2 * tw + 1)
     edge_start = np.concatenate([[0], np.cumsum(edge_len)[:-1]])
-    units["edge_off"] = edge_start + 2 * th
-    iu = ~cflu
+    units["edge_off"] = np.where(interu, 0, edge_start + 2 * th)
+    iu = ~cflu & ~interu
     units["max_w"] = np.where(iu, pw[plane_u] - ux, 0)
     units["max_h"] = np.where(iu, ph[plane_u] - uy, 0)
+    if refs is not None:   # inter parameters (the inter view of the union)
+        ref_stride = np.array([refs[0][p_].shape[1] for p_ in range(3)])
+        iv = units[interu]
+        ib_, ip_ = blk[interu], plane_u[interu]
+        for k in range(2):
+            mvx, mvy = bmv[ib_, k, 0], bmv[ib_, k, 1]
+            mvx = np.where(ip_ > 0, mvx >> 1, mvx)
+            mvy = np.where(ip_ > 0, mvy >> 1, mvy)
+            sx, sy = ux[interu] + (mvx >> 4), uy[interu] + (mvy >> 4)
+            iv[f"src_off{k}"] = sy * ref_stride[ip_] + sx
+            iv[f"mx{k}"] = mvx & 15
+            iv[f"my{k}"] = mvy & 15
+            iv[f"ref{k}"] = k
+        iv["filter2d"] = bfilt[ib_]
+        iv["weight"] = 0
+        units[interu] = iv
     cu = units[cflu]
     cu["cfl_alpha"] = alpha[blk[cflu], plane_u[cflu] - 1]
     cu["cfl_pad_wh"] = 0
@@ -356,7 +404,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
         f = int(flags[i])
         hl, ht = bool(f & abi.IE_HAVE_LEFT), bool(f & abi.IE_HAVE_TOP)
         m, _ = remap_mode(modes[i], angles[i], hl, ht)
-        nd = _NEEDS[m]
+        nd = 0 if interu[i] else _NEEDS[m]   # inter units read only the references
         L = lv[p]
         deps = [-1]
         if nd & _NEED_L:
@@ -440,7 +488,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     recs["mode"], recs["angle"], recs["flags"] = modes, angles, flags
     recs = recs[perm]
     rec_start = unit_start.copy()
-    unit_rec = np.arange(n, dtype=np.int32)
+    unit_rec = np.where(np.isin(units["pred"], (abi.PRED_INTRA, abi.PRED_CFL)), np.arange(n), -1).astype(np.int32)
     rp = np.argsort(run_lv, kind="stable")
     runs = runs[rp]
     run_start = np.searchsorted(run_lv[rp], np.arange(n_levels + 1)).astype(np.int32)
@@ -450,15 +498,22 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     top_rows = [(max(1, h >> s_), w) for (w, h), s_ in zip(planes, sbl)]
     edges = np.zeros(int(edge_len.sum()), cfg.pixel_dtype)
     return IntraFrame(cfg, planes, units, coefs, edges, recs, runs, unit_start, class_start, rec_start,
-                      run_start, steps, unit_rec, np.array(oracle_runs, abi.EDGE_BACKUP_DTYPE), top_rows, sbl)
+                      run_start, steps, unit_rec, np.array(oracle_runs, abi.EDGE_BACKUP_DTYPE), top_rows, sbl,
+                      refs)
 
 
-def frame_batch(fr, dst_ptrs, units, coefs, edges):
-    """abi.FrameBatch of an IntraFrame (cfl_luma = the reconstructed luma)."""
+def frame_batch(fr, dst_ptrs, units, coefs, edges, ref_ptrs=None):
+    """abi.FrameBatch of an IntraFrame (cfl_luma = the reconstructed luma;
+    ref_ptrs[r][p]: addresses of the padded reference planes, mixed frames)."""
     bpp = 1 if fr.cfg.bpc == 8 else 2
     b = abi.FrameBatch()
     for p, (w, h) in enumerate(fr.plane_wh):
         b.dst[p].data, b.dst[p].stride, b.dst[p].w, b.dst[p].h = dst_ptrs[p], w * bpp, w, h
+        for r in range(len(ref_ptrs or [])):
+            a = fr.refs[r][p]
+            b.ref[r][p].data = ref_ptrs[r][p] + fr.ref_origin_offset(p) * bpp
+            b.ref[r][p].stride = a.shape[1] * bpp
+            b.ref[r][p].w, b.ref[r][p].h = w, h
     b.units, b.n_units = units, len(fr.units)
     b.class_start[abi.N_TX] = len(fr.units)   # unused: the driver passes per-level ranges
     b.coef, b.edges = coefs, edges
@@ -512,8 +567,10 @@ class DeviceIntraFrame:
         self.runs = up(fr.runs.view(np.uint8)) if len(fr.runs) else torch.zeros(16, dtype=torch.uint8, device=dev)
         self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fr.plane_wh]
         self.top = [torch.full(s, top_fill, dtype=pdt, device=dev) for s in fr.top_rows]
+        self.refs = [[up(a.view(np.int16) if hbd else a) for a in rp] for rp in (fr.refs or [])]
         d = [t.data_ptr() for t in self.dst]
-        self.rb = frame_batch(fr, d, self.units.data_ptr(), self.coefs.data_ptr(), self.edges.data_ptr())
+        self.rb = frame_batch(fr, d, self.units.data_ptr(), self.coefs.data_ptr(), self.edges.data_ptr(),
+                              [[t.data_ptr() for t in rp] for rp in self.refs])
         self.eb = edge_batch(fr, d, [t.data_ptr() for t in self.top], self.units.data_ptr(),
                              self.edges.data_ptr(), self.recs.data_ptr())
         self._host = [np.ascontiguousarray(a, dtype=np.int32) for a in

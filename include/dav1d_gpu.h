@@ -528,7 +528,9 @@ typedef struct Dav1dGpuIntraEdgeBatch {
     int32_t  bitdepth_max;
 } Dav1dGpuIntraEdgeBatch;
 
-/* A CFL unit's record carries mode DC_PRED, angle 0, flags without the
+/* Records whose unit is neither INTRA nor CFL are skipped (a level's record
+ * range may run parallel to all its units).
+ * A CFL unit's record carries mode DC_PRED, angle 0, flags without the
  * filter / smooth bits (recon_tmpl.c:1393-1410); only its DC source
  * (p.cfl.mode) is written, alpha and padding stay.  Errors: -1 NULL batch or
  * buffers / negative count, -3 launch failure. */

@@ -1796,6 +1796,7 @@ int SFX(oracle_prepare_intra_edges)(const Dav1dGpuIntraEdgeBatch *b)
     for (int i = 0; i < b->n_recs; i++) {
         const Dav1dGpuIntraEdge *r = &b->recs[i];
         Dav1dGpuUnit *u = &b->units[r->unit];
+        if (u->pred != DGPU_PRED_INTRA && u->pred != DGPU_PRED_CFL) continue;   /* not an edge consumer */
         const int pl = u->plane;
         const ptrdiff_t ps = PX(b->pic[pl].stride);
         const pixel *dst = (const pixel *)b->pic[pl].data + (ptrdiff_t)r->y4 * 4 * ps + r->x4 * 4;

@@ -297,7 +297,8 @@ class HostIntraFrame:
         self.unit_rec = np.ascontiguousarray(fr.unit_rec, dtype=np.int32)
         self.oruns = np.ascontiguousarray(fr.oracle_runs) if len(fr.oracle_runs) else np.zeros(1, abi.EDGE_BACKUP_DTYPE)
         d = [a.ctypes.data for a in self.dst]
-        self.rb = intra.frame_batch(fr, d, self.units.ctypes.data, self.coefs.ctypes.data, self.edges.ctypes.data)
+        self.rb = intra.frame_batch(fr, d, self.units.ctypes.data, self.coefs.ctypes.data, self.edges.ctypes.data,
+                                    [[a.ctypes.data for a in rp] for rp in (fr.refs or [])])
         self.eb = intra.edge_batch(fr, d, [a.ctypes.data for a in self.top], self.units.ctypes.data,
                                    self.edges.ctypes.data, self.recs.ctypes.data)
 

@@ -17,7 +17,8 @@ def _frame(**kw):
                                 dict(seed=4, bpc=16, bitdepth_max=1023), dict(seed=5, bpc=16, bitdepth_max=4095),
                                 dict(seed=6, width=480, height=264),
                                 dict(seed=8, width=640, height=384, tile_cols=3, tile_rows=2),
-                                dict(seed=9, tile_cols=2, sb_edge_backup=False)])
+                                dict(seed=9, tile_cols=2, sb_edge_backup=False),
+                                dict(seed=10, inter_frac=0.5), dict(seed=11, inter_frac=0.8, bpc=16, bitdepth_max=1023)])
 def test_level_order_equals_decode_order(pkg, oracle, kw):
     fr = _frame(**kw)
     a = oracle.HostIntraFrame(fr)

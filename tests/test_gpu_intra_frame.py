@@ -53,6 +53,15 @@ def test_intra_frame_variants(oracle, kw):
     _check(oracle, _frame(**kw))
 
 
+@pytest.mark.parametrize("mode", ["persistent", "fused", "staged"])
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+def test_mixed_frame(oracle, mode, bpc, bdmax):
+    """Inter blocks (put / compound avg from padded references) among the
+    intra ones: inter units sit at level 0, intra neighbours read their
+    reconstructed pixels; the edge stage skips records of non-intra units."""
+    _check(oracle, _frame(seed=41, inter_frac=0.5, bpc=bpc, bitdepth_max=bdmax, tile_cols=2), mode=mode)
+
+
 def test_intra_frame_relaunch(oracle):
     """reset() + launch again: the same pixels (the wavefront is repeatable)."""
     import torch
