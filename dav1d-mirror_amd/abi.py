@@ -140,6 +140,17 @@ class IntraSchedule(ctypes.Structure):
                 ("workspace_bytes", ctypes.c_int64)]
 
 
+class RecBlock(ctypes.Structure):
+    """Dav1dGpuRecBlock: one block of one plane, as recon_b_* would run it."""
+    _fields_ = [("plane", ctypes.c_int32), ("x", ctypes.c_int32), ("y", ctypes.c_int32),
+                ("w", ctypes.c_int32), ("h", ctypes.c_int32), ("tx", ctypes.c_int32), ("kind", ctypes.c_int32),
+                ("tile_x0", ctypes.c_int32), ("tile_y0", ctypes.c_int32), ("tile_x1", ctypes.c_int32),
+                ("tile_y1", ctypes.c_int32), ("mvx", ctypes.c_int32 * 2), ("mvy", ctypes.c_int32 * 2),
+                ("ref", ctypes.c_uint8 * 2), ("filter2d", ctypes.c_uint8), ("weight", ctypes.c_uint8),
+                ("mode", ctypes.c_uint8), ("angle", ctypes.c_int8), ("cfl_alpha", ctypes.c_int8),
+                ("flags", ctypes.c_uint8)]
+
+
 _LIB = None
 
 
@@ -181,6 +192,20 @@ def load_lib():
             f.argtypes = [ctypes.POINTER(FrameBatch), ctypes.POINTER(IntraEdgeBatch),
                           ctypes.POINTER(IntraSchedule), ctypes.c_void_p]
             f.restype = ctypes.c_int
+        L.dav1d_gpu_recorder_new.argtypes = [ctypes.c_int] * 5
+        L.dav1d_gpu_recorder_new.restype = ctypes.c_void_p
+        L.dav1d_gpu_recorder_free.argtypes = [ctypes.c_void_p]
+        L.dav1d_gpu_recorder_free.restype = None
+        L.dav1d_gpu_rec_block.argtypes = [ctypes.c_void_p, ctypes.POINTER(RecBlock)]
+        L.dav1d_gpu_rec_block.restype = ctypes.c_int
+        L.dav1d_gpu_rec_residual.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p]
+        L.dav1d_gpu_rec_residual.restype = ctypes.c_int
+        L.dav1d_gpu_recorder_flush.argtypes = [ctypes.c_void_p, ctypes.POINTER(Plane * 3),
+                                               ctypes.POINTER((Plane * 3) * MAX_REFS), ctypes.c_void_p]
+        L.dav1d_gpu_recorder_flush.restype = ctypes.c_int
+        L.dav1d_gpu_recorder_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                               ctypes.POINTER(ctypes.c_int32)]
+        L.dav1d_gpu_recorder_stats.restype = ctypes.c_int
         L.dav1d_gpu_intra_workspace_bytes.argtypes = [ctypes.POINTER(IntraSchedule), ctypes.c_int]
         L.dav1d_gpu_intra_workspace_bytes.restype = ctypes.c_int64
         L.dav1d_gpu_recon_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -204,4 +229,6 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_backup_ipred_edge_8bpc", "dav1d_gpu_backup_ipred_edge_16bpc",
     "dav1d_gpu_recon_intra_frame_8bpc", "dav1d_gpu_recon_intra_frame_16bpc",
     "dav1d_gpu_intra_workspace_bytes",
+    "dav1d_gpu_recorder_new", "dav1d_gpu_recorder_free", "dav1d_gpu_rec_block", "dav1d_gpu_rec_residual",
+    "dav1d_gpu_recorder_flush", "dav1d_gpu_recorder_stats",
 ]

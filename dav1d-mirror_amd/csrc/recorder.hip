@@ -1,0 +1,463 @@
+// recorder.hip -- the batch recorder at the reconstruction seam (SURVEY 8(f)
+// row 2; include/dav1d_gpu.h, Dav1dGpuRecorder).
+//
+// A decoder's recon_b_inter / recon_b_intra (src/recon_tmpl.c:1598, :1195)
+// hand over, per block and plane, what they would have passed to the DSP
+// (one Dav1dGpuRecBlock) and, per coded transform block, what they would
+// have passed to inv_txfm_add (dav1d_gpu_rec_residual).  A flush turns the
+// record into the device's work:
+//   1. transform units in decode order: every transform cell of every block
+//      (recon_b_* iterate the block's transform grid, :1258-1262), carrying
+//      the block's prediction and the cell's residual if one was recorded;
+//   2. per intra / CfL unit the dav1d_prepare_intra_edges record exactly as
+//      recon_b_intra derives it: have_left / have_top against the tile start,
+//      the tile end as (w, h), and the per-transform edge flags of
+//      :1252-1266 from the block's intra_edge_flags;
+//   3. dependency levels at 4x4 granularity: inter units read only their
+//      references (level 0); an intra unit sits one level above every unit
+//      whose pixels the edges of its remapped mode read (CfL: also the
+//      co-located luma);
+//   4. units sorted by (level, size class, kind, mode, type), records in the
+//      same order, coefficients compacted to the stored region, and one
+//      persistent wavefront launch (dav1d_gpu_recon_intra_frame_*).
+// Host code only; the device work runs on the caller's stream.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <numeric>
+#include <vector>
+
+#include "dav1d_gpu.h"
+
+namespace {
+
+struct TxDim { int w, h; };
+constexpr TxDim kTx[DGPU_N_RECT_TX_SIZES] = {
+    {4, 4}, {8, 8}, {16, 16}, {32, 32}, {64, 64}, {4, 8}, {8, 4}, {8, 16}, {16, 8}, {16, 32},
+    {32, 16}, {32, 64}, {64, 32}, {4, 16}, {16, 4}, {8, 32}, {32, 8}, {16, 64}, {64, 16}};
+
+// av1_intra_prediction_edges needs (src/ipred_prepare_tmpl.c:50-75):
+// bit0 left, 1 top, 2 top-left, 3 top-right, 4 bottom-left
+constexpr uint8_t kNeeds[14] = {3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7};
+
+// the mode remap of dav1d_prepare_intra_edges (:83-104)
+int remap_mode(int mode, int angle, bool hl, bool ht) {
+    static const int dir[8] = {90, 180, 45, 135, 113, 157, 203, 67};
+    if (mode >= 1 && mode <= 8) {
+        const int a = dir[mode - 1] + 3 * angle;
+        if (a <= 90) return a < 90 && ht ? DGPU_Z1_PRED : DGPU_VERT_PRED;
+        if (a < 180) return DGPU_Z2_PRED;
+        return a > 180 && hl ? DGPU_Z3_PRED : DGPU_HOR_PRED;
+    }
+    if (mode == 0) return hl ? (ht ? DGPU_DC_PRED : DGPU_LEFT_DC_PRED) : (ht ? DGPU_TOP_DC_PRED : DGPU_DC_128_PRED);
+    if (mode == 12) return hl ? (ht ? DGPU_PAETH_PRED : DGPU_HOR_PRED) : (ht ? DGPU_VERT_PRED : DGPU_DC_128_PRED);
+    return mode;
+}
+
+struct Residual {
+    int plane, x, y, tx, txtp, nzw, nzh;
+    size_t coef;   // offset into the recorder's compact pool
+};
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int grow(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, n) != hipSuccess) return -1;
+        cap = n;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Unit {   // a transform cell before sorting
+    Dav1dGpuUnit u;
+    Dav1dGpuIntraEdge rec;
+    int level;
+    int sortmode;
+};
+
+}  // namespace
+
+struct Dav1dGpuRecorder {
+    int bpc, bdmax, width, height, device;
+    std::vector<Dav1dGpuRecBlock> blocks;
+    std::vector<Residual> residuals;
+    std::vector<int32_t> coef32;   // compact regions (int32 for both ABIs; narrowed at flush)
+    // flush products (kept alive while the device may still read them)
+    std::vector<Dav1dGpuUnit> units;
+    std::vector<Dav1dGpuIntraEdge> recs;
+    std::vector<int32_t> unit_start, class_start, rec_start, run_start;
+    std::vector<uint8_t> coef_pool;
+    DevBuf d_units, d_recs, d_coef, d_edges, d_work;
+    hipEvent_t done = nullptr;
+    int32_t last_units = 0, last_levels = 0;
+};
+
+extern "C" Dav1dGpuRecorder *dav1d_gpu_recorder_new(int bpc, int bitdepth_max, int width, int height, int device) {
+    if ((bpc != 8 && bpc != 16) || width <= 0 || height <= 0 || (width & 7) || (height & 7)) return nullptr;
+    Dav1dGpuRecorder *r = new Dav1dGpuRecorder();
+    r->bpc = bpc;
+    r->bdmax = bpc == 8 ? 255 : bitdepth_max;
+    r->width = width;
+    r->height = height;
+    r->device = device;
+    return r;
+}
+
+extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
+    if (!r) return;
+    if (hipSetDevice(r->device) == hipSuccess) {
+        if (r->done) {
+            (void)hipEventSynchronize(r->done);
+            (void)hipEventDestroy(r->done);
+        }
+        r->d_units.release();
+        r->d_recs.release();
+        r->d_coef.release();
+        r->d_edges.release();
+        r->d_work.release();
+    }
+    delete r;
+}
+
+static bool plane_dims(const Dav1dGpuRecorder *r, int plane, int &w, int &h) {
+    if (plane < 0 || plane > 2) return false;
+    w = plane ? r->width >> 1 : r->width;
+    h = plane ? r->height >> 1 : r->height;
+    return true;
+}
+
+extern "C" int dav1d_gpu_rec_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b) {
+    int pw, ph;
+    if (!r || !b || !plane_dims(r, b->plane, pw, ph)) return -1;
+    if (b->tx < 0 || b->tx >= DGPU_N_RECT_TX_SIZES) return -1;
+    const TxDim t = kTx[b->tx];
+    if (b->x < 0 || b->y < 0 || b->w <= 0 || b->h <= 0 || b->x + b->w > pw || b->y + b->h > ph) return -1;
+    if ((b->x & 3) || (b->y & 3) || b->w % t.w || b->h % t.h) return -1;
+    const bool inter = b->kind == DGPU_PRED_INTER || b->kind == DGPU_PRED_INTER_AVG || b->kind == DGPU_PRED_INTER_WAVG;
+    if (!inter && b->kind != DGPU_PRED_INTRA && b->kind != DGPU_PRED_CFL) return -1;
+    if (b->kind == DGPU_PRED_CFL && (b->plane == 0 || b->w != t.w || b->h != t.h || t.w != t.h || t.w > 32))
+        return -1;   // CfL: one unit per chroma block (cfl_ac + cfl_pred, :1372-1414)
+    if (!inter && b->mode > 13) return -1;
+    if (inter && (b->ref[0] >= DGPU_MAX_REFS || b->ref[1] >= DGPU_MAX_REFS || b->filter2d > 9)) return -1;
+    if (b->tile_x0 < 0 || b->tile_y0 < 0 || b->tile_x1 > pw || b->tile_y1 > ph || b->x < b->tile_x0 ||
+        b->y < b->tile_y0 || b->x + b->w > b->tile_x1 || b->y + b->h > b->tile_y1)
+        return -1;
+    r->blocks.push_back(*b);
+    return 0;
+}
+
+extern "C" int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int y, int tx, int txtp, int eob,
+                                      const void *coef) {
+    int pw, ph;
+    if (!r || !coef || !plane_dims(r, plane, pw, ph) || tx < 0 || tx >= DGPU_N_RECT_TX_SIZES) return -1;
+    if (txtp < 0 || txtp >= DGPU_N_TX_TYPES_PLUS_LL || eob < 0) return -1;
+    const TxDim t = kTx[tx];
+    if (x < 0 || y < 0 || x + t.w > pw || y + t.h > ph || (x & 3) || (y & 3)) return -1;
+    const int sw = std::min(t.w, 32), sh = std::min(t.h, 32);
+    Residual res{plane, x, y, tx, txtp, 0, 0, r->coef32.size()};
+    auto at = [&](int cx, int cy) -> int32_t {   // the reference's layout: coef[cy + cx * sh]
+        return r->bpc == 8 ? ((const int16_t *)coef)[cy + cx * sh] : ((const int32_t *)coef)[cy + cx * sh];
+    };
+    if (eob == 0 && txtp == DGPU_DCT_DCT) {   // the DC-only call (src/itx_tmpl.c:53)
+        r->coef32.push_back(at(0, 0));
+    } else {   // the stored region: the bounding box of the non-zero coefficients
+        int nzw = 1, nzh = 1;
+        for (int cx = 0; cx < sw; cx++)
+            for (int cy = 0; cy < sh; cy++)
+                if (at(cx, cy)) {
+                    nzw = std::max(nzw, cx + 1);
+                    nzh = std::max(nzh, cy + 1);
+                }
+        res.nzw = nzw;
+        res.nzh = nzh;
+        for (int cx = 0; cx < nzw; cx++)
+            for (int cy = 0; cy < nzh; cy++) r->coef32.push_back(at(cx, cy));
+    }
+    r->residuals.push_back(res);
+    return 0;
+}
+
+extern "C" int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_units, int32_t *n_levels) {
+    if (!r) return -1;
+    if (n_units) *n_units = r->last_units;
+    if (n_levels) *n_levels = r->last_levels;
+    return 0;
+}
+
+extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane dst[3],
+                                        const Dav1dGpuPlane ref[DGPU_MAX_REFS][3], void *stream) {
+    constexpr int NC = DGPU_N_RECT_TX_SIZES;
+    if (!r || !dst) return -1;
+    if (hipSetDevice(r->device) != hipSuccess) return -3;
+    if (r->done && hipEventSynchronize(r->done) != hipSuccess) return -3;   // buffers free for reuse
+    const int bpp = r->bpc / 8;
+    int pw[3], ph[3];
+    for (int p = 0; p < 3; p++) plane_dims(r, p, pw[p], ph[p]);
+
+    // residual lookup: per plane, the top-left 4x4 cell of each residual
+    std::vector<int32_t> res_at[3];
+    for (int p = 0; p < 3; p++) res_at[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
+    for (size_t i = 0; i < r->residuals.size(); i++) {
+        const Residual &q = r->residuals[i];
+        res_at[q.plane][(size_t)(q.y / 4) * (pw[q.plane] / 4) + q.x / 4] = (int32_t)i;
+    }
+
+    // 1-3. transform units in decode order, their edge records and levels
+    std::vector<Unit> cells;
+    std::vector<int32_t> lv[3];
+    for (int p = 0; p < 3; p++) lv[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
+    size_t n_res_used = 0;
+    for (const Dav1dGpuRecBlock &b : r->blocks) {
+        const TxDim t = kTx[b.tx];
+        const int p = b.plane, w4p = pw[p] / 4;
+        const bool inter = b.kind == DGPU_PRED_INTER || b.kind == DGPU_PRED_INTER_AVG || b.kind == DGPU_PRED_INTER_WAVG;
+        const bool cfl = b.kind == DGPU_PRED_CFL;
+        const int bw4 = b.w / 4, bh4 = b.h / 4, tw4 = t.w / 4, th4 = t.h / 4;
+        for (int oy = 0; oy < b.h; oy += t.h)
+            for (int ox = 0; ox < b.w; ox += t.w) {
+                Unit c;
+                memset(&c, 0, sizeof(c));
+                const int ux = b.x + ox, uy = b.y + oy, x4 = ux / 4, y4 = uy / 4;
+                Dav1dGpuUnit &u = c.u;
+                u.dst_off = uy * (int)(dst[p].stride / bpp) + ux;
+                u.tx = (uint8_t)b.tx;
+                u.plane = (uint8_t)p;
+                u.pred = (uint8_t)b.kind;
+                u.txtp = DGPU_NO_RESIDUAL;
+                const int ri = res_at[p][(size_t)y4 * w4p + x4];
+                if (ri >= 0 && r->residuals[ri].tx == b.tx) {
+                    const Residual &q = r->residuals[ri];
+                    u.txtp = (uint8_t)q.txtp;
+                    u.nzw = (uint8_t)q.nzw;
+                    u.nzh = (uint8_t)q.nzh;
+                    u.coef_off = (int32_t)q.coef;   // pool offset fixed below
+                    n_res_used++;
+                } else if (ri >= 0) {
+                    return -1;   // a residual whose size differs from its block's transforms
+                }
+                Dav1dGpuIntraEdge &e = c.rec;
+                e.unit = -1;
+                e.x4 = (int16_t)x4;
+                e.y4 = (int16_t)y4;
+                e.w4 = (int16_t)(b.tile_x1 / 4);
+                e.h4 = (int16_t)(b.tile_y1 / 4);
+                int nd = 0;
+                bool hl = ux > b.tile_x0, ht = uy > b.tile_y0;
+                if (inter) {
+                    u.bw4 = (uint8_t)bw4;
+                    u.bh4 = (uint8_t)bh4;
+                    for (int k = 0; k < 2; k++) {
+                        const int rr = b.ref[k];
+                        const int rs = ref ? (int)(ref[rr][p].stride / bpp) : 0;
+                        u.p.inter.src_off[k] = (uy + (b.mvy[k] >> 4)) * rs + ux + (b.mvx[k] >> 4);
+                        u.p.inter.mx[k] = (uint8_t)(b.mvx[k] & 15);
+                        u.p.inter.my[k] = (uint8_t)(b.mvy[k] & 15);
+                        u.p.inter.ref[k] = (uint8_t)rr;
+                    }
+                    u.p.inter.filter2d = b.filter2d;
+                    u.p.inter.weight = b.kind == DGPU_PRED_INTER_WAVG ? b.weight : 0;
+                    c.sortmode = b.filter2d;
+                } else {
+                    int fl = (hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0);
+                    if (!cfl) {   // recon_tmpl.c:1252-1266 (blocks up to 64 wide: one 64x64 step)
+                        const int x = ox / 4, y = oy / 4;
+                        const bool sb_tr = b.flags & DGPU_IE_TOP_HAS_RIGHT, sb_bl = b.flags & DGPU_IE_LEFT_HAS_BOTTOM;
+                        if (!((y > 0 || !sb_tr) && x + tw4 >= bw4)) fl |= DGPU_IE_TOP_HAS_RIGHT;
+                        if (!(x > 0 || (!sb_bl && y + th4 >= bh4))) fl |= DGPU_IE_LEFT_HAS_BOTTOM;
+                        fl |= b.flags & (DGPU_IE_FILTER_EDGE | DGPU_IE_SMOOTH);
+                        e.mode = b.mode;
+                        e.angle = b.angle;
+                        u.p.intra.max_w = (uint16_t)(pw[p] - ux);
+                        u.p.intra.max_h = (uint16_t)(ph[p] - uy);
+                    } else {
+                        e.mode = DGPU_DC_PRED;   // cfl_pred's DC source (:1395-1410)
+                        e.angle = 0;
+                        u.p.cfl.alpha = b.cfl_alpha;
+                        u.p.cfl.luma_off = (2 * uy) * (int)(dst[0].stride / bpp) + 2 * ux;
+                    }
+                    e.flags = (uint8_t)fl;
+                    const int m = remap_mode(e.mode, e.angle, hl, ht);
+                    nd = kNeeds[m];
+                    c.sortmode = 16 + m;
+                }
+                // level: one above every pixel the edges (or CfL luma) read
+                const std::vector<int32_t> &L = lv[p];
+                const int W4 = e.w4, H4 = e.h4;
+                auto cell = [&](int cx, int cy) { return L[(size_t)cy * w4p + cx]; };
+                int d = -1;
+                if (nd & 1) {
+                    if (hl) {
+                        for (int k = y4; k < std::min(y4 + th4, H4); k++) d = std::max(d, cell(x4 - 1, k));
+                        if ((nd & 16) && y4 + th4 < H4 && (e.flags & DGPU_IE_LEFT_HAS_BOTTOM))
+                            for (int k = y4 + th4; k < std::min(y4 + 2 * th4, H4); k++) d = std::max(d, cell(x4 - 1, k));
+                    } else if (ht) {
+                        d = std::max(d, cell(x4, y4 - 1));
+                    }
+                }
+                if (nd & 2) {
+                    if (ht) {
+                        for (int k = x4; k < std::min(x4 + tw4, W4); k++) d = std::max(d, cell(k, y4 - 1));
+                        if ((nd & 8) && x4 + tw4 < W4 && (e.flags & DGPU_IE_TOP_HAS_RIGHT))
+                            for (int k = x4 + tw4; k < std::min(x4 + 2 * tw4, W4); k++) d = std::max(d, cell(k, y4 - 1));
+                    } else if (hl) {
+                        d = std::max(d, cell(x4 - 1, y4));
+                    }
+                }
+                if (nd & 4) {
+                    if (hl && ht) d = std::max(d, cell(x4 - 1, y4 - 1));
+                    else if (hl) d = std::max(d, cell(x4 - 1, y4));
+                    else if (ht) d = std::max(d, cell(x4, y4 - 1));
+                }
+                if (cfl) {
+                    const int lw4 = pw[0] / 4;
+                    for (int cy = 2 * y4; cy < 2 * (y4 + th4); cy++)
+                        for (int cx = 2 * x4; cx < 2 * (x4 + tw4); cx++) {
+                            const int v = lv[0][(size_t)cy * lw4 + cx];
+                            if (v < 0) return -1;   // CfL before its luma
+                            d = std::max(d, v);
+                        }
+                }
+                c.level = d + 1;
+                std::vector<int32_t> &Lw = lv[p];
+                for (int cy = y4; cy < y4 + th4; cy++)
+                    for (int cx = x4; cx < x4 + tw4; cx++) Lw[(size_t)cy * w4p + cx] = c.level;
+                cells.push_back(c);
+            }
+    }
+    if (n_res_used != r->residuals.size()) return -1;   // a residual outside every block
+    const int n = (int)cells.size();
+
+    // 4. level order, size classes inside a level, then kind / mode / type
+    std::vector<int> perm(n);
+    std::iota(perm.begin(), perm.end(), 0);
+    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) {
+        const Unit &x = cells[a], &y = cells[b];
+        if (x.level != y.level) return x.level < y.level;
+        if (x.u.tx != y.u.tx) return x.u.tx < y.u.tx;
+        if (x.u.pred != y.u.pred) return x.u.pred < y.u.pred;
+        if (x.sortmode != y.sortmode) return x.sortmode < y.sortmode;
+        return x.u.txtp < y.u.txtp;
+    });
+    const int n_levels = n ? cells[perm[n - 1]].level + 1 : 0;
+    r->units.resize(n);
+    r->recs.resize(n);
+    r->unit_start.assign(n_levels + 1, 0);
+    r->class_start.assign((size_t)n_levels * (NC + 1), 0);
+    const size_t cb = r->bpc == 8 ? 2 : 4;
+    r->coef_pool.clear();
+    size_t edge_px = 0;
+    for (int i = 0; i < n; i++) {
+        const Unit &c = cells[perm[i]];
+        Dav1dGpuUnit u = c.u;
+        if (u.txtp != DGPU_NO_RESIDUAL) {   // compact region into the pool, in unit order
+            const size_t src = (size_t)u.coef_off, cnt = u.nzw ? (size_t)u.nzw * u.nzh : 1;
+            u.coef_off = (int32_t)(r->coef_pool.size() / cb);
+            for (size_t k = 0; k < cnt; k++) {
+                const int32_t v = r->coef32[src + k];
+                if (cb == 2) {
+                    const int16_t h = (int16_t)v;
+                    r->coef_pool.insert(r->coef_pool.end(), (const uint8_t *)&h, (const uint8_t *)&h + 2);
+                } else {
+                    r->coef_pool.insert(r->coef_pool.end(), (const uint8_t *)&v, (const uint8_t *)&v + 4);
+                }
+            }
+        }
+        if (u.pred == DGPU_PRED_INTRA || u.pred == DGPU_PRED_CFL) {   // an edge slot (the staged path's pool)
+            const TxDim t = kTx[u.tx];
+            u.p.intra.edge_off = (int32_t)(edge_px + 2 * t.h);
+            edge_px += 2 * t.h + 2 * t.w + 1;
+        }
+        r->units[i] = u;
+        Dav1dGpuIntraEdge e = c.rec;
+        e.unit = i;
+        r->recs[i] = e;
+        r->unit_start[c.level + 1] = i + 1;
+        r->class_start[(size_t)c.level * (NC + 1) + u.tx + 1]++;
+    }
+    for (int l = 0; l < n_levels; l++) {
+        if (r->unit_start[l + 1] < r->unit_start[l]) r->unit_start[l + 1] = r->unit_start[l];   // (levels are dense)
+        int32_t *cs = &r->class_start[(size_t)l * (NC + 1)];
+        for (int k = 0; k < NC; k++) cs[k + 1] += cs[k];
+    }
+    r->rec_start = r->unit_start;
+    r->run_start.assign(n_levels + 1, 0);
+    r->last_units = n;
+    r->last_levels = n_levels;
+    if (!n) {
+        r->blocks.clear();
+        r->residuals.clear();
+        r->coef32.clear();
+        return 0;
+    }
+
+    // upload and launch
+    hipStream_t st = (hipStream_t)stream;
+    Dav1dGpuIntraSchedule s;
+    memset(&s, 0, sizeof(s));
+    s.n_levels = n_levels;
+    s.flags = DGPU_IS_FUSED | DGPU_IS_PERSISTENT;
+    s.unit_start = r->unit_start.data();
+    s.class_start = r->class_start.data();
+    s.rec_start = r->rec_start.data();
+    s.run_start = r->run_start.data();
+    const int64_t wsb = dav1d_gpu_intra_workspace_bytes(&s, n);
+    if (wsb < 0) return -2;
+    if (r->d_units.grow((size_t)n * sizeof(Dav1dGpuUnit)) || r->d_recs.grow((size_t)n * sizeof(Dav1dGpuIntraEdge)) ||
+        r->d_coef.grow(std::max<size_t>(r->coef_pool.size(), 16)) || r->d_edges.grow(std::max<size_t>(edge_px * bpp, 16)) ||
+        r->d_work.grow((size_t)wsb))
+        return -3;
+    if (hipMemcpyAsync(r->d_units.p, r->units.data(), (size_t)n * sizeof(Dav1dGpuUnit), hipMemcpyHostToDevice, st) ||
+        hipMemcpyAsync(r->d_recs.p, r->recs.data(), (size_t)n * sizeof(Dav1dGpuIntraEdge), hipMemcpyHostToDevice, st) ||
+        (r->coef_pool.size() &&
+         hipMemcpyAsync(r->d_coef.p, r->coef_pool.data(), r->coef_pool.size(), hipMemcpyHostToDevice, st)))
+        return -3;
+    s.workspace = r->d_work.p;
+    s.workspace_bytes = wsb;
+    Dav1dGpuFrameBatch fb;
+    memset(&fb, 0, sizeof(fb));
+    Dav1dGpuIntraEdgeBatch eb;
+    memset(&eb, 0, sizeof(eb));
+    for (int p = 0; p < 3; p++) {
+        fb.dst[p] = dst[p];
+        eb.pic[p] = dst[p];
+        if (ref)
+            for (int k = 0; k < DGPU_MAX_REFS; k++) fb.ref[k][p] = ref[k][p];
+    }
+    eb.sb_log2[0] = 6;
+    eb.sb_log2[1] = eb.sb_log2[2] = 5;
+    fb.units = (const Dav1dGpuUnit *)r->d_units.p;
+    fb.n_units = n;
+    fb.class_start[NC] = n;
+    fb.coef = r->d_coef.p;
+    fb.edges = r->d_edges.p;
+    fb.bitdepth_max = r->bdmax;
+    fb.cfl_luma = dst[0];
+    fb.cfl_ss = 3;
+    eb.units = (Dav1dGpuUnit *)r->d_units.p;
+    eb.edges = r->d_edges.p;
+    eb.recs = (const Dav1dGpuIntraEdge *)r->d_recs.p;
+    eb.n_recs = n;
+    eb.bitdepth_max = r->bdmax;
+    const int rc = r->bpc == 8 ? dav1d_gpu_recon_intra_frame_8bpc(&fb, &eb, &s, stream)
+                               : dav1d_gpu_recon_intra_frame_16bpc(&fb, &eb, &s, stream);
+    if (rc) return rc;
+    if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return -3;
+    if (hipEventRecord(r->done, st) != hipSuccess) return -3;
+    r->blocks.clear();
+    r->residuals.clear();
+    r->coef32.clear();
+    return 0;
+}

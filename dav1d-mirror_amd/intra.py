@@ -292,6 +292,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     smooth = lambda m: 9 <= m <= 11   # noqa: E731
 
     U = {k: [] for k in ("plane", "x", "y", "tw", "th", "blk", "cfl", "mode", "angle", "flags")}
+    BL = []   # per block and plane, decode order: what recon_b_* hands the recorder
     for b in range(nb):
         x, y, s = int(lx[b]), int(ly[b]), int(ls[b])
         x0, y0, x1, y1 = int(tile_x0[b]), int(tile_y0[b]), int(tile_x1[b]), int(tile_y1[b])
@@ -313,6 +314,18 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
             tw, th = luma_tx if pl == 0 else (ps_, ps_)
             cfl = pl > 0 and bool(is_cfl[b]) and not is_inter[b]
             bw4 = ps_ // 4
+            kind_ = int(bkind[b]) if is_inter[b] else (abi.PRED_CFL if cfl else abi.PRED_INTRA)
+            bfl = (abi.IE_TOP_HAS_RIGHT if tr else 0) | (abi.IE_LEFT_HAS_BOTTOM if bl else 0)
+            if cfg.filter_edge:
+                bfl |= abi.IE_FILTER_EDGE
+            if (ysm if pl == 0 else uvsm):
+                bfl |= abi.IE_SMOOTH
+            mvs = [(int(bmv[b, k, 0]) >> ss, int(bmv[b, k, 1]) >> ss) for k in range(2)]
+            BL.append((pl, px_, py_, ps_, ps_, abi.TX_INDEX[(tw, th)], kind_, x0 >> ss, y0 >> ss, x1 >> ss,
+                       y1 >> ss, mvs[0][0], mvs[1][0], mvs[0][1], mvs[1][1], 0, 1, int(bfilt[b]), 0,
+                       0 if cfl else int(ymode[b] if pl == 0 else uvmode[b]),
+                       0 if cfl else int(yang[b] if pl == 0 else uvang[b]),
+                       int(alpha[b, pl - 1]) if cfl else 0, 0 if cfl or is_inter[b] else bfl))
             for oy in range(0, ps_, th):
                 for ox in range(0, ps_, tw):
                     x4, y4 = ox // 4, oy // 4
@@ -467,6 +480,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
         if i < n:
             steps.append((0, i))
 
+    dec_units = units.copy()
     # level order, size classes inside a level, then pred / mode / type
     perm = np.lexsort((units["txtp"], np.array(modes), units["pred"], units["tx"], level))
     inv = np.empty(n, np.int64)
@@ -497,9 +511,12 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     steps[unit_steps, 1] = inv[steps[unit_steps, 1]]
     top_rows = [(max(1, h >> s_), w) for (w, h), s_ in zip(planes, sbl)]
     edges = np.zeros(int(edge_len.sum()), cfg.pixel_dtype)
-    return IntraFrame(cfg, planes, units, coefs, edges, recs, runs, unit_start, class_start, rec_start,
-                      run_start, steps, unit_rec, np.array(oracle_runs, abi.EDGE_BACKUP_DTYPE), top_rows, sbl,
-                      refs)
+    fr = IntraFrame(cfg, planes, units, coefs, edges, recs, runs, unit_start, class_start, rec_start,
+                    run_start, steps, unit_rec, np.array(oracle_runs, abi.EDGE_BACKUP_DTYPE), top_rows, sbl,
+                    refs)
+    fr.blocks = BL
+    fr.dec_units = dec_units
+    return fr
 
 
 def frame_batch(fr, dst_ptrs, units, coefs, edges, ref_ptrs=None):
@@ -617,3 +634,85 @@ class DeviceIntraFrame:
             a = t.cpu().numpy()
             out.append(a if self.fr.cfg.bpc == 8 else a.view(np.uint16))
         return out
+
+
+class Recorder:
+    """The batch recorder (dav1d_gpu_recorder_*, csrc/recorder.hip): blocks and
+    residuals as recon_b_* would hand them over, one flush per frame."""
+
+    def __init__(self, bpc, bitdepth_max, width, height, device_index=0):
+        self.lib = abi.load_lib()
+        self.bpc = bpc
+        self.h = self.lib.dav1d_gpu_recorder_new(bpc, bitdepth_max, width, height, device_index)
+        if not self.h:
+            raise RuntimeError("dav1d_gpu_recorder_new failed")
+
+    def close(self):
+        if self.h:
+            self.lib.dav1d_gpu_recorder_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def block(self, rb):
+        rc = self.lib.dav1d_gpu_rec_block(self.h, ctypes.byref(rb))
+        if rc:
+            raise ValueError(f"dav1d_gpu_rec_block: {rc}")
+
+    def residual(self, plane, x, y, tx, txtp, eob, coef):
+        c = np.ascontiguousarray(coef, dtype=np.int16 if self.bpc == 8 else np.int32)
+        rc = self.lib.dav1d_gpu_rec_residual(self.h, plane, x, y, tx, txtp, eob, c.ctypes.data)
+        if rc:
+            raise ValueError(f"dav1d_gpu_rec_residual: {rc}")
+
+    def flush(self, dst, refs, stream):
+        """dst: 3 device tensors (h, w); refs: list of [3 device tensors] with
+        their picture origin offsets as (tensor, origin_px) pairs, or None."""
+        bpp = 1 if self.bpc == 8 else 2
+        d = (abi.Plane * 3)()
+        for p, t in enumerate(dst):
+            d[p].data, d[p].stride, d[p].w, d[p].h = t.data_ptr(), t.shape[1] * bpp, t.shape[1], t.shape[0]
+        r = ((abi.Plane * 3) * abi.MAX_REFS)()
+        for k, rp in enumerate(refs or []):
+            for p, (t, org, w, h) in enumerate(rp):
+                r[k][p].data, r[k][p].stride, r[k][p].w, r[k][p].h = t.data_ptr() + org * bpp, t.shape[1] * bpp, w, h
+        rc = self.lib.dav1d_gpu_recorder_flush(self.h, ctypes.byref(d), ctypes.byref(r),
+                                               ctypes.c_void_p(stream.cuda_stream))
+        if rc:
+            raise RuntimeError(f"dav1d_gpu_recorder_flush: {rc}")
+
+    def stats(self):
+        n, lv = ctypes.c_int32(), ctypes.c_int32()
+        self.lib.dav1d_gpu_recorder_stats(self.h, ctypes.byref(n), ctypes.byref(lv))
+        return n.value, lv.value
+
+
+def replay(rec, fr):
+    """Feed an IntraFrame's blocks and residuals to a Recorder, in decode
+    order, the way recon_b_* would (coefficients expanded to the reference's
+    inv_txfm_add layout: column-major, min(h,32) rows)."""
+    for t in fr.blocks:
+        rb = abi.RecBlock()
+        (rb.plane, rb.x, rb.y, rb.w, rb.h, rb.tx, rb.kind, rb.tile_x0, rb.tile_y0, rb.tile_x1, rb.tile_y1,
+         rb.mvx[0], rb.mvx[1], rb.mvy[0], rb.mvy[1], rb.ref[0], rb.ref[1], rb.filter2d, rb.weight, rb.mode,
+         rb.angle, rb.cfl_alpha, rb.flags) = t
+        rec.block(rb)
+    u = fr.dec_units
+    for i in np.nonzero(u["txtp"] != abi.NO_RESIDUAL)[0]:
+        p = int(u["plane"][i])
+        w = fr.plane_wh[p][0]
+        y, x = divmod(int(u["dst_off"][i]), w)
+        tw, th = abi.TX_WH[int(u["tx"][i])]
+        sw, sh = min(tw, 32), min(th, 32)
+        cf = np.zeros(sw * sh, np.int64)
+        nzw, nzh, o = int(u["nzw"][i]), int(u["nzh"][i]), int(u["coef_off"][i])
+        if nzw == 0:
+            cf[0] = fr.coefs[o]
+            eob = 0 if int(u["txtp"][i]) == abi.DCT_DCT else 1
+        else:
+            reg = fr.coefs[o:o + nzw * nzh].reshape(nzw, nzh)   # [x][y]
+            for xx in range(nzw):
+                cf[xx * sh:xx * sh + nzh] = reg[xx]
+            eob = 1
+        rec.residual(p, x, y, int(u["tx"][i]), int(u["txtp"][i]), eob, cf)

@@ -606,6 +606,64 @@ int dav1d_gpu_recon_intra_frame_8bpc(const Dav1dGpuFrameBatch *recon, const Dav1
 int dav1d_gpu_recon_intra_frame_16bpc(const Dav1dGpuFrameBatch *recon, const Dav1dGpuIntraEdgeBatch *edges,
                                       const Dav1dGpuIntraSchedule *s, void *stream);
 
+/* ---- batch recorder ----------------------------------
+ * The reconstruction seam: what recon_b_inter / recon_b_intra
+ * (src/recon_tmpl.c:1598, :1195) would execute per block, recorded instead
+ * (one Dav1dGpuRecBlock per block and plane, one residual per coded
+ * transform block, in decode order), then reconstructed on the device by
+ * one flush: the recorder cuts blocks into transform units, derives each
+ * intra transform block's edge record the way recon_b_intra does
+ * (:1248-1294: have_left / have_top against the tile, the per-transform
+ * TOP_HAS_RIGHT / LEFT_HAS_BOTTOM from the block's edge flags), schedules
+ * dependency levels (inter units at level 0; intra units after every unit
+ * whose pixels their edges or CfL luma read) and runs the persistent
+ * wavefront.  Host C++ (csrc/recorder.cpp); device buffers are the
+ * recorder's own.  4:2:0 only. */
+typedef struct Dav1dGpuRecorder Dav1dGpuRecorder;
+
+typedef struct Dav1dGpuRecBlock {
+    int32_t plane;           /* 0 Y, 1 U, 2 V                                  */
+    int32_t x, y, w, h;      /* the prediction block, plane pixels            */
+    int32_t tx;              /* its transform size (b->tx / uvtx), uniform    */
+    int32_t kind;            /* DGPU_PRED_INTER / INTER_AVG / INTER_WAVG /
+                                INTRA / CFL                                   */
+    int32_t tile_x0, tile_y0, tile_x1, tile_y1;   /* the tile, plane pixels    */
+    /* inter: the mc() call per reference (src/recon_tmpl.c:957): the
+       motion vector in 1/16 plane pixels (chroma already scaled), the ref
+       slot, filter_2d, and the jnt weight for INTER_WAVG                      */
+    int32_t mvx[2], mvy[2];
+    uint8_t ref[2], filter2d, weight;
+    /* intra: the coded mode (DC..PAETH = 0..12, FILTER 13) and angle delta
+       (FILTER: the filter index); CFL: alpha (its DC source is prepared
+       from DC_PRED, :1395-1410)                                              */
+    uint8_t mode;
+    int8_t  angle;
+    int8_t  cfl_alpha;
+    uint8_t flags;           /* DGPU_IE_TOP_HAS_RIGHT / LEFT_HAS_BOTTOM of the
+                                block (intra_edge_flags), DGPU_IE_FILTER_EDGE,
+                                DGPU_IE_SMOOTH                                 */
+} Dav1dGpuRecBlock;
+
+Dav1dGpuRecorder *dav1d_gpu_recorder_new(int bpc, int bitdepth_max, int width, int height, int device);
+void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r);
+/* Record one block / one coded transform block.  coef: the reference's
+ * coefficient layout for inv_txfm_add (int16 8bpc, int32 16bpc; column-major,
+ * min(h,32) rows, min(w,32) columns, src/itx_tmpl.c:82-85); eob as the
+ * decoder passes it (eob == 0 with DCT_DCT is the DC-only call).  A
+ * residual must lie inside a block recorded before it.  0 or -1. */
+int dav1d_gpu_rec_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b);
+int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int y, int tx, int txtp, int eob,
+                           const void *coef);
+/* Build, upload and launch everything recorded since the last flush on
+ * `stream` (the recorder waits for its previous flush before reusing its
+ * buffers).  dst: the picture being reconstructed (CfL reads its luma);
+ * ref: reference planes for inter blocks, edge-replicated as for
+ * dav1d_gpu_recon_*.  Returns 0, -1 bad arguments, or a launch error. */
+int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane dst[3],
+                             const Dav1dGpuPlane ref[DGPU_MAX_REFS][3], void *stream);
+/* Levels and units of the last flush (diagnostics). */
+int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_units, int32_t *n_levels);
+
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split
  * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).

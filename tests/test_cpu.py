@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_header_symbols_exported(pkg):
     hdr = open(os.path.join(ROOT, "include", "dav1d_gpu.h")).read()
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    declared = set(re.findall(r"^\s*(?:int|int64_t|void|const char \*)\s*(dav1d_\w+)\s*\(", hdr, flags=re.M))
+    declared = set(re.findall(r"^\s*(?:int|int64_t|void|const char \*|Dav1dGpuRecorder \*)\s*(dav1d_\w+)\s*\(", hdr, flags=re.M))
     assert len(declared) >= 17
     assert declared == set(pkg.abi.EXPORTED_SYMBOLS)
     lib = ctypes.CDLL(pkg.abi.lib_path())   # loads without touching a device

@@ -1,0 +1,77 @@
+"""CPU tests of the batch recorder (dav1d_gpu_recorder_*):
+the Dav1dGpuRecBlock layout against its ctypes mirror, and the recording
+calls' validation (no device is touched before a flush)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_LAYOUT_C = r"""
+#include <stddef.h>
+#include <stdio.h>
+#include "dav1d_gpu.h"
+#define P(f) printf(#f " %zu\n", offsetof(Dav1dGpuRecBlock, f))
+int main(void) {
+    printf("size %zu\n", sizeof(Dav1dGpuRecBlock));
+    P(plane); P(x); P(y); P(w); P(h); P(tx); P(kind); P(tile_x0); P(tile_y0); P(tile_x1); P(tile_y1);
+    P(mvx); P(mvy); P(ref); P(filter2d); P(weight); P(mode); P(angle); P(cfl_alpha); P(flags);
+    return 0;
+}
+"""
+
+
+def test_rec_block_layout(pkg, tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(_LAYOUT_C)
+    exe = tmp_path / "layout"
+    subprocess.run(["cc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    c = {k: int(v) for k, v in (line.split() for line in out.splitlines())}
+    R = pkg.abi.RecBlock
+    assert c["size"] == ctypes.sizeof(R)
+    for name, _ in R._fields_:
+        assert c[name] == getattr(R, name).offset, name
+
+
+def _blk(pkg, **kw):
+    b = pkg.abi.RecBlock()
+    b.plane, b.x, b.y, b.w, b.h, b.tx, b.kind = 0, 16, 16, 16, 16, pkg.abi.TX_INDEX[(8, 8)], pkg.abi.PRED_INTRA
+    b.tile_x0, b.tile_y0, b.tile_x1, b.tile_y1 = 0, 0, 64, 64
+    for k, v in kw.items():
+        setattr(b, k, v)
+    return b
+
+
+def test_recorder_validation(pkg):
+    L = pkg.abi.load_lib()
+    abi = pkg.abi
+    assert not L.dav1d_gpu_recorder_new(10, 1023, 64, 64, 0)          # bpc 8 or 16
+    assert not L.dav1d_gpu_recorder_new(8, 255, 60, 64, 0)            # 8-px aligned sizes
+    r = L.dav1d_gpu_recorder_new(8, 255, 64, 64, 0)
+    assert r
+    try:
+        rec = lambda **kw: L.dav1d_gpu_rec_block(r, ctypes.byref(_blk(pkg, **kw)))   # noqa: E731
+        assert rec() == 0
+        assert rec(plane=3) == -1
+        assert rec(x=56) == -1                                        # leaves the plane
+        assert rec(w=12) == -1                                        # not a multiple of the transform
+        assert rec(kind=abi.PRED_PAL) == -1                           # not a recordable kind
+        assert rec(mode=14) == -1
+        assert rec(tile_x1=24) == -1                                  # block outside its tile
+        assert rec(kind=abi.PRED_CFL) == -1                           # CfL on luma
+        assert rec(plane=1, x=8, y=8, w=8, h=8, kind=abi.PRED_CFL, tile_x1=32, tile_y1=32) == 0
+        assert rec(plane=1, x=8, y=8, w=16, h=16, kind=abi.PRED_CFL, tile_x1=32, tile_y1=32) == -1   # != tx
+        assert rec(kind=abi.PRED_INTER, filter2d=10) == -1
+        cf = np.zeros(64, np.int16)
+        res = lambda *a: L.dav1d_gpu_rec_residual(r, *a, cf.ctypes.data)   # noqa: E731
+        assert res(0, 16, 16, abi.TX_INDEX[(8, 8)], 0, 0) == 0
+        assert res(0, 60, 16, abi.TX_INDEX[(8, 8)], 0, 0) == -1          # leaves the plane
+        assert res(0, 16, 16, abi.TX_INDEX[(8, 8)], 17, 0) == -1         # no such type
+        assert L.dav1d_gpu_rec_residual(r, 0, 16, 16, 1, 0, 0, None) == -1
+        n, lv = ctypes.c_int32(), ctypes.c_int32()
+        assert L.dav1d_gpu_recorder_stats(r, ctypes.byref(n), ctypes.byref(lv)) == 0 and n.value == 0
+    finally:
+        L.dav1d_gpu_recorder_free(r)
