@@ -24,9 +24,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <numeric>
 #include <vector>
 
@@ -81,6 +83,24 @@ struct DevBuf {
     }
 };
 
+// LSD radix sort of 64-bit keys, 16-bit digits
+void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int bits) {
+    tmp.resize(k.size());
+    std::vector<uint32_t> cnt(1 << 16);
+    for (int sh = 0; sh < bits; sh += 16) {
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (uint64_t v : k) cnt[(v >> sh) & 0xffff]++;
+        uint32_t acc = 0;
+        for (auto &c : cnt) {
+            const uint32_t t = c;
+            c = acc;
+            acc += t;
+        }
+        for (uint64_t v : k) tmp[cnt[(v >> sh) & 0xffff]++] = v;
+        k.swap(tmp);
+    }
+}
+
 struct Unit {   // a transform cell before sorting
     Dav1dGpuUnit u;
     Dav1dGpuIntraEdge rec;
@@ -96,10 +116,13 @@ struct Dav1dGpuRecorder {
     std::vector<Residual> residuals;
     std::vector<int32_t> coef32;   // compact regions (int32 for both ABIs; narrowed at flush)
     // flush products (kept alive while the device may still read them)
-    std::vector<Dav1dGpuUnit> units;
-    std::vector<Dav1dGpuIntraEdge> recs;
     std::vector<int32_t> unit_start, class_start, rec_start, run_start;
-    std::vector<uint8_t> coef_pool;
+    std::vector<Unit> cells;
+    std::vector<uint64_t> keys, keys_tmp;
+    std::vector<int32_t> rank;
+    std::vector<Dav1dGpuUnit> h_units;
+    std::vector<Dav1dGpuIntraEdge> h_recs;
+    std::vector<uint8_t> h_coef;
     DevBuf d_units, d_recs, d_coef, d_edges, d_work;
     hipEvent_t done = nullptr;
     int32_t last_units = 0, last_levels = 0;
@@ -203,6 +226,16 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     if (!r || !dst) return -1;
     if (hipSetDevice(r->device) != hipSuccess) return -3;
     if (r->done && hipEventSynchronize(r->done) != hipSuccess) return -3;   // buffers free for reuse
+    // DAV1D_GPU_REC_TIMING=1: host phase times on stderr (diagnostics)
+    static const bool timing = getenv("DAV1D_GPU_REC_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_0 = now();
+    auto lap = [&](const char *what) {
+        if (!timing) return;
+        const auto t = now();
+        fprintf(stderr, "recorder %-8s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_0).count());
+        t_0 = t;
+    };
     const int bpp = r->bpc / 8;
     int pw[3], ph[3];
     for (int p = 0; p < 3; p++) plane_dims(r, p, pw[p], ph[p]);
@@ -216,7 +249,13 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     }
 
     // 1-3. transform units in decode order, their edge records and levels
-    std::vector<Unit> cells;
+    std::vector<Unit> &cells = r->cells;
+    cells.clear();
+    {
+        size_t nc = 0;
+        for (const Dav1dGpuRecBlock &b : r->blocks) nc += (size_t)(b.w / kTx[b.tx].w) * (b.h / kTx[b.tx].h);
+        cells.reserve(nc);
+    }
     std::vector<int32_t> lv[3];
     for (int p = 0; p < 3; p++) lv[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
     size_t n_res_used = 0;
@@ -338,60 +377,75 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
             }
     }
     if (n_res_used != r->residuals.size()) return -1;   // a residual outside every block
+    lap("cells");
     const int n = (int)cells.size();
 
-    // 4. level order, size classes inside a level, then kind / mode / type
-    std::vector<int> perm(n);
-    std::iota(perm.begin(), perm.end(), 0);
-    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) {
-        const Unit &x = cells[a], &y = cells[b];
-        if (x.level != y.level) return x.level < y.level;
-        if (x.u.tx != y.u.tx) return x.u.tx < y.u.tx;
-        if (x.u.pred != y.u.pred) return x.u.pred < y.u.pred;
-        if (x.sortmode != y.sortmode) return x.sortmode < y.sortmode;
-        return x.u.txtp < y.u.txtp;
-    });
-    const int n_levels = n ? cells[perm[n - 1]].level + 1 : 0;
-    r->units.resize(n);
-    r->recs.resize(n);
+    // 4. level order, size classes inside a level, then kind / mode / type:
+    //    one radix sort of (key << 21 | index)
+    if (n >= (1 << 21)) return -1;
+    std::vector<uint64_t> &keys = r->keys;
+    keys.resize(n);
+    int max_level = 0;
+    for (int i = 0; i < n; i++) {
+        const Unit &c = cells[i];
+        if (c.level >= (1 << 16)) return -1;
+        max_level = std::max(max_level, c.level);
+        const uint64_t key = (uint64_t)c.level << 24 | (uint64_t)c.u.tx << 19 | (uint64_t)c.u.pred << 15 |
+                             (uint64_t)(c.sortmode & 63) << 9 | (uint64_t)(c.u.txtp == DGPU_NO_RESIDUAL ? 511 : c.u.txtp);
+        keys[i] = key << 21 | (uint64_t)i;
+    }
+    radix_sort(keys, r->keys_tmp, 64);
+    lap("sort");
+    const int n_levels = n ? max_level + 1 : 0;
     r->unit_start.assign(n_levels + 1, 0);
     r->class_start.assign((size_t)n_levels * (NC + 1), 0);
     const size_t cb = r->bpc == 8 ? 2 : 4;
-    r->coef_pool.clear();
-    size_t edge_px = 0;
+    // the rank of every decode-order cell, and the level / class ranges
+    std::vector<int32_t> &rank = r->rank;
+    rank.resize(n);
     for (int i = 0; i < n; i++) {
-        const Unit &c = cells[perm[i]];
-        Dav1dGpuUnit u = c.u;
-        if (u.txtp != DGPU_NO_RESIDUAL) {   // compact region into the pool, in unit order
-            const size_t src = (size_t)u.coef_off, cnt = u.nzw ? (size_t)u.nzw * u.nzh : 1;
-            u.coef_off = (int32_t)(r->coef_pool.size() / cb);
-            for (size_t k = 0; k < cnt; k++) {
-                const int32_t v = r->coef32[src + k];
-                if (cb == 2) {
-                    const int16_t h = (int16_t)v;
-                    r->coef_pool.insert(r->coef_pool.end(), (const uint8_t *)&h, (const uint8_t *)&h + 2);
-                } else {
-                    r->coef_pool.insert(r->coef_pool.end(), (const uint8_t *)&v, (const uint8_t *)&v + 4);
-                }
-            }
-        }
+        const uint64_t k = keys[i];
+        const int ci = (int)(k & ((1u << 21) - 1)), level = (int)(k >> 45), tx = (int)((k >> 40) & 31);
+        rank[ci] = i;
+        r->unit_start[level + 1] = i + 1;
+        r->class_start[(size_t)level * (NC + 1) + tx + 1]++;
+    }
+    // then one sequential pass in decode order, scattering to the ranks
+    // (reading the cells in rank order measured 13 ms of cache misses at 4K);
+    // the coefficient pool stays in decode order
+    r->h_units.resize((size_t)n);
+    r->h_recs.resize((size_t)n);
+    r->h_coef.resize(r->coef32.size() * cb);
+    Dav1dGpuUnit *hu = r->h_units.data();
+    Dav1dGpuIntraEdge *hr = r->h_recs.data();
+    if (cb == 2) {
+        int16_t *d16 = (int16_t *)r->h_coef.data();
+        for (size_t k = 0; k < r->coef32.size(); k++) d16[k] = (int16_t)r->coef32[k];
+    } else if (!r->coef32.empty()) {
+        memcpy(r->h_coef.data(), r->coef32.data(), r->coef32.size() * 4);
+    }
+    const size_t coef_at = r->coef32.size();
+    size_t edge_px = 0;
+    for (int ci = 0; ci < n; ci++) {
+        const Unit &c = cells[ci];
+        const int i = rank[ci];
+        Dav1dGpuUnit u = c.u;   // coef_off is already the decode-order pool offset
         if (u.pred == DGPU_PRED_INTRA || u.pred == DGPU_PRED_CFL) {   // an edge slot (the staged path's pool)
             const TxDim t = kTx[u.tx];
             u.p.intra.edge_off = (int32_t)(edge_px + 2 * t.h);
             edge_px += 2 * t.h + 2 * t.w + 1;
         }
-        r->units[i] = u;
+        hu[i] = u;
         Dav1dGpuIntraEdge e = c.rec;
         e.unit = i;
-        r->recs[i] = e;
-        r->unit_start[c.level + 1] = i + 1;
-        r->class_start[(size_t)c.level * (NC + 1) + u.tx + 1]++;
+        hr[i] = e;
     }
     for (int l = 0; l < n_levels; l++) {
         if (r->unit_start[l + 1] < r->unit_start[l]) r->unit_start[l + 1] = r->unit_start[l];   // (levels are dense)
         int32_t *cs = &r->class_start[(size_t)l * (NC + 1)];
         for (int k = 0; k < NC; k++) cs[k + 1] += cs[k];
     }
+    lap("fill");
     r->rec_start = r->unit_start;
     r->run_start.assign(n_levels + 1, 0);
     r->last_units = n;
@@ -416,13 +470,12 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     const int64_t wsb = dav1d_gpu_intra_workspace_bytes(&s, n);
     if (wsb < 0) return -2;
     if (r->d_units.grow((size_t)n * sizeof(Dav1dGpuUnit)) || r->d_recs.grow((size_t)n * sizeof(Dav1dGpuIntraEdge)) ||
-        r->d_coef.grow(std::max<size_t>(r->coef_pool.size(), 16)) || r->d_edges.grow(std::max<size_t>(edge_px * bpp, 16)) ||
+        r->d_coef.grow(std::max<size_t>(coef_at * cb, 16)) || r->d_edges.grow(std::max<size_t>(edge_px * bpp, 16)) ||
         r->d_work.grow((size_t)wsb))
         return -3;
-    if (hipMemcpyAsync(r->d_units.p, r->units.data(), (size_t)n * sizeof(Dav1dGpuUnit), hipMemcpyHostToDevice, st) ||
-        hipMemcpyAsync(r->d_recs.p, r->recs.data(), (size_t)n * sizeof(Dav1dGpuIntraEdge), hipMemcpyHostToDevice, st) ||
-        (r->coef_pool.size() &&
-         hipMemcpyAsync(r->d_coef.p, r->coef_pool.data(), r->coef_pool.size(), hipMemcpyHostToDevice, st)))
+    if (hipMemcpyAsync(r->d_units.p, hu, (size_t)n * sizeof(Dav1dGpuUnit), hipMemcpyHostToDevice, st) ||
+        hipMemcpyAsync(r->d_recs.p, hr, (size_t)n * sizeof(Dav1dGpuIntraEdge), hipMemcpyHostToDevice, st) ||
+        (coef_at && hipMemcpyAsync(r->d_coef.p, r->h_coef.data(), coef_at * cb, hipMemcpyHostToDevice, st)))
         return -3;
     s.workspace = r->d_work.p;
     s.workspace_bytes = wsb;
@@ -451,8 +504,10 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     eb.recs = (const Dav1dGpuIntraEdge *)r->d_recs.p;
     eb.n_recs = n;
     eb.bitdepth_max = r->bdmax;
+    lap("upload");
     const int rc = r->bpc == 8 ? dav1d_gpu_recon_intra_frame_8bpc(&fb, &eb, &s, stream)
                                : dav1d_gpu_recon_intra_frame_16bpc(&fb, &eb, &s, stream);
+    lap("launch");
     if (rc) return rc;
     if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return -3;
     if (hipEventRecord(r->done, st) != hipSuccess) return -3;
