@@ -193,6 +193,49 @@ def intra_breakdown(cfg, dev, stream, steps):
     return out
 
 
+def recorder_breakdown(cfg, dev):
+    """a 4K mixed frame (70% inter blocks) handed to the
+    native batch recorder block by block and residual by residual
+    (dav1d_gpu_rec_*), then one flush: the flush's host time (units, edge
+    records, level schedule, upload) and its device time (HIP events with
+    the GPU kept busy while the host builds), checked against the oracle."""
+    import torch
+    import dav1d_mirror_amd.intra as intra
+    fr = intra.make_intra_frame(intra.IntraConfig(width=cfg.width, height=cfg.height, bpc=cfg.bpc,
+                                                  bitdepth_max=cfg.bitdepth_max, inter_frac=0.7,
+                                                  sb_edge_backup=False))
+    hbd = cfg.bpc != 8
+    pdt = torch.int16 if hbd else torch.uint8
+    dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fr.plane_wh]
+    refs = [[(torch.from_numpy((x.view(np.int16) if hbd else x).copy()).to(dev), fr.ref_origin_offset(p),
+              fr.plane_wh[p][0], fr.plane_wh[p][1]) for p, x in enumerate(rp)] for rp in fr.refs]
+    rec = intra.Recorder(cfg.bpc, cfg.bitdepth_max, cfg.width, cfg.height, dev.index or 0)
+    s = torch.cuda.current_stream(dev)
+    host, devt = [], []
+    for _ in range(2):
+        intra.replay(rec, fr)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(0.2 * 2.0e9))
+        e0.record(s)
+        t0 = time.perf_counter()
+        rec.flush(dst, refs, s)
+        host.append(time.perf_counter() - t0)
+        e1.record(s)
+        torch.cuda.synchronize(dev)
+        devt.append(e0.elapsed_time(e1) * 1e-3)
+    n_units, n_levels = rec.stats()
+    rec.close()
+    ho = ge.load_oracle().HostIntraFrame(fr)
+    ho.run()
+    got = [(t.cpu().numpy().view(np.uint16) if hbd else t.cpu().numpy()) for t in dst]
+    px = sum(w * h for w, h in fr.plane_wh)
+    return {"frame": f"{cfg.width}x{cfg.height}, 70% inter blocks", "units": n_units, "levels": n_levels,
+            "flush_host_ms": round(host[-1] * 1e3, 2), "flush_device_ms": round(devt[-1] * 1e3, 3),
+            "device_gpix_s": round(px / devt[-1] / 1e9, 3),
+            "bit_exact_vs_oracle": all(bool(np.array_equal(g, o)) for g, o in zip(got, ho.dst))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -206,6 +249,7 @@ def main():
     ap.add_argument("--no-families", action="store_true", help="skip the per-family breakdown (N=1)")
     ap.add_argument("--no-tiles", action="store_true", help="skip the tile-batch measurement (N=1)")
     ap.add_argument("--no-intra", action="store_true", help="skip the intra-wavefront measurement (N=1)")
+    ap.add_argument("--no-recorder", action="store_true", help="skip the batch-recorder measurement (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -329,6 +373,8 @@ def main():
             out["tile_batch"] = tile_breakdown(fd, dev, stream, args.steps)
         if not args.no_intra and world == 1 and c.get("kind") == "full":
             out["intra_wavefront"] = intra_breakdown(cfg, dev, stream, args.steps)
+        if not args.no_recorder and world == 1 and c.get("kind") == "full":
+            out["recorder"] = recorder_breakdown(cfg, dev)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
         print(json.dumps(out), flush=True)

@@ -16,6 +16,7 @@
 // bound (DGPU_FLOW_SPIN_LIMIT) turns any unexpected stall into an error
 // flag; a wave that gives up still counts itself done, so the grid drains.
 #pragma once
+#include <mutex>
 #include <vector>
 
 #include "recon_impl.hpp"
@@ -177,6 +178,52 @@ static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<F
     return 0;
 }
 
+// Page-locked staging for the task list: a pageable source would make the
+// copy wait for everything already queued on the stream.  A small pool of
+// buffers, each reusable once the event recorded after its copy has passed.
+struct FlowStage {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+};
+static std::mutex g_stage_mu;
+static std::vector<FlowStage> g_stage;
+
+static FlowStage *flow_stage_get(size_t n) {   // call with g_stage_mu held
+    for (FlowStage &st : g_stage)
+        if (st.cap >= n && hipEventQuery(st.ev) == hipSuccess) return &st;
+    for (FlowStage &st : g_stage)   // a free but small one: grow it
+        if (hipEventQuery(st.ev) == hipSuccess) {
+            (void)hipHostFree(st.p);
+            st.p = nullptr;
+            st.cap = 0;
+            if (hipHostMalloc(&st.p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+            st.cap = n;
+            return &st;
+        }
+    if (g_stage.size() >= 8) {   // all busy: wait for the oldest
+        FlowStage &st = g_stage.front();
+        if (hipEventSynchronize(st.ev) != hipSuccess) return nullptr;
+        if (st.cap < n) {
+            (void)hipHostFree(st.p);
+            st.p = nullptr;
+            st.cap = 0;
+            if (hipHostMalloc(&st.p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+            st.cap = n;
+        }
+        return &st;
+    }
+    g_stage.emplace_back();
+    FlowStage &st = g_stage.back();
+    if (hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(&st.p, n, hipHostMallocDefault) != hipSuccess) {
+        g_stage.pop_back();
+        return nullptr;
+    }
+    st.cap = n;
+    return &st;
+}
+
 template <int BPC>
 static int64_t flow_workspace_bytes(const Dav1dGpuIntraSchedule *s, int n_units) {
     std::vector<FlowTask> t;
@@ -211,13 +258,18 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     f.n_tasks = (int)tasks.size();
     f.level_tasks = (const int32_t *)(ws + ctr_bytes + tasks.size() * sizeof(FlowTask));
     f.trace = (unsigned long long *)(ws + ((base + 15) & ~(size_t)15));
-    // (pageable sources: the copies are staged before these calls return)
-    if (hipMemsetAsync(ws, 0, ctr_bytes, stream) != hipSuccess ||
-        hipMemcpyAsync(ws + ctr_bytes, tasks.data(), tasks.size() * sizeof(FlowTask), hipMemcpyHostToDevice,
-                       stream) != hipSuccess ||
-        hipMemcpyAsync(ws + ctr_bytes + tasks.size() * sizeof(FlowTask), level_tasks.data(),
-                       level_tasks.size() * 4, hipMemcpyHostToDevice, stream) != hipSuccess)
-        return -3;
+    {   // the task list through page-locked staging (asynchronous copy)
+        const size_t tb = tasks.size() * sizeof(FlowTask), lb = level_tasks.size() * 4;
+        std::lock_guard<std::mutex> lock(g_stage_mu);
+        FlowStage *sg = flow_stage_get(tb + lb);
+        if (!sg) return -3;
+        memcpy(sg->p, tasks.data(), tb);
+        memcpy((uint8_t *)sg->p + tb, level_tasks.data(), lb);
+        if (hipMemsetAsync(ws, 0, ctr_bytes, stream) != hipSuccess ||
+            hipMemcpyAsync(ws + ctr_bytes, sg->p, tb + lb, hipMemcpyHostToDevice, stream) != hipSuccess ||
+            hipEventRecord(sg->ev, stream) != hipSuccess)
+            return -3;
+    }
     ReconArgs<BPC> a;
     memset(&a, 0, sizeof(a));
     for (int p = 0; p < 3; p++) {

@@ -83,6 +83,25 @@ struct DevBuf {
     }
 };
 
+struct PinnedBuf {   // page-locked staging, so the uploads do not wait for the stream
+    void *p = nullptr;
+    size_t cap = 0;
+    int grow(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return -1;
+        cap = n;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 // LSD radix sort of 64-bit keys, 16-bit digits
 void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int bits) {
     tmp.resize(k.size());
@@ -123,6 +142,7 @@ struct Dav1dGpuRecorder {
     std::vector<Dav1dGpuUnit> h_units;
     std::vector<Dav1dGpuIntraEdge> h_recs;
     std::vector<uint8_t> h_coef;
+    PinnedBuf pin;   // units | recs | coefficients, copied in one sequential pass
     DevBuf d_units, d_recs, d_coef, d_edges, d_work;
     hipEvent_t done = nullptr;
     int32_t last_units = 0, last_levels = 0;
@@ -146,6 +166,7 @@ extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
             (void)hipEventSynchronize(r->done);
             (void)hipEventDestroy(r->done);
         }
+        r->pin.release();
         r->d_units.release();
         r->d_recs.release();
         r->d_coef.release();
@@ -473,9 +494,16 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         r->d_coef.grow(std::max<size_t>(coef_at * cb, 16)) || r->d_edges.grow(std::max<size_t>(edge_px * bpp, 16)) ||
         r->d_work.grow((size_t)wsb))
         return -3;
-    if (hipMemcpyAsync(r->d_units.p, hu, (size_t)n * sizeof(Dav1dGpuUnit), hipMemcpyHostToDevice, st) ||
-        hipMemcpyAsync(r->d_recs.p, hr, (size_t)n * sizeof(Dav1dGpuIntraEdge), hipMemcpyHostToDevice, st) ||
-        (coef_at && hipMemcpyAsync(r->d_coef.p, r->h_coef.data(), coef_at * cb, hipMemcpyHostToDevice, st)))
+    const size_t bu = (size_t)n * sizeof(Dav1dGpuUnit), br = (size_t)n * sizeof(Dav1dGpuIntraEdge),
+                 bc = coef_at * cb;
+    if (r->pin.grow(bu + br + bc)) return -3;
+    uint8_t *pin = (uint8_t *)r->pin.p;
+    memcpy(pin, hu, bu);
+    memcpy(pin + bu, hr, br);
+    if (bc) memcpy(pin + bu + br, r->h_coef.data(), bc);
+    if (hipMemcpyAsync(r->d_units.p, pin, bu, hipMemcpyHostToDevice, st) ||
+        hipMemcpyAsync(r->d_recs.p, pin + bu, br, hipMemcpyHostToDevice, st) ||
+        (bc && hipMemcpyAsync(r->d_coef.p, pin + bu + br, bc, hipMemcpyHostToDevice, st)))
         return -3;
     s.workspace = r->d_work.p;
     s.workspace_bytes = wsb;
