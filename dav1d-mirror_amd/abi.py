@@ -151,6 +151,27 @@ class RecBlock(ctypes.Structure):
                 ("flags", ctypes.c_uint8)]
 
 
+class FilmGrainData(ctypes.Structure):
+    """Dav1dGpuFilmGrainData: the layout of dav1d's Dav1dFilmGrainData."""
+    _fields_ = [("seed", ctypes.c_uint), ("num_y_points", ctypes.c_int),
+                ("y_points", (ctypes.c_uint8 * 2) * 14), ("chroma_scaling_from_luma", ctypes.c_int),
+                ("num_uv_points", ctypes.c_int * 2), ("uv_points", ((ctypes.c_uint8 * 2) * 10) * 2),
+                ("scaling_shift", ctypes.c_int), ("ar_coeff_lag", ctypes.c_int),
+                ("ar_coeffs_y", ctypes.c_int8 * 24), ("ar_coeffs_uv", (ctypes.c_int8 * 28) * 2),
+                ("ar_coeff_shift", ctypes.c_uint64), ("grain_scale_shift", ctypes.c_int),
+                ("uv_mult", ctypes.c_int * 2), ("uv_luma_mult", ctypes.c_int * 2), ("uv_offset", ctypes.c_int * 2),
+                ("overlap_flag", ctypes.c_int), ("clip_to_restricted_range", ctypes.c_int)]
+
+
+class FilmGrainBatch(ctypes.Structure):
+    _fields_ = [("in_", Plane * 3), ("out", Plane * 3), ("data", FilmGrainData), ("layout", ctypes.c_int32),
+                ("bitdepth_max", ctypes.c_int32), ("is_id", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("scratch", ctypes.c_void_p)]
+
+
+GRAIN_W, GRAIN_H = 82, 73
+GRAIN_SCRATCH_BYTES = 3 * GRAIN_H * GRAIN_W * 2 + 3 * 4096
+
 _LIB = None
 
 
@@ -192,6 +213,10 @@ def load_lib():
             f.argtypes = [ctypes.POINTER(FrameBatch), ctypes.POINTER(IntraEdgeBatch),
                           ctypes.POINTER(IntraSchedule), ctypes.c_void_p]
             f.restype = ctypes.c_int
+        for bpc in (8, 16):
+            f = getattr(L, f"dav1d_gpu_apply_grain_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(FilmGrainBatch), ctypes.c_void_p]
+            f.restype = ctypes.c_int
         L.dav1d_gpu_recorder_new.argtypes = [ctypes.c_int] * 5
         L.dav1d_gpu_recorder_new.restype = ctypes.c_void_p
         L.dav1d_gpu_recorder_free.argtypes = [ctypes.c_void_p]
@@ -231,4 +256,5 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_intra_workspace_bytes",
     "dav1d_gpu_recorder_new", "dav1d_gpu_recorder_free", "dav1d_gpu_rec_block", "dav1d_gpu_rec_residual",
     "dav1d_gpu_recorder_flush", "dav1d_gpu_recorder_stats",
+    "dav1d_gpu_apply_grain_8bpc", "dav1d_gpu_apply_grain_16bpc",
 ]

@@ -664,6 +664,55 @@ int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane dst[3],
 /* Levels and units of the last flush (diagnostics). */
 int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_units, int32_t *n_levels);
 
+/* ---- film grain ----------------------------------------
+ * bitfn(dav1d_apply_grain) (src/fg_apply_tmpl.c:222-241) on the device:
+ * prep (generate_grain_y / generate_grain_uv, src/filmgrain_tmpl.c:51-144;
+ * generate_scaling, fg_apply_tmpl.c:41-97; the copies of planes without
+ * grain) and every 32-row strip of fgy_32x32xn / fguv_32x32xn
+ * (filmgrain_tmpl.c:166-420) in two launches. */
+typedef struct Dav1dGpuFilmGrainData {   /* layout of Dav1dFilmGrainData,
+                                            include/dav1d/headers.h:319-337 */
+    unsigned seed;
+    int num_y_points;
+    uint8_t y_points[14][2];            /* value, scaling */
+    int chroma_scaling_from_luma;
+    int num_uv_points[2];
+    uint8_t uv_points[2][10][2];
+    int scaling_shift;
+    int ar_coeff_lag;
+    int8_t ar_coeffs_y[24];
+    int8_t ar_coeffs_uv[2][25 + 3];
+    uint64_t ar_coeff_shift;
+    int grain_scale_shift;
+    int uv_mult[2];
+    int uv_luma_mult[2];
+    int uv_offset[2];
+    int overlap_flag;
+    int clip_to_restricted_range;
+} Dav1dGpuFilmGrainData;
+
+#define DGPU_GRAIN_W 82
+#define DGPU_GRAIN_H 73
+/* scratch: int16 grain LUTs [3][73][82], then uint8 scaling LUTs [3][4096] */
+#define DGPU_GRAIN_SCRATCH_BYTES (3 * DGPU_GRAIN_H * DGPU_GRAIN_W * 2 + 3 * 4096)
+
+typedef struct Dav1dGpuFilmGrainBatch {
+    Dav1dGpuPlane in[3];     /* device: the reconstructed picture (read)      */
+    Dav1dGpuPlane out[3];    /* device: the output picture (planes without
+                                grain are copied), distinct from `in`        */
+    Dav1dGpuFilmGrainData data;
+    int32_t layout;          /* DAV1D_PIXEL_LAYOUT_*: 1 I420, 2 I422, 3 I444  */
+    int32_t bitdepth_max;
+    int32_t is_id;           /* seq_hdr->mtrx == DAV1D_MC_IDENTITY           */
+    int32_t pad_;
+    void   *scratch;         /* device, DGPU_GRAIN_SCRATCH_BYTES              */
+} Dav1dGpuFilmGrainBatch;
+
+/* in[0].w / h give the picture size.  Errors: -1 NULL / bad layout /
+ * missing scratch, -3 launch failure. */
+int dav1d_gpu_apply_grain_8bpc(const Dav1dGpuFilmGrainBatch *b, void *stream);
+int dav1d_gpu_apply_grain_16bpc(const Dav1dGpuFilmGrainBatch *b, void *stream);
+
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split
  * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).

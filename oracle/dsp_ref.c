@@ -1902,3 +1902,223 @@ int SFX(oracle_recon_intra_frame)(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIn
     }
     return 0;
 }
+
+/* ============================================================ film grain */
+/* SURVEY 8(f) row 4.  Restated from src/filmgrain_tmpl.c and
+ * src/fg_apply_tmpl.c; grain LUTs held as int16 at both bitdepths (the
+ * reference's `entry` is int8 at 8 bpc; every value fits). */
+#define FG_W DGPU_GRAIN_W
+#define FG_H DGPU_GRAIN_H
+
+/* get_random_number, filmgrain_tmpl.c:38-44: 16-bit LFSR, taps 0,1,3,12 */
+static int fg_rand(int bits, unsigned *state)
+{
+    const unsigned r = *state;
+    const unsigned bit = (r ^ (r >> 1) ^ (r >> 3) ^ (r >> 12)) & 1;
+    *state = (r >> 1) | (bit << 15);
+    return (int)((*state >> (16 - bits)) & ((1u << bits) - 1));
+}
+
+static int fg_round2(int x, int shift) { return shift ? (x + (1 << (shift - 1))) >> shift : x; }
+
+/* generate_grain_y_c / generate_grain_uv_c, filmgrain_tmpl.c:51-144.
+ * uv < 0: luma; otherwise chroma plane uv with subsampling sx / sy. */
+static void fg_grain(int16_t buf[FG_H][FG_W], const int16_t luma[FG_H][FG_W], const Dav1dGpuFilmGrainData *d,
+                     int uv, int sx, int sy, int bdmax)
+{
+    const int bd8 = (bdmax == 255 ? 8 : bdmax == 1023 ? 10 : 12) - 8;
+    unsigned seed = d->seed ^ (uv < 0 ? 0 : uv ? 0x49d8 : 0xb524);
+    const int shift = 4 - bd8 + d->grain_scale_shift;
+    const int gmin = -(128 << bd8), gmax = (128 << bd8) - 1;
+    const int cw = uv >= 0 && sx ? 44 : FG_W, ch = uv >= 0 && sy ? 38 : FG_H;
+    for (int y = 0; y < ch; y++)
+        for (int x = 0; x < cw; x++)
+            buf[y][x] = (int16_t)fg_round2(dspt_gaussian[fg_rand(11, &seed)], shift);
+    const int lag = d->ar_coeff_lag;
+    for (int y = 3; y < ch; y++)
+        for (int x = 3; x < cw - 3; x++) {
+            const int8_t *c = uv < 0 ? d->ar_coeffs_y : d->ar_coeffs_uv[uv];
+            int sum = 0, k = 0;
+            for (int dy = -lag; dy <= 0; dy++)
+                for (int dx = -lag; dx <= lag; dx++) {
+                    if (!dx && !dy) {   /* chroma: the co-located luma grain */
+                        if (uv >= 0 && d->num_y_points) {
+                            const int lx = ((x - 3) << sx) + 3, ly = ((y - 3) << sy) + 3;
+                            int l = 0;
+                            for (int i = 0; i <= sy; i++)
+                                for (int j = 0; j <= sx; j++) l += luma[ly + i][lx + j];
+                            sum += fg_round2(l, sx + sy) * c[k];
+                        }
+                        goto done;
+                    }
+                    sum += c[k++] * buf[y + dy][x + dx];
+                }
+        done:;
+            const int g = buf[y][x] + fg_round2(sum, (int)d->ar_coeff_shift);
+            buf[y][x] = (int16_t)(g < gmin ? gmin : g > gmax ? gmax : g);
+        }
+}
+
+/* generate_scaling, fg_apply_tmpl.c:41-97 */
+static void fg_scaling(int bitdepth, const uint8_t pts[][2], int num, uint8_t *sc)
+{
+    const int shx = bitdepth - 8, size = 1 << bitdepth;
+    if (!num) {
+        memset(sc, 0, (size_t)size);
+        return;
+    }
+    memset(sc, pts[0][1], (size_t)(pts[0][0] << shx));
+    for (int i = 0; i < num - 1; i++) {
+        const int bx = pts[i][0], by = pts[i][1], dx = pts[i + 1][0] - bx, dy = pts[i + 1][1] - by;
+        const int delta = dy * ((0x10000 + (dx >> 1)) / dx);
+        for (int x = 0, dd = 0x8000; x < dx; x++, dd += delta) sc[(bx + x) << shx] = (uint8_t)(by + (dd >> 16));
+    }
+    const int n = pts[num - 1][0] << shx;
+    memset(sc + n, pts[num - 1][1], (size_t)(size - n));
+    if (shx) {
+        const int pad = 1 << shx, rnd = pad >> 1;
+        for (int i = 0; i < num - 1; i++) {
+            const int bx = pts[i][0] << shx, dx = (pts[i + 1][0] << shx) - bx;
+            for (int x = 0; x < dx; x += pad) {
+                const int range = sc[bx + x + pad] - sc[bx + x];
+                for (int k = 1, r = rnd; k < pad; k++) {
+                    r += range;
+                    sc[bx + x + k] = (uint8_t)(sc[bx + x] + (r >> shx));
+                }
+            }
+        }
+    }
+}
+
+/* The grain LUTs [3][73][82] (int16) and scaling LUTs [3][4096] the
+ * reference's dav1d_prep_grain builds (fg_apply_tmpl.c:100-130). */
+int SFX(oracle_prep_grain)(const Dav1dGpuFilmGrainData *d, int layout, int bdmax, int16_t *grain, uint8_t *scaling)
+{
+    const int bitdepth = BITDEPTH == 8 ? 8 : bdmax == 1023 ? 10 : 12;
+    const int sx = layout != 3, sy = layout == 1;
+    int16_t (*g)[FG_H][FG_W] = (int16_t (*)[FG_H][FG_W])grain;
+    memset(grain, 0, sizeof(int16_t) * 3 * FG_H * FG_W);
+    memset(scaling, 0, 3 * 4096);
+    fg_grain(g[0], NULL, d, -1, 0, 0, BITDEPTH == 8 ? 255 : bdmax);
+    if (d->num_uv_points[0] || d->chroma_scaling_from_luma) fg_grain(g[1], g[0], d, 0, sx, sy, BITDEPTH == 8 ? 255 : bdmax);
+    if (d->num_uv_points[1] || d->chroma_scaling_from_luma) fg_grain(g[2], g[0], d, 1, sx, sy, BITDEPTH == 8 ? 255 : bdmax);
+    if (d->num_y_points || d->chroma_scaling_from_luma) fg_scaling(bitdepth, d->y_points, d->num_y_points, scaling);
+    if (d->num_uv_points[0]) fg_scaling(bitdepth, d->uv_points[0], d->num_uv_points[0], scaling + 4096);
+    if (d->num_uv_points[1]) fg_scaling(bitdepth, d->uv_points[1], d->num_uv_points[1], scaling + 2 * 4096);
+    return 0;
+}
+
+/* sample_lut, filmgrain_tmpl.c:155-164 */
+static int fg_sample(const int16_t g[FG_H][FG_W], const int off[2][2], int sx, int sy, int bx, int by, int x, int y)
+{
+    const int rv = off[bx][by];
+    const int ox = 3 + (2 >> sx) * (3 + (rv >> 4)), oy = 3 + (2 >> sy) * (3 + (rv & 15));
+    return g[oy + y + (32 >> sy) * by][ox + x + (32 >> sx) * bx];
+}
+
+static int fg_blend(int old, int cur, int w0, int w1, int gmin, int gmax)
+{
+    const int v = fg_round2(old * w0 + cur * w1, 5);
+    return v < gmin ? gmin : v > gmax ? gmax : v;
+}
+
+/* One 32-row strip of one plane: fgy_32x32xn_c (pl 0) / fguv_32x32xn_c
+ * (filmgrain_tmpl.c:166-420), with the odd-width luma padding of
+ * fg_apply_tmpl.c:176-183 read as a clamp. */
+static void fg_strip(const Dav1dGpuFilmGrainBatch *b, const int16_t g[FG_H][FG_W], const uint8_t *sc, int pl,
+                     int row, int sx, int sy)
+{
+    const Dav1dGpuFilmGrainData *d = &b->data;
+    const int bdmax = BITDEPTH == 8 ? 255 : b->bitdepth_max;
+    const int bd8 = (bdmax == 255 ? 8 : bdmax == 1023 ? 10 : 12) - 8;
+    const int gmin = -(128 << bd8), gmax = (128 << bd8) - 1;
+    const int W = b->in[0].w, H = b->in[0].h;
+    const int pw = pl ? (W + sx) >> sx : W;
+    const int bh = pl ? (mini(H - row * 32, 32) + sy) >> sy : mini(H - row * 32, 32);
+    const int ssx = pl ? sx : 0, ssy = pl ? sy : 0;
+    int vmin = 0, vmax = bdmax;
+    if (d->clip_to_restricted_range) {
+        vmin = 16 << bd8;
+        vmax = (pl && !b->is_id ? 240 : 235) << bd8;
+    }
+    const ptrdiff_t is = PX(b->in[pl].stride), os = PX(b->out[pl].stride), ls = PX(b->in[0].stride);
+    const pixel *src = (const pixel *)b->in[pl].data + (ptrdiff_t)row * (32 >> ssy) * is;
+    pixel *dst = (pixel *)b->out[pl].data + (ptrdiff_t)row * (32 >> ssy) * os;
+    const pixel *luma = (const pixel *)b->in[0].data + (ptrdiff_t)row * 32 * ls;
+    const int rows = 1 + (d->overlap_flag && row > 0);
+    unsigned seed[2];
+    for (int i = 0; i < rows; i++) {
+        seed[i] = d->seed;
+        seed[i] ^= (unsigned)((((row - i) * 37 + 178) & 0xFF) << 8);
+        seed[i] ^= (unsigned)(((row - i) * 173 + 105) & 0xFF);
+    }
+    static const int wl[2][2] = { { 27, 17 }, { 17, 27 } };
+    static const int wc[2][2][2] = { { { 27, 17 }, { 17, 27 } }, { { 23, 22 }, { 0, 0 } } };
+    int off[2][2] = { { 0, 0 }, { 0, 0 } };
+    const int step = 32 >> ssx;
+    for (int bx = 0; bx < pw; bx += step) {
+        const int bw = mini(step, pw - bx);
+        if (d->overlap_flag && bx)
+            for (int i = 0; i < rows; i++) off[1][i] = off[0][i];
+        for (int i = 0; i < rows; i++) off[0][i] = fg_rand(8, &seed[i]);
+        const int ys = d->overlap_flag && row ? mini(2 >> ssy, bh) : 0;
+        const int xs = d->overlap_flag && bx ? mini(2 >> ssx, bw) : 0;
+        for (int y = 0; y < bh; y++)
+            for (int x = 0; x < bw; x++) {
+                int gr = fg_sample(g, (const int (*)[2])off, ssx, ssy, 0, 0, x, y);
+                const int (*wx)[2] = pl ? wc[ssx] : wl, (*wy)[2] = pl ? wc[ssy] : wl;
+                if (x < xs) gr = fg_blend(fg_sample(g, (const int (*)[2])off, ssx, ssy, 1, 0, x, y), gr, wx[x][0], wx[x][1], gmin, gmax);
+                if (y < ys) {
+                    int top = fg_sample(g, (const int (*)[2])off, ssx, ssy, 0, 1, x, y);
+                    if (x < xs) top = fg_blend(fg_sample(g, (const int (*)[2])off, ssx, ssy, 1, 1, x, y), top, wx[x][0], wx[x][1], gmin, gmax);
+                    gr = fg_blend(top, gr, wy[y][0], wy[y][1], gmin, gmax);
+                }
+                const int s = src[(ptrdiff_t)y * is + bx + x];
+                int val = s;
+                if (pl) {
+                    const int lx = (bx + x) << ssx, ly = y << ssy;
+                    int avg = luma[(ptrdiff_t)ly * ls + mini(lx, W - 1)];
+                    if (ssx) avg = (avg + luma[(ptrdiff_t)ly * ls + mini(lx + 1, W - 1)] + 1) >> 1;
+                    val = avg;
+                    if (!d->chroma_scaling_from_luma) {
+                        const int comb = avg * d->uv_luma_mult[pl - 1] + s * d->uv_mult[pl - 1];
+                        val = clampi((comb >> 6) + d->uv_offset[pl - 1] * (1 << bd8), 0, bdmax);
+                    }
+                }
+                const int noise = fg_round2(sc[val] * gr, d->scaling_shift);
+                dst[(ptrdiff_t)y * os + bx + x] = (pixel)clampi(s + noise, vmin, vmax);
+            }
+    }
+}
+
+/* bitfn(dav1d_apply_grain) (fg_apply_tmpl.c:222-241) over host planes. */
+int SFX(oracle_apply_grain)(const Dav1dGpuFilmGrainBatch *b)
+{
+    const Dav1dGpuFilmGrainData *d = &b->data;
+    const int bdmax = BITDEPTH == 8 ? 255 : b->bitdepth_max;
+    if (b->layout < 1 || b->layout > 3) return -1;
+    const int sx = b->layout != 3, sy = b->layout == 1;
+    static int16_t grain[3][FG_H][FG_W];
+    static uint8_t scaling[3][4096];
+    SFX(oracle_prep_grain)(d, b->layout, bdmax, &grain[0][0][0], &scaling[0][0]);
+    const int W = b->in[0].w, H = b->in[0].h;
+    const int cw = (W + sx) >> sx, chh = (H + sy) >> sy;
+    /* the planes without grain are copied (fg_apply_tmpl.c:132-160) */
+    for (int pl = 0; pl < 3; pl++) {
+        const int grained = pl ? (d->chroma_scaling_from_luma || d->num_uv_points[pl - 1]) : d->num_y_points;
+        if (grained) continue;
+        const int pw = pl ? cw : W, ph = pl ? chh : H;
+        for (int y = 0; y < ph; y++)
+            memcpy((pixel *)b->out[pl].data + (ptrdiff_t)y * PX(b->out[pl].stride),
+                   (const pixel *)b->in[pl].data + (ptrdiff_t)y * PX(b->in[pl].stride), (size_t)pw * sizeof(pixel));
+    }
+    const int rows = (H + 31) / 32;
+    for (int row = 0; row < rows; row++) {
+        if (d->num_y_points) fg_strip(b, grain[0], scaling[0], 0, row, sx, sy);
+        for (int pl = 1; pl < 3; pl++) {
+            if (d->chroma_scaling_from_luma) fg_strip(b, grain[pl], scaling[0], pl, row, sx, sy);
+            else if (d->num_uv_points[pl - 1]) fg_strip(b, grain[pl], scaling[pl], pl, row, sx, sy);
+        }
+    }
+    return 0;
+}

@@ -24,4 +24,8 @@ int oracle_recon_intra_frame_8bpc(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIn
 int oracle_recon_intra_frame_16bpc(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraEdgeBatch *eb,
                                    const int32_t *steps, int n_steps, const int32_t *unit_rec,
                                    const Dav1dGpuEdgeBackup *runs);
+int oracle_prep_grain_8bpc(const Dav1dGpuFilmGrainData *d, int layout, int bdmax, int16_t *grain, uint8_t *scaling);
+int oracle_prep_grain_16bpc(const Dav1dGpuFilmGrainData *d, int layout, int bdmax, int16_t *grain, uint8_t *scaling);
+int oracle_apply_grain_8bpc(const Dav1dGpuFilmGrainBatch *b);
+int oracle_apply_grain_16bpc(const Dav1dGpuFilmGrainBatch *b);
 #endif

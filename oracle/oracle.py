@@ -330,3 +330,28 @@ class HostIntraFrame:
             recon(ctypes.byref(self.rb), int(fr.unit_start[lv]), int(fr.unit_start[lv + 1]))
             b0, b1 = int(fr.run_start[lv]), int(fr.run_start[lv + 1])
             backup(ctypes.byref(self.eb), runs.ctypes.data + b0 * run_sz, b1 - b0)
+
+
+def apply_grain(case):
+    """A grain.GrainCase through the oracle's dav1d_apply_grain restatement:
+    returns (output planes, grain LUTs [3][73][82], scaling LUTs [3][4096])."""
+    import dav1d_mirror_amd.grain as grain
+    abi = _abi()
+    L = load()
+    sfx = 8 if case.bpc == 8 else 16
+    ins = [np.ascontiguousarray(a) for a in case.planes]
+    outs = [np.zeros_like(a) for a in ins]
+    b = grain.fill_batch(abi.FilmGrainBatch(), case, [(a.ctypes.data, a.shape[1]) for a in ins],
+                         [(a.ctypes.data, a.shape[1]) for a in outs], None)
+    fn = getattr(L, f"oracle_apply_grain_{sfx}bpc")
+    fn.argtypes = [ctypes.POINTER(abi.FilmGrainBatch)]
+    fn.restype = ctypes.c_int
+    assert fn(ctypes.byref(b)) == 0
+    g = np.zeros((3, abi.GRAIN_H, abi.GRAIN_W), np.int16)
+    sc = np.zeros((3, 4096), np.uint8)
+    prep = getattr(L, f"oracle_prep_grain_{sfx}bpc")
+    prep.argtypes = [ctypes.POINTER(abi.FilmGrainData), ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    prep.restype = ctypes.c_int
+    d = abi.FilmGrainData.from_buffer_copy(case.data)
+    assert prep(ctypes.byref(d), case.layout, case.bitdepth_max, g.ctypes.data, sc.ctypes.data) == 0
+    return outs, g, sc
