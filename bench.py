@@ -236,6 +236,39 @@ def recorder_breakdown(cfg, dev):
             "bit_exact_vs_oracle": all(bool(np.array_equal(g, o)) for g, o in zip(got, ho.dst))}
 
 
+def grain_breakdown(cfg, dev, steps):
+    """film grain (dav1d_gpu_apply_grain_*) on a picture
+    of the config's size and bitdepth, lag-3 auto-regression, overlap on,
+    grain on all planes: ms per picture (prep + apply launches) by HIP
+    events, and the oracle's time on one core, bit-exact check."""
+    import torch
+    import dav1d_mirror_amd.grain as grain
+    c = grain.make_grain_case(seed=5, width=cfg.width, height=cfg.height, bpc=cfg.bpc,
+                              bitdepth_max=cfg.bitdepth_max, lag=3, num_y=8, csfl=False, num_uv=(6, 6),
+                              overlap=True)
+    g = grain.DeviceGrain(c, dev)
+    s = torch.cuda.current_stream(dev)
+    for _ in range(3):
+        g.launch(s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = max(steps, 10)
+    e0.record(s)
+    for _ in range(n):
+        g.launch(s)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / n
+    t0 = time.perf_counter()
+    outs, _, _ = ge.load_oracle().apply_grain(c)
+    cpu = time.perf_counter() - t0
+    px = sum(w * h for w, h in c.plane_wh)
+    bpp = 1 if cfg.bpc == 8 else 2
+    return {"picture": f"{cfg.width}x{cfg.height} 4:2:0", "ms_per_picture": round(ms, 4),
+            "gpix_s": round(px / ms / 1e6, 2), "picture_io_bytes": 2 * px * bpp,
+            "oracle_1core_ms": round(cpu * 1e3, 1),
+            "bit_exact_vs_oracle": all(bool(np.array_equal(a, b)) for a, b in zip(g.outputs_host(), outs))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -250,6 +283,7 @@ def main():
     ap.add_argument("--no-tiles", action="store_true", help="skip the tile-batch measurement (N=1)")
     ap.add_argument("--no-intra", action="store_true", help="skip the intra-wavefront measurement (N=1)")
     ap.add_argument("--no-recorder", action="store_true", help="skip the batch-recorder measurement (N=1)")
+    ap.add_argument("--no-grain", action="store_true", help="skip the film-grain measurement (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -375,6 +409,8 @@ def main():
             out["intra_wavefront"] = intra_breakdown(cfg, dev, stream, args.steps)
         if not args.no_recorder and world == 1 and c.get("kind") == "full":
             out["recorder"] = recorder_breakdown(cfg, dev)
+        if not args.no_grain and world == 1:
+            out["film_grain"] = grain_breakdown(cfg, dev, args.steps)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
         print(json.dumps(out), flush=True)

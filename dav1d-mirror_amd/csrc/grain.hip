@@ -22,6 +22,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <array>
+#include <utility>
+
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
 
@@ -68,6 +71,33 @@ __constant__ uint16_t c_jump96[16] = {
     kJump96.c[6], kJump96.c[7], kJump96.c[8],  kJump96.c[9],  kJump96.c[10], kJump96.c[11],
     kJump96.c[12], kJump96.c[13], kJump96.c[14], kJump96.c[15]};
 
+// M^k for k = 0..255 and M^256: a block column's offset is the draw after
+// c + 1 steps of its row seed, computed without stepping
+struct JumpTab { Lin16 m[257]; };
+constexpr JumpTab make_jumps() {
+    JumpTab t{};
+    Lin16 p{};
+    for (int i = 0; i < 16; i++) p.c[i] = (uint16_t)(1u << i);
+    const Lin16 st = lin_step();
+    for (int k = 0; k <= 256; k++) {
+        t.m[k] = p;
+        p = lin_compose(st, p);
+    }
+    return t;
+}
+constexpr JumpTab kJumps = make_jumps();
+template <size_t... I> constexpr auto flat_jumps(std::index_sequence<I...>) {
+    return std::array<uint16_t, sizeof...(I)>{kJumps.m[I / 16].c[I % 16]...};
+}
+__constant__ std::array<uint16_t, 257 * 16> c_jumps = flat_jumps(std::make_index_sequence<257 * 16>());
+
+__device__ __forceinline__ unsigned jump_apply(int k, unsigned s) {
+    unsigned r = 0;
+#pragma unroll
+    for (int b = 0; b < 16; b++) r ^= ((s >> b) & 1) ? c_jumps[k * 16 + b] : 0u;
+    return r;
+}
+
 __device__ __forceinline__ int fg_rand(int bits, unsigned &s) {
     const unsigned bit = (s ^ (s >> 1) ^ (s >> 3) ^ (s >> 12)) & 1;
     s = (s >> 1) | (bit << 15);
@@ -106,8 +136,76 @@ __device__ int scaling_entry(const uint8_t (*pts)[2], int num, int shx, int idx)
     return (b0 + (((pad >> 1) + k * range) >> shx)) & 0xff;
 }
 
+// One plane's auto-regressive filter (filmgrain_tmpl.c:70-88 / 110-142) by
+// one wave: pixels with equal x + 4y are independent (lag <= 3), so the
+// wave sweeps those anti-diagonals, a pixel per lane, coefficients in
+// registers and the taps unrolled.
+// luma_done: the last luma anti-diagonal finished (written by the luma
+// wave, read by the chroma waves, which start as soon as the luma grain
+// they read is final instead of after the whole luma sweep)
+template <int LAG>
+__device__ void ar_sweep(int16_t (*g)[kGW], const int16_t (*gy)[kGW], const int8_t *cf_, int p, int cw, int ch,
+                         int sx, int sy, int num_y, int shift, int gmin, int gmax, int lane, int *luma_done) {
+    constexpr int NT = LAG * (2 * LAG + 1) + LAG;   // taps before the current pixel
+    int cf[NT + 1];
+#pragma unroll
+    for (int k = 0; k <= NT; k++) cf[k] = cf_[k];
+    const bool luma_term = p && num_y;
+    const int tmax = (cw - 4) + 4 * (ch - 1);
+    const int tmax_l = (kGW - 4) + 4 * (kGH - 1);
+    for (int t = 15; t <= tmax; t++) {
+        const int ylo = max(3, (t - (cw - 4) + 3) >> 2), yhi = min(ch - 1, (t - 3) >> 2);
+        if (luma_term) {   // wait for the luma grain this step reads
+            auto need = [&](int yy) {   // the highest luma diagonal pixel (yy, t - 4yy) reads
+                const int xx = t - 4 * yy, lx = ((xx - 3) << sx) + 3 + sx, ly = ((yy - 3) << sy) + 3 + sy;
+                return lx + 4 * ly;
+            };
+            const int req = min(max(need(ylo), need(yhi)), tmax_l);
+            if (lane == 0)
+                for (int it = 0; it < (1 << 22); it++) {
+                    if (__hip_atomic_load(luma_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= req) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        }
+        const int y = ylo + lane, x = t - 4 * y;
+        if (y <= yhi && x >= 3 && x < cw - 3) {
+            int sum = 0, k = 0;
+#pragma unroll
+            for (int dy = -LAG; dy <= 0; dy++)
+#pragma unroll
+                for (int dx = -LAG; dx <= LAG; dx++) {
+                    if (dy == 0 && dx >= 0) continue;
+                    sum += cf[k++] * g[y + dy][x + dx];
+                }
+            if (luma_term) {   // the co-located luma grain (:115-128)
+                const int lx = ((x - 3) << sx) + 3, ly = ((y - 3) << sy) + 3;
+                int l = gy[ly][lx];
+                if (sx) l += gy[ly][lx + 1];
+                if (sy) l += gy[ly + 1][lx] + (sx ? gy[ly + 1][lx + 1] : 0);
+                sum += rnd2(l, sx + sy) * cf[NT];
+            }
+            const int v = g[y][x] + rnd2(sum, shift);
+            g[y][x] = (int16_t)min(max(v, gmin), gmax);
+        }
+        if (p == 0) {   // publish the finished diagonal to the chroma waves
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) __hip_atomic_store(luma_done, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (p == 0 && lane == 0) __hip_atomic_store(luma_done, 1 << 30, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __global__ __launch_bounds__(256) void k_grain_prep(GrainArgs a) {
     __shared__ int16_t g[3][kGH][kGW];
+    __shared__ int luma_done;
+    if (threadIdx.x == 0) luma_done = 0;
     const Dav1dGpuFilmGrainData &d = a.d;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int bd8 = bd8_of(a.bdmax);
@@ -143,40 +241,15 @@ __global__ __launch_bounds__(256) void k_grain_prep(GrainArgs a) {
     auto ar = [&](int p) {
         const int cw = p && sx ? 44 : kGW, ch = p && sy ? 38 : kGH;
         const int8_t *cf = p == 0 ? d.ar_coeffs_y : d.ar_coeffs_uv[p - 1];
-        const int tmax = (cw - 4) + 4 * (ch - 1);
-        for (int t = 3 + 12; t <= tmax; t++) {
-            // pixel y = 3 + lane + y0 with x = t - 4y in [3, cw - 3)
-            const int ylo = max(3, (t - (cw - 4) + 3) / 4), yhi = min(ch - 1, (t - 3) / 4);
-            for (int y = ylo + lane; y <= yhi; y += 64) {
-                const int x = t - 4 * y;
-                if (x < 3 || x >= cw - 3) continue;
-                int sum = 0, k = 0;
-                for (int dy = -lag; dy <= 0; dy++)
-                    for (int dx = -lag; dx <= lag; dx++) {
-                        if (!dx && !dy) {
-                            if (p && d.num_y_points) {
-                                const int lx = ((x - 3) << sx) + 3, ly = ((y - 3) << sy) + 3;
-                                int l = 0;
-                                for (int i = 0; i <= sy; i++)
-                                    for (int j = 0; j <= sx; j++) l += g[0][ly + i][lx + j];
-                                sum += rnd2(l, sx + sy) * cf[k];
-                            }
-                            dy = 1;   // leave both loops
-                            break;
-                        }
-                        sum += cf[k++] * g[p][y + dy][x + dx];
-                    }
-                const int v = g[p][y][x] + rnd2(sum, (int)d.ar_coeff_shift);
-                g[p][y][x] = (int16_t)min(max(v, gmin), gmax);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        switch (lag) {
+            case 0: ar_sweep<0>(g[p], g[0], cf, p, cw, ch, sx, sy, d.num_y_points, (int)d.ar_coeff_shift, gmin, gmax, lane, &luma_done); break;
+            case 1: ar_sweep<1>(g[p], g[0], cf, p, cw, ch, sx, sy, d.num_y_points, (int)d.ar_coeff_shift, gmin, gmax, lane, &luma_done); break;
+            case 2: ar_sweep<2>(g[p], g[0], cf, p, cw, ch, sx, sy, d.num_y_points, (int)d.ar_coeff_shift, gmin, gmax, lane, &luma_done); break;
+            default: ar_sweep<3>(g[p], g[0], cf, p, cw, ch, sx, sy, d.num_y_points, (int)d.ar_coeff_shift, gmin, gmax, lane, &luma_done); break;
         }
     };
-    if (wave == 0) ar(0);
-    __syncthreads();
-    if ((wave == 1 || wave == 2) && need[wave]) ar(wave);
+    if (wave == 0) ar(0);   // the chroma waves follow the luma sweep's front
+    else if ((wave == 1 || wave == 2) && need[wave]) ar(wave);
     __syncthreads();
     // 3. out: grain LUTs and scaling LUTs
     for (int i = threadIdx.x; i < 3 * kGH * kGW; i += 256) a.grain[i] = (&g[0][0][0])[i];
@@ -205,97 +278,141 @@ template <int BPC> struct ApplyArgs {
     const uint8_t *scaling;
 };
 
-// the row seeds' offsets for block column c (the c+1-th 8-bit draw)
-__device__ __forceinline__ int fg_offset(const Dav1dGpuFilmGrainData &d, int row, int c) {
-    unsigned s = d.seed;
+// the row seed's offset for block column c: the (c+1)-th 8-bit draw
+// (fgy_32x32xn, filmgrain_tmpl.c:187-205), by jump-ahead
+__device__ __forceinline__ int fg_offset(unsigned seed, int row, int c) {
+    unsigned s = seed;
     s ^= (unsigned)((((row) * 37 + 178) & 0xFF) << 8);
     s ^= (unsigned)(((row) * 173 + 105) & 0xFF);
-    int v = 0;
-    for (int i = 0; i <= c; i++) v = fg_rand(8, s);
-    return v;
+    int k = c + 1;
+    while (k > 256) {
+        s = jump_apply(256, s);
+        k -= 256;
+    }
+    s = jump_apply(k, s);
+    return (int)((s >> 8) & 0xff);
+}
+
+// One plane of one 32x32-luma block: NP pixels per thread.  Every load of
+// the thread's pixels (picture, luma, grain LUT) is issued before the
+// dependent scaling lookups (LDS), so a thread's pixels overlap their
+// memory latency instead of running one after the other.
+template <int BPC, int NP>
+__device__ __forceinline__ void grain_plane(const ApplyArgs<BPC> &a, const int (&off)[2][2], const uint8_t *sc, int pl,
+                                            int c, int row) {
+    using P = typename Px<BPC>::pixel;
+    const Dav1dGpuFilmGrainData &d = a.d;
+    const int bd8 = bd8_of(a.bdmax);
+    const int gmin = -(128 << bd8), gmax = (128 << bd8) - 1;
+    const int sx = a.layout != 3, sy = a.layout == 1;
+    const int ssx = pl ? sx : 0, ssy = pl ? sy : 0;
+    const int pw = pl ? (a.w + sx) >> sx : a.w;
+    const int bw0 = 32 >> ssx, bh0 = 32 >> ssy, lw = 5 - ssx;
+    const int x0 = c * bw0, y0 = row * bh0;
+    const int bw = min(bw0, pw - x0);
+    const int lrows = min(32, a.h - row * 32);
+    const int bh = pl ? (lrows + ssy) >> ssy : lrows;
+    const int is = pl == 0 ? a.is[0] : pl == 1 ? a.is[1] : a.is[2];
+    const int os = pl == 0 ? a.os[0] : pl == 1 ? a.os[1] : a.os[2];
+    const P *src = (pl == 0 ? a.in[0] : pl == 1 ? a.in[1] : a.in[2]) + (size_t)y0 * is + x0;
+    P *dst = (pl == 0 ? a.out[0] : pl == 1 ? a.out[1] : a.out[2]) + (size_t)y0 * os + x0;
+    const bool grained = pl ? (d.chroma_scaling_from_luma || d.num_uv_points[pl - 1]) : d.num_y_points;
+    if (!grained) {   // fg_apply_tmpl.c:132-160: the plane is copied
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            const int i = threadIdx.x + 256 * k, y = i >> lw, x = i & (bw0 - 1);
+            if (x < bw && y < bh) dst[(size_t)y * os + x] = src[(size_t)y * is + x];
+        }
+        return;
+    }
+    const int16_t *g = a.grain + pl * kGH * kGW;
+    int vmin = 0, vmax = a.bdmax;
+    if (d.clip_to_restricted_range) {
+        vmin = 16 << bd8;
+        vmax = (pl && !a.is_id ? 240 : 235) << bd8;
+    }
+    const int ys = d.overlap_flag && row ? min(2 >> ssy, bh) : 0;
+    const int xs = d.overlap_flag && c ? min(2 >> ssx, bw) : 0;
+    // LUT origins of the four (column, row) offset blocks (sample_lut, :155-164)
+    int org[2][2];
+#pragma unroll
+    for (int bx = 0; bx < 2; bx++)
+#pragma unroll
+        for (int by = 0; by < 2; by++) {
+            const int rv = off[bx][by];
+            org[bx][by] = (3 + (2 >> ssy) * (3 + (rv & 15)) + bh0 * by) * kGW + 3 + (2 >> ssx) * (3 + (rv >> 4)) + bw0 * bx;
+        }
+    auto wgt = [&](int ss, int i, int k) -> int { return ss ? (k ? 22 : 23) : ((i == 0) == (k == 0) ? 27 : 17); };
+    auto blend = [&](int old, int cur, int w0, int w1) { return min(max(rnd2(old * w0 + cur * w1, 5), gmin), gmax); };
+    const P *luma = a.in[0] + (size_t)(row * 32) * a.is[0];
+    int sv[NP], gv[NP], lv[NP];
+    bool ok[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) {   // loads
+        const int i = threadIdx.x + 256 * k, y = i >> lw, x = i & (bw0 - 1);
+        ok[k] = x < bw && y < bh;
+        sv[k] = ok[k] ? (int)src[(size_t)y * is + x] : 0;
+        int gr = g[org[0][0] + y * kGW + x];
+        if (x < xs) gr = blend(g[org[1][0] + y * kGW + x], gr, wgt(ssx, x, 0), wgt(ssx, x, 1));
+        if (y < ys) {
+            int top = g[org[0][1] + y * kGW + x];
+            if (x < xs) top = blend(g[org[1][1] + y * kGW + x], top, wgt(ssx, x, 0), wgt(ssx, x, 1));
+            gr = blend(top, gr, wgt(ssy, y, 0), wgt(ssy, y, 1));
+        }
+        gv[k] = gr;
+        lv[k] = 0;
+        if (pl && ok[k]) {
+            const int lx = (x0 + x) << ssx, ly = y << ssy;
+            int avg = luma[(size_t)ly * a.is[0] + min(lx, a.w - 1)];
+            if (ssx) avg = (avg + luma[(size_t)ly * a.is[0] + min(lx + 1, a.w - 1)] + 1) >> 1;
+            lv[k] = avg;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NP; k++) {   // scaling (LDS), noise, store
+        if (!ok[k]) continue;
+        const int i = threadIdx.x + 256 * k, y = i >> lw, x = i & (bw0 - 1);
+        int val = sv[k];
+        if (pl) {
+            val = lv[k];
+            if (!d.chroma_scaling_from_luma) {
+                const int comb = lv[k] * d.uv_luma_mult[pl - 1] + sv[k] * d.uv_mult[pl - 1];
+                val = min(max((comb >> 6) + d.uv_offset[pl - 1] * (1 << bd8), 0), a.bdmax);
+            }
+        }
+        const int noise = rnd2(sc[val] * gv[k], d.scaling_shift);
+        dst[(size_t)y * os + x] = (P)min(max(sv[k] + noise, vmin), vmax);
+    }
 }
 
 template <int BPC>
 __global__ __launch_bounds__(256) void k_grain_apply(ApplyArgs<BPC> a) {
-    using P = typename Px<BPC>::pixel;
+    constexpr int SC = BPC == 8 ? 256 : 4096;
+    __shared__ int off[2][2];   // [column: this, previous][row: this, previous]
+    __shared__ uint8_t sc[3][SC];
     const Dav1dGpuFilmGrainData &d = a.d;
     const int c = blockIdx.x, row = blockIdx.y;
-    __shared__ int off[2][2];   // [column: this, previous][row: this, previous]
     if (threadIdx.x < 4) {
         const int bc = threadIdx.x & 1, br = threadIdx.x >> 1;
         const bool used = (!bc || (d.overlap_flag && c)) && (!br || (d.overlap_flag && row));
-        off[bc][br] = used ? fg_offset(d, row - br, c - bc) : 0;
+        off[bc][br] = used ? fg_offset(d.seed, row - br, c - bc) : 0;
     }
+    for (int i = threadIdx.x * 4; i < 3 * SC; i += 1024)   // the scaling LUTs (4 KB apart in the scratch)
+        *reinterpret_cast<uint32_t *>(&sc[0][0] + i) =
+            *reinterpret_cast<const uint32_t *>(a.scaling + (i / SC) * 4096 + (i % SC));
     __syncthreads();
-    const int bd8 = bd8_of(a.bdmax);
-    const int gmin = -(128 << bd8), gmax = (128 << bd8) - 1;
-    const int sx = a.layout != 3, sy = a.layout == 1;
-    for (int pl = 0; pl < 3; pl++) {
-        const int ssx = pl ? sx : 0, ssy = pl ? sy : 0;
-        const int pw = pl ? (a.w + sx) >> sx : a.w, ph = pl ? (a.h + sy) >> sy : a.h;
-        const int bw0 = 32 >> ssx, bh0 = 32 >> ssy;
-        const int x0 = c * bw0, y0 = row * bh0;
-        const int bw = min(bw0, pw - x0);
-        // the strip's rows: luma min(32, h - 32 row), chroma (that + ssy) >> ssy
-        const int lrows = min(32, a.h - row * 32);
-        const int bh = pl ? (lrows + ssy) >> ssy : lrows;
-        if (bw <= 0 || bh <= 0) continue;
-        const P *src = a.in[pl] + (size_t)y0 * a.is[pl] + x0;
-        P *dst = a.out[pl] + (size_t)y0 * a.os[pl] + x0;
-        const bool grained = pl ? (d.chroma_scaling_from_luma || d.num_uv_points[pl - 1]) : d.num_y_points;
-        if (!grained) {   // fg_apply_tmpl.c:132-160: the plane is copied
-            for (int i = threadIdx.x; i < bw * bh; i += 256) {
-                const int y = i / bw, x = i % bw;
-                dst[(size_t)y * a.os[pl] + x] = src[(size_t)y * a.is[pl] + x];
-            }
-            continue;
-        }
-        const int16_t *g = a.grain + pl * kGH * kGW;
-        const uint8_t *sc = a.scaling + (pl && !d.chroma_scaling_from_luma ? pl : 0) * 4096;
-        int vmin = 0, vmax = a.bdmax;
-        if (d.clip_to_restricted_range) {
-            vmin = 16 << bd8;
-            vmax = (pl && !a.is_id ? 240 : 235) << bd8;
-        }
-        const int ys = d.overlap_flag && row ? min(2 >> ssy, bh) : 0;
-        const int xs = d.overlap_flag && c ? min(2 >> ssx, bw) : 0;
-        // overlap weights: luma {27,17},{17,27}; chroma subsampled {23,22}
-        auto wgt = [&](int ss, int i, int k) -> int {
-            return ss ? (k ? 22 : 23) : ((i == 0) == (k == 0) ? 27 : 17);
-        };
-        auto sample = [&](int bx, int by, int x, int y) -> int {
-            const int rv = off[bx][by];
-            const int ox = 3 + (2 >> ssx) * (3 + (rv >> 4)), oy = 3 + (2 >> ssy) * (3 + (rv & 15));
-            return g[(oy + y + bh0 * by) * kGW + ox + x + bw0 * bx];
-        };
-        auto blend = [&](int old, int cur, int w0, int w1) {
-            return min(max(rnd2(old * w0 + cur * w1, 5), gmin), gmax);
-        };
-        const P *luma = a.in[0] + (size_t)(row * 32) * a.is[0];
-        for (int i = threadIdx.x; i < bw * bh; i += 256) {
-            const int y = i / bw, x = i % bw;
-            int gr = sample(0, 0, x, y);
-            if (x < xs) gr = blend(sample(1, 0, x, y), gr, wgt(ssx, x, 0), wgt(ssx, x, 1));
-            if (y < ys) {
-                int top = sample(0, 1, x, y);
-                if (x < xs) top = blend(sample(1, 1, x, y), top, wgt(ssx, x, 0), wgt(ssx, x, 1));
-                gr = blend(top, gr, wgt(ssy, y, 0), wgt(ssy, y, 1));
-            }
-            const int s = src[(size_t)y * a.is[pl] + x];
-            int val = s;
-            if (pl) {
-                const int lx = (x0 + x) << ssx, ly = y << ssy;
-                int avg = luma[(size_t)ly * a.is[0] + min(lx, a.w - 1)];
-                if (ssx) avg = (avg + luma[(size_t)ly * a.is[0] + min(lx + 1, a.w - 1)] + 1) >> 1;
-                val = avg;
-                if (!d.chroma_scaling_from_luma) {
-                    const int comb = avg * d.uv_luma_mult[pl - 1] + s * d.uv_mult[pl - 1];
-                    val = min(max((comb >> 6) + d.uv_offset[pl - 1] * (1 << bd8), 0), a.bdmax);
-                }
-            }
-            const int noise = rnd2(sc[val] * gr, d.scaling_shift);
-            dst[(size_t)y * a.os[pl] + x] = (P)min(max(s + noise, vmin), vmax);
-        }
+    int o[2][2] = {{off[0][0], off[0][1]}, {off[1][0], off[1][1]}};
+    const uint8_t *scu = d.chroma_scaling_from_luma ? sc[0] : sc[1], *scv = d.chroma_scaling_from_luma ? sc[0] : sc[2];
+    grain_plane<BPC, 4>(a, o, sc[0], 0, c, row);
+    if (a.layout == 1) {
+        grain_plane<BPC, 1>(a, o, scu, 1, c, row);
+        grain_plane<BPC, 1>(a, o, scv, 2, c, row);
+    } else if (a.layout == 2) {
+        grain_plane<BPC, 2>(a, o, scu, 1, c, row);
+        grain_plane<BPC, 2>(a, o, scv, 2, c, row);
+    } else {
+        grain_plane<BPC, 4>(a, o, scu, 1, c, row);
+        grain_plane<BPC, 4>(a, o, scv, 2, c, row);
     }
 }
 
