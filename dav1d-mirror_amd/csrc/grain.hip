@@ -293,105 +293,137 @@ __device__ __forceinline__ int fg_offset(unsigned seed, int row, int c) {
     return (int)((s >> 8) & 0xff);
 }
 
-// One plane of one 32x32-luma block: NP pixels per thread.  Every load of
-// the thread's pixels (picture, luma, grain LUT) is issued before the
-// dependent scaling lookups (LDS), so a thread's pixels overlap their
-// memory latency instead of running one after the other.
-template <int BPC, int NP>
-__device__ __forceinline__ void grain_plane(const ApplyArgs<BPC> &a, const int (&off)[2][2], const uint8_t *sc, int pl,
-                                            int c, int row) {
+// One plane of one 32x32-luma block, NP pixels per thread, in two phases so
+// a workgroup issues the picture loads of all three planes before its first
+// barrier and the dependent work after: load() reads the pixels (and the
+// co-located luma) or copies a plane without grain; finish() samples the
+// grain LUT with the block's offsets and overlap blends, looks the scaling
+// up in LDS, adds the noise and stores.
+template <int BPC, int NP> struct PlaneJob {
     using P = typename Px<BPC>::pixel;
-    const Dav1dGpuFilmGrainData &d = a.d;
-    const int bd8 = bd8_of(a.bdmax);
-    const int gmin = -(128 << bd8), gmax = (128 << bd8) - 1;
-    const int sx = a.layout != 3, sy = a.layout == 1;
-    const int ssx = pl ? sx : 0, ssy = pl ? sy : 0;
-    const int pw = pl ? (a.w + sx) >> sx : a.w;
-    const int bw0 = 32 >> ssx, bh0 = 32 >> ssy, lw = 5 - ssx;
-    const int x0 = c * bw0, y0 = row * bh0;
-    const int bw = min(bw0, pw - x0);
-    const int lrows = min(32, a.h - row * 32);
-    const int bh = pl ? (lrows + ssy) >> ssy : lrows;
-    const int is = pl == 0 ? a.is[0] : pl == 1 ? a.is[1] : a.is[2];
-    const int os = pl == 0 ? a.os[0] : pl == 1 ? a.os[1] : a.os[2];
-    const P *src = (pl == 0 ? a.in[0] : pl == 1 ? a.in[1] : a.in[2]) + (size_t)y0 * is + x0;
-    P *dst = (pl == 0 ? a.out[0] : pl == 1 ? a.out[1] : a.out[2]) + (size_t)y0 * os + x0;
-    const bool grained = pl ? (d.chroma_scaling_from_luma || d.num_uv_points[pl - 1]) : d.num_y_points;
-    if (!grained) {   // fg_apply_tmpl.c:132-160: the plane is copied
+    int pl, ssx, ssy, bw0, bh0, lw, x0, bw, bh, is, os, c, row;
+    bool grained;
+    const P *src;
+    P *dst;
+    int sv[NP], lv[NP];
+
+    __device__ __forceinline__ void load(const ApplyArgs<BPC> &a, int pl_, int c_, int row_) {
+        const Dav1dGpuFilmGrainData &d = a.d;
+        pl = pl_;
+        c = c_;
+        row = row_;
+        const int sx = a.layout != 3, sy = a.layout == 1;
+        ssx = pl ? sx : 0;
+        ssy = pl ? sy : 0;
+        const int pw = pl ? (a.w + sx) >> sx : a.w;
+        bw0 = 32 >> ssx;
+        bh0 = 32 >> ssy;
+        lw = 5 - ssx;
+        x0 = c * bw0;
+        const int y0 = row * bh0;
+        bw = min(bw0, pw - x0);
+        const int lrows = min(32, a.h - row * 32);
+        bh = pl ? (lrows + ssy) >> ssy : lrows;
+        is = pl == 0 ? a.is[0] : pl == 1 ? a.is[1] : a.is[2];
+        os = pl == 0 ? a.os[0] : pl == 1 ? a.os[1] : a.os[2];
+        src = (pl == 0 ? a.in[0] : pl == 1 ? a.in[1] : a.in[2]) + (size_t)y0 * is + x0;
+        dst = (pl == 0 ? a.out[0] : pl == 1 ? a.out[1] : a.out[2]) + (size_t)y0 * os + x0;
+        grained = pl ? (d.chroma_scaling_from_luma || d.num_uv_points[pl - 1]) : d.num_y_points;
+        const P *luma = a.in[0] + (size_t)(row * 32) * a.is[0];
 #pragma unroll
         for (int k = 0; k < NP; k++) {
             const int i = threadIdx.x + 256 * k, y = i >> lw, x = i & (bw0 - 1);
-            if (x < bw && y < bh) dst[(size_t)y * os + x] = src[(size_t)y * is + x];
-        }
-        return;
-    }
-    const int16_t *g = a.grain + pl * kGH * kGW;
-    int vmin = 0, vmax = a.bdmax;
-    if (d.clip_to_restricted_range) {
-        vmin = 16 << bd8;
-        vmax = (pl && !a.is_id ? 240 : 235) << bd8;
-    }
-    const int ys = d.overlap_flag && row ? min(2 >> ssy, bh) : 0;
-    const int xs = d.overlap_flag && c ? min(2 >> ssx, bw) : 0;
-    // LUT origins of the four (column, row) offset blocks (sample_lut, :155-164)
-    int org[2][2];
-#pragma unroll
-    for (int bx = 0; bx < 2; bx++)
-#pragma unroll
-        for (int by = 0; by < 2; by++) {
-            const int rv = off[bx][by];
-            org[bx][by] = (3 + (2 >> ssy) * (3 + (rv & 15)) + bh0 * by) * kGW + 3 + (2 >> ssx) * (3 + (rv >> 4)) + bw0 * bx;
-        }
-    auto wgt = [&](int ss, int i, int k) -> int { return ss ? (k ? 22 : 23) : ((i == 0) == (k == 0) ? 27 : 17); };
-    auto blend = [&](int old, int cur, int w0, int w1) { return min(max(rnd2(old * w0 + cur * w1, 5), gmin), gmax); };
-    const P *luma = a.in[0] + (size_t)(row * 32) * a.is[0];
-    int sv[NP], gv[NP], lv[NP];
-    bool ok[NP];
-#pragma unroll
-    for (int k = 0; k < NP; k++) {   // loads
-        const int i = threadIdx.x + 256 * k, y = i >> lw, x = i & (bw0 - 1);
-        ok[k] = x < bw && y < bh;
-        sv[k] = ok[k] ? (int)src[(size_t)y * is + x] : 0;
-        int gr = g[org[0][0] + y * kGW + x];
-        if (x < xs) gr = blend(g[org[1][0] + y * kGW + x], gr, wgt(ssx, x, 0), wgt(ssx, x, 1));
-        if (y < ys) {
-            int top = g[org[0][1] + y * kGW + x];
-            if (x < xs) top = blend(g[org[1][1] + y * kGW + x], top, wgt(ssx, x, 0), wgt(ssx, x, 1));
-            gr = blend(top, gr, wgt(ssy, y, 0), wgt(ssy, y, 1));
-        }
-        gv[k] = gr;
-        lv[k] = 0;
-        if (pl && ok[k]) {
-            const int lx = (x0 + x) << ssx, ly = y << ssy;
-            int avg = luma[(size_t)ly * a.is[0] + min(lx, a.w - 1)];
-            if (ssx) avg = (avg + luma[(size_t)ly * a.is[0] + min(lx + 1, a.w - 1)] + 1) >> 1;
-            lv[k] = avg;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < NP; k++) {   // scaling (LDS), noise, store
-        if (!ok[k]) continue;
-        const int i = threadIdx.x + 256 * k, y = i >> lw, x = i & (bw0 - 1);
-        int val = sv[k];
-        if (pl) {
-            val = lv[k];
-            if (!d.chroma_scaling_from_luma) {
-                const int comb = lv[k] * d.uv_luma_mult[pl - 1] + sv[k] * d.uv_mult[pl - 1];
-                val = min(max((comb >> 6) + d.uv_offset[pl - 1] * (1 << bd8), 0), a.bdmax);
+            const bool ok = x < bw && y < bh;
+            sv[k] = ok ? (int)src[(size_t)y * is + x] : 0;
+            lv[k] = 0;
+            if (pl && grained && ok) {
+                const int lx = (x0 + x) << ssx, ly = y << ssy;
+                int avg = luma[(size_t)ly * a.is[0] + min(lx, a.w - 1)];
+                if (ssx) avg = (avg + luma[(size_t)ly * a.is[0] + min(lx + 1, a.w - 1)] + 1) >> 1;
+                lv[k] = avg;
             }
+            if (!grained && ok) dst[(size_t)y * os + x] = (P)sv[k];   // fg_apply_tmpl.c:132-160: copied
         }
-        const int noise = rnd2(sc[val] * gv[k], d.scaling_shift);
-        dst[(size_t)y * os + x] = (P)min(max(sv[k] + noise, vmin), vmax);
     }
-}
 
-template <int BPC>
+    __device__ __forceinline__ void finish(const ApplyArgs<BPC> &a, const int (&off)[2][2], const uint8_t *sc) {
+        if (!grained) return;
+        const Dav1dGpuFilmGrainData &d = a.d;
+        const int bd8 = bd8_of(a.bdmax);
+        const int gmin = -(128 << bd8), gmax = (128 << bd8) - 1;
+        const int16_t *g = a.grain + pl * kGH * kGW;
+        int vmin = 0, vmax = a.bdmax;
+        if (d.clip_to_restricted_range) {
+            vmin = 16 << bd8;
+            vmax = (pl && !a.is_id ? 240 : 235) << bd8;
+        }
+        const int ys = d.overlap_flag && row ? min(2 >> ssy, bh) : 0;
+        const int xs = d.overlap_flag && c ? min(2 >> ssx, bw) : 0;
+        // LUT origins of the four (column, row) offset blocks (sample_lut, :155-164)
+        int org[2][2];
+#pragma unroll
+        for (int bx = 0; bx < 2; bx++)
+#pragma unroll
+            for (int by = 0; by < 2; by++) {
+                const int rv = off[bx][by];
+                org[bx][by] = (3 + (2 >> ssy) * (3 + (rv & 15)) + bh0 * by) * kGW + 3 + (2 >> ssx) * (3 + (rv >> 4)) +
+                              bw0 * bx;
+            }
+        auto wgt = [&](int ss, int i, int k) -> int { return ss ? (k ? 22 : 23) : ((i == 0) == (k == 0) ? 27 : 17); };
+        auto blend = [&](int old, int cur, int w0, int w1) { return min(max(rnd2(old * w0 + cur * w1, 5), gmin), gmax); };
+        int gv[NP];
+#pragma unroll
+        for (int k = 0; k < NP; k++) {   // grain samples (independent loads)
+            const int i = threadIdx.x + 256 * k, y = i >> lw, x = i & (bw0 - 1);
+            int gr = g[org[0][0] + y * kGW + x];
+            if (x < xs) gr = blend(g[org[1][0] + y * kGW + x], gr, wgt(ssx, x, 0), wgt(ssx, x, 1));
+            if (y < ys) {
+                int top = g[org[0][1] + y * kGW + x];
+                if (x < xs) top = blend(g[org[1][1] + y * kGW + x], top, wgt(ssx, x, 0), wgt(ssx, x, 1));
+                gr = blend(top, gr, wgt(ssy, y, 0), wgt(ssy, y, 1));
+            }
+            gv[k] = gr;
+        }
+#pragma unroll
+        for (int k = 0; k < NP; k++) {   // scaling (LDS), noise, store
+            const int i = threadIdx.x + 256 * k, y = i >> lw, x = i & (bw0 - 1);
+            if (x >= bw || y >= bh) continue;
+            int val = sv[k];
+            if (pl) {
+                val = lv[k];
+                if (!d.chroma_scaling_from_luma) {
+                    const int comb = lv[k] * d.uv_luma_mult[pl - 1] + sv[k] * d.uv_mult[pl - 1];
+                    val = min(max((comb >> 6) + d.uv_offset[pl - 1] * (1 << bd8), 0), a.bdmax);
+                }
+            }
+            const int noise = rnd2(sc[val] * gv[k], d.scaling_shift);
+            dst[(size_t)y * os + x] = (P)min(max(sv[k] + noise, vmin), vmax);
+        }
+    }
+};
+
+template <int BPC, int LAYOUT>
 __global__ __launch_bounds__(256) void k_grain_apply(ApplyArgs<BPC> a) {
     constexpr int SC = BPC == 8 ? 256 : 4096;
+    constexpr int NPC = LAYOUT == 1 ? 1 : LAYOUT == 2 ? 2 : 4;   // chroma pixels per thread
     __shared__ int off[2][2];   // [column: this, previous][row: this, previous]
     __shared__ uint8_t sc[3][SC];
     const Dav1dGpuFilmGrainData &d = a.d;
-    const int c = blockIdx.x, row = blockIdx.y;
+    // XCD-contiguous block order: workgroups are dealt round-robin over the
+    // 8 XCDs, so logical block (b % 8) * (nb / 8) + b / 8 gives each XCD a
+    // contiguous run of blocks; a 128-B picture line (4 blocks of one row)
+    // is then read and written through one L2 instead of four
+    const int cols = (a.w + 31) >> 5, nblk = cols * ((a.h + 31) >> 5);
+    const int nb8 = (int)gridDim.x >> 3, b = blockIdx.x;
+    const int lb = (b & 7) * nb8 + (b >> 3);
+    if (lb >= nblk) return;
+    const int c = lb % cols, row = lb / cols;
+    // the picture loads of all three planes first (they need no offsets)
+    PlaneJob<BPC, 4> jy;
+    PlaneJob<BPC, NPC> ju, jv;
+    jy.load(a, 0, c, row);
+    ju.load(a, 1, c, row);
+    jv.load(a, 2, c, row);
     if (threadIdx.x < 4) {
         const int bc = threadIdx.x & 1, br = threadIdx.x >> 1;
         const bool used = (!bc || (d.overlap_flag && c)) && (!br || (d.overlap_flag && row));
@@ -402,18 +434,9 @@ __global__ __launch_bounds__(256) void k_grain_apply(ApplyArgs<BPC> a) {
             *reinterpret_cast<const uint32_t *>(a.scaling + (i / SC) * 4096 + (i % SC));
     __syncthreads();
     int o[2][2] = {{off[0][0], off[0][1]}, {off[1][0], off[1][1]}};
-    const uint8_t *scu = d.chroma_scaling_from_luma ? sc[0] : sc[1], *scv = d.chroma_scaling_from_luma ? sc[0] : sc[2];
-    grain_plane<BPC, 4>(a, o, sc[0], 0, c, row);
-    if (a.layout == 1) {
-        grain_plane<BPC, 1>(a, o, scu, 1, c, row);
-        grain_plane<BPC, 1>(a, o, scv, 2, c, row);
-    } else if (a.layout == 2) {
-        grain_plane<BPC, 2>(a, o, scu, 1, c, row);
-        grain_plane<BPC, 2>(a, o, scv, 2, c, row);
-    } else {
-        grain_plane<BPC, 4>(a, o, scu, 1, c, row);
-        grain_plane<BPC, 4>(a, o, scv, 2, c, row);
-    }
+    jy.finish(a, o, sc[0]);
+    ju.finish(a, o, d.chroma_scaling_from_luma ? sc[0] : sc[1]);
+    jv.finish(a, o, d.chroma_scaling_from_luma ? sc[0] : sc[2]);
 }
 
 template <int BPC>
@@ -452,7 +475,11 @@ static int launch_grain(const Dav1dGpuFilmGrainBatch *b, hipStream_t stream) {
     a.d = b->data;
     a.grain = g.grain;
     a.scaling = g.scaling;
-    k_grain_apply<BPC><<<dim3((w + 31) / 32, (h + 31) / 32), 256, 0, stream>>>(a);
+    const int nblk = ((w + 31) / 32) * ((h + 31) / 32);
+    const dim3 grid((unsigned)((nblk + 7) & ~7));
+    if (b->layout == 1) k_grain_apply<BPC, 1><<<grid, 256, 0, stream>>>(a);
+    else if (b->layout == 2) k_grain_apply<BPC, 2><<<grid, 256, 0, stream>>>(a);
+    else k_grain_apply<BPC, 3><<<grid, 256, 0, stream>>>(a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         fprintf(stderr, "dav1d-gpu: film grain launch failed: %s\n", hipGetErrorString(e));
