@@ -100,39 +100,38 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
     const int cls = __builtin_amdgcn_readfirstlane(task.cls);
     const int first = __builtin_amdgcn_readfirstlane(task.first);
     const int count = __builtin_amdgcn_readfirstlane(task.count);
-    if (level > 0) {
-        int ok = 1;
-        if (lane == 0) {
-            const int need = f.level_tasks[level - 1];
-            int *done = &f.ctr[kFlowCtrHead + kFlowCtrStride * (level - 1)];
-            for (int it = 0;; it++) {
-                if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
-                if (it >= DGPU_FLOW_SPIN_LIMIT ||
-                    __hip_atomic_load(&f.ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    ok = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(DGPU_FLOW_SLEEP);
-            }
-            if (!ok) __hip_atomic_store(&f.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // a wave that gave up still counts itself done, so no later wave
-        // waits on it longer than its own bound
-        if (!__builtin_amdgcn_readfirstlane(ok)) {
-            if (lane == 0)
-                __hip_atomic_fetch_add(&f.ctr[kFlowCtrHead + kFlowCtrStride * level], 1, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        // the previous levels' picture / top_edge stores are visible from here
-        if (!DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    if constexpr (DGPU_FLOW_TRACE) tr1 = __builtin_amdgcn_s_memrealtime();
     const int lg = (int)((kLog2Lanes >> (3 * cls)) & 7);
     const int ui = first + min(lane >> lg, count - 1);
     const Dav1dGpuUnit u = a.units[ui];
     const Dav1dGpuIntraEdge rec = a.recs[ui];
-    dispatch<BPC, GROUP_ALL_IE>(a, pt, u, rec, cls, first, count, lds, 0);
+    // the level wait runs inside the class code, after the coefficient loads
+    // and the transforms and before the edge gather (recon_kernel.hpp)
+    auto wait = [&]() {
+        if (level > 0) {
+            int ok = 1;
+            if (lane == 0) {
+                const int need = f.level_tasks[level - 1];
+                int *done = &f.ctr[kFlowCtrHead + kFlowCtrStride * (level - 1)];
+                for (int it = 0;; it++) {
+                    if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+                    if (it >= DGPU_FLOW_SPIN_LIMIT ||
+                        __hip_atomic_load(&f.ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        ok = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(DGPU_FLOW_SLEEP);
+                }
+                // a wave that gives up flags the error and carries on (its
+                // pixels are then wrong, but every wave still finishes)
+                if (!ok) __hip_atomic_store(&f.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __builtin_amdgcn_wave_barrier();
+            // the previous levels' picture / top_edge stores are visible from here
+            if (!DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        if constexpr (DGPU_FLOW_TRACE) tr1 = __builtin_amdgcn_s_memrealtime();
+    };
+    dispatch<BPC, GROUP_ALL_IE>(a, pt, u, rec, cls, first, count, lds, 0, wait);
     if constexpr (DGPU_FLOW_TRACE) {
         __builtin_amdgcn_s_waitcnt(0);
         tr2 = __builtin_amdgcn_s_memrealtime();

@@ -42,23 +42,24 @@ constexpr uint64_t kLog2Lanes = pack_log2_lanes(std::make_integer_sequence<int, 
 #ifndef DGPU_ONLY_CLASS
 #define DGPU_ONLY_CLASS -1   // build-time probe: compile a single class (resource studies)
 #endif
-template <int BPC, int TX, int GRP>
+template <int BPC, int TX, int GRP, typename WaitT = NoWait>
 __device__ __forceinline__ void run_class(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
-                                          const Dav1dGpuIntraEdge &rec, int first, int count, uint8_t *lds, int gw) {
+                                          const Dav1dGpuIntraEdge &rec, int first, int count, uint8_t *lds, int gw,
+                                          const WaitT &wait = WaitT()) {
     if constexpr (TX < DGPU_N_RECT_TX_SIZES && in_group(TX, GRP) &&
                   (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS))
-        recon_units<BPC, TX, GRP == GROUP_WARP, gathers(GRP)>(a, pt, u, rec, first, count, lds, gw, GRP);
+        recon_units<BPC, TX, GRP == GROUP_WARP, gathers(GRP)>(a, pt, u, rec, first, count, lds, gw, GRP, wait);
 }
 
 // One switch (a compact compare tree) instead of a chain of class tests
 // spread between the inlined class bodies: the chain's targets were cold
 // instruction-cache lines on every wave's way to its class.
-template <int BPC, int GRP>
+template <int BPC, int GRP, typename WaitT = NoWait>
 __device__ __forceinline__ void dispatch(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
                                          const Dav1dGpuIntraEdge &rec, int cls, int first, int count, uint8_t *lds,
-                                         int gw) {
+                                         int gw, const WaitT &wait = WaitT()) {
 #define DGPU_CASE(T) \
-    case T: run_class<BPC, T, GRP>(a, pt, u, rec, first, count, lds, gw); break;
+    case T: run_class<BPC, T, GRP>(a, pt, u, rec, first, count, lds, gw, wait); break;
     switch (cls) {
         DGPU_CASE(0) DGPU_CASE(1) DGPU_CASE(2) DGPU_CASE(3) DGPU_CASE(4) DGPU_CASE(5) DGPU_CASE(6)
         DGPU_CASE(7) DGPU_CASE(8) DGPU_CASE(9) DGPU_CASE(10) DGPU_CASE(11) DGPU_CASE(12) DGPU_CASE(13)

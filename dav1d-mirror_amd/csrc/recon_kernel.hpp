@@ -1093,10 +1093,15 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
 
 // ---------------------------------------------------------------- kernel --
 
-template <int BPC, int TX, bool WARPK, bool GATHER = false>
+struct NoWait {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+template <int BPC, int TX, bool WARPK, bool GATHER = false, typename WaitT = NoWait>
 __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt,
                                             const Dav1dGpuUnit &u_in, const Dav1dGpuIntraEdge &rec, int first,
-                                            int count, uint8_t *wave_lds, int gw, int grp) {
+                                            int count, uint8_t *wave_lds, int gw, int grp,
+                                            const WaitT &wait = WaitT()) {
     using CL = Cls<TX>;
     using SL = Slot<BPC, TX>;
     using P = typename Px<BPC>::pixel;
@@ -1159,35 +1164,6 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     constexpr bool NW = !WARPK;   // the warp launch compiles only the WARP prediction
     const bool edged = NW && (pred == DGPU_PRED_INTRA || pred == DGPU_PRED_CFL);   // same edge_off in both views
     if (edged && !GATHER) est.load(a.edges + u.p.intra.edge_off - 2 * H, SL::EDGE * (int)sizeof(P), l);
-    IeCtx<P> iec;
-    if constexpr (GATHER && !DGPU_IE_NOGATHER) {   // dav1d_prepare_intra_edges, every entry straight into LDS
-        if (edged) {
-            const PlaneTabIE<BPC> &pti = static_cast<const PlaneTabIE<BPC> &>(pt);
-            iec = ie_setup<P>(rec, pt.dst[plane], ds, pti.top[plane], pti.top_stride[plane], pti.sb_log2[plane],
-                              W / 4, H / 4, bdmax);
-            // every entry's load first (a fixed, unrolled count per lane, so
-            // the loads go out together), then the LDS writes
-            constexpr int NE = 2 * W + 2 * H + 1, EPL = (NE + G - 1) / G;
-            P *tw_ = reinterpret_cast<P *>(src) + 2 * H;
-            int ev[EPL];
-#pragma unroll
-            for (int k = 0; k < EPL; k++) {
-                const int i = -2 * H + l + k * G;
-                bool need;
-                ev[k] = (i <= 2 * W && ie_need(iec, i)) ? ie_value(iec, i, need) : -1;
-            }
-#pragma unroll
-            for (int k = 0; k < EPL; k++)
-                if (ev[k] >= 0) tw_[-2 * H + l + k * G] = (P)ev[k];
-            ug.p.intra.mode = (uint8_t)iec.mode;   // CFL: its DC source, the same byte
-            if (pred != DGPU_PRED_CFL) ug.p.intra.angle = ie_angle_field(rec, iec.angle);
-            if (l == 0) {
-                a.units_rw[first + g].p.intra.mode = ug.p.intra.mode;
-                if (pred != DGPU_PRED_CFL) a.units_rw[first + g].p.intra.angle = ug.p.intra.angle;
-            }
-        }
-    }
-
     // read for every unit (only inter kinds use it; the bank math below stays
     // in range for any byte).  Selecting it on `inter` gave inter-intra units
     // Filter2d 0 in the second launch's kernel (measured on MI355X, cause
@@ -1345,6 +1321,43 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     }
 
     wave_sync();
+    // GATHER: the edges come last, after the coefficient loads and both
+    // transform passes, which need nothing from the neighbours; `wait` (the
+    // persistent kernel's level wait) is the first point that does, so a
+    // wave does all of that while the previous level finishes
+    if constexpr (GATHER) {
+        wait();
+    }
+    IeCtx<P> iec;
+    if constexpr (GATHER && !DGPU_IE_NOGATHER) {   // dav1d_prepare_intra_edges, every entry straight into LDS
+        if (edged) {
+            const PlaneTabIE<BPC> &pti = static_cast<const PlaneTabIE<BPC> &>(pt);
+            iec = ie_setup<P>(rec, pt.dst[plane], ds, pti.top[plane], pti.top_stride[plane], pti.sb_log2[plane],
+                              W / 4, H / 4, bdmax);
+            // every entry's load first (a fixed, unrolled count per lane, so
+            // the loads go out together), then the LDS writes
+            constexpr int NE = 2 * W + 2 * H + 1, EPL = (NE + G - 1) / G;
+            P *tw_ = reinterpret_cast<P *>(src) + 2 * H;
+            int ev[EPL];
+#pragma unroll
+            for (int k = 0; k < EPL; k++) {
+                const int i = -2 * H + l + k * G;
+                bool need;
+                ev[k] = (i <= 2 * W && ie_need(iec, i)) ? ie_value(iec, i, need) : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < EPL; k++)
+                if (ev[k] >= 0) tw_[-2 * H + l + k * G] = (P)ev[k];
+            ug.p.intra.mode = (uint8_t)iec.mode;   // CFL: its DC source, the same byte
+            if (pred != DGPU_PRED_CFL) ug.p.intra.angle = ie_angle_field(rec, iec.angle);
+            if (l == 0) {
+                a.units_rw[first + g].p.intra.mode = ug.p.intra.mode;
+                if (pred != DGPU_PRED_CFL) a.units_rw[first + g].p.intra.angle = ug.p.intra.angle;
+            }
+        }
+    }
+
+    if constexpr (GATHER) wave_sync();
     mark(5);
 
     // ---------------- P5/P6: prediction + residual -> picture ----------------

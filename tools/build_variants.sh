@@ -15,7 +15,7 @@ build() {
     done
     wait
     local objs=""
-    for s in runtime mc ipred itx recon8 recon16 tile8 tile16 edges recon_ie8 recon_ie16; do
+    for s in runtime mc ipred itx recon8 recon16 tile8 tile16 edges recon_ie8 recon_ie16 recorder grain; do
         if [ -f build/var/$name.$s.o ] && [[ " ${TUS:-recon8 recon16} " == *" $s "* ]]; then objs="$objs build/var/$name.$s.o"; else objs="$objs build/$s.o"; fi
     done
     $HIPCC $F -shared -o libdav1d_gpu.$name.so $objs
