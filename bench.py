@@ -159,7 +159,8 @@ def intra_breakdown(cfg, dev, stream, steps):
     """an all-intra frame of the config's size and
     bitdepth reconstructed on the device by the intra wavefront
     (dav1d_gpu_recon_intra_frame_*: persistent, one launch per frame whose
-    waves wait on per-level counters; and fused, one launch per level), one
+    waves wait on their producers' tasks; levels, the same launch waiting on
+    per-level counters; and fused, one launch per level), one
     tile and 2x2 tiles; beside it the oracle in the decoder's own order on
     one host core.  Reported beside the headline, not part of it."""
     import dav1d_mirror_amd.intra as intra
@@ -170,7 +171,7 @@ def intra_breakdown(cfg, dev, stream, steps):
                                                       bitdepth_max=cfg.bitdepth_max, tile_cols=tiles[0],
                                                       tile_rows=tiles[1]))
         ms = {}
-        for mode in ("persistent", "fused"):
+        for mode in ("persistent", "levels", "fused"):
             frame = intra.DeviceIntraFrame(fr, dev, mode=mode)
             for _ in range(2):
                 frame.launch(stream)
@@ -187,6 +188,7 @@ def intra_breakdown(cfg, dev, stream, steps):
         px = sum(w * h for w, h in fr.plane_wh)
         out[name] = {"units": int(len(fr.units)), "levels": int(fr.n_levels), "ms_per_frame": round(ks * 1e3, 3),
                      "gpix_s": round(px / ks / 1e9, 4), "us_per_level": round(ks * 1e6 / fr.n_levels, 2),
+                     "levels_ms_per_frame": round(ms["levels"] * 1e3, 3),
                      "fused_ms_per_frame": round(ms["fused"] * 1e3, 3),
                      "oracle_1core_ms": round(cpu_s * 1e3, 2), "flow_error": flow_error,
                      "bit_exact_vs_oracle": all(bool(np.array_equal(g, o)) for g, o in zip(got, ho.dst))}

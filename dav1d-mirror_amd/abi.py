@@ -137,7 +137,9 @@ class IntraSchedule(ctypes.Structure):
                 ("run_start", ctypes.c_void_p),
                 ("runs", ctypes.c_void_p),
                 ("workspace", ctypes.c_void_p),
-                ("workspace_bytes", ctypes.c_int64)]
+                ("workspace_bytes", ctypes.c_int64),
+                ("dep_start", ctypes.c_void_p),
+                ("deps", ctypes.c_void_p)]
 
 
 class RecBlock(ctypes.Structure):

@@ -16,6 +16,7 @@
 // bound (DGPU_FLOW_SPIN_LIMIT) turns any unexpected stall into an error
 // flag; a wave that gives up still counts itself done, so the grid drains.
 #pragma once
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -53,6 +54,9 @@ struct FlowArgs {
     int n_tasks;
     const int32_t *level_tasks;   // tasks per level
     int *ctr;
+    int *done;                    // dataflow: per-unit completion flags
+    const int32_t *dep_start;     // dataflow: per unit, its producer units (CSR); NULL: levels
+    const int32_t *deps;
     unsigned long long *trace;    // DGPU_FLOW_TRACE: [ticket][4] start, ready, computed, released
 };
 
@@ -107,7 +111,28 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
     // the level wait runs inside the class code, after the coefficient loads
     // and the transforms and before the edge gather (recon_kernel.hpp)
     auto wait = [&]() {
-        if (level > 0) {
+        if (f.dep_start) {   // dataflow: the producers of the task's units, one per lane
+            const int d0 = f.dep_start[first], nd = f.dep_start[first + count] - d0;
+            // the class code has let lanes past its units go: the live lanes
+            // are a prefix of the wave
+            const int nl = __popcll(__ballot(1));
+            int ok = 1;
+            for (int j0 = 0; j0 < nd; j0 += nl) {
+                const int j = j0 + lane, dep = j < nd ? f.deps[d0 + j] : -1;
+                for (int it = 0;; it++) {
+                    const int v = dep < 0 ? 1 : __hip_atomic_load(&f.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(v != 0)) break;
+                    if (it >= DGPU_FLOW_SPIN_LIMIT ||
+                        __hip_atomic_load(&f.ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        ok = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(DGPU_FLOW_SLEEP);
+                }
+            }
+            if (!ok && lane == 0) __hip_atomic_store(&f.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (nd && !DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        } else if (level > 0) {
             int ok = 1;
             if (lane == 0) {
                 const int need = f.level_tasks[level - 1];
@@ -139,9 +164,13 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
     // this task's stores reach agent scope before it is counted
     if (!DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     else __builtin_amdgcn_s_waitcnt(0);
-    if (lane == 0)
+    if (f.dep_start) {   // (all lanes are live again here)
+        for (int i = lane; i < count; i += 64)
+            __hip_atomic_store(&f.done[first + i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (lane == 0) {
         __hip_atomic_fetch_add(&f.ctr[kFlowCtrHead + kFlowCtrStride * level], 1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+    }
     if constexpr (DGPU_FLOW_TRACE) {
         const unsigned long long tr3 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
@@ -223,13 +252,48 @@ static FlowStage *flow_stage_get(size_t n) {   // call with g_stage_mu held
     return &st;
 }
 
+// host: check the schedule's producer lists (per unit, level order): in
+// range, and every producer of a task's units in an earlier task (units of a
+// task are contiguous, so a task's list is one slice of deps); returns the
+// number of entries, or -2
+static int64_t flow_check_deps(const Dav1dGpuIntraSchedule *s, int n_units, const std::vector<FlowTask> &tasks) {
+    if (!s->dep_start || !s->deps) return 0;
+    const int32_t *ds = s->dep_start;
+    if (ds[0] != 0) return -2;
+    for (int u = 0; u < n_units; u++)
+        if (ds[u + 1] < ds[u]) return -2;
+    for (const FlowTask &t : tasks)
+        for (int k = ds[t.first]; k < ds[t.first + t.count]; k++)
+            if ((uint32_t)s->deps[k] >= (uint32_t)t.first) return -2;   // (negative: huge)
+    return ds[n_units];
+}
+
+// workspace layout: counters | unit done flags | tasks | level counts | dep_start | deps | trace
+struct FlowLayout {
+    size_t ctr, done, tasks, level, dstart, deps, trace, total;
+};
+static FlowLayout flow_layout(int n_levels, size_t n_tasks, int n_units, int64_t n_deps, bool dataflow) {
+    FlowLayout L;
+    const size_t nu = dataflow ? (size_t)n_units : 0;
+    L.ctr = 0;
+    L.done = flow_ctr_ints(n_levels) * 4;
+    L.tasks = L.done + ((nu * 4 + 15) & ~(size_t)15);
+    L.level = L.tasks + n_tasks * sizeof(FlowTask);
+    L.dstart = L.level + (size_t)(n_levels > 0 ? n_levels : 1) * 4;
+    L.deps = L.dstart + (dataflow ? nu + 1 : 0) * 4;
+    L.trace = (L.deps + (size_t)n_deps * 4 + 15) & ~(size_t)15;
+    L.total = DGPU_FLOW_TRACE ? L.trace + n_tasks * 32 : L.deps + (size_t)n_deps * 4;
+    return L;
+}
+
 template <int BPC>
 static int64_t flow_workspace_bytes(const Dav1dGpuIntraSchedule *s, int n_units) {
     std::vector<FlowTask> t;
     std::vector<int32_t> lt;
     if (flow_tasks(s, n_units, t, lt)) return -2;
-    const size_t base = flow_ctr_ints(s->n_levels) * 4 + t.size() * sizeof(FlowTask) + lt.size() * 4;
-    return (int64_t)(DGPU_FLOW_TRACE ? ((base + 15) & ~(size_t)15) + t.size() * 32 : base);
+    const int64_t nd = flow_check_deps(s, n_units, t);
+    if (nd < 0) return -2;
+    return (int64_t)flow_layout(s->n_levels, t.size(), n_units, nd, s->dep_start && s->deps).total;
 }
 
 template <int BPC>
@@ -246,26 +310,35 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     int rc = flow_tasks(s, b->n_units, tasks, level_tasks);
     if (rc) return rc;
     if (tasks.empty()) return 0;
-    const size_t ctr_bytes = flow_ctr_ints(s->n_levels) * 4;
-    const size_t base = ctr_bytes + tasks.size() * sizeof(FlowTask) + level_tasks.size() * 4;
-    const size_t need = DGPU_FLOW_TRACE ? ((base + 15) & ~(size_t)15) + tasks.size() * 32 : base;
-    if ((size_t)s->workspace_bytes < need || ((uintptr_t)s->workspace & 15)) return -5;
+    const int64_t nd = flow_check_deps(s, b->n_units, tasks);
+    if (nd < 0) return -2;
+    const bool dataflow = s->dep_start && s->deps;
+    const FlowLayout Lw = flow_layout(s->n_levels, tasks.size(), b->n_units, nd, dataflow);
+    if ((size_t)s->workspace_bytes < Lw.total || ((uintptr_t)s->workspace & 15)) return -5;
     uint8_t *ws = (uint8_t *)s->workspace;
     FlowArgs f;
     f.ctr = (int *)ws;
-    f.tasks = (const FlowTask *)(ws + ctr_bytes);
+    f.done = (int *)(ws + Lw.done);
+    f.tasks = (const FlowTask *)(ws + Lw.tasks);
     f.n_tasks = (int)tasks.size();
-    f.level_tasks = (const int32_t *)(ws + ctr_bytes + tasks.size() * sizeof(FlowTask));
-    f.trace = (unsigned long long *)(ws + ((base + 15) & ~(size_t)15));
-    {   // the task list through page-locked staging (asynchronous copy)
-        const size_t tb = tasks.size() * sizeof(FlowTask), lb = level_tasks.size() * 4;
+    f.level_tasks = (const int32_t *)(ws + Lw.level);
+    f.dep_start = dataflow ? (const int32_t *)(ws + Lw.dstart) : nullptr;
+    f.deps = (const int32_t *)(ws + Lw.deps);
+    f.trace = (unsigned long long *)(ws + Lw.trace);
+    {   // the task list and producer lists through page-locked staging (asynchronous copy)
+        const size_t up = Lw.deps + (size_t)nd * 4 - Lw.tasks;
         std::lock_guard<std::mutex> lock(g_stage_mu);
-        FlowStage *sg = flow_stage_get(tb + lb);
+        FlowStage *sg = flow_stage_get(up);
         if (!sg) return -3;
-        memcpy(sg->p, tasks.data(), tb);
-        memcpy((uint8_t *)sg->p + tb, level_tasks.data(), lb);
-        if (hipMemsetAsync(ws, 0, ctr_bytes, stream) != hipSuccess ||
-            hipMemcpyAsync(ws + ctr_bytes, sg->p, tb + lb, hipMemcpyHostToDevice, stream) != hipSuccess ||
+        uint8_t *st = (uint8_t *)sg->p;
+        memcpy(st, tasks.data(), tasks.size() * sizeof(FlowTask));
+        memcpy(st + (Lw.level - Lw.tasks), level_tasks.data(), level_tasks.size() * 4);
+        if (dataflow) {
+            memcpy(st + (Lw.dstart - Lw.tasks), s->dep_start, ((size_t)b->n_units + 1) * 4);
+            memcpy(st + (Lw.deps - Lw.tasks), s->deps, (size_t)nd * 4);
+        }
+        if (hipMemsetAsync(ws, 0, Lw.tasks, stream) != hipSuccess ||   // counters and done flags
+            hipMemcpyAsync(ws + Lw.tasks, sg->p, up, hipMemcpyHostToDevice, stream) != hipSuccess ||
             hipEventRecord(sg->ev, stream) != hipSuccess)
             return -3;
     }

@@ -16,10 +16,11 @@
 //   3. dependency levels at 4x4 granularity: inter units read only their
 //      references (level 0); an intra unit sits one level above every unit
 //      whose pixels the edges of its remapped mode read (CfL: also the
-//      co-located luma);
+//      co-located luma), and those units are its producers;
 //   4. units sorted by (level, size class, kind, mode, type), records in the
 //      same order, coefficients compacted to the stored region, and one
-//      persistent wavefront launch (dav1d_gpu_recon_intra_frame_*).
+//      persistent wavefront launch (dav1d_gpu_recon_intra_frame_*) whose
+//      waves wait for their producers only.
 // Host code only; the device work runs on the caller's stream.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -139,6 +140,7 @@ struct Dav1dGpuRecorder {
     std::vector<Unit> cells;
     std::vector<uint64_t> keys, keys_tmp;
     std::vector<int32_t> rank;
+    std::vector<int32_t> prod_start, prod, dep_start, deps;   // producers: decode order, then level order
     std::vector<Dav1dGpuUnit> h_units;
     std::vector<Dav1dGpuIntraEdge> h_recs;
     std::vector<uint8_t> h_coef;
@@ -277,8 +279,14 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         for (const Dav1dGpuRecBlock &b : r->blocks) nc += (size_t)(b.w / kTx[b.tx].w) * (b.h / kTx[b.tx].h);
         cells.reserve(nc);
     }
-    std::vector<int32_t> lv[3];
-    for (int p = 0; p < 3; p++) lv[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
+    std::vector<int32_t> lv[3], own[3];   // per 4x4: level, and the decode-order cell writing it
+    for (int p = 0; p < 3; p++) {
+        lv[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
+        own[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
+    }
+    std::vector<int32_t> &prod_start = r->prod_start, &prod = r->prod;
+    prod_start.assign(1, 0);
+    prod.clear();
     size_t n_res_used = 0;
     for (const Dav1dGpuRecBlock &b : r->blocks) {
         const TxDim t = kTx[b.tx];
@@ -353,47 +361,59 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     nd = kNeeds[m];
                     c.sortmode = 16 + m;
                 }
-                // level: one above every pixel the edges (or CfL luma) read
-                const std::vector<int32_t> &L = lv[p];
+                // level: one above every pixel the edges (or CfL luma) read;
+                // producers: the cells that wrote those pixels
                 const int W4 = e.w4, H4 = e.h4;
-                auto cell = [&](int cx, int cy) { return L[(size_t)cy * w4p + cx]; };
+                const size_t p0 = prod.size();
                 int d = -1;
+                auto cell = [&](int cx, int cy) {
+                    const size_t at = (size_t)cy * w4p + cx;
+                    d = std::max(d, lv[p][at]);
+                    if (prod.size() == p0 || prod.back() != own[p][at]) prod.push_back(own[p][at]);
+                };
                 if (nd & 1) {
                     if (hl) {
-                        for (int k = y4; k < std::min(y4 + th4, H4); k++) d = std::max(d, cell(x4 - 1, k));
+                        for (int k = y4; k < std::min(y4 + th4, H4); k++) cell(x4 - 1, k);
                         if ((nd & 16) && y4 + th4 < H4 && (e.flags & DGPU_IE_LEFT_HAS_BOTTOM))
-                            for (int k = y4 + th4; k < std::min(y4 + 2 * th4, H4); k++) d = std::max(d, cell(x4 - 1, k));
+                            for (int k = y4 + th4; k < std::min(y4 + 2 * th4, H4); k++) cell(x4 - 1, k);
                     } else if (ht) {
-                        d = std::max(d, cell(x4, y4 - 1));
+                        cell(x4, y4 - 1);
                     }
                 }
                 if (nd & 2) {
                     if (ht) {
-                        for (int k = x4; k < std::min(x4 + tw4, W4); k++) d = std::max(d, cell(k, y4 - 1));
+                        for (int k = x4; k < std::min(x4 + tw4, W4); k++) cell(k, y4 - 1);
                         if ((nd & 8) && x4 + tw4 < W4 && (e.flags & DGPU_IE_TOP_HAS_RIGHT))
-                            for (int k = x4 + tw4; k < std::min(x4 + 2 * tw4, W4); k++) d = std::max(d, cell(k, y4 - 1));
+                            for (int k = x4 + tw4; k < std::min(x4 + 2 * tw4, W4); k++) cell(k, y4 - 1);
                     } else if (hl) {
-                        d = std::max(d, cell(x4 - 1, y4));
+                        cell(x4 - 1, y4);
                     }
                 }
                 if (nd & 4) {
-                    if (hl && ht) d = std::max(d, cell(x4 - 1, y4 - 1));
-                    else if (hl) d = std::max(d, cell(x4 - 1, y4));
-                    else if (ht) d = std::max(d, cell(x4, y4 - 1));
+                    if (hl && ht) cell(x4 - 1, y4 - 1);
+                    else if (hl) cell(x4 - 1, y4);
+                    else if (ht) cell(x4, y4 - 1);
                 }
                 if (cfl) {
                     const int lw4 = pw[0] / 4;
                     for (int cy = 2 * y4; cy < 2 * (y4 + th4); cy++)
                         for (int cx = 2 * x4; cx < 2 * (x4 + tw4); cx++) {
-                            const int v = lv[0][(size_t)cy * lw4 + cx];
-                            if (v < 0) return -1;   // CfL before its luma
-                            d = std::max(d, v);
+                            const size_t at = (size_t)cy * lw4 + cx;
+                            if (lv[0][at] < 0) return -1;   // CfL before its luma
+                            d = std::max(d, lv[0][at]);
+                            if (prod.size() == p0 || prod.back() != own[0][at]) prod.push_back(own[0][at]);
                         }
                 }
+                std::sort(prod.begin() + p0, prod.end());   // duplicate-free
+                prod.erase(std::unique(prod.begin() + p0, prod.end()), prod.end());
+                prod_start.push_back((int32_t)prod.size());
                 c.level = d + 1;
-                std::vector<int32_t> &Lw = lv[p];
+                const int ci = (int)cells.size();
                 for (int cy = y4; cy < y4 + th4; cy++)
-                    for (int cx = x4; cx < x4 + tw4; cx++) Lw[(size_t)cy * w4p + cx] = c.level;
+                    for (int cx = x4; cx < x4 + tw4; cx++) {
+                        lv[p][(size_t)cy * w4p + cx] = c.level;
+                        own[p][(size_t)cy * w4p + cx] = ci;
+                    }
                 cells.push_back(c);
             }
     }
@@ -461,6 +481,15 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         e.unit = i;
         hr[i] = e;
     }
+    // the producer lists in level order (the persistent kernel's dataflow waits)
+    r->dep_start.assign((size_t)n + 1, 0);
+    for (int ci = 0; ci < n; ci++) r->dep_start[rank[ci] + 1] = prod_start[ci + 1] - prod_start[ci];
+    for (int i = 0; i < n; i++) r->dep_start[i + 1] += r->dep_start[i];
+    r->deps.resize(prod.size());
+    for (int ci = 0; ci < n; ci++) {
+        int32_t *o = &r->deps[r->dep_start[rank[ci]]];
+        for (int k = prod_start[ci]; k < prod_start[ci + 1]; k++) *o++ = rank[prod[k]];
+    }
     for (int l = 0; l < n_levels; l++) {
         if (r->unit_start[l + 1] < r->unit_start[l]) r->unit_start[l + 1] = r->unit_start[l];   // (levels are dense)
         int32_t *cs = &r->class_start[(size_t)l * (NC + 1)];
@@ -488,6 +517,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     s.class_start = r->class_start.data();
     s.rec_start = r->rec_start.data();
     s.run_start = r->run_start.data();
+    s.dep_start = r->dep_start.data();
+    s.deps = r->deps.data();
     const int64_t wsb = dav1d_gpu_intra_workspace_bytes(&s, n);
     if (wsb < 0) return -2;
     if (r->d_units.grow((size_t)n * sizeof(Dav1dGpuUnit)) || r->d_recs.grow((size_t)n * sizeof(Dav1dGpuIntraEdge)) ||

@@ -213,6 +213,8 @@ class IntraFrame:
     top_rows: list           # top_edge shapes (rows, w) per plane
     sb_log2: tuple
     refs: list = None        # [ref][plane] padded reference planes (mixed frames)
+    dep_start: np.ndarray = None   # int32 [n + 1]: per unit (level order), its producers (CSR)
+    deps: np.ndarray = None        # int32, level-order unit indices
 
     def ref_origin_offset(self, plane):
         return self.cfg.ref_pad * self.refs[0][plane].shape[1] + self.cfg.ref_pad
@@ -407,8 +409,11 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     units[cflu] = cu
 
     # dependency levels, at 4x4 granularity per plane
+    # (and the producers: the units owning the 4x4s a unit reads)
     lv = [np.full((h // 4, w // 4), -1, np.int64) for (w, h) in planes]
+    own = [np.full((h // 4, w // 4), -1, np.int64) for (w, h) in planes]
     level = np.zeros(n, np.int64)
+    producers = []
     modes, angles = U["mode"], U["angle"]
     for i in range(n):
         p, x4, y4 = int(plane_u[i]), int(ux[i]) // 4, int(uy[i]) // 4
@@ -418,31 +423,36 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
         hl, ht = bool(f & abi.IE_HAVE_LEFT), bool(f & abi.IE_HAVE_TOP)
         m, _ = remap_mode(modes[i], angles[i], hl, ht)
         nd = 0 if interu[i] else _NEEDS[m]   # inter units read only the references
-        L = lv[p]
-        deps = [-1]
+        L, O = lv[p], own[p]
+        reads = []   # (plane, rows, cols) regions read
         if nd & _NEED_L:
             if hl:
-                deps.append(L[y4:min(y4 + t4h, h4), x4 - 1].max())
+                reads.append((p, slice(y4, min(y4 + t4h, h4)), slice(x4 - 1, x4)))
                 if nd & _NEED_BL and y4 + t4h < h4 and (f & abi.IE_LEFT_HAS_BOTTOM):
-                    deps.append(L[y4 + t4h:min(y4 + 2 * t4h, h4), x4 - 1].max())
+                    reads.append((p, slice(y4 + t4h, min(y4 + 2 * t4h, h4)), slice(x4 - 1, x4)))
             elif ht:
-                deps.append(L[y4 - 1, x4])
+                reads.append((p, slice(y4 - 1, y4), slice(x4, x4 + 1)))
         if nd & _NEED_T:
             if ht:
-                deps.append(L[y4 - 1, x4:min(x4 + t4w, w4)].max())
+                reads.append((p, slice(y4 - 1, y4), slice(x4, min(x4 + t4w, w4))))
                 if nd & _NEED_TR and x4 + t4w < w4 and (f & abi.IE_TOP_HAS_RIGHT):
-                    deps.append(L[y4 - 1, x4 + t4w:min(x4 + 2 * t4w, w4)].max())
+                    reads.append((p, slice(y4 - 1, y4), slice(x4 + t4w, min(x4 + 2 * t4w, w4))))
             elif hl:
-                deps.append(L[y4, x4 - 1])
-        if nd & _NEED_TL:
-            deps.append(L[y4 - 1, x4 - 1] if hl and ht else L[y4, x4 - 1] if hl else L[y4 - 1, x4] if ht else -1)
+                reads.append((p, slice(y4, y4 + 1), slice(x4 - 1, x4)))
+        if nd & _NEED_TL and (hl or ht):
+            ry, rx = (y4 - 1, x4 - 1) if hl and ht else (y4, x4 - 1) if hl else (y4 - 1, x4)
+            reads.append((p, slice(ry, ry + 1), slice(rx, rx + 1)))
         if cflu[i]:
-            luma = lv[0][2 * y4:2 * (y4 + t4h), 2 * x4:2 * (x4 + t4w)]
-            assert luma.min() >= 0          # the block's luma precedes its chroma
-            deps.append(luma.max())
-        d = max(int(v) for v in deps)
+            reads.append((0, slice(2 * y4, 2 * (y4 + t4h)), slice(2 * x4, 2 * (x4 + t4w))))
+        d, pr = -1, set()
+        for (q, ry, rx) in reads:
+            assert lv[q][ry, rx].min() >= 0     # (a block's luma precedes its chroma)
+            d = max(d, int(lv[q][ry, rx].max()))
+            pr.update(int(v) for v in np.unique(own[q][ry, rx]))
         level[i] = d + 1
+        producers.append(sorted(pr))
         L[y4:y4 + t4h, x4:x4 + t4w] = d + 1
+        O[y4:y4 + t4h, x4:x4 + t4w] = i
     for L in lv:
         assert L.min() >= 0
 
@@ -511,9 +521,12 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     steps[unit_steps, 1] = inv[steps[unit_steps, 1]]
     top_rows = [(max(1, h >> s_), w) for (w, h), s_ in zip(planes, sbl)]
     edges = np.zeros(int(edge_len.sum()), cfg.pixel_dtype)
+    dep_start = np.zeros(n + 1, np.int32)
+    dep_start[1:] = np.cumsum([len(producers[j]) for j in perm])
+    deps = np.array([inv[q] for j in perm for q in producers[j]], np.int32)
     fr = IntraFrame(cfg, planes, units, coefs, edges, recs, runs, unit_start, class_start, rec_start,
                     run_start, steps, unit_rec, np.array(oracle_runs, abi.EDGE_BACKUP_DTYPE), top_rows, sbl,
-                    refs)
+                    refs, dep_start, deps)
     fr.blocks = BL
     fr.dec_units = dec_units
     return fr
@@ -563,13 +576,17 @@ class DeviceIntraFrame:
     """An IntraFrame on one GPU; launch() runs the whole wavefront
     (dav1d_gpu_recon_intra_frame_*) on a stream."""
 
-    MODES = ("persistent", "fused", "staged")
+    MODES = ("persistent", "levels", "fused", "staged")
 
     def __init__(self, fr, device="cuda:0", top_fill=0x5A, mode="persistent"):
-        """mode: persistent -- one launch per frame (DGPU_IS_PERSISTENT);
-        fused -- one launch per level (DGPU_IS_FUSED); staged -- edge stage,
-        unit batch and backup runs per level."""
+        """mode: persistent -- one launch per frame (DGPU_IS_PERSISTENT), a
+        wave waits for the tasks of its units' producers (dataflow); levels --
+        the same launch, a wave waits for the whole previous level; fused --
+        one launch per level (DGPU_IS_FUSED); staged -- edge stage, unit
+        batch and backup runs per level."""
         assert mode in self.MODES
+        dataflow = mode == "persistent"
+        mode = "persistent" if mode == "levels" else mode
         import torch
         self.torch, self.fr = torch, fr
         dev = torch.device(device)
@@ -597,6 +614,10 @@ class DeviceIntraFrame:
         s.flags = {"persistent": abi.IS_FUSED | abi.IS_PERSISTENT, "fused": abi.IS_FUSED, "staged": 0}[mode]
         s.unit_start, s.class_start, s.rec_start, s.run_start = (a.ctypes.data for a in self._host)
         s.runs = self.runs.data_ptr()
+        if mode == "persistent" and dataflow and fr.dep_start is not None:
+            self._host += [np.ascontiguousarray(fr.dep_start, np.int32),
+                           np.ascontiguousarray(fr.deps if len(fr.deps) else np.zeros(1, np.int32), np.int32)]
+            s.dep_start, s.deps = self._host[-2].ctypes.data, self._host[-1].ctypes.data
         self.sched = s
         self.lib = abi.load_lib()
         self.workspace = None

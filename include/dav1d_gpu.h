@@ -588,6 +588,12 @@ typedef struct Dav1dGpuIntraSchedule {
     void    *workspace;          /* device, 16-B aligned (DGPU_IS_PERSISTENT):
                                     counters + the task list                  */
     int64_t  workspace_bytes;    /* >= dav1d_gpu_intra_workspace_bytes()       */
+    /* optional (DGPU_IS_PERSISTENT): the units each unit reads pixels of,
+       host CSR over recon->units (producers at lower levels).  Given, a
+       wave waits only for the tasks holding its units' producers instead of
+       the whole previous level (dataflow); NULL: level barriers.            */
+    const int32_t *dep_start;    /* n_units + 1                                */
+    const int32_t *deps;
 } Dav1dGpuIntraSchedule;
 
 /* Workspace a DGPU_IS_PERSISTENT schedule needs (bytes), or -2 if the

@@ -332,6 +332,58 @@ class HostIntraFrame:
             backup(ctypes.byref(self.eb), runs.ctypes.data + b0 * run_sz, b1 - b0)
 
 
+    def run_dataflow(self, seed=0):
+        """Unit by unit in a random order that respects only the producer
+        lists (fr.dep_start / fr.deps): what the persistent kernel's
+        dataflow waits allow.  A unit that ends a superblock row backs its
+        bottom row up right after it, as the fused kernel does."""
+        import heapq
+        abi = _abi()
+        fr = self.fr
+        L = load()
+        sfx = 8 if fr.cfg.bpc == 8 else 16
+        prep = getattr(L, f"oracle_prepare_intra_edges_{sfx}bpc")
+        recon = getattr(L, f"oracle_recon_units_{sfx}bpc")
+        backup = getattr(L, f"oracle_backup_ipred_edge_{sfx}bpc")
+        n = len(fr.units)
+        ds, dp = fr.dep_start, fr.deps
+        users = [[] for _ in range(n)]
+        waiting = np.diff(ds).astype(np.int64)
+        for u in range(n):
+            for q in dp[ds[u]:ds[u + 1]]:
+                users[int(q)].append(u)
+        rng = np.random.default_rng(seed)
+        pri = rng.random(n)
+        ready = [(pri[u], u) for u in range(n) if waiting[u] == 0]
+        heapq.heapify(ready)
+        rec_sz = fr.recs.dtype.itemsize
+        e = abi.IntraEdgeBatch.from_buffer_copy(self.eb)
+        run = np.zeros(1, abi.EDGE_BACKUP_DTYPE)
+        done = 0
+        while ready:
+            _, u = heapq.heappop(ready)
+            done += 1
+            if fr.unit_rec[u] >= 0:
+                e.recs = self.recs.ctypes.data + int(fr.unit_rec[u]) * rec_sz
+                e.n_recs = 1
+                prep(ctypes.byref(e))
+            recon(ctypes.byref(self.rb), u, u + 1)
+            un = fr.units[u]
+            p = int(un["plane"])
+            w = fr.plane_wh[p][0]
+            tw, th = abi.TX_WH[un["tx"]]
+            y, x = divmod(int(un["dst_off"]), w)
+            sh = 1 << fr.sb_log2[p]
+            if fr.cfg.sb_edge_backup and (y + th) % sh == 0 and y + th < fr.plane_wh[p][1]:
+                run[0] = (p, (y + th) // sh - 1, x, tw)
+                backup(ctypes.byref(self.eb), run.ctypes.data, 1)
+            for v in users[u]:
+                waiting[v] -= 1
+                if waiting[v] == 0:
+                    heapq.heappush(ready, (pri[v], v))
+        assert done == n   # the producer graph is acyclic
+
+
 def apply_grain(case):
     """A grain.GrainCase through the oracle's dav1d_apply_grain restatement:
     returns (output planes, grain LUTs [3][73][82], scaling LUTs [3][4096])."""

@@ -31,6 +31,39 @@ def test_level_order_equals_decode_order(pkg, oracle, kw):
     assert np.array_equal(a.units, b.units)
 
 
+@pytest.mark.parametrize("kw", [dict(seed=21), dict(seed=22, cfl_frac=1.0, bpc=16, bitdepth_max=1023),
+                                dict(seed=23, width=640, height=384, tile_cols=3, tile_rows=2),
+                                dict(seed=24, tile_cols=2, sb_edge_backup=False), dict(seed=25, inter_frac=0.5)])
+def test_dataflow_order_equals_decode_order(pkg, oracle, kw):
+    """Any order the producer lists allow (the persistent kernel's dataflow
+    waits) gives the decoder's pixels."""
+    fr = _frame(**kw)
+    a = oracle.HostIntraFrame(fr)
+    a.run()
+    for seed in (1, 2):
+        b = oracle.HostIntraFrame(fr)
+        b.run_dataflow(seed)
+        for p in range(3):
+            assert np.array_equal(a.dst[p], b.dst[p]), (seed, p)
+            assert np.array_equal(a.top[p][:-1], b.top[p][:-1]), (seed, p)
+        assert np.array_equal(a.units, b.units)
+
+
+def test_producer_lists(pkg):
+    """A unit's level is one more than its highest producer's (0 without
+    producers), producers sit at lower levels, lists are duplicate-free."""
+    fr = _frame(seed=26, inter_frac=0.3)
+    n = len(fr.units)
+    lvl = np.repeat(np.arange(fr.n_levels), np.diff(fr.unit_start))
+    assert fr.dep_start[0] == 0 and fr.dep_start[-1] == len(fr.deps) and len(fr.dep_start) == n + 1
+    for u in range(n):
+        d = fr.deps[fr.dep_start[u]:fr.dep_start[u + 1]]
+        assert len(np.unique(d)) == len(d)
+        assert lvl[u] == (lvl[d].max() + 1 if len(d) else 0)
+        if fr.units["pred"][u] not in (pkg.abi.PRED_INTRA, pkg.abi.PRED_CFL):
+            assert len(d) == 0                                  # inter units read only references
+
+
 def test_schedule_invariants(pkg):
     abi = pkg.abi
     fr = _frame(seed=7)

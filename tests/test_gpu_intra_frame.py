@@ -35,11 +35,11 @@ def _frame(**kw):
     return intra.make_intra_frame(intra.IntraConfig(**kw))
 
 
-@pytest.mark.parametrize("mode", ["persistent", "fused", "staged"])
+@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged"])
 @pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023), (16, 4095)])
 def test_intra_frame(oracle, bpc, bdmax, mode):
-    """persistent: one launch per frame, waves wait on per-level counters;
-    fused: one launch per level (edges gathered in the reconstruction
+    """persistent: one launch per frame, waves wait on their producers'
+    task flags; levels: the same, waiting on per-level counters; fused: one launch per level (edges gathered in the reconstruction
     kernel, backups with the stores); staged: edge stage, unit batch and
     backup runs as three launches per level."""
     _check(oracle, _frame(seed=31, bpc=bpc, bitdepth_max=bdmax), mode=mode)
@@ -53,7 +53,7 @@ def test_intra_frame_variants(oracle, kw):
     _check(oracle, _frame(**kw))
 
 
-@pytest.mark.parametrize("mode", ["persistent", "fused", "staged"])
+@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged"])
 @pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
 def test_mixed_frame(oracle, mode, bpc, bdmax):
     """Inter blocks (put / compound avg from padded references) among the
@@ -74,16 +74,17 @@ def test_intra_frame_relaunch(oracle):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("mode", ["persistent", "fused", "staged"])
+@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged"])
 def test_intra_frame_1080p(oracle, mode):
     """A 1080p intra frame (partial superblock row at the bottom)."""
     _check(oracle, _frame(seed=37, width=1920, height=1080), mode=mode)
 
 
-def test_intra_frame_4k_persistent(oracle):
+@pytest.mark.parametrize("mode", ["persistent", "levels"])
+def test_intra_frame_4k_persistent(oracle, mode):
     """A 4K intra frame (1603 levels) through the persistent kernel, twice."""
     import torch
-    dev, ho = _check(oracle, _frame(seed=40, width=3840, height=2160))
+    dev, ho = _check(oracle, _frame(seed=40, width=3840, height=2160), mode=mode)
     dev.reset()
     dev.launch()
     torch.cuda.synchronize()

@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture one frame in a HIP graph, time replays")
-    ap.add_argument("--mode", default="persistent", choices=["persistent", "fused", "staged"])
+    ap.add_argument("--mode", default="persistent", choices=["persistent", "levels", "fused", "staged"])
     ap.add_argument("--tiles", default="1x1", help="tile columns x rows")
     a = ap.parse_args()
     import __graft_entry__ as ge
