@@ -171,6 +171,13 @@ class FilmGrainBatch(ctypes.Structure):
                 ("scratch", ctypes.c_void_p)]
 
 
+class CdefFrame(ctypes.Structure):
+    """Dav1dGpuCdefFrame: one frame of bytefn(dav1d_cdef_brow) work."""
+    _fields_ = [("in_", Plane * 3), ("out", Plane * 3), ("cdef_idx", ctypes.c_void_p), ("noskip", ctypes.c_void_p),
+                ("layout", ctypes.c_int32), ("bitdepth_max", ctypes.c_int32), ("damping", ctypes.c_int32),
+                ("pad_", ctypes.c_int32), ("y_strength", ctypes.c_uint8 * 8), ("uv_strength", ctypes.c_uint8 * 8)]
+
+
 GRAIN_W, GRAIN_H = 82, 73
 GRAIN_SCRATCH_BYTES = 3 * GRAIN_H * GRAIN_W * 2 + 3 * 4096
 
@@ -219,6 +226,10 @@ def load_lib():
             f = getattr(L, f"dav1d_gpu_apply_grain_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(FilmGrainBatch), ctypes.c_void_p]
             f.restype = ctypes.c_int
+        for bpc in (8, 16):
+            f = getattr(L, f"dav1d_gpu_cdef_frame_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(CdefFrame), ctypes.c_void_p]
+            f.restype = ctypes.c_int
         L.dav1d_gpu_recorder_new.argtypes = [ctypes.c_int] * 5
         L.dav1d_gpu_recorder_new.restype = ctypes.c_void_p
         L.dav1d_gpu_recorder_free.argtypes = [ctypes.c_void_p]
@@ -259,4 +270,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_recorder_new", "dav1d_gpu_recorder_free", "dav1d_gpu_rec_block", "dav1d_gpu_rec_residual",
     "dav1d_gpu_recorder_flush", "dav1d_gpu_recorder_stats",
     "dav1d_gpu_apply_grain_8bpc", "dav1d_gpu_apply_grain_16bpc",
+    "dav1d_cdef_dsp_init_8bpc", "dav1d_cdef_dsp_init_16bpc",
+    "dav1d_cdef_dsp_init_gpu_8bpc", "dav1d_cdef_dsp_init_gpu_16bpc",
+    "dav1d_gpu_cdef_frame_8bpc", "dav1d_gpu_cdef_frame_16bpc",
 ]

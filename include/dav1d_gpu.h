@@ -719,6 +719,66 @@ typedef struct Dav1dGpuFilmGrainBatch {
 int dav1d_gpu_apply_grain_8bpc(const Dav1dGpuFilmGrainBatch *b, void *stream);
 int dav1d_gpu_apply_grain_16bpc(const Dav1dGpuFilmGrainBatch *b, void *stream);
 
+/* ---- CDEF (the first post-filter) -----------------------
+ * Per-call tier: Dav1dCdefDSPContext (src/cdef.h:64-67; decl_cdef_fn :53-58,
+ * decl_cdef_dir_fn :60-62) with the reference's init hook name
+ * bitfn(dav1d_cdef_dsp_init) (src/cdef_tmpl.c:316-331).  fb[0] 8x8 (luma and
+ * 4:4:4 chroma), fb[1] 4x8 (4:2:2), fb[2] 4x4 (4:2:0).  `left` is pixel[h][2]. */
+enum Dav1dGpuCdefEdgeFlags {   /* CdefEdgeFlags, src/cdef.h:36-41 */
+    DGPU_CDEF_HAVE_LEFT = 1, DGPU_CDEF_HAVE_RIGHT = 2,
+    DGPU_CDEF_HAVE_TOP = 4, DGPU_CDEF_HAVE_BOTTOM = 8
+};
+#define DGPU_CDEF_TYPES(sfx, pixel, HBD)                                       \
+typedef void (*dgpu_cdef_fn_##sfx)(pixel *dst, ptrdiff_t stride,              \
+    const pixel (*left)[2], const pixel *top, const pixel *bottom,            \
+    int pri_strength, int sec_strength, int dir, int damping, int edges HBD); \
+typedef int (*dgpu_cdef_dir_fn_##sfx)(const pixel *dst, ptrdiff_t dst_stride, \
+    unsigned *var HBD);                                                       \
+typedef struct Dav1dCdefDSPContext_##sfx {                                    \
+    dgpu_cdef_dir_fn_##sfx dir;                                               \
+    dgpu_cdef_fn_##sfx fb[3];   /* 444/luma, 422, 420 */                      \
+} Dav1dCdefDSPContext_##sfx;
+DGPU_CDEF_TYPES(8bpc, uint8_t, DGPU_HBD_NONE)
+DGPU_CDEF_TYPES(16bpc, uint16_t, DGPU_HBD_ARG)
+void dav1d_cdef_dsp_init_8bpc(Dav1dCdefDSPContext_8bpc *c);
+void dav1d_cdef_dsp_init_16bpc(Dav1dCdefDSPContext_16bpc *c);
+void dav1d_cdef_dsp_init_gpu_8bpc(Dav1dCdefDSPContext_8bpc *c);
+void dav1d_cdef_dsp_init_gpu_16bpc(Dav1dCdefDSPContext_16bpc *c);
+
+/* Frame tier: bytefn(dav1d_cdef_brow) (src/cdef_apply_tmpl.c:97-309) over a
+ * whole frame, as dav1d_filter_sbrow_cdef (src/recon_tmpl.c:2076-2102) runs it
+ * superblock row by superblock row after deblocking.  Every 8x8 block reads
+ * only deblocked, pre-CDEF pixels (the reference keeps them through its
+ * cdef_line / lr_bak backups, :41-89, :132-200), so the device reads `in` and
+ * writes `out`, a distinct picture: filtered blocks, and every other pixel of
+ * the frame's 8x8 grid copied.
+ *   The grid: bw = (in[0].w + 3) >> 2 and bh = (in[0].h + 3) >> 2 4x4 units
+ * (f->bw, f->bh); blocks are 8x8 luma at even (bx, by), the last one may
+ * cover 4 px past the picture as in the reference, so both pictures must be
+ * readable / writable over ((bw + 1) & ~1) * 4 by ((bh + 1) & ~1) * 4 luma
+ * pixels (and the chroma equivalent), which dav1d's picture allocation
+ * (src/picture.c:49-66) guarantees.  Pixels outside that grid are
+ * unavailable (CDEF_HAVE_* cleared at the frame edges, :106, :127, :143-181).
+ *   cdef_idx: per 64x64 luma superblock, [(bh + 15) >> 4][(bw + 15) >> 4],
+ * lflvl[].cdef_idx (-1: not coded, skipped).  noskip: per 8x8 luma block,
+ * [(bh + 1) >> 1][(bw + 1) >> 1], nonzero when lflvl[].noskip_mask has either
+ * of the block's two bits (:159-161, :185-189). */
+typedef struct Dav1dGpuCdefFrame {
+    Dav1dGpuPlane in[3];          /* device: deblocked picture (read only)   */
+    Dav1dGpuPlane out[3];         /* device: output picture, distinct        */
+    const int8_t *cdef_idx;       /* device                                  */
+    const uint8_t *noskip;        /* device                                  */
+    int32_t layout;               /* 0 I400, 1 I420, 2 I422, 3 I444          */
+    int32_t bitdepth_max;
+    int32_t damping;              /* frame_hdr->cdef.damping (3..6)          */
+    int32_t pad_;
+    uint8_t y_strength[8];        /* frame_hdr->cdef.y_strength / uv_strength */
+    uint8_t uv_strength[8];
+} Dav1dGpuCdefFrame;
+/* Errors: -1 NULL / bad layout / in == out, -3 launch failure. */
+int dav1d_gpu_cdef_frame_8bpc(const Dav1dGpuCdefFrame *f, void *stream);
+int dav1d_gpu_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, void *stream);
+
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split
  * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).

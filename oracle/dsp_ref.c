@@ -2122,3 +2122,343 @@ int SFX(oracle_apply_grain)(const Dav1dGpuFilmGrainBatch *b)
     }
     return 0;
 }
+
+/* ================================================================== CDEF */
+/* SURVEY 8(f) row 3.  Restated from src/cdef_tmpl.c (the DSP entries) and
+ * src/cdef_apply_tmpl.c (bytefn(dav1d_cdef_brow), the frame walker), driven
+ * superblock row by superblock row as dav1d_filter_sbrow_cdef
+ * (src/recon_tmpl.c:2076-2102) does, single-threaded (have_tt = 0). */
+
+/* The primary / secondary tap directions as (dy, dx) of the two taps, the AV1
+ * CDEF direction set (dav1d_cdef_directions, src/tables.c:400-413, holds the
+ * same offsets in a 12-wide buffer, padded cyclically so dir + 2 and dir - 2
+ * need no wrap). */
+static const int8_t cdef_dyx[8][2][2] = {
+    { { -1, 1 }, { -2, 2 } }, { { 0, 1 }, { -1, 2 } }, { { 0, 1 }, { 0, 2 } }, { { 0, 1 }, { 1, 2 } },
+    { { 1, 1 }, { 2, 2 } },   { { 1, 0 }, { 2, 1 } },  { { 1, 0 }, { 2, 0 } }, { { 1, 0 }, { 2, -1 } },
+};
+
+static inline int ulog2i(unsigned v) { return 31 - __builtin_clz(v); }
+
+/* constrain(), cdef_tmpl.c:37-42 */
+static inline int cdef_constrain(int diff, int threshold, int shift)
+{
+    const int adiff = diff < 0 ? -diff : diff;
+    const int v = mini(adiff, maxi(0, threshold - (adiff >> shift)));
+    return diff < 0 ? -v : v;
+}
+
+/* cdef_filter_block_c, cdef_tmpl.c:104-215, with padding() (:44-102): the
+ * 2-px neighbourhood of the w x h block, INT16_MIN where an edge flag says
+ * the pixels are absent.  A tap reading INT16_MIN contributes nothing
+ * (constrain -> 0) and never wins the min (unsigned compare, :139) or the
+ * max (signed). */
+static void cdef_filter(pixel *dst, ptrdiff_t stride, const pixel (*left)[2], const pixel *top,
+                        const pixel *bottom, int pri, int sec, int dir, int damping, int edges,
+                        int w, int h, int bdmax)
+{
+    const ptrdiff_t ps = PX(stride);
+    int t[12][12];   /* rows -2 .. h+1, columns -2 .. w+1 */
+    for (int y = -2; y < h + 2; y++)
+        for (int x = -2; x < w + 2; x++) {
+            const int have = (y >= 0 || (edges & DGPU_CDEF_HAVE_TOP)) && (y < h || (edges & DGPU_CDEF_HAVE_BOTTOM)) &&
+                             (x >= 0 || (edges & DGPU_CDEF_HAVE_LEFT)) && (x < w || (edges & DGPU_CDEF_HAVE_RIGHT));
+            int v = INT16_MIN;
+            if (have) {
+                if (y < 0) v = top[(y + 2) * ps + x];
+                else if (y >= h) v = bottom[(y - h) * ps + x];
+                else if (x < 0) v = left[y][2 + x];
+                else v = dst[y * ps + x];
+            }
+            t[y + 2][x + 2] = v;
+        }
+    const int bd8 = bits_of(bdmax) - 8;
+    const int pri_tap = 4 - ((pri >> bd8) & 1);
+    const int pri_shift = pri ? maxi(0, damping - ulog2i((unsigned)pri)) : 0;
+    const int sec_shift = sec ? damping - ulog2i((unsigned)sec) : 0;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const int px = t[y + 2][x + 2];
+            int sum = 0, mx = px, mn = px;
+            for (int k = 0; k < 2; k++) {
+                const int tp = k ? (pri_tap & 3) | 2 : pri_tap, ts = 2 - k;
+                int s[6];
+                s[0] = t[y + 2 + cdef_dyx[dir][k][0]][x + 2 + cdef_dyx[dir][k][1]];
+                s[1] = t[y + 2 - cdef_dyx[dir][k][0]][x + 2 - cdef_dyx[dir][k][1]];
+                s[2] = t[y + 2 + cdef_dyx[(dir + 2) & 7][k][0]][x + 2 + cdef_dyx[(dir + 2) & 7][k][1]];
+                s[3] = t[y + 2 - cdef_dyx[(dir + 2) & 7][k][0]][x + 2 - cdef_dyx[(dir + 2) & 7][k][1]];
+                s[4] = t[y + 2 + cdef_dyx[(dir + 6) & 7][k][0]][x + 2 + cdef_dyx[(dir + 6) & 7][k][1]];
+                s[5] = t[y + 2 - cdef_dyx[(dir + 6) & 7][k][0]][x + 2 - cdef_dyx[(dir + 6) & 7][k][1]];
+                if (pri) {
+                    sum += tp * cdef_constrain(s[0] - px, pri, pri_shift);
+                    sum += tp * cdef_constrain(s[1] - px, pri, pri_shift);
+                }
+                if (sec)
+                    for (int i = 2; i < 6; i++) sum += ts * cdef_constrain(s[i] - px, sec, sec_shift);
+                for (int i = pri ? 0 : 2; i < 6; i++) {
+                    if ((unsigned)s[i] < (unsigned)mn) mn = s[i];
+                    if (s[i] > mx) mx = s[i];
+                }
+            }
+            int v = px + ((sum - (sum < 0) + 8) >> 4);
+            if (pri && sec) v = clampi(v, mn, mx);   /* only the pri+sec path clips, :164 vs :183 / :209 */
+            dst[y * ps + x] = (pixel)v;
+        }
+}
+
+/* cdef_find_dir_c, cdef_tmpl.c:238-304 */
+static int cdef_find_dir(const pixel *img, ptrdiff_t stride, unsigned *var, int bdmax)
+{
+    const int bd8 = bits_of(bdmax) - 8;
+    int hv[2][8] = { { 0 } }, diag[2][15] = { { 0 } }, alt[4][11] = { { 0 } };
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+            const int px = (img[y * PX(stride) + x] >> bd8) - 128;
+            diag[0][y + x] += px;
+            alt[0][y + (x >> 1)] += px;
+            hv[0][y] += px;
+            alt[1][3 + y - (x >> 1)] += px;
+            diag[1][7 + y - x] += px;
+            alt[2][3 - (y >> 1) + x] += px;
+            hv[1][x] += px;
+            alt[3][(y >> 1) + x] += px;
+        }
+    static const unsigned div_table[7] = { 840, 420, 280, 210, 168, 140, 120 };
+    unsigned cost[8] = { 0 };
+    for (int n = 0; n < 8; n++) {
+        cost[2] += (unsigned)(hv[0][n] * hv[0][n]);
+        cost[6] += (unsigned)(hv[1][n] * hv[1][n]);
+    }
+    cost[2] *= 105;
+    cost[6] *= 105;
+    for (int n = 0; n < 7; n++) {
+        cost[0] += (unsigned)(diag[0][n] * diag[0][n] + diag[0][14 - n] * diag[0][14 - n]) * div_table[n];
+        cost[4] += (unsigned)(diag[1][n] * diag[1][n] + diag[1][14 - n] * diag[1][14 - n]) * div_table[n];
+    }
+    cost[0] += (unsigned)(diag[0][7] * diag[0][7]) * 105;
+    cost[4] += (unsigned)(diag[1][7] * diag[1][7]) * 105;
+    for (int n = 0; n < 4; n++) {
+        unsigned c = 0;
+        for (int m = 0; m < 5; m++) c += (unsigned)(alt[n][3 + m] * alt[n][3 + m]);
+        c *= 105;
+        for (int m = 0; m < 3; m++)
+            c += (unsigned)(alt[n][m] * alt[n][m] + alt[n][10 - m] * alt[n][10 - m]) * div_table[2 * m + 1];
+        cost[2 * n + 1] = c;
+    }
+    int best = 0;
+    for (int n = 1; n < 8; n++)
+        if (cost[n] > cost[best]) best = n;
+    *var = (cost[best] - cost[best ^ 4]) >> 10;
+    return best;
+}
+
+static void cdef_fb8x8(pixel *d, ptrdiff_t s, const pixel (*l)[2], const pixel *t, const pixel *b, int pri, int sec,
+                       int dir, int damping, int edges BDPARAM)
+{ BD_DECL cdef_filter(d, s, l, t, b, pri, sec, dir, damping, edges, 8, 8, bdmax_); }
+static void cdef_fb4x8(pixel *d, ptrdiff_t s, const pixel (*l)[2], const pixel *t, const pixel *b, int pri, int sec,
+                       int dir, int damping, int edges BDPARAM)
+{ BD_DECL cdef_filter(d, s, l, t, b, pri, sec, dir, damping, edges, 4, 8, bdmax_); }
+static void cdef_fb4x4(pixel *d, ptrdiff_t s, const pixel (*l)[2], const pixel *t, const pixel *b, int pri, int sec,
+                       int dir, int damping, int edges BDPARAM)
+{ BD_DECL cdef_filter(d, s, l, t, b, pri, sec, dir, damping, edges, 4, 4, bdmax_); }
+static int cdef_dir_entry(const pixel *img, ptrdiff_t s, unsigned *var BDPARAM)
+{ BD_DECL return cdef_find_dir(img, s, var, bdmax_); }
+
+/* bitfn(dav1d_cdef_dsp_init), cdef_tmpl.c:316-331 */
+#if BITDEPTH == 8
+void oracle_cdef_dsp_init_8bpc(Dav1dCdefDSPContext_8bpc *c)
+#else
+void oracle_cdef_dsp_init_16bpc(Dav1dCdefDSPContext_16bpc *c)
+#endif
+{
+    c->dir = cdef_dir_entry;
+    c->fb[0] = cdef_fb8x8;
+    c->fb[1] = cdef_fb4x8;
+    c->fb[2] = cdef_fb4x4;
+}
+
+/* adjust_strength, cdef_apply_tmpl.c:91-95 */
+static int cdef_adjust_strength(int strength, unsigned var)
+{
+    if (!var) return 0;
+    const int i = var >> 6 ? mini(ulog2i(var >> 6), 12) : 0;
+    return (strength * (4 + i) + 8) >> 4;
+}
+
+typedef struct {
+    const Dav1dGpuCdefFrame *f;
+    pixel *p[3];                 /* the picture being filtered in place       */
+    ptrdiff_t ps[3];             /* strides in pixels                         */
+    pixel *line[2][3];           /* f->lf.cdef_line[toggle][plane], 2 rows    */
+    int toggle;                  /* tc->top_pre_cdef_toggle                   */
+    int bw, bh, bdmax;
+} CdefWalk;
+
+/* backup2lines, cdef_apply_tmpl.c:41-63 (positive strides) */
+static void cdef_backup2lines(CdefWalk *c, pixel *const ptrs[3], int dst_toggle)
+{
+    const int layout = c->f->layout;
+    memcpy(c->line[dst_toggle][0], ptrs[0] + 6 * c->ps[0], 2 * c->ps[0] * sizeof(pixel));
+    if (layout == 0) return;
+    const int off = layout == 1 ? 2 : 6;
+    for (int pl = 1; pl < 3; pl++)
+        memcpy(c->line[dst_toggle][pl], ptrs[pl] + off * c->ps[pl], 2 * c->ps[pl] * sizeof(pixel));
+}
+
+/* backup2x8, cdef_apply_tmpl.c:65-89 */
+static void cdef_backup2x8(CdefWalk *c, pixel dst[3][8][2], pixel *const src[3], int x_off, int flag)
+{
+    const int layout = c->f->layout;
+    if (flag & 1)
+        for (int y = 0; y < 8; y++) memcpy(dst[0][y], &src[0][y * c->ps[0] + x_off - 2], 2 * sizeof(pixel));
+    if (layout == 0 || !(flag & 2)) return;
+    const int ss_ver = layout == 1, ss_hor = layout != 3;
+    x_off >>= ss_hor;
+    for (int y = 0; y < (8 >> ss_ver); y++) {
+        memcpy(dst[1][y], &src[1][y * c->ps[1] + x_off - 2], 2 * sizeof(pixel));
+        memcpy(dst[2][y], &src[2][y * c->ps[2] + x_off - 2], 2 * sizeof(pixel));
+    }
+}
+
+/* bytefn(dav1d_cdef_brow), cdef_apply_tmpl.c:97-309, have_tt = 0 */
+static void cdef_brow(CdefWalk *c, pixel *const p[3], int by_start, int by_end)
+{
+    const Dav1dGpuCdefFrame *f = c->f;
+    const int bd8 = bits_of(c->bdmax) - 8;
+    int edges = DGPU_CDEF_HAVE_BOTTOM | (by_start > 0 ? DGPU_CDEF_HAVE_TOP : 0);
+    pixel *ptrs[3] = { p[0], p[1], p[2] };
+    const int sbsz = 16, sb64w = (c->bw + 15) >> 4, b8w = (c->bw + 1) >> 1;
+    const int damping = f->damping + bd8;
+    const int layout = f->layout;
+    const int uv_idx = 3 - layout;
+    const int ss_ver = layout == 1, ss_hor = layout != 3;
+    static const uint8_t uv_dirs[2][8] = { { 0, 1, 2, 3, 4, 5, 6, 7 }, { 7, 0, 2, 4, 5, 6, 6, 6 } };
+    const uint8_t *uv_dir = uv_dirs[layout == 2];
+    static void (*const fb[3])(pixel *, ptrdiff_t, const pixel (*)[2], const pixel *, const pixel *, int, int, int,
+                               int, int BDPARAM) = { cdef_fb8x8, cdef_fb4x8, cdef_fb4x4 };
+#if BITDEPTH == 16
+    const int bitdepth_max = c->bdmax;
+#endif
+    pixel lr_bak[2][3][8][2];
+    int bit = 0;
+    for (int by = by_start; by < by_end; by += 2, edges |= DGPU_CDEF_HAVE_TOP) {
+        const int tf = c->toggle;
+        if (by + 2 >= c->bh) edges &= ~DGPU_CDEF_HAVE_BOTTOM;
+        if (edges & DGPU_CDEF_HAVE_BOTTOM) cdef_backup2lines(c, ptrs, !tf);
+        pixel *iptrs[3] = { ptrs[0], ptrs[1], ptrs[2] };
+        edges &= ~DGPU_CDEF_HAVE_LEFT;
+        edges |= DGPU_CDEF_HAVE_RIGHT;
+        int prev_flag = 0, last_skip = 1;
+        for (int sbx = 0; sbx < sb64w; sbx++, edges |= DGPU_CDEF_HAVE_LEFT) {
+            const int cdef_idx = f->cdef_idx[(by >> 4) * sb64w + sbx];
+            if (cdef_idx == -1 || (!f->y_strength[cdef_idx] && !f->uv_strength[cdef_idx])) {
+                last_skip = 1;
+                goto next_sb;
+            }
+            const int y_lvl = f->y_strength[cdef_idx], uv_lvl = f->uv_strength[cdef_idx];
+            const int flag = !!y_lvl + (!!uv_lvl << 1);
+            const int y_pri_lvl = (y_lvl >> 2) << bd8;
+            int y_sec_lvl = y_lvl & 3;
+            y_sec_lvl += y_sec_lvl == 3;
+            y_sec_lvl <<= bd8;
+            const int uv_pri_lvl = (uv_lvl >> 2) << bd8;
+            int uv_sec_lvl = uv_lvl & 3;
+            uv_sec_lvl += uv_sec_lvl == 3;
+            uv_sec_lvl <<= bd8;
+            pixel *bptrs[3] = { iptrs[0], iptrs[1], iptrs[2] };
+            for (int bx = sbx * sbsz; bx < mini((sbx + 1) * sbsz, c->bw); bx += 2, edges |= DGPU_CDEF_HAVE_LEFT) {
+                if (bx + 2 >= c->bw) edges &= ~DGPU_CDEF_HAVE_RIGHT;
+                if (!f->noskip[(by >> 1) * b8w + (bx >> 1)]) {
+                    last_skip = 1;
+                    goto next_b;
+                }
+                const int do_left = last_skip ? flag : (prev_flag ^ flag) & flag;
+                prev_flag = flag;
+                if (do_left && (edges & DGPU_CDEF_HAVE_LEFT)) cdef_backup2x8(c, lr_bak[bit], bptrs, 0, do_left);
+                if (edges & DGPU_CDEF_HAVE_RIGHT) cdef_backup2x8(c, lr_bak[!bit], bptrs, 8, flag);
+                int dir = 0;
+                unsigned variance = 0;
+                if (y_pri_lvl || uv_pri_lvl) dir = cdef_find_dir(bptrs[0], c->ps[0] * (ptrdiff_t)sizeof(pixel),
+                                                                 &variance, c->bdmax);
+                const pixel *top = &c->line[tf][0][bx * 4], *bot = bptrs[0] + 8 * c->ps[0];
+                if (y_pri_lvl) {
+                    const int adj = cdef_adjust_strength(y_pri_lvl, variance);
+                    if (adj || y_sec_lvl)
+                        fb[0](bptrs[0], c->ps[0] * sizeof(pixel), (const pixel (*)[2])lr_bak[bit][0], top, bot, adj,
+                              y_sec_lvl, dir, damping, edges BDARG);
+                } else if (y_sec_lvl) {
+                    fb[0](bptrs[0], c->ps[0] * sizeof(pixel), (const pixel (*)[2])lr_bak[bit][0], top, bot, 0,
+                          y_sec_lvl, 0, damping, edges BDARG);
+                }
+                if (uv_lvl && layout) {
+                    const int uvdir = uv_pri_lvl ? uv_dir[dir] : 0;
+                    for (int pl = 1; pl <= 2; pl++) {
+                        top = &c->line[tf][pl][(bx * 4) >> ss_hor];
+                        bot = bptrs[pl] + (8 >> ss_ver) * c->ps[pl];
+                        fb[uv_idx](bptrs[pl], c->ps[pl] * sizeof(pixel), (const pixel (*)[2])lr_bak[bit][pl], top,
+                                   bot, uv_pri_lvl, uv_sec_lvl, uvdir, damping - 1, edges BDARG);
+                    }
+                }
+                bit ^= 1;
+                last_skip = 0;
+            next_b:
+                bptrs[0] += 8;
+                bptrs[1] += 8 >> ss_hor;
+                bptrs[2] += 8 >> ss_hor;
+            }
+        next_sb:
+            iptrs[0] += sbsz * 4;
+            iptrs[1] += (sbsz * 4) >> ss_hor;
+            iptrs[2] += (sbsz * 4) >> ss_hor;
+        }
+        ptrs[0] += 8 * c->ps[0];
+        ptrs[1] += (8 * c->ps[1]) >> ss_ver;
+        ptrs[2] += (8 * c->ps[2]) >> ss_ver;
+        c->toggle ^= 1;
+    }
+}
+
+/* The frame: `out` <- `in` over the 8x8 grid, then dav1d_filter_sbrow_cdef
+ * (recon_tmpl.c:2076-2102) for every superblock row of sb_step 16 (sb128 = 0)
+ * or 32 (sb128 = 1) 4x4 units, filtering `out` in place. */
+#if BITDEPTH == 8
+int oracle_cdef_frame_8bpc(const Dav1dGpuCdefFrame *f, int sb128)
+#else
+int oracle_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, int sb128)
+#endif
+{
+    if (!f || f->layout < 0 || f->layout > 3 || !f->cdef_idx || !f->noskip) return -1;
+    CdefWalk c;
+    memset(&c, 0, sizeof(c));
+    c.f = f;
+    c.bdmax = BITDEPTH == 8 ? 255 : f->bitdepth_max;
+    c.bw = (f->in[0].w + 3) >> 2;
+    c.bh = (f->in[0].h + 3) >> 2;
+    const int np = f->layout ? 3 : 1, ss_hor = f->layout != 3, ss_ver = f->layout == 1;
+    const int gw = ((c.bw + 1) & ~1) * 4, gh = ((c.bh + 1) & ~1) * 4;
+    for (int pl = 0; pl < np; pl++) {
+        const int w = pl ? gw >> ss_hor : gw, h = pl ? gh >> ss_ver : gh;
+        c.p[pl] = (pixel *)f->out[pl].data;
+        c.ps[pl] = PX(f->out[pl].stride);
+        for (int y = 0; y < h; y++)
+            memcpy(c.p[pl] + y * c.ps[pl], (const pixel *)f->in[pl].data + y * PX(f->in[pl].stride),
+                   (size_t)w * sizeof(pixel));
+        for (int t = 0; t < 2; t++) c.line[t][pl] = calloc((size_t)2 * c.ps[pl], sizeof(pixel));
+    }
+    const int sbsz = sb128 ? 32 : 16, sbh = (c.bh + sbsz - 1) / sbsz;
+    for (int sby = 0; sby < sbh; sby++) {
+        const int start = sby * sbsz, y = start * 4;
+        pixel *p[3] = { c.p[0] + y * c.ps[0], NULL, NULL };
+        for (int pl = 1; pl < np; pl++) p[pl] = c.p[pl] + ((y * c.ps[pl]) >> ss_ver);
+        if (sby) {
+            pixel *p_up[3] = { p[0] - 8 * c.ps[0], NULL, NULL };
+            for (int pl = 1; pl < np; pl++) p_up[pl] = p[pl] - ((8 * c.ps[pl]) >> ss_ver);
+            cdef_brow(&c, p_up, start - 2, start);
+        }
+        const int n_blks = sbsz - 2 * (sby + 1 < sbh);
+        cdef_brow(&c, p, start, mini(start + n_blks, c.bh));
+    }
+    for (int pl = 0; pl < np; pl++)
+        for (int t = 0; t < 2; t++) free(c.line[t][pl]);
+    return 0;
+}

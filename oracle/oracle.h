@@ -28,4 +28,8 @@ int oracle_prep_grain_8bpc(const Dav1dGpuFilmGrainData *d, int layout, int bdmax
 int oracle_prep_grain_16bpc(const Dav1dGpuFilmGrainData *d, int layout, int bdmax, int16_t *grain, uint8_t *scaling);
 int oracle_apply_grain_8bpc(const Dav1dGpuFilmGrainBatch *b);
 int oracle_apply_grain_16bpc(const Dav1dGpuFilmGrainBatch *b);
+void oracle_cdef_dsp_init_8bpc(Dav1dCdefDSPContext_8bpc *c);
+void oracle_cdef_dsp_init_16bpc(Dav1dCdefDSPContext_16bpc *c);
+int oracle_cdef_frame_8bpc(const Dav1dGpuCdefFrame *f, int sb128);
+int oracle_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, int sb128);
 #endif

@@ -407,3 +407,39 @@ def apply_grain(case):
     d = abi.FilmGrainData.from_buffer_copy(case.data)
     assert prep(ctypes.byref(d), case.layout, case.bitdepth_max, g.ctypes.data, sc.ctypes.data) == 0
     return outs, g, sc
+
+
+def cdef_frame(case, sb128=0):
+    """A cdef.CdefCase through the oracle's dav1d_filter_sbrow_cdef /
+    dav1d_cdef_brow restatement (in place on a copy, with the reference's
+    line and column backups); returns the output planes over the 8x8 grid."""
+    import dav1d_mirror_amd.cdef as cdef
+    abi = _abi()
+    L = load()
+    sfx = 8 if case.bpc == 8 else 16
+    ins = [np.ascontiguousarray(a) for a in case.planes]
+    outs = [np.zeros_like(a) for a in ins]
+    idx = np.ascontiguousarray(case.cdef_idx, np.int8)
+    nsk = np.ascontiguousarray(case.noskip, np.uint8)
+    f = cdef.fill_frame(abi.CdefFrame(), case, [(a.ctypes.data, a.shape[1]) for a in ins],
+                        [(a.ctypes.data, a.shape[1]) for a in outs], idx.ctypes.data, nsk.ctypes.data)
+    fn = getattr(L, f"oracle_cdef_frame_{sfx}bpc")
+    fn.argtypes = [ctypes.POINTER(abi.CdefFrame), ctypes.c_int]
+    fn.restype = ctypes.c_int
+    assert fn(ctypes.byref(f), sb128) == 0
+    return outs
+
+
+def cdef_dsp(bpc):
+    """(dir, fb[3]) of the oracle's bitfn(dav1d_cdef_dsp_init) as ctypes callables."""
+    L = load()
+    hbd = [] if bpc == 8 else [ctypes.c_int]
+    dir_t = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_ssize_t, ctypes.POINTER(ctypes.c_uint), *hbd)
+    fb_t = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, *hbd)
+
+    class Ctx(ctypes.Structure):
+        _fields_ = [("dir", dir_t), ("fb", fb_t * 3)]
+    c = Ctx()
+    getattr(L, f"oracle_cdef_dsp_init_{bpc}bpc")(ctypes.byref(c))
+    return c

@@ -395,6 +395,58 @@ static void BD(check_itx)(void) {
     free(c_dst.buf); free(a_dst.buf);
 }
 
+/* init_tmp, tests/checkasm/cdef.c:42-53: under- / overflow / random fills */
+static void BD(cdef_fill)(pixel *buf, int n, int bdmax) {
+    const int fill_type = rnd() & 7;
+    for (int i = 0; i < n; i++)
+        buf[i] = fill_type == 0 ? (rnd() & 1) : fill_type == 1 ? bdmax - (rnd() & 1) : (rnd() & bdmax);
+}
+
+/* tests/checkasm/cdef.c:55-144: cdef_dir on random blocks, every fb entry
+ * over strengths (pri / sec / both) x 8 directions x 16 edge sets; the whole
+ * source buffer compared, so writes outside the w x h block fail too. */
+static void BD(check_cdef)(void) {
+    BD(Dav1dCdefDSPContext) ref, gpu;
+    BD(oracle_cdef_dsp_init)(&ref);
+    BD(dav1d_cdef_dsp_init)(&gpu);
+    for (int i = 0; i < (g_quick ? 64 : 512); i++) {
+        pixel src[64];
+        const int bdmax = BDMAX_RAND();
+        BD(cdef_fill)(src, 64, bdmax);
+        unsigned cv = 0, av = 1;
+        const int cd = ref.dir(src, 8 * sizeof(pixel), &cv HBD_ARG(bdmax));
+        const int ad = gpu.dir(src, 8 * sizeof(pixel), &av HBD_ARG(bdmax));
+        report("cdef_dir", cd == ad && cv == av, "dir %d/%d var %u/%u", cd, ad, cv, av);
+    }
+    static const int dims[3][2] = { { 8, 8 }, { 4, 8 }, { 4, 4 } };
+    for (int f = 0; f < 3; f++) {
+        const int w = dims[f][0], h = dims[f][1];
+        for (int s = 1; s <= 3; s++)
+            for (int dir = 0; dir < 8; dir++)
+                for (int edges = 0; edges <= 15; edges++) {
+                    pixel c_src[16 * 10 + 16], a_src[16 * 10 + 16], top_buf[16 * 2 + 16], bot_buf[16 * 2 + 16];
+                    pixel left[8][2];
+                    const int bdmax = BDMAX_RAND();
+                    const int bd8 = (bdmax == 255 ? 8 : bdmax == 1023 ? 10 : 12) - 8;
+                    BD(cdef_fill)(c_src, 16 * 10 + 16, bdmax);
+                    BD(cdef_fill)(top_buf, 16 * 2 + 16, bdmax);
+                    BD(cdef_fill)(bot_buf, 16 * 2 + 16, bdmax);
+                    BD(cdef_fill)(&left[0][0], 16, bdmax);
+                    memcpy(a_src, c_src, sizeof(c_src));
+                    const int pri = s & 2 ? (1 + (int)(rnd() % 15)) << bd8 : 0;
+                    const int sec = s & 1 ? 1 << ((rnd() % 3) + bd8) : 0;
+                    const int damping = 3 + (rnd() & 3) + bd8 - (w == 4 || (rnd() & 1));
+                    const ptrdiff_t stride = 16 * sizeof(pixel);
+                    ref.fb[f](c_src + 8, stride, (const pixel (*)[2])left, top_buf + 8, bot_buf + 8, pri, sec, dir,
+                              damping, edges HBD_ARG(bdmax));
+                    gpu.fb[f](a_src + 8, stride, (const pixel (*)[2])left, top_buf + 8, bot_buf + 8, pri, sec, dir,
+                              damping, edges HBD_ARG(bdmax));
+                    report("cdef_filter", !memcmp(c_src, a_src, sizeof(c_src)),
+                           "%dx%d pri %d sec %d dir %d damping %d edges %d", w, h, pri, sec, dir, damping, edges);
+                }
+    }
+}
+
 #undef pixel
 #undef coef
 #undef BD
