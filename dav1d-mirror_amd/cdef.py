@@ -28,7 +28,7 @@ class CdefCase:
     y_strength: list       # 8 entries, (pri << 2) | sec
     uv_strength: list
     cdef_idx: np.ndarray   # int8 [(bh + 15) >> 4][(bw + 15) >> 4]
-    noskip: np.ndarray     # uint8 [(bh + 1) >> 1][(bw + 1) >> 1]
+    noskip: np.ndarray     # uint8 [bh >> 1][bw >> 1]
     planes: list           # 1 or 3 pixel arrays over the 8x8 grid (deblocked picture)
 
     @property
@@ -38,8 +38,7 @@ class CdefCase:
     @property
     def grid(self):
         """Luma size of the 8x8 block grid the reference walks (f->bw, f->bh rounded to 8 px)."""
-        bw, bh = (self.width + 3) >> 2, (self.height + 3) >> 2
-        return ((bw + 1) & ~1) * 4, ((bh + 1) & ~1) * 4
+        return ((self.width + 7) >> 3) * 8, ((self.height + 7) >> 3) * 8
 
     def plane_wh(self, p):
         """Visible size of plane p."""
@@ -74,8 +73,8 @@ def make_cdef_case(seed=1, width=256, height=128, bpc=8, bitdepth_max=255, layou
     rng = np.random.default_rng(seed)
     bdmax = 255 if bpc == 8 else bitdepth_max
     pdt = np.uint8 if bpc == 8 else np.uint16
-    bw, bh = (width + 3) >> 2, (height + 3) >> 2
-    gw, gh = ((bw + 1) & ~1) * 4, ((bh + 1) & ~1) * 4
+    bw, bh = ((width + 7) >> 3) << 1, ((height + 7) >> 3) << 1   # f->bw, f->bh (src/decode.c:3598)
+    gw, gh = bw * 4, bh * 4
     sx, sy = int(layout != 3), int(layout == 1)
     planes = [_content(rng, gh, gw, bdmax).astype(pdt)]
     if layout:
@@ -90,7 +89,7 @@ def make_cdef_case(seed=1, width=256, height=128, bpc=8, bitdepth_max=255, layou
     sbw, sbh = (bw + 15) >> 4, (bh + 15) >> 4
     cdef_idx = rng.integers(0, n_idx, (sbh, sbw)).astype(np.int8)
     cdef_idx[rng.random((sbh, sbw)) < p_skip_sb] = -1
-    noskip = (rng.random(((bh + 1) >> 1, (bw + 1) >> 1)) < p_noskip).astype(np.uint8)
+    noskip = (rng.random((bh >> 1, bw >> 1)) < p_noskip).astype(np.uint8)
     d = int(rng.integers(3, 7)) if damping is None else damping
     return CdefCase(bpc, bdmax, layout, width, height, d, ys, uvs, cdef_idx, noskip, planes)
 

@@ -372,11 +372,11 @@ static int launch_cdef(const Dav1dGpuCdefFrame *f, hipStream_t stream) {
     if (w <= 0 || h <= 0 || f->damping < 3 || f->damping > 6) return -1;
     for (int i = 0; i < 8; i++)
         if (f->y_strength[i] > 63 || f->uv_strength[i] > 63) return -1;
-    const int bw = (w + 3) >> 2, bh = (h + 3) >> 2;
-    a.gw = ((bw + 1) & ~1) * 4;
-    a.gh = ((bh + 1) & ~1) * 4;
-    a.b8w = (bw + 1) >> 1;
-    a.b8h = (bh + 1) >> 1;
+    const int bw = ((w + 7) >> 3) << 1, bh = ((h + 7) >> 3) << 1;   // f->bw, f->bh (src/decode.c:3598)
+    a.gw = bw * 4;
+    a.gh = bh * 4;
+    a.b8w = bw >> 1;
+    a.b8h = bh >> 1;
     a.sbw = (bw + 15) >> 4;
     a.sbh = (bh + 15) >> 4;
     a.idx = f->cdef_idx;

@@ -752,16 +752,17 @@ void dav1d_cdef_dsp_init_gpu_16bpc(Dav1dCdefDSPContext_16bpc *c);
  * cdef_line / lr_bak backups, :41-89, :132-200), so the device reads `in` and
  * writes `out`, a distinct picture: filtered blocks, and every other pixel of
  * the frame's 8x8 grid copied.
- *   The grid: bw = (in[0].w + 3) >> 2 and bh = (in[0].h + 3) >> 2 4x4 units
- * (f->bw, f->bh); blocks are 8x8 luma at even (bx, by), the last one may
- * cover 4 px past the picture as in the reference, so both pictures must be
- * readable / writable over ((bw + 1) & ~1) * 4 by ((bh + 1) & ~1) * 4 luma
- * pixels (and the chroma equivalent), which dav1d's picture allocation
- * (src/picture.c:49-66) guarantees.  Pixels outside that grid are
- * unavailable (CDEF_HAVE_* cleared at the frame edges, :106, :127, :143-181).
+ *   The grid: f->bw = ((in[0].w + 7) >> 3) << 1 by f->bh = ((in[0].h + 7) >> 3)
+ * << 1 4x4 units (src/decode.c:3598-3599); blocks are 8x8 luma at even
+ * (bx, by), the last one may cover 4 px past the picture as in the
+ * reference, so both pictures must be readable / writable over 4 * bw by
+ * 4 * bh luma pixels (and the chroma equivalent), which dav1d's picture
+ * allocation (src/picture.c:49-66) guarantees; data and strides aligned to
+ * 4 pixels.  Pixels outside that grid are unavailable (CDEF_HAVE_* cleared
+ * at the frame edges, :106, :127, :143-181).
  *   cdef_idx: per 64x64 luma superblock, [(bh + 15) >> 4][(bw + 15) >> 4],
  * lflvl[].cdef_idx (-1: not coded, skipped).  noskip: per 8x8 luma block,
- * [(bh + 1) >> 1][(bw + 1) >> 1], nonzero when lflvl[].noskip_mask has either
+ * [bh >> 1][bw >> 1], nonzero when lflvl[].noskip_mask has either
  * of the block's two bits (:159-161, :185-189). */
 typedef struct Dav1dGpuCdefFrame {
     Dav1dGpuPlane in[3];          /* device: deblocked picture (read only)   */
@@ -775,7 +776,8 @@ typedef struct Dav1dGpuCdefFrame {
     uint8_t y_strength[8];        /* frame_hdr->cdef.y_strength / uv_strength */
     uint8_t uv_strength[8];
 } Dav1dGpuCdefFrame;
-/* Errors: -1 NULL / bad layout / in == out, -3 launch failure. */
+/* Errors: -1 NULL / bad layout / in == out / bad damping or strength,
+ * -3 launch failure, -4 misaligned planes. */
 int dav1d_gpu_cdef_frame_8bpc(const Dav1dGpuCdefFrame *f, void *stream);
 int dav1d_gpu_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, void *stream);
 

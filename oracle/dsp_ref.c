@@ -2432,10 +2432,10 @@ int oracle_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, int sb128)
     memset(&c, 0, sizeof(c));
     c.f = f;
     c.bdmax = BITDEPTH == 8 ? 255 : f->bitdepth_max;
-    c.bw = (f->in[0].w + 3) >> 2;
-    c.bh = (f->in[0].h + 3) >> 2;
+    c.bw = ((f->in[0].w + 7) >> 3) << 1;   /* f->bw, f->bh: src/decode.c:3598-3599 */
+    c.bh = ((f->in[0].h + 7) >> 3) << 1;
     const int np = f->layout ? 3 : 1, ss_hor = f->layout != 3, ss_ver = f->layout == 1;
-    const int gw = ((c.bw + 1) & ~1) * 4, gh = ((c.bh + 1) & ~1) * 4;
+    const int gw = c.bw * 4, gh = c.bh * 4;
     for (int pl = 0; pl < np; pl++) {
         const int w = pl ? gw >> ss_hor : gw, h = pl ? gh >> ss_ver : gh;
         c.p[pl] = (pixel *)f->out[pl].data;

@@ -103,7 +103,7 @@ def np_cdef_frame(case):
     src/cdef_apply_tmpl.c:124-296)."""
     bdmax, lay = case.bitdepth_max, case.layout
     bd8 = bdmax.bit_length() - 8
-    bw, bh = (case.width + 3) >> 2, (case.height + 3) >> 2
+    bw, bh = ((case.width + 7) >> 3) << 1, ((case.height + 7) >> 3) << 1
     sx, sy = int(lay != 3), int(lay == 1)
     pads, outs = [], []
     for a in case.planes:
