@@ -32,6 +32,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
 #include "runtime.hpp"
@@ -42,13 +44,17 @@ constexpr int kNone = -32768;
 
 // (dy, dx) of a direction's two taps: the AV1 CDEF direction set
 // (dav1d_cdef_directions, src/tables.c:400-413, as offsets in a 12-wide
-// buffer with cyclic padding for dir +- 2)
-__constant__ static const int8_t kCdefDyx[8][2][2] = {
-    { { -1, 1 }, { -2, 2 } }, { { 0, 1 }, { -1, 2 } }, { { 0, 1 }, { 0, 2 } }, { { 0, 1 }, { 1, 2 } },
-    { { 1, 1 }, { 2, 2 } },   { { 1, 0 }, { 2, 1 } },  { { 1, 0 }, { 2, 0 } }, { { 1, 0 }, { 2, -1 } },
-};
-// uv_dirs, src/cdef_apply_tmpl.c:115-117 (4:2:2 remaps the luma direction)
-__constant__ static const uint8_t kUvDir422[8] = { 7, 0, 2, 4, 5, 6, 6, 6 };
+// buffer with cyclic padding for dir +- 2).  Held as nibbles (value + 2,
+// direction d in bits 4d..4d+3) so a lane-varying direction costs shifts,
+// not a memory load:
+//   k = 0: dy -1 0 0 0 1 1 1 1, dx 1 1 1 1 1 0 0 0
+//   k = 1: dy -2 -1 0 1 2 2 2 2, dx 2 2 2 2 2 1 0 -1
+constexpr uint32_t kDy0 = 0x33332221u, kDx0 = 0x22233333u, kDy1 = 0x44443210u, kDx1 = 0x12344444u;
+__device__ __forceinline__ int dir_nib(uint32_t c, int d) { return (int)((c >> (4 * d)) & 15) - 2; }
+__device__ __forceinline__ int dir_off(int d, int k, int S) {
+    return k ? dir_nib(kDy1, d) * S + dir_nib(kDx1, d) : dir_nib(kDy0, d) * S + dir_nib(kDx0, d);
+}
+
 
 __device__ __forceinline__ int ulog2d(unsigned v) { return 31 - __builtin_clz(v); }
 
@@ -72,9 +78,9 @@ struct CdefTaps {
         tap1 = (tap0 & 3) | 2;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            o[k][0] = kCdefDyx[dir][k][0] * S + kCdefDyx[dir][k][1];
-            o[k][1] = kCdefDyx[(dir + 2) & 7][k][0] * S + kCdefDyx[(dir + 2) & 7][k][1];
-            o[k][2] = kCdefDyx[(dir + 6) & 7][k][0] * S + kCdefDyx[(dir + 6) & 7][k][1];
+            o[k][0] = dir_off(dir, k, S);
+            o[k][1] = dir_off((dir + 2) & 7, k, S);
+            o[k][2] = dir_off((dir + 6) & 7, k, S);
         }
     }
     // one output pixel from the int16 tile at c (the pixel itself)
@@ -222,30 +228,58 @@ template <int BPC> struct CdefArgs {
 
 // Stage rows [y0 - 2, y0 + H + 2) and columns [x0 - 4, x0 + W + 4) of one
 // plane into an int16 tile of row stride W + 8; INT16_MIN outside the grid
-// (gw x gh: multiples of 4, so a 4-px group is wholly in or out).
+// (gw x gh: multiples of 4, so a 4-px group is wholly in or out).  load()
+// issues every global load of the thread; store() writes the tile, so the
+// three planes' loads are all in flight before the first store waits.
 template <int BPC, int W, int H>
-__device__ __forceinline__ void stage(int16_t *t, const typename Px<BPC>::pixel *src, int stride, int x0, int y0,
-                                      int gw, int gh) {
-    constexpr int G = (W + 8) / 4, R = H + 4, S = W + 8;
-    for (int i = threadIdx.x; i < G * R; i += blockDim.x) {
-        const int r = i / G, g = i - r * G;
-        const int Y = y0 - 2 + r, X = x0 - 4 + 4 * g;
-        int16_t v[4] = { kNone, kNone, kNone, kNone };
-        if (Y >= 0 && Y < gh && X >= 0 && X < gw) Quad<BPC>::load(src + (size_t)Y * stride + X, v);
-        *reinterpret_cast<uint2 *>(&t[r * S + 4 * g]) =
-            make_uint2((uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16),
-                       (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16));
+struct Stage {
+    static constexpr int G = (W + 8) / 4, R = H + 4, S = W + 8, N = (G * R + 255) / 256;
+    using Raw = typename std::conditional<BPC == 8, uint32_t, uint2>::type;
+    Raw raw[N];
+    bool ok[N];
+    __device__ __forceinline__ void load(const typename Px<BPC>::pixel *src, int stride, int x0, int y0, int gw,
+                                         int gh) {
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            const int i = threadIdx.x + 256 * n, r = i / G, g = i - r * G;
+            const int Y = y0 - 2 + r, X = x0 - 4 + 4 * g;
+            ok[n] = i < G * R && Y >= 0 && Y < gh && X >= 0 && X < gw;
+            if (ok[n]) raw[n] = *reinterpret_cast<const Raw *>(src + (size_t)Y * stride + X);
+        }
     }
-}
+    __device__ __forceinline__ void store(int16_t *t) const {
+#pragma unroll
+        for (int n = 0; n < N; n++) {
+            const int i = threadIdx.x + 256 * n, r = i / G, g = i - r * G;
+            if (i >= G * R) break;
+            uint2 v = make_uint2(0x80008000u, 0x80008000u);   // INT16_MIN x 4
+            if (ok[n]) {
+                if constexpr (BPC == 8) {
+                    const uint32_t w = raw[n];
+                    v.x = (w & 0xff) | ((w & 0xff00) << 8);
+                    v.y = ((w >> 16) & 0xff) | ((w >> 8) & 0xff0000);
+                } else {
+                    v = raw[n];
+                }
+            }
+            *reinterpret_cast<uint2 *>(&t[r * S + 4 * g]) = v;
+        }
+    }
+};
 
-// Filter (or copy) one row of BW pixels of a block from its tile.
-template <int BPC, int BW>
-__device__ __forceinline__ void row_out(typename Px<BPC>::pixel *dst, const int16_t *c, const CdefTaps *tp) {
-    int v[BW];
+// Filter (FILT) or copy one column of BH pixels of a block from its tile.
+template <int BPC, int BH, bool FILT>
+__device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const int16_t *c, int S,
+                                        const CdefTaps &tp) {
+    using P = typename Px<BPC>::pixel;
 #pragma unroll
-    for (int x = 0; x < BW; x++) v[x] = tp ? tp->px(c + x) : c[x];
-#pragma unroll
-    for (int x = 0; x < BW; x += 4) Quad<BPC>::store(dst + x, v + x);
+    for (int y = 0; y < BH; y++) dst[y * ds] = (P)(FILT ? tp.px(c + y * S) : c[y * S]);
+}
+template <int BPC, int BH>
+__device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const int16_t *c, int S,
+                                        const CdefTaps &tp, bool filt) {
+    if (filt) col_out<BPC, BH, true>(dst, ds, c, S, tp);
+    else col_out<BPC, BH, false>(dst, ds, c, S, tp);
 }
 
 template <int BPC, int LAYOUT>
@@ -258,6 +292,8 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
     __shared__ __attribute__((aligned(16))) int16_t tl[(64 + 4) * LS];
     __shared__ __attribute__((aligned(16))) int16_t tc[LAYOUT ? 2 : 1][LAYOUT ? (CH + 4) * CS : 8];
     __shared__ unsigned cost[8][64];
+    __shared__ uint8_t skip[64];
+    __shared__ uint8_t bdir[64], bpri[64];   // per block: direction, adjusted luma strength (<= 240)
 
     // XCD-contiguous superblock order: workgroups are dealt round-robin over
     // the 8 XCDs, so logical superblock (b % 8) * (n / 8) + b / 8 keeps a run
@@ -275,10 +311,23 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
     const int damping = a.damping + bd8;
 
     const int x0 = sbx * 64, y0 = sby * 64;
-    stage<BPC, 64, 64>(tl, a.in[0], a.is[0], x0, y0, a.gw, a.gh);
-    if (LAYOUT) {
-        stage<BPC, CW, CH>(tc[0], a.in[1], a.is[1], x0 >> SX, y0 >> SY, a.gw >> SX, a.gh >> SY);
-        stage<BPC, CW, CH>(tc[LAYOUT ? 1 : 0], a.in[2], a.is[2], x0 >> SX, y0 >> SY, a.gw >> SX, a.gh >> SY);
+    {
+        Stage<BPC, 64, 64> sy;
+        Stage<BPC, CW, CH> su, sv;
+        sy.load(a.in[0], a.is[0], x0, y0, a.gw, a.gh);
+        if (LAYOUT) {
+            su.load(a.in[1], a.is[1], x0 >> SX, y0 >> SY, a.gw >> SX, a.gh >> SY);
+            sv.load(a.in[2], a.is[2], x0 >> SX, y0 >> SY, a.gw >> SX, a.gh >> SY);
+        }
+        if (threadIdx.x < 64) {   // the superblock's skip flags (:185-189)
+            const int gx8 = sbx * 8 + (threadIdx.x & 7), gy8 = sby * 8 + (threadIdx.x >> 3);
+            skip[threadIdx.x] = gx8 < a.b8w && gy8 < a.b8h ? !a.noskip[gy8 * a.b8w + gx8] : 1;
+        }
+        sy.store(tl);
+        if (LAYOUT) {
+            su.store(tc[0]);
+            sv.store(tc[LAYOUT ? 1 : 0]);
+        }
     }
     __syncthreads();
 
@@ -301,51 +350,59 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
             cdef_costs(q, v, &cost[0][blk], 64);
         }
         __syncthreads();
+        if (threadIdx.x < 64) {
+            unsigned var;
+            const int d = cdef_best(&cost[0][threadIdx.x], 64, var);
+            bdir[threadIdx.x] = (uint8_t)d;
+            bpri[threadIdx.x] = (uint8_t)(ypri ? adjust_strength(ypri, var) : 0);   // :237-246
+        }
+        __syncthreads();
     }
 
-    // luma: 64 blocks x 8 rows
-    for (int t = threadIdx.x; t < 64 * 8; t += 256) {
-        const int blk = t >> 3, row = t & 7, bx8 = blk & 7, by8 = blk >> 3;
+    // Column tasks: the lanes of a wave take consecutive columns of one row
+    // of blocks and walk them down, so a tap instruction reads 64
+    // consecutive int16 (plus each block's direction offset).  (A row per
+    // lane put the lanes' rows 72 int16 apart, 8 lanes per LDS bank.)
+    // luma: 8 rows of blocks x 64 columns
+    for (int t = threadIdx.x; t < 8 * 64; t += 256) {
+        const int by8 = t >> 6, l = t & 63, bx8 = l >> 3, x = l & 7, blk = by8 * 8 + bx8;
         const int gx8 = sbx * 8 + bx8, gy8 = sby * 8 + by8;
         if (gx8 >= a.b8w || gy8 >= a.b8h) continue;
-        const int16_t *c = &tl[(by8 * 8 + row + 2) * LS + bx8 * 8 + 4];
-        P *dst = a.out[0] + (size_t)(gy8 * 8 + row) * a.os[0] + gx8 * 8;
+        const int16_t *c = &tl[(by8 * 8 + 2) * LS + bx8 * 8 + 4 + x];
+        P *dst = a.out[0] + (size_t)(gy8 * 8) * a.os[0] + gx8 * 8 + x;
         CdefTaps tp;
         bool filt = false;
-        if (active && a.noskip[gy8 * a.b8w + gx8]) {
-            int dir = 0;
-            unsigned var = 0;
-            if (need_dir) dir = cdef_best(&cost[0][blk], 64, var);
-            const int pri = ypri ? adjust_strength(ypri, var) : 0;   // :237-246
+        if (active && !skip[blk]) {
+            const int pri = ypri ? bpri[blk] : 0;
             if (pri || ysec) {
-                tp.init(pri, ysec, ypri ? dir : 0, damping, bd8, LS);
+                tp.init(pri, ysec, ypri ? bdir[blk] : 0, damping, bd8, LS);
                 filt = true;
             }
         }
-        row_out<BPC, 8>(dst, c, filt ? &tp : nullptr);
+        col_out<BPC, 8>(dst, a.os[0], c, LS, tp, filt);
     }
     if (!LAYOUT) return;
-    // chroma: 2 planes x 64 blocks x CBH rows of CBW pixels (:248-286)
-    for (int t = threadIdx.x; t < 2 * 64 * CBH; t += 256) {
-        const int pl = t / (64 * CBH), r = t - pl * 64 * CBH;
-        const int blk = r / CBH, row = r - blk * CBH, bx8 = blk & 7, by8 = blk >> 3;
+    // chroma: 2 planes x 8 rows of blocks x 8 * CBW columns (:248-286)
+    constexpr int LB = 8 * CBW;
+    for (int t = threadIdx.x; t < 2 * 8 * LB; t += 256) {
+        const int pl = t / (8 * LB), r = t - pl * 8 * LB;
+        const int by8 = r / LB, l = r - by8 * LB, bx8 = l / CBW, x = l - bx8 * CBW, blk = by8 * 8 + bx8;
         const int gx8 = sbx * 8 + bx8, gy8 = sby * 8 + by8;
         if (gx8 >= a.b8w || gy8 >= a.b8h) continue;
-        const int16_t *c = &tc[pl][(by8 * CBH + row + 2) * CS + bx8 * CBW + 4];
-        P *dst = a.out[1 + pl] + (size_t)(gy8 * CBH + row) * a.os[1 + pl] + gx8 * CBW;
+        const int16_t *c = &tc[pl][(by8 * CBH + 2) * CS + bx8 * CBW + 4 + x];
+        P *dst = a.out[1 + pl] + (size_t)(gy8 * CBH) * a.os[1 + pl] + gx8 * CBW + x;
         CdefTaps tp;
         bool filt = false;
-        if (uvlvl && a.noskip[gy8 * a.b8w + gx8]) {
+        if (uvlvl && !skip[blk]) {
             int dir = 0;
             if (uvpri) {
-                unsigned var;
-                dir = cdef_best(&cost[0][blk], 64, var);
-                if (LAYOUT == 2) dir = kUvDir422[dir];
+                dir = bdir[blk];
+                if (LAYOUT == 2) dir = (int)((0x66654207u >> (4 * dir)) & 15);   // uv_dirs[1], :115-117
             }
             tp.init(uvpri, uvsec, dir, damping - 1, bd8, CS);
             filt = true;
         }
-        row_out<BPC, CBW>(dst, c, filt ? &tp : nullptr);
+        col_out<BPC, CBH>(dst, a.os[1 + pl], c, CS, tp, filt);
     }
 }
 
