@@ -178,6 +178,18 @@ class CdefFrame(ctypes.Structure):
                 ("pad_", ctypes.c_int32), ("y_strength", ctypes.c_uint8 * 8), ("uv_strength", ctypes.c_uint8 * 8)]
 
 
+class FilterLUT(ctypes.Structure):
+    """Dav1dGpuFilterLUT: Av1FilterLUT (src/lf_mask.h:35-39)."""
+    _fields_ = [("e", ctypes.c_uint8 * 64), ("i", ctypes.c_uint8 * 64), ("sharp", ctypes.c_uint64 * 2)]
+
+
+class LoopFilterFrame(ctypes.Structure):
+    """Dav1dGpuLoopFilterFrame: one frame of deblocking."""
+    _fields_ = [("pic", Plane * 3), ("masks", ctypes.c_void_p), ("level", ctypes.c_void_p),
+                ("b4_stride", ctypes.c_int64), ("lut", FilterLUT), ("layout", ctypes.c_int32),
+                ("bitdepth_max", ctypes.c_int32), ("filter_uv", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
 GRAIN_W, GRAIN_H = 82, 73
 GRAIN_SCRATCH_BYTES = 3 * GRAIN_H * GRAIN_W * 2 + 3 * 4096
 
@@ -227,6 +239,9 @@ def load_lib():
             f.argtypes = [ctypes.POINTER(FilmGrainBatch), ctypes.c_void_p]
             f.restype = ctypes.c_int
         for bpc in (8, 16):
+            f = getattr(L, f"dav1d_gpu_loopfilter_frame_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(LoopFilterFrame), ctypes.c_void_p]
+            f.restype = ctypes.c_int
             f = getattr(L, f"dav1d_gpu_cdef_frame_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(CdefFrame), ctypes.c_void_p]
             f.restype = ctypes.c_int
@@ -273,4 +288,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_cdef_dsp_init_8bpc", "dav1d_cdef_dsp_init_16bpc",
     "dav1d_cdef_dsp_init_gpu_8bpc", "dav1d_cdef_dsp_init_gpu_16bpc",
     "dav1d_gpu_cdef_frame_8bpc", "dav1d_gpu_cdef_frame_16bpc",
+    "dav1d_loop_filter_dsp_init_8bpc", "dav1d_loop_filter_dsp_init_16bpc",
+    "dav1d_loop_filter_dsp_init_gpu_8bpc", "dav1d_loop_filter_dsp_init_gpu_16bpc",
+    "dav1d_gpu_loopfilter_frame_8bpc", "dav1d_gpu_loopfilter_frame_16bpc",
 ]

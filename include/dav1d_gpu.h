@@ -781,6 +781,68 @@ typedef struct Dav1dGpuCdefFrame {
 int dav1d_gpu_cdef_frame_8bpc(const Dav1dGpuCdefFrame *f, void *stream);
 int dav1d_gpu_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, void *stream);
 
+/* ---- deblocking loop filter --------------------------
+ * Per-call tier: Dav1dLoopFilterDSPContext (src/loopfilter.h:39-52) with the
+ * reference's init name bitfn(dav1d_loop_filter_dsp_init)
+ * (src/loopfilter_tmpl.c:257-272): loop_filter_sb[plane 0 y / 1 uv][0 column
+ * edges (h) / 1 row edges (v)].  The limit LUT is Av1FilterLUT
+ * (src/lf_mask.h:35-39). */
+typedef struct Dav1dGpuFilterLUT {
+    uint8_t e[64];
+    uint8_t i[64];
+    uint64_t sharp[2];
+} Dav1dGpuFilterLUT;
+#define DGPU_LPF_TYPES(sfx, pixel, HBD)                                        \
+typedef void (*dgpu_loopfilter_sb_fn_##sfx)(pixel *dst, ptrdiff_t stride,     \
+    const uint32_t *mask, const uint8_t (*lvl)[4], ptrdiff_t lvl_stride,      \
+    const Dav1dGpuFilterLUT *lut, int w HBD);                                 \
+typedef struct Dav1dLoopFilterDSPContext_##sfx {                              \
+    dgpu_loopfilter_sb_fn_##sfx loop_filter_sb[2][2];                         \
+} Dav1dLoopFilterDSPContext_##sfx;
+DGPU_LPF_TYPES(8bpc, uint8_t, DGPU_HBD_NONE)
+DGPU_LPF_TYPES(16bpc, uint16_t, DGPU_HBD_ARG)
+void dav1d_loop_filter_dsp_init_8bpc(Dav1dLoopFilterDSPContext_8bpc *c);
+void dav1d_loop_filter_dsp_init_16bpc(Dav1dLoopFilterDSPContext_16bpc *c);
+void dav1d_loop_filter_dsp_init_gpu_8bpc(Dav1dLoopFilterDSPContext_8bpc *c);
+void dav1d_loop_filter_dsp_init_gpu_16bpc(Dav1dLoopFilterDSPContext_16bpc *c);
+
+/* Frame tier: dav1d_loopfilter_sbrow_cols / _rows (src/lf_apply_tmpl.c:
+ * 314-466) for every superblock row, as dav1d_filter_sbrow_deblock_cols /
+ * _rows run them (src/recon_tmpl.c:2037-2069), in place, in two launches:
+ * every column edge of the frame, then every row edge.  Within one pass no
+ * two edges touch the same pixels (a filter of length n needs transform
+ * blocks of at least n on both sides), and a superblock row's row edges
+ * touch no pixel the next row's column edges read, so this order gives the
+ * reference's pixels.
+ *   masks: f->lf.mask, one Av1Filter per 128x128 area (src/lf_mask.h:49-56),
+ * [sb128h][sb128w], AFTER the tile-edge fixups dav1d_loopfilter_sbrow_cols
+ * applies to them (:327-393; host bit operations, done before upload).
+ * level: f->lf.level (uint8_t[4] per 4x4 block, luma index [0] column / [1]
+ * row edges; chroma [2] u / [3] v at chroma 4x4 coordinates), row stride
+ * f->b4_stride entries.  Edges at the picture's left and top are not
+ * filtered; rows are honoured per 64-row half that starts inside the
+ * picture, columns of column edges below f->w4 (:176-210). */
+typedef struct Dav1dGpuAv1Filter {   /* Av1Filter, src/lf_mask.h:49-56 */
+    uint16_t filter_y[2][32][3][2];
+    uint16_t filter_uv[2][32][2][2];
+    int8_t cdef_idx[4];
+    uint16_t noskip_mask[16][2];
+} Dav1dGpuAv1Filter;
+typedef struct Dav1dGpuLoopFilterFrame {
+    Dav1dGpuPlane pic[3];         /* device: the picture, filtered in place  */
+    const Dav1dGpuAv1Filter *masks;   /* device                              */
+    const uint8_t *level;         /* device: f->lf.level                     */
+    int64_t b4_stride;            /* f->b4_stride                            */
+    Dav1dGpuFilterLUT lut;        /* f->lf.lim_lut                           */
+    int32_t layout;               /* 0 I400, 1 I420, 2 I422, 3 I444          */
+    int32_t bitdepth_max;
+    int32_t filter_uv;            /* loopfilter.level_u || level_v           */
+    int32_t pad_;
+} Dav1dGpuLoopFilterFrame;
+/* Errors: -1 NULL / bad layout, -3 launch failure. */
+int dav1d_gpu_loopfilter_frame_8bpc(const Dav1dGpuLoopFilterFrame *f, void *stream);
+int dav1d_gpu_loopfilter_frame_16bpc(const Dav1dGpuLoopFilterFrame *f, void *stream);
+
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split
  * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).

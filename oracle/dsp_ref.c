@@ -2462,3 +2462,245 @@ int oracle_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, int sb128)
         for (int t = 0; t < 2; t++) free(c.line[t][pl]);
     return 0;
 }
+
+/* ============================================================ loop filter */
+/* SURVEY 8(f) row 3.  Restated from src/loopfilter_tmpl.c (the DSP entries)
+ * and src/lf_apply_tmpl.c (the superblock-row walkers, without the tile-edge
+ * mask fixups of :327-393, which the frame contract applies beforehand). */
+
+/* loop_filter(), loopfilter_tmpl.c:37-161: 4 lines of one edge segment;
+ * stridea steps along the edge, strideb across it (pixels) */
+static void lpf_edge(pixel *dst, int E, int I, int H, ptrdiff_t stridea, ptrdiff_t strideb, int wd, int bdmax)
+{
+    const int bd8 = bits_of(bdmax) - 8, F = 1 << bd8;
+    E <<= bd8; I <<= bd8; H <<= bd8;
+    const int dlo = -128 * (1 << bd8), dhi = 128 * (1 << bd8) - 1;
+    for (int i = 0; i < 4; i++, dst += stridea) {
+#define PX_(k) dst[strideb * (k)]
+        int p[7], q[7];
+        for (int k = 0; k < 7; k++) p[k] = q[k] = 0;
+        p[1] = PX_(-2); p[0] = PX_(-1); q[0] = PX_(0); q[1] = PX_(1);
+        int fm = abs(p[1] - p[0]) <= I && abs(q[1] - q[0]) <= I && abs(p[0] - q[0]) * 2 + (abs(p[1] - q[1]) >> 1) <= E;
+        if (wd > 4) {
+            p[2] = PX_(-3); q[2] = PX_(2);
+            fm &= abs(p[2] - p[1]) <= I && abs(q[2] - q[1]) <= I;
+            if (wd > 6) {
+                p[3] = PX_(-4); q[3] = PX_(3);
+                fm &= abs(p[3] - p[2]) <= I && abs(q[3] - q[2]) <= I;
+            }
+        }
+        if (!fm) continue;
+        int flat8out = 0, flat8in = 0;
+        if (wd >= 16) {
+            for (int k = 4; k < 7; k++) { p[k] = PX_(-1 - k); q[k] = PX_(k); }
+            flat8out = abs(p[6] - p[0]) <= F && abs(p[5] - p[0]) <= F && abs(p[4] - p[0]) <= F &&
+                       abs(q[4] - q[0]) <= F && abs(q[5] - q[0]) <= F && abs(q[6] - q[0]) <= F;
+        }
+        if (wd >= 6) flat8in = abs(p[2] - p[0]) <= F && abs(p[1] - p[0]) <= F && abs(q[1] - q[0]) <= F && abs(q[2] - q[0]) <= F;
+        if (wd >= 8) flat8in &= abs(p[3] - p[0]) <= F && abs(q[3] - q[0]) <= F;
+        if (wd >= 16 && flat8out && flat8in) {
+            /* 13-tap smoothing of p5..q5 over p6..q6 (:94-117) */
+            int out[12];
+            const int P6 = p[6], P5 = p[5], P4 = p[4], P3 = p[3], P2 = p[2], P1 = p[1], P0 = p[0];
+            const int Q0 = q[0], Q1 = q[1], Q2 = q[2], Q3 = q[3], Q4 = q[4], Q5 = q[5], Q6 = q[6];
+            out[0] = (P6 * 7 + P5 * 2 + P4 * 2 + P3 + P2 + P1 + P0 + Q0 + 8) >> 4;
+            out[1] = (P6 * 5 + P5 * 2 + P4 * 2 + P3 * 2 + P2 + P1 + P0 + Q0 + Q1 + 8) >> 4;
+            out[2] = (P6 * 4 + P5 + P4 * 2 + P3 * 2 + P2 * 2 + P1 + P0 + Q0 + Q1 + Q2 + 8) >> 4;
+            out[3] = (P6 * 3 + P5 + P4 + P3 * 2 + P2 * 2 + P1 * 2 + P0 + Q0 + Q1 + Q2 + Q3 + 8) >> 4;
+            out[4] = (P6 * 2 + P5 + P4 + P3 + P2 * 2 + P1 * 2 + P0 * 2 + Q0 + Q1 + Q2 + Q3 + Q4 + 8) >> 4;
+            out[5] = (P6 + P5 + P4 + P3 + P2 + P1 * 2 + P0 * 2 + Q0 * 2 + Q1 + Q2 + Q3 + Q4 + Q5 + 8) >> 4;
+            out[6] = (P5 + P4 + P3 + P2 + P1 + P0 * 2 + Q0 * 2 + Q1 * 2 + Q2 + Q3 + Q4 + Q5 + Q6 + 8) >> 4;
+            out[7] = (P4 + P3 + P2 + P1 + P0 + Q0 * 2 + Q1 * 2 + Q2 * 2 + Q3 + Q4 + Q5 + Q6 * 2 + 8) >> 4;
+            out[8] = (P3 + P2 + P1 + P0 + Q0 + Q1 * 2 + Q2 * 2 + Q3 * 2 + Q4 + Q5 + Q6 * 3 + 8) >> 4;
+            out[9] = (P2 + P1 + P0 + Q0 + Q1 + Q2 * 2 + Q3 * 2 + Q4 * 2 + Q5 + Q6 * 4 + 8) >> 4;
+            out[10] = (P1 + P0 + Q0 + Q1 + Q2 + Q3 * 2 + Q4 * 2 + Q5 * 2 + Q6 * 5 + 8) >> 4;
+            out[11] = (P0 + Q0 + Q1 + Q2 + Q3 + Q4 * 2 + Q5 * 2 + Q6 * 7 + 8) >> 4;
+            for (int o = 0; o < 12; o++) PX_(o - 6) = (pixel)out[o];
+        } else if (wd >= 8 && flat8in) {
+            const int P3 = p[3], P2 = p[2], P1 = p[1], P0 = p[0], Q0 = q[0], Q1 = q[1], Q2 = q[2], Q3 = q[3];
+            PX_(-3) = (pixel)((P3 * 3 + 2 * P2 + P1 + P0 + Q0 + 4) >> 3);
+            PX_(-2) = (pixel)((P3 * 2 + P2 + 2 * P1 + P0 + Q0 + Q1 + 4) >> 3);
+            PX_(-1) = (pixel)((P3 + P2 + P1 + 2 * P0 + Q0 + Q1 + Q2 + 4) >> 3);
+            PX_(0) = (pixel)((P2 + P1 + P0 + 2 * Q0 + Q1 + Q2 + Q3 + 4) >> 3);
+            PX_(1) = (pixel)((P1 + P0 + Q0 + 2 * Q1 + Q2 + Q3 * 2 + 4) >> 3);
+            PX_(2) = (pixel)((P0 + Q0 + Q1 + 2 * Q2 + Q3 * 3 + 4) >> 3);
+        } else if (wd == 6 && flat8in) {
+            const int P2 = p[2], P1 = p[1], P0 = p[0], Q0 = q[0], Q1 = q[1], Q2 = q[2];
+            PX_(-2) = (pixel)((P2 * 3 + 2 * P1 + 2 * P0 + Q0 + 4) >> 3);
+            PX_(-1) = (pixel)((P2 + 2 * P1 + 2 * P0 + 2 * Q0 + Q1 + 4) >> 3);
+            PX_(0) = (pixel)((P1 + 2 * P0 + 2 * Q0 + 2 * Q1 + Q2 + 4) >> 3);
+            PX_(1) = (pixel)((P0 + 2 * Q0 + 2 * Q1 + Q2 * 3 + 4) >> 3);
+        } else {
+            const int hev = abs(p[1] - p[0]) > H || abs(q[1] - q[0]) > H;
+            if (hev) {
+                int f = clampi(p[1] - q[1], dlo, dhi);
+                f = clampi(3 * (q[0] - p[0]) + f, dlo, dhi);
+                const int f1 = mini(f + 4, (128 << bd8) - 1) >> 3, f2 = mini(f + 3, (128 << bd8) - 1) >> 3;
+                PX_(-1) = (pixel)clampi(p[0] + f2, 0, bdmax);
+                PX_(0) = (pixel)clampi(q[0] - f1, 0, bdmax);
+            } else {
+                const int f = clampi(3 * (q[0] - p[0]), dlo, dhi);
+                const int f1 = mini(f + 4, (128 << bd8) - 1) >> 3, f2 = mini(f + 3, (128 << bd8) - 1) >> 3;
+                PX_(-1) = (pixel)clampi(p[0] + f2, 0, bdmax);
+                PX_(0) = (pixel)clampi(q[0] - f1, 0, bdmax);
+                const int f3 = (f1 + 1) >> 1;
+                PX_(-2) = (pixel)clampi(p[1] + f3, 0, bdmax);
+                PX_(1) = (pixel)clampi(q[1] - f3, 0, bdmax);
+            }
+        }
+#undef PX_
+    }
+}
+
+/* loop_filter_{h,v}_sb128{y,uv}_c, loopfilter_tmpl.c:163-245.  vert = 1: the
+ * row-edge (v) filters, bits are columns; uv = 1: two sizes (4, 6). */
+static void lpf_sb(pixel *dst, ptrdiff_t stride, const uint32_t *vmask, const uint8_t (*l)[4], ptrdiff_t b4_stride,
+                   const Dav1dGpuFilterLUT *lut, int vert, int uv, int bdmax)
+{
+    const unsigned vm = vmask[0] | vmask[1] | (uv ? 0 : vmask[2]);
+    const ptrdiff_t ps = PX(stride);
+    for (unsigned b = 1; vm & ~(b - 1); b <<= 1, dst += vert ? 4 : 4 * ps, l += vert ? 1 : b4_stride) {
+        if (!(vm & b)) continue;
+        const int L = l[0][0] ? l[0][0] : l[vert ? -b4_stride : -1][0];
+        if (!L) continue;
+        const int idx = uv ? !!(vmask[1] & b) : (vmask[2] & b) ? 2 : !!(vmask[1] & b);
+        const int wd = uv ? 4 + 2 * idx : 4 << idx;
+        lpf_edge(dst, lut->e[L], lut->i[L], L >> 4, vert ? 1 : ps, vert ? ps : 1, wd, bdmax);
+    }
+}
+
+static void lpf_h_y(pixel *d, ptrdiff_t s, const uint32_t *m, const uint8_t (*l)[4], ptrdiff_t b4s,
+                    const Dav1dGpuFilterLUT *lut, int w BDPARAM)
+{ BD_DECL (void)w; lpf_sb(d, s, m, l, b4s, lut, 0, 0, bdmax_); }
+static void lpf_v_y(pixel *d, ptrdiff_t s, const uint32_t *m, const uint8_t (*l)[4], ptrdiff_t b4s,
+                    const Dav1dGpuFilterLUT *lut, int w BDPARAM)
+{ BD_DECL (void)w; lpf_sb(d, s, m, l, b4s, lut, 1, 0, bdmax_); }
+static void lpf_h_uv(pixel *d, ptrdiff_t s, const uint32_t *m, const uint8_t (*l)[4], ptrdiff_t b4s,
+                     const Dav1dGpuFilterLUT *lut, int w BDPARAM)
+{ BD_DECL (void)w; lpf_sb(d, s, m, l, b4s, lut, 0, 1, bdmax_); }
+static void lpf_v_uv(pixel *d, ptrdiff_t s, const uint32_t *m, const uint8_t (*l)[4], ptrdiff_t b4s,
+                     const Dav1dGpuFilterLUT *lut, int w BDPARAM)
+{ BD_DECL (void)w; lpf_sb(d, s, m, l, b4s, lut, 1, 1, bdmax_); }
+
+#if BITDEPTH == 8
+void oracle_loop_filter_dsp_init_8bpc(Dav1dLoopFilterDSPContext_8bpc *c)
+#else
+void oracle_loop_filter_dsp_init_16bpc(Dav1dLoopFilterDSPContext_16bpc *c)
+#endif
+{
+    c->loop_filter_sb[0][0] = lpf_h_y;
+    c->loop_filter_sb[0][1] = lpf_v_y;
+    c->loop_filter_sb[1][0] = lpf_h_uv;
+    c->loop_filter_sb[1][1] = lpf_v_uv;
+}
+
+/* dav1d_loopfilter_sbrow_cols / _rows (lf_apply_tmpl.c:314-466) with
+ * filter_plane_{cols,rows}_{y,uv} (:176-312), driven per superblock row as
+ * dav1d_filter_sbrow_deblock_cols / _rows (recon_tmpl.c:2037-2069). */
+#if BITDEPTH == 8
+int oracle_loopfilter_frame_8bpc(const Dav1dGpuLoopFilterFrame *F, int sb128)
+#else
+int oracle_loopfilter_frame_16bpc(const Dav1dGpuLoopFilterFrame *F, int sb128)
+#endif
+{
+    if (!F || F->layout < 0 || F->layout > 3 || !F->masks || !F->level) return -1;
+    const int bdmax = BITDEPTH == 8 ? 255 : F->bitdepth_max;
+    const int W = F->pic[0].w, Hh = F->pic[0].h;
+    const int w4 = (W + 3) >> 2, h4 = (Hh + 3) >> 2;
+    const int bw = ((W + 7) >> 3) << 1, bh = ((Hh + 7) >> 3) << 1;
+    const int sb128w = (bw + 31) >> 5, sb_step = sb128 ? 32 : 16, sbh = (bh + sb_step - 1) / sb_step;
+    const int is_sb64 = !sb128, layout = F->layout;
+    const int ss_ver = layout == 1, ss_hor = layout != 3;
+    const ptrdiff_t b4s = (ptrdiff_t)F->b4_stride;
+    const uint8_t (*level)[4] = (const uint8_t (*)[4])F->level;
+    pixel *p0 = (pixel *)F->pic[0].data;
+    const ptrdiff_t ys = PX(F->pic[0].stride), uvs = layout ? PX(F->pic[1].stride) : 0;
+    for (int sby = 0; sby < sbh; sby++) {
+        const Dav1dGpuAv1Filter *lflvl = F->masks + (sby >> is_sb64) * sb128w;
+        const int starty4 = (sby & is_sb64) << 4;
+        const int sbsz = 32 >> is_sb64;
+        const int endy4 = starty4 + mini(h4 - sby * sbsz, sbsz);
+        const int uv_endy4 = (endy4 + ss_ver) >> ss_ver;
+        const int y = sby * sbsz * 4;
+        pixel *py = p0 + y * ys;
+        pixel *pu = layout ? (pixel *)F->pic[1].data + ((y * uvs) >> ss_ver) : NULL;
+        pixel *pv = layout ? (pixel *)F->pic[2].data + ((y * uvs) >> ss_ver) : NULL;
+        /* columns (sbrow_cols :395-421) */
+        for (int x = 0; x < sb128w; x++) {
+            const uint8_t (*lvl)[4] = level + b4s * sby * sbsz + 32 * x;
+            const uint16_t (*mask)[3][2] = lflvl[x].filter_y[0];
+            const int w = mini(32, w4 - x * 32);
+            for (int c = 0; c < w; c++) {
+                if (!x && !c) continue;
+                uint32_t hm[4];
+                for (int i = 0; i < 3; i++) {
+                    if (!starty4) {
+                        hm[i] = mask[c][i][0];
+                        if (endy4 > 16) hm[i] |= (unsigned)mask[c][i][1] << 16;
+                    } else {
+                        hm[i] = mask[c][i][1];
+                    }
+                }
+                hm[3] = 0;
+                lpf_sb(py + x * 128 + c * 4, ys * sizeof(pixel), hm, (const uint8_t (*)[4])&lvl[c][0], b4s,
+                       &F->lut, 0, 0, bdmax);
+            }
+        }
+        if (layout && F->filter_uv) {
+            for (int x = 0; x < sb128w; x++) {
+                const uint8_t (*lvl)[4] = level + b4s * ((sby * sbsz) >> ss_ver) + (32 >> ss_hor) * x;
+                const uint16_t (*mask)[2][2] = lflvl[x].filter_uv[0];
+                const int w = (mini(32, w4 - x * 32) + ss_hor) >> ss_hor;
+                const int cst = starty4 >> ss_ver, cend = uv_endy4;
+                for (int c = 0; c < w; c++) {
+                    if (!x && !c) continue;
+                    uint32_t hm[3];
+                    for (int i = 0; i < 2; i++) {
+                        if (!cst) {
+                            hm[i] = mask[c][i][0];
+                            if (cend > (16 >> ss_ver)) hm[i] |= (unsigned)mask[c][i][1] << (16 >> ss_ver);
+                        } else {
+                            hm[i] = mask[c][i][1];
+                        }
+                    }
+                    hm[2] = 0;
+                    const ptrdiff_t off = x * (128 >> ss_hor) + c * 4;
+                    lpf_sb(pu + off, uvs * sizeof(pixel), hm, (const uint8_t (*)[4])&lvl[c][2], b4s, &F->lut, 0, 1,
+                           bdmax);
+                    lpf_sb(pv + off, uvs * sizeof(pixel), hm, (const uint8_t (*)[4])&lvl[c][3], b4s, &F->lut, 0, 1,
+                           bdmax);
+                }
+            }
+        }
+        /* rows (sbrow_rows :424-466) */
+        for (int x = 0; x < sb128w; x++) {
+            const uint8_t (*lvl)[4] = level + b4s * sby * sbsz + 32 * x;
+            const uint16_t (*mask)[3][2] = lflvl[x].filter_y[1];
+            pixel *d = py + x * 128;
+            for (int r = starty4; r < endy4; r++, d += 4 * ys, lvl += b4s) {
+                if (!sby && !r) continue;
+                const uint32_t vm[4] = { mask[r][0][0] | ((unsigned)mask[r][0][1] << 16),
+                                         mask[r][1][0] | ((unsigned)mask[r][1][1] << 16),
+                                         mask[r][2][0] | ((unsigned)mask[r][2][1] << 16), 0 };
+                lpf_sb(d, ys * sizeof(pixel), vm, (const uint8_t (*)[4])&lvl[0][1], b4s, &F->lut, 1, 0, bdmax);
+            }
+        }
+        if (layout && F->filter_uv) {
+            for (int x = 0; x < sb128w; x++) {
+                const uint8_t (*lvl)[4] = level + b4s * ((sby * sbsz) >> ss_ver) + (32 >> ss_hor) * x;
+                const uint16_t (*mask)[2][2] = lflvl[x].filter_uv[1];
+                ptrdiff_t off = x * (128 >> ss_hor);
+                for (int r = starty4 >> ss_ver; r < uv_endy4; r++, off += 4 * uvs, lvl += b4s) {
+                    if (!sby && !r) continue;
+                    const uint32_t vm[3] = { mask[r][0][0] | ((unsigned)mask[r][0][1] << (16 >> ss_hor)),
+                                             mask[r][1][0] | ((unsigned)mask[r][1][1] << (16 >> ss_hor)), 0 };
+                    lpf_sb(pu + off, uvs * sizeof(pixel), vm, (const uint8_t (*)[4])&lvl[0][2], b4s, &F->lut, 1, 1,
+                           bdmax);
+                    lpf_sb(pv + off, uvs * sizeof(pixel), vm, (const uint8_t (*)[4])&lvl[0][3], b4s, &F->lut, 1, 1,
+                           bdmax);
+                }
+            }
+        }
+    }
+    return 0;
+}

@@ -32,4 +32,8 @@ void oracle_cdef_dsp_init_8bpc(Dav1dCdefDSPContext_8bpc *c);
 void oracle_cdef_dsp_init_16bpc(Dav1dCdefDSPContext_16bpc *c);
 int oracle_cdef_frame_8bpc(const Dav1dGpuCdefFrame *f, int sb128);
 int oracle_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, int sb128);
+void oracle_loop_filter_dsp_init_8bpc(Dav1dLoopFilterDSPContext_8bpc *c);
+void oracle_loop_filter_dsp_init_16bpc(Dav1dLoopFilterDSPContext_16bpc *c);
+int oracle_loopfilter_frame_8bpc(const Dav1dGpuLoopFilterFrame *f, int sb128);
+int oracle_loopfilter_frame_16bpc(const Dav1dGpuLoopFilterFrame *f, int sb128);
 #endif

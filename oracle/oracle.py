@@ -443,3 +443,22 @@ def cdef_dsp(bpc):
     c = Ctx()
     getattr(L, f"oracle_cdef_dsp_init_{bpc}bpc")(ctypes.byref(c))
     return c
+
+
+def loopfilter_frame(case):
+    """An lpf.LpfCase through the oracle's dav1d_loopfilter_sbrow_cols /
+    _rows restatement, superblock row by superblock row; returns the planes."""
+    import dav1d_mirror_amd.lpf as lpf
+    abi = _abi()
+    L = load()
+    sfx = 8 if case.bpc == 8 else 16
+    pics = [np.ascontiguousarray(a).copy() for a in case.planes]
+    masks = np.ascontiguousarray(case.masks)
+    level = np.ascontiguousarray(case.level)
+    f = lpf.fill_frame(abi.LoopFilterFrame(), case, [(a.ctypes.data, a.shape[1]) for a in pics],
+                       masks.ctypes.data, level.ctypes.data)
+    fn = getattr(L, f"oracle_loopfilter_frame_{sfx}bpc")
+    fn.argtypes = [ctypes.POINTER(abi.LoopFilterFrame), ctypes.c_int]
+    fn.restype = ctypes.c_int
+    assert fn(ctypes.byref(f), case.sb128) == 0
+    return pics

@@ -447,6 +447,93 @@ static void BD(check_cdef)(void) {
     }
 }
 
+/* init_lpf_border, tests/checkasm/loopfilter.c:35-91: random, long flat,
+ * short flat, or normal / hev lines across an edge */
+static void BD(lpf_border)(pixel *dst, ptrdiff_t stride, int E, int I, int bdmax) {
+    const int bd8 = (bdmax == 255 ? 8 : bdmax == 1023 ? 10 : 12) - 8, F = 1 << bd8;
+    E <<= bd8; I <<= bd8;
+    const int type = rnd() % 4, edge_diff = (int)(rnd() % ((E + 2) * 4)) - 2 * (E + 2);
+#define CLP(v) ((pixel)imin(imax((v), 0), bdmax))
+    if (type == 0) {
+        for (int i = -8; i < 8; i++) dst[i * stride] = rnd() & bdmax;
+    } else if (type == 1) {
+        dst[-8 * stride] = rnd() & bdmax; dst[7 * stride] = rnd() & bdmax; dst[0] = rnd() & bdmax;
+        dst[-stride] = CLP(dst[0] + edge_diff);
+        for (int i = 1; i < 7; i++) {
+            dst[-(1 + i) * stride] = CLP(dst[-stride] + (int)(rnd() % (2 * (F + 1))) - (F + 1));
+            dst[i * stride] = CLP(dst[0] + (int)(rnd() % (2 * (F + 1))) - (F + 1));
+        }
+    } else {
+        for (int i = 4; i < 8; i++) { dst[-(1 + i) * stride] = rnd() & bdmax; dst[i * stride] = rnd() & bdmax; }
+        dst[0] = rnd() & bdmax;
+        dst[-stride] = CLP(dst[0] + edge_diff);
+        for (int i = 1; i < 4; i++) {
+            if (type == 2) {
+                dst[-(1 + i) * stride] = CLP(dst[-stride] + (int)(rnd() % (2 * (F + 1))) - (F + 1));
+                dst[i * stride] = CLP(dst[0] + (int)(rnd() % (2 * (F + 1))) - (F + 1));
+            } else {
+                dst[-(1 + i) * stride] = CLP(dst[-i * stride] + (int)(rnd() % (2 * (I + 1))) - (I + 1));
+                dst[i * stride] = CLP(dst[(i - 1) * stride] + (int)(rnd() % (2 * (I + 1))) - (I + 1));
+            }
+        }
+    }
+#undef CLP
+}
+
+/* tests/checkasm/loopfilter.c:93-203: every loop_filter_sb entry, every
+ * filter length, random masks / levels / sharpness; the whole buffer compared */
+static void BD(check_lpf)(void) {
+    BD(Dav1dLoopFilterDSPContext) ref, gpu;
+    BD(oracle_loop_filter_dsp_init)(&ref);
+    BD(dav1d_loop_filter_dsp_init)(&gpu);
+    static const char *names[4] = { "lpf_h_sb_y", "lpf_v_sb_y", "lpf_h_sb_uv", "lpf_v_sb_uv" };
+    for (int e = 0; e < 4; e++) {
+        const int uv = e >> 1, dir = e & 1, n_blks = uv ? 16 : 32, lf_idx = uv ? 2 : dir;
+        for (int rep = 0; rep < (g_quick ? 4 : 16); rep++) {
+            static pixel c_mem[128 * 16], a_mem[128 * 16];
+            const int w = dir ? n_blks * 4 : 16, h = dir ? 16 : n_blks * 4;
+            pixel *c_dst = dir ? c_mem + n_blks * 4 * 8 : c_mem + 8, *a_dst = dir ? a_mem + n_blks * 4 * 8 : a_mem + 8;
+            const ptrdiff_t stride = w * sizeof(pixel), b4_stride = dir ? 32 : 2;
+            Dav1dGpuFilterLUT lut;
+            const int sharp = rnd() & 7;
+            for (int level = 0; level < 64; level++) {
+                int limit = level;
+                if (sharp > 0) { limit >>= (sharp + 3) >> 2; limit = imin(limit, 9 - sharp); }
+                limit = imax(limit, 1);
+                lut.i[level] = limit;
+                lut.e[level] = 2 * (level + 2) + limit;
+            }
+            lut.sharp[0] = (sharp + 3) >> 2;
+            lut.sharp[1] = sharp ? 9 - sharp : 0xff;
+            for (int i = 0; i < (uv ? 2 : 3); i++) {
+                uint32_t vmask[4] = { 0 };
+                uint8_t l[32 * 2][4];
+                memset(l, 0, sizeof(l));
+                for (int j = 0; j < n_blks; j++) {
+                    const int idx = rnd() % (i + 2);
+                    if (idx) vmask[idx - 1] |= 1U << j;
+                    if (dir) { l[j][lf_idx] = rnd() & 63; l[j + 32][lf_idx] = rnd() & 63; }
+                    else { l[j * 2][lf_idx] = rnd() & 63; l[j * 2 + 1][lf_idx] = rnd() & 63; }
+                }
+                const int bdmax = BDMAX_RAND();
+                for (int k = 0; k < 128 * 16; k++) c_mem[k] = rnd() & bdmax;
+                for (int k = 0; k < 4 * n_blks; k++) {
+                    const int x = k >> 2;
+                    const int L = dir ? (l[32 + x][lf_idx] ? l[32 + x][lf_idx] : l[x][lf_idx])
+                                      : (l[2 * x + 1][lf_idx] ? l[2 * x + 1][lf_idx] : l[2 * x][lf_idx]);
+                    BD(lpf_border)(c_dst + k * (dir ? 1 : 16), dir ? n_blks * 4 : 1, lut.e[L], lut.i[L], bdmax);
+                }
+                memcpy(a_mem, c_mem, sizeof(c_mem));
+                const uint8_t (*lp)[4] = (const uint8_t (*)[4])&l[dir ? 32 : 1][lf_idx];
+                ref.loop_filter_sb[uv][dir](c_dst, stride, vmask, lp, b4_stride, &lut, n_blks HBD_ARG(bdmax));
+                gpu.loop_filter_sb[uv][dir](a_dst, stride, vmask, lp, b4_stride, &lut, n_blks HBD_ARG(bdmax));
+                report(names[e], !memcmp(c_mem, a_mem, sizeof(c_mem)), "sizes<=%d rep %d bdmax %d", i, rep, bdmax);
+            }
+            (void)h;
+        }
+    }
+}
+
 #undef pixel
 #undef coef
 #undef BD
