@@ -306,6 +306,45 @@ def cdef_breakdown(cfg, dev, steps):
             "bit_exact_vs_oracle": all(bool(np.array_equal(a, b)) for a, b in zip(d.outputs_host(), want))}
 
 
+def lpf_breakdown(cfg, dev, steps):
+    """the deblocking loop filter (dav1d_gpu_loopfilter_
+    frame_*: every column edge, then every row edge) on a synthetic frame of
+    the config's size and bitdepth, 4:2:0, random transform quadtree per 64x64
+    with the edge masks and levels it implies: us per frame (both launches)
+    by HIP events over repeated in-place launches, algorithmic GB/s (each
+    pass reads and writes the picture once), the oracle's superblock-row
+    walker on one core, bit-exact check from the unfiltered picture."""
+    import torch
+    import dav1d_mirror_amd.lpf as lpf
+    c = lpf.make_lpf_case(seed=11, width=cfg.width, height=cfg.height, bpc=cfg.bpc,
+                          bitdepth_max=cfg.bitdepth_max, layout=1)
+    d = lpf.DeviceLpf(c, dev)
+    s = torch.cuda.current_stream(dev)
+    for _ in range(3):
+        d.launch(s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = max(steps, 20)
+    e0.record(s)
+    for _ in range(n):
+        d.launch(s)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / n
+    d.reset()
+    d.launch(s)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    want = ge.load_oracle().loopfilter_frame(c)
+    cpu = time.perf_counter() - t0
+    nbytes = lpf.algorithmic_bytes(c)
+    px = sum(w * h for w, h in (c.plane_wh(p) for p in range(3)))
+    return {"frame": f"{cfg.width}x{cfg.height} 4:2:0", "us_per_frame": round(us, 2),
+            "gpix_s": round(px / us / 1e3, 2), "algorithmic_bytes": nbytes,
+            "achieved_gbs": round(nbytes / us / 1e3, 1), "frac_of_hbm_peak": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+            "kernel": f"k_lpf<{cfg.bpc},0> + k_lpf<{cfg.bpc},1>", "oracle_1core_ms": round(cpu * 1e3, 1),
+            "bit_exact_vs_oracle": all(bool(np.array_equal(a, b)) for a, b in zip(d.outputs_host(), want))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -322,6 +361,7 @@ def main():
     ap.add_argument("--no-recorder", action="store_true", help="skip the batch-recorder measurement (N=1)")
     ap.add_argument("--no-grain", action="store_true", help="skip the film-grain measurement (N=1)")
     ap.add_argument("--no-cdef", action="store_true", help="skip the CDEF measurement (N=1)")
+    ap.add_argument("--no-lpf", action="store_true", help="skip the deblocking measurement (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -451,6 +491,8 @@ def main():
             out["film_grain"] = grain_breakdown(cfg, dev, args.steps)
         if not args.no_cdef and world == 1:
             out["cdef"] = cdef_breakdown(cfg, dev, args.steps)
+        if not args.no_lpf and world == 1:
+            out["loop_filter"] = lpf_breakdown(cfg, dev, args.steps)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
         print(json.dumps(out), flush=True)
