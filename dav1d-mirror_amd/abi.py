@@ -190,6 +190,15 @@ class LoopFilterFrame(ctypes.Structure):
                 ("bitdepth_max", ctypes.c_int32), ("filter_uv", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
+class _LrSgr(ctypes.Structure):
+    _fields_ = [("s0", ctypes.c_uint32), ("s1", ctypes.c_uint32), ("w0", ctypes.c_int16), ("w1", ctypes.c_int16)]
+
+
+class LrParams(ctypes.Union):
+    """Dav1dGpuLrParams: LooprestorationParams (src/looprestoration.h:47-53)."""
+    _fields_ = [("filter", (ctypes.c_int16 * 8) * 2), ("sgr", _LrSgr)]
+
+
 GRAIN_W, GRAIN_H = 82, 73
 GRAIN_SCRATCH_BYTES = 3 * GRAIN_H * GRAIN_W * 2 + 3 * 4096
 
@@ -291,4 +300,6 @@ EXPORTED_SYMBOLS = [
     "dav1d_loop_filter_dsp_init_8bpc", "dav1d_loop_filter_dsp_init_16bpc",
     "dav1d_loop_filter_dsp_init_gpu_8bpc", "dav1d_loop_filter_dsp_init_gpu_16bpc",
     "dav1d_gpu_loopfilter_frame_8bpc", "dav1d_gpu_loopfilter_frame_16bpc",
+    "dav1d_loop_restoration_dsp_init_8bpc", "dav1d_loop_restoration_dsp_init_16bpc",
+    "dav1d_loop_restoration_dsp_init_gpu_8bpc", "dav1d_loop_restoration_dsp_init_gpu_16bpc",
 ]

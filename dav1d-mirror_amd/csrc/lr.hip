@@ -1,0 +1,262 @@
+// lr.hip -- loop restoration on the device (include/
+// dav1d_gpu.h, Dav1dLoopRestorationDSPContext): the per-call entries of
+// src/looprestoration_tmpl.c (wiener_c :134-190, sgr_5x5_c / sgr_3x3_c /
+// sgr_mix_c :449-525) for one restoration-unit stripe per call.
+//
+// One 256-thread workgroup per 32-column strip of the unit.  The strip's
+// (h + 6) x (32 + 6) context is built in LDS with padding()'s rules
+// (:40-132) in closed form: rows above / below from the loop-filtered `lpf`
+// rows (0, 0, 1 above; 6, 7, 7 below) or the first / last row, columns left
+// of the unit from `left` or replicated, right of it from the picture or
+// replicated.  Wiener: the horizontal 7-tap pass into LDS (uint16 range
+// clip), then the vertical one.  Self-guided: A / B (box sums, the
+// dav1d_sgr_x_by_x lookup and the inversion, with the reference's unsigned
+// arithmetic) at every position the 6- / 8-neighbour weighting reads, then
+// the weighting and the w0 / w1 blend.  Latency-bound per call like the
+// other per-call entries; the frame form (dav1d_lr_sbrow, lr_apply_tmpl.c)
+// is not built yet.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "dav1d_gpu.h"
+#include "dsp_common.hpp"
+#include "runtime.hpp"
+
+namespace dgpu {
+
+constexpr int kLrSW = 32;              // strip width
+constexpr int kLrTW = kLrSW + 6;       // tile width
+constexpr int kLrTH = 64 + 6;          // tile height
+
+template <int BPC> struct LrArgs {
+    using P = typename Px<BPC>::pixel;
+    const P *src;     // the unit's pixels (rows 0..h-1), pitch ss
+    P *dst;           // output rect, pitch ds
+    const P *top;     // lpf rows 0-1 (HAVE_TOP), pitch ts
+    const P *bot;     // lpf rows 6-7 (HAVE_BOTTOM), pitch bs
+    const P *left;    // [h][4]
+    int ss, ds, ts, bs;
+    int w, h, edges, kind, bdmax;   // kind: 0 wiener, 1 sgr 5x5, 2 sgr 3x3, 3 mix
+    Dav1dGpuLrParams prm;
+};
+
+// padding() in closed form: tile value at tmp row r, column c (tmp (r, c)
+// is unit pixel (r - 3, c - 3))
+template <int BPC>
+__device__ __forceinline__ int lr_tmp(const LrArgs<BPC> &a, int r, int c) {
+    const bool hl = a.edges & DGPU_LR_HAVE_LEFT, hr = a.edges & DGPU_LR_HAVE_RIGHT;
+    if (!hr && c >= a.w + 3) c = a.w + 2;   // :110-118
+    if (!hl && c < 3) c = 3;                // :120-126
+    const int x = c - 3;
+    if (r < 3) {
+        if (a.edges & DGPU_LR_HAVE_TOP) return a.top[(r == 2) * a.ts + x];
+        return x < 0 ? a.left[x + 4] : a.src[x];
+    }
+    if (r < a.h + 3) {
+        const int j = r - 3;
+        return x < 0 ? a.left[j * 4 + x + 4] : a.src[(size_t)j * a.ss + x];
+    }
+    if (a.edges & DGPU_LR_HAVE_BOTTOM) return a.bot[(r > a.h + 3) * a.bs + x];
+    return x < 0 ? a.left[(a.h - 1) * 4 + x + 4] : a.src[(size_t)(a.h - 1) * a.ss + x];
+}
+
+// A / B of selfguided_filter (:373-392) at unit position (j, i) for box
+// radius R (n = 25 or 9), from the tile (columns relative to the strip)
+template <int R>
+__device__ __forceinline__ void lr_ab(const int (*T)[kLrTW], int j, int il, unsigned s, int bd8, int &A, int &B) {
+    constexpr int n = (2 * R + 1) * (2 * R + 1);
+    constexpr unsigned one_by_x = n == 25 ? 164 : 455;
+    int sum = 0, sumsq = 0;
+#pragma unroll
+    for (int dy = -R; dy <= R; dy++)
+#pragma unroll
+        for (int dx = -R; dx <= R; dx++) {
+            const int v = T[j + 3 + dy][il + 3 + dx];
+            sum += v;
+            sumsq += v * v;
+        }
+    const int a = (sumsq + ((1 << (2 * bd8)) >> 1)) >> (2 * bd8);
+    const int b = (sum + ((1 << bd8) >> 1)) >> bd8;
+    const unsigned p = (unsigned)max(a * n - b * b, 0);
+    const unsigned z = (p * s + (1u << 19)) >> 20;
+    const unsigned x = dspt_sgr_x_by_x[min(z, 255u)];
+    A = (int)((x * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
+    B = (int)x;
+}
+
+template <int BPC>
+__global__ __launch_bounds__(256) void k_lr(LrArgs<BPC> a) {
+    using P = typename Px<BPC>::pixel;
+    using C = typename Px<BPC>::coef;
+    __shared__ int T[kLrTH][kLrTW];
+    __shared__ int AB[2][66][kLrSW + 2];   // A, B at unit rows -1..h, strip columns -1..sw
+    __shared__ int HOR[kLrTH][kLrSW];
+    const int x0 = blockIdx.x * kLrSW, sw = min(kLrSW, a.w - x0), h = a.h;
+    const int bd8 = bits_of(a.bdmax) - 8;
+    for (int k = threadIdx.x; k < (h + 6) * (sw + 6); k += 256) {
+        const int r = k / (sw + 6), c = k - r * (sw + 6);
+        T[r][c] = lr_tmp<BPC>(a, r, x0 + c);
+    }
+    __syncthreads();
+    constexpr int NP = (64 * kLrSW + 255) / 256;
+    if (a.kind == 0) {   // wiener_c, :157-189
+        const int bd = bd8 + 8;
+        const int rbh = 3 + (bd == 12) * 2, clip_limit = 1 << (bd + 1 + 7 - rbh);
+        for (int k = threadIdx.x; k < (h + 6) * sw; k += 256) {
+            const int r = k / sw, i = k - r * sw;
+            int sum = 1 << (bd + 6);
+            if (BPC == 8) sum += T[r][i + 3] * 128;
+#pragma unroll
+            for (int t = 0; t < 7; t++) sum += T[r][i + t] * a.prm.filter[0][t];
+            HOR[r][i] = clampi((sum + (1 << (rbh - 1))) >> rbh, 0, clip_limit - 1);
+        }
+        __syncthreads();
+        const int rbv = 11 - (bd == 12) * 2, round_offset = 1 << (bd + (rbv - 1));
+        for (int k = threadIdx.x; k < h * sw; k += 256) {
+            const int j = k / sw, i = k - j * sw;
+            int sum = -round_offset;
+#pragma unroll
+            for (int t = 0; t < 7; t++) sum += HOR[j + t][i] * a.prm.filter[1][t];
+            a.dst[(size_t)j * a.ds + x0 + i] = (P)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, a.bdmax);
+        }
+        return;
+    }
+    int v[NP];
+#pragma unroll
+    for (int m = 0; m < NP; m++) v[m] = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const bool five = pass == 0;
+        if (five ? a.kind == 2 : a.kind == 1) continue;
+        // A / B at unit rows -1..h (every other row from -1 for 5x5, :375)
+        for (int k = threadIdx.x; k < (h + 2) * (sw + 2); k += 256) {
+            const int jj = k / (sw + 2), ii = k - jj * (sw + 2), j = jj - 1;
+            if (five && !(j & 1)) continue;
+            int A, B;
+            if (five) lr_ab<2>(T, j, ii - 1, a.prm.sgr.s0, bd8, A, B);
+            else lr_ab<1>(T, j, ii - 1, a.prm.sgr.s1, bd8, A, B);
+            AB[0][jj][ii] = A;
+            AB[1][jj][ii] = B;
+        }
+        __syncthreads();
+        const int wgt = five ? a.prm.sgr.w0 : a.prm.sgr.w1;
+#pragma unroll
+        for (int m = 0; m < NP; m++) {
+            const int k = threadIdx.x + 256 * m;
+            if (k >= h * sw) break;
+            const int j = k / sw, i = k - j * sw, jj = j + 1, ii = i + 1;
+            const int px = T[j + 3][i + 3];
+            const int(*A)[kLrSW + 2] = AB[0];
+            const int(*B)[kLrSW + 2] = AB[1];
+            int aa, bb, sh;
+            if (five) {
+                if (!(j & 1)) {   // SIX_NEIGHBORS, :397-405
+                    aa = (B[jj - 1][ii] + B[jj + 1][ii]) * 6 +
+                         (B[jj - 1][ii - 1] + B[jj + 1][ii - 1] + B[jj - 1][ii + 1] + B[jj + 1][ii + 1]) * 5;
+                    bb = (A[jj - 1][ii] + A[jj + 1][ii]) * 6 +
+                         (A[jj - 1][ii - 1] + A[jj + 1][ii - 1] + A[jj - 1][ii + 1] + A[jj + 1][ii + 1]) * 5;
+                    sh = 9;
+                } else {          // :411-415
+                    aa = B[jj][ii] * 6 + (B[jj][ii - 1] + B[jj][ii + 1]) * 5;
+                    bb = A[jj][ii] * 6 + (A[jj][ii - 1] + A[jj][ii + 1]) * 5;
+                    sh = 8;
+                }
+            } else {              // EIGHT_NEIGHBORS, :430-439
+                aa = (B[jj][ii] + B[jj][ii - 1] + B[jj][ii + 1] + B[jj - 1][ii] + B[jj + 1][ii]) * 4 +
+                     (B[jj - 1][ii - 1] + B[jj + 1][ii - 1] + B[jj - 1][ii + 1] + B[jj + 1][ii + 1]) * 3;
+                bb = (A[jj][ii] + A[jj][ii - 1] + A[jj][ii + 1] + A[jj - 1][ii] + A[jj + 1][ii]) * 4 +
+                     (A[jj - 1][ii - 1] + A[jj + 1][ii - 1] + A[jj - 1][ii + 1] + A[jj + 1][ii + 1]) * 3;
+                sh = 9;
+            }
+            const int d = (int)(C)((bb - aa * px + (1 << (sh - 1))) >> sh);   // stored as coef
+            v[m] += wgt * d;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int m = 0; m < NP; m++) {
+        const int k = threadIdx.x + 256 * m;
+        if (k >= h * sw) break;
+        const int j = k / sw, i = k - j * sw;
+        a.dst[(size_t)j * a.ds + x0 + i] = (P)clampi(T[j + 3][i + 3] + ((v[m] + (1 << 10)) >> 11), 0, a.bdmax);
+    }
+}
+
+template <int BPC>
+static void lr_t(typename Px<BPC>::pixel *p, ptrdiff_t stride, const typename Px<BPC>::pixel (*left)[4],
+                 const typename Px<BPC>::pixel *lpf, int w, int h, const Dav1dGpuLrParams *params, int edges,
+                 int kind, int bdmax) {
+    using P = typename Px<BPC>::pixel;
+    constexpr long B = sizeof(P);
+    if (w <= 0 || h <= 0) return;
+    const long hl = (edges & DGPU_LR_HAVE_LEFT) ? 3 : 0, hr = (edges & DGPU_LR_HAVE_RIGHT) ? 3 : 0;
+    Stager st;
+    const int ip = st.in(p, stride, -hl * B, (w + hr) * B, 0, h);
+    const int op = st.out(p, stride, 0, w * B, 0, h);
+    const int il = hl ? st.in1(left, (long)h * 4 * B) : -1;
+    const int it = (edges & DGPU_LR_HAVE_TOP) ? st.in(lpf, stride, -hl * B, (w + hr) * B, 0, 2) : -1;
+    const int ib = (edges & DGPU_LR_HAVE_BOTTOM) ? st.in(lpf, stride, -hl * B, (w + hr) * B, 6, 8) : -1;
+    st.upload();
+    LrArgs<BPC> a;
+    memset(&a, 0, sizeof(a));
+    a.src = st.origin<const P>(ip);
+    a.ss = (int)(st.pitch(ip) / B);
+    a.dst = st.origin<P>(op);
+    a.ds = (int)(st.pitch(op) / B);
+    a.left = il >= 0 ? st.origin<const P>(il) : nullptr;
+    a.top = it >= 0 ? st.origin<const P>(it) : nullptr;
+    a.ts = it >= 0 ? (int)(st.pitch(it) / B) : 0;
+    a.bot = ib >= 0 ? st.origin<const P>(ib) + 6 * (st.pitch(ib) / B) : nullptr;   // row 6
+    a.bs = ib >= 0 ? (int)(st.pitch(ib) / B) : 0;
+    a.w = w;
+    a.h = h;
+    a.edges = edges;
+    a.kind = kind;
+    a.bdmax = bdmax;
+    a.prm = *params;
+    k_lr<BPC><<<(w + kLrSW - 1) / kLrSW, 256, 0, st.stream()>>>(a);
+    st.finish();
+}
+
+#define LR_ENTRIES(BPC, P, BDP, BDV)                                                                      \
+template <int KIND>                                                                                       \
+static void lr_##BPC(P *d, ptrdiff_t s, const P (*l)[4], const P *lpf, int w, int h,                      \
+                     const Dav1dGpuLrParams *prm, int edges BDP)                                          \
+{ lr_t<BPC>(d, s, l, lpf, w, h, prm, edges, KIND, BDV); }
+
+#define BD8_PARAM
+#define BD8_VAL 255
+#define BD16_PARAM , int bitdepth_max
+#define BD16_VAL bitdepth_max
+LR_ENTRIES(8, uint8_t, BD8_PARAM, BD8_VAL)
+LR_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
+
+#define FILL_LR(BPC, c)                                      \
+    do {                                                     \
+        c->wiener[0] = c->wiener[1] = lr_##BPC<0>;           \
+        c->sgr[0] = lr_##BPC<1>;                             \
+        c->sgr[1] = lr_##BPC<2>;                             \
+        c->sgr[2] = lr_##BPC<3>;                             \
+    } while (0)
+
+}  // namespace dgpu
+
+using namespace dgpu;
+
+// bitfn(dav1d_loop_restoration_dsp_init) replacement, src/looprestoration_tmpl.c:539-558
+extern "C" void dav1d_loop_restoration_dsp_init_gpu_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc) {
+    (void)bpc;
+    FILL_LR(8, c);
+}
+extern "C" void dav1d_loop_restoration_dsp_init_gpu_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc) {
+    (void)bpc;
+    FILL_LR(16, c);
+}
+extern "C" void dav1d_loop_restoration_dsp_init_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc) {
+    (void)bpc;
+    FILL_LR(8, c);
+}
+extern "C" void dav1d_loop_restoration_dsp_init_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc) {
+    (void)bpc;
+    FILL_LR(16, c);
+}

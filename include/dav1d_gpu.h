@@ -843,6 +843,35 @@ typedef struct Dav1dGpuLoopFilterFrame {
 int dav1d_gpu_loopfilter_frame_8bpc(const Dav1dGpuLoopFilterFrame *f, void *stream);
 int dav1d_gpu_loopfilter_frame_16bpc(const Dav1dGpuLoopFilterFrame *f, void *stream);
 
+/* ---- loop restoration -------------------------------
+ * Per-call tier: Dav1dLoopRestorationDSPContext (src/looprestoration.h:
+ * 62-72) with the reference's init name bitfn(dav1d_loop_restoration_dsp_init)
+ * (src/looprestoration_tmpl.c:539-558): wiener[0/1] (7-tap / 5-tap, the same
+ * function in C), sgr[0] 5x5, sgr[1] 3x3, sgr[2] mix.  One restoration unit
+ * stripe per call: w <= 384, h <= 64; `left` is pixel[h][4]; `lpf` holds the
+ * two loop-filtered rows above (rows 0-1) and below (rows 6-7) at `stride`. */
+enum Dav1dGpuLrEdgeFlags {   /* LrEdgeFlags, src/looprestoration.h:35-40 */
+    DGPU_LR_HAVE_LEFT = 1, DGPU_LR_HAVE_RIGHT = 2, DGPU_LR_HAVE_TOP = 4, DGPU_LR_HAVE_BOTTOM = 8
+};
+typedef union Dav1dGpuLrParams {   /* LooprestorationParams, :47-53 */
+    int16_t filter[2][8] __attribute__((aligned(16)));
+    struct { uint32_t s0, s1; int16_t w0, w1; } sgr;
+} Dav1dGpuLrParams;
+#define DGPU_LR_TYPES(sfx, pixel, HBD)                                         \
+typedef void (*dgpu_lr_fn_##sfx)(pixel *dst, ptrdiff_t stride,                \
+    const pixel (*left)[4], const pixel *lpf, int w, int h,                   \
+    const Dav1dGpuLrParams *params, int edges HBD);                           \
+typedef struct Dav1dLoopRestorationDSPContext_##sfx {                         \
+    dgpu_lr_fn_##sfx wiener[2];                                               \
+    dgpu_lr_fn_##sfx sgr[3];                                                  \
+} Dav1dLoopRestorationDSPContext_##sfx;
+DGPU_LR_TYPES(8bpc, uint8_t, DGPU_HBD_NONE)
+DGPU_LR_TYPES(16bpc, uint16_t, DGPU_HBD_ARG)
+void dav1d_loop_restoration_dsp_init_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc);
+void dav1d_loop_restoration_dsp_init_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc);
+void dav1d_loop_restoration_dsp_init_gpu_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc);
+void dav1d_loop_restoration_dsp_init_gpu_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc);
+
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split
  * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).

@@ -2704,3 +2704,179 @@ int oracle_loopfilter_frame_16bpc(const Dav1dGpuLoopFilterFrame *F, int sb128)
     }
     return 0;
 }
+
+/* ====================================================== loop restoration */
+/* SURVEY 8(f) row 3.  Restated from src/looprestoration_tmpl.c. */
+#define LR_ST 390   /* REST_UNIT_STRIDE: 256 * 1.5 + 3 + 3 */
+
+/* padding(), looprestoration_tmpl.c:40-132: the (h + 6) x (w + 6) stripe
+ * with 3 rows / columns of context, from the loop-filtered rows above and
+ * below (lpf rows 0-1 and 6-7), the left columns and edge replication */
+static void lr_padding(pixel *dst, const pixel *p, ptrdiff_t stride, const pixel (*left)[4], const pixel *lpf,
+                       int unit_w, int stripe_h, int edges)
+{
+    const int hl = !!(edges & DGPU_LR_HAVE_LEFT), hr = !!(edges & DGPU_LR_HAVE_RIGHT);
+    const ptrdiff_t ps = PX(stride);
+    unit_w += 3 * hl + 3 * hr;
+    pixel *dst_l = dst + 3 * !hl;
+    p -= 3 * hl;
+    lpf -= 3 * hl;
+    if (edges & DGPU_LR_HAVE_TOP) {
+        memcpy(dst_l, lpf, unit_w * sizeof(pixel));
+        memcpy(dst_l + LR_ST, lpf, unit_w * sizeof(pixel));
+        memcpy(dst_l + 2 * LR_ST, lpf + ps, unit_w * sizeof(pixel));
+    } else {
+        for (int r = 0; r < 3; r++) {
+            memcpy(dst_l + r * LR_ST, p, unit_w * sizeof(pixel));
+            if (hl) memcpy(dst_l + r * LR_ST, &left[0][1], 3 * sizeof(pixel));
+        }
+    }
+    pixel *dst_tl = dst_l + 3 * LR_ST;
+    if (edges & DGPU_LR_HAVE_BOTTOM) {
+        memcpy(dst_tl + stripe_h * LR_ST, lpf + 6 * ps, unit_w * sizeof(pixel));
+        memcpy(dst_tl + (stripe_h + 1) * LR_ST, lpf + 7 * ps, unit_w * sizeof(pixel));
+        memcpy(dst_tl + (stripe_h + 2) * LR_ST, lpf + 7 * ps, unit_w * sizeof(pixel));
+    } else {
+        for (int r = 0; r < 3; r++) {
+            memcpy(dst_tl + (stripe_h + r) * LR_ST, p + (stripe_h - 1) * ps, unit_w * sizeof(pixel));
+            if (hl) memcpy(dst_tl + (stripe_h + r) * LR_ST, &left[stripe_h - 1][1], 3 * sizeof(pixel));
+        }
+    }
+    for (int j = 0; j < stripe_h; j++)
+        memcpy(dst_tl + j * LR_ST + 3 * hl, p + j * ps + 3 * hl, (unit_w - 3 * hl) * sizeof(pixel));
+    if (!hr)
+        for (int j = 0; j < stripe_h + 6; j++)
+            for (int k = 0; k < 3; k++) dst_l[j * LR_ST + unit_w + k] = dst_l[j * LR_ST + unit_w - 1];
+    if (!hl) {
+        for (int j = 0; j < stripe_h + 6; j++)
+            for (int k = 0; k < 3; k++) dst[j * LR_ST + k] = dst_l[j * LR_ST];
+    } else {
+        for (int j = 0; j < stripe_h; j++) memcpy(dst + (3 + j) * LR_ST, &left[j][1], 3 * sizeof(pixel));
+    }
+}
+
+/* wiener_c, :134-190 (7-tap; the 5-tap entry is the same function) */
+static void lr_wiener(pixel *p, ptrdiff_t stride, const pixel (*left)[4], const pixel *lpf, int w, int h,
+                      const Dav1dGpuLrParams *params, int edges BDPARAM)
+{
+    BD_DECL
+    static pixel tmp[70 * LR_ST];
+    static uint16_t hor[70 * LR_ST];
+    lr_padding(tmp, p, stride, left, lpf, w, h, edges);
+    const int bd = bits_of(bdmax_);
+    const int rbh = 3 + (bd == 12) * 2, clip_limit = 1 << (bd + 1 + 7 - rbh);
+    for (int j = 0; j < h + 6; j++)
+        for (int i = 0; i < w; i++) {
+            int sum = 1 << (bd + 6);
+            if (BITDEPTH == 8) sum += tmp[j * LR_ST + i + 3] * 128;
+            for (int k = 0; k < 7; k++) sum += tmp[j * LR_ST + i + k] * params->filter[0][k];
+            hor[j * LR_ST + i] = (uint16_t)clampi((sum + (1 << (rbh - 1))) >> rbh, 0, clip_limit - 1);
+        }
+    const int rbv = 11 - (bd == 12) * 2, round_offset = 1 << (bd + (rbv - 1));
+    for (int j = 0; j < h; j++)
+        for (int i = 0; i < w; i++) {
+            int sum = -round_offset;
+            for (int k = 0; k < 7; k++) sum += hor[(j + k) * LR_ST + i] * params->filter[1][k];
+            p[j * PX(stride) + i] = (pixel)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, bdmax_);
+        }
+}
+
+/* selfguided_filter, :350-447: box sums (boxsum5 / boxsum3, :214-348)
+ * computed directly per position, A / B and their inversion with the
+ * reference's unsigned arithmetic, then the 6- / 8-neighbour weighting;
+ * dst: h x w, row stride 384 */
+static void lr_selfguided(int32_t *dst, const pixel *src, int w, int h, int n, unsigned s, int bdmax)
+{
+    static int32_t A[66][386], B[66][386];   /* p rows -1..h, columns -1..w */
+    const unsigned one_by_x = n == 25 ? 164 : 455;
+    const int r = n == 25 ? 2 : 1, bd8 = bits_of(bdmax) - 8, step = (n == 25) + 1;
+    for (int j = -1; j < h + 1; j += step)
+        for (int i = -1; i < w + 1; i++) {
+            int sum = 0, sumsq = 0;
+            for (int dy = -r; dy <= r; dy++)
+                for (int dx = -r; dx <= r; dx++) {
+                    const int v = src[(j + 3 + dy) * LR_ST + i + 3 + dx];
+                    sum += v;
+                    sumsq += v * v;
+                }
+            const int a = (sumsq + ((1 << (2 * bd8)) >> 1)) >> (2 * bd8);
+            const int b = (sum + ((1 << bd8) >> 1)) >> bd8;
+            const unsigned pp = (unsigned)maxi(a * n - b * b, 0);
+            const unsigned z = (pp * s + (1u << 19)) >> 20;
+            const unsigned x = dspt_sgr_x_by_x[z < 255 ? z : 255];
+            A[j + 1][i + 1] = (int32_t)((x * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
+            B[j + 1][i + 1] = (int32_t)x;
+        }
+#define AA(y, x) A[(y) + 1][(x) + 1]
+#define BB(y, x) B[(y) + 1][(x) + 1]
+    for (int j = 0; j < h; j++)
+        for (int i = 0; i < w; i++) {
+            const int px = src[(j + 3) * LR_ST + i + 3];
+            int a, b, sh;
+            if (n == 25) {
+                if (!(j & 1)) {   /* rows between two computed rows (SIX_NEIGHBORS) */
+                    a = (BB(j - 1, i) + BB(j + 1, i)) * 6 +
+                        (BB(j - 1, i - 1) + BB(j + 1, i - 1) + BB(j - 1, i + 1) + BB(j + 1, i + 1)) * 5;
+                    b = (AA(j - 1, i) + AA(j + 1, i)) * 6 +
+                        (AA(j - 1, i - 1) + AA(j + 1, i - 1) + AA(j - 1, i + 1) + AA(j + 1, i + 1)) * 5;
+                    sh = 9;
+                } else {
+                    a = BB(j, i) * 6 + (BB(j, i - 1) + BB(j, i + 1)) * 5;
+                    b = AA(j, i) * 6 + (AA(j, i - 1) + AA(j, i + 1)) * 5;
+                    sh = 8;
+                }
+            } else {
+                a = (BB(j, i) + BB(j, i - 1) + BB(j, i + 1) + BB(j - 1, i) + BB(j + 1, i)) * 4 +
+                    (BB(j - 1, i - 1) + BB(j + 1, i - 1) + BB(j - 1, i + 1) + BB(j + 1, i + 1)) * 3;
+                b = (AA(j, i) + AA(j, i - 1) + AA(j, i + 1) + AA(j - 1, i) + AA(j + 1, i)) * 4 +
+                    (AA(j - 1, i - 1) + AA(j + 1, i - 1) + AA(j - 1, i + 1) + AA(j + 1, i + 1)) * 3;
+                sh = 9;
+            }
+            const int v = (b - a * px + (1 << (sh - 1))) >> sh;
+            dst[j * 384 + i] = (int32_t)(coef)v;   /* stored as coef (:361-364) */
+        }
+#undef AA
+#undef BB
+}
+
+/* sgr_5x5_c / sgr_3x3_c / sgr_mix_c, :449-525 */
+static void lr_sgr(pixel *p, ptrdiff_t stride, const pixel (*left)[4], const pixel *lpf, int w, int h,
+                   const Dav1dGpuLrParams *params, int edges, int kind, int bdmax)
+{
+    static pixel tmp[70 * LR_ST];
+    static int32_t d0[64 * 384], d1[64 * 384];
+    lr_padding(tmp, p, stride, left, lpf, w, h, edges);
+    if (kind != 1) lr_selfguided(d0, tmp, w, h, 25, params->sgr.s0, bdmax);
+    if (kind != 0) lr_selfguided(d1, tmp, w, h, 9, params->sgr.s1, bdmax);
+    for (int j = 0; j < h; j++)
+        for (int i = 0; i < w; i++) {
+            const int v = kind == 0 ? params->sgr.w0 * d0[j * 384 + i]
+                        : kind == 1 ? params->sgr.w1 * d1[j * 384 + i]
+                                    : params->sgr.w0 * d0[j * 384 + i] + params->sgr.w1 * d1[j * 384 + i];
+            pixel *q = p + j * PX(stride) + i;
+            *q = (pixel)clampi(*q + ((v + (1 << 10)) >> 11), 0, bdmax);
+        }
+}
+static void lr_sgr5(pixel *p, ptrdiff_t s, const pixel (*l)[4], const pixel *lpf, int w, int h,
+                    const Dav1dGpuLrParams *pr, int e BDPARAM)
+{ BD_DECL lr_sgr(p, s, l, lpf, w, h, pr, e, 0, bdmax_); }
+static void lr_sgr3(pixel *p, ptrdiff_t s, const pixel (*l)[4], const pixel *lpf, int w, int h,
+                    const Dav1dGpuLrParams *pr, int e BDPARAM)
+{ BD_DECL lr_sgr(p, s, l, lpf, w, h, pr, e, 1, bdmax_); }
+static void lr_sgrmix(pixel *p, ptrdiff_t s, const pixel (*l)[4], const pixel *lpf, int w, int h,
+                      const Dav1dGpuLrParams *pr, int e BDPARAM)
+{ BD_DECL lr_sgr(p, s, l, lpf, w, h, pr, e, 2, bdmax_); }
+
+/* bitfn(dav1d_loop_restoration_dsp_init), :539-558 */
+#if BITDEPTH == 8
+void oracle_loop_restoration_dsp_init_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc)
+#else
+void oracle_loop_restoration_dsp_init_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc)
+#endif
+{
+    (void)bpc;
+    c->wiener[0] = c->wiener[1] = lr_wiener;
+    c->sgr[0] = lr_sgr5;
+    c->sgr[1] = lr_sgr3;
+    c->sgr[2] = lr_sgrmix;
+}

@@ -462,3 +462,18 @@ def loopfilter_frame(case):
     fn.restype = ctypes.c_int
     assert fn(ctypes.byref(f), case.sb128) == 0
     return pics
+
+
+def lr_dsp(bpc, bitdepth=None):
+    """wiener[2] + sgr[3] of the oracle's bitfn(dav1d_loop_restoration_dsp_init) as ctypes callables."""
+    abi = _abi()
+    L = load()
+    hbd = [] if bpc == 8 else [ctypes.c_int]
+    fn_t = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                            ctypes.c_int, ctypes.POINTER(abi.LrParams), ctypes.c_int, *hbd)
+
+    class Ctx(ctypes.Structure):
+        _fields_ = [("wiener", fn_t * 2), ("sgr", fn_t * 3)]
+    c = Ctx()
+    getattr(L, f"oracle_loop_restoration_dsp_init_{bpc}bpc")(ctypes.byref(c), bitdepth or bpc)
+    return c

@@ -3,7 +3,7 @@
  * strategy (tests/checkasm/checkasm.c:808-862) with the CPU oracle as
  * func_ref and the GPU-backed DSP tables (include/dav1d_gpu.h) as func_new.
  *
- *   checkasm_gpu [--test=mc|ipred|itx|cdef|lpf|all] [--bpc=8|16|all] [--seed=N] [--quick]
+ *   checkasm_gpu [--test=mc|ipred|itx|cdef|lpf|lr|all] [--bpc=8|16|all] [--seed=N] [--quick]
  *
  * Prints one line per failing case and a summary line per function:
  *   RESULT <name>_<bpc>bpc pass=<n> fail=<n>
@@ -18,6 +18,7 @@
 
 #include "dav1d_gpu.h"
 #include "oracle.h"
+#include "../dav1d-mirror_amd/csrc/dsp_tables.h"
 
 static int g_quick;
 static int g_bpc_now;
@@ -199,6 +200,7 @@ int main(int argc, char **argv) {
         if (all || !strcmp(test, "itx")) { rnd_seed(seed); b == 8 ? check_itx_8bpc() : check_itx_16bpc(); }
         if (all || !strcmp(test, "cdef")) { rnd_seed(seed); b == 8 ? check_cdef_8bpc() : check_cdef_16bpc(); }
         if (all || !strcmp(test, "lpf")) { rnd_seed(seed); b == 8 ? check_lpf_8bpc() : check_lpf_16bpc(); }
+        if (all || !strcmp(test, "lr")) { rnd_seed(seed); b == 8 ? check_lr_8bpc() : check_lr_16bpc(); }
     }
     for (int i = 0; i < g_nstats; i++)
         printf("RESULT %s pass=%ld fail=%ld\n", g_stats[i].name, g_stats[i].pass, g_stats[i].fail);

@@ -534,6 +534,73 @@ static void BD(check_lpf)(void) {
     }
 }
 
+/* init_tmp, tests/checkasm/looprestoration.c:40-51: a noisy checkerboard */
+static void BD(lr_fill)(pixel *buf, ptrdiff_t stride_px, int w, int h, int bdmax) {
+    const int noise_mask = bdmax >> 4, x_off = rnd() & 7, y_off = rnd() & 7;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            buf[y * stride_px + x] = (pixel)(((((x + x_off) ^ (y + y_off)) & 8) ? bdmax : 0) ^ (rnd() & noise_mask));
+}
+
+/* tests/checkasm/looprestoration.c:53-196: wiener 7 / 5 tap and sgr 5x5 /
+ * 3x3 / mix over the 16 edge sets, random unit sizes (w <= 384, h <= 64),
+ * bpc 8 or 10 / 12; the whole 448 x 64 buffer compared */
+static void BD(check_lr)(void) {
+    static pixel c_mem[448 * 64 + 64], a_mem[448 * 64 + 64], edge_buf[448 * 8 + 64], left[64][4];
+    pixel *const c_dst = c_mem + 64, *const a_dst = a_mem + 64, *const h_edge = edge_buf + 64;
+    const ptrdiff_t stride = 448 * sizeof(pixel);
+    static const struct { const char *name; uint8_t idx; } sgr_data[3] = { { "sgr_5x5", 14 }, { "sgr_3x3", 10 },
+                                                                          { "sgr_mix", 0 } };
+    const int bpc_lo = BITDEPTH == 16 ? 10 : 8, bpc_hi = BITDEPTH == 16 ? 12 : 8;
+    for (int bpc = bpc_lo; bpc <= bpc_hi; bpc += 2) {
+        BD(Dav1dLoopRestorationDSPContext) ref, gpu;
+        BD(oracle_loop_restoration_dsp_init)(&ref, bpc);
+        BD(dav1d_loop_restoration_dsp_init)(&gpu, bpc);
+        const int bdmax = (1 << bpc) - 1;
+        for (int f = 0; f < 5; f++)
+            for (int rep = 0; rep < (g_quick ? 1 : 3); rep++) {
+                Dav1dGpuLrParams prm;
+                memset(&prm, 0, sizeof(prm));
+                if (f < 2) {
+                    const int t = f;
+                    for (int d = 0; d < 2; d++) {
+                        int16_t *fl = prm.filter[d];
+                        fl[0] = fl[6] = t ? 0 : (rnd() & 15) - 5;
+                        fl[1] = fl[5] = (rnd() & 31) - 23;
+                        fl[2] = fl[4] = (rnd() & 63) - 17;
+                        fl[3] = (d ? 128 : 0) - (fl[0] + fl[1] + fl[2]) * 2;
+                        if (!d && BITDEPTH != 8) fl[3] += 128;
+                    }
+                } else {
+                    const uint16_t *sp = &dspt_sgr_params[sgr_data[f - 2].idx * 2];
+                    prm.sgr.s0 = sp[0];
+                    prm.sgr.s1 = sp[1];
+                    prm.sgr.w0 = sp[0] ? (rnd() & 127) - 96 : 0;
+                    prm.sgr.w1 = (sp[1] ? 160 - (rnd() & 127) : 33) - prm.sgr.w0;
+                }
+                const int base_w = 1 + (rnd() % 384), base_h = 1 + (rnd() & 63);
+                BD(lr_fill)(c_mem, 448, 448, 64, bdmax);
+                BD(lr_fill)(edge_buf, 448, 448, 8, bdmax);
+                BD(lr_fill)(&left[0][0], 4, 4, 64, bdmax);
+                for (int edges = 0; edges <= 15; edges++) {
+                    const int w = (edges & DGPU_LR_HAVE_RIGHT) ? 256 : base_w;
+                    const int h = (edges & DGPU_LR_HAVE_BOTTOM) ? 64 : base_h;
+                    memcpy(a_mem, c_mem, sizeof(c_mem));
+                    if (f < 2) {
+                        ref.wiener[f](c_dst, stride, (const pixel (*)[4])left, h_edge, w, h, &prm, edges HBD_ARG(bdmax));
+                        gpu.wiener[f](a_dst, stride, (const pixel (*)[4])left, h_edge, w, h, &prm, edges HBD_ARG(bdmax));
+                    } else {
+                        ref.sgr[f - 2](c_dst, stride, (const pixel (*)[4])left, h_edge, w, h, &prm, edges HBD_ARG(bdmax));
+                        gpu.sgr[f - 2](a_dst, stride, (const pixel (*)[4])left, h_edge, w, h, &prm, edges HBD_ARG(bdmax));
+                    }
+                    report(f < 2 ? (f ? "wiener_5tap" : "wiener_7tap") : sgr_data[f - 2].name,
+                           !memcmp(c_mem, a_mem, sizeof(c_mem)), "%dx%d edges %d bpc %d", w, h, edges, bpc);
+                    memcpy(c_mem, a_mem, sizeof(c_mem));   /* both outputs equal or reported; keep going */
+                }
+            }
+    }
+}
+
 #undef pixel
 #undef coef
 #undef BD

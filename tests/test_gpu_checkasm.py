@@ -1,7 +1,7 @@
 """The checkasm-style harness (tests/checkasm_gpu.c): every per-call DSP
 table entry (mc/mct/scaled/avg/w_avg/mask/w_mask/blend*/warp/emu_edge/resize,
-14 intra modes + cfl + pal, 156 itx entries, cdef dir + fb[3], loop_filter_sb[2][2]) at 8 and
-16 bpc, byte-exact
+14 intra modes + cfl + pal, 156 itx entries, cdef dir + fb[3], loop_filter_sb[2][2],
+wiener[2] + sgr[3]) at 8 and 16 bpc, byte-exact
 against the oracle with 8-px guard bands and coefficient-zeroing checks."""
 import os
 import re
@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("test", ["mc", "ipred", "itx", "cdef", "lpf"])
+@pytest.mark.parametrize("test", ["mc", "ipred", "itx", "cdef", "lpf", "lr"])
 def test_checkasm(test):
     exe = os.path.join(HERE, "checkasm_gpu")
     assert os.path.exists(exe), "build with __graft_entry__.build()"
