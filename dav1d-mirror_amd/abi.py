@@ -199,6 +199,19 @@ class LrParams(ctypes.Union):
     _fields_ = [("filter", (ctypes.c_int16 * 8) * 2), ("sgr", _LrSgr)]
 
 
+class LrUnit(ctypes.Structure):
+    """Dav1dGpuLrUnit: Av1RestorationUnit (src/lf_mask.h:41-47)."""
+    _fields_ = [("type", ctypes.c_uint8), ("filter_h", ctypes.c_int8 * 3), ("filter_v", ctypes.c_int8 * 3),
+                ("sgr_weights", ctypes.c_int8 * 2)]
+
+
+class LrFrame(ctypes.Structure):
+    _fields_ = [("in_", Plane * 3), ("lpf", Plane * 3), ("out", Plane * 3), ("units", ctypes.c_void_p * 3),
+                ("unit_rows", ctypes.c_int32 * 3), ("unit_cols", ctypes.c_int32 * 3),
+                ("unit_size_log2", ctypes.c_int32 * 2), ("layout", ctypes.c_int32), ("bitdepth_max", ctypes.c_int32),
+                ("sb128", ctypes.c_int32), ("restore_planes", ctypes.c_int32)]
+
+
 GRAIN_W, GRAIN_H = 82, 73
 GRAIN_SCRATCH_BYTES = 3 * GRAIN_H * GRAIN_W * 2 + 3 * 4096
 
@@ -248,6 +261,9 @@ def load_lib():
             f.argtypes = [ctypes.POINTER(FilmGrainBatch), ctypes.c_void_p]
             f.restype = ctypes.c_int
         for bpc in (8, 16):
+            f = getattr(L, f"dav1d_gpu_lr_frame_{bpc}bpc")
+            f.argtypes = [ctypes.POINTER(LrFrame), ctypes.c_void_p]
+            f.restype = ctypes.c_int
             f = getattr(L, f"dav1d_gpu_loopfilter_frame_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(LoopFilterFrame), ctypes.c_void_p]
             f.restype = ctypes.c_int
@@ -302,4 +318,5 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_loopfilter_frame_8bpc", "dav1d_gpu_loopfilter_frame_16bpc",
     "dav1d_loop_restoration_dsp_init_8bpc", "dav1d_loop_restoration_dsp_init_16bpc",
     "dav1d_loop_restoration_dsp_init_gpu_8bpc", "dav1d_loop_restoration_dsp_init_gpu_16bpc",
+    "dav1d_gpu_lr_frame_8bpc", "dav1d_gpu_lr_frame_16bpc",
 ]

@@ -13,8 +13,13 @@
 // dav1d_sgr_x_by_x lookup and the inversion, with the reference's unsigned
 // arithmetic) at every position the 6- / 8-neighbour weighting reads, then
 // the weighting and the w0 / w1 blend.  Latency-bound per call like the
-// other per-call entries; the frame form (dav1d_lr_sbrow, lr_apply_tmpl.c)
-// is not built yet.
+// other per-call entries.
+//
+// Frame tier, k_lr_frame: bytefn(dav1d_lr_sbrow) (lr_apply_tmpl.c:169-202)
+// for a whole frame in one launch, one workgroup per (plane, stripe,
+// 32-column strip), the same strip code with the stripe's context rows from
+// the deblocked picture (what dav1d_copy_lpf saves) and the unit's left and
+// right columns from the pre-LR picture (what lr_sbrow backs up).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
@@ -35,7 +40,7 @@ template <int BPC> struct LrArgs {
     P *dst;           // output rect, pitch ds
     const P *top;     // lpf rows 0-1 (HAVE_TOP), pitch ts
     const P *bot;     // lpf rows 6-7 (HAVE_BOTTOM), pitch bs
-    const P *left;    // [h][4]
+    const P *left;    // [h][4]; null: the columns left of the unit are src's
     int ss, ds, ts, bs;
     int w, h, edges, kind, bdmax;   // kind: 0 wiener, 1 sgr 5x5, 2 sgr 3x3, 3 mix
     Dav1dGpuLrParams prm;
@@ -51,14 +56,14 @@ __device__ __forceinline__ int lr_tmp(const LrArgs<BPC> &a, int r, int c) {
     const int x = c - 3;
     if (r < 3) {
         if (a.edges & DGPU_LR_HAVE_TOP) return a.top[(r == 2) * a.ts + x];
-        return x < 0 ? a.left[x + 4] : a.src[x];
+        return x < 0 && a.left ? a.left[x + 4] : a.src[x];
     }
     if (r < a.h + 3) {
         const int j = r - 3;
-        return x < 0 ? a.left[j * 4 + x + 4] : a.src[(size_t)j * a.ss + x];
+        return x < 0 && a.left ? a.left[j * 4 + x + 4] : a.src[(ptrdiff_t)j * a.ss + x];
     }
     if (a.edges & DGPU_LR_HAVE_BOTTOM) return a.bot[(r > a.h + 3) * a.bs + x];
-    return x < 0 ? a.left[(a.h - 1) * 4 + x + 4] : a.src[(size_t)(a.h - 1) * a.ss + x];
+    return x < 0 && a.left ? a.left[(a.h - 1) * 4 + x + 4] : a.src[(ptrdiff_t)(a.h - 1) * a.ss + x];
 }
 
 // A / B of selfguided_filter (:373-392) at unit position (j, i) for box
@@ -85,14 +90,15 @@ __device__ __forceinline__ void lr_ab(const int (*T)[kLrTW], int j, int il, unsi
     B = (int)x;
 }
 
+// One 32-column strip (columns x0.. of the unit) of one stripe.
 template <int BPC>
-__global__ __launch_bounds__(256) void k_lr(LrArgs<BPC> a) {
+__device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     using P = typename Px<BPC>::pixel;
     using C = typename Px<BPC>::coef;
     __shared__ int T[kLrTH][kLrTW];
     __shared__ int AB[2][66][kLrSW + 2];   // A, B at unit rows -1..h, strip columns -1..sw
     __shared__ int HOR[kLrTH][kLrSW];
-    const int x0 = blockIdx.x * kLrSW, sw = min(kLrSW, a.w - x0), h = a.h;
+    const int sw = min(kLrSW, a.w - x0), h = a.h;
     const int bd8 = bits_of(a.bdmax) - 8;
     for (int k = threadIdx.x; k < (h + 6) * (sw + 6); k += 256) {
         const int r = k / (sw + 6), c = k - r * (sw + 6);
@@ -183,6 +189,143 @@ __global__ __launch_bounds__(256) void k_lr(LrArgs<BPC> a) {
 }
 
 template <int BPC>
+__global__ __launch_bounds__(256) void k_lr(LrArgs<BPC> a) {
+    lr_strip<BPC>(a, blockIdx.x * kLrSW);
+}
+
+// ---- frame tier ------------------------------------------------------------
+template <int BPC> struct LrFrameArgs {
+    using P = typename Px<BPC>::pixel;
+    const P *in[3];
+    const P *lpf[3];
+    P *out[3];
+    const Dav1dGpuLrUnit *units[3];
+    int is[3], ls[3], os[3], w[3], h[3], rows[3], cols[3], log2[3], restore[3], ss_ver[3];
+    int sb128, bdmax;
+};
+
+// lr_stripe's filter parameters (src/lr_apply_tmpl.c:51-80); kind 0 wiener,
+// 1 sgr 5x5, 2 3x3, 3 mix
+__device__ __forceinline__ int lr_params(const Dav1dGpuLrUnit &u, bool hbd, Dav1dGpuLrParams &prm) {
+    if (u.type == 2) {
+        for (int d = 0; d < 2; d++) {
+            const int8_t *f = d ? u.filter_v : u.filter_h;
+            prm.filter[d][0] = prm.filter[d][6] = f[0];
+            prm.filter[d][1] = prm.filter[d][5] = f[1];
+            prm.filter[d][2] = prm.filter[d][4] = f[2];
+            prm.filter[d][3] = (int16_t)((d ? 128 : 0) - (f[0] + f[1] + f[2]) * 2 + (!d && hbd ? 128 : 0));
+            prm.filter[d][7] = 0;
+        }
+        return 0;
+    }
+    const int s0 = dspt_sgr_params[(u.type - 3) * 2], s1 = dspt_sgr_params[(u.type - 3) * 2 + 1];
+    prm.sgr.s0 = (uint32_t)s0;
+    prm.sgr.s1 = (uint32_t)s1;
+    prm.sgr.w0 = u.sgr_weights[0];
+    prm.sgr.w1 = (int16_t)(128 - (u.sgr_weights[0] + u.sgr_weights[1]));
+    return !!s0 + !!s1 * 2;
+}
+
+// One (plane, stripe, 32-column strip): stripes are 64 rows (the first 8
+// luma rows shorter, :45-46), units unit_size columns (the last takes the
+// rest, :135-166) and a superblock row's unit row is chosen as lr_sbrow does
+// (:124-127).
+template <int BPC>
+__global__ __launch_bounds__(256) void k_lr_frame(LrFrameArgs<BPC> f) {
+    using P = typename Px<BPC>::pixel;
+    const int pl = blockIdx.z, w = f.w[pl], h = f.h[pl], sv = f.ss_ver[pl];
+    const int xs = blockIdx.x * kLrSW;
+    if (xs >= w) return;
+    const int S64 = 64 >> sv, S8 = 8 >> sv, k = blockIdx.y;
+    const int y0 = k ? k * S64 - S8 : 0, y1 = min((k + 1) * S64 - S8, h);
+    if (y0 >= h) return;
+    const int us = 1 << f.log2[pl];
+    const int ucol = min(xs >> f.log2[pl], f.cols[pl] - 1);
+    const int ux0 = ucol * us, ux1 = ucol == f.cols[pl] - 1 ? w : ux0 + us;
+    const int sby = k >> f.sb128;   // the superblock row of this stripe
+    const int row_y = sby * (S64 << f.sb128);
+    int aligned = row_y & ~(us - 1);
+    if (aligned && aligned + (us >> 1) > h) aligned -= us;
+    const int urow = min(aligned >> f.log2[pl], f.rows[pl] - 1);
+    const Dav1dGpuLrUnit &u = f.units[pl][(size_t)urow * f.cols[pl] + ucol];
+    const P *src = f.in[pl] + (size_t)y0 * f.is[pl];
+    P *dst = f.out[pl] + (size_t)y0 * f.os[pl];
+    if (!f.restore[pl] || u.type == 0) {   // copied
+        const int sw = min(kLrSW, w - xs);
+        for (int t = threadIdx.x; t < (y1 - y0) * sw; t += 256) {
+            const int j = t / sw, i = t - j * sw;
+            dst[(size_t)j * f.os[pl] + xs + i] = src[(size_t)j * f.is[pl] + xs + i];
+        }
+        return;
+    }
+    LrArgs<BPC> a;
+    a.src = src + ux0;
+    a.ss = f.is[pl];
+    a.dst = dst + ux0;
+    a.ds = f.os[pl];
+    a.left = nullptr;
+    const bool bottom = y1 < h;
+    a.edges = (y0 > 0 ? DGPU_LR_HAVE_TOP : 0) | (bottom ? DGPU_LR_HAVE_BOTTOM : 0) |
+              (ux0 > 0 ? DGPU_LR_HAVE_LEFT : 0) | (ux1 < w ? DGPU_LR_HAVE_RIGHT : 0);
+    // lr_lpf_line (dav1d_copy_lpf's backup_lpf, lf_apply_tmpl.c:40-100):
+    // rows y0 - 2, y0 - 1 above and y1, y1 + 1 below (y1 again past the plane)
+    a.top = y0 > 0 ? f.lpf[pl] + (size_t)(y0 - 2) * f.ls[pl] + ux0 : nullptr;
+    a.ts = f.ls[pl];
+    a.bot = bottom ? f.lpf[pl] + (size_t)y1 * f.ls[pl] + ux0 : nullptr;
+    a.bs = y1 + 1 < h ? f.ls[pl] : 0;
+    a.w = ux1 - ux0;
+    a.h = y1 - y0;
+    a.bdmax = f.bdmax;
+    a.kind = lr_params(u, BPC != 8, a.prm);
+    lr_strip<BPC>(a, xs - ux0);
+}
+
+template <int BPC>
+static int launch_lr_frame(const Dav1dGpuLrFrame *F, hipStream_t stream) {
+    using P = typename Px<BPC>::pixel;
+    constexpr int B = BPC / 8;
+    if (!F || F->layout < 0 || F->layout > 3) return -1;
+    const int np = F->layout ? 3 : 1;
+    LrFrameArgs<BPC> f;
+    memset(&f, 0, sizeof(f));
+    int maxw = 0, maxh = 0;
+    for (int p = 0; p < np; p++) {
+        if (!F->in[p].data || !F->out[p].data || F->in[p].data == F->out[p].data) return -1;
+        f.restore[p] = (F->restore_planes >> p) & 1;
+        if (f.restore[p] && (!F->lpf[p].data || !F->units[p] || F->unit_rows[p] <= 0 || F->unit_cols[p] <= 0))
+            return -1;
+        const int l2 = F->unit_size_log2[!!p];
+        if (f.restore[p] && (l2 < 5 || l2 > 8)) return -1;
+        f.in[p] = (const P *)F->in[p].data;
+        f.lpf[p] = (const P *)F->lpf[p].data;
+        f.out[p] = (P *)F->out[p].data;
+        f.units[p] = F->units[p];
+        f.is[p] = (int)(F->in[p].stride / B);
+        f.ls[p] = (int)(F->lpf[p].stride / B);
+        f.os[p] = (int)(F->out[p].stride / B);
+        f.w[p] = F->in[p].w;
+        f.h[p] = F->in[p].h;
+        f.rows[p] = F->unit_rows[p];
+        f.cols[p] = F->unit_cols[p];
+        f.log2[p] = l2;
+        f.ss_ver[p] = p && F->layout == 1;
+        maxw = max(maxw, f.w[p]);
+        maxh = max(maxh, f.h[p]);
+    }
+    f.sb128 = F->sb128;
+    f.bdmax = BPC == 8 ? 255 : F->bitdepth_max;
+    const int stripes = (maxh + 8 + 63) / 64 + 1;
+    const dim3 grid((unsigned)((maxw + kLrSW - 1) / kLrSW), (unsigned)stripes, (unsigned)np);
+    k_lr_frame<BPC><<<grid, 256, 0, stream>>>(f);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        fprintf(stderr, "dav1d-gpu: loop restoration launch failed: %s\n", hipGetErrorString(e));
+        return -3;
+    }
+    return 0;
+}
+
+template <int BPC>
 static void lr_t(typename Px<BPC>::pixel *p, ptrdiff_t stride, const typename Px<BPC>::pixel (*left)[4],
                  const typename Px<BPC>::pixel *lpf, int w, int h, const Dav1dGpuLrParams *params, int edges,
                  int kind, int bdmax) {
@@ -251,6 +394,12 @@ extern "C" void dav1d_loop_restoration_dsp_init_gpu_8bpc(Dav1dLoopRestorationDSP
 extern "C" void dav1d_loop_restoration_dsp_init_gpu_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc) {
     (void)bpc;
     FILL_LR(16, c);
+}
+extern "C" int dav1d_gpu_lr_frame_8bpc(const Dav1dGpuLrFrame *f, void *stream) {
+    return launch_lr_frame<8>(f, (hipStream_t)stream);
+}
+extern "C" int dav1d_gpu_lr_frame_16bpc(const Dav1dGpuLrFrame *f, void *stream) {
+    return launch_lr_frame<16>(f, (hipStream_t)stream);
 }
 extern "C" void dav1d_loop_restoration_dsp_init_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc) {
     (void)bpc;

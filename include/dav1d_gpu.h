@@ -872,6 +872,44 @@ void dav1d_loop_restoration_dsp_init_16bpc(Dav1dLoopRestorationDSPContext_16bpc 
 void dav1d_loop_restoration_dsp_init_gpu_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc);
 void dav1d_loop_restoration_dsp_init_gpu_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc);
 
+/* Frame tier: bytefn(dav1d_lr_sbrow) (src/lr_apply_tmpl.c:169-202, with
+ * lr_sbrow :99-167 and lr_stripe :36-97) for every superblock row, as
+ * dav1d_filter_sbrow_lr runs it, without super-res.  Every stripe (64 rows,
+ * the first one 8 luma rows shorter) of every restoration unit reads: its
+ * own rows and the 3 columns on either side from `in` (the CDEF output;
+ * dav1d keeps the left ones in pre_lr_border, :150-151), the 2 rows above
+ * and below the stripe from `lpf` (the deblocked, pre-CDEF picture that
+ * dav1d_copy_lpf saves into lr_lpf_line, lf_apply_tmpl.c:40-174), with
+ * padding() at the picture edges.  One launch; `out` is a distinct picture
+ * (units that are not restored are copied).
+ *   units[p]: the plane's restoration units, [unit_rows[p]][unit_cols[p]]
+ * with unit_cols = max(1, (w + half) / unit_size) (the last unit takes the
+ * rest, lr_sbrow's x loop) and the unit row of a superblock row chosen as
+ * lr_sbrow does (:124-127); the per-128x128 lr_mask entries of dav1d map to
+ * it one to one. */
+typedef struct Dav1dGpuLrUnit {   /* Av1RestorationUnit, src/lf_mask.h:41-47 */
+    uint8_t type;                 /* Dav1dRestorationType: 0 none, 2 wiener,
+                                     3 + sgr_idx self-guided                 */
+    int8_t filter_h[3];
+    int8_t filter_v[3];
+    int8_t sgr_weights[2];
+} Dav1dGpuLrUnit;
+typedef struct Dav1dGpuLrFrame {
+    Dav1dGpuPlane in[3];          /* device: CDEF output (pre-LR), read      */
+    Dav1dGpuPlane lpf[3];         /* device: deblocked, pre-CDEF picture     */
+    Dav1dGpuPlane out[3];         /* device: restored picture, distinct      */
+    const Dav1dGpuLrUnit *units[3];
+    int32_t unit_rows[3], unit_cols[3];
+    int32_t unit_size_log2[2];    /* restoration.unit_size[luma, chroma]     */
+    int32_t layout;               /* 0 I400, 1 I420, 2 I422, 3 I444          */
+    int32_t bitdepth_max;
+    int32_t sb128;
+    int32_t restore_planes;       /* LR_RESTORE_Y 1 | U 2 | V 4              */
+} Dav1dGpuLrFrame;
+/* Errors: -1 NULL / bad layout / bad unit grid, -3 launch failure. */
+int dav1d_gpu_lr_frame_8bpc(const Dav1dGpuLrFrame *f, void *stream);
+int dav1d_gpu_lr_frame_16bpc(const Dav1dGpuLrFrame *f, void *stream);
+
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split
  * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).

@@ -2880,3 +2880,135 @@ void oracle_loop_restoration_dsp_init_16bpc(Dav1dLoopRestorationDSPContext_16bpc
     c->sgr[1] = lr_sgr3;
     c->sgr[2] = lr_sgrmix;
 }
+
+/* bytefn(dav1d_lr_sbrow), lr_apply_tmpl.c:169-202, with lr_sbrow (:99-167)
+ * and lr_stripe (:36-97), for every superblock row, single-threaded, no
+ * super-res.  lr_lpf_line is restated per stripe: dav1d_copy_lpf's
+ * backup_lpf (lf_apply_tmpl.c:40-100) keeps, for each stripe boundary B of
+ * the deblocked picture, rows B - 2, B - 1 (above) and B, B + 1 (below; B
+ * again when B + 1 is past the plane). */
+static void lr_unit_params(const Dav1dGpuLrUnit *u, Dav1dGpuLrParams *prm, int *kind)
+{
+    memset(prm, 0, sizeof(*prm));
+    if (u->type == 2) {   /* lr_stripe :51-69 */
+        int16_t (*f)[8] = prm->filter;
+        f[0][0] = f[0][6] = u->filter_h[0];
+        f[0][1] = f[0][5] = u->filter_h[1];
+        f[0][2] = f[0][4] = u->filter_h[2];
+        f[0][3] = -(f[0][0] + f[0][1] + f[0][2]) * 2;
+        if (BITDEPTH != 8) f[0][3] += 128;
+        f[1][0] = f[1][6] = u->filter_v[0];
+        f[1][1] = f[1][5] = u->filter_v[1];
+        f[1][2] = f[1][4] = u->filter_v[2];
+        f[1][3] = 128 - (f[1][0] + f[1][1] + f[1][2]) * 2;
+        *kind = 0;
+    } else {              /* :70-80 */
+        const unsigned short *sp = &dspt_sgr_params[(u->type - 3) * 2];
+        prm->sgr.s0 = sp[0];
+        prm->sgr.s1 = sp[1];
+        prm->sgr.w0 = u->sgr_weights[0];
+        prm->sgr.w1 = 128 - (u->sgr_weights[0] + u->sgr_weights[1]);
+        *kind = 1 + (!!sp[0] + !!sp[1] * 2 - 1);   /* 1 5x5, 2 3x3, 3 mix */
+    }
+}
+
+#if BITDEPTH == 8
+int oracle_lr_frame_8bpc(const Dav1dGpuLrFrame *F)
+#else
+int oracle_lr_frame_16bpc(const Dav1dGpuLrFrame *F)
+#endif
+{
+    if (!F || F->layout < 0 || F->layout > 3) return -1;
+    const int bdmax = BITDEPTH == 8 ? 255 : F->bitdepth_max;
+    const int H0 = F->in[0].h, sb_shift = 6 + F->sb128;
+    const int bh = ((H0 + 7) >> 3) << 1, sbh = (bh + (16 << F->sb128) - 1) >> (4 + F->sb128);
+#if BITDEPTH == 16
+    const int bitdepth_max = bdmax;
+#endif
+    for (int pl = 0; pl < (F->layout ? 3 : 1); pl++) {   /* filter a copy of `in`, as dav1d filters its picture */
+        const ptrdiff_t is = PX(F->in[pl].stride), os = PX(F->out[pl].stride);
+        for (int y = 0; y < F->in[pl].h; y++)
+            memcpy((pixel *)F->out[pl].data + y * os, (const pixel *)F->in[pl].data + y * is,
+                   (size_t)F->in[pl].w * sizeof(pixel));
+    }
+    for (int pl = 0; pl < (F->layout ? 3 : 1); pl++) {
+        if (!(F->restore_planes & (1 << pl))) continue;
+        const int ss_ver = pl && F->layout == 1;
+        const int w = F->in[pl].w, h = F->in[pl].h;
+        const ptrdiff_t ls = PX(F->lpf[pl].stride), os = PX(F->out[pl].stride);
+        pixel *P = (pixel *)F->out[pl].data;
+        const pixel *D = (const pixel *)F->lpf[pl].data;
+        const int unit_size = 1 << F->unit_size_log2[!!pl], half = unit_size >> 1, max_unit = unit_size + half;
+        pixel *lpf = calloc((size_t)8 * os, sizeof(pixel));   /* lr_lpf_line rows, the picture's stride */
+        static pixel border[2][128 + 8][4];
+        for (int sby = 0; sby < sbh; sby++) {   /* dav1d_lr_sbrow :169-202 */
+            const int not_last = sby + 1 < sbh, off = (8 * !!sby) >> ss_ver;
+            const int next_row_y = (sby + 1) << (sb_shift - ss_ver);
+            const int row_h = mini(next_row_y - (8 >> ss_ver) * not_last, h);
+            const int y0 = (sby << (sb_shift - ss_ver)) - off;
+            if (y0 >= h) break;
+            /* lr_sbrow :99-167 */
+            const int row_y = y0 + ((8 >> ss_ver) * !!y0);
+            int aligned = row_y & ~(unit_size - 1);
+            if (aligned && aligned + half > h) aligned -= unit_size;
+            const int urow = aligned >> F->unit_size_log2[!!pl];
+            const Dav1dGpuLrUnit *urow_p = F->units[pl] + (ptrdiff_t)mini(urow, F->unit_rows[pl] - 1) * F->unit_cols[pl];
+            int edges = (y0 > 0 ? DGPU_LR_HAVE_TOP : 0) | DGPU_LR_HAVE_RIGHT;
+            int x = 0, bit = 0, ucol = 0;
+            int restore = urow_p[0].type != 0;
+            pixel *p = P + y0 * os;
+            for (;; bit ^= 1) {
+                const int last = !(x + max_unit <= w);
+                const int unit_w = last ? w - x : unit_size;
+                if (last) edges &= ~DGPU_LR_HAVE_RIGHT;
+                const int restore_next = !last && urow_p[ucol + 1].type != 0;
+                if (restore_next)   /* backup4xU: the next unit's left columns, pre-LR */
+                    for (int j = 0; j < row_h - y0; j++)
+                        memcpy(border[bit][j], p + j * os + unit_size - 4, 4 * sizeof(pixel));
+                if (restore) {      /* lr_stripe :36-97 */
+                    Dav1dGpuLrParams prm;
+                    int kind;
+                    lr_unit_params(&urow_p[ucol], &prm, &kind);
+                    int yy = y0, e = edges;
+                    int stripe_h = mini((64 - 8 * !yy) >> ss_ver, row_h - yy);
+                    const pixel (*left)[4] = (const pixel (*)[4])border[!bit];
+                    pixel *q = p;
+                    while (yy + stripe_h <= row_h) {
+                        const int have_bottom = sby + 1 != sbh || yy + stripe_h != row_h;
+                        e = (e & ~DGPU_LR_HAVE_BOTTOM) | (have_bottom ? DGPU_LR_HAVE_BOTTOM : 0);
+                        /* this stripe's lr_lpf_line rows at columns x - 3 .. x + unit_w + 3 */
+                        for (int c = -3; c < unit_w + 3; c++) {
+                            const int cx = x + c;
+                            if (cx < 0 || cx >= w) continue;
+                            if (yy > 0) {
+                                lpf[0 * os + cx] = D[(yy - 2) * ls + cx];
+                                lpf[1 * os + cx] = D[(yy - 1) * ls + cx];
+                            }
+                            const int B = yy + stripe_h;
+                            if (have_bottom) {
+                                lpf[6 * os + cx] = D[B * ls + cx];
+                                lpf[7 * os + cx] = D[(B + 1 < h ? B + 1 : B) * ls + cx];
+                            }
+                        }
+                        if (kind == 0) lr_wiener(q, os * sizeof(pixel), left, lpf + x, unit_w, stripe_h, &prm, e BDARG);
+                        else lr_sgr(q, os * sizeof(pixel), left, lpf + x, unit_w, stripe_h, &prm, e, kind - 1, bdmax);
+                        left += stripe_h;
+                        yy += stripe_h;
+                        q += stripe_h * os;
+                        e |= DGPU_LR_HAVE_TOP;
+                        stripe_h = mini(64 >> ss_ver, row_h - yy);
+                        if (stripe_h == 0) break;
+                    }
+                }
+                if (last) break;
+                x += unit_size;
+                p += unit_size;
+                ucol++;
+                edges |= DGPU_LR_HAVE_LEFT;
+                restore = restore_next;
+            }
+        }
+        free(lpf);
+    }
+    return 0;
+}

@@ -38,4 +38,6 @@ int oracle_loopfilter_frame_8bpc(const Dav1dGpuLoopFilterFrame *f, int sb128);
 int oracle_loopfilter_frame_16bpc(const Dav1dGpuLoopFilterFrame *f, int sb128);
 void oracle_loop_restoration_dsp_init_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc);
 void oracle_loop_restoration_dsp_init_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc);
+int oracle_lr_frame_8bpc(const Dav1dGpuLrFrame *f);
+int oracle_lr_frame_16bpc(const Dav1dGpuLrFrame *f);
 #endif

@@ -477,3 +477,22 @@ def lr_dsp(bpc, bitdepth=None):
     c = Ctx()
     getattr(L, f"oracle_loop_restoration_dsp_init_{bpc}bpc")(ctypes.byref(c), bitdepth or bpc)
     return c
+
+
+def lr_frame(case):
+    """An lr.LrCase through the oracle's dav1d_lr_sbrow restatement; returns the planes."""
+    import dav1d_mirror_amd.lr as lr
+    abi = _abi()
+    L = load()
+    sfx = 8 if case.bpc == 8 else 16
+    ins = [np.ascontiguousarray(a) for a in case.ins]
+    lpfs = [np.ascontiguousarray(a) for a in case.lpfs]
+    outs = [np.zeros_like(a) for a in ins]
+    f = lr.fill_frame(abi.LrFrame(), case, [(a.ctypes.data, a.shape[1]) for a in ins],
+                      [(a.ctypes.data, a.shape[1]) for a in lpfs], [(a.ctypes.data, a.shape[1]) for a in outs],
+                      [ctypes.addressof(u) for (u, _, _) in case.units])
+    fn = getattr(L, f"oracle_lr_frame_{sfx}bpc")
+    fn.argtypes = [ctypes.POINTER(abi.LrFrame)]
+    fn.restype = ctypes.c_int
+    assert fn(ctypes.byref(f)) == 0
+    return outs
