@@ -345,6 +345,41 @@ def lpf_breakdown(cfg, dev, steps):
             "bit_exact_vs_oracle": all(bool(np.array_equal(a, b)) for a, b in zip(d.outputs_host(), want))}
 
 
+def lr_breakdown(cfg, dev, steps):
+    """loop restoration (dav1d_gpu_lr_frame_*:
+    dav1d_lr_sbrow over a frame) on a synthetic CDEF output of the config's
+    size and bitdepth, 4:2:0, 64-px luma / 32-px chroma units, a mix of
+    Wiener, self-guided and unrestored units: us per frame by HIP events,
+    algorithmic GB/s (picture read once, written once), the oracle's walker on
+    one core, bit-exact check."""
+    import torch
+    import dav1d_mirror_amd.lr as lr
+    c = lr.make_lr_case(seed=11, width=cfg.width, height=cfg.height, bpc=cfg.bpc, bitdepth_max=cfg.bitdepth_max,
+                        layout=1, unit_log2=(6, 5))
+    d = lr.DeviceLr(c, dev)
+    s = torch.cuda.current_stream(dev)
+    for _ in range(3):
+        d.launch(s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = max(steps, 20)
+    e0.record(s)
+    for _ in range(n):
+        d.launch(s)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / n
+    t0 = time.perf_counter()
+    want = ge.load_oracle().lr_frame(c)
+    cpu = time.perf_counter() - t0
+    nbytes = lr.algorithmic_bytes(c)
+    px = sum(w * h for w, h in (c.plane_wh(p) for p in range(3)))
+    return {"frame": f"{cfg.width}x{cfg.height} 4:2:0", "us_per_frame": round(us, 2),
+            "gpix_s": round(px / us / 1e3, 2), "algorithmic_bytes": nbytes,
+            "achieved_gbs": round(nbytes / us / 1e3, 1), "frac_of_hbm_peak": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+            "kernel": f"k_lr_frame<{cfg.bpc}>", "oracle_1core_ms": round(cpu * 1e3, 1),
+            "bit_exact_vs_oracle": all(bool(np.array_equal(a, b)) for a, b in zip(d.outputs_host(), want))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -362,6 +397,7 @@ def main():
     ap.add_argument("--no-grain", action="store_true", help="skip the film-grain measurement (N=1)")
     ap.add_argument("--no-cdef", action="store_true", help="skip the CDEF measurement (N=1)")
     ap.add_argument("--no-lpf", action="store_true", help="skip the deblocking measurement (N=1)")
+    ap.add_argument("--no-lr", action="store_true", help="skip the loop-restoration measurement (N=1)")
     args = ap.parse_args()
 
     import torch
@@ -493,6 +529,8 @@ def main():
             out["cdef"] = cdef_breakdown(cfg, dev, args.steps)
         if not args.no_lpf and world == 1:
             out["loop_filter"] = lpf_breakdown(cfg, dev, args.steps)
+        if not args.no_lr and world == 1:
+            out["loop_restoration"] = lr_breakdown(cfg, dev, args.steps)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
         print(json.dumps(out), flush=True)
