@@ -40,7 +40,13 @@
 
 namespace dgpu {
 
-constexpr int kNone = -32768;
+// Marker for pixels outside the frame's 8x8 grid.  The reference uses
+// INT16_MIN (padding(), src/cdef_tmpl.c:44-54); any value whose distance
+// from every pixel is at least 2^14 behaves the same (constrain() returns 0
+// for it at every strength / damping the format allows: thr << shift < 2^9;
+// it never wins the unsigned min or the signed max), and -16384 keeps every
+// difference inside int16 for the packed filter below.
+constexpr int kNone = -16384;
 
 // (dy, dx) of a direction's two taps: the AV1 CDEF direction set
 // (dav1d_cdef_directions, src/tables.c:400-413, as offsets in a 12-wide
@@ -101,6 +107,47 @@ struct CdefTaps {
         }
         const int v = p + ((sum - (sum < 0) + 8) >> 4);
         return pri && sec ? min(max(v, mn), mx) : v;
+    }
+    // Two pixels at once (c0 and c1, e.g. two rows of a column) in packed
+    // 16-bit math (v_pk_*): every value and difference fits int16 with the
+    // kNone marker, the sums too (|sum| <= 12 taps * 4 * 240).
+    __device__ __forceinline__ void px2(const int16_t *c0, const int16_t *c1, int &o0, int &o1) const {
+        typedef short s2 __attribute__((ext_vector_type(2)));
+        typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+        const s2 zero = { 0, 0 };
+        const s2 p = { c0[0], c1[0] };
+        const s2 tp = { (short)pri, (short)pri }, ts = { (short)sec, (short)sec };
+        const s2 shp = { (short)pri_shift, (short)pri_shift }, shs = { (short)sec_shift, (short)sec_shift };
+        s2 sum = zero, mx = p;
+        u2 mn = __builtin_bit_cast(u2, p);
+        auto cons = [&](s2 t, s2 thr, s2 sh) {
+            const s2 d = t - p;
+            const s2 ad = __builtin_elementwise_max(d, zero - d);
+            const s2 v = __builtin_elementwise_min(ad, __builtin_elementwise_max(zero, thr - (ad >> sh)));
+            const s2 sg = d >> (s2){ 15, 15 };
+            return (s2)((v ^ sg) - sg);
+        };
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const s2 a = { c0[o[k][0]], c1[o[k][0]] }, b = { c0[-o[k][0]], c1[-o[k][0]] };
+            const s2 s0 = { c0[o[k][1]], c1[o[k][1]] }, s1 = { c0[-o[k][1]], c1[-o[k][1]] };
+            const s2 s2_ = { c0[o[k][2]], c1[o[k][2]] }, s3 = { c0[-o[k][2]], c1[-o[k][2]] };
+            const short wp = (short)(k ? tap1 : tap0), ws = (short)(2 - k);
+            sum += (s2){ wp, wp } * (cons(a, tp, shp) + cons(b, tp, shp));
+            sum += (s2){ ws, ws } * (cons(s0, ts, shs) + cons(s1, ts, shs) + cons(s2_, ts, shs) + cons(s3, ts, shs));
+            mn = __builtin_elementwise_min(mn, __builtin_elementwise_min(
+                     __builtin_elementwise_min(__builtin_bit_cast(u2, a), __builtin_bit_cast(u2, b)),
+                     __builtin_elementwise_min(__builtin_elementwise_min(__builtin_bit_cast(u2, s0), __builtin_bit_cast(u2, s1)),
+                                               __builtin_elementwise_min(__builtin_bit_cast(u2, s2_), __builtin_bit_cast(u2, s3)))));
+            mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(
+                     __builtin_elementwise_max(a, b),
+                     __builtin_elementwise_max(__builtin_elementwise_max(s0, s1), __builtin_elementwise_max(s2_, s3))));
+        }
+        const s2 neg = (s2)(sum < zero) & (s2){ 1, 1 };
+        s2 v = p + ((sum - neg + (s2){ 8, 8 }) >> (s2){ 4, 4 });
+        if (pri && sec) v = __builtin_elementwise_min(__builtin_elementwise_max(v, __builtin_bit_cast(s2, mn)), mx);
+        o0 = v.x;
+        o1 = v.y;
     }
 };
 
@@ -252,7 +299,7 @@ struct Stage {
         for (int n = 0; n < N; n++) {
             const int i = threadIdx.x + 256 * n, r = i / G, g = i - r * G;
             if (i >= G * R) break;
-            uint2 v = make_uint2(0x80008000u, 0x80008000u);   // INT16_MIN x 4
+            uint2 v = make_uint2(0xc000c000u, 0xc000c000u);   // kNone x 4
             if (ok[n]) {
                 if constexpr (BPC == 8) {
                     const uint32_t w = raw[n];
@@ -273,7 +320,12 @@ __device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, co
                                         const CdefTaps &tp) {
     using P = typename Px<BPC>::pixel;
 #pragma unroll
-    for (int y = 0; y < BH; y++) dst[y * ds] = (P)(FILT ? tp.px(c + y * S) : c[y * S]);
+    for (int y = 0; y < BH; y += 2) {
+        int v0 = c[y * S], v1 = c[(y + 1) * S];
+        if (FILT) tp.px2(c + y * S, c + (y + 1) * S, v0, v1);
+        dst[y * ds] = (P)v0;
+        dst[(y + 1) * ds] = (P)v1;
+    }
 }
 template <int BPC, int BH>
 __device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const int16_t *c, int S,
