@@ -108,14 +108,16 @@ struct CdefTaps {
         const int v = p + ((sum - (sum < 0) + 8) >> 4);
         return pri && sec ? min(max(v, mn), mx) : v;
     }
-    // Two pixels at once (c0 and c1, e.g. two rows of a column) in packed
-    // 16-bit math (v_pk_*): every value and difference fits int16 with the
-    // kNone marker, the sums too (|sum| <= 12 taps * 4 * 240).
-    __device__ __forceinline__ void px2(const int16_t *c0, const int16_t *c1, int &o0, int &o1) const {
+    // Two pixels at once (rows y and y + 1 of a column) in packed 16-bit
+    // math (v_pk_*), from a pair-interleaved tile whose dword (r, c) holds
+    // rows r and r + 1 of column c: a tap of the pair is one 32-bit LDS read.
+    // Every value and difference fits int16 with the kNone marker, the sums
+    // too (|sum| <= 12 taps * 4 * 240).
+    __device__ __forceinline__ void px2(const uint32_t *c, int &o0, int &o1) const {
         typedef short s2 __attribute__((ext_vector_type(2)));
         typedef unsigned short u2 __attribute__((ext_vector_type(2)));
         const s2 zero = { 0, 0 };
-        const s2 p = { c0[0], c1[0] };
+        const s2 p = __builtin_bit_cast(s2, c[0]);
         const s2 tp = { (short)pri, (short)pri }, ts = { (short)sec, (short)sec };
         const s2 shp = { (short)pri_shift, (short)pri_shift }, shs = { (short)sec_shift, (short)sec_shift };
         s2 sum = zero, mx = p;
@@ -129,9 +131,9 @@ struct CdefTaps {
         };
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            const s2 a = { c0[o[k][0]], c1[o[k][0]] }, b = { c0[-o[k][0]], c1[-o[k][0]] };
-            const s2 s0 = { c0[o[k][1]], c1[o[k][1]] }, s1 = { c0[-o[k][1]], c1[-o[k][1]] };
-            const s2 s2_ = { c0[o[k][2]], c1[o[k][2]] }, s3 = { c0[-o[k][2]], c1[-o[k][2]] };
+            const s2 a = __builtin_bit_cast(s2, c[o[k][0]]), b = __builtin_bit_cast(s2, c[-o[k][0]]);
+            const s2 s0 = __builtin_bit_cast(s2, c[o[k][1]]), s1 = __builtin_bit_cast(s2, c[-o[k][1]]);
+            const s2 s2_ = __builtin_bit_cast(s2, c[o[k][2]]), s3 = __builtin_bit_cast(s2, c[-o[k][2]]);
             const short wp = (short)(k ? tap1 : tap0), ws = (short)(2 - k);
             sum += (s2){ wp, wp } * (cons(a, tp, shp) + cons(b, tp, shp));
             sum += (s2){ ws, ws } * (cons(s0, ts, shs) + cons(s1, ts, shs) + cons(s2_, ts, shs) + cons(s3, ts, shs));
@@ -280,55 +282,60 @@ template <int BPC> struct CdefArgs {
 // three planes' loads are all in flight before the first store waits.
 template <int BPC, int W, int H>
 struct Stage {
-    static constexpr int G = (W + 8) / 4, R = H + 4, S = W + 8, N = (G * R + 255) / 256;
+    // pair-interleaved: dword (r, c) = rows r and r + 1 of column c, for the
+    // H + 3 pairs of the H + 4 staged rows
+    static constexpr int G = (W + 8) / 4, R = H + 3, S = W + 8, N = (G * R + 255) / 256;
     using Raw = typename std::conditional<BPC == 8, uint32_t, uint2>::type;
-    Raw raw[N];
-    bool ok[N];
+    Raw raw[N], raw2[N];
+    bool ok[N], ok2[N];
     __device__ __forceinline__ void load(const typename Px<BPC>::pixel *src, int stride, int x0, int y0, int gw,
                                          int gh) {
 #pragma unroll
         for (int n = 0; n < N; n++) {
             const int i = threadIdx.x + 256 * n, r = i / G, g = i - r * G;
             const int Y = y0 - 2 + r, X = x0 - 4 + 4 * g;
-            ok[n] = i < G * R && Y >= 0 && Y < gh && X >= 0 && X < gw;
+            const bool col = i < G * R && X >= 0 && X < gw;
+            ok[n] = col && Y >= 0 && Y < gh;
+            ok2[n] = col && Y + 1 >= 0 && Y + 1 < gh;
             if (ok[n]) raw[n] = *reinterpret_cast<const Raw *>(src + (size_t)Y * stride + X);
+            if (ok2[n]) raw2[n] = *reinterpret_cast<const Raw *>(src + (size_t)(Y + 1) * stride + X);
         }
     }
-    __device__ __forceinline__ void store(int16_t *t) const {
+    static __device__ __forceinline__ uint32_t px(const Raw &w, bool ok, int k) {
+        if (!ok) return 0xc000u;   // kNone
+        if constexpr (BPC == 8) return (w >> (8 * k)) & 0xff;
+        else return ((k < 2 ? w.x : w.y) >> (16 * (k & 1))) & 0xffff;
+    }
+    __device__ __forceinline__ void store(uint32_t *t) const {
 #pragma unroll
         for (int n = 0; n < N; n++) {
             const int i = threadIdx.x + 256 * n, r = i / G, g = i - r * G;
             if (i >= G * R) break;
-            uint2 v = make_uint2(0xc000c000u, 0xc000c000u);   // kNone x 4
-            if (ok[n]) {
-                if constexpr (BPC == 8) {
-                    const uint32_t w = raw[n];
-                    v.x = (w & 0xff) | ((w & 0xff00) << 8);
-                    v.y = ((w >> 16) & 0xff) | ((w >> 8) & 0xff0000);
-                } else {
-                    v = raw[n];
-                }
-            }
-            *reinterpret_cast<uint2 *>(&t[r * S + 4 * g]) = v;
+            uint4 v;
+            v.x = px(raw[n], ok[n], 0) | (px(raw2[n], ok2[n], 0) << 16);
+            v.y = px(raw[n], ok[n], 1) | (px(raw2[n], ok2[n], 1) << 16);
+            v.z = px(raw[n], ok[n], 2) | (px(raw2[n], ok2[n], 2) << 16);
+            v.w = px(raw[n], ok[n], 3) | (px(raw2[n], ok2[n], 3) << 16);
+            *reinterpret_cast<uint4 *>(&t[r * S + 4 * g]) = v;
         }
     }
 };
 
-// Filter (FILT) or copy one column of BH pixels of a block from its tile.
+// Filter (FILT) or copy one column of BH pixels of a block from its pair tile.
 template <int BPC, int BH, bool FILT>
-__device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const int16_t *c, int S,
+__device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const uint32_t *c, int S,
                                         const CdefTaps &tp) {
     using P = typename Px<BPC>::pixel;
 #pragma unroll
     for (int y = 0; y < BH; y += 2) {
-        int v0 = c[y * S], v1 = c[(y + 1) * S];
-        if (FILT) tp.px2(c + y * S, c + (y + 1) * S, v0, v1);
+        int v0 = (int)(c[y * S] & 0xffff), v1 = (int)(c[y * S] >> 16);
+        if (FILT) tp.px2(c + y * S, v0, v1);
         dst[y * ds] = (P)v0;
         dst[(y + 1) * ds] = (P)v1;
     }
 }
 template <int BPC, int BH>
-__device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const int16_t *c, int S,
+__device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const uint32_t *c, int S,
                                         const CdefTaps &tp, bool filt) {
     if (filt) col_out<BPC, BH, true>(dst, ds, c, S, tp);
     else col_out<BPC, BH, false>(dst, ds, c, S, tp);
@@ -341,8 +348,8 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
     constexpr int LS = 64 + 8;                      // luma tile stride
     constexpr int CW = 64 >> SX, CH = 64 >> SY, CS = CW + 8;
     constexpr int CBW = 8 >> SX, CBH = 8 >> SY;     // chroma block
-    __shared__ __attribute__((aligned(16))) int16_t tl[(64 + 4) * LS];
-    __shared__ __attribute__((aligned(16))) int16_t tc[LAYOUT ? 2 : 1][LAYOUT ? (CH + 4) * CS : 8];
+    __shared__ __attribute__((aligned(16))) uint32_t tl[(64 + 3) * LS];   // pair tiles
+    __shared__ __attribute__((aligned(16))) uint32_t tc[LAYOUT ? 2 : 1][LAYOUT ? (CH + 3) * CS : 4];
     __shared__ unsigned cost[8][64];
     __shared__ uint8_t skip[64];
     __shared__ uint8_t bdir[64], bpri[64];   // per block: direction, adjusted luma strength (<= 240)
@@ -390,14 +397,17 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
         const int bx8 = blk & 7, by8 = blk >> 3;
         if (sbx * 8 + bx8 < a.b8w && sby * 8 + by8 < a.b8h) {
             int v[8][8];
-            const int16_t *c = &tl[(by8 * 8 + 2) * LS + bx8 * 8 + 4];
+            const uint32_t *c = &tl[(by8 * 8 + 2) * LS + bx8 * 8 + 4];
 #pragma unroll
-            for (int y = 0; y < 8; y++) {
-                const uint4 r = *reinterpret_cast<const uint4 *>(c + y * LS);
-                const uint32_t w[4] = { r.x, r.y, r.z, r.w };
+            for (int y = 0; y < 8; y += 2) {   // one pair row gives two block rows
+                const uint4 r0 = *reinterpret_cast<const uint4 *>(c + y * LS);
+                const uint4 r1 = *reinterpret_cast<const uint4 *>(c + y * LS + 4);
+                const uint32_t w[8] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w };
 #pragma unroll
-                for (int x = 0; x < 8; x++)
-                    v[y][x] = ((int)((w[x >> 1] >> (16 * (x & 1))) & 0xffff) >> bd8) - 128;
+                for (int x = 0; x < 8; x++) {
+                    v[y][x] = ((int)(w[x] & 0xffff) >> bd8) - 128;
+                    v[y + 1][x] = ((int)(w[x] >> 16) >> bd8) - 128;
+                }
             }
             cdef_costs(q, v, &cost[0][blk], 64);
         }
@@ -420,7 +430,7 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
         const int by8 = t >> 6, l = t & 63, bx8 = l >> 3, x = l & 7, blk = by8 * 8 + bx8;
         const int gx8 = sbx * 8 + bx8, gy8 = sby * 8 + by8;
         if (gx8 >= a.b8w || gy8 >= a.b8h) continue;
-        const int16_t *c = &tl[(by8 * 8 + 2) * LS + bx8 * 8 + 4 + x];
+        const uint32_t *c = &tl[(by8 * 8 + 2) * LS + bx8 * 8 + 4 + x];
         P *dst = a.out[0] + (size_t)(gy8 * 8) * a.os[0] + gx8 * 8 + x;
         CdefTaps tp;
         bool filt = false;
@@ -441,7 +451,7 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
         const int by8 = r / LB, l = r - by8 * LB, bx8 = l / CBW, x = l - bx8 * CBW, blk = by8 * 8 + bx8;
         const int gx8 = sbx * 8 + bx8, gy8 = sby * 8 + by8;
         if (gx8 >= a.b8w || gy8 >= a.b8h) continue;
-        const int16_t *c = &tc[pl][(by8 * CBH + 2) * CS + bx8 * CBW + 4 + x];
+        const uint32_t *c = &tc[pl][(by8 * CBH + 2) * CS + bx8 * CBW + 4 + x];
         P *dst = a.out[1 + pl] + (size_t)(gy8 * CBH) * a.os[1 + pl] + gx8 * CBW + x;
         CdefTaps tp;
         bool filt = false;
