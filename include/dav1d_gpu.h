@@ -14,6 +14,10 @@
  *     init hooks  bitfn(dav1d_mc_dsp_init)         src/mc_tmpl.c:915
  *                 bitfn(dav1d_intra_pred_dsp_init) src/ipred_tmpl.c:740
  *                 bitfn(dav1d_itx_dsp_init)        src/itx_tmpl.c:200
+ *     and, for the post-filters, further below:
+ *       Dav1dLoopFilterDSPContext      src/loopfilter.h:39-52
+ *       Dav1dCdefDSPContext            src/cdef.h:64-67
+ *       Dav1dLoopRestorationDSPContext src/looprestoration.h:62-72
  *     The struct layouts below are layout-identical to the reference ones
  *     (arrays of function pointers in the same order), so a pointer to the
  *     reference's context can be passed straight in.
@@ -22,6 +26,8 @@
  *     frame (or superblock row) of transform-block units: prediction
  *     (mc / mct+avg / intra) fused with inv_txfm_add.  All pointers are
  *     device pointers already resident in HBM; see dav1d_gpu_recon_*.
+ *     Frame-tier entries also cover the intra wavefront, the batch recorder,
+ *     deblocking, CDEF, loop restoration and film grain. 
  *
  * Strides are in BYTES and may be negative, as in the reference.  16bpc entry
  * points take the trailing `bitdepth_max` argument (0x3ff or 0xfff) except
