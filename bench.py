@@ -51,27 +51,43 @@ def log(*a):
 
 
 def cpu_baseline(fd, budget_s=12.0):
-    """The oracle (C restatement of dav1d's C DSP) on this host's cores,
-    single thread, over whole frames until ~budget_s of CPU work."""
+    """The oracle (C restatement of dav1d's C DSP) on this host's cores over
+    whole frames: first on every usable core (the box's CPU share: at most 16
+    threads, units split into contiguous ranges), then single-thread beside
+    it, each for about budget_s / 2 of wall time."""
     orc = ge.load_oracle()
     hf = orc.HostFrame(fd)
-    frames = 0
-    t0 = time.perf_counter()
-    while True:
-        hf.run(threads=1)
-        frames += 1
-        el = time.perf_counter() - t0
-        if el > budget_s or frames >= 64:
-            break
-    px = fd.stats["pixels"] * frames
-    return {"value": round(px / el / 1e9, 5), "unit": "Gpixels/s", "cores": 1, "kind": "port",
-            "sample": f"{frames} full frame(s) of the same batch ({fd.stats['pixels']} px each), "
-                      f"{el:.1f} s single-thread, oracle/dsp_ref.c -O2 (restatement of dav1d C, not dav1d)"}
+
+    def timed(threads, budget):
+        frames = 0
+        t0 = time.perf_counter()
+        while True:
+            hf.run(threads=threads)
+            frames += 1
+            el = time.perf_counter() - t0
+            if el > budget or frames >= 64:
+                return frames, el
+
+    nthr = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
+    fm, em = timed(nthr, budget_s / 2)
+    f1, e1 = timed(1, budget_s / 2)
+    px = fd.stats["pixels"]
+    return {"value": round(px * fm / em / 1e9, 5), "unit": "Gpixels/s", "cores": nthr, "kind": "port",
+            "sample": f"{fm} full frame(s) of the same batch ({px} px each), {em:.1f} s on {nthr} threads "
+                      f"(unit ranges split per thread), oracle/dsp_ref.c -O2 (restatement of dav1d C, not dav1d; "
+                      f"AVX2 baseline unavailable: no nasm/meson)",
+            "single_thread": {"value": round(px * f1 / e1 / 1e9, 5), "cores": 1,
+                              "sample": f"{f1} full frame(s), {e1:.1f} s single-thread"}}
 
 
-# rocprofv3 PMC summaries of the current kernels (tools/prof.sh + tools/pmc_summary.py)
-PMC_SUMMARY = {8: os.path.join(ROOT, "profiles", "r2", "r2a_pmc_summary.json"),
-               16: os.path.join(ROOT, "profiles", "r2", "r2a_10bit_pmc_summary.json")}
+# rocprofv3 summaries of the current kernels (tools/prof.sh + tools/pmc_summary.py):
+# the kernel-trace averages (cross-check of the event timing below) and the
+# PMC traffic of separate FETCH_SIZE / WRITE_SIZE passes
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r3")
+PMC_SUMMARY = {8: os.path.join(PROFILE_DIR, "r3_pmc_summary.json"),
+               16: os.path.join(PROFILE_DIR, "r3_10bit_pmc_summary.json")}
+KERNEL_STATS = {8: os.path.join(PROFILE_DIR, "r3_kernel_stats.csv"),
+                16: os.path.join(PROFILE_DIR, "r3_10bit_kernel_stats.csv")}
 
 
 def pmc_traffic(bpc):
@@ -95,6 +111,23 @@ def pmc_traffic(bpc):
                       "not these scattered row loads)")
 
 
+def rocprof_kernel_us(bpc):
+    """Average duration (us) of the frame's k_recon launches in the committed
+    rocprofv3 --kernel-trace --stats summary (sum over the launch groups of
+    one frame), or None."""
+    import csv
+    try:
+        rows = list(csv.DictReader(open(KERNEL_STATS[bpc])))
+    except OSError:
+        return None
+    us = 0.0
+    for r in rows:
+        name = r.get("Name", "")
+        if f"k_recon<{bpc}," in name or f"k_reconILi{bpc}E" in name:
+            us += float(r["AverageNs"]) / 1e3
+    return round(us, 2) if us else None
+
+
 FAMILIES = {
     # per-family frames (SURVEY 8(d): "also report per-family Gpix/s")
     "mc": "inter only: mc put / mct x2 + avg per block, no residual",
@@ -114,6 +147,31 @@ def kernel_seconds(frame, stream, n):
         b.record(stream)
     torch.cuda.synchronize()
     return float(np.mean([a.elapsed_time(b) for a, b in evs])) * 1e-3
+
+
+def config_legs(dev, stream, steps):
+    """BASELINE.json configs[1] and configs[3] at N=1 beside the headline:
+    the 1080p mc-only frame and the 10-bit 4K full frame, one launch each
+    (kernel time by HIP events on the launch stream)."""
+    import dav1d_mirror_amd.workload as wl
+    import dav1d_mirror_amd.batch as bt
+    out = {}
+    for name in ("1080p-mc", "4k-10bit"):
+        c = dict(CONFIGS[name])
+        label = c.pop("label")
+        fd = wl.make_frame(wl.FrameConfig(**c))
+        frame = bt.DeviceFrame(fd, dev)
+        for _ in range(3):
+            frame.launch(stream)
+        ks = kernel_seconds(frame, stream, max(steps, 10))
+        b = fd.stats["total_bytes"]
+        out[name] = {"workload": label, "units": fd.n_units, "pixels": fd.stats["pixels"],
+                     "kernel_us": round(ks * 1e6, 2), "gpix_s": round(fd.stats["pixels"] / ks / 1e9, 2),
+                     "algorithmic_bytes": b, "achieved_gbs": round(b / ks / 1e9, 1),
+                     "frac": round(b / ks / 1e9 / HBM_PEAK_GBS, 4), "desc_bytes": fd.stats["desc_bytes"],
+                     "rocprof_kernel_us": rocprof_kernel_us(c.get("bpc", 8)) if name == "4k-10bit" else None}
+        del frame
+    return out
 
 
 def family_breakdown(base_cfg, dev, stream, steps):
@@ -391,6 +449,7 @@ def main():
     ap.add_argument("--feed", default="local", choices=["local", "rccl"],
                     help="local: each rank generates its frame; rccl: rank 0 generates all and scatters")
     ap.add_argument("--no-families", action="store_true", help="skip the per-family breakdown (N=1)")
+    ap.add_argument("--no-configs", action="store_true", help="skip the 1080p-mc / 4k-10bit legs (N=1)")
     ap.add_argument("--no-tiles", action="store_true", help="skip the tile-batch measurement (N=1)")
     ap.add_argument("--no-intra", action="store_true", help="skip the intra-wavefront measurement (N=1)")
     ap.add_argument("--no-recorder", action="store_true", help="skip the batch-recorder measurement (N=1)")
@@ -506,15 +565,24 @@ def main():
                 "kernel": f"k_recon<{cfg.bpc},*> (main group: all classes up to 32x32 in one launch; "
                           "the 64-point group launches only when such units exist; events bracket the step)",
                 "kernel_us": round(kern_s * 1e6, 2),
+                "rocprof_kernel_us": rocprof_kernel_us(cfg.bpc) if args.config != "1080p-mc" else None,
+                "rocprof_source": os.path.relpath(KERNEL_STATS[cfg.bpc], ROOT),
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "bytes_breakdown": {k: fd.stats[k] for k in
-                                    ("ref_bytes", "edge_bytes", "coef_bytes", "dst_bytes", "desc_bytes")},
+                                    ("ref_bytes", "edge_bytes", "coef_bytes", "dst_bytes", "dst_read_bytes",
+                                     "aux_bytes")},
+                "desc_bytes": fd.stats["desc_bytes"],
+                "accounting": "achieved = algorithmic bytes per launch (SURVEY 8(d): per-block reference "
+                              "footprints + edges + stored coefficients + output, no descriptors) / mean "
+                              "launch duration by HIP events on the launch stream",
             },
         }
         if check is not None:
             out["config"]["bit_exact_vs_oracle"] = check
         if feed is not None:
             out["feed"] = feed
+        if not args.no_configs and world == 1 and args.config == "4k":
+            out["configs"] = config_legs(dev, stream, args.steps)
         if not args.no_families and world == 1 and c.get("kind") == "full":
             out["families"] = family_breakdown(cfg, dev, stream, args.steps)
         if not args.no_tiles and world == 1:

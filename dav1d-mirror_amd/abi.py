@@ -284,6 +284,10 @@ def load_lib():
         L.dav1d_gpu_recorder_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
                                                ctypes.POINTER(ctypes.c_int32)]
         L.dav1d_gpu_recorder_stats.restype = ctypes.c_int
+        L.dav1d_gpu_recorder_status.argtypes = [ctypes.c_void_p]
+        L.dav1d_gpu_recorder_status.restype = ctypes.c_int
+        L.dav1d_gpu_get_error.restype = ctypes.c_int
+        L.dav1d_gpu_clear_error.restype = ctypes.c_int
         L.dav1d_gpu_intra_workspace_bytes.argtypes = [ctypes.POINTER(IntraSchedule), ctypes.c_int]
         L.dav1d_gpu_intra_workspace_bytes.restype = ctypes.c_int64
         L.dav1d_gpu_recon_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -301,6 +305,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_intra_pred_dsp_init_gpu_8bpc", "dav1d_intra_pred_dsp_init_gpu_16bpc",
     "dav1d_itx_dsp_init_gpu_8bpc", "dav1d_itx_dsp_init_gpu_16bpc",
     "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version",
+    "dav1d_gpu_get_error", "dav1d_gpu_clear_error",
     "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc", "dav1d_gpu_recon_lds_bytes",
     "dav1d_gpu_recon_tiles_8bpc", "dav1d_gpu_recon_tiles_16bpc",
     "dav1d_gpu_prepare_intra_edges_8bpc", "dav1d_gpu_prepare_intra_edges_16bpc",
@@ -308,7 +313,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_recon_intra_frame_8bpc", "dav1d_gpu_recon_intra_frame_16bpc",
     "dav1d_gpu_intra_workspace_bytes",
     "dav1d_gpu_recorder_new", "dav1d_gpu_recorder_free", "dav1d_gpu_rec_block", "dav1d_gpu_rec_residual",
-    "dav1d_gpu_recorder_flush", "dav1d_gpu_recorder_stats",
+    "dav1d_gpu_recorder_flush", "dav1d_gpu_recorder_stats", "dav1d_gpu_recorder_status",
     "dav1d_gpu_apply_grain_8bpc", "dav1d_gpu_apply_grain_16bpc",
     "dav1d_cdef_dsp_init_8bpc", "dav1d_cdef_dsp_init_16bpc",
     "dav1d_cdef_dsp_init_gpu_8bpc", "dav1d_cdef_dsp_init_gpu_16bpc",

@@ -576,7 +576,7 @@ __global__ __launch_bounds__(64) void k_cdef_dir(const typename Px<BPC>::pixel *
 }
 
 template <int BPC, int W, int H>
-static void cdef_fb_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride, const typename Px<BPC>::pixel (*left)[2],
+static bool cdef_fb_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride, const typename Px<BPC>::pixel (*left)[2],
                       const typename Px<BPC>::pixel *top, const typename Px<BPC>::pixel *bottom, int pri, int sec,
                       int dir, int damping, int edges, int bdmax) {
     using P = typename Px<BPC>::pixel;
@@ -590,43 +590,57 @@ static void cdef_fb_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride, const type
     const int il = (edges & DGPU_CDEF_HAVE_LEFT) ? st.in1(left, 2 * H * B) : -1;
     const int it = (edges & DGPU_CDEF_HAVE_TOP) ? st.in(top, stride, xs * B, xe * B, 0, 2) : -1;
     const int ib = (edges & DGPU_CDEF_HAVE_BOTTOM) ? st.in(bottom, stride, xs * B, xe * B, 0, 2) : -1;
-    st.upload();
+    if (!st.upload()) return false;
     k_cdef_fb<BPC><<<1, 64, 0, st.stream()>>>(
         st.origin<P>(od), st.pitch(od) / B, st.origin<const P>(id), st.pitch(id) / B,
         il >= 0 ? st.origin<const P>(il) : nullptr, it >= 0 ? st.origin<const P>(it) : nullptr,
         it >= 0 ? st.pitch(it) / B : 0, ib >= 0 ? st.origin<const P>(ib) : nullptr, ib >= 0 ? st.pitch(ib) / B : 0,
         pri, sec, dir, damping, edges, W, H, bdmax);
-    st.finish();
+    return st.finish();
 }
 
 template <int BPC>
-static int cdef_dir_t(const typename Px<BPC>::pixel *img, ptrdiff_t stride, unsigned *var, int bdmax) {
+static bool cdef_dir_t(const typename Px<BPC>::pixel *img, ptrdiff_t stride, unsigned *var, int *dir, int bdmax) {
     using P = typename Px<BPC>::pixel;
     constexpr long B = sizeof(P);
     int32_t res[2] = { 0, 0 };
     Stager st;
     const int ii = st.in(img, stride, 0, 8 * B, 0, 8);
     const int orr = st.out1(res, sizeof(res));
-    st.upload();
+    if (!st.upload()) return false;
     k_cdef_dir<BPC><<<1, 64, 0, st.stream()>>>(st.origin<const P>(ii), st.pitch(ii) / B, st.origin<int32_t>(orr),
                                                bdmax);
-    st.finish();
+    if (!st.finish()) return false;
     *var = (unsigned)res[1];
-    return res[0];
+    *dir = res[0];
+    return true;
 }
+
+// The caller's entries before dav1d_cdef_dsp_init_gpu_* overwrote them (run
+// when the GPU path fails: runtime.hpp's error contract).
+static Dav1dCdefDSPContext_8bpc g_fb8;
+static Dav1dCdefDSPContext_16bpc g_fb16;
 
 #define CDEF_ENTRIES(BPC, P, BDP, BDV)                                                                    \
 template <int W, int H>                                                                                   \
 static void cdef_fb_##BPC(P *d, ptrdiff_t s, const P (*l)[2], const P *t, const P *b, int pri, int sec,  \
                           int dir, int damping, int edges BDP)                                            \
-{ cdef_fb_t<BPC, W, H>(d, s, l, t, b, pri, sec, dir, damping, edges, BDV); }                             \
+{ DGPU_OR_FALLBACK((cdef_fb_t<BPC, W, H>(d, s, l, t, b, pri, sec, dir, damping, edges, BDV)),            \
+                   g_fb##BPC.fb[W == 8 ? 0 : H == 8 ? 1 : 2], d, s, l, t, b, pri, sec, dir, damping,     \
+                   edges BDV##_ARG); }                                                                    \
 static int cdef_dir_##BPC(const P *img, ptrdiff_t s, unsigned *var BDP)                                   \
-{ return cdef_dir_t<BPC>(img, s, var, BDV); }
+{                                                                                                         \
+    int dir = 0;                                                                                          \
+    if (cdef_dir_t<BPC>(img, s, var, &dir, BDV)) return dir;                                              \
+    return g_fb##BPC.dir ? g_fb##BPC.dir(img, s, var BDV##_ARG) : 0;                                      \
+}
 
 #define BD8_PARAM
 #define BD8_VAL 255
+#define BD8_VAL_ARG
 #define BD16_PARAM , int bitdepth_max
 #define BD16_VAL bitdepth_max
+#define BD16_VAL_ARG , bitdepth_max
 CDEF_ENTRIES(8, uint8_t, BD8_PARAM, BD8_VAL)
 CDEF_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 
@@ -643,8 +657,19 @@ CDEF_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 using namespace dgpu;
 
 // bitfn(dav1d_cdef_dsp_init) replacement, src/cdef_tmpl.c:316-331
-extern "C" void dav1d_cdef_dsp_init_gpu_8bpc(Dav1dCdefDSPContext_8bpc *c) { FILL_CDEF(8, c); }
-extern "C" void dav1d_cdef_dsp_init_gpu_16bpc(Dav1dCdefDSPContext_16bpc *c) { FILL_CDEF(16, c); }
+// The _gpu_ hooks keep the caller's previous entries as fallbacks.
+extern "C" void dav1d_cdef_dsp_init_gpu_8bpc(Dav1dCdefDSPContext_8bpc *c) {
+    Dav1dCdefDSPContext_8bpc g{}, *gp = &g;
+    FILL_CDEF(8, gp);
+    save_fallback(&g_fb8, c, gp);
+    FILL_CDEF(8, c);
+}
+extern "C" void dav1d_cdef_dsp_init_gpu_16bpc(Dav1dCdefDSPContext_16bpc *c) {
+    Dav1dCdefDSPContext_16bpc g{}, *gp = &g;
+    FILL_CDEF(16, gp);
+    save_fallback(&g_fb16, c, gp);
+    FILL_CDEF(16, c);
+}
 extern "C" void dav1d_cdef_dsp_init_8bpc(Dav1dCdefDSPContext_8bpc *c) { FILL_CDEF(8, c); }
 extern "C" void dav1d_cdef_dsp_init_16bpc(Dav1dCdefDSPContext_16bpc *c) { FILL_CDEF(16, c); }
 

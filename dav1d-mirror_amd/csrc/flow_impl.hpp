@@ -58,6 +58,7 @@ struct FlowArgs {
     const int32_t *dep_start;     // dataflow: per unit, its producer units (CSR); NULL: levels
     const int32_t *deps;
     unsigned long long *trace;    // DGPU_FLOW_TRACE: [ticket][4] start, ready, computed, released
+    int spin_limit;               // polls before a wave gives up (DGPU_FLOW_SPIN_LIMIT)
 };
 
 template <int BPC>
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
                 for (int it = 0;; it++) {
                     const int v = dep < 0 ? 1 : __hip_atomic_load(&f.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (__all(v != 0)) break;
-                    if (it >= DGPU_FLOW_SPIN_LIMIT ||
+                    if (it >= f.spin_limit ||
                         __hip_atomic_load(&f.ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                         ok = 0;
                         break;
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
                 int *done = &f.ctr[kFlowCtrHead + kFlowCtrStride * (level - 1)];
                 for (int it = 0;; it++) {
                     if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
-                    if (it >= DGPU_FLOW_SPIN_LIMIT ||
+                    if (it >= f.spin_limit ||
                         __hip_atomic_load(&f.ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                         ok = 0;
                         break;
@@ -209,19 +210,22 @@ static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<F
 // Page-locked staging for the task list: a pageable source would make the
 // copy wait for everything already queued on the stream.  A small pool of
 // buffers, each reusable once the event recorded after its copy has passed.
+// Buffers and events belong to the device they were made on (recorders may
+// run on different devices): a buffer is only reused on its own device.
 struct FlowStage {
     void *p = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
+    int device = -1;
 };
 static std::mutex g_stage_mu;
 static std::vector<FlowStage> g_stage;
 
-static FlowStage *flow_stage_get(size_t n) {   // call with g_stage_mu held
+static FlowStage *flow_stage_get(size_t n, int device) {   // call with g_stage_mu held
     for (FlowStage &st : g_stage)
-        if (st.cap >= n && hipEventQuery(st.ev) == hipSuccess) return &st;
+        if (st.device == device && st.cap >= n && hipEventQuery(st.ev) == hipSuccess) return &st;
     for (FlowStage &st : g_stage)   // a free but small one: grow it
-        if (hipEventQuery(st.ev) == hipSuccess) {
+        if (st.device == device && hipEventQuery(st.ev) == hipSuccess) {
             (void)hipHostFree(st.p);
             st.p = nullptr;
             st.cap = 0;
@@ -229,8 +233,16 @@ static FlowStage *flow_stage_get(size_t n) {   // call with g_stage_mu held
             st.cap = n;
             return &st;
         }
-    if (g_stage.size() >= 8) {   // all busy: wait for the oldest
-        FlowStage &st = g_stage.front();
+    int mine = 0;
+    for (FlowStage &st : g_stage) mine += st.device == device;
+    if (mine >= 8) {   // all busy: wait for this device's oldest
+        FlowStage *old = nullptr;
+        for (FlowStage &st : g_stage)
+            if (st.device == device) {
+                old = &st;
+                break;
+            }
+        FlowStage &st = *old;
         if (hipEventSynchronize(st.ev) != hipSuccess) return nullptr;
         if (st.cap < n) {
             (void)hipHostFree(st.p);
@@ -243,6 +255,7 @@ static FlowStage *flow_stage_get(size_t n) {   // call with g_stage_mu held
     }
     g_stage.emplace_back();
     FlowStage &st = g_stage.back();
+    st.device = device;
     if (hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&st.p, n, hipHostMallocDefault) != hipSuccess) {
         g_stage.pop_back();
@@ -325,10 +338,16 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     f.dep_start = dataflow ? (const int32_t *)(ws + Lw.dstart) : nullptr;
     f.deps = (const int32_t *)(ws + Lw.deps);
     f.trace = (unsigned long long *)(ws + Lw.trace);
+    // DAV1D_GPU_FLOW_SPIN_LIMIT (tests): a smaller poll bound makes waves give
+    // up early, to exercise the error word's reporting
+    f.spin_limit = DGPU_FLOW_SPIN_LIMIT;
+    if (const char *sl = getenv("DAV1D_GPU_FLOW_SPIN_LIMIT")) f.spin_limit = (int)strtol(sl, nullptr, 0);
     {   // the task list and producer lists through page-locked staging (asynchronous copy)
         const size_t up = Lw.deps + (size_t)nd * 4 - Lw.tasks;
         std::lock_guard<std::mutex> lock(g_stage_mu);
-        FlowStage *sg = flow_stage_get(up);
+        int device = 0;
+        if (hipGetDevice(&device) != hipSuccess) return -3;
+        FlowStage *sg = flow_stage_get(up, device);
         if (!sg) return -3;
         uint8_t *st = (uint8_t *)sg->p;
         memcpy(st, tasks.data(), tasks.size() * sizeof(FlowTask));
@@ -337,10 +356,14 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
             memcpy(st + (Lw.dstart - Lw.tasks), s->dep_start, ((size_t)b->n_units + 1) * 4);
             memcpy(st + (Lw.deps - Lw.tasks), s->deps, (size_t)nd * 4);
         }
-        if (hipMemsetAsync(ws, 0, Lw.tasks, stream) != hipSuccess ||   // counters and done flags
-            hipMemcpyAsync(ws + Lw.tasks, sg->p, up, hipMemcpyHostToDevice, stream) != hipSuccess ||
-            hipEventRecord(sg->ev, stream) != hipSuccess)
+        if (hipMemsetAsync(ws, 0, Lw.tasks, stream) != hipSuccess) return -3;   // counters and done flags
+        // once the copy may be queued, the buffer is busy until the stream
+        // has passed it: on a later failure drain the stream before returning
+        if (hipMemcpyAsync(ws + Lw.tasks, sg->p, up, hipMemcpyHostToDevice, stream) != hipSuccess ||
+            hipEventRecord(sg->ev, stream) != hipSuccess) {
+            (void)hipStreamSynchronize(stream);
             return -3;
+        }
     }
     ReconArgs<BPC> a;
     memset(&a, 0, sizeof(a));

@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void k_pal(typename Px<BPC>::pixel *dst, ptrdi
 
 // ---------------------------------------------------------------------------
 template <int BPC>
-static void run_ipred(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
+static bool run_ipred(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
                       const typename Px<BPC>::pixel *tl, int w, int h, int mode, int angle,
                       int max_w, int max_h, const int16_t *ac, int alpha, int cfl, int bdmax) {
     using P = typename Px<BPC>::pixel;
@@ -355,7 +355,7 @@ static void run_ipred(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
     const int ie = st.in1(tl - 2 * h, (long)(2 * h + 2 * w + 1) * B);
     const int ia = cfl ? st.in1(ac, (long)w * h * 2) : -1;
     const int od = st.out(dst, stride, 0, w * B, 0, h);
-    st.upload();
+    if (!st.upload()) return false;
     IpredArgs<BPC> a;
     a.dst = st.origin<P>(od);
     a.ds = st.pitch(od) / B;
@@ -366,11 +366,11 @@ static void run_ipred(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
     a.alpha = alpha;
     a.cfl = cfl;
     k_ipred<BPC><<<1, 256, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
 
 template <int BPC, int SSH, int SSV>
-static void cfl_ac_t(int16_t *ac, const typename Px<BPC>::pixel *y, ptrdiff_t stride, int w_pad,
+static bool cfl_ac_run(int16_t *ac, const typename Px<BPC>::pixel *y, ptrdiff_t stride, int w_pad,
                      int h_pad, int cw, int ch) {
     using P = typename Px<BPC>::pixel;
     constexpr long B = sizeof(P);
@@ -378,18 +378,18 @@ static void cfl_ac_t(int16_t *ac, const typename Px<BPC>::pixel *y, ptrdiff_t st
     Stager st;
     const int iy = st.in(y, stride, 0, vw * B, 0, vh);
     const int oa = st.out1(ac, (long)cw * ch * 2);
-    st.upload();
+    if (!st.upload()) return false;
     CflAcArgs<BPC> a;
     a.ac = st.origin<int16_t>(oa);
     a.y = st.origin<const P>(iy);
     a.ys = st.pitch(iy) / B;
     a.w_pad = w_pad; a.h_pad = h_pad; a.cw = cw; a.ch = ch; a.ssh = SSH; a.ssv = SSV;
     k_cfl_ac<BPC><<<1, 256, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
 
 template <int BPC>
-static void pal_pred_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
+static bool pal_pred_run(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
                        const typename Px<BPC>::pixel *pal, const uint8_t *idx, int w, int h) {
     using P = typename Px<BPC>::pixel;
     constexpr long B = sizeof(P);
@@ -397,25 +397,40 @@ static void pal_pred_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
     const int ip = st.in1(pal, 8 * B);
     const int ii = st.in1(idx, (long)w * h / 2);
     const int od = st.out(dst, stride, 0, w * B, 0, h);
-    st.upload();
+    if (!st.upload()) return false;
     k_pal<BPC><<<1, 256, 0, st.stream()>>>(st.origin<P>(od), st.pitch(od) / B,
                                            st.origin<const P>(ip), st.origin<const uint8_t>(ii), w, h);
-    st.finish();
+    return st.finish();
 }
+
+// The caller's entries before dav1d_intra_pred_dsp_init_gpu_* overwrote
+// them (run when the GPU path fails: runtime.hpp's error contract).
+static Dav1dIntraPredDSPContext_8bpc g_fb8;
+static Dav1dIntraPredDSPContext_16bpc g_fb16;
 
 #define IPRED_ENTRIES(BPC, P, BDP, BDV)                                                        \
 template <int MODE>                                                                            \
 static void ipred_##BPC(P *d, ptrdiff_t s, const P *tl, int w, int h, int a, int mw, int mh BDP)\
-{ run_ipred<BPC>(d, s, tl, w, h, MODE, a, mw, mh, nullptr, 0, 0, BDV); }                       \
+{ DGPU_OR_FALLBACK((run_ipred<BPC>(d, s, tl, w, h, MODE, a, mw, mh, nullptr, 0, 0, BDV)),      \
+                   g_fb##BPC.intra_pred[MODE], d, s, tl, w, h, a, mw, mh BDV##_ARG); }         \
 template <int MODE>                                                                            \
 static void cfl_##BPC(P *d, ptrdiff_t s, const P *tl, int w, int h, const int16_t *ac,         \
                       int alpha BDP)                                                           \
-{ run_ipred<BPC>(d, s, tl, w, h, MODE, 0, 0, 0, ac, alpha, 1, BDV); }
+{ DGPU_OR_FALLBACK((run_ipred<BPC>(d, s, tl, w, h, MODE, 0, 0, 0, ac, alpha, 1, BDV)),         \
+                   g_fb##BPC.cfl_pred[MODE], d, s, tl, w, h, ac, alpha BDV##_ARG); }           \
+template <int SSH, int SSV>                                                                    \
+static void cfl_ac_##BPC(int16_t *ac, const P *y, ptrdiff_t s, int wp, int hp, int cw, int ch) \
+{ DGPU_OR_FALLBACK((cfl_ac_run<BPC, SSH, SSV>(ac, y, s, wp, hp, cw, ch)),                      \
+                   g_fb##BPC.cfl_ac[SSH + SSV == 2 ? 0 : SSH ? 1 : 2], ac, y, s, wp, hp, cw, ch); } \
+static void pal_pred_##BPC(P *d, ptrdiff_t s, const P *pal, const uint8_t *idx, int w, int h)  \
+{ DGPU_OR_FALLBACK((pal_pred_run<BPC>(d, s, pal, idx, w, h)), g_fb##BPC.pal_pred, d, s, pal, idx, w, h); }
 
 #define BD8_PARAM
 #define BD8_VAL 255
+#define BD8_VAL_ARG
 #define BD16_PARAM , int bitdepth_max
 #define BD16_VAL bitdepth_max
+#define BD16_VAL_ARG , bitdepth_max
 IPRED_ENTRIES(8, uint8_t, BD8_PARAM, BD8_VAL)
 IPRED_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 
@@ -435,14 +450,14 @@ IPRED_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
         c->intra_pred[DGPU_SMOOTH_H_PRED] = ipred_##BPC<DGPU_SMOOTH_H_PRED>;                   \
         c->intra_pred[DGPU_PAETH_PRED] = ipred_##BPC<DGPU_PAETH_PRED>;                         \
         c->intra_pred[DGPU_FILTER_PRED] = ipred_##BPC<DGPU_FILTER_PRED>;                       \
-        c->cfl_ac[0] = cfl_ac_t<BPC, 1, 1>;                                                    \
-        c->cfl_ac[1] = cfl_ac_t<BPC, 1, 0>;                                                    \
-        c->cfl_ac[2] = cfl_ac_t<BPC, 0, 0>;                                                    \
+        c->cfl_ac[0] = cfl_ac_##BPC<1, 1>;                                                     \
+        c->cfl_ac[1] = cfl_ac_##BPC<1, 0>;                                                     \
+        c->cfl_ac[2] = cfl_ac_##BPC<0, 0>;                                                     \
         c->cfl_pred[DGPU_DC_PRED] = cfl_##BPC<DGPU_DC_PRED>;                                   \
         c->cfl_pred[DGPU_DC_128_PRED] = cfl_##BPC<DGPU_DC_128_PRED>;                           \
         c->cfl_pred[DGPU_TOP_DC_PRED] = cfl_##BPC<DGPU_TOP_DC_PRED>;                           \
         c->cfl_pred[DGPU_LEFT_DC_PRED] = cfl_##BPC<DGPU_LEFT_DC_PRED>;                         \
-        c->pal_pred = pal_pred_t<BPC>;                                                         \
+        c->pal_pred = pal_pred_##BPC;                                                          \
     } while (0)
 
 }  // namespace dgpu
@@ -450,7 +465,18 @@ IPRED_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 using namespace dgpu;
 
 // bitfn(dav1d_intra_pred_dsp_init) replacement, src/ipred_tmpl.c:740-774
-extern "C" void dav1d_intra_pred_dsp_init_gpu_8bpc(Dav1dIntraPredDSPContext_8bpc *c) { FILL_IPRED(8, c); }
-extern "C" void dav1d_intra_pred_dsp_init_gpu_16bpc(Dav1dIntraPredDSPContext_16bpc *c) { FILL_IPRED(16, c); }
+// The _gpu_ hooks keep the caller's previous entries as fallbacks.
+extern "C" void dav1d_intra_pred_dsp_init_gpu_8bpc(Dav1dIntraPredDSPContext_8bpc *c) {
+    Dav1dIntraPredDSPContext_8bpc g{}, *gp = &g;
+    FILL_IPRED(8, gp);
+    save_fallback(&g_fb8, c, gp);
+    FILL_IPRED(8, c);
+}
+extern "C" void dav1d_intra_pred_dsp_init_gpu_16bpc(Dav1dIntraPredDSPContext_16bpc *c) {
+    Dav1dIntraPredDSPContext_16bpc g{}, *gp = &g;
+    FILL_IPRED(16, gp);
+    save_fallback(&g_fb16, c, gp);
+    FILL_IPRED(16, c);
+}
 extern "C" void dav1d_intra_pred_dsp_init_8bpc(Dav1dIntraPredDSPContext_8bpc *c) { FILL_IPRED(8, c); }
 extern "C" void dav1d_intra_pred_dsp_init_16bpc(Dav1dIntraPredDSPContext_16bpc *c) { FILL_IPRED(16, c); }

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(64) void k_itx(typename Px<BPC>::pixel *dst, ptrdif
 }
 
 template <int BPC, int TX, int TP>
-static void itx_entry(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
+static bool itx_entry(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
                       typename Px<BPC>::coef *coef, int eob, int bdmax) {
     using P = typename Px<BPC>::pixel;
     using C = typename Px<BPC>::coef;
@@ -116,17 +116,24 @@ static void itx_entry(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
     Stager st;
     const int ic = st.inout1(coef, (long)SW * SH * sizeof(C));
     const int od = st.inout(dst, stride, 0, W * B, 0, H);
-    st.upload();
+    if (!st.upload()) return false;
     k_itx<BPC, TX><<<1, 64, 0, st.stream()>>>(st.origin<P>(od), st.pitch(od) / B, st.origin<C>(ic),
                                               eob, TP, bdmax);
-    st.finish();
+    return st.finish();
 }
 
+// The caller's entries before dav1d_itx_dsp_init_gpu_* overwrote them (run
+// when the GPU path fails: runtime.hpp's error contract).
+static Dav1dInvTxfmDSPContext_8bpc g_fb8;
+static Dav1dInvTxfmDSPContext_16bpc g_fb16;
+
 template <int TX, int TP>
-static void itx8(uint8_t *d, ptrdiff_t s, int16_t *c, int eob) { itx_entry<8, TX, TP>(d, s, c, eob, 255); }
+static void itx8(uint8_t *d, ptrdiff_t s, int16_t *c, int eob) {
+    DGPU_OR_FALLBACK((itx_entry<8, TX, TP>(d, s, c, eob, 255)), g_fb8.itxfm_add[TX][TP], d, s, c, eob);
+}
 template <int TX, int TP>
 static void itx16(uint16_t *d, ptrdiff_t s, int32_t *c, int eob, int bdmax) {
-    itx_entry<16, TX, TP>(d, s, c, eob, bdmax);
+    DGPU_OR_FALLBACK((itx_entry<16, TX, TP>(d, s, c, eob, bdmax)), g_fb16.itxfm_add[TX][TP], d, s, c, eob, bdmax);
 }
 
 template <typename Ctx, int TX, int TP>
@@ -153,20 +160,29 @@ using namespace dgpu;
 
 // bitfn(dav1d_itx_dsp_init) replacement, src/itx_tmpl.c:200-284.  Entries
 // the reference leaves unset stay NULL; `bpc` selects nothing here (one
-// kernel set covers 10 and 12 bit through bitdepth_max).
+// kernel set covers 10 and 12 bit through bitdepth_max).  The _gpu_ hooks
+// keep the caller's previous entries as fallbacks.
 extern "C" void dav1d_itx_dsp_init_gpu_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int bpc) {
     (void)bpc;
-    memset(c, 0, sizeof(*c));
+    Dav1dInvTxfmDSPContext_8bpc g{};
+    fill_all(&g, false, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
+    save_fallback(&g_fb8, c, &g);
     fill_all(c, false, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 extern "C" void dav1d_itx_dsp_init_gpu_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc) {
     (void)bpc;
-    memset(c, 0, sizeof(*c));
+    Dav1dInvTxfmDSPContext_16bpc g{};
+    fill_all(&g, true, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
+    save_fallback(&g_fb16, c, &g);
     fill_all(c, true, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 extern "C" void dav1d_itx_dsp_init_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int bpc) {
-    dav1d_itx_dsp_init_gpu_8bpc(c, bpc);
+    (void)bpc;
+    memset(c, 0, sizeof(*c));
+    fill_all(c, false, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 extern "C" void dav1d_itx_dsp_init_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc) {
-    dav1d_itx_dsp_init_gpu_16bpc(c, bpc);
+    (void)bpc;
+    memset(c, 0, sizeof(*c));
+    fill_all(c, true, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }

@@ -264,7 +264,7 @@ __global__ __launch_bounds__(128) void k_lpf_sb(LpfSegs segs) {
 
 // loop_filter_{h,v}_sb128{y,uv}_c (src/loopfilter_tmpl.c:163-245)
 template <int BPC, int VERT, int UV>
-static void lpf_sb_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride, const uint32_t *vmask, const uint8_t (*l)[4],
+static bool lpf_sb_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride, const uint32_t *vmask, const uint8_t (*l)[4],
                      ptrdiff_t b4_stride, const Dav1dGpuFilterLUT *lut, int bdmax) {
     using P = typename Px<BPC>::pixel;
     constexpr long B = sizeof(P);
@@ -287,8 +287,8 @@ static void lpf_sb_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride, const uint3
                               : st.inout(dst, stride, -r * B, r * B, 4L * k, 4L * k + 4);
         pend[n++] = { rect, k, lut->e[L], lut->i[L], L >> 4, wd };
     }
-    if (!n) return;
-    st.upload();
+    if (!n) return true;
+    if (!st.upload()) return false;
     LpfSegs s;
     memset(&s, 0, sizeof(s));
     for (int i = 0; i < n; i++) {
@@ -302,19 +302,27 @@ static void lpf_sb_t(typename Px<BPC>::pixel *dst, ptrdiff_t stride, const uint3
     s.vert = VERT;
     s.bdmax = bdmax;
     k_lpf_sb<BPC><<<1, 128, 0, st.stream()>>>(s);
-    st.finish();
+    return st.finish();
 }
+
+// The caller's entries before dav1d_loop_filter_dsp_init_gpu_* overwrote
+// them (run when the GPU path fails: runtime.hpp's error contract).
+static Dav1dLoopFilterDSPContext_8bpc g_fb8;
+static Dav1dLoopFilterDSPContext_16bpc g_fb16;
 
 #define LPF_ENTRIES(BPC, P, BDP, BDV)                                                                     \
 template <int VERT, int UV>                                                                               \
 static void lpf_##BPC(P *d, ptrdiff_t s, const uint32_t *m, const uint8_t (*l)[4], ptrdiff_t b4s,          \
                       const Dav1dGpuFilterLUT *lut, int w BDP)                                            \
-{ (void)w; lpf_sb_t<BPC, VERT, UV>(d, s, m, l, b4s, lut, BDV); }
+{ DGPU_OR_FALLBACK((lpf_sb_t<BPC, VERT, UV>(d, s, m, l, b4s, lut, BDV)),                                 \
+                   g_fb##BPC.loop_filter_sb[UV][VERT], d, s, m, l, b4s, lut, w BDV##_ARG); }
 
 #define BD8_PARAM
 #define BD8_VAL 255
+#define BD8_VAL_ARG
 #define BD16_PARAM , int bitdepth_max
 #define BD16_VAL bitdepth_max
+#define BD16_VAL_ARG , bitdepth_max
 LPF_ENTRIES(8, uint8_t, BD8_PARAM, BD8_VAL)
 LPF_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 
@@ -331,8 +339,19 @@ LPF_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 using namespace dgpu;
 
 // bitfn(dav1d_loop_filter_dsp_init) replacement, src/loopfilter_tmpl.c:257-272
-extern "C" void dav1d_loop_filter_dsp_init_gpu_8bpc(Dav1dLoopFilterDSPContext_8bpc *c) { FILL_LPF(8, c); }
-extern "C" void dav1d_loop_filter_dsp_init_gpu_16bpc(Dav1dLoopFilterDSPContext_16bpc *c) { FILL_LPF(16, c); }
+// The _gpu_ hooks keep the caller's previous entries as fallbacks.
+extern "C" void dav1d_loop_filter_dsp_init_gpu_8bpc(Dav1dLoopFilterDSPContext_8bpc *c) {
+    Dav1dLoopFilterDSPContext_8bpc g{}, *gp = &g;
+    FILL_LPF(8, gp);
+    save_fallback(&g_fb8, c, gp);
+    FILL_LPF(8, c);
+}
+extern "C" void dav1d_loop_filter_dsp_init_gpu_16bpc(Dav1dLoopFilterDSPContext_16bpc *c) {
+    Dav1dLoopFilterDSPContext_16bpc g{}, *gp = &g;
+    FILL_LPF(16, gp);
+    save_fallback(&g_fb16, c, gp);
+    FILL_LPF(16, c);
+}
 extern "C" void dav1d_loop_filter_dsp_init_8bpc(Dav1dLoopFilterDSPContext_8bpc *c) { FILL_LPF(8, c); }
 extern "C" void dav1d_loop_filter_dsp_init_16bpc(Dav1dLoopFilterDSPContext_16bpc *c) { FILL_LPF(16, c); }
 

@@ -326,12 +326,12 @@ static int launch_lr_frame(const Dav1dGpuLrFrame *F, hipStream_t stream) {
 }
 
 template <int BPC>
-static void lr_t(typename Px<BPC>::pixel *p, ptrdiff_t stride, const typename Px<BPC>::pixel (*left)[4],
+static bool lr_t(typename Px<BPC>::pixel *p, ptrdiff_t stride, const typename Px<BPC>::pixel (*left)[4],
                  const typename Px<BPC>::pixel *lpf, int w, int h, const Dav1dGpuLrParams *params, int edges,
                  int kind, int bdmax) {
     using P = typename Px<BPC>::pixel;
     constexpr long B = sizeof(P);
-    if (w <= 0 || h <= 0) return;
+    if (w <= 0 || h <= 0) return true;
     const long hl = (edges & DGPU_LR_HAVE_LEFT) ? 3 : 0, hr = (edges & DGPU_LR_HAVE_RIGHT) ? 3 : 0;
     Stager st;
     const int ip = st.in(p, stride, -hl * B, (w + hr) * B, 0, h);
@@ -339,7 +339,7 @@ static void lr_t(typename Px<BPC>::pixel *p, ptrdiff_t stride, const typename Px
     const int il = hl ? st.in1(left, (long)h * 4 * B) : -1;
     const int it = (edges & DGPU_LR_HAVE_TOP) ? st.in(lpf, stride, -hl * B, (w + hr) * B, 0, 2) : -1;
     const int ib = (edges & DGPU_LR_HAVE_BOTTOM) ? st.in(lpf, stride, -hl * B, (w + hr) * B, 6, 8) : -1;
-    st.upload();
+    if (!st.upload()) return false;
     LrArgs<BPC> a;
     memset(&a, 0, sizeof(a));
     a.src = st.origin<const P>(ip);
@@ -358,19 +358,30 @@ static void lr_t(typename Px<BPC>::pixel *p, ptrdiff_t stride, const typename Px
     a.bdmax = bdmax;
     a.prm = *params;
     k_lr<BPC><<<(w + kLrSW - 1) / kLrSW, 256, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
+
+// The caller's entries before dav1d_loop_restoration_dsp_init_gpu_*
+// overwrote them (run when the GPU path fails: runtime.hpp's error
+// contract).  KIND 0 serves both Wiener slots: the 7-tap entry wiener[0]
+// handles any Wiener filter, so it is the fallback for both.
+static Dav1dLoopRestorationDSPContext_8bpc g_fb8;
+static Dav1dLoopRestorationDSPContext_16bpc g_fb16;
 
 #define LR_ENTRIES(BPC, P, BDP, BDV)                                                                      \
 template <int KIND>                                                                                       \
 static void lr_##BPC(P *d, ptrdiff_t s, const P (*l)[4], const P *lpf, int w, int h,                      \
                      const Dav1dGpuLrParams *prm, int edges BDP)                                          \
-{ lr_t<BPC>(d, s, l, lpf, w, h, prm, edges, KIND, BDV); }
+{ DGPU_OR_FALLBACK((lr_t<BPC>(d, s, l, lpf, w, h, prm, edges, KIND, BDV)),                               \
+                   KIND == 0 ? g_fb##BPC.wiener[0] : g_fb##BPC.sgr[KIND ? KIND - 1 : 0], d, s, l, lpf,    \
+                   w, h, prm, edges BDV##_ARG); }
 
 #define BD8_PARAM
 #define BD8_VAL 255
+#define BD8_VAL_ARG
 #define BD16_PARAM , int bitdepth_max
 #define BD16_VAL bitdepth_max
+#define BD16_VAL_ARG , bitdepth_max
 LR_ENTRIES(8, uint8_t, BD8_PARAM, BD8_VAL)
 LR_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 
@@ -387,12 +398,19 @@ LR_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 using namespace dgpu;
 
 // bitfn(dav1d_loop_restoration_dsp_init) replacement, src/looprestoration_tmpl.c:539-558
+// The _gpu_ hooks keep the caller's previous entries as fallbacks.
 extern "C" void dav1d_loop_restoration_dsp_init_gpu_8bpc(Dav1dLoopRestorationDSPContext_8bpc *c, int bpc) {
     (void)bpc;
+    Dav1dLoopRestorationDSPContext_8bpc g{}, *gp = &g;
+    FILL_LR(8, gp);
+    save_fallback(&g_fb8, c, gp);
     FILL_LR(8, c);
 }
 extern "C" void dav1d_loop_restoration_dsp_init_gpu_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc) {
     (void)bpc;
+    Dav1dLoopRestorationDSPContext_16bpc g{}, *gp = &g;
+    FILL_LR(16, gp);
+    save_fallback(&g_fb16, c, gp);
     FILL_LR(16, c);
 }
 extern "C" int dav1d_gpu_lr_frame_8bpc(const Dav1dGpuLrFrame *f, void *stream) {

@@ -309,7 +309,7 @@ template <> struct HostPx<8> { static constexpr int bdmax(int) { return 255; } }
 template <> struct HostPx<16> { static int bdmax(int v) { return v; } };
 
 template <int BPC, int F, bool SCALED>
-static void run_mc(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
+static bool run_mc(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
                    const typename Px<BPC>::pixel *src, ptrdiff_t src_stride, int w, int h,
                    int mx, int my, int dx, int dy, int bdmax) {
     using P = typename Px<BPC>::pixel;
@@ -342,7 +342,7 @@ static void run_mc(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, int16_t *
     Stager st;
     const int is = st.in(src, src_stride, c0 * B, c1 * B, r0, r1);
     const int od = dst ? st.out(dst, dst_stride, 0, w * B, 0, h) : st.out1(tmp, (long)w * h * 2);
-    st.upload();
+    if (!st.upload()) return false;
     McArgs<BPC> a;
     a.dst = dst ? st.origin<P>(od) : nullptr;
     a.ds = dst ? st.pitch(od) / B : 0;
@@ -354,34 +354,45 @@ static void run_mc(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, int16_t *
     a.scaled = SCALED;
     a.bdmax = bdmax;
     k_mc<BPC><<<grid16(w, h), 256, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
+
+// The caller's entries before dav1d_mc_dsp_init_gpu_* overwrote them (C
+// defaults, run when the GPU path fails: runtime.hpp's error contract).
+static Dav1dMCDSPContext_8bpc g_fb8;
+static Dav1dMCDSPContext_16bpc g_fb16;
 
 // --- 8bpc / 16bpc signature adapters --------------------------------------
 #define BD8_PARAM
 #define BD8_VAL 255
+#define BD8_VAL_ARG
 #define BD16_PARAM , int bitdepth_max
 #define BD16_VAL bitdepth_max
+#define BD16_VAL_ARG , bitdepth_max
 
 #define MC_ENTRIES(BPC, P, BDP, BDV)                                                           \
 template <int F> static void put_##BPC(P *d, ptrdiff_t ds, const P *s, ptrdiff_t ss, int w,    \
                                        int h, int mx, int my BDP)                              \
-{ run_mc<BPC, F, false>(d, ds, nullptr, s, ss, w, h, mx, my, 0, 0, BDV); }                     \
+{ DGPU_OR_FALLBACK((run_mc<BPC, F, false>(d, ds, nullptr, s, ss, w, h, mx, my, 0, 0, BDV)),    \
+                   g_fb##BPC.mc[F], d, ds, s, ss, w, h, mx, my BDV##_ARG); }                   \
 template <int F> static void prep_##BPC(int16_t *t, const P *s, ptrdiff_t ss, int w, int h,    \
                                         int mx, int my BDP)                                    \
-{ run_mc<BPC, F, false>(nullptr, 0, t, s, ss, w, h, mx, my, 0, 0, BDV); }                      \
+{ DGPU_OR_FALLBACK((run_mc<BPC, F, false>(nullptr, 0, t, s, ss, w, h, mx, my, 0, 0, BDV)),     \
+                   g_fb##BPC.mct[F], t, s, ss, w, h, mx, my BDV##_ARG); }                      \
 template <int F> static void put_scaled_##BPC(P *d, ptrdiff_t ds, const P *s, ptrdiff_t ss,    \
                                               int w, int h, int mx, int my, int dx, int dy BDP)\
-{ run_mc<BPC, F, true>(d, ds, nullptr, s, ss, w, h, mx, my, dx, dy, BDV); }                    \
+{ DGPU_OR_FALLBACK((run_mc<BPC, F, true>(d, ds, nullptr, s, ss, w, h, mx, my, dx, dy, BDV)),   \
+                   g_fb##BPC.mc_scaled[F], d, ds, s, ss, w, h, mx, my, dx, dy BDV##_ARG); }    \
 template <int F> static void prep_scaled_##BPC(int16_t *t, const P *s, ptrdiff_t ss, int w,    \
                                                int h, int mx, int my, int dx, int dy BDP)      \
-{ run_mc<BPC, F, true>(nullptr, 0, t, s, ss, w, h, mx, my, dx, dy, BDV); }
+{ DGPU_OR_FALLBACK((run_mc<BPC, F, true>(nullptr, 0, t, s, ss, w, h, mx, my, dx, dy, BDV)),    \
+                   g_fb##BPC.mct_scaled[F], t, s, ss, w, h, mx, my, dx, dy BDV##_ARG); }
 
 MC_ENTRIES(8, uint8_t, BD8_PARAM, BD8_VAL)
 MC_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 
 template <int BPC>
-static void run_avg(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, const int16_t *t1,
+static bool run_avg(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, const int16_t *t1,
                     const int16_t *t2, int w, int h, int kind, int weight, const uint8_t *mask_in,
                     uint8_t *mask_out, int sign, int ssh, int ssv, int bdmax) {
     using P = typename Px<BPC>::pixel;
@@ -392,7 +403,7 @@ static void run_avg(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, const in
     const int im = kind == 2 ? st.in1(mask_in, n) : -1;
     const int om = kind == 3 ? st.out1(mask_out, (long)(w >> ssh) * (h >> ssv)) : -1;
     const int od = st.out(dst, dst_stride, 0, w * B, 0, h);
-    st.upload();
+    if (!st.upload()) return false;
     AvgArgs<BPC> a;
     a.dst = st.origin<P>(od);
     a.ds = st.pitch(od) / B;
@@ -403,28 +414,32 @@ static void run_avg(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, const in
     a.w = w; a.h = h; a.kind = kind; a.weight = weight; a.sign = sign; a.ssh = ssh; a.ssv = ssv;
     a.bdmax = bdmax;
     k_avg<BPC><<<grid16(w, h), 256, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
 
 #define AVG_ENTRIES(BPC, P, BDP, BDV)                                                          \
 static void avg_##BPC(P *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h BDP)\
-{ run_avg<BPC>(d, ds, a, b, w, h, 0, 0, nullptr, nullptr, 0, 0, 0, BDV); }                     \
+{ DGPU_OR_FALLBACK((run_avg<BPC>(d, ds, a, b, w, h, 0, 0, nullptr, nullptr, 0, 0, 0, BDV)),    \
+                   g_fb##BPC.avg, d, ds, a, b, w, h BDV##_ARG); }                              \
 static void w_avg_##BPC(P *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h,  \
                         int wt BDP)                                                            \
-{ run_avg<BPC>(d, ds, a, b, w, h, 1, wt, nullptr, nullptr, 0, 0, 0, BDV); }                    \
+{ DGPU_OR_FALLBACK((run_avg<BPC>(d, ds, a, b, w, h, 1, wt, nullptr, nullptr, 0, 0, 0, BDV)),   \
+                   g_fb##BPC.w_avg, d, ds, a, b, w, h, wt BDV##_ARG); }                        \
 static void mask_##BPC(P *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h,   \
                        const uint8_t *m BDP)                                                   \
-{ run_avg<BPC>(d, ds, a, b, w, h, 2, 0, m, nullptr, 0, 0, 0, BDV); }                           \
+{ DGPU_OR_FALLBACK((run_avg<BPC>(d, ds, a, b, w, h, 2, 0, m, nullptr, 0, 0, 0, BDV)),          \
+                   g_fb##BPC.mask, d, ds, a, b, w, h, m BDV##_ARG); }                          \
 template <int SSH, int SSV>                                                                    \
 static void w_mask_##BPC(P *d, ptrdiff_t ds, const int16_t *a, const int16_t *b, int w, int h, \
                          uint8_t *m, int sign BDP)                                             \
-{ run_avg<BPC>(d, ds, a, b, w, h, 3, 0, nullptr, m, sign, SSH, SSV, BDV); }
+{ DGPU_OR_FALLBACK((run_avg<BPC>(d, ds, a, b, w, h, 3, 0, nullptr, m, sign, SSH, SSV, BDV)),   \
+                   g_fb##BPC.w_mask[SSH + SSV], d, ds, a, b, w, h, m, sign BDV##_ARG); }
 
 AVG_ENTRIES(8, uint8_t, BD8_PARAM, BD8_VAL)
 AVG_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 
 template <int BPC>
-static void run_blend(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
+static bool run_blend(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
                       const typename Px<BPC>::pixel *tmp, int w, int h, const uint8_t *mask,
                       int kind) {
     using P = typename Px<BPC>::pixel;
@@ -435,7 +450,7 @@ static void run_blend(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
     const long cw = kind == 1 ? (w * 3) >> 2 : w;
     const long ch = kind == 2 ? (h * 3) >> 2 : h;
     const int od = st.inout(dst, dst_stride, 0, cw * B, 0, ch);
-    st.upload();
+    if (!st.upload()) return false;
     BlendArgs<BPC> a;
     a.dst = st.origin<P>(od);
     a.ds = st.pitch(od) / B;
@@ -443,11 +458,11 @@ static void run_blend(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
     a.mask = im >= 0 ? st.origin<const uint8_t>(im) : nullptr;
     a.w = w; a.h = h; a.kind = kind;
     k_blend<BPC><<<grid16(w, h), 256, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
 
 template <int BPC>
-static void run_warp(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
+static bool run_warp(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
                      ptrdiff_t tmp_stride, const typename Px<BPC>::pixel *src,
                      ptrdiff_t src_stride, const int16_t *abcd, int mx, int my, int bdmax) {
     using P = typename Px<BPC>::pixel;
@@ -456,7 +471,7 @@ static void run_warp(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, int16_t
     const int is = st.in(src, src_stride, -3 * B, 12 * B, -3, 12);
     const int od = dst ? st.out(dst, dst_stride, 0, 8 * B, 0, 8)
                        : st.out(tmp, tmp_stride * 2, 0, 16, 0, 8);
-    st.upload();
+    if (!st.upload()) return false;
     WarpArgs<BPC> a;
     a.dst = dst ? st.origin<P>(od) : nullptr;
     a.ds = dst ? st.pitch(od) / B : 0;
@@ -467,11 +482,11 @@ static void run_warp(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride, int16_t
     a.a0 = abcd[0]; a.a1 = abcd[1]; a.a2 = abcd[2]; a.a3 = abcd[3];
     a.mx = mx; a.my = my; a.bdmax = bdmax;
     k_warp<BPC><<<1, 64, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
 
 template <int BPC>
-static void emu_edge_t(intptr_t bw, intptr_t bh, intptr_t iw, intptr_t ih, intptr_t x, intptr_t y,
+static bool emu_edge_t(intptr_t bw, intptr_t bh, intptr_t iw, intptr_t ih, intptr_t x, intptr_t y,
                        typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
                        const typename Px<BPC>::pixel *ref, ptrdiff_t ref_stride) {
     using P = typename Px<BPC>::pixel;
@@ -482,7 +497,7 @@ static void emu_edge_t(intptr_t bw, intptr_t bh, intptr_t iw, intptr_t ih, intpt
     Stager st;
     const int ir = st.in(ref, ref_stride, sx0 * B, (sx1 + 1) * B, sy0, sy1 + 1);
     const int od = st.out(dst, dst_stride, 0, bw * B, 0, bh);
-    st.upload();
+    if (!st.upload()) return false;
     EmuArgs<BPC> a;
     a.dst = st.origin<P>(od);
     a.ds = st.pitch(od) / B;
@@ -490,11 +505,11 @@ static void emu_edge_t(intptr_t bw, intptr_t bh, intptr_t iw, intptr_t ih, intpt
     a.rs = st.pitch(ir) / B;
     a.bw = (int)bw; a.bh = (int)bh; a.iw = (int)iw; a.ih = (int)ih; a.x = (int)x; a.y = (int)y;
     k_emu_edge<BPC><<<grid16((int)bw, (int)bh), 256, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
 
 template <int BPC>
-static void run_resize(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
+static bool run_resize(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
                        const typename Px<BPC>::pixel *src, ptrdiff_t src_stride, int dst_w, int h,
                        int src_w, int dx, int mx0, int bdmax) {
     using P = typename Px<BPC>::pixel;
@@ -502,7 +517,7 @@ static void run_resize(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
     Stager st;
     const int is = st.in(src, src_stride, 0, src_w * B, 0, h);
     const int od = st.out(dst, dst_stride, 0, dst_w * B, 0, h);
-    st.upload();
+    if (!st.upload()) return false;
     ResizeArgs<BPC> a;
     a.dst = st.origin<P>(od);
     a.ds = st.pitch(od) / B;
@@ -510,25 +525,32 @@ static void run_resize(typename Px<BPC>::pixel *dst, ptrdiff_t dst_stride,
     a.ss = st.pitch(is) / B;
     a.dst_w = dst_w; a.h = h; a.src_w = src_w; a.dx = dx; a.mx0 = mx0; a.bdmax = bdmax;
     k_resize<BPC><<<dim3((dst_w + 63) / 64, (h + 3) / 4), 256, 0, st.stream()>>>(a);
-    st.finish();
+    return st.finish();
 }
 
 #define MISC_ENTRIES(BPC, P, BDP, BDV)                                                         \
 static void blend_##BPC(P *d, ptrdiff_t ds, const P *t, int w, int h, const uint8_t *m)        \
-{ run_blend<BPC>(d, ds, t, w, h, m, 0); }                                                      \
+{ DGPU_OR_FALLBACK((run_blend<BPC>(d, ds, t, w, h, m, 0)), g_fb##BPC.blend, d, ds, t, w, h, m); }\
 static void blend_v_##BPC(P *d, ptrdiff_t ds, const P *t, int w, int h)                        \
-{ run_blend<BPC>(d, ds, t, w, h, nullptr, 1); }                                                \
+{ DGPU_OR_FALLBACK((run_blend<BPC>(d, ds, t, w, h, nullptr, 1)), g_fb##BPC.blend_v, d, ds, t, w, h); }\
 static void blend_h_##BPC(P *d, ptrdiff_t ds, const P *t, int w, int h)                        \
-{ run_blend<BPC>(d, ds, t, w, h, nullptr, 2); }                                                \
+{ DGPU_OR_FALLBACK((run_blend<BPC>(d, ds, t, w, h, nullptr, 2)), g_fb##BPC.blend_h, d, ds, t, w, h); }\
 static void warp_##BPC(P *d, ptrdiff_t ds, const P *s, ptrdiff_t ss, const int16_t *abcd,      \
                        int mx, int my BDP)                                                     \
-{ run_warp<BPC>(d, ds, nullptr, 0, s, ss, abcd, mx, my, BDV); }                                \
+{ DGPU_OR_FALLBACK((run_warp<BPC>(d, ds, nullptr, 0, s, ss, abcd, mx, my, BDV)),               \
+                   g_fb##BPC.warp8x8, d, ds, s, ss, abcd, mx, my BDV##_ARG); }                 \
 static void warpt_##BPC(int16_t *t, ptrdiff_t ts, const P *s, ptrdiff_t ss,                    \
                         const int16_t *abcd, int mx, int my BDP)                               \
-{ run_warp<BPC>(nullptr, 0, t, ts, s, ss, abcd, mx, my, BDV); }                                \
+{ DGPU_OR_FALLBACK((run_warp<BPC>(nullptr, 0, t, ts, s, ss, abcd, mx, my, BDV)),               \
+                   g_fb##BPC.warp8x8t, t, ts, s, ss, abcd, mx, my BDV##_ARG); }                \
+static void emu_edge_##BPC(intptr_t bw, intptr_t bh, intptr_t iw, intptr_t ih, intptr_t x,     \
+                           intptr_t y, P *d, ptrdiff_t ds, const P *r, ptrdiff_t rs)           \
+{ DGPU_OR_FALLBACK((emu_edge_t<BPC>(bw, bh, iw, ih, x, y, d, ds, r, rs)),                      \
+                   g_fb##BPC.emu_edge, bw, bh, iw, ih, x, y, d, ds, r, rs); }                  \
 static void resize_##BPC(P *d, ptrdiff_t ds, const P *s, ptrdiff_t ss, int dw, int h, int sw,  \
                          int dx, int mx BDP)                                                   \
-{ run_resize<BPC>(d, ds, s, ss, dw, h, sw, dx, mx, BDV); }
+{ DGPU_OR_FALLBACK((run_resize<BPC>(d, ds, s, ss, dw, h, sw, dx, mx, BDV)),                    \
+                   g_fb##BPC.resize, d, ds, s, ss, dw, h, sw, dx, mx BDV##_ARG); }
 
 MISC_ENTRIES(8, uint8_t, BD8_PARAM, BD8_VAL)
 MISC_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
@@ -558,7 +580,7 @@ MISC_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
         c->w_mask[2] = w_mask_##BPC<1, 1>;                                                     \
         c->blend = blend_##BPC; c->blend_v = blend_v_##BPC; c->blend_h = blend_h_##BPC;        \
         c->warp8x8 = warp_##BPC; c->warp8x8t = warpt_##BPC;                                    \
-        c->emu_edge = emu_edge_t<BPC>; c->resize = resize_##BPC;                               \
+        c->emu_edge = emu_edge_##BPC; c->resize = resize_##BPC;                               \
     } while (0)
 
 }  // namespace dgpu
@@ -566,7 +588,18 @@ MISC_ENTRIES(16, uint16_t, BD16_PARAM, BD16_VAL)
 using namespace dgpu;
 
 // bitfn(dav1d_mc_dsp_init) replacement, src/mc_tmpl.c:915-957
-extern "C" void dav1d_mc_dsp_init_gpu_8bpc(Dav1dMCDSPContext_8bpc *c) { FILL_MC(8, c); }
-extern "C" void dav1d_mc_dsp_init_gpu_16bpc(Dav1dMCDSPContext_16bpc *c) { FILL_MC(16, c); }
+// The _gpu_ hooks keep the caller's previous entries as fallbacks.
+extern "C" void dav1d_mc_dsp_init_gpu_8bpc(Dav1dMCDSPContext_8bpc *c) {
+    Dav1dMCDSPContext_8bpc g{}, *gp = &g;
+    FILL_MC(8, gp);
+    save_fallback(&g_fb8, c, gp);
+    FILL_MC(8, c);
+}
+extern "C" void dav1d_mc_dsp_init_gpu_16bpc(Dav1dMCDSPContext_16bpc *c) {
+    Dav1dMCDSPContext_16bpc g{}, *gp = &g;
+    FILL_MC(16, gp);
+    save_fallback(&g_fb16, c, gp);
+    FILL_MC(16, c);
+}
 extern "C" void dav1d_mc_dsp_init_8bpc(Dav1dMCDSPContext_8bpc *c) { FILL_MC(8, c); }
 extern "C" void dav1d_mc_dsp_init_16bpc(Dav1dMCDSPContext_16bpc *c) { FILL_MC(16, c); }

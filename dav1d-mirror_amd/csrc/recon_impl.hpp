@@ -142,7 +142,12 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     if (count <= 0) return;
     // this lane's unit descriptor (lanes past the last unit re-read it)
     const int ui_ = first + min((int)(threadIdx.x & 63) >> lg, count - 1);
-    const Dav1dGpuUnit u = units[ui_];
+    Dav1dGpuUnit u;
+    {
+        const u32x4 d0 = gld_meta<u32x4>(units + ui_), d1 = gld_meta<u32x4>(reinterpret_cast<const uint8_t *>(units + ui_) + 16);
+        __builtin_memcpy(&u, &d0, 16);
+        __builtin_memcpy(reinterpret_cast<uint8_t *>(&u) + 16, &d1, 16);
+    }
     Dav1dGpuIntraEdge rec{};
     if constexpr (gathers(GRP)) rec = a.recs[ui_];   // its edge record, in the same round trip
     // per-wave copy of the plane table: lane-indexed vector loads of the

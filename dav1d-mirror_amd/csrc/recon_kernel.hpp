@@ -351,6 +351,16 @@ __device__ __forceinline__ void vdot4x4(const uint32_t (*a)[4], const uint4 &tv,
 template <typename T> __device__ __forceinline__ T gld(const void *p) {
     return *(const __attribute__((address_space(1))) T *)p;
 }
+// Loads of data each unit reads once (descriptors, coefficients, edges):
+// DGPU_NT_META=1 marks them non-temporal so they do not displace the
+// picture lines still being written in L2 (experiment knob)
+#ifndef DGPU_NT_META
+#define DGPU_NT_META 0
+#endif
+template <typename T> __device__ __forceinline__ T gld_meta(const void *p) {
+    if constexpr (DGPU_NT_META) return __builtin_nontemporal_load((const __attribute__((address_space(1))) T *)p);
+    else return gld<T>(p);
+}
 template <typename T> __device__ __forceinline__ void gst(void *p, T v) {
     *(__attribute__((address_space(1))) T *)p = v;
 }
@@ -376,7 +386,7 @@ template <int MAXN, int G> struct Stage {
         const uint8_t *s = reinterpret_cast<const uint8_t *>(src) - sk;
         nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
 #pragma unroll
-        for (int k = 0; k < IT; k++) v[k] = gld<u32x4>(s + 16 * min(l + k * G, nch - 1));   // clamped
+        for (int k = 0; k < IT; k++) v[k] = gld_meta<u32x4>(s + 16 * min(l + k * G, nch - 1));   // clamped
     }
     __device__ __forceinline__ int commit(uint8_t *dst, int l) const {
 #pragma unroll

@@ -147,6 +147,7 @@ struct Dav1dGpuRecorder {
     PinnedBuf pin;   // units | recs | coefficients, copied in one sequential pass
     DevBuf d_units, d_recs, d_coef, d_edges, d_work;
     hipEvent_t done = nullptr;
+    bool pending_check = false;   // the last flush's error word not read yet
     int32_t last_units = 0, last_levels = 0;
 };
 
@@ -236,6 +237,26 @@ extern "C" int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int
     return 0;
 }
 
+// The last flush's outcome, once it has finished: its persistent
+// wavefront's error word (workspace int32 [1], set by a wave that gave up
+// waiting for its producers) is read back and cleared.  -6: the picture of
+// that flush is incomplete; -3: HIP error.
+static int recorder_poll(Dav1dGpuRecorder *r) {
+    if (!r->pending_check) return 0;
+    r->pending_check = false;
+    int32_t flag = 0;
+    if (hipEventSynchronize(r->done) != hipSuccess ||
+        hipMemcpy(&flag, (const int32_t *)r->d_work.p + 1, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return -3;
+    return flag ? -6 : 0;
+}
+
+extern "C" int dav1d_gpu_recorder_status(Dav1dGpuRecorder *r) {
+    if (!r) return -1;
+    if (hipSetDevice(r->device) != hipSuccess) return -3;
+    return recorder_poll(r);
+}
+
 extern "C" int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_units, int32_t *n_levels) {
     if (!r) return -1;
     if (n_units) *n_units = r->last_units;
@@ -249,6 +270,13 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     if (!r || !dst) return -1;
     if (hipSetDevice(r->device) != hipSuccess) return -3;
     if (r->done && hipEventSynchronize(r->done) != hipSuccess) return -3;   // buffers free for reuse
+    // a previous flush whose wavefront gave up waiting is reported once,
+    // here if dav1d_gpu_recorder_status did not report it: nothing is
+    // launched and the recording is kept for a retry
+    {
+        const int st = recorder_poll(r);
+        if (st) return st;
+    }
     // DAV1D_GPU_REC_TIMING=1: host phase times on stderr (diagnostics)
     static const bool timing = getenv("DAV1D_GPU_REC_TIMING") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -329,6 +357,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     u.bh4 = (uint8_t)bh4;
                     for (int k = 0; k < 2; k++) {
                         const int rr = b.ref[k];
+                        // every reference an inter block reads must be given
+                        if (k == 0 || b.kind != DGPU_PRED_INTER)
+                            if (!ref || !ref[rr][p].data) return -1;
                         const int rs = ref ? (int)(ref[rr][p].stride / bpp) : 0;
                         u.p.inter.src_off[k] = (uy + (b.mvy[k] >> 4)) * rs + ux + (b.mvx[k] >> 4);
                         u.p.inter.mx[k] = (uint8_t)(b.mvx[k] & 15);
@@ -366,10 +397,13 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 const int W4 = e.w4, H4 = e.h4;
                 const size_t p0 = prod.size();
                 int d = -1;
+                // a pixel no cell of this flush wrote came from an earlier
+                // flush on the same stream: no producer, level 0 for it
                 auto cell = [&](int cx, int cy) {
                     const size_t at = (size_t)cy * w4p + cx;
                     d = std::max(d, lv[p][at]);
-                    if (prod.size() == p0 || prod.back() != own[p][at]) prod.push_back(own[p][at]);
+                    const int32_t o = own[p][at];
+                    if (o >= 0 && (prod.size() == p0 || prod.back() != o)) prod.push_back(o);
                 };
                 if (nd & 1) {
                     if (hl) {
@@ -399,9 +433,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     for (int cy = 2 * y4; cy < 2 * (y4 + th4); cy++)
                         for (int cx = 2 * x4; cx < 2 * (x4 + tw4); cx++) {
                             const size_t at = (size_t)cy * lw4 + cx;
-                            if (lv[0][at] < 0) return -1;   // CfL before its luma
-                            d = std::max(d, lv[0][at]);
-                            if (prod.size() == p0 || prod.back() != own[0][at]) prod.push_back(own[0][at]);
+                            d = std::max(d, lv[0][at]);   // (luma of an earlier flush: no producer)
+                            const int32_t o = own[0][at];
+                            if (o >= 0 && (prod.size() == p0 || prod.back() != o)) prod.push_back(o);
                         }
                 }
                 std::sort(prod.begin() + p0, prod.end());   // duplicate-free
@@ -570,6 +604,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     if (rc) return rc;
     if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return -3;
     if (hipEventRecord(r->done, st) != hipSuccess) return -3;
+    r->pending_check = true;
     r->blocks.clear();
     r->residuals.clear();
     r->coef32.clear();

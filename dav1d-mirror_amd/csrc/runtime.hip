@@ -5,28 +5,66 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "dav1d_gpu.h"
 
 namespace dgpu {
 
-[[noreturn]] void fatal(const char *what, hipError_t e) {
-    fprintf(stderr, "dav1d-gpu: fatal HIP error in %s: %s (%d)\n", what,
-            hipGetErrorString(e), (int)e);
-    abort();
+// ---- sticky error ------------------------------------------
+static std::atomic<int> g_error{0};        // first latched error, 0 = none
+static std::atomic<long> g_fail_after{-2}; // DAV1D_GPU_FAIL_AFTER: -2 unread, -1 off
+
+// Test hook: DAV1D_GPU_FAIL_AFTER=n makes the (n+1)-th HIP call of the
+// per-call tier fail as if the runtime had returned an error.
+static bool injected_failure() {
+    long n = g_fail_after.load(std::memory_order_relaxed);
+    if (n == -2) {
+        const char *e = getenv("DAV1D_GPU_FAIL_AFTER");
+        n = e ? strtol(e, nullptr, 0) : -1;
+        g_fail_after.store(n);
+    }
+    if (n < 0) return false;
+    return g_fail_after.fetch_sub(1) == 0;
+}
+
+void latch_error(int code, const char *what) {
+    int expect = 0;
+    if (g_error.compare_exchange_strong(expect, code))
+        fprintf(stderr, "dav1d-gpu: %s failed (error %d); GPU DSP entries disabled until "
+                        "dav1d_gpu_clear_error()\n", what, code);
+}
+
+bool gpu_usable() { return g_error.load(std::memory_order_relaxed) == 0; }
+
+bool hip_ok(hipError_t e, const char *what) {
+    if (e == hipSuccess && injected_failure()) e = hipErrorUnknown;
+    if (e == hipSuccess) return true;
+    latch_error((int)e, what);
+    return false;
 }
 
 static thread_local int tls_device_req = 0;
 static thread_local ThreadCtx tls_ctx;
 
-void ThreadCtx::reserve(size_t bytes) {
-    if (bytes <= cap) return;
+bool ThreadCtx::reserve(size_t bytes) {
+    if (bytes <= cap) return true;
     size_t n = cap ? cap : (size_t)1 << 20;
     while (n < bytes) n <<= 1;
-    if (host) hip_check(hipHostFree(host), "hipHostFree");
-    if (dev) hip_check(hipFree(dev), "hipFree");
-    hip_check(hipHostMalloc((void **)&host, n, hipHostMallocDefault), "hipHostMalloc");
-    hip_check(hipMalloc((void **)&dev, n), "hipMalloc");
+    if (host) (void)hipHostFree(host);
+    if (dev) (void)hipFree(dev);
+    host = dev = nullptr;
+    cap = 0;
+    if (!hip_ok(hipHostMalloc((void **)&host, n, hipHostMallocDefault), "hipHostMalloc")) {
+        host = nullptr;
+        return false;
+    }
+    if (!hip_ok(hipMalloc((void **)&dev, n), "hipMalloc")) {
+        dev = nullptr;
+        return false;
+    }
     cap = n;
+    return true;
 }
 
 ThreadCtx::~ThreadCtx() {
@@ -41,27 +79,31 @@ ThreadCtx::~ThreadCtx() {
     cap = 0;
 }
 
-ThreadCtx &thread_ctx() {
+ThreadCtx *thread_ctx() {
     ThreadCtx &c = tls_ctx;
     if (c.device != tls_device_req || !c.stream) {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
-            fprintf(stderr, "dav1d-gpu: no HIP device available; the GPU DSP tables "
-                            "cannot run (no CPU fallback by design)\n");
-            abort();
+            latch_error(-1, "device lookup (no HIP device)");
+            return nullptr;
         }
-        hip_check(hipSetDevice(tls_device_req), "hipSetDevice");
-        if (c.stream) hip_check(hipStreamDestroy(c.stream), "hipStreamDestroy");
-        if (c.host) hip_check(hipHostFree(c.host), "hipHostFree");
-        if (c.dev) hip_check(hipFree(c.dev), "hipFree");
+        if (!hip_ok(hipSetDevice(tls_device_req), "hipSetDevice")) return nullptr;
+        if (c.stream) (void)hipStreamDestroy(c.stream);
+        if (c.host) (void)hipHostFree(c.host);
+        if (c.dev) (void)hipFree(c.dev);
+        c.stream = nullptr;
         c.host = c.dev = nullptr;
         c.cap = 0;
-        hip_check(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate");
+        c.device = -1;
+        if (!hip_ok(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate")) {
+            c.stream = nullptr;
+            return nullptr;
+        }
         c.device = tls_device_req;
-    } else {
-        hip_check(hipSetDevice(c.device), "hipSetDevice");
+    } else if (!hip_ok(hipSetDevice(c.device), "hipSetDevice")) {
+        return nullptr;
     }
-    return c;
+    return &c;
 }
 
 int Stager::add(const void *base, ptrdiff_t stride, long bx0, long bx1, long y0, long y1, int dir) {
@@ -77,8 +119,12 @@ int Stager::add(const void *base, ptrdiff_t stride, long bx0, long bx1, long y0,
     return (int)rects_.size() - 1;
 }
 
-void Stager::upload() {
-    ctx_ = &thread_ctx();
+bool Stager::upload() {
+    ctx_ = nullptr;
+    if (!gpu_usable()) return false;
+    ThreadCtx *c = thread_ctx();
+    if (!c) return false;
+    ctx_ = c;
     // inputs, then in/out, then outputs: H2D covers [0, in_end_), D2H covers
     // the in/out + output tail.
     size_t off = 0;
@@ -93,7 +139,7 @@ void Stager::upload() {
         if (pass == 2) in_end_ = off;
     }
     total_ = off ? off : 256;
-    ctx_->reserve(total_);
+    if (!ctx_->reserve(total_)) return false;
     size_t out_begin = in_end_;
     for (auto &r : rects_)
         if (r.dir == 3 && r.off < out_begin) out_begin = r.off;
@@ -103,20 +149,26 @@ void Stager::upload() {
         for (long y = r.y0; y < r.y1; y++)
             memcpy(ctx_->host + r.off + (y - r.y0) * r.pitch, r.base + y * r.stride + r.bx0, rb);
     }
-    if (in_end_)
-        hip_check(hipMemcpyAsync(ctx_->dev, ctx_->host, in_end_, hipMemcpyHostToDevice, ctx_->stream),
-                  "H2D");
+    if (in_end_ &&
+        !hip_ok(hipMemcpyAsync(ctx_->dev, ctx_->host, in_end_, hipMemcpyHostToDevice, ctx_->stream), "H2D"))
+        return false;
+    return true;
 }
 
-void Stager::finish() {
-    hip_check(hipGetLastError(), "kernel launch");
+bool Stager::finish() {
+    if (!ctx_) return false;
+    // every step must succeed before the first output byte is scattered back
+    bool ok = hip_ok(hipGetLastError(), "kernel launch");
     size_t lo = total_;
     for (auto &r : rects_)
         if ((r.dir & 2) && r.off < lo) lo = r.off;
-    if (lo < total_)
-        hip_check(hipMemcpyAsync(ctx_->host + lo, ctx_->dev + lo, total_ - lo, hipMemcpyDeviceToHost,
-                                 ctx_->stream), "D2H");
-    hip_check(hipStreamSynchronize(ctx_->stream), "hipStreamSynchronize");
+    if (ok && lo < total_)
+        ok = hip_ok(hipMemcpyAsync(ctx_->host + lo, ctx_->dev + lo, total_ - lo, hipMemcpyDeviceToHost,
+                                   ctx_->stream), "D2H");
+    // drain the stream even after a failure: the staging buffer is reused
+    const hipError_t se = hipStreamSynchronize(ctx_->stream);
+    ok = ok && hip_ok(se, "hipStreamSynchronize");
+    if (!ok) return false;
     for (auto &r : rects_) {
         if (!(r.dir & 2)) continue;
         const long rb = r.bx1 - r.bx0;
@@ -124,6 +176,7 @@ void Stager::finish() {
         for (long y = r.y0; y < r.y1; y++)
             memcpy(b + y * r.stride + r.bx0, ctx_->host + r.off + (y - r.y0) * r.pitch, rb);
     }
+    return true;
 }
 
 }  // namespace dgpu
@@ -141,4 +194,8 @@ extern "C" int dav1d_gpu_set_device(int device) {
     return 0;
 }
 
-extern "C" const char *dav1d_gpu_version(void) { return "dav1d-gpu gfx950 r1"; }
+extern "C" const char *dav1d_gpu_version(void) { return "dav1d-gpu gfx950 r3"; }
+
+extern "C" int dav1d_gpu_get_error(void) { return dgpu::g_error.load(); }
+
+extern "C" int dav1d_gpu_clear_error(void) { return dgpu::g_error.exchange(0); }

@@ -15,10 +15,39 @@
 
 namespace dgpu {
 
-[[noreturn]] void fatal(const char *what, hipError_t e);
-inline void hip_check(hipError_t e, const char *what) {
-    if (e != hipSuccess) fatal(what, e);
+// Error contract: a per-call entry never aborts and never
+// writes part of its outputs.  A HIP failure latches a process-wide sticky
+// error (dav1d_gpu_get_error) and the entry then runs the C default the
+// caller's table held before the _gpu_ hook overwrote it (the fallback
+// tables below), or, when the library replaced the whole table, leaves its
+// outputs untouched.  Once latched, later entries skip the GPU until the
+// caller clears the error (the reference's own error latch,
+// src/thread_task.c:453 / src/lib.c:715, is checked the same way).
+bool hip_ok(hipError_t e, const char *what);   // false: error latched
+void latch_error(int code, const char *what);
+bool gpu_usable();                             // no error latched
+
+// The caller's table entries before a _gpu_ hook overwrote them: every slot
+// of `caller` that is not the GPU entry itself (a second hook call must not
+// make the GPU its own fallback).  Contexts are arrays of function pointers.
+template <typename Ctx>
+inline void save_fallback(Ctx *fb, const Ctx *caller, const Ctx *gpu) {
+    constexpr int n = sizeof(Ctx) / sizeof(void *);
+    static_assert(sizeof(Ctx) % sizeof(void *) == 0, "function-pointer tables only");
+    void *const *c = reinterpret_cast<void *const *>(caller);
+    void *const *g = reinterpret_cast<void *const *>(gpu);
+    void **f = reinterpret_cast<void **>(fb);
+    for (int i = 0; i < n; i++)
+        if (c[i] != g[i]) f[i] = c[i];
 }
+// run the fallback entry when the GPU path did not complete
+#define DGPU_OR_FALLBACK(ok, fn, ...)          \
+    do {                                       \
+        if (!(ok)) {                           \
+            auto f_ = (fn);                    \
+            if (f_) f_(__VA_ARGS__);           \
+        }                                      \
+    } while (0)
 
 struct ThreadCtx {
     int device = -1;
@@ -26,13 +55,13 @@ struct ThreadCtx {
     uint8_t *host = nullptr;  // pinned
     uint8_t *dev = nullptr;
     size_t cap = 0;
-    void reserve(size_t bytes);
+    bool reserve(size_t bytes);
     // A worker thread's stream and staging buffers die with the thread
     // (dav1d starts and joins its n_tc workers per decoder instance, so a
     // long-running process would otherwise leak them on every instance).
     ~ThreadCtx();
 };
-ThreadCtx &thread_ctx();
+ThreadCtx *thread_ctx();   // nullptr (error latched) when no usable device
 
 // A rectangle of bytes relative to a caller base pointer:
 // rows [y0, y1), byte columns [bx0, bx1), caller row stride `stride` (may be
@@ -60,16 +89,18 @@ public:
     int inout1(void *b, long bytes) { return add(b, 0, 0, bytes, 0, 1, 3); }
 
     // Lays out the buffer and uploads the inputs; after this origin()/pitch()
-    // are valid and the caller launches its kernel on stream().
-    void upload();
+    // are valid and the caller launches its kernel on stream().  false: the
+    // GPU is unusable (error latched); launch nothing, write nothing.
+    [[nodiscard]] bool upload();
     template <typename T> T *origin(int i) const {
         const Rect &r = rects_[i];
         return reinterpret_cast<T *>(ctx_->dev + r.off - r.y0 * (long)r.pitch - r.bx0);
     }
     ptrdiff_t pitch(int i) const { return (ptrdiff_t)rects_[i].pitch; }
     hipStream_t stream() const { return ctx_->stream; }
-    // Downloads outputs, waits, scatters them back into the caller's memory.
-    void finish();
+    // Downloads outputs, waits, scatters them back into the caller's memory
+    // -- all of them, or (on any HIP error, then latched) none: false.
+    [[nodiscard]] bool finish();
 
 private:
     ThreadCtx *ctx_ = nullptr;

@@ -703,17 +703,39 @@ class Recorder:
         if rc:
             raise RuntimeError(f"dav1d_gpu_recorder_flush: {rc}")
 
+    def status(self):
+        """The last flush's outcome (dav1d_gpu_recorder_status): 0, -6 (its
+        wavefront gave up waiting: incomplete picture) or -3."""
+        return self.lib.dav1d_gpu_recorder_status(self.h)
+
+    def flush_rc(self, dst, refs, stream):
+        """flush() returning the library's code instead of raising."""
+        try:
+            self.flush(dst, refs, stream)
+            return 0
+        except RuntimeError as e:
+            return int(str(e).rsplit(":", 1)[1])
+
     def stats(self):
         n, lv = ctypes.c_int32(), ctypes.c_int32()
         self.lib.dav1d_gpu_recorder_stats(self.h, ctypes.byref(n), ctypes.byref(lv))
         return n.value, lv.value
 
 
-def replay(rec, fr):
+def replay(rec, fr, rows=None):
     """Feed an IntraFrame's blocks and residuals to a Recorder, in decode
     order, the way recon_b_* would (coefficients expanded to the reference's
-    inv_txfm_add layout: column-major, min(h,32) rows)."""
+    inv_txfm_add layout: column-major, min(h,32) rows).  rows=(y0, y1): only
+    the blocks (and their residuals) of luma superblock rows [y0, y1) in
+    pixels (chroma: the co-located half), for flushes per superblock row."""
+    def inside(p, y):
+        if rows is None:
+            return True
+        s = 1 if p else 0
+        return (rows[0] >> s) <= y < (rows[1] >> s)
     for t in fr.blocks:
+        if not inside(t[0], t[2]):
+            continue
         rb = abi.RecBlock()
         (rb.plane, rb.x, rb.y, rb.w, rb.h, rb.tx, rb.kind, rb.tile_x0, rb.tile_y0, rb.tile_x1, rb.tile_y1,
          rb.mvx[0], rb.mvx[1], rb.mvy[0], rb.mvy[1], rb.ref[0], rb.ref[1], rb.filter2d, rb.weight, rb.mode,
@@ -724,6 +746,8 @@ def replay(rec, fr):
         p = int(u["plane"][i])
         w = fr.plane_wh[p][0]
         y, x = divmod(int(u["dst_off"][i]), w)
+        if not inside(p, y):
+            continue
         tw, th = abi.TX_WH[int(u["tx"][i])]
         sw, sh = min(tw, 32), min(th, 32)
         cf = np.zeros(sw * sh, np.int64)

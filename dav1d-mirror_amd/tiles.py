@@ -319,8 +319,7 @@ def build_tiles(fd):
 
     stats = dict(fd.stats)
     desc = n_tiles_all * TILE_DTYPE.itemsize + npred * PRED_DTYPE.itemsize + len(xu) * TX_DTYPE.itemsize
-    stats["total_bytes"] = stats["total_bytes"] - stats["desc_bytes"] + desc
-    stats["desc_bytes"] = desc
+    stats["desc_bytes"] = desc   # the tile / pred / tx records: not in total_bytes (algorithmic)
     stats["n_tiles"] = n_tiles_all
     stats["n_preds"] = npred
     stats["n_txs"] = len(xu)

@@ -524,8 +524,10 @@ def make_frame(cfg: FrameConfig) -> FrameData:
 def algorithmic_bytes(fd: FrameData):
     """Bytes the reconstruction must move per frame: the
     reference footprint each mc call reads, edge arrays, stored
-    coefficients, one write of every output pixel, and the 32-B unit
-    descriptors."""
+    coefficients, one write of every output pixel (plus the picture read of
+    residual-only units and the aux records).  The batch's own 32-B unit
+    descriptors are the builder's format, not algorithmic work: reported as
+    desc_bytes, outside total_bytes."""
     u = fd.units
     bpp = 1 if fd.cfg.bpc == 8 else 2
     cb = 2 if fd.cfg.bpc == 8 else 4
@@ -577,7 +579,7 @@ def algorithmic_bytes(fd: FrameData):
         "desc_bytes": int(len(u)) * 32,
         "pixels": out_px,
         "total_bytes": int(src.sum()) * bpp + int(edge.sum()) * bpp + int(ncoef.sum()) * cb
-                       + out_px * bpp + dst_read + aux_bytes + int(len(u)) * 32,
+                       + out_px * bpp + dst_read + aux_bytes,
         "n_intra": int(intra.sum()),
         "n_cfl": int(cfl.sum()),
         "n_inter": int(inter.sum()),

@@ -33,9 +33,15 @@
  * points take the trailing `bitdepth_max` argument (0x3ff or 0xfff) except
  * blend*, emu_edge, cfl_ac and pal_pred (src/mc.h:96-108, src/ipred.h:56-78).
  *
- * Errors: the per-call entries return void like the reference.  A HIP failure
- * inside one is fatal (message on stderr, abort()): the tables never silently
- * fall back to CPU code.  The batch entry points return 0 or a negative error.
+ * Errors: the per-call entries return void like the reference
+ * and never abort or write part of their outputs.  A HIP failure latches a
+ * sticky, process-wide error (dav1d_gpu_get_error) that the caller checks at a
+ * flush point, as dav1d checks its own task error latch (src/thread_task.c:
+ * 453, src/lib.c:715); the failed call -- and every later one until
+ * dav1d_gpu_clear_error -- then runs the entry the caller's table held before
+ * the *_gpu_* hook overwrote it (the C default), or, when the library filled
+ * the whole table (no previous entry), leaves its outputs untouched.  The
+ * batch entry points return 0 or a negative error.
  */
 #ifndef DAV1D_GPU_H
 #define DAV1D_GPU_H
@@ -194,8 +200,15 @@ void dav1d_itx_dsp_init_gpu_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc);
 int dav1d_gpu_device_count(void);
 /* Device used by the calling thread's per-call entries (default 0). */
 int dav1d_gpu_set_device(int device);
-/* Library build identification, e.g. "dav1d-gpu gfx950 r1". */
+/* Library build identification, e.g. "dav1d-gpu gfx950 r3". */
 const char *dav1d_gpu_version(void);
+/* Sticky error of the per-call tier: 0, or the first HIP error code (-1: no
+ * device) latched since the last clear.  While it is set the per-call entries
+ * do not touch the GPU (fallback entries, or no output).  clear returns the
+ * previous value and re-enables the GPU path.  Test hook: the environment
+ * variable DAV1D_GPU_FAIL_AFTER=n fails the (n+1)-th HIP call of the tier. */
+int dav1d_gpu_get_error(void);
+int dav1d_gpu_clear_error(void);
 
 /* ---- batch tier ----------------------------------------------------------
  * A batch is an array of transform-block "units" (one per inv_txfm_add call
@@ -675,6 +688,12 @@ int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane dst[3],
                              const Dav1dGpuPlane ref[DGPU_MAX_REFS][3], void *stream);
 /* Levels and units of the last flush (diagnostics). */
 int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_units, int32_t *n_levels);
+/* Outcome of the last flush (waits for it): 0, -6 if its wavefront gave up
+ * waiting for producers (that picture is incomplete), -3 on a HIP error.  An
+ * outcome is reported once: a -6 not read here is returned by the next flush,
+ * which then launches nothing and keeps its recording.  A flush also returns
+ * -1 when an inter block names a reference plane that `ref` leaves NULL. */
+int dav1d_gpu_recorder_status(Dav1dGpuRecorder *r);
 
 /* ---- film grain ----------------------------------------
  * bitfn(dav1d_apply_grain) (src/fg_apply_tmpl.c:222-241) on the device:

@@ -73,6 +73,12 @@ def test_batch_4k_full_bitexact(pkg, oracle):
     _check(_frame(pkg), oracle, threads=8)
 
 
+def test_batch_4k_10bit_bitexact(pkg, oracle):
+    """BASELINE config 4 at its full size: 3840x2160, 16bpc ABI,
+    bitdepth_max 1023, int32 coefficients."""
+    _check(_frame(pkg, bpc=16, bitdepth_max=1023), oracle, threads=8)
+
+
 def test_batch_1080p_mc_bitexact(pkg, oracle):
     """BASELINE config 2 at its full size."""
     _check(_frame(pkg, width=1920, height=1080, kind="mc"), oracle, threads=8)

@@ -15,7 +15,7 @@ build() {
     done
     wait
     local objs=""
-    for s in runtime mc ipred itx recon8 recon16 tile8 tile16 edges recon_ie8 recon_ie16 recorder grain; do
+    for s in runtime mc ipred itx recon8 recon16 tile8 tile16 edges recon_ie8 recon_ie16 recorder grain cdef lpf lr; do
         if [ -f build/var/$name.$s.o ] && [[ " ${TUS:-recon8 recon16} " == *" $s "* ]]; then objs="$objs build/var/$name.$s.o"; else objs="$objs build/$s.o"; fi
     done
     $HIPCC $F -shared -o libdav1d_gpu.$name.so $objs
@@ -38,6 +38,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         ftrace127) TUS="recon_ie8" build ftrace127 -DDGPU_FLOW_TRACE=1 -DDGPU_FLOW_SLEEP=127 ;;
         fsleep32) TUS="recon_ie8" build fsleep32 -DDGPU_FLOW_SLEEP=32 ;;
         fsleep127) TUS="recon_ie8" build fsleep127 -DDGPU_FLOW_SLEEP=127 ;;
+        ntmeta) build ntmeta -DDGPU_NT_META=1 ;;
         nomc) build nomc -DDGPU_ABL_MC=1 ;;
         nostore) build nostore -DDGPU_ABL_STORE=1 ;;
         noitx) build noitx -DDGPU_ABL_ITX=1 ;;
