@@ -20,7 +20,9 @@ NO_RESIDUAL = 0xFF          # txtp value: prediction only (no inv_txfm_add)
 
 PRED_NONE, PRED_INTER, PRED_INTER_AVG, PRED_INTRA, PRED_CFL = 0, 1, 2, 3, 4
 PRED_INTER_WAVG, PRED_INTER_MASK, PRED_PAL, PRED_WARP, PRED_INTER_INTRA = 5, 6, 7, 8, 9
-SECOND_LAUNCH_KINDS = (PRED_WARP, PRED_INTER_INTRA)   # the batch's class_warp sub-ranges
+PRED_INTER_WMASK, PRED_INTER_OBMC, PRED_INTER_SCALED = 10, 11, 12
+SECOND_LAUNCH_KINDS = (PRED_WARP, PRED_INTER_INTRA, PRED_INTER_WMASK, PRED_INTER_OBMC,
+                       PRED_INTER_SCALED)   # the batch's class_warp sub-ranges
 INTER_KINDS = (PRED_INTER, PRED_INTER_AVG, PRED_INTER_WAVG, PRED_INTER_MASK)
 COMPOUND_KINDS = (PRED_INTER_AVG, PRED_INTER_WAVG, PRED_INTER_MASK)
 FILTER_2D_BILINEAR = 9

@@ -18,7 +18,10 @@ def _ptr(t):
 class DeviceFrame:
     """A FrameData uploaded to one GPU, plus its output planes."""
 
-    def __init__(self, fd, device="cuda:0", zero_coefs=False):
+    def __init__(self, fd, device="cuda:0", zero_coefs=False, dst_planes=None):
+        """dst_planes: optional device tensors to reconstruct into, (rows >=
+        h, stride in pixels >= w) each -- e.g. a frame chain's 128-aligned
+        pictures -- instead of exact-size planes of its own."""
         import torch
         self.torch = torch
         self.fd = fd
@@ -39,7 +42,9 @@ class DeviceFrame:
             self.refs.append(planes)
         cl = fd.cfl_luma if fd.cfg.bpc == 8 else fd.cfl_luma.view(np.int16)
         self.cfl_luma = torch.from_numpy(cl.copy()).to(dev)
-        if fd.dst_init is not None:
+        if dst_planes is not None:
+            self.dst = list(dst_planes)
+        elif fd.dst_init is not None:
             self.dst = [torch.from_numpy((a if fd.cfg.bpc == 8 else a.view(np.int16)).copy()).to(dev)
                         for a in fd.dst_init]
         else:
@@ -59,7 +64,7 @@ class DeviceFrame:
         for p in range(3):
             w, h = fd.plane_wh[p]
             b.dst[p].data = self.dst[p].data_ptr()
-            b.dst[p].stride = w * bpp
+            b.dst[p].stride = self.dst[p].shape[1] * bpp
             b.dst[p].w, b.dst[p].h = w, h
             for r in range(len(self.refs)):
                 t = self.refs[r][p]
@@ -100,8 +105,9 @@ class DeviceFrame:
     def planes_host(self):
         """Reconstructed planes as numpy arrays (uint8 / uint16)."""
         out = []
-        for t in self.dst:
-            a = t.cpu().numpy()
+        for p, t in enumerate(self.dst):
+            w, h = self.fd.plane_wh[p]
+            a = t[:h, :w].cpu().numpy()
             out.append(a if self.fd.cfg.bpc == 8 else a.view(np.uint16))
         return out
 
@@ -127,7 +133,9 @@ class DeviceTiles:
         self.aux_pool = up(td.aux_pool) if td.aux_pool is not None else None
         self.refs = [[up(a if not hbd else a.view(np.int16)) for a in rp] for rp in fd.refs]
         self.cfl_luma = up(fd.cfl_luma if not hbd else fd.cfl_luma.view(np.int16))
-        if fd.dst_init is not None:
+        if dst_planes is not None:
+            self.dst = list(dst_planes)
+        elif fd.dst_init is not None:
             self.dst = [up(a if not hbd else a.view(np.int16)) for a in fd.dst_init]
         else:
             self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fd.plane_wh]
@@ -142,7 +150,7 @@ class DeviceTiles:
         for p in range(3):
             w, h = fd.plane_wh[p]
             b.dst[p].data = self.dst[p].data_ptr()
-            b.dst[p].stride = w * bpp
+            b.dst[p].stride = self.dst[p].shape[1] * bpp
             b.dst[p].w, b.dst[p].h = w, h
             for r in range(len(self.refs)):
                 t = self.refs[r][p]

@@ -47,8 +47,19 @@ __device__ __forceinline__ void run_class(const ReconArgs<BPC> &a, const PlaneTa
                                           const Dav1dGpuIntraEdge &rec, int first, int count, uint8_t *lds, int gw,
                                           const WaitT &wait = WaitT()) {
     if constexpr (TX < DGPU_N_RECT_TX_SIZES && in_group(TX, GRP) &&
-                  (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS))
-        recon_units<BPC, TX, GRP == GROUP_WARP, gathers(GRP)>(a, pt, u, rec, first, count, lds, gw, GRP, wait);
+                  (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS)) {
+        if constexpr (GRP == GROUP_WARP) {
+            // the second launch: w_mask / OBMC / scaled units in their own
+            // function, warp and inter-intra in recon_units (per unit: a wave
+            // at the boundary of the two sorted runs holds both)
+            const bool ext = u.pred == DGPU_PRED_INTER_WMASK || u.pred == DGPU_PRED_INTER_OBMC ||
+                             u.pred == DGPU_PRED_INTER_SCALED;
+            if (ext) recon_units_ext<BPC, TX>(a, pt, u, first, count, lds);
+            else recon_units<BPC, TX, true, false>(a, pt, u, rec, first, count, lds, gw, GRP, wait);
+        } else {
+            recon_units<BPC, TX, false, gathers(GRP)>(a, pt, u, rec, first, count, lds, gw, GRP, wait);
+        }
+    }
 }
 
 // One switch (a compact compare tree) instead of a chain of class tests
@@ -142,12 +153,8 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     if (count <= 0) return;
     // this lane's unit descriptor (lanes past the last unit re-read it)
     const int ui_ = first + min((int)(threadIdx.x & 63) >> lg, count - 1);
-    Dav1dGpuUnit u;
-    {
-        const u32x4 d0 = gld_meta<u32x4>(units + ui_), d1 = gld_meta<u32x4>(reinterpret_cast<const uint8_t *>(units + ui_) + 16);
-        __builtin_memcpy(&u, &d0, 16);
-        __builtin_memcpy(reinterpret_cast<uint8_t *>(&u) + 16, &d1, 16);
-    }
+    // (a struct load: assembling it from vector loads spilled it to scratch)
+    const Dav1dGpuUnit u = units[ui_];
     Dav1dGpuIntraEdge rec{};
     if constexpr (gathers(GRP)) rec = a.recs[ui_];   // its edge record, in the same round trip
     // per-wave copy of the plane table: lane-indexed vector loads of the

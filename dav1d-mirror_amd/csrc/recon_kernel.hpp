@@ -247,6 +247,11 @@ template <int BPC, int TX> struct Slot {
     static constexpr int SRC = cmax((CL::SEQREF ? 1 : 2) * MID, EB + cmax(FE, PT));
     static constexpr int BYTES = CFR + TMP + SRC;
     static constexpr int WAVE = CL::U * BYTES;
+    // the second launch (WARP group): INTER_SCALED keeps its h-pass output
+    // as int16 [rows][W] with rows <= 2H + 8 (steps dx, dy <= 2048)
+    static constexpr int SCALED = a16((2 * H + 8) * W * 2);
+    static constexpr int BYTES_W = CFR + TMP + cmax(SRC, SCALED);
+    static constexpr int WAVE_W = CL::U * BYTES_W;
 };
 
 // LDS bytes per wave of a launch group: its largest class slot set; the warp
@@ -254,7 +259,10 @@ template <int BPC, int TX> struct Slot {
 template <int BPC, int GRP, int... TX>
 __host__ __device__ constexpr int group_wave_lds(std::integer_sequence<int, TX...>) {
     int m = 0;
-    ((m = (in_group(TX, GRP) && Slot<BPC, TX>::WAVE > m) ? Slot<BPC, TX>::WAVE : m), ...);
+    if constexpr (GRP == GROUP_WARP)
+        ((m = (in_group(TX, GRP) && Slot<BPC, TX>::WAVE_W > m) ? Slot<BPC, TX>::WAVE_W : m), ...);
+    else
+        ((m = (in_group(TX, GRP) && Slot<BPC, TX>::WAVE > m) ? Slot<BPC, TX>::WAVE : m), ...);
     return m;
 }
 template <int BPC> inline constexpr int kWarpTabOff =
@@ -351,16 +359,6 @@ __device__ __forceinline__ void vdot4x4(const uint32_t (*a)[4], const uint4 &tv,
 template <typename T> __device__ __forceinline__ T gld(const void *p) {
     return *(const __attribute__((address_space(1))) T *)p;
 }
-// Loads of data each unit reads once (descriptors, coefficients, edges):
-// DGPU_NT_META=1 marks them non-temporal so they do not displace the
-// picture lines still being written in L2 (experiment knob)
-#ifndef DGPU_NT_META
-#define DGPU_NT_META 0
-#endif
-template <typename T> __device__ __forceinline__ T gld_meta(const void *p) {
-    if constexpr (DGPU_NT_META) return __builtin_nontemporal_load((const __attribute__((address_space(1))) T *)p);
-    else return gld<T>(p);
-}
 template <typename T> __device__ __forceinline__ void gst(void *p, T v) {
     *(__attribute__((address_space(1))) T *)p = v;
 }
@@ -386,7 +384,7 @@ template <int MAXN, int G> struct Stage {
         const uint8_t *s = reinterpret_cast<const uint8_t *>(src) - sk;
         nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
 #pragma unroll
-        for (int k = 0; k < IT; k++) v[k] = gld_meta<u32x4>(s + 16 * min(l + k * G, nch - 1));   // clamped
+        for (int k = 0; k < IT; k++) v[k] = gld<u32x4>(s + 16 * min(l + k * G, nch - 1));   // clamped
     }
     __device__ __forceinline__ int commit(uint8_t *dst, int l) const {
 #pragma unroll
@@ -1138,7 +1136,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     Dav1dGpuUnit ug = u_in;   // GATHER: the edge stage rewrites its mode / angle
     const Dav1dGpuUnit &u = GATHER ? ug : u_in;
     mark(1);   // the descriptor was loaded by the kernel prologue (lane's unit = first + g)
-    uint8_t *slot = wave_lds + g * SL::BYTES;
+    uint8_t *slot = wave_lds + g * (WARPK ? SL::BYTES_W : SL::BYTES);
     uint8_t *cfl = slot;                                           // staged coefs, then residual
     TT *res = reinterpret_cast<TT *>(slot);
     TT *tmp = reinterpret_cast<TT *>(slot + SL::CFR);
@@ -1658,6 +1656,364 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(p3), "v"(v0), "v"(v1), "v"(v2), "v"(v3));
     }
 #endif
+}
+
+
+// ------------------------------------------------- the second launch's kinds --
+// INTER_WMASK, INTER_OBMC and INTER_SCALED units (include/dav1d_gpu.h): run
+// by the WARP group's kernel beside warp / inter-intra, in a function of
+// their own so that the main kernel's code (recon_units above, which sits at
+// the edge of its 5-wave register budget) is not perturbed by them.  Same
+// phases as recon_units: staged coefficients, both transform passes into the
+// LDS residual, then the prediction + residual per 4x2 task.
+template <int BPC, int TX>
+__device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt,
+                                                const Dav1dGpuUnit &u, int first, int count, uint8_t *wave_lds) {
+    using CL = Cls<TX>;
+    using SL = Slot<BPC, TX>;
+    using P = typename Px<BPC>::pixel;
+    using C = typename Px<BPC>::coef;
+    using TT = typename Tmp<BPC>::T;
+    constexpr int W = CL::W, H = CL::H, SW = CL::SW, SH = CL::SH, G = CL::G, QW = CL::QW, NT = CL::NT;
+    constexpr int TPL = CL::TPL;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / G, l = lane % G;
+    if (g >= count) return;
+    uint8_t *slot = wave_lds + g * SL::BYTES_W;
+    uint8_t *cfl = slot;
+    TT *res = reinterpret_cast<TT *>(slot);
+    TT *tmp = reinterpret_cast<TT *>(slot + SL::CFR);
+    uint8_t *src = slot + SL::CFR + SL::TMP;
+    uint32_t *mid0 = reinterpret_cast<uint32_t *>(src);
+    uint32_t *mid1 = reinterpret_cast<uint32_t *>(src + (CL::SEQREF ? 0 : SL::MID));
+
+    const int plane = u.plane;
+    const int bdmax = a.bdmax;
+    const int ib = Px<BPC>::ibits(bdmax);
+    const int pred = u.pred;
+    const bool wm = pred == DGPU_PRED_INTER_WMASK, ob = pred == DGPU_PRED_INTER_OBMC;
+    const bool sc = pred == DGPU_PRED_INTER_SCALED;
+    const int txtp = u.txtp;
+    const bool nores = txtp == DGPU_NO_RESIDUAL;
+    const int nzw = u.nzw, nzh = u.nzh;
+    const bool dconly = !nores && nzw == 0;
+    const bool haveres = !nores && !dconly;
+    P *dstp = pt.dst[plane] + u.dst_off;
+    const int ds = pt.dst_stride[plane];
+    const int auxo = a.aux[first + g];
+
+    // ---- loads: coefficients and the first reference's footprint rows
+    C *cf = a.coef + u.coef_off;
+    const int ncoef = nores ? 0 : dconly ? 1 : nzw * nzh;
+    Stage<CL::SW * CL::SH * (int)sizeof(C), G> cst;
+    if (ncoef) cst.load(cf, ncoef * (int)sizeof(C), l);
+    const int f2d = u.p.inter.filter2d;
+    const bool bil = f2d == DGPU_FILTER_2D_BILINEAR;
+    const int ftype = bil ? 0 : (int)((0x951a62840ull >> (4 * f2d)) & 15);   // type_h | type_v << 2
+    const int bw = u.bw4 * 4, bh = u.bh4 * 4;
+    const int bank_h = mc_bank(ftype & 3, bil, bw), bank_v = mc_bank(ftype >> 2, bil, bh);
+    const uint4 tv0 = reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[0]];
+    const uint4 tv1 = reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[1]];
+    auto hinit = [&](HPass<BPC, TX> &hp, int k) {
+        const int r = u.p.inter.ref[k];
+        const int rs = pt.ref_stride[r * 3 + plane];
+        const P *org = pt.ref[r * 3 + plane] + u.p.inter.src_off[k] - 3 * rs - 3;
+        hp.init(org, rs, k ? mid1 : mid0, bank_h, u.p.inter.mx[k], l, 0, H + 7);
+    };
+    HPass<BPC, TX> hp0;
+    if (wm || ob) {
+        hinit(hp0, 0);
+        hp0.load(0);
+    }
+    int cfsk = 0;
+    if (ncoef) cfsk = cst.commit(cfl, l);
+    if (wm || ob) {
+        hp0.compute(0, ib);
+        hp0.rest(ib);
+        if (!CL::SEQREF && wm) {
+            HPass<BPC, TX> hp1;
+            hinit(hp1, 1);
+            hp1.load(0);
+            hp1.compute(0, ib);
+            hp1.rest(ib);
+        }
+    }
+    wave_sync();
+    if (a.zero_coefs && ncoef)
+        for (int i = l; i < ncoef; i += G) cf[i] = 0;
+
+    // ---- row, then column transforms into the residual (as recon_units)
+    int dcres = 0;
+    if (dconly) {   // src/itx_tmpl.c:53-65
+        int dc = reinterpret_cast<const C *>(cfl + cfsk)[0];
+        if (CL::RECT2) dc = r8s(dc);
+        dc = r8s(dc);
+        dc = (dc + ((1 << CL::SHIFT) >> 1)) >> CL::SHIFT;
+        dcres = (dc * 181 + 128 + 2048) >> 12;
+    }
+    const Clip rc = ItxClip<BPC>::row(bdmax), cc = ItxClip<BPC>::col(bdmax);
+    if (haveres) {
+        const C *cs = reinterpret_cast<const C *>(cfl + cfsk);
+#pragma unroll
+        for (int k = 0; k < (SH + G - 1) / G; k++) {
+            const int r = l + k * G;
+            if (r < SH) {
+                TT *trow = tmp + r * W;
+                int c[W];
+#pragma unroll
+                for (int x = 0; x < W; x++) {
+                    int v = 0;
+                    if (x < SW && r < nzh) {
+                        v = cs[x * nzh + r];
+                        v = x < nzw ? v : 0;
+                    }
+                    c[x] = CL::RECT2 ? r8s(v) : v;
+                }
+                if (r < nzh) tx1d<W, 1>(kind_h(txtp), c, rc);
+                constexpr int RND = (1 << CL::SHIFT) >> 1;
+#pragma unroll
+                for (int x = 0; x < W; x++) trow[x] = (TT)cc((c[x] + RND) >> CL::SHIFT);
+            }
+        }
+    }
+    wave_sync();
+    if (haveres) {
+#pragma unroll
+        for (int k = 0; k < (W + G - 1) / G; k++) {
+            const int x = l + k * G;
+            if (x < W) {
+                int col[H];
+#pragma unroll
+                for (int y = 0; y < H; y++) col[y] = y < SH ? (int)tmp[y * W + x] : 0;
+                tx1d<H, 1>(kind_v(txtp), col, cc);
+                TT *rcol = res + x * H;
+#pragma unroll
+                for (int y = 0; y < H; y++) rcol[y] = (TT)((col[y] + 8) >> 4);
+            }
+        }
+    }
+    wave_sync();
+
+    auto emit = [&](int j, int q, const int *pv) {   // + residual, clip, store 2 rows of 4
+#pragma unroll
+        for (int rr = 0; rr < 2; rr++) {
+            int o[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int rv = haveres ? (int)res[(4 * q + i) * H + 2 * j + rr] : dcres;
+                o[i] = clampi(pv[4 * rr + i] + rv, 0, bdmax);
+            }
+            P *row = dstp + (2 * j + rr) * ds + 4 * q;
+            if constexpr (BPC == 8)
+                gst<uint32_t>(row, (uint32_t)o[0] | o[1] << 8 | o[2] << 16 | (uint32_t)o[3] << 24);
+            else
+                gst<u32x2>(row, u32x2{(uint32_t)o[0] | o[1] << 16, (uint32_t)o[2] | (uint32_t)o[3] << 16});
+        }
+    };
+    const int psh = 6 + ib, pkp = kMidBias<BPC> + (1 << (psh - 1));   // put rounding
+
+    if (wm) {   // COMP_INTER_SEG luma: mct x2, w_mask_c (src/mc_tmpl.c:683-726)
+        constexpr int KP = kMidBias<BPC> + 32;
+        int q0[CL::SEQREF ? TPL : 1][8];
+        if constexpr (CL::SEQREF) {   // the first ref's prep values held while the second's h-pass reuses the tile
+#pragma unroll
+            for (int k = 0; k < TPL; k++) {
+                const int t = l + k * G;
+                if (t < NT) mc_vtask<W>(mid0, t / QW, t % QW, tv0, KP, 6, q0[k]);
+            }
+            wave_sync();
+            HPass<BPC, TX> hp1;
+            hinit(hp1, 1);
+            hp1.load(0);
+            hp1.compute(0, ib);
+            hp1.rest(ib);
+            wave_sync();
+        }
+        const int sign = u.p.inter.weight;
+        const int msh = bits_of(bdmax) + ib - 4, mrnd = 1 << (msh - 5);
+        // the mask at the chroma layout's resolution (cfl_ss), row stride
+        // bw >> ss_hor; aux = the unit's top-left value in it
+        uint8_t *mo = const_cast<uint8_t *>(a.aux_pool) + auxo;
+        const int ssh = a.cfl_ss & 1, ssv = (a.cfl_ss >> 1) & 1, ms = bw >> ssh;
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t >= NT) break;
+            const int j = t / QW, q = t % QW;
+            int p0[8], p1[8], pv[8], mm[8];
+            if constexpr (CL::SEQREF) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) p0[i] = q0[k][i];
+            } else {
+                mc_vtask<W>(mid0, j, q, tv0, KP, 6, p0);
+            }
+            mc_vtask<W>(mid1, j, q, tv1, KP, 6, p1);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {   // p = prep + PREP_BIAS: the bias terms cancel
+                const int m = min(38 + ((abs(p0[i] - p1[i]) + mrnd) >> msh), 64);
+                mm[i] = m;
+                pv[i] = clampi((p0[i] * m + p1[i] * (64 - m) + (32 << ib)) >> (ib + 6), 0, bdmax);
+            }
+            if (!ssh) {
+#pragma unroll
+                for (int rr = 0; rr < 2; rr++)
+                    gst<uint32_t>(mo + (2 * j + rr) * ms + 4 * q, (uint32_t)mm[4 * rr] | mm[4 * rr + 1] << 8 |
+                                                                      mm[4 * rr + 2] << 16 |
+                                                                      (uint32_t)mm[4 * rr + 3] << 24);
+            } else if (!ssv) {
+#pragma unroll
+                for (int rr = 0; rr < 2; rr++) {
+                    const int v0 = (mm[4 * rr] + mm[4 * rr + 1] + 1 - sign) >> 1;
+                    const int v1 = (mm[4 * rr + 2] + mm[4 * rr + 3] + 1 - sign) >> 1;
+                    gst<uint16_t>(mo + (2 * j + rr) * ms + 2 * q, (uint16_t)(v0 | v1 << 8));
+                }
+            } else {
+                const int v0 = (mm[0] + mm[1] + mm[4] + mm[5] + 2 - sign) >> 2;
+                const int v1 = (mm[2] + mm[3] + mm[6] + mm[7] + 2 - sign) >> 2;
+                gst<uint16_t>(mo + j * ms + 2 * q, (uint16_t)(v0 | v1 << 8));
+            }
+            emit(j, q, pv);
+        }
+    } else if (ob) {
+        // the block's own put prediction, then the neighbours' predictions
+        // over the unit's overlap regions (the lap calls), blended in the
+        // reference's order: every blend_h (above) before every blend_v (left)
+        const int sh = psh, kp = pkp;
+        int ipv[TPL][8];
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t < NT) {
+                int t0[8];
+                mc_vtask<W>(mid0, t / QW, t % QW, tv0, kp, sh, t0);
+#pragma unroll
+                for (int i = 0; i < 8; i++) ipv[k][i] = clampi(t0[i], 0, bdmax);
+            }
+        }
+        const uint8_t *rec = a.aux_pool + auxo;
+        const int ne = gld<int>(rec);
+        int nmax = ne;   // the loop runs to the most entries of the wave's units
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
+#pragma unroll 1
+        for (int e = 0; e < nmax; e++) {
+            wave_sync();   // the intermediate tile is free
+            const bool has = e < ne;
+            const u32x4 er = has ? gld<u32x4>(rec + 16 + 16 * e) : u32x4{0, 0, 0, 0};
+            const int ef2d = (er[1] >> 16) & 0xff, eref = er[1] >> 24;
+            const bool ebil = ef2d == DGPU_FILTER_2D_BILINEAR;
+            const int eft = ebil ? 0 : (int)((0x951a62840ull >> (4 * ef2d)) & 15);
+            const int ebh = mc_bank(eft & 3, ebil, (int)(er[3] & 0xff) * 4);
+            const int ebv = mc_bank(eft >> 2, ebil, (int)((er[3] >> 8) & 0xff) * 4);
+            if (has) {
+                HPass<BPC, TX> hp;
+                const int rs = pt.ref_stride[eref * 3 + plane];
+                const P *org = pt.ref[eref * 3 + plane] + (int)er[0] - 3 * rs - 3;
+                hp.init(org, rs, mid0, ebh, (int)(er[1] & 0xff), l, 0, H + 7);
+                hp.load(0);
+                hp.compute(0, ib);
+                hp.rest(ib);
+            }
+            wave_sync();
+            const uint4 etv = reinterpret_cast<const uint4 *>(dspt_mc16)[ebv * 16 + ((er[1] >> 8) & 0xff)];
+            const int x0 = er[2] & 0xff, y0 = (er[2] >> 8) & 0xff, x1 = (er[2] >> 16) & 0xff, y1 = er[2] >> 24;
+            const int dir = (er[3] >> 16) & 0xff, moff = er[3] >> 24;
+#pragma unroll
+            for (int k = 0; k < TPL; k++) {
+                const int t = l + k * G;
+                const int j = t / QW, q = t % QW;
+                if (has && t < NT && 2 * j + 1 >= y0 && 2 * j < y1 && 4 * q + 3 >= x0 && 4 * q < x1) {
+                    int lap[8];
+                    mc_vtask<W>(mid0, j, q, etv, kp, sh, lap);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const int x = 4 * q + (i & 3), y = 2 * j + (i >> 2);
+                        if (x >= x0 && x < x1 && y >= y0 && y < y1) {   // blend_px, src/mc_tmpl.c:640
+                            const int m = dspt_obmc[moff + (dir ? x : y)];
+                            ipv[k][i] = (ipv[k][i] * (64 - m) + clampi(lap[i], 0, bdmax) * m + 32) >> 6;
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < TPL; k++) {
+            const int t = l + k * G;
+            if (t < NT) emit(t / QW, t % QW, ipv[k]);
+        }
+    } else if (sc) {   // scaled references, second launch: put_8tap_scaled, or
+        // prep_8tap_scaled x2 + avg / w_avg (src/mc_tmpl.c:173-328; bilinear
+        // :452-585 as the (64 - 4m, 4m) bank, m = 0 the identity)
+        const uint8_t *rec = a.aux_pool + auxo;
+        const int nref = gld<int>(rec) & 3;
+        int16_t *mids = reinterpret_cast<int16_t *>(mid0);
+        const int fb_h = mc_bank(ftype & 3, bil, bw), fb_v = mc_bank(ftype >> 2, bil, bh);
+        int q0[TPL][8];
+#pragma unroll 1
+        for (int k = 0; k < 2; k++) {
+            wave_sync();
+            const bool act = k < nref;
+            const u32x4 rr = act ? gld<u32x4>(rec + 16 + 16 * k) : u32x4{0, 0, 0, 0};
+            const int smx = (int)(rr[1] & 0xffff), smy = (int)(rr[1] >> 16);
+            const int sdx = (int)(rr[2] & 0xffff), sdy = (int)(rr[2] >> 16);
+            const int r = u.p.inter.ref[k];
+            const int rs = pt.ref_stride[r * 3 + plane];
+            const P *org = pt.ref[r * 3 + plane] + (int)rr[0] - 3 * rs - 3;
+            const int rows = min((((H - 1) * sdy + smy) >> 10) + 8, 2 * H + 8);   // (bound: the LDS area)
+            const int hsh = 6 - ib, hrnd = (1 << hsh) >> 1;
+            if (act) {
+#pragma unroll 1
+                for (int it = l; it < rows * W; it += G) {
+                    const int row = it / W, x = it - row * W;
+                    const int pos = smx + x * sdx;
+                    const P *sp = org + row * rs + (pos >> 10);
+                    const uint2 tp = reinterpret_cast<const uint2 *>(dspt_mc8)[fb_h * 16 + ((pos & 1023) >> 6)];
+                    int acc = 0;
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+                        acc += __builtin_amdgcn_sbfe((int)(i < 4 ? tp.x : tp.y), 8 * (i & 3), 8) * (int)gld<P>(sp + i);
+                    mids[row * W + x] = (int16_t)((acc + hrnd) >> hsh);
+                }
+            }
+            wave_sync();
+#pragma unroll
+            for (int kt = 0; kt < TPL; kt++) {
+                const int t = l + kt * G;
+                if (!act || t >= NT) continue;
+                const int j = t / QW, qq = t % QW;
+                int pv[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int x = 4 * qq + (i & 3), y = 2 * j + (i >> 2);
+                    const int pos = smy + y * sdy;
+                    const uint2 tp = reinterpret_cast<const uint2 *>(dspt_mc8)[fb_v * 16 + ((pos & 1023) >> 6)];
+                    const int16_t *mc_ = mids + (pos >> 10) * W + x;
+                    int acc = 0;
+#pragma unroll
+                    for (int tt = 0; tt < 8; tt++)
+                        acc += __builtin_amdgcn_sbfe((int)(tt < 4 ? tp.x : tp.y), 8 * (tt & 3), 8) * (int)mc_[tt * W];
+                    pv[i] = acc;
+                }
+                if (nref == 1) {   // put: (sum + (32 << ib)) >> (6 + ib), clipped
+#pragma unroll
+                    for (int i = 0; i < 8; i++) pv[i] = clampi((pv[i] + (32 << ib)) >> (6 + ib), 0, bdmax);
+                    emit(j, qq, pv);
+                } else if (k == 0) {   // prep + PREP_BIAS of the first reference, kept
+#pragma unroll
+                    for (int i = 0; i < 8; i++) q0[kt][i] = (pv[i] + 32) >> 6;
+                } else {
+                    const int wt = u.p.inter.weight;   // 0: avg_c, 1..15: w_avg_c (src/mc_tmpl.c:587-620)
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const int p1 = (pv[i] + 32) >> 6;
+                        pv[i] = wt ? clampi((q0[kt][i] * wt + p1 * (16 - wt) + (8 << ib)) >> (ib + 4), 0, bdmax)
+                                   : clampi((q0[kt][i] + p1 + (1 << ib)) >> (ib + 1), 0, bdmax);
+                    }
+                    emit(j, qq, pv);
+                }
+            }
+        }
+    }
 }
 
 }  // namespace dgpu

@@ -145,6 +145,7 @@ struct Dav1dGpuRecorder {
     std::vector<Dav1dGpuIntraEdge> h_recs;
     std::vector<uint8_t> h_coef;
     PinnedBuf pin;   // units | recs | coefficients, copied in one sequential pass
+    PinnedBuf flag;  // the last flush's wavefront error word, copied back on its stream
     DevBuf d_units, d_recs, d_coef, d_edges, d_work;
     hipEvent_t done = nullptr;
     bool pending_check = false;   // the last flush's error word not read yet
@@ -170,6 +171,7 @@ extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
             (void)hipEventDestroy(r->done);
         }
         r->pin.release();
+        r->flag.release();
         r->d_units.release();
         r->d_recs.release();
         r->d_coef.release();
@@ -244,11 +246,9 @@ extern "C" int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int
 static int recorder_poll(Dav1dGpuRecorder *r) {
     if (!r->pending_check) return 0;
     r->pending_check = false;
-    int32_t flag = 0;
-    if (hipEventSynchronize(r->done) != hipSuccess ||
-        hipMemcpy(&flag, (const int32_t *)r->d_work.p + 1, 4, hipMemcpyDeviceToHost) != hipSuccess)
-        return -3;
-    return flag ? -6 : 0;
+    // the flush copied its error word to page-locked memory before `done`
+    if (hipEventSynchronize(r->done) != hipSuccess) return -3;
+    return *(volatile int32_t *)r->flag.p ? -6 : 0;
 }
 
 extern "C" int dav1d_gpu_recorder_status(Dav1dGpuRecorder *r) {
@@ -603,6 +603,10 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     lap("launch");
     if (rc) return rc;
     if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return -3;
+    // the wavefront's error word (workspace int32 [1]) follows on the stream
+    if (r->flag.grow(16) ||
+        hipMemcpyAsync(r->flag.p, (const int32_t *)r->d_work.p + 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return -3;
     if (hipEventRecord(r->done, st) != hipSuccess) return -3;
     r->pending_check = true;
     r->blocks.clear();

@@ -73,6 +73,12 @@ class FrameConfig:
     # emu_edge would read) instead of random pixels: then every footprint,
     # clamped or read from the padding, sees the same values
     edge_pad: bool = True
+    # prediction only (no inv_txfm_add) for every kind, and units of at most
+    # unit_split px per side cut from the prediction blocks instead of their
+    # transform blocks (0: transform blocks): the same blocks cut two ways
+    # must give the same picture (tests/test_cpu.py)
+    no_residual: bool = False
+    unit_split: int = 0
 
     @property
     def ref_pad(self):
@@ -220,6 +226,154 @@ def make_residuals(rng, tx, tw, th, bdmax, coef_dtype):
     return txtp, nzw, nzh, coef_off, coefs
 
 
+def _ext2_records(cfg, rng, units, pk, plane_u, ux, uy, tw, th, blk, bsz, lx, ly, ls, mv, ref_stride, planes):
+    """aux records of the "ext2" kinds (include/dav1d_gpu.h, Dav1dGpuPredKind):
+
+    * INTER_WMASK luma units / their chroma INTER_MASK units: the block's seg
+      mask at 4:2:0 resolution, (s/2)^2 bytes, written by the luma units
+      (w_mask_420) and read by the chroma ones (recon_tmpl.c:1854, :1900);
+      p.inter.weight = mask_sign.
+    * INTER_OBMC: the neighbour predictions of obmc() (recon_tmpl.c:1071-1133)
+      with the reference's geometry: above (when the block is not on the top
+      row; chroma only if bw + bh >= 16 plane pixels), up to min(log2 w4, 4)
+      inter neighbours of random widths, lap size ow4 x (oh4 * 3 + 3) >> 2,
+      blend_h over (v_mul * oh4 * 3) >> 2 rows with obmc_masks[v_mul * oh4];
+      left (not on the left column), blend_v over (h_mul * ow4 * 3) >> 2
+      columns with obmc_masks[h_mul * ow4]; each clipped to the unit.
+    * INTER_SCALED: per reference a step dx, dy in [256, 2048] and a 1/1024
+      phase; the unit's integer position and phase are the block's call's at
+      its top-left (running sums, src/mc_tmpl.c:182-199).  Positions are kept
+      inside the padded reference planes."""
+    n = len(units)
+    xr = np.random.default_rng(cfg.seed ^ 0xA2A2)
+    aux = np.zeros(n, np.int32)
+    chunks, off = [], 0
+
+    def put(rec):
+        nonlocal off
+        rec = np.asarray(rec, np.uint8)
+        pad = (-len(rec)) % 16
+        at = off
+        chunks.append(rec)
+        if pad:
+            chunks.append(np.zeros(pad, np.uint8))
+        off += len(rec) + pad
+        return at
+
+    nb = len(lx)
+    sign = xr.integers(0, 2, nb)
+    # ---- w_mask: one 4:2:0 mask chunk per block
+    wm_blk = np.unique(blk[pk == abi.PRED_INTER_WMASK])
+    chunk_at = {}
+    for b in wm_blk:
+        cs = int(ls[b]) // 2
+        chunk_at[b] = put(np.zeros(cs * cs, np.uint8))
+    for i in np.nonzero((pk == abi.PRED_INTER_WMASK) | ((pk == abi.PRED_INTER_MASK) & np.isin(blk, wm_blk)))[0]:
+        b = int(blk[i])
+        s_ = int(bsz[i])
+        bx0, by0 = (int(lx[b]) >> (1 if plane_u[i] else 0)), (int(ly[b]) >> (1 if plane_u[i] else 0))
+        if plane_u[i] == 0:
+            aux[i] = chunk_at[b] + ((int(uy[i]) - by0) >> 1) * (s_ >> 1) + ((int(ux[i]) - bx0) >> 1)
+            units["weight"][i] = sign[b]
+        else:
+            aux[i] = chunk_at[b] + (int(uy[i]) - by0) * s_ + (int(ux[i]) - bx0)
+    # ---- OBMC: block-level neighbour lists, then per unit the clipped entries
+    nb_list = {}
+    for b in np.unique(blk[pk == abi.PRED_INTER_OBMC]):
+        bw4 = int(ls[b]) // 4
+        lw = bw4.bit_length() - 1          # dav1d_block_dimensions[bs][2] (square blocks)
+        ents = {"top": [], "left": []}
+        if ly[b] > 0:
+            x = 0
+            while x < bw4 and len(ents["top"]) < min(lw, 4):
+                step4 = int(np.clip(1 << int(xr.integers(1, 5)), 2, 16))
+                if xr.random() < 0.8:
+                    ents["top"].append((x, step4, xr.integers(-48 * 16, 48 * 16 + 1, 2), int(xr.integers(0, 10)),
+                                        int(xr.integers(0, 2))))
+                x += step4
+        if lx[b] > 0:
+            y = 0
+            while y < bw4 and len(ents["left"]) < min(lw, 4):
+                step4 = int(np.clip(1 << int(xr.integers(1, 5)), 2, 16))
+                if xr.random() < 0.8:
+                    ents["left"].append((y, step4, xr.integers(-48 * 16, 48 * 16 + 1, 2), int(xr.integers(0, 10)),
+                                         int(xr.integers(0, 2))))
+                y += step4
+        nb_list[b] = ents
+    for i in np.nonzero(pk == abi.PRED_INTER_OBMC)[0]:
+        b, p = int(blk[i]), int(plane_u[i])
+        sub = 1 if p else 0
+        hm = vm = 4 >> sub                 # h_mul, v_mul (4:2:0)
+        bw4 = int(ls[b]) // 4
+        bx0, by0 = int(lx[b]) >> sub, int(ly[b]) >> sub
+        ox, oy = int(ux[i]) - bx0, int(uy[i]) - by0   # the unit in the block
+        w_, h_ = int(tw[i]), int(th[i])
+        rs = int(ref_stride[p])
+        rec = []
+        regions = []
+        if not p or bw4 * hm + bw4 * vm >= 16:
+            for (x, step4, m_, f2d, r) in nb_list[b]["top"]:
+                ow4, oh4 = min(step4, bw4), min(bw4, 16) >> 1
+                regions.append((0, x * hm, x * hm + ow4 * hm, 0, (vm * oh4 * 3) >> 2, ow4, (oh4 * 3 + 3) >> 2,
+                                vm * oh4, m_, f2d, r))
+        for (y, step4, m_, f2d, r) in nb_list[b]["left"]:
+            ow4, oh4 = min(bw4, 16) >> 1, min(step4, bw4)
+            regions.append((1, 0, (hm * ow4 * 3) >> 2, y * vm, y * vm + oh4 * vm, ow4, oh4, hm * ow4, m_, f2d, r))
+        for (dr, xa, xb, ya, yb, lw4, lh4, mbase, m_, f2d, r) in regions:
+            x0, x1 = max(xa - ox, 0), min(xb - ox, w_)
+            y0, y1 = max(ya - oy, 0), min(yb - oy, h_)
+            if x0 >= x1 or y0 >= y1:
+                continue
+            mvx, mvy = (int(m_[0]) >> 1, int(m_[1]) >> 1) if p else (int(m_[0]), int(m_[1]))
+            soff = (int(uy[i]) + (mvy >> 4)) * rs + int(ux[i]) + (mvx >> 4)
+            e = np.zeros(16, np.uint8)
+            e[0:4] = np.array([soff], "<i4").view(np.uint8)
+            # lap call size in plane pixels / 4 (its filter banks)
+            # lap size in 4-px units (2 px -> 0: both mean "<= 4", the 4-tap bank)
+            e[4:16] = [mvx & 15, mvy & 15, f2d, r, x0, y0, x1, y1, (lw4 * hm) // 4, (lh4 * vm) // 4, dr,
+                       mbase + (ox if dr else oy)]
+            rec.append(e)
+        hdr = np.zeros(16, np.uint8)
+        hdr[0:4] = np.array([len(rec)], "<i4").view(np.uint8)
+        aux[i] = put(np.concatenate([hdr] + rec))
+    # ---- scaled references
+    pad = cfg.ref_pad
+    nref_b = xr.integers(1, 3, nb)
+    wt_b = np.where(xr.random(nb) < 0.5, 0, xr.integers(1, 16, nb))
+    steps = xr.integers(256, 2049, size=(nb, 2, 2))
+    phase = xr.integers(0, 1024, size=(nb, 2, 2))
+    for i in np.nonzero(pk == abi.PRED_INTER_SCALED)[0]:
+        b, p = int(blk[i]), int(plane_u[i])
+        sub = 1 if p else 0
+        pw, ph = planes[p]
+        s_ = int(bsz[i])
+        bx0, by0 = int(lx[b]) >> sub, int(ly[b]) >> sub
+        ox, oy = int(ux[i]) - bx0, int(uy[i]) - by0
+        rs = int(ref_stride[p])
+        recs = []
+        for k in range(int(nref_b[b])):
+            dx, dy = int(steps[b, k, 0]), int(steps[b, k, 1])
+            mx0, my0 = int(phase[b, k, 0]), int(phase[b, k, 1])
+            mvx, mvy = int(mv[b, k, 0]) >> 4 >> sub, int(mv[b, k, 1]) >> 4 >> sub
+            # the block's integer origin, kept so its footprint stays inside
+            # the padded plane: columns origin - 3 .. origin + ((s-1)dx+mx)>>10 + 4
+            span_x, span_y = ((s_ - 1) * dx + mx0) >> 10, ((s_ - 1) * dy + my0) >> 10
+            gx = int(np.clip(bx0 + mvx, -pad + 4, pw + pad - 6 - span_x))
+            gy = int(np.clip(by0 + mvy, -pad + 4, ph + pad - 6 - span_y))
+            px_, py_ = mx0 + ox * dx, my0 + oy * dy
+            ex = gx + (px_ >> 10)
+            ey = gy + (py_ >> 10)
+            r = np.zeros(16, np.uint8)
+            r[0:4] = np.array([ey * rs + ex], "<i4").view(np.uint8)
+            r[4:12] = np.array([px_ & 1023, py_ & 1023, dx, dy], "<u2").view(np.uint8)
+            recs.append(r)
+        hdr = np.zeros(16, np.uint8)
+        hdr[0:4] = np.array([len(recs)], "<i4").view(np.uint8)
+        aux[i] = put(np.concatenate([hdr] + recs))
+        units["weight"][i] = wt_b[b] if len(recs) == 2 else 0
+    return aux, (np.concatenate(chunks) if chunks else np.zeros(16, np.uint8))
+
+
 def make_frame(cfg: FrameConfig) -> FrameData:
     rng = np.random.default_rng(cfg.seed)
     W, H = cfg.width, cfg.height
@@ -252,6 +406,13 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         kind = np.select([e < 0.18, e < 0.30, e < 0.44, e < 0.58, e < 0.74, e < 0.88],
                          [abi.PRED_INTER, abi.PRED_INTER_AVG, abi.PRED_INTER_WAVG, abi.PRED_INTER_MASK,
                           abi.PRED_PAL, abi.PRED_WARP], abi.PRED_INTER_INTRA)
+    elif cfg.kind == "ext2":
+        # the second launch's reference-semantics kinds: w_mask compound
+        # (COMP_INTER_SEG), OBMC and scaled references, beside plain put
+        rng.random(nb)
+        e = np.random.default_rng(cfg.seed ^ 0xE2E2).random(nb)
+        kind = np.select([e < 0.3, e < 0.6, e < 0.9], [abi.PRED_INTER_WMASK, abi.PRED_INTER_OBMC,
+                                                       abi.PRED_INTER_SCALED], abi.PRED_INTER)
     elif cfg.kind in ("ipred", "itx"):
         rng.random(nb)   # keep the later draws aligned with "full"
         kind = np.full(nb, abi.PRED_INTRA if cfg.kind == "ipred" else abi.PRED_NONE)
@@ -282,11 +443,13 @@ def make_frame(cfg: FrameConfig) -> FrameData:
             s = int(bs[b])
             if cfg.kind == "mc":
                 tw = th = min(s, cfg.mc_split)
+            elif cfg.unit_split:
+                tw = th = min(s, cfg.unit_split)
             else:
                 cands = _tx_candidates(s, cfg.tx64)
                 if kind[b] == abi.PRED_WARP and plane == 0:   # warp units are whole 8x8s
                     cands = [c for c in cands if min(c) >= 8]
-                if kind[b] == abi.PRED_INTER_INTRA:   # second launch: no 64-point class
+                if kind[b] in abi.SECOND_LAUNCH_KINDS:   # second launch: no 64-point class
                     cands = [c for c in cands if max(c) <= 32]
                 tw, th = cands[(b * 7 + plane * 3 + int(rng.integers(0, 1 << 20))) % len(cands)]
                 if plane > 0 and cfl_blk[b]:
@@ -318,6 +481,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     units["plane"] = plane_u
     pk = kind[blk].copy()
     pk[(pk == abi.PRED_WARP) & (plane_u > 0)] = abi.PRED_INTER   # chroma of warped blocks: translation
+    # chroma of COMP_INTER_SEG blocks: mask_c on the luma's seg mask (recon_tmpl.c:1900)
+    pk[(pk == abi.PRED_INTER_WMASK) & (plane_u > 0)] = abi.PRED_INTER_MASK
     cfl = (plane_u > 0) & cfl_blk[blk]
     pk[cfl] = abi.PRED_CFL
     units["pred"] = pk
@@ -325,7 +490,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     units["bh4"] = bsz // 4
 
     # inter parameters
-    inter = np.isin(pk, abi.INTER_KINDS + (abi.PRED_INTER_INTRA,))
+    inter = np.isin(pk, abi.INTER_KINDS + (abi.PRED_INTER_INTRA, abi.PRED_INTER_WMASK, abi.PRED_INTER_OBMC,
+                         abi.PRED_INTER_SCALED))
     ref_stride = np.array([refs[0][p].shape[1] for p in range(3)])
     src_xy = np.zeros((n, 2, 2), np.int32)
     for k in range(2):
@@ -411,6 +577,10 @@ def make_frame(cfg: FrameConfig) -> FrameData:
             off += len(rec) + (-len(rec)) % 16
             chunks.append(np.zeros((-len(rec)) % 16, np.uint8))
 
+    if cfg.kind == "ext2":
+        aux, aux_pool = _ext2_records(cfg, rng, units, pk, plane_u, ux, uy, tw, th, blk, bsz, lx, ly, ls, mv,
+                                      ref_stride, planes)
+
     # intra parameters
     intra = pk == abi.PRED_INTRA
     m = mode[blk]
@@ -470,7 +640,7 @@ def make_frame(cfg: FrameConfig) -> FrameData:
     edges = rng.integers(0, bdmax + 1, size=max(int(edge_len.sum()), 1), dtype=cfg.pixel_dtype)
 
     # transform types, coefficient regions and coefficients
-    if cfg.kind in ("mc", "ipred"):
+    if cfg.kind in ("mc", "ipred") or cfg.no_residual:
         units["txtp"] = abi.NO_RESIDUAL
         coefs = np.zeros(1, cfg.coef_dtype)
     else:
@@ -541,8 +711,9 @@ def algorithmic_bytes(fd: FrameData):
     first = first[inter[first]]
     src = np.zeros(len(u), np.int64)
     for k in range(2):
-        use = np.isin(u["pred"], (abi.PRED_INTER, abi.PRED_INTER_INTRA)) if k == 0 else np.zeros(len(u), bool)
-        use = use | np.isin(u["pred"], abi.COMPOUND_KINDS)
+        use = np.isin(u["pred"], (abi.PRED_INTER, abi.PRED_INTER_INTRA, abi.PRED_INTER_OBMC,
+                                  abi.PRED_INTER_SCALED)) if k == 0 else np.zeros(len(u), bool)
+        use = use | np.isin(u["pred"], abi.COMPOUND_KINDS + (abi.PRED_INTER_WMASK,))
         mx, my = u[f"mx{k}"], u[f"my{k}"]
         fh = np.where(mx > 0, np.where(bw > 4, 7, 3), 0)
         fv = np.where(my > 0, np.where(bh > 4, 7, 3), 0)

@@ -260,6 +260,53 @@ enum Dav1dGpuPredKind {
                                 uint8 mode, uint8 0, uint16 angle, int32
                                 mask_off (aux_pool offset of the unit's
                                 top-left mask value, stride bw4 * 4)         */
+    DGPU_PRED_INTER_WMASK = 10,/* COMP_INTER_SEG luma: mct x2 -> w_mask_c
+                                (src/mc_tmpl.c:683-740, recon_tmpl.c:1854),
+                                ref[0] = tmp[mask_sign], ref[1] = the other;
+                                p.inter.weight = mask_sign.  The unit WRITES
+                                its part of the block's seg mask at the chroma
+                                layout's resolution (cfl_ss below): aux[unit]
+                                = aux_pool offset of the unit's top-left mask
+                                value, row stride (bw4 * 4) >> ss_hor.  The
+                                block's chroma units are INTER_MASK units on
+                                that mask (recon_tmpl.c:1900); they may share
+                                the batch: WMASK units run in the second
+                                launch, which completes first               */
+    DGPU_PRED_INTER_OBMC = 11,/* overlapped block MC (obmc(), recon_tmpl.c:
+                                1071-1133): mc put from ref 0, then for every
+                                neighbour prediction overlapping the unit the
+                                neighbour's put (the lap call) blended in:
+                                blend_h for the ones above, then blend_v for
+                                the ones to the left (src/mc_tmpl.c:655-681).
+                                aux[unit] = offset of a 16-byte aligned record:
+                                int32 n, 12 pad bytes, then n entries of 16 B:
+                                  int32 src_off (ref-plane offset of the
+                                    integer position of unit pixel (0, 0)
+                                    under the neighbour's mv),
+                                  uint8 mx, my, filter2d, ref,
+                                  uint8 x0, y0, x1, y1 (the overlap, unit
+                                    pixels, [x0, x1) x [y0, y1)),
+                                  uint8 lap_w4, lap_h4 (the lap call's size:
+                                    its filter banks, src/mc_tmpl.c:99-107),
+                                  uint8 dir (0 above: mask by row; 1 left:
+                                    by column),
+                                  uint8 mask_off (the mask value of unit row
+                                    / column i is dav1d_obmc_masks[mask_off
+                                    + i]);
+                                entries above first, in decode order        */
+    DGPU_PRED_INTER_SCALED = 12,/* references of another size (mc() with
+                                refp->p.p.w != f->cur.p.w, recon_tmpl.c:
+                                1006-1060): put_8tap_scaled (one ref) or
+                                prep_8tap_scaled x2 + avg / w_avg
+                                (p.inter.weight 0 = avg, 1..15 = jnt weight;
+                                src/mc_tmpl.c:173-328, bilinear :452-585).
+                                aux[unit] = offset of a 16-byte aligned
+                                record: int32 n_refs (1 or 2), 12 pad bytes,
+                                then per ref 16 B: int32 src_off (ref-plane
+                                offset of the integer source position of
+                                unit pixel (0, 0)), uint16 mx, my (its
+                                1/1024 phase, 0..1023), uint16 dx, dy (the
+                                steps, 1..2048), 4 pad bytes                 */
 };
 
 /* txtp value of a prediction-only unit (no inv_txfm_add): mc-only batches */
@@ -339,14 +386,17 @@ typedef struct Dav1dGpuFrameBatch {
     Dav1dGpuPlane cfl_luma; /* luma that CFL units read (the reconstructed
                              luma of the same blocks); must not be a plane
                              this batch writes: units run unordered          */
-    int32_t  cfl_ss;      /* chroma subsampling of CFL units: ss_hor |
-                             ss_ver << 1 (3 = 4:2:0, 1 = 4:2:2, 0 = 4:4:4)  */
+    int32_t  cfl_ss;      /* chroma subsampling of the frame (CFL units'
+                             luma, INTER_WMASK masks): ss_hor | ss_ver << 1
+                             (3 = 4:2:0, 1 = 4:2:2, 0 = 4:4:4)              */
     const int32_t *aux;   /* device, one int32 per unit (by unit index): the
                              aux_pool byte offset of an INTER_MASK unit's
                              mask or a PAL unit's palette record; only those
                              kinds read it (may be NULL without them)      */
-    const void *aux_pool; /* device pool of masks (u8) / palette records   */
-    int32_t  class_warp[DGPU_N_RECT_TX_SIZES]; /* WARP and INTER_INTRA units
+    const void *aux_pool; /* device pool of masks (u8) / palette records;
+                             INTER_WMASK units write their masks into it    */
+    int32_t  class_warp[DGPU_N_RECT_TX_SIZES]; /* WARP, INTER_INTRA, INTER_
+                             WMASK, INTER_OBMC and INTER_SCALED units
                              at the end of each class range (units sorted
                              so); they run in a second launch whose kernel
                              keeps their registers out of the main kernel.

@@ -147,8 +147,9 @@ static void prep_8tap(int16_t *tmp, const pixel *src, ptrdiff_t src_stride,
  * ((mx + x*dx) & 1023) >> 6; rows likewise with my/dy. */
 static void scaled_8tap(pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
                         const pixel *src, ptrdiff_t src_stride, int w, int h,
-                        int mx, int my, int dx, int dy, int ftype, int bdmax)
-{
+                        int mx, int my, int dx, int dy, int ftype, int bw, int bh, int bdmax)
+{   /* bw / bh: the call's w / h the 4-tap bank choice follows (GET_H_FILTER /
+     * GET_V_FILTER, :99-108); a unit inside a block passes the block's */
     const int ib = IBITS(bdmax);
     const ptrdiff_t ss = PX(src_stride), ds = PX(dst_stride);
     const int rows = (((h - 1) * dy + my) >> 10) + 8;
@@ -157,7 +158,7 @@ static void scaled_8tap(pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
         const pixel *s = &src[(r - 3) * ss];
         for (int x = 0; x < w; x++) {
             const int pos = mx + x * dx;
-            const int8_t *fh = kern8(ftype & 3, (pos & 1023) >> 6, w);
+            const int8_t *fh = kern8(ftype & 3, (pos & 1023) >> 6, bw);
             const int off = pos >> 10;
             mid[r * 128 + x] = fh ? rshift_rnd(taps8(&s[off], 1, fh), 6 - ib) : s[off] << ib;
         }
@@ -165,7 +166,7 @@ static void scaled_8tap(pixel *dst, ptrdiff_t dst_stride, int16_t *tmp,
     for (int y = 0; y < h; y++) {
         const int pos = my + y * dy;
         const int16_t *m = &mid[((pos >> 10) + 3) * 128];
-        const int8_t *fv = kern8(ftype >> 2, (pos & 1023) >> 6, h);
+        const int8_t *fv = kern8(ftype >> 2, (pos & 1023) >> 6, bh);
         for (int x = 0; x < w; x++) {
             if (dst) {
                 dst[y * ds + x] = fv ? clampi(rshift_rnd(taps8_i16(&m[x], 128, fv), 6 + ib), 0, bdmax)
@@ -735,11 +736,11 @@ static void prep_##name(int16_t *t, const pixel *s, ptrdiff_t ss,               
 static void put_scaled_##name(pixel *d, ptrdiff_t ds, const pixel *s,           \
                               ptrdiff_t ss, int w, int h, int mx, int my,       \
                               int dx, int dy BDPARAM)                           \
-{ BD_DECL scaled_8tap(d, ds, NULL, s, ss, w, h, mx, my, dx, dy, ft, bdmax_); }  \
+{ BD_DECL scaled_8tap(d, ds, NULL, s, ss, w, h, mx, my, dx, dy, ft, w, h, bdmax_); }  \
 static void prep_scaled_##name(int16_t *t, const pixel *s, ptrdiff_t ss,        \
                                int w, int h, int mx, int my, int dx, int dy     \
                                BDPARAM)                                         \
-{ BD_DECL scaled_8tap(NULL, 0, t, s, ss, w, h, mx, my, dx, dy, ft, bdmax_); }
+{ BD_DECL scaled_8tap(NULL, 0, t, s, ss, w, h, mx, my, dx, dy, ft, w, h, bdmax_); }
 
 /* filter_type = type_h | type_v << 2, REGULAR 0 / SMOOTH 1 / SHARP 2 */
 MC_WRAPPERS(regular,        0 | 0 << 2)
@@ -1437,9 +1438,10 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
         const ptrdiff_t ds = b->dst[pl].stride;
         pixel *dst = (pixel *)b->dst[pl].data + u->dst_off;
         if (u->pred == DGPU_PRED_INTER || u->pred == DGPU_PRED_INTER_AVG ||
-            u->pred == DGPU_PRED_INTER_WAVG || u->pred == DGPU_PRED_INTER_MASK) {
+            u->pred == DGPU_PRED_INTER_WAVG || u->pred == DGPU_PRED_INTER_MASK ||
+            u->pred == DGPU_PRED_INTER_WMASK || u->pred == DGPU_PRED_INTER_OBMC) {
             const int f2d = u->p.inter.filter2d;
-            const int comp = u->pred != DGPU_PRED_INTER;
+            const int comp = u->pred != DGPU_PRED_INTER && u->pred != DGPU_PRED_INTER_OBMC;
             for (int k = 0; k <= comp; k++) {
                 const int r = u->p.inter.ref[k];
                 const pixel *src = (const pixel *)b->ref[r][pl].data + u->p.inter.src_off[k];
@@ -1463,6 +1465,49 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
                 for (int y = 0; y < h; y++)
                     for (int x = 0; x < w; x++) m[y * w + x] = ms[y * (u->bw4 * 4) + x];
                 avg_blend(dst, ds, t1, t2, w, h, 2, 0, m, bdmax);
+            } else if (u->pred == DGPU_PRED_INTER_WMASK) {
+                /* COMP_INTER_SEG luma (src/recon_tmpl.c:1854): w_mask_c over
+                 * the unit -- pointwise per 2x2, so the block's call
+                 * restricted to it -- and its mask values stored into the
+                 * block's mask, row stride bw >> ss_hor */
+                const int ssh = b->cfl_ss & 1, ssv = (b->cfl_ss >> 1) & 1;
+                uint8_t m[64 * 64];
+                w_mask(dst, ds, t1, t2, w, h, m, u->p.inter.weight, ssh, ssv, bdmax);
+                uint8_t *mo = (uint8_t *)b->aux_pool + b->aux[i];
+                const int mw = w >> ssh, mstride = (u->bw4 * 4) >> ssh;
+                for (int y = 0; y < (h >> ssv); y++) memcpy(mo + y * mstride, m + y * mw, mw);
+            } else if (u->pred == DGPU_PRED_INTER_OBMC) {
+                /* obmc() (src/recon_tmpl.c:1071-1133) on the unit: after the
+                 * block's put, every neighbour prediction overlapping it --
+                 * the lap mc() call of :1100 / :1122 on the overlap, with the
+                 * lap call's size for its filter banks -- blended as
+                 * blend_h / blend_v do (src/mc_tmpl.c:655-681), with the
+                 * mask value of the pixel's block row / column */
+                const uint8_t *rec = (const uint8_t *)b->aux_pool + b->aux[i];
+                int32_t ne;
+                memcpy(&ne, rec, 4);
+                for (int e = 0; e < ne; e++) {
+                    const uint8_t *er = rec + 16 + 16 * e;
+                    int32_t soff;
+                    memcpy(&soff, er, 4);
+                    const int emx = er[4], emy = er[5], ef2d = er[6], eref = er[7];
+                    const int x0 = er[8], y0 = er[9], x1 = er[10], y1 = er[11];
+                    const int lw = er[12] * 4, lh = er[13] * 4, dir = er[14], moff = er[15];
+                    const int rw = x1 - x0, rh = y1 - y0;
+                    if (rw <= 0 || rh <= 0) continue;
+                    const ptrdiff_t ess = b->ref[eref][pl].stride;
+                    const pixel *esrc = (const pixel *)b->ref[eref][pl].data + soff + y0 * PX(ess) + x0;
+                    pixel lap[64 * 64];
+                    if (ef2d == DGPU_FILTER_2D_BILINEAR)
+                        bilin_mc(lap, rw * sizeof(pixel), NULL, esrc, ess, rw, rh, emx, emy, bdmax);
+                    else
+                        put_8tap(lap, rw * sizeof(pixel), esrc, ess, rw, rh, emx, emy, ftype_of[ef2d], lw, lh, bdmax);
+                    for (int y = y0; y < y1; y++)
+                        for (int x = x0; x < x1; x++) {
+                            pixel *d = &dst[y * PX(ds) + x];
+                            *d = (pixel)blend_px(*d, lap[(y - y0) * rw + (x - x0)], dspt_obmc[moff + (dir ? x : y)]);
+                        }
+                }
             }
         } else if (u->pred == DGPU_PRED_INTER_INTRA) {
             /* recon_b_inter's inter-intra (src/recon_tmpl.c:1540-1580): the
@@ -1494,6 +1539,39 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
                     const int m = mk[y * (u->bw4 * 4) + x];
                     *d = (pixel)((*d * (64 - m) + tile[y * w + x] * m + 32) >> 6);
                 }
+        } else if (u->pred == DGPU_PRED_INTER_SCALED) {
+            /* mc() with a reference of another size (src/recon_tmpl.c:
+             * 1006-1060): put_8tap_scaled, or prep_8tap_scaled x2 + avg /
+             * w_avg, from the unit's own integer position and 1/1024 phase
+             * (the block's call restricted to the unit: a column's position
+             * is mx + x * dx, a row's my + y * dy, as the reference's running
+             * sums compute them); the 4-tap banks follow the block size */
+            const uint8_t *rec = (const uint8_t *)b->aux_pool + b->aux[i];
+            int32_t nref;
+            memcpy(&nref, rec, 4);
+            nref &= 3;
+            const int f2d = u->p.inter.filter2d;
+            for (int k = 0; k < nref; k++) {
+                const uint8_t *rr = rec + 16 + 16 * k;
+                int32_t soff;
+                uint16_t sm[4];
+                memcpy(&soff, rr, 4);
+                memcpy(sm, rr + 4, 8);
+                const int r = u->p.inter.ref[k];
+                const pixel *src = (const pixel *)b->ref[r][pl].data + soff;
+                const ptrdiff_t ss = b->ref[r][pl].stride;
+                pixel *pd = nref == 1 ? dst : NULL;
+                int16_t *pt = nref == 1 ? NULL : (k ? t2 : t1);
+                if (f2d == DGPU_FILTER_2D_BILINEAR)
+                    bilin_scaled(pd, ds, pt, src, ss, w, h, sm[0], sm[1], sm[2], sm[3], bdmax);
+                else
+                    scaled_8tap(pd, ds, pt, src, ss, w, h, sm[0], sm[1], sm[2], sm[3], ftype_of[f2d], u->bw4 * 4,
+                                u->bh4 * 4, bdmax);
+            }
+            if (nref == 2) {
+                if (u->p.inter.weight) avg_blend(dst, ds, t1, t2, w, h, 1, u->p.inter.weight, NULL, bdmax);
+                else avg_blend(dst, ds, t1, t2, w, h, 0, 0, NULL, bdmax);
+            }
         } else if (u->pred == DGPU_PRED_WARP) {
             /* recon_tmpl.c warp_affine (:1063-1100): warp8x8 for each 8x8 of
              * the unit with its own source position and mx / my */

@@ -110,6 +110,10 @@ class HostFrame:
         fn = L.oracle_recon_units_8bpc if self.fd.cfg.bpc == 8 else L.oracle_recon_units_16bpc
         if u1 is None:
             u1 = self.fd.n_units
+        # INTER_WMASK units write the seg masks their blocks' chroma units
+        # read: run them first (re-running them below is idempotent)
+        for i in np.nonzero(self.units["pred"][u0:u1] == _abi().PRED_INTER_WMASK)[0]:
+            fn(ctypes.byref(self.batch), int(u0 + i), int(u0 + i + 1))
         if threads <= 1:
             fn(ctypes.byref(self.batch), u0, u1)
             return

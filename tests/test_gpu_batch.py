@@ -126,7 +126,8 @@ def test_smoke_entry():
 
 @pytest.mark.parametrize("kind,bpc,bdmax", [("ipred", 8, 255), ("itx", 8, 255), ("ipred", 16, 1023),
                                             ("itx", 16, 4095), ("ext", 8, 255), ("ext", 16, 1023),
-                                            ("ext", 16, 4095)])
+                                            ("ext", 16, 4095), ("ext2", 8, 255), ("ext2", 16, 1023),
+                                            ("ext2", 16, 4095)])
 def test_batch_family(pkg, oracle, kind, bpc, bdmax):
     """The per-family frames of the bench breakdown: intra/CfL prediction
     only, inv_txfm_add onto an existing picture (PRED_NONE: the kernel's
@@ -165,3 +166,27 @@ def test_batch_ragged_subsets(pkg, oracle, kind):
         sub.blk = fd.blk[keep]
         sub.stats = wl.algorithmic_bytes(sub)
         _check(sub, oracle)
+
+
+@pytest.mark.parametrize("bpc,bdmax,seed", [(8, 255, 71), (16, 1023, 72), (16, 4095, 73)])
+def test_batch_ext2_masks_and_cut(pkg, oracle, bpc, bdmax, seed):
+    """The second launch's kinds (w_mask compound writing the seg mask its
+    chroma INTER_MASK units read, OBMC, scaled references): the picture and
+    the device-written seg masks equal the oracle's; prediction-only units
+    cut from transform blocks and from whole blocks agree on the device."""
+    import torch
+    import dav1d_mirror_amd.batch as bt
+    fd = _frame(pkg, width=512, height=256, bpc=bpc, bitdepth_max=bdmax, kind="ext2", seed=seed)
+    dev = _check(fd, oracle)
+    hf = oracle.HostFrame(fd)
+    hf.run()
+    assert np.array_equal(dev.aux_pool.cpu().numpy(), hf.aux_pool)
+    pics = []
+    for split in (0, 32):
+        f = _frame(pkg, width=512, height=256, bpc=bpc, bitdepth_max=bdmax, kind="ext2", seed=seed,
+                   no_residual=True, unit_split=split)
+        d = bt.DeviceFrame(f, "cuda:0")
+        d.launch()
+        torch.cuda.synchronize()
+        pics.append(d.planes_host())
+    assert all(np.array_equal(a, b) for a, b in zip(*pics))

@@ -38,7 +38,6 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         ftrace127) TUS="recon_ie8" build ftrace127 -DDGPU_FLOW_TRACE=1 -DDGPU_FLOW_SLEEP=127 ;;
         fsleep32) TUS="recon_ie8" build fsleep32 -DDGPU_FLOW_SLEEP=32 ;;
         fsleep127) TUS="recon_ie8" build fsleep127 -DDGPU_FLOW_SLEEP=127 ;;
-        ntmeta) build ntmeta -DDGPU_NT_META=1 ;;
         nomc) build nomc -DDGPU_ABL_MC=1 ;;
         nostore) build nostore -DDGPU_ABL_STORE=1 ;;
         noitx) build noitx -DDGPU_ABL_ITX=1 ;;
