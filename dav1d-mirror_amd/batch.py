@@ -133,9 +133,7 @@ class DeviceTiles:
         self.aux_pool = up(td.aux_pool) if td.aux_pool is not None else None
         self.refs = [[up(a if not hbd else a.view(np.int16)) for a in rp] for rp in fd.refs]
         self.cfl_luma = up(fd.cfl_luma if not hbd else fd.cfl_luma.view(np.int16))
-        if dst_planes is not None:
-            self.dst = list(dst_planes)
-        elif fd.dst_init is not None:
+        if fd.dst_init is not None:
             self.dst = [up(a if not hbd else a.view(np.int16)) for a in fd.dst_init]
         else:
             self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fd.plane_wh]

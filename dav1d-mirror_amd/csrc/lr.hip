@@ -66,21 +66,51 @@ __device__ __forceinline__ int lr_tmp(const LrArgs<BPC> &a, int r, int c) {
     return x < 0 && a.left ? a.left[(a.h - 1) * 4 + x + 4] : a.src[(ptrdiff_t)(a.h - 1) * a.ss + x];
 }
 
-// A / B of selfguided_filter (:373-392) at unit position (j, i) for box
-// radius R (n = 25 or 9), from the tile (columns relative to the strip)
+// Vertical box sums of radius R for selfguided_filter's box_sum (:373-376):
+// VS[jj][c] = sum of tile column c over the 2R + 1 rows around unit row
+// jj - 1, VQ the same of the squares, for jj = 0..h + 1 and every tile
+// column.  A thread runs down a chunk of one column with a running sum (two
+// reads per row instead of 2R + 1).
+constexpr int kLrVH = 66;   // rows of the vertical sums: unit rows -1..64
 template <int R>
-__device__ __forceinline__ void lr_ab(const int (*T)[kLrTW], int j, int il, unsigned s, int bd8, int &A, int &B) {
+__device__ __forceinline__ void lr_vsums(const int (*T)[kLrTW], int (*VS)[kLrTW], int (*VQ)[kLrTW], int h, int sw) {
+    constexpr int CH = 11;   // rows per chunk
+    const int ncol = sw + 6, nrow = h + 2, nchunk = (nrow + CH - 1) / CH;
+    for (int t = threadIdx.x; t < ncol * nchunk; t += 256) {
+        const int ck = t / ncol, c = t - ck * ncol;
+        const int jj0 = ck * CH, jj1 = min(jj0 + CH, nrow);
+        int s = 0, q = 0;   // tile rows jj + 2 - R .. jj + 2 + R (unit row jj - 1 is tile row jj + 2)
+#pragma unroll
+        for (int d = -R; d <= R; d++) {
+            const int v = T[jj0 + 2 + d][c];
+            s += v;
+            q += v * v;
+        }
+        VS[jj0][c] = s;
+        VQ[jj0][c] = q;
+        for (int jj = jj0 + 1; jj < jj1; jj++) {
+            const int vi = T[jj + 2 + R][c], vo = T[jj + 1 - R][c];
+            s += vi - vo;
+            q += vi * vi - vo * vo;
+            VS[jj][c] = s;
+            VQ[jj][c] = q;
+        }
+    }
+}
+
+// A / B of selfguided_filter (:373-392) at unit position (jj - 1, ii - 1)
+// for box radius R (n = 25 or 9): the horizontal sum of the vertical sums
+template <int R>
+__device__ __forceinline__ void lr_ab(const int (*VS)[kLrTW], const int (*VQ)[kLrTW], int jj, int ii, unsigned s,
+                                     int bd8, int &A, int &B) {
     constexpr int n = (2 * R + 1) * (2 * R + 1);
     constexpr unsigned one_by_x = n == 25 ? 164 : 455;
     int sum = 0, sumsq = 0;
 #pragma unroll
-    for (int dy = -R; dy <= R; dy++)
-#pragma unroll
-        for (int dx = -R; dx <= R; dx++) {
-            const int v = T[j + 3 + dy][il + 3 + dx];
-            sum += v;
-            sumsq += v * v;
-        }
+    for (int dx = -R; dx <= R; dx++) {
+        sum += VS[jj][ii + 2 + dx];
+        sumsq += VQ[jj][ii + 2 + dx];
+    }
     const int a = (sumsq + ((1 << (2 * bd8)) >> 1)) >> (2 * bd8);
     const int b = (sum + ((1 << bd8) >> 1)) >> bd8;
     const unsigned p = (unsigned)max(a * n - b * b, 0);
@@ -97,7 +127,12 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     using C = typename Px<BPC>::coef;
     __shared__ int T[kLrTH][kLrTW];
     __shared__ int AB[2][66][kLrSW + 2];   // A, B at unit rows -1..h, strip columns -1..sw
-    __shared__ int HOR[kLrTH][kLrSW];
+    // Wiener's horizontal pass, or the self-guided vertical box sums
+    __shared__ int SCR[2 * kLrVH * kLrTW];
+    int(*HOR)[kLrSW] = reinterpret_cast<int(*)[kLrSW]>(SCR);
+    int(*VS)[kLrTW] = reinterpret_cast<int(*)[kLrTW]>(SCR);
+    int(*VQ)[kLrTW] = reinterpret_cast<int(*)[kLrTW]>(SCR + kLrVH * kLrTW);
+    static_assert(kLrTH * kLrSW <= 2 * kLrVH * kLrTW, "HOR fits the scratch");
     const int sw = min(kLrSW, a.w - x0), h = a.h;
     const int bd8 = bits_of(a.bdmax) - 8;
     for (int k = threadIdx.x; k < (h + 6) * (sw + 6); k += 256) {
@@ -134,13 +169,16 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     for (int pass = 0; pass < 2; pass++) {
         const bool five = pass == 0;
         if (five ? a.kind == 2 : a.kind == 1) continue;
+        if (five) lr_vsums<2>(T, VS, VQ, h, sw);
+        else lr_vsums<1>(T, VS, VQ, h, sw);
+        __syncthreads();
         // A / B at unit rows -1..h (every other row from -1 for 5x5, :375)
         for (int k = threadIdx.x; k < (h + 2) * (sw + 2); k += 256) {
             const int jj = k / (sw + 2), ii = k - jj * (sw + 2), j = jj - 1;
             if (five && !(j & 1)) continue;
             int A, B;
-            if (five) lr_ab<2>(T, j, ii - 1, a.prm.sgr.s0, bd8, A, B);
-            else lr_ab<1>(T, j, ii - 1, a.prm.sgr.s1, bd8, A, B);
+            if (five) lr_ab<2>(VS, VQ, jj, ii, a.prm.sgr.s0, bd8, A, B);
+            else lr_ab<1>(VS, VQ, jj, ii, a.prm.sgr.s1, bd8, A, B);
             AB[0][jj][ii] = A;
             AB[1][jj][ii] = B;
         }

@@ -268,8 +268,13 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                                         const Dav1dGpuPlane ref[DGPU_MAX_REFS][3], void *stream) {
     constexpr int NC = DGPU_N_RECT_TX_SIZES;
     if (!r || !dst) return -1;
-    if (hipSetDevice(r->device) != hipSuccess) return -3;
-    if (r->done && hipEventSynchronize(r->done) != hipSuccess) return -3;   // buffers free for reuse
+    // DAV1D_GPU_REC_HOSTONLY=1 (diagnostics, no device needed): run the host
+    // phases only and drop the recording before the upload
+    static const bool host_only = getenv("DAV1D_GPU_REC_HOSTONLY") != nullptr;
+    if (!host_only) {
+        if (hipSetDevice(r->device) != hipSuccess) return -3;
+        if (r->done && hipEventSynchronize(r->done) != hipSuccess) return -3;   // buffers free for reuse
+    }
     // a previous flush whose wavefront gave up waiting is reported once,
     // here if dav1d_gpu_recorder_status did not report it: nothing is
     // launched and the recording is kept for a retry
@@ -534,7 +539,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     r->run_start.assign(n_levels + 1, 0);
     r->last_units = n;
     r->last_levels = n_levels;
-    if (!n) {
+    if (!n || host_only) {
         r->blocks.clear();
         r->residuals.clear();
         r->coef32.clear();

@@ -1,0 +1,509 @@
+"""A second, independent restatement of the core DSP path in numpy -- the
+inverse transforms of src/itx_1d.c / src/itx_tmpl.c and the motion
+compensation of src/mc_tmpl.c -- checked against the C oracle
+(oracle/dsp_ref.c, through its per-call tables oracle_{itx,mc}_dsp_init_*)
+over checkasm's iteration spaces (tests/checkasm/itx.c:249-318,
+tests/checkasm/mc.c:43-300), at 8, 10 and 12 bit.
+
+The reference holds no known-answer vectors for these functions, so this
+is what pins the oracle beyond its own golden regression file: two
+transcriptions of the reference, written apart (the numpy one uses the
+direct rotation products in int64 where the reference and the C oracle use
+their overflow-free (c - 4096) forms, vectorised over whole batches of
+rows), must agree bit for bit.  Not restated here: the 64-point DCT (the C
+oracle alone covers it).
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---------------------------------------------------------------- tables ---
+def _table(name):
+    """A constant table from csrc/dsp_tables.h (generated from src/tables.c)."""
+    txt = open(os.path.join(ROOT, "dav1d-mirror_amd", "csrc", "dsp_tables.h")).read()
+    m = re.search(name + r"\[[^\]]*\] = \{(.*?)\};", txt, re.S)
+    return np.array([int(v) for v in re.findall(r"-?\d+", m.group(1))], np.int64)
+
+
+SUBPEL = _table("dspt_subpel").reshape(6, 15, 8)   # dav1d_mc_subpel_filters: regular, smooth, sharp, 4-tap x2, bilinear
+OBMC = _table("dspt_obmc")
+
+
+# ------------------------------------------------------ 1-D transforms ---
+# Each takes (N, n) int64 rows and returns (N, n); `cl` clips to the pass's
+# range after every sum, as the reference's CLIP does.
+def _r(x, sh):
+    return (x + (1 << (sh - 1))) >> sh
+
+
+def _s181(x):
+    return (x * 181 + 128) >> 8
+
+
+def dct4(c, cl):
+    i0, i1, i2, i3 = c.T
+    t0, t1 = _s181(i0 + i2), _s181(i0 - i2)
+    t2 = _r(i1 * 1567 - i3 * 3784, 12)
+    t3 = _r(i1 * 3784 + i3 * 1567, 12)
+    return np.stack([cl(t0 + t3), cl(t1 + t2), cl(t1 - t2), cl(t0 - t3)], 1)
+
+
+def dct8(c, cl):
+    e = dct4(c[:, 0::2], cl)
+    i1, i3, i5, i7 = c[:, 1], c[:, 3], c[:, 5], c[:, 7]
+    t4a, t7a = _r(i1 * 799 - i7 * 4017, 12), _r(i1 * 4017 + i7 * 799, 12)
+    t5a, t6a = _r(i5 * 1703 - i3 * 1138, 11), _r(i5 * 1138 + i3 * 1703, 11)
+    t4, t5a, t7, t6a = cl(t4a + t5a), cl(t4a - t5a), cl(t7a + t6a), cl(t7a - t6a)
+    t5, t6 = _s181(t6a - t5a), _s181(t6a + t5a)
+    o = [t7, t6, t5, t4]
+    return np.stack([cl(e[:, i] + o[i]) for i in range(4)] + [cl(e[:, 3 - i] - o[3 - i]) for i in range(4)], 1)
+
+
+def _join(e, o, cl):
+    n = e.shape[1]
+    return np.concatenate([cl(e + o), cl(e - o)[:, ::-1]], 1) if n else e
+
+
+def dct16(c, cl):
+    e = dct8(c[:, 0::2], cl)
+    i = {k: c[:, k] for k in range(1, 16, 2)}
+    t8a, t15a = _r(i[1] * 401 - i[15] * 4076, 12), _r(i[1] * 4076 + i[15] * 401, 12)
+    t9a, t14a = _r(i[9] * 1583 - i[7] * 1299, 11), _r(i[9] * 1299 + i[7] * 1583, 11)
+    t10a, t13a = _r(i[5] * 1931 - i[11] * 3612, 12), _r(i[5] * 3612 + i[11] * 1931, 12)
+    t11a, t12a = _r(i[13] * 3920 - i[3] * 1189, 12), _r(i[13] * 1189 + i[3] * 3920, 12)
+    t8, t9, t10, t11 = cl(t8a + t9a), cl(t8a - t9a), cl(t11a - t10a), cl(t11a + t10a)
+    t12, t13, t14, t15 = cl(t12a + t13a), cl(t12a - t13a), cl(t15a - t14a), cl(t15a + t14a)
+    t9a, t14a = _r(t14 * 1567 - t9 * 3784, 12), _r(t14 * 3784 + t9 * 1567, 12)
+    t10a, t13a = _r(-(t13 * 3784 + t10 * 1567), 12), _r(t13 * 1567 - t10 * 3784, 12)
+    t8a, t9, t10, t11a = cl(t8 + t11), cl(t9a + t10a), cl(t9a - t10a), cl(t8 - t11)
+    t12a, t13, t14, t15a = cl(t15 - t12), cl(t14a - t13a), cl(t14a + t13a), cl(t15 + t12)
+    t10a, t13a, t11, t12 = _s181(t13 - t10), _s181(t13 + t10), _s181(t12a - t11a), _s181(t12a + t11a)
+    o = np.stack([t15a, t14, t13a, t12, t11, t10a, t9, t8a], 1)
+    return _join(e, o, cl)
+
+
+def dct32(c, cl):
+    e = dct16(c[:, 0::2], cl)
+    i = {k: c[:, k] for k in range(1, 32, 2)}
+    # (in_a, in_b, c_a, c_b, shift): ta = in_a*ca - in_b*cb, tb = in_a*cb + in_b*ca
+    rot = [(1, 31, 201, 4091), (17, 15, 3035, 2751), (9, 23, 1751, 3703), (25, 7, 3857, 1380),
+           (5, 27, 995, 3973), (21, 11, 3513, 2106), (13, 19, 2440, 3290), (29, 3, 4052, 601)]
+    t = {}
+    pairs = [(16, 31), (17, 30), (18, 29), (19, 28), (20, 27), (21, 26), (22, 25), (23, 24)]
+    for (a, b, ca, cb), (lo, hi) in zip(rot, pairs):
+        if lo == 22:   # the 11-bit pair (1220, 1645) == (2440, 3290) / 2
+            t[lo], t[hi] = _r(i[a] * 1220 - i[b] * 1645, 11), _r(i[a] * 1645 + i[b] * 1220, 11)
+        elif lo in (17, 19, 21, 23):
+            t[lo], t[hi] = _r(i[a] * ca - i[b] * cb, 12), _r(i[a] * cb + i[b] * ca, 12)
+        else:
+            t[lo], t[hi] = _r(i[a] * ca - i[b] * cb, 12), _r(i[a] * cb + i[b] * ca, 12)
+    u = {}
+    for g in range(16, 32, 4):
+        u[g], u[g + 1] = cl(t[g] + t[g + 1]), cl(t[g] - t[g + 1])
+        u[g + 2], u[g + 3] = cl(t[g + 3] - t[g + 2]), cl(t[g + 3] + t[g + 2])
+    v17, v30 = _r(u[30] * 799 - u[17] * 4017, 12), _r(u[30] * 4017 + u[17] * 799, 12)
+    v18, v29 = _r(-(u[29] * 4017 + u[18] * 799), 12), _r(u[29] * 799 - u[18] * 4017, 12)
+    v21, v26 = _r(u[26] * 1703 - u[21] * 1138, 11), _r(u[26] * 1138 + u[21] * 1703, 11)
+    v22, v25 = _r(-(u[25] * 1138 + u[22] * 1703), 11), _r(u[25] * 1703 - u[22] * 1138, 11)
+    w16, w17, w18, w19 = cl(u[16] + u[19]), cl(v17 + v18), cl(v17 - v18), cl(u[16] - u[19])
+    w20, w21, w22, w23 = cl(u[23] - u[20]), cl(v22 - v21), cl(v22 + v21), cl(u[23] + u[20])
+    w24, w25, w26, w27 = cl(u[24] + u[27]), cl(v25 + v26), cl(v25 - v26), cl(u[24] - u[27])
+    w28, w29, w30, w31 = cl(u[31] - u[28]), cl(v30 - v29), cl(v30 + v29), cl(u[31] + u[28])
+    x18, x29 = _r(w29 * 1567 - w18 * 3784, 12), _r(w29 * 3784 + w18 * 1567, 12)
+    x19, x28 = _r(w28 * 1567 - w19 * 3784, 12), _r(w28 * 3784 + w19 * 1567, 12)
+    x20, x27 = _r(-(w27 * 3784 + w20 * 1567), 12), _r(w27 * 1567 - w20 * 3784, 12)
+    x21, x26 = _r(-(w26 * 3784 + w21 * 1567), 12), _r(w26 * 1567 - w21 * 3784, 12)
+    y16, y17, y18, y19 = cl(w16 + w23), cl(w17 + w22), cl(x18 + x21), cl(x19 + x20)
+    y20, y21, y22, y23 = cl(x19 - x20), cl(x18 - x21), cl(w17 - w22), cl(w16 - w23)
+    y24, y25, y26, y27 = cl(w31 - w24), cl(w30 - w25), cl(x29 - x26), cl(x28 - x27)
+    y28, y29, y30, y31 = cl(x28 + x27), cl(x29 + x26), cl(w30 + w25), cl(w31 + w24)
+    o = np.stack([y31, y30, y29, y28, _s181(y27 + y20), _s181(y26 + y21), _s181(y25 + y22), _s181(y24 + y23),
+                  _s181(y24 - y23), _s181(y25 - y22), _s181(y26 - y21), _s181(y27 - y20), y19, y18, y17, y16], 1)
+    return _join(e, o, cl)
+
+
+def adst4(c, cl):
+    i0, i1, i2, i3 = c.T
+    return np.stack([_r(1321 * i0 + 3803 * i2 + 2482 * i3 + 3344 * i1, 12),
+                     _r(2482 * i0 - 1321 * i2 - 3803 * i3 + 3344 * i1, 12),
+                     (209 * (i0 - i2 + i3) + 128) >> 8,
+                     _r(3803 * i0 + 2482 * i2 - 1321 * i3 - 3344 * i1, 12)], 1)
+
+
+def adst8(c, cl):
+    i = c.T
+    t0a, t1a = _r(4076 * i[7] + 401 * i[0], 12), _r(401 * i[7] - 4076 * i[0], 12)
+    t2a, t3a = _r(3612 * i[5] + 1931 * i[2], 12), _r(1931 * i[5] - 3612 * i[2], 12)
+    t4a, t5a = _r(1299 * i[3] + 1583 * i[4], 11), _r(1583 * i[3] - 1299 * i[4], 11)
+    t6a, t7a = _r(1189 * i[1] + 3920 * i[6], 12), _r(3920 * i[1] - 1189 * i[6], 12)
+    t0, t1, t2, t3 = cl(t0a + t4a), cl(t1a + t5a), cl(t2a + t6a), cl(t3a + t7a)
+    t4, t5, t6, t7 = cl(t0a - t4a), cl(t1a - t5a), cl(t2a - t6a), cl(t3a - t7a)
+    t4a, t5a = _r(3784 * t4 + 1567 * t5, 12), _r(1567 * t4 - 3784 * t5, 12)
+    t6a, t7a = _r(3784 * t7 - 1567 * t6, 12), _r(1567 * t7 + 3784 * t6, 12)
+    o = [None] * 8
+    o[0], o[7] = cl(t0 + t2), -cl(t1 + t3)
+    t2, t3 = cl(t0 - t2), cl(t1 - t3)
+    o[1], o[6] = -cl(t4a + t6a), cl(t5a + t7a)
+    t6, t7 = cl(t4a - t6a), cl(t5a - t7a)
+    o[3], o[4], o[2], o[5] = -_s181(t2 + t3), _s181(t2 - t3), _s181(t6 + t7), -_s181(t6 - t7)
+    return np.stack(o, 1)
+
+
+def adst16(c, cl):
+    i = c.T
+    t = [None] * 16
+    spec = [(15, 0, 4091, 201), (13, 2, 3973, 995), (11, 4, 3703, 1751), (9, 6, 1645 * 2, 1220 * 2)]
+    for k, (a, b, ca, cb) in enumerate(spec):
+        if k == 3:   # the 11-bit pair
+            t[6], t[7] = _r(i[9] * 1645 + i[6] * 1220, 11), _r(i[9] * 1220 - i[6] * 1645, 11)
+        else:
+            t[2 * k], t[2 * k + 1] = _r(i[a] * ca + i[b] * cb, 12), _r(i[a] * cb - i[b] * ca, 12)
+    t[8], t[9] = _r(i[7] * 2751 + i[8] * 3035, 12), _r(i[7] * 3035 - i[8] * 2751, 12)
+    t[10], t[11] = _r(i[5] * 2106 + i[10] * 3513, 12), _r(i[5] * 3513 - i[10] * 2106, 12)
+    t[12], t[13] = _r(i[3] * 1380 + i[12] * 3857, 12), _r(i[3] * 3857 - i[12] * 1380, 12)
+    t[14], t[15] = _r(i[1] * 601 + i[14] * 4052, 12), _r(i[1] * 4052 - i[14] * 601, 12)
+    a = [cl(t[k] + t[k + 8]) for k in range(8)] + [cl(t[k] - t[k + 8]) for k in range(8)]
+    b8, b9 = _r(a[8] * 4017 + a[9] * 799, 12), _r(a[8] * 799 - a[9] * 4017, 12)
+    b10, b11 = _r(a[10] * 2276 + a[11] * 3406, 12), _r(a[10] * 3406 - a[11] * 2276, 12)
+    b12, b13 = _r(a[13] * 4017 - a[12] * 799, 12), _r(a[13] * 799 + a[12] * 4017, 12)
+    b14, b15 = _r(a[15] * 2276 - a[14] * 3406, 12), _r(a[15] * 3406 + a[14] * 2276, 12)
+    c0, c1, c2, c3 = cl(a[0] + a[4]), cl(a[1] + a[5]), cl(a[2] + a[6]), cl(a[3] + a[7])
+    c4, c5, c6, c7 = cl(a[0] - a[4]), cl(a[1] - a[5]), cl(a[2] - a[6]), cl(a[3] - a[7])
+    c8, c9, c10, c11 = cl(b8 + b12), cl(b9 + b13), cl(b10 + b14), cl(b11 + b15)
+    c12, c13, c14, c15 = cl(b8 - b12), cl(b9 - b13), cl(b10 - b14), cl(b11 - b15)
+    d4, d5 = _r(c4 * 3784 + c5 * 1567, 12), _r(c4 * 1567 - c5 * 3784, 12)
+    d6, d7 = _r(c7 * 3784 - c6 * 1567, 12), _r(c7 * 1567 + c6 * 3784, 12)
+    d12, d13 = _r(c12 * 3784 + c13 * 1567, 12), _r(c12 * 1567 - c13 * 3784, 12)
+    d14, d15 = _r(c15 * 3784 - c14 * 1567, 12), _r(c15 * 1567 + c14 * 3784, 12)
+    o = [None] * 16
+    o[0], o[15] = cl(c0 + c2), -cl(c1 + c3)
+    e2, e3 = cl(c0 - c2), cl(c1 - c3)
+    o[3], o[12] = -cl(d4 + d6), cl(d5 + d7)
+    e6, e7 = cl(d4 - d6), cl(d5 - d7)
+    o[1], o[14] = -cl(c8 + c10), cl(c9 + c11)
+    e10, e11 = cl(c8 - c10), cl(c9 - c11)
+    o[2], o[13] = cl(d12 + d14), -cl(d13 + d15)
+    e14, e15 = cl(d12 - d14), cl(d13 - d15)
+    o[7], o[8], o[4], o[11] = -_s181(e2 + e3), _s181(e2 - e3), _s181(e6 + e7), -_s181(e6 - e7)
+    o[6], o[9], o[5], o[10] = _s181(e10 + e11), -_s181(e10 - e11), -_s181(e14 + e15), _s181(e14 - e15)
+    return np.stack(o, 1)
+
+
+def identity(c, cl):
+    n = c.shape[1]
+    if n == 4:
+        return c + _r(c * 1697, 12)
+    if n == 8:
+        return c * 2
+    if n == 16:
+        return 2 * c + _r(c * 1697, 11)
+    return c * 4
+
+
+DCT = {4: dct4, 8: dct8, 16: dct16, 32: dct32}
+ADST = {4: adst4, 8: adst8, 16: adst16}
+
+
+def tx1d(kind, c, cl):
+    n = c.shape[1]
+    if kind == "dct":
+        return DCT[n](c, cl)
+    if kind == "identity":
+        return identity(c, cl)
+    o = ADST[n](c, cl)
+    return o[:, ::-1] if kind == "flipadst" else o
+
+
+# TxfmType (src/levels.h:80-100): the name is VERTICAL_HORIZONTAL
+_TYPES = ["DCT_DCT", "ADST_DCT", "DCT_ADST", "ADST_ADST", "FLIPADST_DCT", "DCT_FLIPADST", "FLIPADST_FLIPADST",
+          "ADST_FLIPADST", "FLIPADST_ADST", "IDTX", "V_DCT", "H_DCT", "V_ADST", "H_ADST", "V_FLIPADST", "H_FLIPADST"]
+
+
+def kinds(tp):
+    """(horizontal, vertical) 1-D kinds of TxfmType tp."""
+    nm = _TYPES[tp]
+    if nm == "IDTX":
+        return "identity", "identity"
+    if nm.startswith("V_"):
+        return "identity", nm[2:].lower()
+    if nm.startswith("H_"):
+        return nm[2:].lower(), "identity"
+    v, h = nm.split("_")
+    return h.lower(), v.lower()
+
+
+SHIFT = {(4, 4): 0, (4, 8): 0, (8, 4): 0, (4, 16): 1, (16, 4): 1, (8, 8): 1, (8, 16): 1, (16, 8): 1,
+         (16, 32): 1, (32, 16): 1, (8, 32): 2, (32, 8): 2, (16, 16): 2, (32, 32): 2}
+
+
+def inv_txfm_add(dst, coeff, eob, w, h, tp, bdmax):
+    """inv_txfm_add_c (src/itx_tmpl.c:40-100) for one block: returns the new
+    dst; coeff (column-major, min(h,32) rows) is zeroed in place."""
+    bd8 = bdmax.bit_length() - 8
+    shift = SHIFT[(w, h)]
+    rect2 = w * 2 == h or h * 2 == w
+    rnd = (1 << shift) >> 1
+    if tp == 0 and eob < 1:   # has_dconly: DCT_DCT only
+        dc = int(coeff[0])
+        coeff[0] = 0
+        if rect2:
+            dc = _s181(dc)
+        dc = _s181(dc)
+        dc = (dc + rnd) >> shift
+        dc = (dc * 181 + 128 + 2048) >> 12
+        return np.clip(dst + dc, 0, bdmax)
+    sw, sh = min(w, 32), min(h, 32)
+    rmin = -32768 if bd8 == 0 else -((bdmax + 1) << 7)
+    cmin = -32768 if bd8 == 0 else -((bdmax + 1) << 5)
+    rcl = lambda v: np.clip(v, rmin, ~rmin)  # noqa: E731
+    ccl = lambda v: np.clip(v, cmin, ~cmin)  # noqa: E731
+    kh, kv = kinds(tp)
+    rows = np.zeros((sh, w), np.int64)
+    rows[:, :sw] = coeff[:sw * sh].astype(np.int64).reshape(sw, sh).T
+    if rect2:
+        rows = _s181(rows)
+    rows = tx1d(kh, rows, rcl)
+    coeff[:sw * sh] = 0
+    tmp = np.zeros((h, w), np.int64)
+    tmp[:sh] = ccl((rows + rnd) >> shift)
+    cols = tx1d(kv, tmp.T.copy(), ccl).T
+    return np.clip(dst + ((cols + 8) >> 4), 0, bdmax)
+
+
+def wht_add(dst, coeff, bdmax):
+    """inv_txfm_add_wht_wht_4x4_c (src/itx_tmpl.c:166-185)."""
+    def wht(c):
+        i0, i1, i2, i3 = c.T
+        t0, t2 = i0 + i1, i2 - i3
+        t4 = (t0 - t2) >> 1
+        t3, t1 = t4 - i3, t4 - i1
+        return np.stack([t0 - t3, t3, t1, t2 + t1], 1)
+    rows = wht(coeff[:16].astype(np.int64).reshape(4, 4).T >> 2)
+    coeff[:16] = 0
+    return np.clip(dst + wht(rows.T.copy()).T, 0, bdmax)
+
+
+# ------------------------------------------------------- the oracle side ---
+TX_WH = [(4, 4), (8, 8), (16, 16), (32, 32), (64, 64), (4, 8), (8, 4), (8, 16), (16, 8), (16, 32), (32, 16),
+         (32, 64), (64, 32), (4, 16), (16, 4), (8, 32), (32, 8), (16, 64), (64, 16)]
+
+
+def _oracle_lib():
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    return L
+
+
+def _itx_table(L, hbd):
+    t = (ctypes.c_void_p * (19 * 17))()
+    getattr(L, f"oracle_itx_dsp_init_{16 if hbd else 8}bpc")(ctypes.byref(t), 10 if hbd else 8)
+    return t
+
+
+@pytest.mark.parametrize("bdmax", [255, 1023, 4095])
+def test_itx_numpy_restatement_matches_oracle(bdmax):
+    hbd = bdmax > 255
+    L = _oracle_lib()
+    tab = _itx_table(L, hbd)
+    pdt, cdt = (np.uint16, np.int32) if hbd else (np.uint8, np.int16)
+    args = [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p, ctypes.c_int] + ([ctypes.c_int] if hbd else [])
+    FN = ctypes.CFUNCTYPE(None, *args)
+    rng = np.random.default_rng(bdmax)
+    n_cases = 0
+    cmax = 32767 if not hbd else (~(~127 << (bdmax.bit_length()))) & 0x7fffffff
+    for tx, (w, h) in enumerate(TX_WH):
+        if max(w, h) == 64:
+            continue
+        sw, sh = min(w, 32), min(h, 32)
+        for tp in range(17):
+            if not tab[tx * 17 + tp]:
+                continue
+            fn = FN(tab[tx * 17 + tp])
+            for it in range(6):
+                # checkasm's eob sweep: DC-only, a partial region, the full
+                # region; magnitudes from small to clip-saturating
+                dst = rng.integers(0, bdmax + 1, (h, w)).astype(pdt)
+                cf = np.zeros(sw * sh, cdt)
+                reg = [(1, 1), (max(1, sw // 2), max(1, sh // 2)), (sw, sh)][it % 3]
+                amp = [64, bdmax * 8, cmax][it // 3 % 3] if tp != 16 else 64 * 4
+                blk = rng.integers(-amp, amp + 1, size=(reg[0], reg[1]))
+                for x in range(reg[0]):
+                    cf[x * sh:x * sh + reg[1]] = blk[x]
+                eob = 0 if it == 0 else 1 + int(rng.integers(0, sw * sh))
+                if tp == 16:   # WHT_WHT (lossless 4x4)
+                    want = wht_add(dst.astype(np.int64), cf.copy().astype(np.int64), bdmax)
+                else:
+                    want = inv_txfm_add(dst.astype(np.int64), cf.astype(np.int64).copy(), eob, w, h, tp, bdmax)
+                got, gcf = dst.copy(), cf.copy()
+                a = [got.ctypes.data, w * got.itemsize, gcf.ctypes.data, eob] + ([bdmax] if hbd else [])
+                fn(*a)
+                assert np.array_equal(got, want.astype(pdt)), f"tx {w}x{h} type {tp} case {it}"
+                assert not gcf.any(), f"tx {w}x{h} type {tp}: coefficients not zeroed"
+                n_cases += 1
+    assert n_cases > 800
+
+
+# ------------------------------------------------------------------- mc ---
+def _bank(t, m, n):
+    """GET_H_FILTER / GET_V_FILTER (src/mc_tmpl.c:99-108): None for m == 0."""
+    if not m:
+        return None
+    return SUBPEL[t if n > 4 else 3 + (t & 1), m - 1]
+
+
+def _taps(src, x0, y0, w, h, f, horiz):
+    """sum_k f[k] * src[.. -3 + k ..] over the (h, w) output window at (y0, x0)."""
+    acc = np.zeros((h, w), np.int64)
+    for k in range(8):
+        if horiz:
+            acc += f[k] * src[y0:y0 + h, x0 - 3 + k:x0 - 3 + k + w]
+        else:
+            acc += f[k] * src[y0 - 3 + k:y0 - 3 + k + h, x0:x0 + w]
+    return acc
+
+
+def mc_8tap(src, x0, y0, w, h, mx, my, ftype, bdmax, prep):
+    """put_8tap_c / prep_8tap_c (src/mc_tmpl.c:113-171, :223-282) with the
+    copy / prep_c paths (:52-75); src is int64 with a >= 3-px border."""
+    ib = 4 if bdmax == 255 else 14 - bdmax.bit_length()
+    pb = 0 if bdmax == 255 else 8192
+    fh, fv = _bank(ftype & 3, mx, w), _bank(ftype >> 2, my, h)
+    if fh is not None and fv is not None:
+        mid = np.zeros((h + 7, w), np.int64)
+        mid[:] = _r(_taps(src, x0, y0 - 3, w, h + 7, fh, True), 6 - ib)
+        v = np.zeros((h, w), np.int64)
+        for k in range(8):
+            v += fv[k] * mid[k:k + h]
+        return _r(v, 6) - pb if prep else np.clip(_r(v, 6 + ib), 0, bdmax)
+    if fh is not None:
+        s = _taps(src, x0, y0, w, h, fh, True)
+        return _r(s, 6 - ib) - pb if prep else np.clip((s + 32 + ((1 << (6 - ib)) >> 1)) >> 6, 0, bdmax)
+    if fv is not None:
+        s = _taps(src, x0, y0, w, h, fv, False)
+        return _r(s, 6 - ib) - pb if prep else np.clip(_r(s, 6), 0, bdmax)
+    p = src[y0:y0 + h, x0:x0 + w]
+    return (p << ib) - pb if prep else p.copy()
+
+
+def mc_bilin(src, x0, y0, w, h, mx, my, bdmax, prep):
+    """put_bilin_c / prep_bilin_c (src/mc_tmpl.c:395-450, :493-546)."""
+    ib = 4 if bdmax == 255 else 14 - bdmax.bit_length()
+    pb = 0 if bdmax == 255 else 8192
+    bil = lambda a, b, m: 16 * a + m * (b - a)  # noqa: E731
+    s = src
+    if mx and my:
+        m0 = _r(bil(s[y0:y0 + h + 1, x0:x0 + w], s[y0:y0 + h + 1, x0 + 1:x0 + w + 1], mx), 4 - ib) if ib < 4 else \
+            bil(s[y0:y0 + h + 1, x0:x0 + w], s[y0:y0 + h + 1, x0 + 1:x0 + w + 1], mx)
+        v = bil(m0[:h], m0[1:h + 1], my)
+        return _r(v, 4) - pb if prep else np.clip(_r(v, 4 + ib), 0, bdmax)
+    if mx:
+        p = bil(s[y0:y0 + h, x0:x0 + w], s[y0:y0 + h, x0 + 1:x0 + w + 1], mx)
+        q = _r(p, 4 - ib) if ib < 4 else p
+        return q - pb if prep else np.clip(_r(q, ib), 0, bdmax)
+    if my:
+        p = bil(s[y0:y0 + h, x0:x0 + w], s[y0 + 1:y0 + h + 1, x0:x0 + w], my)
+        return (_r(p, 4 - ib) if ib < 4 else p) - pb if prep else np.clip(_r(p, 4), 0, bdmax)
+    p = s[y0:y0 + h, x0:x0 + w]
+    return (p << ib) - pb if prep else p.copy()
+
+
+FT = [0 | 0 << 2, 0 | 1 << 2, 0 | 2 << 2, 2 | 0 << 2, 2 | 1 << 2, 2 | 2 << 2, 1 | 0 << 2, 1 | 1 << 2, 1 | 2 << 2]
+
+
+@pytest.mark.parametrize("bdmax", [255, 1023, 4095])
+def test_mc_numpy_restatement_matches_oracle(bdmax):
+    """mc[10] / mct[10] over checkasm's (w, h) space (tests/checkasm/mc.c:
+    43-56, :139), random sub-pel positions, and the compound blends avg /
+    w_avg / mask / w_mask (444 / 422 / 420) on their outputs."""
+    hbd = bdmax > 255
+    L = _oracle_lib()
+    tab = (ctypes.c_void_p * 53)()
+    getattr(L, f"oracle_mc_dsp_init_{16 if hbd else 8}bpc")(ctypes.byref(tab))
+    pdt = np.uint16 if hbd else np.uint8
+    bpp = 2 if hbd else 1
+    VP, SZ, I = ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_int
+    extra = [I] if hbd else []
+    PUT = ctypes.CFUNCTYPE(None, VP, SZ, VP, SZ, I, I, I, I, *extra)
+    PREP = ctypes.CFUNCTYPE(None, VP, VP, SZ, I, I, I, I, *extra)
+    AVG = ctypes.CFUNCTYPE(None, VP, SZ, VP, VP, I, I, *extra)
+    WAVG = ctypes.CFUNCTYPE(None, VP, SZ, VP, VP, I, I, I, *extra)
+    MASK = ctypes.CFUNCTYPE(None, VP, SZ, VP, VP, I, I, VP, *extra)
+    WMASK = ctypes.CFUNCTYPE(None, VP, SZ, VP, VP, I, I, VP, I, *extra)
+    rng = np.random.default_rng(bdmax + 7)
+    ib = 4 if not hbd else 14 - bdmax.bit_length()
+    pb = 0 if not hbd else 8192
+    S = 160
+    src = rng.integers(0, bdmax + 1, (S, S + 16)).astype(pdt)
+    s64 = src.astype(np.int64)
+    ex = [bdmax] if hbd else []
+    n = 0
+    for w in (2, 4, 8, 16, 32, 64, 128):
+        for h in (2, 4, 6, 8, 12, 16, 24, 32, 64, 128):
+            if h > 4 * w or w > 8 * h:
+                continue
+            for f in range(10):
+                mx, my = (int(v) for v in rng.integers(0, 16, 2))
+                if n % 7 == 0:
+                    mx = 0
+                if n % 11 == 0:
+                    my = 0
+                n += 1
+                x0, y0 = 8, 8
+                # put
+                dst = np.zeros((h, w), pdt)
+                PUT(tab[f])(dst.ctypes.data, w * bpp, src.ctypes.data + (y0 * src.shape[1] + x0) * bpp,
+                            src.shape[1] * bpp, w, h, mx, my, *ex)
+                want = mc_bilin(s64, x0, y0, w, h, mx, my, bdmax, False) if f == 9 else \
+                    mc_8tap(s64, x0, y0, w, h, mx, my, FT[f], bdmax, False)
+                assert np.array_equal(dst, want.astype(pdt)), f"put f{f} {w}x{h} m{mx},{my}"
+                if w < 4 or h < 2:
+                    continue
+                # prep (mct: w >= 4)
+                tmp = np.zeros((h, w), np.int16)
+                PREP(tab[20 + f])(tmp.ctypes.data, src.ctypes.data + (y0 * src.shape[1] + x0) * bpp,
+                                  src.shape[1] * bpp, w, h, mx, my, *ex)
+                want = mc_bilin(s64, x0, y0, w, h, mx, my, bdmax, True) if f == 9 else \
+                    mc_8tap(s64, x0, y0, w, h, mx, my, FT[f], bdmax, True)
+                assert np.array_equal(tmp, want.astype(np.int16)), f"prep f{f} {w}x{h} m{mx},{my}"
+    # compound blends on random prep outputs (avg_c / w_avg_c / mask_c / w_mask_c, :587-726)
+    for w, h in ((4, 4), (8, 16), (16, 4), (32, 32), (64, 16), (128, 64)):
+        lo, hi = -pb - (1 << (ib + 4)), (bdmax << ib) - pb + (1 << (ib + 4))
+        t1 = rng.integers(lo, hi, (h, w)).astype(np.int16)
+        t2 = rng.integers(lo, hi, (h, w)).astype(np.int16)
+        a, b = t1.astype(np.int64), t2.astype(np.int64)
+        dst = np.zeros((h, w), pdt)
+        AVG(tab[40])(dst.ctypes.data, w * bpp, t1.ctypes.data, t2.ctypes.data, w, h, *ex)
+        assert np.array_equal(dst, np.clip((a + b + (1 << ib) + 2 * pb) >> (ib + 1), 0, bdmax).astype(pdt))
+        wt = int(rng.integers(1, 16))
+        WAVG(tab[41])(dst.ctypes.data, w * bpp, t1.ctypes.data, t2.ctypes.data, w, h, wt, *ex)
+        want = np.clip((a * wt + b * (16 - wt) + (8 << ib) + 16 * pb) >> (ib + 4), 0, bdmax)
+        assert np.array_equal(dst, want.astype(pdt))
+        m = rng.integers(0, 65, (h, w)).astype(np.uint8)
+        MASK(tab[42])(dst.ctypes.data, w * bpp, t1.ctypes.data, t2.ctypes.data, w, h, m.ctypes.data, *ex)
+        mm = m.astype(np.int64)
+        want = np.clip((a * mm + b * (64 - mm) + (32 << ib) + 64 * pb) >> (ib + 6), 0, bdmax)
+        assert np.array_equal(dst, want.astype(pdt))
+        bits = bdmax.bit_length()
+        msh = bits + ib - 4
+        mw = np.minimum(38 + ((np.abs(a - b) + (1 << (msh - 5))) >> msh), 64)
+        blend = np.clip((a * mw + b * (64 - mw) + (32 << ib) + 64 * pb) >> (ib + 6), 0, bdmax)
+        for k, (ssh, ssv) in enumerate(((0, 0), (1, 0), (1, 1))):
+            for sign in (0, 1):
+                mo = np.zeros(w * h, np.uint8)
+                WMASK(tab[43 + k])(dst.ctypes.data, w * bpp, t1.ctypes.data, t2.ctypes.data, w, h,
+                                   mo.ctypes.data, sign, *ex)
+                assert np.array_equal(dst, blend.astype(pdt))
+                if not ssh:
+                    wm = mw
+                elif not ssv:
+                    wm = (mw[:, 0::2] + mw[:, 1::2] + 1 - sign) >> 1
+                else:
+                    wm = (mw[0::2, 0::2] + mw[0::2, 1::2] + mw[1::2, 0::2] + mw[1::2, 1::2] + 2 - sign) >> 2
+                got = mo[:wm.size].reshape(wm.shape)
+                assert np.array_equal(got, wm.astype(np.uint8)), f"w_mask {ssh}{ssv} sign {sign} {w}x{h}"
+    assert n > 300
