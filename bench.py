@@ -174,6 +174,38 @@ def config_legs(dev, stream, steps):
     return out
 
 
+def cold_mall_leg(fd, dev, stream, steps, copies=6):
+    """The headline frame with the 256 MB MALL (Infinity Cache) cold: launches
+    rotate over `copies` device-resident copies of the frame (distinct
+    buffers, > 256 MB together), so each launch's reads miss the MALL left
+    by the previous one and FETCH_SIZE-style accounting measures HBM."""
+    import dav1d_mirror_amd.batch as bt
+    frames = [bt.DeviceFrame(fd, dev) for _ in range(copies)]
+    foot = sum(sum(t.numel() * t.element_size() for t in f.device_tensors()) for f in frames)
+    for f in frames:
+        f.launch(stream)
+    n = max(steps, 12)
+    n -= n % copies
+    evs = [(torch_event(), torch_event()) for _ in range(n)]
+    for i, (a, b) in enumerate(evs):
+        a.record(stream)
+        frames[i % copies].launch(stream)
+        b.record(stream)
+    import torch
+    torch.cuda.synchronize()
+    ks = float(np.mean([a.elapsed_time(b) for a, b in evs])) * 1e-3
+    b = fd.stats["total_bytes"]
+    del frames
+    return {"copies": copies, "footprint_bytes": int(foot), "kernel_us": round(ks * 1e6, 2),
+            "gpix_s": round(fd.stats["pixels"] / ks / 1e9, 2), "achieved_gbs": round(b / ks / 1e9, 1),
+            "frac": round(b / ks / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def torch_event():
+    import torch
+    return torch.cuda.Event(enable_timing=True)
+
+
 def family_breakdown(base_cfg, dev, stream, steps):
     import dav1d_mirror_amd.workload as wl
     import dav1d_mirror_amd.batch as bt
@@ -583,6 +615,8 @@ def main():
             out["feed"] = feed
         if not args.no_configs and world == 1 and args.config == "4k":
             out["configs"] = config_legs(dev, stream, args.steps)
+        if not args.no_configs and world == 1 and args.config == "4k":
+            out["cold_mall"] = cold_mall_leg(fd, dev, stream, args.steps)
         if not args.no_families and world == 1 and c.get("kind") == "full":
             out["families"] = family_breakdown(cfg, dev, stream, args.steps)
         if not args.no_tiles and world == 1:

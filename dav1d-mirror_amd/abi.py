@@ -214,6 +214,30 @@ class LrFrame(ctypes.Structure):
                 ("sb128", ctypes.c_int32), ("restore_planes", ctypes.c_int32)]
 
 
+class PictureParameters(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_int), ("h", ctypes.c_int), ("layout", ctypes.c_int), ("bpc", ctypes.c_int)]
+
+
+class Picture(ctypes.Structure):   # Dav1dGpuPicture == Dav1dPicture (272 bytes)
+    _fields_ = [("seq_hdr", ctypes.c_void_p), ("frame_hdr", ctypes.c_void_p), ("data", ctypes.c_void_p * 3),
+                ("stride", ctypes.c_ssize_t * 2), ("p", PictureParameters), ("m_", ctypes.c_uint8 * 48),
+                ("content_light", ctypes.c_void_p), ("mastering_display", ctypes.c_void_p),
+                ("itut_t35", ctypes.c_void_p), ("n_itut_t35", ctypes.c_size_t), ("reserved", ctypes.c_size_t * 4),
+                ("refs_", ctypes.c_void_p * 5), ("reserved_ref", ctypes.c_size_t * 4), ("ref", ctypes.c_void_p),
+                ("allocator_data", ctypes.c_void_p)]
+
+
+PIC_ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(Picture), ctypes.c_void_p)
+PIC_RELEASE_FN = ctypes.CFUNCTYPE(None, ctypes.POINTER(Picture), ctypes.c_void_p)
+
+
+class PicAllocator(ctypes.Structure):   # Dav1dGpuPicAllocator == Dav1dPicAllocator
+    _fields_ = [("cookie", ctypes.c_void_p), ("alloc_picture_callback", PIC_ALLOC_FN),
+                ("release_picture_callback", PIC_RELEASE_FN)]
+
+
+PIC_DEVICE, PIC_HOST_MAPPED = 0, 1
+
 GRAIN_W, GRAIN_H = 82, 73
 GRAIN_SCRATCH_BYTES = 3 * GRAIN_H * GRAIN_W * 2 + 3 * 4096
 
@@ -289,6 +313,12 @@ def load_lib():
         L.dav1d_gpu_recorder_status.argtypes = [ctypes.c_void_p]
         L.dav1d_gpu_recorder_status.restype = ctypes.c_int
         L.dav1d_gpu_get_error.restype = ctypes.c_int
+        L.dav1d_gpu_pic_allocator_init.argtypes = [ctypes.POINTER(PicAllocator), ctypes.c_int, ctypes.c_int]
+        L.dav1d_gpu_pic_allocator_init.restype = ctypes.c_int
+        L.dav1d_gpu_pic_allocator_close.argtypes = [ctypes.POINTER(PicAllocator)]
+        L.dav1d_gpu_pic_allocator_close.restype = ctypes.c_int
+        L.dav1d_gpu_picture_plane.argtypes = [ctypes.POINTER(Picture), ctypes.c_int, ctypes.POINTER(Plane)]
+        L.dav1d_gpu_picture_plane.restype = ctypes.c_int
         L.dav1d_gpu_clear_error.restype = ctypes.c_int
         L.dav1d_gpu_intra_workspace_bytes.argtypes = [ctypes.POINTER(IntraSchedule), ctypes.c_int]
         L.dav1d_gpu_intra_workspace_bytes.restype = ctypes.c_int64
@@ -308,6 +338,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_itx_dsp_init_gpu_8bpc", "dav1d_itx_dsp_init_gpu_16bpc",
     "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version",
     "dav1d_gpu_get_error", "dav1d_gpu_clear_error",
+    "dav1d_gpu_pic_allocator_init", "dav1d_gpu_pic_allocator_close", "dav1d_gpu_picture_plane",
     "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc", "dav1d_gpu_recon_lds_bytes",
     "dav1d_gpu_recon_tiles_8bpc", "dav1d_gpu_recon_tiles_16bpc",
     "dav1d_gpu_prepare_intra_edges_8bpc", "dav1d_gpu_prepare_intra_edges_16bpc",

@@ -111,6 +111,12 @@ class DeviceFrame:
             out.append(a if self.fd.cfg.bpc == 8 else a.view(np.uint16))
         return out
 
+    def device_tensors(self):
+        """Every device buffer the batch reads or writes (footprint accounting)."""
+        ts = [self.units, self.coefs, self.edges, self.cfl_luma] + list(self.dst)
+        ts += [t for planes in self.refs for t in planes]
+        return ts + [t for t in (self.aux, self.aux_pool) if t is not None]
+
 
 class DeviceTiles:
     """A TileData (tiles.build_tiles) uploaded to one GPU, plus its output

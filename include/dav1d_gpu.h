@@ -745,6 +745,58 @@ int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_units, int32_
  * -1 when an inter block names a reference plane that `ref` leaves NULL. */
 int dav1d_gpu_recorder_status(Dav1dGpuRecorder *r);
 
+/* ---- device-visible pictures ---------------------------
+ * A Dav1dPicAllocator (include/dav1d/picture.h:107-145) whose pictures live
+ * in HBM, so a decoder's reconstructed, post-filtered and output pictures
+ * stay resident between the frame-tier entries above (recorder flush ->
+ * deblock -> CDEF -> LR -> grain) instead of crossing PCIe.  The layouts
+ * below are layout-identical to Dav1dPicture / Dav1dPicAllocator (x86-64;
+ * header types kept opaque), so `Dav1dSettings.allocator` can be set from
+ * dav1d_gpu_pic_allocator_init() directly.  Plane geometry is
+ * dav1d_default_picture_alloc's (src/picture.c:46-83): width and height
+ * aligned to 128, strides padded by DAV1D_PICTURE_ALIGNMENT when a multiple
+ * of 1024, planes 64-byte aligned and the allocation padded by 64 bytes. */
+typedef struct Dav1dGpuPictureParameters {   /* Dav1dPictureParameters */
+    int w, h;
+    int layout;                  /* enum Dav1dPixelLayout: 0 I400 .. 3 I444 */
+    int bpc;
+} Dav1dGpuPictureParameters;
+
+typedef struct Dav1dGpuPicture {             /* Dav1dPicture, 272 bytes */
+    void *seq_hdr, *frame_hdr;
+    void *data[3];
+    ptrdiff_t stride[2];
+    Dav1dGpuPictureParameters p;
+    struct { int64_t timestamp, duration, offset; size_t size; const uint8_t *ud_data; void *ud_ref; } m;
+    void *content_light, *mastering_display, *itut_t35;
+    size_t n_itut_t35;
+    uintptr_t reserved[4];
+    void *frame_hdr_ref, *seq_hdr_ref, *content_light_ref, *mastering_display_ref, *itut_t35_ref;
+    uintptr_t reserved_ref[4];
+    void *ref;
+    void *allocator_data;
+} Dav1dGpuPicture;
+
+typedef struct Dav1dGpuPicAllocator {        /* Dav1dPicAllocator */
+    void *cookie;
+    int (*alloc_picture_callback)(Dav1dGpuPicture *pic, void *cookie);
+    void (*release_picture_callback)(Dav1dGpuPicture *pic, void *cookie);
+} Dav1dGpuPicAllocator;
+
+#define DGPU_PIC_DEVICE      0   /* hipMalloc: HBM, device access only (an all-GPU pixel path) */
+#define DGPU_PIC_HOST_MAPPED 1   /* page-locked host memory mapped into the device: both sides
+                                    may touch the pixels (a mixed CPU / GPU decoder)          */
+
+/* Fill `a` with callbacks allocating on `device`; released buffers are
+ * pooled per size and reused (release may come from any thread).  0 or -1.
+ * alloc returns 0 or -ENOMEM like dav1d's own. */
+int dav1d_gpu_pic_allocator_init(Dav1dGpuPicAllocator *a, int device, int flags);
+/* Free the pool (every picture must have been released).  Returns the
+ * number of pictures still outstanding (0 when clean). */
+int dav1d_gpu_pic_allocator_close(Dav1dGpuPicAllocator *a);
+/* A picture's plane as the frame-tier entries take it (w / h visible). */
+int dav1d_gpu_picture_plane(const Dav1dGpuPicture *pic, int plane, Dav1dGpuPlane *out);
+
 /* ---- film grain ----------------------------------------
  * bitfn(dav1d_apply_grain) (src/fg_apply_tmpl.c:222-241) on the device:
  * prep (generate_grain_y / generate_grain_uv, src/filmgrain_tmpl.c:51-144;
