@@ -46,24 +46,23 @@ template <int BPC> struct LrArgs {
     Dav1dGpuLrParams prm;
 };
 
-// padding() in closed form: tile value at tmp row r, column c (tmp (r, c)
-// is unit pixel (r - 3, c - 3))
+// padding() in closed form: the address of the tile value at tmp row r,
+// column c (tmp (r, c) is unit pixel (r - 3, c - 3)), selected without
+// branches so that a thread's loads of the whole tile go out together
 template <int BPC>
-__device__ __forceinline__ int lr_tmp(const LrArgs<BPC> &a, int r, int c) {
+__device__ __forceinline__ const typename Px<BPC>::pixel *lr_tmp_ptr(const LrArgs<BPC> &a, int r, int c) {
+    using P = typename Px<BPC>::pixel;
     const bool hl = a.edges & DGPU_LR_HAVE_LEFT, hr = a.edges & DGPU_LR_HAVE_RIGHT;
     if (!hr && c >= a.w + 3) c = a.w + 2;   // :110-118
     if (!hl && c < 3) c = 3;                // :120-126
     const int x = c - 3;
-    if (r < 3) {
-        if (a.edges & DGPU_LR_HAVE_TOP) return a.top[(r == 2) * a.ts + x];
-        return x < 0 && a.left ? a.left[x + 4] : a.src[x];
-    }
-    if (r < a.h + 3) {
-        const int j = r - 3;
-        return x < 0 && a.left ? a.left[j * 4 + x + 4] : a.src[(ptrdiff_t)j * a.ss + x];
-    }
-    if (a.edges & DGPU_LR_HAVE_BOTTOM) return a.bot[(r > a.h + 3) * a.bs + x];
-    return x < 0 && a.left ? a.left[(a.h - 1) * 4 + x + 4] : a.src[(ptrdiff_t)(a.h - 1) * a.ss + x];
+    const bool top = r < 3, bot = r >= a.h + 3;
+    // the unit row the value comes from when no lpf row replaces it
+    const int j = top ? 0 : bot ? a.h - 1 : r - 3;
+    const P *p = x < 0 && a.left ? a.left + j * 4 + x + 4 : a.src + (ptrdiff_t)j * a.ss + x;
+    if (top && (a.edges & DGPU_LR_HAVE_TOP)) p = a.top + (r == 2) * a.ts + x;
+    if (bot && (a.edges & DGPU_LR_HAVE_BOTTOM)) p = a.bot + (r > a.h + 3) * a.bs + x;
+    return p;
 }
 
 // Vertical box sums of radius R for selfguided_filter's box_sum (:373-376):
@@ -75,9 +74,12 @@ constexpr int kLrVH = 66;   // rows of the vertical sums: unit rows -1..64
 template <int R>
 __device__ __forceinline__ void lr_vsums(const int (*T)[kLrTW], int (*VS)[kLrTW], int (*VQ)[kLrTW], int h, int sw) {
     constexpr int CH = 11;   // rows per chunk
-    const int ncol = sw + 6, nrow = h + 2, nchunk = (nrow + CH - 1) / CH;
-    for (int t = threadIdx.x; t < ncol * nchunk; t += 256) {
-        const int ck = t / ncol, c = t - ck * ncol;
+    // (every index below is divided by a compile-time stride: a division by
+    // a runtime strip width cost ~40 VALU per use and dominated the kernel)
+    const int nrow = h + 2, nchunk = (nrow + CH - 1) / CH;
+    for (int t = threadIdx.x; t < kLrTW * nchunk; t += 256) {
+        const int ck = t / kLrTW, c = t - ck * kLrTW;
+        if (c >= sw + 6) continue;
         const int jj0 = ck * CH, jj1 = min(jj0 + CH, nrow);
         int s = 0, q = 0;   // tile rows jj + 2 - R .. jj + 2 + R (unit row jj - 1 is tile row jj + 2)
 #pragma unroll
@@ -102,7 +104,7 @@ __device__ __forceinline__ void lr_vsums(const int (*T)[kLrTW], int (*VS)[kLrTW]
 // for box radius R (n = 25 or 9): the horizontal sum of the vertical sums
 template <int R>
 __device__ __forceinline__ void lr_ab(const int (*VS)[kLrTW], const int (*VQ)[kLrTW], int jj, int ii, unsigned s,
-                                     int bd8, int &A, int &B) {
+                                     int bd8, const uint8_t *x_by_x, int &A, int &B) {
     constexpr int n = (2 * R + 1) * (2 * R + 1);
     constexpr unsigned one_by_x = n == 25 ? 164 : 455;
     int sum = 0, sumsq = 0;
@@ -115,7 +117,7 @@ __device__ __forceinline__ void lr_ab(const int (*VS)[kLrTW], const int (*VQ)[kL
     const int b = (sum + ((1 << bd8) >> 1)) >> bd8;
     const unsigned p = (unsigned)max(a * n - b * b, 0);
     const unsigned z = (p * s + (1u << 19)) >> 20;
-    const unsigned x = dspt_sgr_x_by_x[min(z, 255u)];
+    const unsigned x = x_by_x[min(z, 255u)];   // the block's LDS copy
     A = (int)((x * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
     B = (int)x;
 }
@@ -129,23 +131,41 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     __shared__ int AB[2][66][kLrSW + 2];   // A, B at unit rows -1..h, strip columns -1..sw
     // Wiener's horizontal pass, or the self-guided vertical box sums
     __shared__ int SCR[2 * kLrVH * kLrTW];
+    // sgr_x_by_x in LDS: a global-memory lookup per A / B position put one
+    // memory round trip per loop iteration on the block's critical path
+    __shared__ uint8_t XBX[256];
+    if (a.kind) XBX[threadIdx.x] = dspt_sgr_x_by_x[threadIdx.x];
     int(*HOR)[kLrSW] = reinterpret_cast<int(*)[kLrSW]>(SCR);
     int(*VS)[kLrTW] = reinterpret_cast<int(*)[kLrTW]>(SCR);
     int(*VQ)[kLrTW] = reinterpret_cast<int(*)[kLrTW]>(SCR + kLrVH * kLrTW);
     static_assert(kLrTH * kLrSW <= 2 * kLrVH * kLrTW, "HOR fits the scratch");
     const int sw = min(kLrSW, a.w - x0), h = a.h;
     const int bd8 = bits_of(a.bdmax) - 8;
-    for (int k = threadIdx.x; k < (h + 6) * (sw + 6); k += 256) {
-        const int r = k / (sw + 6), c = k - r * (sw + 6);
-        T[r][c] = lr_tmp<BPC>(a, r, x0 + c);
+    {   // every load of the thread's share first, then the LDS writes
+        constexpr int NL = (kLrTH * kLrTW + 255) / 256;
+        const int n = (h + 6) * kLrTW;
+        int tv[NL];
+#pragma unroll
+        for (int m = 0; m < NL; m++) {
+            const int k = threadIdx.x + 256 * m;
+            const int r = k / kLrTW, c = k - r * kLrTW;
+            tv[m] = k < n && c < sw + 6 ? (int)*lr_tmp_ptr<BPC>(a, r, x0 + c) : 0;
+        }
+#pragma unroll
+        for (int m = 0; m < NL; m++) {
+            const int k = threadIdx.x + 256 * m;
+            const int r = k / kLrTW, c = k - r * kLrTW;
+            if (k < n) T[r][c] = tv[m];
+        }
     }
     __syncthreads();
     constexpr int NP = (64 * kLrSW + 255) / 256;
     if (a.kind == 0) {   // wiener_c, :157-189
         const int bd = bd8 + 8;
         const int rbh = 3 + (bd == 12) * 2, clip_limit = 1 << (bd + 1 + 7 - rbh);
-        for (int k = threadIdx.x; k < (h + 6) * sw; k += 256) {
-            const int r = k / sw, i = k - r * sw;
+        for (int k = threadIdx.x; k < (h + 6) * kLrSW; k += 256) {
+            const int r = k / kLrSW, i = k % kLrSW;
+            if (i >= sw) continue;
             int sum = 1 << (bd + 6);
             if (BPC == 8) sum += T[r][i + 3] * 128;
 #pragma unroll
@@ -154,8 +174,9 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
         }
         __syncthreads();
         const int rbv = 11 - (bd == 12) * 2, round_offset = 1 << (bd + (rbv - 1));
-        for (int k = threadIdx.x; k < h * sw; k += 256) {
-            const int j = k / sw, i = k - j * sw;
+        for (int k = threadIdx.x; k < h * kLrSW; k += 256) {
+            const int j = k / kLrSW, i = k % kLrSW;
+            if (i >= sw) continue;
             int sum = -round_offset;
 #pragma unroll
             for (int t = 0; t < 7; t++) sum += HOR[j + t][i] * a.prm.filter[1][t];
@@ -173,12 +194,12 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
         else lr_vsums<1>(T, VS, VQ, h, sw);
         __syncthreads();
         // A / B at unit rows -1..h (every other row from -1 for 5x5, :375)
-        for (int k = threadIdx.x; k < (h + 2) * (sw + 2); k += 256) {
-            const int jj = k / (sw + 2), ii = k - jj * (sw + 2), j = jj - 1;
-            if (five && !(j & 1)) continue;
+        for (int k = threadIdx.x; k < (h + 2) * (kLrSW + 2); k += 256) {
+            const int jj = k / (kLrSW + 2), ii = k - jj * (kLrSW + 2), j = jj - 1;
+            if (ii >= sw + 2 || (five && !(j & 1))) continue;
             int A, B;
-            if (five) lr_ab<2>(VS, VQ, jj, ii, a.prm.sgr.s0, bd8, A, B);
-            else lr_ab<1>(VS, VQ, jj, ii, a.prm.sgr.s1, bd8, A, B);
+            if (five) lr_ab<2>(VS, VQ, jj, ii, a.prm.sgr.s0, bd8, XBX, A, B);
+            else lr_ab<1>(VS, VQ, jj, ii, a.prm.sgr.s1, bd8, XBX, A, B);
             AB[0][jj][ii] = A;
             AB[1][jj][ii] = B;
         }
@@ -187,8 +208,9 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
 #pragma unroll
         for (int m = 0; m < NP; m++) {
             const int k = threadIdx.x + 256 * m;
-            if (k >= h * sw) break;
-            const int j = k / sw, i = k - j * sw, jj = j + 1, ii = i + 1;
+            if (k >= h * kLrSW) break;
+            const int j = k / kLrSW, i = k % kLrSW, jj = j + 1, ii = i + 1;
+            if (i >= sw) continue;
             const int px = T[j + 3][i + 3];
             const int(*A)[kLrSW + 2] = AB[0];
             const int(*B)[kLrSW + 2] = AB[1];
@@ -220,9 +242,10 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
 #pragma unroll
     for (int m = 0; m < NP; m++) {
         const int k = threadIdx.x + 256 * m;
-        if (k >= h * sw) break;
-        const int j = k / sw, i = k - j * sw;
-        a.dst[(size_t)j * a.ds + x0 + i] = (P)clampi(T[j + 3][i + 3] + ((v[m] + (1 << 10)) >> 11), 0, a.bdmax);
+        if (k >= h * kLrSW) break;
+        const int j = k / kLrSW, i = k % kLrSW;
+        if (i < sw)
+            a.dst[(size_t)j * a.ds + x0 + i] = (P)clampi(T[j + 3][i + 3] + ((v[m] + (1 << 10)) >> 11), 0, a.bdmax);
     }
 }
 
@@ -289,10 +312,18 @@ __global__ __launch_bounds__(256) void k_lr_frame(LrFrameArgs<BPC> f) {
     const P *src = f.in[pl] + (size_t)y0 * f.is[pl];
     P *dst = f.out[pl] + (size_t)y0 * f.os[pl];
     if (!f.restore[pl] || u.type == 0) {   // copied
-        const int sw = min(kLrSW, w - xs);
-        for (int t = threadIdx.x; t < (y1 - y0) * sw; t += 256) {
-            const int j = t / sw, i = t - j * sw;
-            dst[(size_t)j * f.os[pl] + xs + i] = src[(size_t)j * f.is[pl] + xs + i];
+        const int sw = min(kLrSW, w - xs), n = (y1 - y0) * kLrSW;   // <= 64 rows x 32
+        constexpr int NC = (64 * kLrSW + 255) / 256;
+        P cv[NC];
+#pragma unroll
+        for (int m = 0; m < NC; m++) {   // loads first, then the stores
+            const int t = threadIdx.x + 256 * m, j = t / kLrSW, i = t % kLrSW;
+            if (t < n && i < sw) cv[m] = src[(size_t)j * f.is[pl] + xs + i];
+        }
+#pragma unroll
+        for (int m = 0; m < NC; m++) {
+            const int t = threadIdx.x + 256 * m, j = t / kLrSW, i = t % kLrSW;
+            if (t < n && i < sw) dst[(size_t)j * f.os[pl] + xs + i] = cv[m];
         }
         return;
     }

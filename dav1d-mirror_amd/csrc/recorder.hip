@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <chrono>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include "dav1d_gpu.h"
@@ -103,11 +104,12 @@ struct PinnedBuf {   // page-locked staging, so the uploads do not wait for the 
     }
 };
 
-// LSD radix sort of 64-bit keys, 16-bit digits
-void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int bits) {
+// LSD radix sort of 64-bit keys on bits [lo, hi), 16-bit digits (stable, so
+// keys whose low bits hold their input index need not sort those)
+void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int lo, int hi) {
     tmp.resize(k.size());
     std::vector<uint32_t> cnt(1 << 16);
-    for (int sh = 0; sh < bits; sh += 16) {
+    for (int sh = lo; sh < hi; sh += 16) {
         std::fill(cnt.begin(), cnt.end(), 0);
         for (uint64_t v : k) cnt[(v >> sh) & 0xffff]++;
         uint32_t acc = 0;
@@ -118,6 +120,44 @@ void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int bits) 
         }
         for (uint64_t v : k) tmp[cnt[(v >> sh) & 0xffff]++] = v;
         k.swap(tmp);
+    }
+}
+
+// emu_edge per transform unit (src/recon_tmpl.c:986-999): a footprint that
+// leaves its reference picture is copied, every read clamped, into a scratch
+// plane of kEmuStride pixels per row, one (H + 7)-row band per copy
+constexpr int kEmuStride = 128;
+struct EmuJob {
+    int32_t x0, y0;   // the footprint's top-left in the reference (may be outside)
+    int32_t r0;       // its first scratch row
+    uint8_t w, h, slot, plane;
+};
+static_assert(sizeof(EmuJob) == 16, "EmuJob layout");
+
+struct EmuArgs {
+    const void *ref[DGPU_MAX_REFS - 1][3];
+    int32_t stride[DGPU_MAX_REFS - 1][3];   // pixels
+    int32_t w[DGPU_MAX_REFS - 1][3], h[DGPU_MAX_REFS - 1][3];
+    void *out;
+    const EmuJob *jobs;
+    int32_t n;
+};
+
+// one 64-lane workgroup per footprint: lanes along the row, clamped reads
+template <typename P>
+__global__ __launch_bounds__(64) void k_emu_footprints(EmuArgs a) {
+    const int j = blockIdx.x;
+    if (j >= a.n) return;
+    const EmuJob jb = a.jobs[j];
+    const P *ref = static_cast<const P *>(a.ref[jb.slot][jb.plane]);
+    const int rs = a.stride[jb.slot][jb.plane], rw = a.w[jb.slot][jb.plane], rh = a.h[jb.slot][jb.plane];
+    P *out = static_cast<P *>(a.out) + (size_t)jb.r0 * kEmuStride;
+    for (int c = threadIdx.x; c < jb.w; c += 64) {
+        const int x = min(max(jb.x0 + c, 0), rw - 1);
+        for (int i = 0; i < jb.h; i++) {
+            const int y = min(max(jb.y0 + i, 0), rh - 1);
+            out[(size_t)i * kEmuStride + c] = ref[(size_t)y * rs + x];
+        }
     }
 }
 
@@ -134,19 +174,18 @@ struct Dav1dGpuRecorder {
     int bpc, bdmax, width, height, device;
     std::vector<Dav1dGpuRecBlock> blocks;
     std::vector<Residual> residuals;
-    std::vector<int32_t> coef32;   // compact regions (int32 for both ABIs; narrowed at flush)
+    std::vector<uint8_t> coefb;    // compact regions in the ABI's coefficient type (int16 / int32)
     // flush products (kept alive while the device may still read them)
     std::vector<int32_t> unit_start, class_start, rec_start, run_start;
     std::vector<Unit> cells;
     std::vector<uint64_t> keys, keys_tmp;
     std::vector<int32_t> rank;
     std::vector<int32_t> prod_start, prod, dep_start, deps;   // producers: decode order, then level order
-    std::vector<Dav1dGpuUnit> h_units;
-    std::vector<Dav1dGpuIntraEdge> h_recs;
-    std::vector<uint8_t> h_coef;
-    PinnedBuf pin;   // units | recs | coefficients, copied in one sequential pass
+    std::vector<EmuJob> emu;     // clamped footprint copies of this flush
+    std::vector<uint8_t> h_host;   // DAV1D_GPU_REC_HOSTONLY: stands in for the pinned buffer
+    PinnedBuf pin;   // units | recs | coefficients | emu jobs, written in place by the fill
     PinnedBuf flag;  // the last flush's wavefront error word, copied back on its stream
-    DevBuf d_units, d_recs, d_coef, d_edges, d_work;
+    DevBuf d_units, d_recs, d_coef, d_edges, d_work, d_emu, d_emu_jobs;
     hipEvent_t done = nullptr;
     bool pending_check = false;   // the last flush's error word not read yet
     int32_t last_units = 0, last_levels = 0;
@@ -177,6 +216,8 @@ extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
         r->d_coef.release();
         r->d_edges.release();
         r->d_work.release();
+        r->d_emu.release();
+        r->d_emu_jobs.release();
     }
     delete r;
 }
@@ -200,7 +241,7 @@ extern "C" int dav1d_gpu_rec_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *
     if (b->kind == DGPU_PRED_CFL && (b->plane == 0 || b->w != t.w || b->h != t.h || t.w != t.h || t.w > 32))
         return -1;   // CfL: one unit per chroma block (cfl_ac + cfl_pred, :1372-1414)
     if (!inter && b->mode > 13) return -1;
-    if (inter && (b->ref[0] >= DGPU_MAX_REFS || b->ref[1] >= DGPU_MAX_REFS || b->filter2d > 9)) return -1;
+    if (inter && (b->ref[0] >= DGPU_REC_EMU_SLOT || b->ref[1] >= DGPU_REC_EMU_SLOT || b->filter2d > 9)) return -1;
     if (b->tile_x0 < 0 || b->tile_y0 < 0 || b->tile_x1 > pw || b->tile_y1 > ph || b->x < b->tile_x0 ||
         b->y < b->tile_y0 || b->x + b->w > b->tile_x1 || b->y + b->h > b->tile_y1)
         return -1;
@@ -216,12 +257,18 @@ extern "C" int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int
     const TxDim t = kTx[tx];
     if (x < 0 || y < 0 || x + t.w > pw || y + t.h > ph || (x & 3) || (y & 3)) return -1;
     const int sw = std::min(t.w, 32), sh = std::min(t.h, 32);
-    Residual res{plane, x, y, tx, txtp, 0, 0, r->coef32.size()};
+    const size_t cb = r->bpc == 8 ? 2 : 4;
+    Residual res{plane, x, y, tx, txtp, 0, 0, r->coefb.size() / cb};
     auto at = [&](int cx, int cy) -> int32_t {   // the reference's layout: coef[cy + cx * sh]
         return r->bpc == 8 ? ((const int16_t *)coef)[cy + cx * sh] : ((const int32_t *)coef)[cy + cx * sh];
     };
+    auto put = [&](int cx, int cy) {   // appended in the ABI's coefficient type
+        const size_t o = r->coefb.size();
+        r->coefb.resize(o + cb);
+        memcpy(&r->coefb[o], (const uint8_t *)coef + (size_t)(cy + cx * sh) * cb, cb);
+    };
     if (eob == 0 && txtp == DGPU_DCT_DCT) {   // the DC-only call (src/itx_tmpl.c:53)
-        r->coef32.push_back(at(0, 0));
+        put(0, 0);
     } else {   // the stored region: the bounding box of the non-zero coefficients
         int nzw = 1, nzh = 1;
         for (int cx = 0; cx < sw; cx++)
@@ -233,7 +280,7 @@ extern "C" int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int
         res.nzw = nzw;
         res.nzh = nzh;
         for (int cx = 0; cx < nzw; cx++)
-            for (int cy = 0; cy < nzh; cy++) r->coef32.push_back(at(cx, cy));
+            for (int cy = 0; cy < nzh; cy++) put(cx, cy);
     }
     r->residuals.push_back(res);
     return 0;
@@ -317,6 +364,10 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         lv[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
         own[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
     }
+    lap("maps");
+    r->emu.clear();
+    int32_t emu_rows = 0;
+    size_t edge_px = 0;   // the edge pool (the staged path's), decode order
     std::vector<int32_t> &prod_start = r->prod_start, &prod = r->prod;
     prod_start.assign(1, 0);
     prod.clear();
@@ -366,10 +417,28 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         if (k == 0 || b.kind != DGPU_PRED_INTER)
                             if (!ref || !ref[rr][p].data) return -1;
                         const int rs = ref ? (int)(ref[rr][p].stride / bpp) : 0;
-                        u.p.inter.src_off[k] = (uy + (b.mvy[k] >> 4)) * rs + ux + (b.mvx[k] >> 4);
+                        const int ix = ux + (b.mvx[k] >> 4), iy = uy + (b.mvy[k] >> 4);
+                        u.p.inter.src_off[k] = iy * rs + ix;
                         u.p.inter.mx[k] = (uint8_t)(b.mvx[k] & 15);
                         u.p.inter.my[k] = (uint8_t)(b.mvy[k] & 15);
                         u.p.inter.ref[k] = (uint8_t)rr;
+                        if (k == 0 || b.kind != DGPU_PRED_INTER) {
+                            // the unit kernel reads the footprint with both
+                            // 8-tap margins whatever the fraction, and its
+                            // aligned row loads may run up to 16 bytes past
+                            // the last pixel: direct only when all of that
+                            // stays inside the picture, else a clamped copy
+                            const int rw = ref[rr][p].w, rh = ref[rr][p].h;
+                            const bool inside = ix - 3 >= 0 && iy - 3 >= 0 && ix + t.w + 4 <= rw &&
+                                                iy + t.h + 4 <= rh && (iy + t.h + 4 < rh || (ix + t.w + 4) * bpp + 16 <= rs * bpp);
+                            if (!inside) {
+                                r->emu.push_back(EmuJob{ix - 3, iy - 3, emu_rows, (uint8_t)(t.w + 7), (uint8_t)(t.h + 7),
+                                                        (uint8_t)rr, (uint8_t)p});
+                                u.p.inter.src_off[k] = (emu_rows + 3) * kEmuStride + 3;
+                                u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
+                                emu_rows += t.h + 7;
+                            }
+                        }
                     }
                     u.p.inter.filter2d = b.filter2d;
                     u.p.inter.weight = b.kind == DGPU_PRED_INTER_WAVG ? b.weight : 0;
@@ -393,6 +462,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         u.p.cfl.luma_off = (2 * uy) * (int)(dst[0].stride / bpp) + 2 * ux;
                     }
                     e.flags = (uint8_t)fl;
+                    u.p.intra.edge_off = (int32_t)(edge_px + 2 * t.h);   // CFL: the same field
+                    edge_px += 2 * t.h + 2 * t.w + 1;
                     const int m = remap_mode(e.mode, e.angle, hl, ht);
                     nd = kNeeds[m];
                     c.sortmode = 16 + m;
@@ -461,7 +532,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     const int n = (int)cells.size();
 
     // 4. level order, size classes inside a level, then kind / mode / type:
-    //    one radix sort of (key << 21 | index)
+    //    one LSD radix sort of (key << 21 | decode index) on the key bits only
+    //    (stable: equal keys stay in decode order).  Key: level | tx (5) |
+    //    pred (4) | mode (6) | type (5, NO_RESIDUAL last)
     if (n >= (1 << 21)) return -1;
     std::vector<uint64_t> &keys = r->keys;
     keys.resize(n);
@@ -470,11 +543,15 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         const Unit &c = cells[i];
         if (c.level >= (1 << 16)) return -1;
         max_level = std::max(max_level, c.level);
-        const uint64_t key = (uint64_t)c.level << 24 | (uint64_t)c.u.tx << 19 | (uint64_t)c.u.pred << 15 |
-                             (uint64_t)(c.sortmode & 63) << 9 | (uint64_t)(c.u.txtp == DGPU_NO_RESIDUAL ? 511 : c.u.txtp);
+        const uint64_t key = (uint64_t)c.level << 20 | (uint64_t)c.u.tx << 15 | (uint64_t)c.u.pred << 11 |
+                             (uint64_t)(c.sortmode & 63) << 5 | (uint64_t)(c.u.txtp == DGPU_NO_RESIDUAL ? 31 : c.u.txtp);
         keys[i] = key << 21 | (uint64_t)i;
     }
-    radix_sort(keys, r->keys_tmp, 64);
+    {
+        int lb = 0;
+        while ((1 << lb) <= max_level) lb++;
+        radix_sort(keys, r->keys_tmp, 21, 21 + 20 + lb);
+    }
     lap("sort");
     const int n_levels = n ? max_level + 1 : 0;
     r->unit_start.assign(n_levels + 1, 0);
@@ -485,54 +562,60 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     rank.resize(n);
     for (int i = 0; i < n; i++) {
         const uint64_t k = keys[i];
-        const int ci = (int)(k & ((1u << 21) - 1)), level = (int)(k >> 45), tx = (int)((k >> 40) & 31);
+        const int ci = (int)(k & ((1u << 21) - 1)), level = (int)(k >> 41), tx = (int)((k >> 36) & 31);
         rank[ci] = i;
         r->unit_start[level + 1] = i + 1;
         r->class_start[(size_t)level * (NC + 1) + tx + 1]++;
-    }
-    // then one sequential pass in decode order, scattering to the ranks
-    // (reading the cells in rank order measured 13 ms of cache misses at 4K);
-    // the coefficient pool stays in decode order
-    r->h_units.resize((size_t)n);
-    r->h_recs.resize((size_t)n);
-    r->h_coef.resize(r->coef32.size() * cb);
-    Dav1dGpuUnit *hu = r->h_units.data();
-    Dav1dGpuIntraEdge *hr = r->h_recs.data();
-    if (cb == 2) {
-        int16_t *d16 = (int16_t *)r->h_coef.data();
-        for (size_t k = 0; k < r->coef32.size(); k++) d16[k] = (int16_t)r->coef32[k];
-    } else if (!r->coef32.empty()) {
-        memcpy(r->h_coef.data(), r->coef32.data(), r->coef32.size() * 4);
-    }
-    const size_t coef_at = r->coef32.size();
-    size_t edge_px = 0;
-    for (int ci = 0; ci < n; ci++) {
-        const Unit &c = cells[ci];
-        const int i = rank[ci];
-        Dav1dGpuUnit u = c.u;   // coef_off is already the decode-order pool offset
-        if (u.pred == DGPU_PRED_INTRA || u.pred == DGPU_PRED_CFL) {   // an edge slot (the staged path's pool)
-            const TxDim t = kTx[u.tx];
-            u.p.intra.edge_off = (int32_t)(edge_px + 2 * t.h);
-            edge_px += 2 * t.h + 2 * t.w + 1;
-        }
-        hu[i] = u;
-        Dav1dGpuIntraEdge e = c.rec;
-        e.unit = i;
-        hr[i] = e;
     }
     // the producer lists in level order (the persistent kernel's dataflow waits)
     r->dep_start.assign((size_t)n + 1, 0);
     for (int ci = 0; ci < n; ci++) r->dep_start[rank[ci] + 1] = prod_start[ci + 1] - prod_start[ci];
     for (int i = 0; i < n; i++) r->dep_start[i + 1] += r->dep_start[i];
     r->deps.resize(prod.size());
-    for (int ci = 0; ci < n; ci++) {
-        int32_t *o = &r->deps[r->dep_start[rank[ci]]];
-        for (int k = prod_start[ci]; k < prod_start[ci + 1]; k++) *o++ = rank[prod[k]];
-    }
     for (int l = 0; l < n_levels; l++) {
         if (r->unit_start[l + 1] < r->unit_start[l]) r->unit_start[l + 1] = r->unit_start[l];   // (levels are dense)
         int32_t *cs = &r->class_start[(size_t)l * (NC + 1)];
         for (int k = 0; k < NC; k++) cs[k + 1] += cs[k];
+    }
+    // 5. the upload image, written in place (page-locked, or a host vector
+    //    for DAV1D_GPU_REC_HOSTONLY): units and records scattered to their
+    //    ranks, the coefficient pool (decode order) and the emu jobs, by
+    //    several threads over disjoint ranges
+    const size_t coef_at = r->coefb.size() / cb;
+    const size_t bu = (size_t)n * sizeof(Dav1dGpuUnit), br = (size_t)n * sizeof(Dav1dGpuIntraEdge),
+                 bc = coef_at * cb, be = r->emu.size() * sizeof(EmuJob);
+    uint8_t *img;
+    if (host_only) {
+        r->h_host.resize(bu + br + bc + be);
+        img = r->h_host.data();
+    } else {
+        if (r->pin.grow(bu + br + bc + be)) return -3;
+        img = (uint8_t *)r->pin.p;
+    }
+    Dav1dGpuUnit *hu = (Dav1dGpuUnit *)img;
+    Dav1dGpuIntraEdge *hr = (Dav1dGpuIntraEdge *)(img + bu);
+    {
+        const int nt = n < 32768 ? 1 : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        auto work = [&](int t) {
+            const int c0 = (int)((int64_t)n * t / nt), c1 = (int)((int64_t)n * (t + 1) / nt);
+            for (int ci = c0; ci < c1; ci++) {
+                const Unit &c = cells[ci];
+                const int i = rank[ci];
+                hu[i] = c.u;   // coef_off / edge_off are decode-order pool offsets
+                Dav1dGpuIntraEdge e = c.rec;
+                e.unit = i;
+                hr[i] = e;
+                int32_t *o = &r->deps[r->dep_start[i]];
+                for (int k = prod_start[ci]; k < prod_start[ci + 1]; k++) *o++ = rank[prod[k]];
+            }
+            const size_t b0 = bc * t / nt, b1 = bc * (t + 1) / nt;
+            if (b1 > b0) memcpy(img + bu + br + b0, r->coefb.data() + b0, b1 - b0);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; t++) th.emplace_back(work, t);
+        work(0);
+        for (auto &x : th) x.join();
+        if (be) memcpy(img + bu + br + bc, r->emu.data(), be);
     }
     lap("fill");
     r->rec_start = r->unit_start;
@@ -542,7 +625,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     if (!n || host_only) {
         r->blocks.clear();
         r->residuals.clear();
-        r->coef32.clear();
+        r->coefb.clear();
         return 0;
     }
 
@@ -564,17 +647,32 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         r->d_coef.grow(std::max<size_t>(coef_at * cb, 16)) || r->d_edges.grow(std::max<size_t>(edge_px * bpp, 16)) ||
         r->d_work.grow((size_t)wsb))
         return -3;
-    const size_t bu = (size_t)n * sizeof(Dav1dGpuUnit), br = (size_t)n * sizeof(Dav1dGpuIntraEdge),
-                 bc = coef_at * cb;
-    if (r->pin.grow(bu + br + bc)) return -3;
-    uint8_t *pin = (uint8_t *)r->pin.p;
-    memcpy(pin, hu, bu);
-    memcpy(pin + bu, hr, br);
-    if (bc) memcpy(pin + bu + br, r->h_coef.data(), bc);
+    if (be && (r->d_emu_jobs.grow(be) || r->d_emu.grow((size_t)emu_rows * kEmuStride * bpp + 256))) return -3;
+    const uint8_t *pin = img;
     if (hipMemcpyAsync(r->d_units.p, pin, bu, hipMemcpyHostToDevice, st) ||
         hipMemcpyAsync(r->d_recs.p, pin + bu, br, hipMemcpyHostToDevice, st) ||
-        (bc && hipMemcpyAsync(r->d_coef.p, pin + bu + br, bc, hipMemcpyHostToDevice, st)))
+        (bc && hipMemcpyAsync(r->d_coef.p, pin + bu + br, bc, hipMemcpyHostToDevice, st)) ||
+        (be && hipMemcpyAsync(r->d_emu_jobs.p, pin + bu + br + bc, be, hipMemcpyHostToDevice, st)))
         return -3;
+    if (be) {   // the clamped footprints, before the wavefront reads them
+        EmuArgs ea;
+        memset(&ea, 0, sizeof(ea));
+        for (int k = 0; k < DGPU_MAX_REFS - 1; k++)
+            for (int p = 0; p < 3; p++) {
+                ea.ref[k][p] = ref[k][p].data;
+                ea.stride[k][p] = (int32_t)(ref[k][p].stride / bpp);
+                ea.w[k][p] = ref[k][p].w;
+                ea.h[k][p] = ref[k][p].h;
+            }
+        ea.out = r->d_emu.p;
+        ea.jobs = (const EmuJob *)r->d_emu_jobs.p;
+        ea.n = (int32_t)r->emu.size();
+        if (r->bpc == 8)
+            k_emu_footprints<uint8_t><<<dim3(ea.n), 64, 0, st>>>(ea);
+        else
+            k_emu_footprints<uint16_t><<<dim3(ea.n), 64, 0, st>>>(ea);
+        if (hipGetLastError() != hipSuccess) return -3;
+    }
     s.workspace = r->d_work.p;
     s.workspace_bytes = wsb;
     Dav1dGpuFrameBatch fb;
@@ -585,7 +683,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         fb.dst[p] = dst[p];
         eb.pic[p] = dst[p];
         if (ref)
-            for (int k = 0; k < DGPU_MAX_REFS; k++) fb.ref[k][p] = ref[k][p];
+            for (int k = 0; k < DGPU_REC_EMU_SLOT; k++) fb.ref[k][p] = ref[k][p];
+        if (be) fb.ref[DGPU_REC_EMU_SLOT][p] = Dav1dGpuPlane{r->d_emu.p, (int64_t)kEmuStride * bpp, kEmuStride, emu_rows};
     }
     eb.sb_log2[0] = 6;
     eb.sb_log2[1] = eb.sb_log2[2] = 5;
@@ -616,6 +715,6 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     r->pending_check = true;
     r->blocks.clear();
     r->residuals.clear();
-    r->coef32.clear();
+    r->coefb.clear();
     return 0;
 }

@@ -692,8 +692,18 @@ int dav1d_gpu_recon_intra_frame_16bpc(const Dav1dGpuFrameBatch *recon, const Dav
  * TOP_HAS_RIGHT / LEFT_HAS_BOTTOM from the block's edge flags), schedules
  * dependency levels (inter units at level 0; intra units after every unit
  * whose pixels their edges or CfL luma read) and runs the persistent
- * wavefront.  Host C++ (csrc/recorder.cpp); device buffers are the
- * recorder's own.  4:2:0 only. */
+ * wavefront.  Host C++ (csrc/recorder.hip); device buffers are the
+ * recorder's own.  4:2:0 only.
+ *
+ * References need no padding: mc() replaces a footprint that leaves the
+ * reference picture with an emu_edge copy (src/recon_tmpl.c:986-999,
+ * src/mc_tmpl.c:827-875), i.e. every read is clamped to the picture.  The
+ * recorder does the same per transform unit: a unit whose footprint (with
+ * the 8-tap margins) is not inside ref[slot][plane].w x .h gets a clamped
+ * copy of it in a device scratch plane (filled on the flush's stream
+ * before the wavefront), read through reference slot DGPU_REC_EMU_SLOT,
+ * which callers therefore leave unused. */
+#define DGPU_REC_EMU_SLOT (DGPU_MAX_REFS - 1)
 typedef struct Dav1dGpuRecorder Dav1dGpuRecorder;
 
 typedef struct Dav1dGpuRecBlock {
@@ -732,8 +742,9 @@ int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int y, int tx,
 /* Build, upload and launch everything recorded since the last flush on
  * `stream` (the recorder waits for its previous flush before reusing its
  * buffers).  dst: the picture being reconstructed (CfL reads its luma);
- * ref: reference planes for inter blocks, edge-replicated as for
- * dav1d_gpu_recon_*.  Returns 0, -1 bad arguments, or a launch error. */
+ * ref: reference planes for inter blocks (w / h: the picture size every
+ * read is clamped to; no padding needed; slot DGPU_REC_EMU_SLOT is the
+ * recorder's).  Returns 0, -1 bad arguments, or a launch error. */
 int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane dst[3],
                              const Dav1dGpuPlane ref[DGPU_MAX_REFS][3], void *stream);
 /* Levels and units of the last flush (diagnostics). */
