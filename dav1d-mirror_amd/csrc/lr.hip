@@ -46,25 +46,6 @@ template <int BPC> struct LrArgs {
     Dav1dGpuLrParams prm;
 };
 
-// padding() in closed form: the address of the tile value at tmp row r,
-// column c (tmp (r, c) is unit pixel (r - 3, c - 3)), selected without
-// branches so that a thread's loads of the whole tile go out together
-template <int BPC>
-__device__ __forceinline__ const typename Px<BPC>::pixel *lr_tmp_ptr(const LrArgs<BPC> &a, int r, int c) {
-    using P = typename Px<BPC>::pixel;
-    const bool hl = a.edges & DGPU_LR_HAVE_LEFT, hr = a.edges & DGPU_LR_HAVE_RIGHT;
-    if (!hr && c >= a.w + 3) c = a.w + 2;   // :110-118
-    if (!hl && c < 3) c = 3;                // :120-126
-    const int x = c - 3;
-    const bool top = r < 3, bot = r >= a.h + 3;
-    // the unit row the value comes from when no lpf row replaces it
-    const int j = top ? 0 : bot ? a.h - 1 : r - 3;
-    const P *p = x < 0 && a.left ? a.left + j * 4 + x + 4 : a.src + (ptrdiff_t)j * a.ss + x;
-    if (top && (a.edges & DGPU_LR_HAVE_TOP)) p = a.top + (r == 2) * a.ts + x;
-    if (bot && (a.edges & DGPU_LR_HAVE_BOTTOM)) p = a.bot + (r > a.h + 3) * a.bs + x;
-    return p;
-}
-
 // Vertical box sums of radius R for selfguided_filter's box_sum (:373-376):
 // VS[jj][c] = sum of tile column c over the 2R + 1 rows around unit row
 // jj - 1, VQ the same of the squares, for jj = 0..h + 1 and every tile
@@ -72,7 +53,8 @@ __device__ __forceinline__ const typename Px<BPC>::pixel *lr_tmp_ptr(const LrArg
 // reads per row instead of 2R + 1).
 constexpr int kLrVH = 66;   // rows of the vertical sums: unit rows -1..64
 template <int R>
-__device__ __forceinline__ void lr_vsums(const int (*T)[kLrTW], int (*VS)[kLrTW], int (*VQ)[kLrTW], int h, int sw) {
+__device__ __forceinline__ void lr_vsums(const int16_t (*T)[kLrTW], int16_t (*VS)[kLrTW], int (*VQ)[kLrTW], int h,
+                                         int sw) {
     constexpr int CH = 11;   // rows per chunk
     // (every index below is divided by a compile-time stride: a division by
     // a runtime strip width cost ~40 VALU per use and dominated the kernel)
@@ -88,13 +70,13 @@ __device__ __forceinline__ void lr_vsums(const int (*T)[kLrTW], int (*VS)[kLrTW]
             s += v;
             q += v * v;
         }
-        VS[jj0][c] = s;
+        VS[jj0][c] = (int16_t)s;   // <= 5 x 4095
         VQ[jj0][c] = q;
         for (int jj = jj0 + 1; jj < jj1; jj++) {
             const int vi = T[jj + 2 + R][c], vo = T[jj + 1 - R][c];
             s += vi - vo;
             q += vi * vi - vo * vo;
-            VS[jj][c] = s;
+            VS[jj][c] = (int16_t)s;
             VQ[jj][c] = q;
         }
     }
@@ -102,8 +84,10 @@ __device__ __forceinline__ void lr_vsums(const int (*T)[kLrTW], int (*VS)[kLrTW]
 
 // A / B of selfguided_filter (:373-392) at unit position (jj - 1, ii - 1)
 // for box radius R (n = 25 or 9): the horizontal sum of the vertical sums
+// (a register-sliding variant, a thread per row segment, measured slower:
+// fewer busy lanes and a longer dependent chain per thread)
 template <int R>
-__device__ __forceinline__ void lr_ab(const int (*VS)[kLrTW], const int (*VQ)[kLrTW], int jj, int ii, unsigned s,
+__device__ __forceinline__ void lr_ab(const int16_t (*VS)[kLrTW], const int (*VQ)[kLrTW], int jj, int ii, unsigned s,
                                      int bd8, const uint8_t *x_by_x, int &A, int &B) {
     constexpr int n = (2 * R + 1) * (2 * R + 1);
     constexpr unsigned one_by_x = n == 25 ? 164 : 455;
@@ -127,66 +111,103 @@ template <int BPC>
 __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     using P = typename Px<BPC>::pixel;
     using C = typename Px<BPC>::coef;
-    __shared__ int T[kLrTH][kLrTW];
-    __shared__ int AB[2][66][kLrSW + 2];   // A, B at unit rows -1..h, strip columns -1..sw
+    // 16-bit tiles and scratch where the values fit (pixels, Wiener's clipped
+    // horizontal sums, 5-row box sums, B = x_by_x <= 255): 31.8 KB, five
+    // workgroups per CU
+    __shared__ int16_t T[kLrTH][kLrTW];
+    __shared__ int AA[66][kLrSW + 2];        // A at unit rows -1..h, strip columns -1..sw
+    __shared__ uint8_t BB[66][kLrSW + 2];    // B
     // Wiener's horizontal pass, or the self-guided vertical box sums
-    __shared__ int SCR[2 * kLrVH * kLrTW];
+    __shared__ int SCR[kLrVH * kLrTW + (kLrVH * kLrTW + 1) / 2];
     // sgr_x_by_x in LDS: a global-memory lookup per A / B position put one
     // memory round trip per loop iteration on the block's critical path
     __shared__ uint8_t XBX[256];
     if (a.kind) XBX[threadIdx.x] = dspt_sgr_x_by_x[threadIdx.x];
-    int(*HOR)[kLrSW] = reinterpret_cast<int(*)[kLrSW]>(SCR);
-    int(*VS)[kLrTW] = reinterpret_cast<int(*)[kLrTW]>(SCR);
-    int(*VQ)[kLrTW] = reinterpret_cast<int(*)[kLrTW]>(SCR + kLrVH * kLrTW);
-    static_assert(kLrTH * kLrSW <= 2 * kLrVH * kLrTW, "HOR fits the scratch");
+    int16_t(*HOR)[kLrSW] = reinterpret_cast<int16_t(*)[kLrSW]>(SCR);
+    int(*VQ)[kLrTW] = reinterpret_cast<int(*)[kLrTW]>(SCR);
+    int16_t(*VS)[kLrTW] = reinterpret_cast<int16_t(*)[kLrTW]>(SCR + kLrVH * kLrTW);
+    static_assert(kLrTH * kLrSW * 2 <= (int)sizeof(SCR), "HOR fits the scratch");
     const int sw = min(kLrSW, a.w - x0), h = a.h;
     const int bd8 = bits_of(a.bdmax) - 8;
-    {   // every load of the thread's share first, then the LDS writes
-        constexpr int NL = (kLrTH * kLrTW + 255) / 256;
-        const int n = (h + 6) * kLrTW;
-        int tv[NL];
+    {   // a thread per tile column and sixth of the rows: the column's
+        // padding() case once, then per row only the row's source; every
+        // load first, then the LDS writes
+        constexpr int RG = 256 / kLrTW, NR = (kLrTH + RG - 1) / RG;   // 6 row groups, 12 rows each
+        const int c = threadIdx.x % kLrTW, rg = threadIdx.x / kLrTW;
+        const bool hl = a.edges & DGPU_LR_HAVE_LEFT, hr = a.edges & DGPU_LR_HAVE_RIGHT;
+        int cc = x0 + c;
+        if (!hr && cc >= a.w + 3) cc = a.w + 2;   // :110-118
+        if (!hl && cc < 3) cc = 3;                // :120-126
+        const int x = cc - 3;
+        const bool lft = x < 0 && a.left;
+        const bool col_ok = rg < RG && c < sw + 6;
+        const bool ht = a.edges & DGPU_LR_HAVE_TOP, hb = a.edges & DGPU_LR_HAVE_BOTTOM;
+        int tv[NR];
 #pragma unroll
-        for (int m = 0; m < NL; m++) {
-            const int k = threadIdx.x + 256 * m;
-            const int r = k / kLrTW, c = k - r * kLrTW;
-            tv[m] = k < n && c < sw + 6 ? (int)*lr_tmp_ptr<BPC>(a, r, x0 + c) : 0;
+        for (int i = 0; i < NR; i++) {
+            const int r = rg + RG * i;
+            const int j = min(max(r - 3, 0), h - 1);
+            const P *p = lft ? a.left + j * 4 + x + 4 : a.src + (ptrdiff_t)j * a.ss + x;
+            if (r < 3 && ht) p = a.top + (r == 2) * a.ts + x;
+            if (r >= h + 3 && hb) p = a.bot + (r > h + 3) * a.bs + x;
+            tv[i] = col_ok && r < h + 6 ? (int)*p : 0;
         }
 #pragma unroll
-        for (int m = 0; m < NL; m++) {
-            const int k = threadIdx.x + 256 * m;
-            const int r = k / kLrTW, c = k - r * kLrTW;
-            if (k < n) T[r][c] = tv[m];
+        for (int i = 0; i < NR; i++) {
+            const int r = rg + RG * i;
+            if (col_ok && r < h + 6) T[r][c] = (int16_t)tv[i];
         }
     }
     __syncthreads();
     constexpr int NP = (64 * kLrSW + 255) / 256;
+    // the weighting's / Wiener vertical pass's thread layout: column wi,
+    // rows wj0 .. wj0 + wrpt - 1
+    const int wi = threadIdx.x & (kLrSW - 1), wrpt = (h + 7) >> 3, wj0 = (threadIdx.x >> 5) * wrpt;
+    static_assert(kLrSW == 32, "8 row groups of 32 columns");
     if (a.kind == 0) {   // wiener_c, :157-189
         const int bd = bd8 + 8;
         const int rbh = 3 + (bd == 12) * 2, clip_limit = 1 << (bd + 1 + 7 - rbh);
-        for (int k = threadIdx.x; k < (h + 6) * kLrSW; k += 256) {
-            const int r = k / kLrSW, i = k % kLrSW;
-            if (i >= sw) continue;
-            int sum = 1 << (bd + 6);
-            if (BPC == 8) sum += T[r][i + 3] * 128;
+        // horizontal: a thread per (row, 8 columns), its 14 tile values read once
+        for (int k = threadIdx.x; k < (h + 6) * 4; k += 256) {
+            const int r = k >> 2, i0 = (k & 3) * 8;
+            if (i0 >= sw) continue;
+            int tv[14];
 #pragma unroll
-            for (int t = 0; t < 7; t++) sum += T[r][i + t] * a.prm.filter[0][t];
-            HOR[r][i] = clampi((sum + (1 << (rbh - 1))) >> rbh, 0, clip_limit - 1);
+            for (int t = 0; t < 14; t++) tv[t] = T[r][i0 + t];
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                int sum = 1 << (bd + 6);
+                if (BPC == 8) sum += tv[t + 3] * 128;
+#pragma unroll
+                for (int q = 0; q < 7; q++) sum += tv[t + q] * a.prm.filter[0][q];
+                if (i0 + t < sw) HOR[r][i0 + t] = (int16_t)clampi((sum + (1 << (rbh - 1))) >> rbh, 0, clip_limit - 1);   // < 2^15
+            }
         }
         __syncthreads();
+        // vertical: a thread slides down its column, each row read once
         const int rbv = 11 - (bd == 12) * 2, round_offset = 1 << (bd + (rbv - 1));
-        for (int k = threadIdx.x; k < h * kLrSW; k += 256) {
-            const int j = k / kLrSW, i = k % kLrSW;
-            if (i >= sw) continue;
-            int sum = -round_offset;
+        if (wj0 < h && wi < sw) {
+            int hv[7];
 #pragma unroll
-            for (int t = 0; t < 7; t++) sum += HOR[j + t][i] * a.prm.filter[1][t];
-            a.dst[(size_t)j * a.ds + x0 + i] = (P)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, a.bdmax);
+            for (int t = 0; t < 6; t++) hv[t] = HOR[wj0 + t][wi];
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const int j = wj0 + r;
+                if (r >= wrpt || j >= h) break;
+                hv[6] = HOR[j + 6][wi];
+                int sum = -round_offset;
+#pragma unroll
+                for (int t = 0; t < 7; t++) sum += hv[t] * a.prm.filter[1][t];
+                a.dst[(size_t)j * a.ds + x0 + wi] = (P)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, a.bdmax);
+#pragma unroll
+                for (int t = 0; t < 6; t++) hv[t] = hv[t + 1];
+            }
         }
         return;
     }
-    int v[NP];
+    int v[8];
 #pragma unroll
-    for (int m = 0; m < NP; m++) v[m] = 0;
+    for (int m = 0; m < 8; m++) v[m] = 0;
     for (int pass = 0; pass < 2; pass++) {
         const bool five = pass == 0;
         if (five ? a.kind == 2 : a.kind == 1) continue;
@@ -194,58 +215,78 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
         else lr_vsums<1>(T, VS, VQ, h, sw);
         __syncthreads();
         // A / B at unit rows -1..h (every other row from -1 for 5x5, :375)
-        for (int k = threadIdx.x; k < (h + 2) * (kLrSW + 2); k += 256) {
-            const int jj = k / (kLrSW + 2), ii = k - jj * (kLrSW + 2), j = jj - 1;
-            if (ii >= sw + 2 || (five && !(j & 1))) continue;
+        // (5x5: only the odd unit rows, jj = 0, 2, .. <= h + 1)
+        const int nab = five ? (h + 1) / 2 + 1 : h + 2;
+        for (int k = threadIdx.x; k < nab * (kLrSW + 2); k += 256) {
+            const int q = k / (kLrSW + 2), ii = k - q * (kLrSW + 2), jj = five ? 2 * q : q;
+            if (ii >= sw + 2) continue;
             int A, B;
             if (five) lr_ab<2>(VS, VQ, jj, ii, a.prm.sgr.s0, bd8, XBX, A, B);
             else lr_ab<1>(VS, VQ, jj, ii, a.prm.sgr.s1, bd8, XBX, A, B);
-            AB[0][jj][ii] = A;
-            AB[1][jj][ii] = B;
+            AA[jj][ii] = A;
+            BB[jj][ii] = (uint8_t)B;
         }
         __syncthreads();
         const int wgt = five ? a.prm.sgr.w0 : a.prm.sgr.w1;
+        // the weighting (:397-439), a thread per column and run of RPT rows
+        // sliding down it: each A / B row is read once per thread as a
+        // (sum over columns ii-1..ii+1, centre) pair, from which the 6/5 and
+        // 4/3 neighbour weights follow:
+        //   EIGHT: 4 s1 + 3 (s0 + s2) + c0 + c2;  SIX (even j): 5 (s0 + s2) +
+        //   c0 + c2;  odd j: 5 s1 + c1  (rows 0/1/2 = unit rows j-1, j, j+1)
+        if (wj0 < h && wi < sw) {
+            const int ii = wi + 1;
+            int s0a = 0, c0a = 0, s0b = 0, c0b = 0, s1a = 0, c1a = 0, s1b = 0, c1b = 0;
+            auto row = [&](int k, int &sa, int &ca, int &sb, int &cb) {
+                const int a0 = AA[k][ii - 1], a1 = AA[k][ii], a2 = AA[k][ii + 1];
+                const int b0 = BB[k][ii - 1], b1 = BB[k][ii], b2 = BB[k][ii + 1];
+                sa = a0 + a1 + a2;
+                ca = a1;
+                sb = b0 + b1 + b2;
+                cb = b1;
+            };
+            // (5x5: only even A / B rows exist; odd ones are never read)
+            if (!five || !(wj0 & 1)) row(wj0, s0a, c0a, s0b, c0b);
+            if (!five || (wj0 & 1)) row(wj0 + 1, s1a, c1a, s1b, c1b);
 #pragma unroll
-        for (int m = 0; m < NP; m++) {
-            const int k = threadIdx.x + 256 * m;
-            if (k >= h * kLrSW) break;
-            const int j = k / kLrSW, i = k % kLrSW, jj = j + 1, ii = i + 1;
-            if (i >= sw) continue;
-            const int px = T[j + 3][i + 3];
-            const int(*A)[kLrSW + 2] = AB[0];
-            const int(*B)[kLrSW + 2] = AB[1];
-            int aa, bb, sh;
-            if (five) {
-                if (!(j & 1)) {   // SIX_NEIGHBORS, :397-405
-                    aa = (B[jj - 1][ii] + B[jj + 1][ii]) * 6 +
-                         (B[jj - 1][ii - 1] + B[jj + 1][ii - 1] + B[jj - 1][ii + 1] + B[jj + 1][ii + 1]) * 5;
-                    bb = (A[jj - 1][ii] + A[jj + 1][ii]) * 6 +
-                         (A[jj - 1][ii - 1] + A[jj + 1][ii - 1] + A[jj - 1][ii + 1] + A[jj + 1][ii + 1]) * 5;
+            for (int r = 0; r < 8; r++) {
+                const int j = wj0 + r;
+                if (r >= wrpt || j >= h) break;
+                int s2a = 0, c2a = 0, s2b = 0, c2b = 0;
+                if (!five || !(j & 1)) row(j + 2, s2a, c2a, s2b, c2b);
+                int aa, bb, sh;
+                if (five) {
+                    if (!(j & 1)) {
+                        aa = 5 * (s0b + s2b) + c0b + c2b;
+                        bb = 5 * (s0a + s2a) + c0a + c2a;
+                        sh = 9;
+                    } else {
+                        aa = 5 * s1b + c1b;
+                        bb = 5 * s1a + c1a;
+                        sh = 8;
+                    }
+                } else {
+                    aa = 4 * s1b + 3 * (s0b + s2b) + c0b + c2b;
+                    bb = 4 * s1a + 3 * (s0a + s2a) + c0a + c2a;
                     sh = 9;
-                } else {          // :411-415
-                    aa = B[jj][ii] * 6 + (B[jj][ii - 1] + B[jj][ii + 1]) * 5;
-                    bb = A[jj][ii] * 6 + (A[jj][ii - 1] + A[jj][ii + 1]) * 5;
-                    sh = 8;
                 }
-            } else {              // EIGHT_NEIGHBORS, :430-439
-                aa = (B[jj][ii] + B[jj][ii - 1] + B[jj][ii + 1] + B[jj - 1][ii] + B[jj + 1][ii]) * 4 +
-                     (B[jj - 1][ii - 1] + B[jj + 1][ii - 1] + B[jj - 1][ii + 1] + B[jj + 1][ii + 1]) * 3;
-                bb = (A[jj][ii] + A[jj][ii - 1] + A[jj][ii + 1] + A[jj - 1][ii] + A[jj + 1][ii]) * 4 +
-                     (A[jj - 1][ii - 1] + A[jj + 1][ii - 1] + A[jj - 1][ii + 1] + A[jj + 1][ii + 1]) * 3;
-                sh = 9;
+                const int px = T[j + 3][wi + 3];
+                const int d = (int)(C)((bb - aa * px + (1 << (sh - 1))) >> sh);   // stored as coef
+                v[r] += wgt * d;
+                s0a = s1a, c0a = c1a, s0b = s1b, c0b = c1b;
+                s1a = s2a, c1a = c2a, s1b = s2b, c1b = c2b;
             }
-            const int d = (int)(C)((bb - aa * px + (1 << (sh - 1))) >> sh);   // stored as coef
-            v[m] += wgt * d;
         }
         __syncthreads();
     }
+    if (wj0 < h && wi < sw) {
 #pragma unroll
-    for (int m = 0; m < NP; m++) {
-        const int k = threadIdx.x + 256 * m;
-        if (k >= h * kLrSW) break;
-        const int j = k / kLrSW, i = k % kLrSW;
-        if (i < sw)
-            a.dst[(size_t)j * a.ds + x0 + i] = (P)clampi(T[j + 3][i + 3] + ((v[m] + (1 << 10)) >> 11), 0, a.bdmax);
+        for (int r = 0; r < 8; r++) {
+            const int j = wj0 + r;
+            if (r >= wrpt || j >= h) break;
+            a.dst[(size_t)j * a.ds + x0 + wi] =
+                (P)clampi(T[j + 3][wi + 3] + ((v[r] + (1 << 10)) >> 11), 0, a.bdmax);
+        }
     }
 }
 
@@ -292,7 +333,7 @@ __device__ __forceinline__ int lr_params(const Dav1dGpuLrUnit &u, bool hbd, Dav1
 // rest, :135-166) and a superblock row's unit row is chosen as lr_sbrow does
 // (:124-127).
 template <int BPC>
-__global__ __launch_bounds__(256) void k_lr_frame(LrFrameArgs<BPC> f) {
+__global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     using P = typename Px<BPC>::pixel;
     const int pl = blockIdx.z, w = f.w[pl], h = f.h[pl], sv = f.ss_ver[pl];
     const int xs = blockIdx.x * kLrSW;
