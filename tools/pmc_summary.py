@@ -16,7 +16,7 @@ import os
 
 
 def short(name):
-    for k in ("k_recon", "k_tiles"):
+    for k in ("k_recon", "k_tiles", "k_lr_frame", "k_cdef", "k_lpf", "k_grain"):
         if k in name:
             return name[name.index(k):].split("(")[0]
     return None
