@@ -302,6 +302,9 @@ def load_lib():
         L.dav1d_gpu_recorder_free.restype = None
         L.dav1d_gpu_rec_block.argtypes = [ctypes.c_void_p, ctypes.POINTER(RecBlock)]
         L.dav1d_gpu_rec_block.restype = ctypes.c_int
+        L.dav1d_gpu_rec_block_aux.argtypes = [ctypes.c_void_p, ctypes.POINTER(RecBlock), ctypes.c_void_p,
+                                              ctypes.c_size_t]
+        L.dav1d_gpu_rec_block_aux.restype = ctypes.c_int
         L.dav1d_gpu_rec_residual.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p]
         L.dav1d_gpu_rec_residual.restype = ctypes.c_int
         L.dav1d_gpu_recorder_flush.argtypes = [ctypes.c_void_p, ctypes.POINTER(Plane * 3),
@@ -345,7 +348,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_backup_ipred_edge_8bpc", "dav1d_gpu_backup_ipred_edge_16bpc",
     "dav1d_gpu_recon_intra_frame_8bpc", "dav1d_gpu_recon_intra_frame_16bpc",
     "dav1d_gpu_intra_workspace_bytes",
-    "dav1d_gpu_recorder_new", "dav1d_gpu_recorder_free", "dav1d_gpu_rec_block", "dav1d_gpu_rec_residual",
+    "dav1d_gpu_recorder_new", "dav1d_gpu_recorder_free", "dav1d_gpu_rec_block", "dav1d_gpu_rec_block_aux", "dav1d_gpu_rec_residual",
     "dav1d_gpu_recorder_flush", "dav1d_gpu_recorder_stats", "dav1d_gpu_recorder_status",
     "dav1d_gpu_apply_grain_8bpc", "dav1d_gpu_apply_grain_16bpc",
     "dav1d_cdef_dsp_init_8bpc", "dav1d_cdef_dsp_init_16bpc",

@@ -43,6 +43,8 @@ static int launch_ie(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *
     a.cfl_luma = (const P *)b->cfl_luma.data;
     a.cfl_luma_stride = (int)(b->cfl_luma.stride / B);
     a.cfl_ss = b->cfl_ss;
+    a.aux = b->aux;   // INTER_MASK masks / PAL records (recorder flushes)
+    a.aux_pool = (const uint8_t *)b->aux_pool;
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;
     int rc = launch_group<BPC, GROUP_HUGE_IE>(a, b, ~0u, stream);

@@ -166,13 +166,56 @@ struct Unit {   // a transform cell before sorting
     Dav1dGpuIntraEdge rec;
     int level;
     int sortmode;
+    int32_t aux;   // aux_pool offset (INTER_MASK / PAL), else 0
 };
+
+// kinds recorded with block data (dav1d_gpu_rec_block_aux); the last four
+// are predicted by the launch ahead of the wavefront
+inline bool is_ext_kind(int k) {
+    return k == DGPU_PRED_INTER_MASK || k == DGPU_PRED_PAL || k == DGPU_PRED_WARP || k == DGPU_PRED_INTER_WMASK ||
+           k == DGPU_PRED_INTER_OBMC || k == DGPU_PRED_INTER_SCALED;
+}
+inline bool is_prelaunch_kind(int k) {
+    return k == DGPU_PRED_WARP || k == DGPU_PRED_INTER_WMASK || k == DGPU_PRED_INTER_OBMC ||
+           k == DGPU_PRED_INTER_SCALED;
+}
+inline bool is_mc_kind(int k) {   // the flow kinds that read references through src_off
+    return k == DGPU_PRED_INTER || k == DGPU_PRED_INTER_AVG || k == DGPU_PRED_INTER_WAVG ||
+           k == DGPU_PRED_INTER_MASK;
+}
+inline int tx_of(int w, int h) {
+    for (int t = 0; t < DGPU_N_RECT_TX_SIZES; t++)
+        if (kTx[t].w == w && kTx[t].h == h) return t;
+    return -1;
+}
+
+struct ObmcBlockLap {   // dav1d_gpu_rec_block_aux INTER_OBMC entry (24 B)
+    int32_t mvx, mvy;
+    uint8_t filter2d, ref, x0, y0, x1, y1, lap_w4, lap_h4, dir, mask_off, pad_[6];
+};
+struct ObmcUnitLap {    // Dav1dGpuPredKind INTER_OBMC unit entry (16 B)
+    int32_t src_off;
+    uint8_t mx, my, filter2d, ref, x0, y0, x1, y1, lap_w4, lap_h4, dir, mask_off;
+};
+struct ScaledBlockRef {   // INTER_SCALED block record, per ref
+    int32_t x, y;
+    uint16_t mx, my, dx, dy;
+};
+struct ScaledUnitRef {
+    int32_t src_off;
+    uint16_t mx, my, dx, dy;
+    uint32_t pad_;
+};
+static_assert(sizeof(ObmcBlockLap) == 24 && sizeof(ObmcUnitLap) == 16 && sizeof(ScaledBlockRef) == 16 &&
+              sizeof(ScaledUnitRef) == 16, "aux record layouts");
 
 }  // namespace
 
 struct Dav1dGpuRecorder {
     int bpc, bdmax, width, height, device;
     std::vector<Dav1dGpuRecBlock> blocks;
+    std::vector<int64_t> block_aux;   // per block: offset into baux, -1 none
+    std::vector<uint8_t> baux;        // dav1d_gpu_rec_block_aux data
     std::vector<Residual> residuals;
     std::vector<uint8_t> coefb;    // compact regions in the ABI's coefficient type (int16 / int32)
     // flush products (kept alive while the device may still read them)
@@ -182,10 +225,13 @@ struct Dav1dGpuRecorder {
     std::vector<int32_t> rank;
     std::vector<int32_t> prod_start, prod, dep_start, deps;   // producers: decode order, then level order
     std::vector<EmuJob> emu;     // clamped footprint copies of this flush
+    std::vector<uint8_t> auxp;   // the aux pool: masks, palette / warp / OBMC / scaled records
+    std::vector<Dav1dGpuUnit> xunits;   // the launch ahead of the wavefront (class order)
+    std::vector<int32_t> xaux;
     std::vector<uint8_t> h_host;   // DAV1D_GPU_REC_HOSTONLY: stands in for the pinned buffer
     PinnedBuf pin;   // units | recs | coefficients | emu jobs, written in place by the fill
     PinnedBuf flag;  // the last flush's wavefront error word, copied back on its stream
-    DevBuf d_units, d_recs, d_coef, d_edges, d_work, d_emu, d_emu_jobs;
+    DevBuf d_units, d_recs, d_coef, d_edges, d_work, d_emu, d_emu_jobs, d_aux, d_auxp, d_xunits, d_xaux;
     hipEvent_t done = nullptr;
     bool pending_check = false;   // the last flush's error word not read yet
     int32_t last_units = 0, last_levels = 0;
@@ -218,6 +264,10 @@ extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
         r->d_work.release();
         r->d_emu.release();
         r->d_emu_jobs.release();
+        r->d_aux.release();
+        r->d_auxp.release();
+        r->d_xunits.release();
+        r->d_xaux.release();
     }
     delete r;
 }
@@ -229,15 +279,17 @@ static bool plane_dims(const Dav1dGpuRecorder *r, int plane, int &w, int &h) {
     return true;
 }
 
-extern "C" int dav1d_gpu_rec_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b) {
+static int check_block(const Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, bool ext) {
     int pw, ph;
     if (!r || !b || !plane_dims(r, b->plane, pw, ph)) return -1;
     if (b->tx < 0 || b->tx >= DGPU_N_RECT_TX_SIZES) return -1;
     const TxDim t = kTx[b->tx];
     if (b->x < 0 || b->y < 0 || b->w <= 0 || b->h <= 0 || b->x + b->w > pw || b->y + b->h > ph) return -1;
     if ((b->x & 3) || (b->y & 3) || b->w % t.w || b->h % t.h) return -1;
-    const bool inter = b->kind == DGPU_PRED_INTER || b->kind == DGPU_PRED_INTER_AVG || b->kind == DGPU_PRED_INTER_WAVG;
-    if (!inter && b->kind != DGPU_PRED_INTRA && b->kind != DGPU_PRED_CFL) return -1;
+    if (ext != is_ext_kind(b->kind)) return -1;
+    const bool inter = b->kind == DGPU_PRED_INTER || b->kind == DGPU_PRED_INTER_AVG ||
+                       b->kind == DGPU_PRED_INTER_WAVG || (ext && b->kind != DGPU_PRED_PAL);
+    if (!inter && b->kind != DGPU_PRED_INTRA && b->kind != DGPU_PRED_CFL && b->kind != DGPU_PRED_PAL) return -1;
     if (b->kind == DGPU_PRED_CFL && (b->plane == 0 || b->w != t.w || b->h != t.h || t.w != t.h || t.w > 32))
         return -1;   // CfL: one unit per chroma block (cfl_ac + cfl_pred, :1372-1414)
     if (!inter && b->mode > 13) return -1;
@@ -245,7 +297,61 @@ extern "C" int dav1d_gpu_rec_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *
     if (b->tile_x0 < 0 || b->tile_y0 < 0 || b->tile_x1 > pw || b->tile_y1 > ph || b->x < b->tile_x0 ||
         b->y < b->tile_y0 || b->x + b->w > b->tile_x1 || b->y + b->h > b->tile_y1)
         return -1;
+    return 0;
+}
+
+extern "C" int dav1d_gpu_rec_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b) {
+    if (check_block(r, b, false)) return -1;
     r->blocks.push_back(*b);
+    r->block_aux.push_back(-1);
+    return 0;
+}
+
+extern "C" int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, const void *aux,
+                                       size_t aux_bytes) {
+    if (check_block(r, b, true)) return -1;
+    const size_t bpp = r->bpc / 8, w = b->w, h = b->h;
+    size_t need = 0;
+    switch (b->kind) {
+    case DGPU_PRED_INTER_MASK:
+        if (!aux) {   // a COMPOUND_SEG chroma block: the last INTER_WMASK block's mask
+            if (b->plane == 0) return -1;
+            r->blocks.push_back(*b);
+            r->block_aux.push_back(-1);
+            return 0;
+        }
+        need = w * h;
+        break;
+    case DGPU_PRED_PAL: need = 8 * bpp + (w / 2) * h; break;
+    case DGPU_PRED_WARP:
+        if ((w & 7) || (h & 7) || (b->x & 7) || (b->y & 7)) return -1;
+        need = 16 + (w / 8) * (h / 8) * 8;
+        break;
+    case DGPU_PRED_INTER_WMASK:
+        if (b->plane != 0 || b->weight > 1) return -1;
+        r->blocks.push_back(*b);
+        r->block_aux.push_back(-1);
+        return 0;
+    case DGPU_PRED_INTER_OBMC: {
+        if (!aux || aux_bytes < 16) return -1;
+        const int32_t n = *(const int32_t *)aux;
+        if (n < 0 || n > 64) return -1;
+        need = 16 + sizeof(ObmcBlockLap) * (size_t)n;
+        break;
+    }
+    case DGPU_PRED_INTER_SCALED: {
+        if (!aux || aux_bytes < 16) return -1;
+        const int32_t n = *(const int32_t *)aux;
+        if (n != 1 && n != 2) return -1;
+        need = 16 + 16 * (size_t)n;
+        break;
+    }
+    default: return -1;
+    }
+    if (!aux || aux_bytes != need) return -1;
+    r->blocks.push_back(*b);
+    r->block_aux.push_back((int64_t)r->baux.size());
+    r->baux.insert(r->baux.end(), (const uint8_t *)aux, (const uint8_t *)aux + aux_bytes);
     return 0;
 }
 
@@ -372,22 +478,147 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     prod_start.assign(1, 0);
     prod.clear();
     size_t n_res_used = 0;
-    for (const Dav1dGpuRecBlock &b : r->blocks) {
+    // the aux pool (16-byte aligned records) and the launch ahead of the
+    // wavefront (WARP / INTER_WMASK / INTER_OBMC / INTER_SCALED predictions)
+    std::vector<uint8_t> &auxp = r->auxp;
+    auxp.clear();
+    std::vector<Dav1dGpuUnit> &xunits = r->xunits;
+    std::vector<int32_t> &xaux = r->xaux;
+    xunits.clear();
+    xaux.clear();
+    auto aux_alloc = [&](size_t nbytes) -> int32_t {
+        const size_t o = (auxp.size() + 15) & ~(size_t)15;
+        auxp.resize(o + nbytes);
+        return (int32_t)o;
+    };
+    int32_t wm_off = -1, wm_w = 0, wm_h = 0;   // the last INTER_WMASK block's seg mask (4:2:0)
+    for (size_t bi = 0; bi < r->blocks.size(); bi++) {
+        const Dav1dGpuRecBlock &b = r->blocks[bi];
         const TxDim t = kTx[b.tx];
         const int p = b.plane, w4p = pw[p] / 4;
-        const bool inter = b.kind == DGPU_PRED_INTER || b.kind == DGPU_PRED_INTER_AVG || b.kind == DGPU_PRED_INTER_WAVG;
-        const bool cfl = b.kind == DGPU_PRED_CFL;
+        const bool inter = is_mc_kind(b.kind);
+        const bool cfl = b.kind == DGPU_PRED_CFL, pal = b.kind == DGPU_PRED_PAL;
+        const bool pre = is_prelaunch_kind(b.kind);
+        const uint8_t *bdata = r->block_aux[bi] >= 0 ? &r->baux[(size_t)r->block_aux[bi]] : nullptr;
         const int bw4 = b.w / 4, bh4 = b.h / 4, tw4 = t.w / 4, th4 = t.h / 4;
+        const int ds_px = (int)(dst[p].stride / bpp);
+        // every reference an inter block reads must be given
+        if (inter || pre) {
+            const int nref = b.kind == DGPU_PRED_INTER || b.kind == DGPU_PRED_WARP || b.kind == DGPU_PRED_INTER_OBMC ? 1
+                             : b.kind == DGPU_PRED_INTER_SCALED ? *(const int32_t *)bdata : 2;
+            for (int k = 0; k < nref; k++)
+                if (!ref || !ref[b.ref[k]][p].data) return -1;
+        }
+        int32_t mask_base = 0, mask_stride = 0;   // INTER_MASK: the block's mask
+        if (b.kind == DGPU_PRED_INTER_MASK) {
+            if (bdata) {
+                mask_base = aux_alloc((size_t)b.w * b.h);
+                memcpy(&auxp[mask_base], bdata, (size_t)b.w * b.h);
+                mask_stride = b.w;
+            } else {   // COMPOUND_SEG chroma: the luma block's w_mask output
+                if (wm_off < 0 || b.w != wm_w || b.h != wm_h) return -1;
+                mask_base = wm_off;
+                mask_stride = wm_w;
+            }
+        }
+        if (pre) {   // prediction units of at most 32 x 32, no residual
+            const int uw = std::min(b.w, 32), uh = std::min(b.h, 32), utx = tx_of(uw, uh);
+            if (utx < 0) return -1;
+            if (b.kind == DGPU_PRED_INTER_WMASK) {   // its seg mask at the 4:2:0 chroma resolution
+                wm_w = b.w >> 1;
+                wm_h = b.h >> 1;
+                wm_off = aux_alloc((size_t)wm_w * wm_h);
+            }
+            for (int oy = 0; oy < b.h; oy += uh)
+                for (int ox = 0; ox < b.w; ox += uw) {
+                    const int ux = b.x + ox, uy = b.y + oy;
+                    Dav1dGpuUnit u;
+                    memset(&u, 0, sizeof(u));
+                    u.dst_off = uy * ds_px + ux;
+                    u.tx = (uint8_t)utx;
+                    u.plane = (uint8_t)p;
+                    u.pred = (uint8_t)b.kind;
+                    u.txtp = DGPU_NO_RESIDUAL;
+                    u.bw4 = (uint8_t)bw4;
+                    u.bh4 = (uint8_t)bh4;
+                    for (int k = 0; k < 2; k++) {
+                        const int rr = b.ref[k];
+                        const int rs = ref && ref[rr][p].data ? (int)(ref[rr][p].stride / bpp) : 0;
+                        u.p.inter.src_off[k] = (uy + (b.mvy[k] >> 4)) * rs + ux + (b.mvx[k] >> 4);
+                        u.p.inter.mx[k] = (uint8_t)(b.mvx[k] & 15);
+                        u.p.inter.my[k] = (uint8_t)(b.mvy[k] & 15);
+                        u.p.inter.ref[k] = (uint8_t)rr;
+                    }
+                    u.p.inter.filter2d = b.filter2d;
+                    u.p.inter.weight = b.weight;
+                    int32_t ao = 0;
+                    if (b.kind == DGPU_PRED_INTER_WMASK) {
+                        ao = wm_off + (oy >> 1) * wm_w + (ox >> 1);
+                    } else if (b.kind == DGPU_PRED_WARP) {   // abcd, then the unit's 8x8s
+                        const int gw = b.w / 8, nx = uw / 8, ny = uh / 8;
+                        ao = aux_alloc(16 + 8 * (size_t)nx * ny);
+                        memcpy(&auxp[ao], bdata, 8);
+                        for (int sy = 0; sy < ny; sy++)
+                            memcpy(&auxp[ao + 16 + 8 * sy * nx], bdata + 16 + 8 * ((oy / 8 + sy) * gw + ox / 8), 8 * nx);
+                    } else if (b.kind == DGPU_PRED_INTER_OBMC) {   // the laps overlapping the unit
+                        const int n = *(const int32_t *)bdata;
+                        const ObmcBlockLap *lb = (const ObmcBlockLap *)(bdata + 16);
+                        std::vector<ObmcUnitLap> ents;
+                        for (int k = 0; k < n; k++) {
+                            const ObmcBlockLap &e = lb[k];
+                            const int x0 = std::max((int)e.x0 - ox, 0), x1 = std::min((int)e.x1 - ox, uw);
+                            const int y0 = std::max((int)e.y0 - oy, 0), y1 = std::min((int)e.y1 - oy, uh);
+                            if (x0 >= x1 || y0 >= y1) continue;
+                            if (e.ref >= DGPU_REC_EMU_SLOT || !ref || !ref[e.ref][p].data || e.filter2d > 9) return -1;
+                            const int rs = (int)(ref[e.ref][p].stride / bpp);
+                            ObmcUnitLap q;
+                            q.src_off = (uy + (e.mvy >> 4)) * rs + ux + (e.mvx >> 4);
+                            q.mx = (uint8_t)(e.mvx & 15);
+                            q.my = (uint8_t)(e.mvy & 15);
+                            q.filter2d = e.filter2d;
+                            q.ref = e.ref;
+                            q.x0 = (uint8_t)x0, q.y0 = (uint8_t)y0, q.x1 = (uint8_t)x1, q.y1 = (uint8_t)y1;
+                            q.lap_w4 = e.lap_w4, q.lap_h4 = e.lap_h4, q.dir = e.dir;
+                            q.mask_off = (uint8_t)(e.mask_off + (e.dir ? ox : oy));
+                            ents.push_back(q);
+                        }
+                        ao = aux_alloc(16 + 16 * ents.size());
+                        const int32_t ne = (int32_t)ents.size();
+                        memset(&auxp[ao], 0, 16);
+                        memcpy(&auxp[ao], &ne, 4);
+                        if (ne) memcpy(&auxp[ao + 16], ents.data(), 16 * ents.size());
+                    } else {   // INTER_SCALED: the unit's integer position and phase (running sums)
+                        const int n = *(const int32_t *)bdata;
+                        const ScaledBlockRef *sb = (const ScaledBlockRef *)(bdata + 16);
+                        ao = aux_alloc(16 + 16 * (size_t)n);
+                        memset(&auxp[ao], 0, 16 + 16 * (size_t)n);
+                        memcpy(&auxp[ao], &n, 4);
+                        for (int k = 0; k < n; k++) {
+                            const int rs = (int)(ref[b.ref[k]][p].stride / bpp);
+                            const int px_ = sb[k].mx + ox * sb[k].dx, py_ = sb[k].my + oy * sb[k].dy;
+                            ScaledUnitRef q;
+                            q.src_off = (sb[k].y + (py_ >> 10)) * rs + sb[k].x + (px_ >> 10);
+                            q.mx = (uint16_t)(px_ & 1023), q.my = (uint16_t)(py_ & 1023);
+                            q.dx = sb[k].dx, q.dy = sb[k].dy;
+                            q.pad_ = 0;
+                            memcpy(&auxp[ao + 16 + 16 * k], &q, 16);
+                        }
+                        if (n == 1) u.p.inter.weight = 0;
+                    }
+                    xunits.push_back(u);
+                    xaux.push_back(ao);
+                }
+        }
         for (int oy = 0; oy < b.h; oy += t.h)
             for (int ox = 0; ox < b.w; ox += t.w) {
                 Unit c;
                 memset(&c, 0, sizeof(c));
                 const int ux = b.x + ox, uy = b.y + oy, x4 = ux / 4, y4 = uy / 4;
                 Dav1dGpuUnit &u = c.u;
-                u.dst_off = uy * (int)(dst[p].stride / bpp) + ux;
+                u.dst_off = uy * ds_px + ux;
                 u.tx = (uint8_t)b.tx;
                 u.plane = (uint8_t)p;
-                u.pred = (uint8_t)b.kind;
+                u.pred = (uint8_t)(pre ? DGPU_PRED_NONE : b.kind);
                 u.txtp = DGPU_NO_RESIDUAL;
                 const int ri = res_at[p][(size_t)y4 * w4p + x4];
                 if (ri >= 0 && r->residuals[ri].tx == b.tx) {
@@ -399,6 +630,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     n_res_used++;
                 } else if (ri >= 0) {
                     return -1;   // a residual whose size differs from its block's transforms
+                } else if (pre) {
+                    continue;   // predicted ahead of the wavefront, nothing to add
                 }
                 Dav1dGpuIntraEdge &e = c.rec;
                 e.unit = -1;
@@ -408,7 +641,18 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 e.h4 = (int16_t)(b.tile_y1 / 4);
                 int nd = 0;
                 bool hl = ux > b.tile_x0, ht = uy > b.tile_y0;
-                if (inter) {
+                if (pre) {   // PRED_NONE: the residual onto the launch-ahead prediction
+                    c.sortmode = 0;
+                } else if (pal) {   // pal_pred: palette, then the unit's rows of the index map
+                    const int bw2 = b.w / 2;
+                    c.aux = aux_alloc(16 + (size_t)(t.w / 2) * t.h);
+                    memset(&auxp[c.aux], 0, 16);
+                    memcpy(&auxp[c.aux], bdata, 8 * (size_t)bpp);
+                    for (int yy = 0; yy < t.h; yy++)
+                        memcpy(&auxp[c.aux + 16 + yy * (t.w / 2)], bdata + 8 * bpp + (size_t)(oy + yy) * bw2 + ox / 2,
+                               t.w / 2);
+                    c.sortmode = 15;
+                } else if (inter) {
                     u.bw4 = (uint8_t)bw4;
                     u.bh4 = (uint8_t)bh4;
                     for (int k = 0; k < 2; k++) {
@@ -442,6 +686,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     }
                     u.p.inter.filter2d = b.filter2d;
                     u.p.inter.weight = b.kind == DGPU_PRED_INTER_WAVG ? b.weight : 0;
+                    if (b.kind == DGPU_PRED_INTER_MASK) c.aux = mask_base + oy * mask_stride + ox;
                     c.sortmode = b.filter2d;
                 } else {
                     int fl = (hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0);
@@ -582,18 +827,41 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     //    ranks, the coefficient pool (decode order) and the emu jobs, by
     //    several threads over disjoint ranges
     const size_t coef_at = r->coefb.size() / cb;
+    // image: units | records | coefficients | emu jobs | per-unit aux |
+    //        launch-ahead units (class order) | their aux | aux pool
+    const size_t nx = r->xunits.size();
     const size_t bu = (size_t)n * sizeof(Dav1dGpuUnit), br = (size_t)n * sizeof(Dav1dGpuIntraEdge),
-                 bc = coef_at * cb, be = r->emu.size() * sizeof(EmuJob);
+                 bc = coef_at * cb, be = r->emu.size() * sizeof(EmuJob), ba = (size_t)n * 4,
+                 bxu = nx * sizeof(Dav1dGpuUnit), bxa = nx * 4, bp = r->auxp.size();
+    const size_t o_c = bu + br, o_e = o_c + bc, o_a = o_e + be, o_xu = o_a + ba, o_xa = o_xu + bxu,
+                 o_p = o_xa + bxa, o_end = o_p + bp;
     uint8_t *img;
     if (host_only) {
-        r->h_host.resize(bu + br + bc + be);
+        r->h_host.resize(o_end);
         img = r->h_host.data();
     } else {
-        if (r->pin.grow(bu + br + bc + be)) return -3;
+        if (r->pin.grow(o_end)) return -3;
         img = (uint8_t *)r->pin.p;
     }
     Dav1dGpuUnit *hu = (Dav1dGpuUnit *)img;
     Dav1dGpuIntraEdge *hr = (Dav1dGpuIntraEdge *)(img + bu);
+    int32_t *ha = (int32_t *)(img + o_a);
+    // the launch-ahead units in class order (a counting sort by size class)
+    int32_t x_class[DGPU_N_RECT_TX_SIZES + 1] = {0};
+    if (nx) {
+        for (const Dav1dGpuUnit &u : r->xunits) x_class[u.tx + 1]++;
+        for (int k = 0; k < NC; k++) x_class[k + 1] += x_class[k];
+        int32_t at[DGPU_N_RECT_TX_SIZES];
+        memcpy(at, x_class, sizeof(at));
+        Dav1dGpuUnit *xu = (Dav1dGpuUnit *)(img + o_xu);
+        int32_t *xa = (int32_t *)(img + o_xa);
+        for (size_t i = 0; i < nx; i++) {
+            const int k = at[r->xunits[i].tx]++;
+            xu[k] = r->xunits[i];
+            xa[k] = r->xaux[i];
+        }
+    }
+    if (bp) memcpy(img + o_p, r->auxp.data(), bp);
     {
         const int nt = n < 32768 ? 1 : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
         auto work = [&](int t) {
@@ -602,6 +870,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 const Unit &c = cells[ci];
                 const int i = rank[ci];
                 hu[i] = c.u;   // coef_off / edge_off are decode-order pool offsets
+                ha[i] = c.aux;
                 Dav1dGpuIntraEdge e = c.rec;
                 e.unit = i;
                 hr[i] = e;
@@ -609,23 +878,28 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 for (int k = prod_start[ci]; k < prod_start[ci + 1]; k++) *o++ = rank[prod[k]];
             }
             const size_t b0 = bc * t / nt, b1 = bc * (t + 1) / nt;
-            if (b1 > b0) memcpy(img + bu + br + b0, r->coefb.data() + b0, b1 - b0);
+            if (b1 > b0) memcpy(img + o_c + b0, r->coefb.data() + b0, b1 - b0);
         };
         std::vector<std::thread> th;
         for (int t = 1; t < nt; t++) th.emplace_back(work, t);
         work(0);
         for (auto &x : th) x.join();
-        if (be) memcpy(img + bu + br + bc, r->emu.data(), be);
+        if (be) memcpy(img + o_e, r->emu.data(), be);
     }
     lap("fill");
     r->rec_start = r->unit_start;
     r->run_start.assign(n_levels + 1, 0);
     r->last_units = n;
     r->last_levels = n_levels;
-    if (!n || host_only) {
+    auto drop_recording = [&] {
         r->blocks.clear();
+        r->block_aux.clear();
+        r->baux.clear();
         r->residuals.clear();
         r->coefb.clear();
+    };
+    if ((!n && !nx) || host_only) {
+        drop_recording();
         return 0;
     }
 
@@ -641,18 +915,25 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     s.run_start = r->run_start.data();
     s.dep_start = r->dep_start.data();
     s.deps = r->deps.data();
-    const int64_t wsb = dav1d_gpu_intra_workspace_bytes(&s, n);
+    const int64_t wsb = n ? dav1d_gpu_intra_workspace_bytes(&s, n) : 16;
     if (wsb < 0) return -2;
     if (r->d_units.grow((size_t)n * sizeof(Dav1dGpuUnit)) || r->d_recs.grow((size_t)n * sizeof(Dav1dGpuIntraEdge)) ||
         r->d_coef.grow(std::max<size_t>(coef_at * cb, 16)) || r->d_edges.grow(std::max<size_t>(edge_px * bpp, 16)) ||
         r->d_work.grow((size_t)wsb))
         return -3;
     if (be && (r->d_emu_jobs.grow(be) || r->d_emu.grow((size_t)emu_rows * kEmuStride * bpp + 256))) return -3;
+    if (r->d_aux.grow(ba) || r->d_auxp.grow(std::max<size_t>(bp, 16)) ||
+        (nx && (r->d_xunits.grow(bxu) || r->d_xaux.grow(bxa))))
+        return -3;
     const uint8_t *pin = img;
-    if (hipMemcpyAsync(r->d_units.p, pin, bu, hipMemcpyHostToDevice, st) ||
-        hipMemcpyAsync(r->d_recs.p, pin + bu, br, hipMemcpyHostToDevice, st) ||
-        (bc && hipMemcpyAsync(r->d_coef.p, pin + bu + br, bc, hipMemcpyHostToDevice, st)) ||
-        (be && hipMemcpyAsync(r->d_emu_jobs.p, pin + bu + br + bc, be, hipMemcpyHostToDevice, st)))
+    if ((bu && hipMemcpyAsync(r->d_units.p, pin, bu, hipMemcpyHostToDevice, st)) ||
+        (br && hipMemcpyAsync(r->d_recs.p, pin + bu, br, hipMemcpyHostToDevice, st)) ||
+        (bc && hipMemcpyAsync(r->d_coef.p, pin + o_c, bc, hipMemcpyHostToDevice, st)) ||
+        (be && hipMemcpyAsync(r->d_emu_jobs.p, pin + o_e, be, hipMemcpyHostToDevice, st)) ||
+        (ba && hipMemcpyAsync(r->d_aux.p, pin + o_a, ba, hipMemcpyHostToDevice, st)) ||
+        (nx && hipMemcpyAsync(r->d_xunits.p, pin + o_xu, bxu, hipMemcpyHostToDevice, st)) ||
+        (nx && hipMemcpyAsync(r->d_xaux.p, pin + o_xa, bxa, hipMemcpyHostToDevice, st)) ||
+        (bp && hipMemcpyAsync(r->d_auxp.p, pin + o_p, bp, hipMemcpyHostToDevice, st)))
         return -3;
     if (be) {   // the clamped footprints, before the wavefront reads them
         EmuArgs ea;
@@ -696,25 +977,37 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     fb.bitdepth_max = r->bdmax;
     fb.cfl_luma = dst[0];
     fb.cfl_ss = 3;
+    fb.aux = (const int32_t *)r->d_aux.p;
+    fb.aux_pool = r->d_auxp.p;
+    if (nx) {   // WARP / INTER_WMASK / INTER_OBMC / INTER_SCALED predictions ahead of the wavefront
+        Dav1dGpuFrameBatch xb = fb;
+        xb.units = (const Dav1dGpuUnit *)r->d_xunits.p;
+        xb.n_units = (int32_t)nx;
+        for (int k = 0; k <= NC; k++) xb.class_start[k] = x_class[k];
+        for (int k = 0; k < NC; k++) xb.class_warp[k] = x_class[k + 1] - x_class[k];
+        xb.aux = (const int32_t *)r->d_xaux.p;
+        const int xrc = r->bpc == 8 ? dav1d_gpu_recon_8bpc(&xb, stream) : dav1d_gpu_recon_16bpc(&xb, stream);
+        if (xrc) return xrc;
+    }
     eb.units = (Dav1dGpuUnit *)r->d_units.p;
     eb.edges = r->d_edges.p;
     eb.recs = (const Dav1dGpuIntraEdge *)r->d_recs.p;
     eb.n_recs = n;
     eb.bitdepth_max = r->bdmax;
     lap("upload");
-    const int rc = r->bpc == 8 ? dav1d_gpu_recon_intra_frame_8bpc(&fb, &eb, &s, stream)
-                               : dav1d_gpu_recon_intra_frame_16bpc(&fb, &eb, &s, stream);
-    lap("launch");
-    if (rc) return rc;
+    if (n) {
+        const int rc = r->bpc == 8 ? dav1d_gpu_recon_intra_frame_8bpc(&fb, &eb, &s, stream)
+                                   : dav1d_gpu_recon_intra_frame_16bpc(&fb, &eb, &s, stream);
+        lap("launch");
+        if (rc) return rc;
+    }
     if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return -3;
     // the wavefront's error word (workspace int32 [1]) follows on the stream
-    if (r->flag.grow(16) ||
-        hipMemcpyAsync(r->flag.p, (const int32_t *)r->d_work.p + 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (n && (r->flag.grow(16) ||
+              hipMemcpyAsync(r->flag.p, (const int32_t *)r->d_work.p + 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess))
         return -3;
     if (hipEventRecord(r->done, st) != hipSuccess) return -3;
-    r->pending_check = true;
-    r->blocks.clear();
-    r->residuals.clear();
-    r->coefb.clear();
+    r->pending_check = n > 0;
+    drop_recording();
     return 0;
 }

@@ -184,6 +184,10 @@ class IntraConfig:
     inter_frac: float = 0.0
     mv_range: int = 32
     ref_pad: int = 64
+    # recorder kinds with block data (dav1d_gpu_rec_block_aux): this fraction
+    # of inter blocks becomes INTER_MASK / WARP / INTER_OBMC / INTER_WMASK /
+    # INTER_SCALED, and half as many intra blocks become palette blocks
+    ext_frac: float = 0.0
 
     @property
     def pixel_dtype(self):
@@ -222,6 +226,213 @@ class IntraFrame:
     @property
     def n_levels(self):
         return len(self.unit_start) - 1
+
+
+class _ExtBuilder:
+    """Blocks of the recorder kinds with block data (make_intra_frame's
+    ext_frac): the dav1d_gpu_rec_block_aux data handed to the recorder, and
+    -- independently of the recorder's own cutting (csrc/recorder.hip) --
+    the unit records of the same blocks for the oracle's decoder-order walk:
+    launch-ahead kinds (WARP / INTER_WMASK / INTER_OBMC / INTER_SCALED) as
+    prediction units of at most 32 x 32 (the unit batch's records,
+    include/dav1d_gpu.h Dav1dGpuPredKind), INTER_MASK / PAL per transform
+    unit.  OBMC and scaled geometry as in workload._ext2_records."""
+    PRE = (abi.PRED_WARP, abi.PRED_INTER_WMASK, abi.PRED_INTER_OBMC, abi.PRED_INTER_SCALED)
+
+    def __init__(self, cfg, rng, bdmax, refs):
+        self.cfg, self.rng, self.bdmax, self.refs = cfg, rng, bdmax, refs
+        self.chunks, self.off, self.used = [], 0, False
+        self.bd = {}     # (block, plane) -> block state
+        self.bb = {}     # block -> plane-independent draws
+
+    def put(self, rec):
+        rec = np.ascontiguousarray(rec, np.uint8).ravel()
+        at = self.off
+        pad = (-len(rec)) % 16
+        self.chunks.append(rec)
+        if pad:
+            self.chunks.append(np.zeros(pad, np.uint8))
+        self.off += len(rec) + pad
+        self.used = True
+        return at
+
+    def pool(self):
+        return np.concatenate(self.chunks) if self.chunks else np.zeros(16, np.uint8)
+
+    @staticmethod
+    def plane_kind(k, pl):
+        if not k:
+            return 0
+        if k == abi.PRED_WARP and pl:
+            return abi.PRED_INTER        # chroma of a warped block: translation
+        if k == abi.PRED_INTER_WMASK and pl:
+            return abi.PRED_INTER_MASK   # COMPOUND_SEG chroma: the luma's w_mask output
+        return k
+
+    def _block(self, b):
+        if b not in self.bb:
+            r = self.rng
+            self.bb[b] = dict(sign=int(r.integers(0, 2)), nref=int(r.integers(1, 3)),
+                              wt=int(0 if r.random() < 0.5 else r.integers(1, 16)),
+                              steps=r.integers(256, 2049, size=(2, 2)), phase=r.integers(0, 1024, size=(2, 2)),
+                              abcd=r.integers(-1024, 1025, 4).astype(np.int16), obmc=None)
+        return self.bb[b]
+
+    def weight(self, b, kind):
+        if kind == abi.PRED_INTER_WMASK:
+            return self._block(b)["sign"]
+        if kind == abi.PRED_INTER_SCALED:
+            bb = self._block(b)
+            return bb["wt"] if bb["nref"] == 2 else 0
+        return 0
+
+    def _obmc_lists(self, b, bw4):
+        bb = self._block(b)
+        if bb["obmc"] is None:
+            r, mr = self.rng, self.cfg.mv_range * 16
+            lw = bw4.bit_length() - 1
+            ents = {"top": [], "left": []}
+            for side in ("top", "left"):
+                pos = 0
+                while pos < bw4 and len(ents[side]) < min(lw, 4):
+                    step4 = int(np.clip(1 << int(r.integers(1, 5)), 2, 16))
+                    if r.random() < 0.8:
+                        ents[side].append((pos, step4, r.integers(-mr, mr + 1, 2), int(r.integers(0, 10)),
+                                           int(r.integers(0, 2))))
+                    pos += step4
+            bb["obmc"] = ents
+        return bb["obmc"]
+
+    def block_data(self, b, pl, kind, px, py, s, mvs, lx, ly, ls):
+        """The block's dav1d_gpu_rec_block_aux data: bytes, None (no data),
+        or False for a kind recorded with dav1d_gpu_rec_block."""
+        cfg, r = self.cfg, self.rng
+        bpp = 1 if cfg.bpc == 8 else 2
+        st = {"s": s, "px": px, "py": py, "mvs": mvs}
+        self.bd[(b, pl)] = st
+        if kind == abi.PRED_INTER_MASK:
+            if self._block(b).get("wm") is not None and pl:   # COMPOUND_SEG chroma
+                st["mask_at"], st["mask_stride"] = self._block(b)["wm"], s
+                return None
+            st["mask"] = r.integers(0, 65, (s, s)).astype(np.uint8)
+            return st["mask"].tobytes()
+        if kind == abi.PRED_PAL:
+            st["pal"] = r.integers(0, self.bdmax + 1, 8).astype(cfg.pixel_dtype)
+            idx = r.integers(0, 8, (s, s))
+            st["idx"] = (idx[:, 0::2] | (idx[:, 1::2] << 4)).astype(np.uint8)   # [s][s/2]
+            return st["pal"].tobytes() + st["idx"].tobytes()
+        if kind == abi.PRED_INTER_WMASK:
+            self._block(b)["wm"] = self.put(np.zeros((s // 2) * (s // 2), np.uint8))
+            st["wm"] = self._block(b)["wm"]
+            return None
+        if kind == abi.PRED_WARP:
+            a_ = self._block(b)["abcd"]
+            n8 = s // 8
+            sub = np.zeros((n8, n8), dtype=[("x", "<i2"), ("y", "<i2"), ("mx", "<i2"), ("my", "<i2")])
+            mvx, mvy = mvs[0][0] >> 4, mvs[0][1] >> 4
+            for sy in range(n8):
+                for sx in range(n8):
+                    sub["x"][sy, sx] = px + 8 * sx + mvx + int(r.integers(-2, 3))
+                    sub["y"][sy, sx] = py + 8 * sy + mvy + int(r.integers(-2, 3))
+                    sub["mx"][sy, sx] = ((int(r.integers(0, 65536)) - 4 * int(a_[0]) - 7 * int(a_[1])) & ~63) >> 6
+                    sub["my"][sy, sx] = ((int(r.integers(0, 65536)) - 4 * int(a_[2]) - 4 * int(a_[3])) & ~63) >> 6
+            st["warp"] = sub
+            return a_.tobytes() + bytes(8) + sub.tobytes()
+        if kind == abi.PRED_INTER_OBMC:
+            sub_ = 1 if pl else 0
+            hm = vm = 4 >> sub_
+            bw4 = int(ls[b]) // 4
+            lists = self._obmc_lists(b, bw4)
+            ents = []
+            if ly[b] > 0 and (not pl or bw4 * hm + bw4 * vm >= 16):
+                for (x, step4, m_, f2d, rr) in lists["top"]:
+                    ow4, oh4 = min(step4, bw4), min(bw4, 16) >> 1
+                    ents.append((0, x * hm, x * hm + ow4 * hm, 0, (vm * oh4 * 3) >> 2, ow4, (oh4 * 3 + 3) >> 2,
+                                 vm * oh4, m_, f2d, rr))
+            if lx[b] > 0:
+                for (y, step4, m_, f2d, rr) in lists["left"]:
+                    ow4, oh4 = min(bw4, 16) >> 1, min(step4, bw4)
+                    ents.append((1, 0, (hm * ow4 * 3) >> 2, y * vm, y * vm + oh4 * vm, ow4, oh4, hm * ow4, m_, f2d, rr))
+            blk = np.zeros(16 + 24 * len(ents), np.uint8)
+            blk[0:4] = np.array([len(ents)], "<i4").view(np.uint8)
+            laps = []
+            for k, (dr, xa, xb, ya, yb, lw4, lh4, mbase, m_, f2d, rr) in enumerate(ents):
+                mvx, mvy = (int(m_[0]) >> 1, int(m_[1]) >> 1) if pl else (int(m_[0]), int(m_[1]))
+                e = blk[16 + 24 * k:16 + 24 * (k + 1)]
+                e[0:8] = np.array([mvx, mvy], "<i4").view(np.uint8)
+                e[8:18] = [f2d, rr, xa, ya, xb, yb, (lw4 * hm) // 4, (lh4 * vm) // 4, dr, mbase]
+                laps.append((mvx, mvy, f2d, rr, xa, ya, xb, yb, (lw4 * hm) // 4, (lh4 * vm) // 4, dr, mbase))
+            st["laps"] = laps
+            return blk.tobytes()
+        if kind == abi.PRED_INTER_SCALED:
+            bb = self._block(b)
+            sub_ = 1 if pl else 0
+            pw_, ph_ = (cfg.width >> sub_, cfg.height >> sub_)
+            pad = cfg.ref_pad
+            recs = []
+            for k in range(bb["nref"]):
+                dx, dy = int(bb["steps"][k, 0]), int(bb["steps"][k, 1])
+                mx0, my0 = int(bb["phase"][k, 0]), int(bb["phase"][k, 1])
+                span_x, span_y = ((s - 1) * dx + mx0) >> 10, ((s - 1) * dy + my0) >> 10
+                gx = int(np.clip(px + (mvs[k][0] >> 4), -pad + 4, pw_ + pad - 6 - span_x))
+                gy = int(np.clip(py + (mvs[k][1] >> 4), -pad + 4, ph_ + pad - 6 - span_y))
+                recs.append((gx, gy, mx0, my0, dx, dy))
+            st["scaled"] = recs
+            blk = np.zeros(16 + 16 * len(recs), np.uint8)
+            blk[0:4] = np.array([len(recs)], "<i4").view(np.uint8)
+            for k, (gx, gy, mx0, my0, dx, dy) in enumerate(recs):
+                blk[16 + 16 * k:24 + 16 * k] = np.array([gx, gy], "<i4").view(np.uint8)
+                blk[24 + 16 * k:32 + 16 * k] = np.array([mx0, my0, dx, dy], "<u2").view(np.uint8)
+            return blk.tobytes()
+        return False
+
+    def unit_record(self, b, pl, kind, ox, oy, uw, uh, ux, uy):
+        """The oracle's aux value for a unit of the block at (ox, oy)."""
+        st = self.bd[(b, pl)]
+        s = st["s"]
+        bpp = 1 if self.cfg.bpc == 8 else 2
+        if kind == abi.PRED_INTER_MASK:
+            if "mask_at" not in st:
+                st["mask_at"], st["mask_stride"] = self.put(st["mask"]), s
+            return st["mask_at"] + oy * st["mask_stride"] + ox
+        if kind == abi.PRED_PAL:
+            rec = np.zeros(16 + (uw // 2) * uh, np.uint8)
+            rec[:8 * bpp] = st["pal"].view(np.uint8)
+            rec[16:] = st["idx"][oy:oy + uh, ox // 2:(ox + uw) // 2].ravel()
+            return self.put(rec)
+        if kind == abi.PRED_INTER_WMASK:
+            return st["wm"] + (oy >> 1) * (s >> 1) + (ox >> 1)
+        if kind == abi.PRED_WARP:
+            a_ = self._block(b)["abcd"]
+            sub = st["warp"][oy // 8:(oy + uh) // 8, ox // 8:(ox + uw) // 8]
+            return self.put(np.concatenate([a_.view(np.uint8), np.zeros(8, np.uint8),
+                                            np.ascontiguousarray(sub).view(np.uint8).ravel()]))
+        rs = self.refs[0][pl].shape[1]
+        if kind == abi.PRED_INTER_OBMC:
+            ents = []
+            for (mvx, mvy, f2d, rr, xa, ya, xb, yb, lw4, lh4, dr, mbase) in st["laps"]:
+                x0, x1 = max(xa - ox, 0), min(xb - ox, uw)
+                y0, y1 = max(ya - oy, 0), min(yb - oy, uh)
+                if x0 >= x1 or y0 >= y1:
+                    continue
+                e = np.zeros(16, np.uint8)
+                e[0:4] = np.array([(uy + (mvy >> 4)) * rs + ux + (mvx >> 4)], "<i4").view(np.uint8)
+                e[4:16] = [mvx & 15, mvy & 15, f2d, rr, x0, y0, x1, y1, lw4, lh4, dr, mbase + (ox if dr else oy)]
+                ents.append(e)
+            hdr = np.zeros(16, np.uint8)
+            hdr[0:4] = np.array([len(ents)], "<i4").view(np.uint8)
+            return self.put(np.concatenate([hdr] + ents))
+        if kind == abi.PRED_INTER_SCALED:
+            recs = st["scaled"]
+            out = np.zeros(16 + 16 * len(recs), np.uint8)
+            out[0:4] = np.array([len(recs)], "<i4").view(np.uint8)
+            for k, (gx, gy, mx0, my0, dx, dy) in enumerate(recs):
+                px_, py_ = mx0 + ox * dx, my0 + oy * dy
+                out[16 + 16 * k:20 + 16 * k] = np.array([(gy + (py_ >> 10)) * rs + gx + (px_ >> 10)],
+                                                        "<i4").view(np.uint8)
+                out[20 + 16 * k:28 + 16 * k] = np.array([px_ & 1023, py_ & 1023, dx, dy], "<u2").view(np.uint8)
+            return self.put(out)
+        raise ValueError(kind)
 
 
 def _morton(x, y):
@@ -286,6 +497,18 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
                 rp.append(np.ascontiguousarray(np.pad(a_, ((pad, pad), (pad, stride - pw_ - pad)), mode="edge")))
             refs.append(rp)
     is_inter = bkind != abi.PRED_INTRA
+    xk = np.zeros(nb, np.int64)   # a block's recorder kind with block data, 0 none
+    xr = np.random.default_rng(cfg.seed ^ 0xE7E7)
+    if cfg.ext_frac > 0:
+        ext_kinds = np.array([abi.PRED_INTER_MASK, abi.PRED_WARP, abi.PRED_INTER_OBMC, abi.PRED_INTER_WMASK,
+                              abi.PRED_INTER_SCALED])
+        xk = np.where(is_inter & (xr.random(nb) < cfg.ext_frac), ext_kinds[xr.integers(0, 5, nb)], 0)
+        pal_b = ~is_inter & (xr.random(nb) < cfg.ext_frac * 0.5)
+        xk = np.where(pal_b, abi.PRED_PAL, xk)
+        ymode[pal_b] = abi.DC_PRED     # palette blocks code DC_PRED (no smooth context)
+        uvmode[pal_b] = abi.DC_PRED
+        is_cfl[pal_b] = False
+    XB = _ExtBuilder(cfg, xr, bdmax, refs)
     # decode index of the block covering each luma 4x4
     bmap = np.full((H // 4, W // 4), -1, np.int64)
     for b in range(nb):
@@ -293,8 +516,10 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     assert bmap.min() >= 0
     smooth = lambda m: 9 <= m <= 11   # noqa: E731
 
-    U = {k: [] for k in ("plane", "x", "y", "tw", "th", "blk", "cfl", "mode", "angle", "flags")}
+    U = {k: [] for k in ("plane", "x", "y", "tw", "th", "blk", "cfl", "mode", "angle", "flags", "pred", "aux",
+                         "bsz", "weight", "nores")}
     BL = []   # per block and plane, decode order: what recon_b_* hands the recorder
+    BLX = []  # per BL entry: its dav1d_gpu_rec_block_aux data (bytes), None, or False (plain block)
     for b in range(nb):
         x, y, s = int(lx[b]), int(ly[b]), int(ls[b])
         x0, y0, x1, y1 = int(tile_x0[b]), int(tile_y0[b]), int(tile_x1[b]), int(tile_y1[b])
@@ -317,17 +542,32 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
             cfl = pl > 0 and bool(is_cfl[b]) and not is_inter[b]
             bw4 = ps_ // 4
             kind_ = int(bkind[b]) if is_inter[b] else (abi.PRED_CFL if cfl else abi.PRED_INTRA)
+            xkind = XB.plane_kind(int(xk[b]), pl)
+            if xkind:
+                kind_ = xkind
             bfl = (abi.IE_TOP_HAS_RIGHT if tr else 0) | (abi.IE_LEFT_HAS_BOTTOM if bl else 0)
             if cfg.filter_edge:
                 bfl |= abi.IE_FILTER_EDGE
             if (ysm if pl == 0 else uvsm):
                 bfl |= abi.IE_SMOOTH
             mvs = [(int(bmv[b, k, 0]) >> ss, int(bmv[b, k, 1]) >> ss) for k in range(2)]
+            weight = XB.weight(b, kind_)
             BL.append((pl, px_, py_, ps_, ps_, abi.TX_INDEX[(tw, th)], kind_, x0 >> ss, y0 >> ss, x1 >> ss,
-                       y1 >> ss, mvs[0][0], mvs[1][0], mvs[0][1], mvs[1][1], 0, 1, int(bfilt[b]), 0,
+                       y1 >> ss, mvs[0][0], mvs[1][0], mvs[0][1], mvs[1][1], 0, 1, int(bfilt[b]), weight,
                        0 if cfl else int(ymode[b] if pl == 0 else uvmode[b]),
                        0 if cfl else int(yang[b] if pl == 0 else uvang[b]),
                        int(alpha[b, pl - 1]) if cfl else 0, 0 if cfl or is_inter[b] else bfl))
+            BLX.append(XB.block_data(b, pl, kind_, px_, py_, ps_, mvs, lx, ly, ls))
+            if kind_ in XB.PRE:   # prediction units ahead of the wavefront, <= 32 x 32
+                us = min(ps_, 32)
+                for oy in range(0, ps_, us):
+                    for ox in range(0, ps_, us):
+                        rec_ = XB.unit_record(b, pl, kind_, ox, oy, us, us, px_ + ox, py_ + oy)
+                        for k_, v_ in (("plane", pl), ("x", px_ + ox), ("y", py_ + oy), ("tw", us), ("th", us),
+                                       ("blk", b), ("cfl", False), ("mode", 0), ("angle", 0), ("flags", 0),
+                                       ("pred", kind_), ("aux", rec_), ("bsz", ps_), ("weight", weight),
+                                       ("nores", True)):
+                            U[k_].append(v_)
             for oy in range(0, ps_, th):
                 for ox in range(0, ps_, tw):
                     x4, y4 = ox // 4, oy // 4
@@ -351,6 +591,13 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
                     U["mode"].append(abi.DC_PRED if cfl else int(ymode[b] if pl == 0 else uvmode[b]))
                     U["angle"].append(0 if cfl else int(yang[b] if pl == 0 else uvang[b]))
                     U["flags"].append(fl)
+                    U["pred"].append(abi.PRED_NONE if kind_ in XB.PRE else kind_)
+                    U["aux"].append(XB.unit_record(b, pl, kind_, ox, oy, tw, th, px_ + ox, py_ + oy)
+                                    if kind_ in (abi.PRED_INTER_MASK, abi.PRED_PAL) else -1)
+                    U["bsz"].append(ps_)
+                    U["weight"].append(weight)
+                    # residual-only units of launch-ahead blocks: some carry none
+                    U["nores"].append(kind_ in XB.PRE and XB.rng.random() < 0.3)
     plane_u = np.array(U["plane"], np.int32)
     ux, uy = np.array(U["x"], np.int32), np.array(U["y"], np.int32)
     tw, th = np.array(U["tw"], np.int32), np.array(U["th"], np.int32)
@@ -374,11 +621,14 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     units["dst_off"] = uy * pw[plane_u] + ux
     units["tx"] = tx
     units["plane"] = plane_u
-    interu = is_inter[blk]
-    units["pred"] = np.where(interu, bkind[blk], np.where(cflu, abi.PRED_CFL, abi.PRED_INTRA))
-    bsz = ls[blk] >> np.where(plane_u > 0, 1, 0)
+    predu = np.array(U["pred"], np.int32)
+    units["pred"] = predu
+    # units that read no picture pixels: inter kinds, palette, residual-only
+    interu = ~np.isin(predu, (abi.PRED_INTRA, abi.PRED_CFL))
+    bsz = np.array(U["bsz"], np.int32)
     units["bw4"] = units["bh4"] = np.where(interu, bsz // 4, 0)
     txtp, nzw, nzh, coef_off, coefs = make_residuals(rng, tx, tw, th, bdmax, cfg.coef_dtype)
+    txtp = np.where(np.array(U["nores"], bool), abi.NO_RESIDUAL, txtp)
     units["txtp"], units["nzw"], units["nzh"], units["coef_off"] = txtp, nzw, nzh, coef_off
     edge_len = np.where(interu, 0, 2 * th + 2 * tw + 1)
     edge_start = np.concatenate([[0], np.cumsum(edge_len)[:-1]])
@@ -400,7 +650,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
             iv[f"my{k}"] = mvy & 15
             iv[f"ref{k}"] = k
         iv["filter2d"] = bfilt[ib_]
-        iv["weight"] = 0
+        iv["weight"] = np.array(U["weight"], np.int32)[interu]
         units[interu] = iv
     cu = units[cflu]
     cu["cfl_alpha"] = alpha[blk[cflu], plane_u[cflu] - 1]
@@ -511,6 +761,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     recs["w4"], recs["h4"] = tx1 // 4, ty1 // 4
     recs["mode"], recs["angle"], recs["flags"] = modes, angles, flags
     recs = recs[perm]
+    aux = np.array(U["aux"], np.int64)[perm].astype(np.int32)
     rec_start = unit_start.copy()
     unit_rec = np.where(np.isin(units["pred"], (abi.PRED_INTRA, abi.PRED_CFL)), np.arange(n), -1).astype(np.int32)
     rp = np.argsort(run_lv, kind="stable")
@@ -528,11 +779,14 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
                     run_start, steps, unit_rec, np.array(oracle_runs, abi.EDGE_BACKUP_DTYPE), top_rows, sbl,
                     refs, dep_start, deps)
     fr.blocks = BL
+    fr.block_aux = BLX
     fr.dec_units = dec_units
+    fr.aux = aux if XB.used else None
+    fr.aux_pool = XB.pool() if XB.used else None
     return fr
 
 
-def frame_batch(fr, dst_ptrs, units, coefs, edges, ref_ptrs=None):
+def frame_batch(fr, dst_ptrs, units, coefs, edges, ref_ptrs=None, aux=None, aux_pool=None):
     """abi.FrameBatch of an IntraFrame (cfl_luma = the reconstructed luma;
     ref_ptrs[r][p]: addresses of the padded reference planes, mixed frames)."""
     bpp = 1 if fr.cfg.bpc == 8 else 2
@@ -551,6 +805,8 @@ def frame_batch(fr, dst_ptrs, units, coefs, edges, ref_ptrs=None):
     W, H = fr.plane_wh[0]
     b.cfl_luma.data, b.cfl_luma.stride, b.cfl_luma.w, b.cfl_luma.h = dst_ptrs[0], W * bpp, W, H
     b.cfl_ss = 3
+    if aux is not None:   # per-unit aux offsets (unit order) and the aux pool
+        b.aux, b.aux_pool = aux, aux_pool
     return b
 
 
@@ -681,6 +937,13 @@ class Recorder:
         if rc:
             raise ValueError(f"dav1d_gpu_rec_block: {rc}")
 
+    def block_aux(self, rb, data):
+        """dav1d_gpu_rec_block_aux: a block with its kind's data (bytes or None)."""
+        buf = None if data is None else ctypes.create_string_buffer(bytes(data), len(data))
+        rc = self.lib.dav1d_gpu_rec_block_aux(self.h, ctypes.byref(rb), buf, 0 if data is None else len(data))
+        if rc:
+            raise ValueError(f"dav1d_gpu_rec_block_aux: {rc}")
+
     def residual(self, plane, x, y, tx, txtp, eob, coef):
         c = np.ascontiguousarray(coef, dtype=np.int16 if self.bpc == 8 else np.int32)
         rc = self.lib.dav1d_gpu_rec_residual(self.h, plane, x, y, tx, txtp, eob, c.ctypes.data)
@@ -733,14 +996,18 @@ def replay(rec, fr, rows=None):
             return True
         s = 1 if p else 0
         return (rows[0] >> s) <= y < (rows[1] >> s)
-    for t in fr.blocks:
+    bx = getattr(fr, "block_aux", None) or [False] * len(fr.blocks)
+    for t, data in zip(fr.blocks, bx):
         if not inside(t[0], t[2]):
             continue
         rb = abi.RecBlock()
         (rb.plane, rb.x, rb.y, rb.w, rb.h, rb.tx, rb.kind, rb.tile_x0, rb.tile_y0, rb.tile_x1, rb.tile_y1,
          rb.mvx[0], rb.mvx[1], rb.mvy[0], rb.mvy[1], rb.ref[0], rb.ref[1], rb.filter2d, rb.weight, rb.mode,
          rb.angle, rb.cfl_alpha, rb.flags) = t
-        rec.block(rb)
+        if data is False:
+            rec.block(rb)
+        else:
+            rec.block_aux(rb, data)
     u = fr.dec_units
     for i in np.nonzero(u["txtp"] != abi.NO_RESIDUAL)[0]:
         p = int(u["plane"][i])

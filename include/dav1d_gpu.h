@@ -711,7 +711,9 @@ typedef struct Dav1dGpuRecBlock {
     int32_t x, y, w, h;      /* the prediction block, plane pixels            */
     int32_t tx;              /* its transform size (b->tx / uvtx), uniform    */
     int32_t kind;            /* DGPU_PRED_INTER / INTER_AVG / INTER_WAVG /
-                                INTRA / CFL                                   */
+                                INTRA / CFL, or (with dav1d_gpu_rec_block_aux)
+                                INTER_MASK / PAL / WARP / INTER_WMASK /
+                                INTER_OBMC / INTER_SCALED                     */
     int32_t tile_x0, tile_y0, tile_x1, tile_y1;   /* the tile, plane pixels    */
     /* inter: the mc() call per reference (src/recon_tmpl.c:957): the
        motion vector in 1/16 plane pixels (chroma already scaled), the ref
@@ -739,6 +741,41 @@ void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r);
 int dav1d_gpu_rec_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b);
 int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int y, int tx, int txtp, int eob,
                            const void *coef);
+/* A block of a kind that carries data beside its Dav1dGpuRecBlock, with that
+ * data for the whole block (the recorder cuts it per unit).  Layouts, plane
+ * pixels, block-relative:
+ *   INTER_MASK  (mask(), src/mc_tmpl.c:622-639; wedge / seg compound):
+ *               uint8 mask[h][w] 0..64; aux = NULL for a chroma block of a
+ *               COMPOUND_SEG prediction: the mask the last INTER_WMASK block
+ *               wrote (recon_tmpl.c:1900)
+ *   PAL         (pal_pred, ipred_tmpl.c:717-730, recon_tmpl.c:1233-1250,
+ *               1425-1445): pixel pal[8] then uint8 idx[h][w / 2] (two 4-bit
+ *               indices per byte, low nibble first, as t->scratch.pal_idx_*)
+ *   WARP        (warp_affine, recon_tmpl.c:1134-1193): int16 abcd[4], 8 pad
+ *               bytes, then per 8x8 of the block (row-major) int16 x, y, mx >> 6,
+ *               my >> 6 as Dav1dGpuPredKind WARP's unit record
+ *   INTER_WMASK (COMPOUND_SEG luma, w_mask, recon_tmpl.c:1854): no data
+ *               (weight = mask_sign); writes the seg mask its chroma blocks'
+ *               INTER_MASK (aux = NULL) read
+ *   INTER_OBMC  (obmc(), recon_tmpl.c:1071-1133): int32 n, 12 pad bytes, then
+ *               n lap entries of 24 B: int32 mvx, mvy (the neighbour's mv,
+ *               1/16 plane px), uint8 filter2d, ref, x0, y0, x1, y1 (the
+ *               overlap, block px [x0, x1) x [y0, y1)), lap_w4, lap_h4 (the
+ *               lap call's size, plane px / 4), dir (0 above, 1 left),
+ *               mask_off (block row / column i blends with
+ *               dav1d_obmc_masks[mask_off + i]), 6 pad bytes; above first
+ *   INTER_SCALED (mc() of a scaled reference, recon_tmpl.c:1006-1060):
+ *               int32 n_refs, 12 pad bytes, then per ref 16 B: int32 x, y
+ *               (integer source position of block pixel (0, 0): pos >> 10),
+ *               uint16 mx, my (pos & 1023), uint16 dx, dy (steps)
+ * INTER_WMASK / OBMC / SCALED / WARP predictions run in a launch of their own
+ * ahead of the wavefront (dav1d_gpu_recon_*'s second launch), cut into
+ * prediction units of at most 32 x 32; their residuals are added by PRED_NONE
+ * units in the wavefront.  Those four kinds read their references directly:
+ * the reference planes need the padding the unit batch documents (the
+ * emu_edge clamp covers INTER / INTER_AVG / INTER_WAVG / INTER_MASK).
+ * INTER_INTRA is not recorded.  0 or -1. */
+int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, const void *aux, size_t aux_bytes);
 /* Build, upload and launch everything recorded since the last flush on
  * `stream` (the recorder waits for its previous flush before reusing its
  * buffers).  dst: the picture being reconstructed (CfL reads its luma);

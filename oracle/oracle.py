@@ -301,8 +301,14 @@ class HostIntraFrame:
         self.unit_rec = np.ascontiguousarray(fr.unit_rec, dtype=np.int32)
         self.oruns = np.ascontiguousarray(fr.oracle_runs) if len(fr.oracle_runs) else np.zeros(1, abi.EDGE_BACKUP_DTYPE)
         d = [a.ctypes.data for a in self.dst]
+        # recorder kinds with block data: per-unit aux offsets and a writable
+        # pool (INTER_WMASK units write the seg mask their chroma units read)
+        self.aux = None if getattr(fr, "aux", None) is None else np.ascontiguousarray(fr.aux, dtype=np.int32)
+        self.aux_pool = None if self.aux is None else np.ascontiguousarray(fr.aux_pool, dtype=np.uint8).copy()
         self.rb = intra.frame_batch(fr, d, self.units.ctypes.data, self.coefs.ctypes.data, self.edges.ctypes.data,
-                                    [[a.ctypes.data for a in rp] for rp in (fr.refs or [])])
+                                    [[a.ctypes.data for a in rp] for rp in (fr.refs or [])],
+                                    None if self.aux is None else self.aux.ctypes.data,
+                                    None if self.aux is None else self.aux_pool.ctypes.data)
         self.eb = intra.edge_batch(fr, d, [a.ctypes.data for a in self.top], self.units.ctypes.data,
                                    self.edges.ctypes.data, self.recs.ctypes.data)
 

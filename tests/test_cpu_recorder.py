@@ -75,3 +75,41 @@ def test_recorder_validation(pkg):
         assert L.dav1d_gpu_recorder_stats(r, ctypes.byref(n), ctypes.byref(lv)) == 0 and n.value == 0
     finally:
         L.dav1d_gpu_recorder_free(r)
+
+
+def test_recorder_block_aux_validation(pkg):
+    """dav1d_gpu_rec_block_aux: the data size each kind documents, the kinds
+    it takes (and that dav1d_gpu_rec_block refuses them), COMPOUND_SEG
+    chroma without data only on chroma planes, WARP on 8-px geometry."""
+    L = pkg.abi.load_lib()
+    abi = pkg.abi
+    r = L.dav1d_gpu_recorder_new(8, 255, 64, 64, 0)
+    assert r
+    try:
+        def rec(data, **kw):
+            b = _blk(pkg, **kw)
+            buf = None if data is None else ctypes.create_string_buffer(bytes(data), len(data))
+            return L.dav1d_gpu_rec_block_aux(r, ctypes.byref(b), buf, 0 if data is None else len(data))
+        assert rec(bytes(256), kind=abi.PRED_INTER_MASK) == 0
+        assert rec(bytes(255), kind=abi.PRED_INTER_MASK) == -1
+        assert rec(None, kind=abi.PRED_INTER_MASK) == -1                      # luma needs its mask
+        assert rec(None, kind=abi.PRED_INTER_MASK, plane=1, x=8, y=8, w=8, h=8, tile_x1=32, tile_y1=32) == 0
+        assert rec(bytes(8 + 8 * 16), kind=abi.PRED_PAL) == 0
+        assert rec(bytes(8 + 8 * 15), kind=abi.PRED_PAL) == -1
+        assert rec(bytes(16 + 4 * 8), kind=abi.PRED_WARP) == 0
+        assert rec(bytes(16 + 4 * 8), kind=abi.PRED_WARP, x=20) == -1         # 8-px aligned
+        assert rec(None, kind=abi.PRED_INTER_WMASK) == 0
+        assert rec(None, kind=abi.PRED_INTER_WMASK, weight=2) == -1           # mask_sign 0 / 1
+        obmc = np.zeros(16 + 24 * 2, np.uint8)
+        obmc[0] = 2
+        assert rec(obmc.tobytes(), kind=abi.PRED_INTER_OBMC) == 0
+        assert rec(obmc[:-1].tobytes(), kind=abi.PRED_INTER_OBMC) == -1
+        sc = np.zeros(16 + 16 * 2, np.uint8)
+        sc[0] = 2
+        assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == 0
+        sc[0] = 3
+        assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == -1
+        assert rec(bytes(16), kind=abi.PRED_INTER) == -1                      # no data kind
+        assert L.dav1d_gpu_rec_block(r, ctypes.byref(_blk(pkg, kind=abi.PRED_WARP))) == -1
+    finally:
+        L.dav1d_gpu_recorder_free(r)

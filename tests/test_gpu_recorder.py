@@ -183,3 +183,50 @@ def test_recorder_unpadded_references(oracle, bpc, bdmax, seed):
     assert rec.status() == 0
     _compare(fr, dst, oracle)
     rec.close()
+
+
+@pytest.mark.parametrize("bpc,bdmax,seed", [(8, 255, 81), (16, 1023, 82), (16, 4095, 83)])
+def test_recorder_block_data_kinds(oracle, bpc, bdmax, seed):
+    """Blocks recorded with their data (dav1d_gpu_rec_block_aux): INTER_MASK
+    (caller masks, and COMPOUND_SEG chroma on the luma's w_mask output),
+    palette, WARP, INTER_WMASK, INTER_OBMC and INTER_SCALED, beside intra /
+    CfL / inter blocks whose edges read them.  The recorder cuts the
+    launch-ahead kinds into prediction units and adds their residuals in the
+    wavefront; the oracle walks its own cut of the same blocks in decoder
+    order (dav1d_mirror_amd.intra._ExtBuilder)."""
+    import torch
+    import dav1d_mirror_amd.intra as intra
+    fr = intra.make_intra_frame(intra.IntraConfig(seed=seed, width=384, height=256, bpc=bpc, bitdepth_max=bdmax,
+                                                  inter_frac=0.6, ext_frac=0.7, sb_edge_backup=False))
+    kinds = set(int(k) for k in fr.units["pred"])
+    import dav1d_mirror_amd.abi as abi
+    assert {abi.PRED_INTER_MASK, abi.PRED_PAL, abi.PRED_WARP, abi.PRED_INTER_WMASK, abi.PRED_INTER_OBMC,
+            abi.PRED_INTER_SCALED} <= kinds
+    dst, refs = _setup(fr)
+    rec = intra.Recorder(fr.cfg.bpc, fr.cfg.bitdepth_max, fr.cfg.width, fr.cfg.height)
+    intra.replay(rec, fr)
+    rec.flush(dst, refs, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert rec.status() == 0
+    _compare(fr, dst, oracle)
+    rec.close()
+
+
+def test_recorder_block_data_per_superblock_row(oracle):
+    """The same kinds flushed per 64-px superblock row: a COMPOUND_SEG chroma
+    block finds its luma's mask in the same flush; flushes with only
+    launch-ahead work are valid."""
+    import torch
+    import dav1d_mirror_amd.intra as intra
+    fr = intra.make_intra_frame(intra.IntraConfig(seed=84, width=384, height=256, inter_frac=0.7, ext_frac=0.8,
+                                                  sb_edge_backup=False))
+    dst, refs = _setup(fr)
+    rec = intra.Recorder(fr.cfg.bpc, fr.cfg.bitdepth_max, fr.cfg.width, fr.cfg.height)
+    s = torch.cuda.current_stream()
+    for y0 in range(0, fr.cfg.height, 64):
+        intra.replay(rec, fr, rows=(y0, y0 + 64))
+        rec.flush(dst, refs, s)
+    assert rec.status() == 0
+    torch.cuda.synchronize()
+    _compare(fr, dst, oracle)
+    rec.close()
