@@ -617,6 +617,7 @@ def main():
                 "parallelism": f"frame-sharded x{world}",
                 "zero_coefs": False,
                 "launches_per_step": 1,
+                "library_sources": dict(zip(("built_from", "tree", "matches_tree"), pkg.abi.build_stamp())),
             },
             "roofline": {
                 "bound": "hbm",

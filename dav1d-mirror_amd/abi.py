@@ -267,6 +267,7 @@ def load_lib():
         L.dav1d_gpu_recon_16bpc.restype = ctypes.c_int
         L.dav1d_gpu_device_count.restype = ctypes.c_int
         L.dav1d_gpu_version.restype = ctypes.c_char_p
+        L.dav1d_gpu_source_hash.restype = ctypes.c_char_p
         for bpc in (8, 16):
             f = getattr(L, f"dav1d_gpu_recon_tiles_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(TileBatch), ctypes.c_void_p]
@@ -339,7 +340,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_mc_dsp_init_gpu_8bpc", "dav1d_mc_dsp_init_gpu_16bpc",
     "dav1d_intra_pred_dsp_init_gpu_8bpc", "dav1d_intra_pred_dsp_init_gpu_16bpc",
     "dav1d_itx_dsp_init_gpu_8bpc", "dav1d_itx_dsp_init_gpu_16bpc",
-    "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version",
+    "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version", "dav1d_gpu_source_hash",
     "dav1d_gpu_get_error", "dav1d_gpu_clear_error",
     "dav1d_gpu_pic_allocator_init", "dav1d_gpu_pic_allocator_close", "dav1d_gpu_picture_plane",
     "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc", "dav1d_gpu_recon_lds_bytes",
@@ -361,3 +362,17 @@ EXPORTED_SYMBOLS = [
     "dav1d_loop_restoration_dsp_init_gpu_8bpc", "dav1d_loop_restoration_dsp_init_gpu_16bpc",
     "dav1d_gpu_lr_frame_8bpc", "dav1d_gpu_lr_frame_16bpc",
 ]
+
+
+def build_stamp():
+    """(library source hash, hash of the sources in this tree, equal?): a
+    library built from other sources than the tree's is stale."""
+    import importlib.util
+    import pathlib
+    root = pathlib.Path(__file__).resolve().parents[1]
+    spec = importlib.util.spec_from_file_location("_dgpu_src_hash", root / "tools" / "src_hash.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    lib = load_lib().dav1d_gpu_source_hash().decode()
+    tree = mod.source_hash(str(root))
+    return lib, tree, lib == tree

@@ -202,6 +202,8 @@ int dav1d_gpu_device_count(void);
 int dav1d_gpu_set_device(int device);
 /* Library build identification, e.g. "dav1d-gpu gfx950 r3". */
 const char *dav1d_gpu_version(void);
+/* SHA-1 of the sources the library was built from (tools/src_hash.py). */
+const char *dav1d_gpu_source_hash(void);
 /* Sticky error of the per-call tier: 0, or the first HIP error code (-1: no
  * device) latched since the last clear.  While it is set the per-call entries
  * do not touch the GPU (fallback entries, or no output).  clear returns the
