@@ -238,7 +238,7 @@ struct Dav1dGpuRecorder {
 };
 
 extern "C" Dav1dGpuRecorder *dav1d_gpu_recorder_new(int bpc, int bitdepth_max, int width, int height, int device) {
-    if ((bpc != 8 && bpc != 16) || width <= 0 || height <= 0 || (width & 7) || (height & 7)) return nullptr;
+    if ((bpc != 8 && bpc != 16) || width <= 0 || height <= 0) return nullptr;
     Dav1dGpuRecorder *r = new Dav1dGpuRecorder();
     r->bpc = bpc;
     r->bdmax = bpc == 8 ? 255 : bitdepth_max;
@@ -272,19 +272,26 @@ extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
     delete r;
 }
 
+// the plane's part of the decoder's block grid: 4 * f->bw x 4 * f->bh, the
+// picture size rounded up to 8 (src/decode.c), >> 1 for 4:2:0 chroma.
+// Blocks start inside it and may run past it into the picture's padding;
+// transform blocks start inside it (recon_tmpl.c:1208 w4 / h4 clip)
 static bool plane_dims(const Dav1dGpuRecorder *r, int plane, int &w, int &h) {
     if (plane < 0 || plane > 2) return false;
-    w = plane ? r->width >> 1 : r->width;
-    h = plane ? r->height >> 1 : r->height;
+    const int gw = (r->width + 7) & ~7, gh = (r->height + 7) & ~7;
+    w = plane ? gw >> 1 : gw;
+    h = plane ? gh >> 1 : gh;
     return true;
 }
+constexpr int kMapPad4 = 32;   // 4x4 cells past the grid a transform block can reach (128 px)
 
 static int check_block(const Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, bool ext) {
     int pw, ph;
     if (!r || !b || !plane_dims(r, b->plane, pw, ph)) return -1;
     if (b->tx < 0 || b->tx >= DGPU_N_RECT_TX_SIZES) return -1;
     const TxDim t = kTx[b->tx];
-    if (b->x < 0 || b->y < 0 || b->w <= 0 || b->h <= 0 || b->x + b->w > pw || b->y + b->h > ph) return -1;
+    if (b->x < 0 || b->y < 0 || b->w <= 0 || b->h <= 0 || b->x >= pw || b->y >= ph || b->w > 128 || b->h > 128)
+        return -1;
     if ((b->x & 3) || (b->y & 3) || b->w % t.w || b->h % t.h) return -1;
     if (ext != is_ext_kind(b->kind)) return -1;
     const bool inter = b->kind == DGPU_PRED_INTER || b->kind == DGPU_PRED_INTER_AVG ||
@@ -292,11 +299,14 @@ static int check_block(const Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, boo
     if (!inter && b->kind != DGPU_PRED_INTRA && b->kind != DGPU_PRED_CFL && b->kind != DGPU_PRED_PAL) return -1;
     if (b->kind == DGPU_PRED_CFL && (b->plane == 0 || b->w != t.w || b->h != t.h || t.w != t.h || t.w > 32))
         return -1;   // CfL: one unit per chroma block (cfl_ac + cfl_pred, :1372-1414)
-    if (!inter && b->mode > 13) return -1;
+    if (b->kind == DGPU_PRED_CFL ? ((b->mode & 15) >= b->w / 4 || (b->mode >> 4) >= b->h / 4)
+                                 : (!inter && b->mode > 13))
+        return -1;   // CFL: mode = cfl_ac's w_pad | h_pad << 4
     if (inter && (b->ref[0] >= DGPU_REC_EMU_SLOT || b->ref[1] >= DGPU_REC_EMU_SLOT || b->filter2d > 9)) return -1;
     if (b->tile_x0 < 0 || b->tile_y0 < 0 || b->tile_x1 > pw || b->tile_y1 > ph || b->x < b->tile_x0 ||
-        b->y < b->tile_y0 || b->x + b->w > b->tile_x1 || b->y + b->h > b->tile_y1)
-        return -1;
+        b->y < b->tile_y0 || b->x >= b->tile_x1 || b->y >= b->tile_y1 ||
+        (b->x + b->w > b->tile_x1 && b->tile_x1 != pw) || (b->y + b->h > b->tile_y1 && b->tile_y1 != ph))
+        return -1;   // inside its tile; only the grid's last tiles' blocks overhang
     return 0;
 }
 
@@ -361,7 +371,7 @@ extern "C" int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int
     if (!r || !coef || !plane_dims(r, plane, pw, ph) || tx < 0 || tx >= DGPU_N_RECT_TX_SIZES) return -1;
     if (txtp < 0 || txtp >= DGPU_N_TX_TYPES_PLUS_LL || eob < 0) return -1;
     const TxDim t = kTx[tx];
-    if (x < 0 || y < 0 || x + t.w > pw || y + t.h > ph || (x & 3) || (y & 3)) return -1;
+    if (x < 0 || y < 0 || x >= pw || y >= ph || (x & 3) || (y & 3)) return -1;   // starts inside the grid
     const int sw = std::min(t.w, 32), sh = std::min(t.h, 32);
     const size_t cb = r->bpc == 8 ? 2 : 4;
     Residual res{plane, x, y, tx, txtp, 0, 0, r->coefb.size() / cb};
@@ -449,12 +459,18 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     int pw[3], ph[3];
     for (int p = 0; p < 3; p++) plane_dims(r, p, pw[p], ph[p]);
 
+    // per-4x4 maps over the grid plus the overhang transform blocks can reach
+    int mw[3], mh[3];
+    for (int p = 0; p < 3; p++) {
+        mw[p] = pw[p] / 4 + kMapPad4;
+        mh[p] = ph[p] / 4 + kMapPad4;
+    }
     // residual lookup: per plane, the top-left 4x4 cell of each residual
     std::vector<int32_t> res_at[3];
-    for (int p = 0; p < 3; p++) res_at[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
+    for (int p = 0; p < 3; p++) res_at[p].assign((size_t)mw[p] * mh[p], -1);
     for (size_t i = 0; i < r->residuals.size(); i++) {
         const Residual &q = r->residuals[i];
-        res_at[q.plane][(size_t)(q.y / 4) * (pw[q.plane] / 4) + q.x / 4] = (int32_t)i;
+        res_at[q.plane][(size_t)(q.y / 4) * mw[q.plane] + q.x / 4] = (int32_t)i;
     }
 
     // 1-3. transform units in decode order, their edge records and levels
@@ -465,11 +481,11 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         for (const Dav1dGpuRecBlock &b : r->blocks) nc += (size_t)(b.w / kTx[b.tx].w) * (b.h / kTx[b.tx].h);
         cells.reserve(nc);
     }
-    std::vector<int32_t> lv[3], own[3];   // per 4x4: level, and the decode-order cell writing it
-    for (int p = 0; p < 3; p++) {
-        lv[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
-        own[p].assign((size_t)(pw[p] / 4) * (ph[p] / 4), -1);
-    }
+    // per 4x4: level and the decode-order cell writing it, side by side (one
+    // cache line per lookup)
+    struct LvOwn { int32_t lv, own; };
+    std::vector<LvOwn> lvown[3];
+    for (int p = 0; p < 3; p++) lvown[p].assign((size_t)mw[p] * mh[p], LvOwn{-1, -1});
     lap("maps");
     r->emu.clear();
     int32_t emu_rows = 0;
@@ -495,12 +511,16 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     for (size_t bi = 0; bi < r->blocks.size(); bi++) {
         const Dav1dGpuRecBlock &b = r->blocks[bi];
         const TxDim t = kTx[b.tx];
-        const int p = b.plane, w4p = pw[p] / 4;
+        const int p = b.plane, w4p = mw[p];
+        // the part of the block the decoder iterates: w4 / h4 clipped to the
+        // grid (recon_tmpl.c:1208); transform blocks start inside it
         const bool inter = is_mc_kind(b.kind);
         const bool cfl = b.kind == DGPU_PRED_CFL, pal = b.kind == DGPU_PRED_PAL;
         const bool pre = is_prelaunch_kind(b.kind);
         const uint8_t *bdata = r->block_aux[bi] >= 0 ? &r->baux[(size_t)r->block_aux[bi]] : nullptr;
         const int bw4 = b.w / 4, bh4 = b.h / 4, tw4 = t.w / 4, th4 = t.h / 4;
+        const int bwc = std::min(b.w, pw[p] - b.x), bhc = std::min(b.h, ph[p] - b.y);
+        const int bw4c = bwc / 4, bh4c = bhc / 4;
         const int ds_px = (int)(dst[p].stride / bpp);
         // every reference an inter block reads must be given
         if (inter || pre) {
@@ -529,8 +549,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 wm_h = b.h >> 1;
                 wm_off = aux_alloc((size_t)wm_w * wm_h);
             }
-            for (int oy = 0; oy < b.h; oy += uh)
-                for (int ox = 0; ox < b.w; ox += uw) {
+            for (int oy = 0; oy < bhc; oy += uh)
+                for (int ox = 0; ox < bwc; ox += uw) {
                     const int ux = b.x + ox, uy = b.y + oy;
                     Dav1dGpuUnit u;
                     memset(&u, 0, sizeof(u));
@@ -609,9 +629,10 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     xaux.push_back(ao);
                 }
         }
-        for (int oy = 0; oy < b.h; oy += t.h)
-            for (int ox = 0; ox < b.w; ox += t.w) {
-                Unit c;
+        for (int oy = 0; oy < bhc; oy += t.h)
+            for (int ox = 0; ox < bwc; ox += t.w) {
+                cells.emplace_back();   // built in place (popped again when skipped)
+                Unit &c = cells.back();
                 memset(&c, 0, sizeof(c));
                 const int ux = b.x + ox, uy = b.y + oy, x4 = ux / 4, y4 = uy / 4;
                 Dav1dGpuUnit &u = c.u;
@@ -631,6 +652,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 } else if (ri >= 0) {
                     return -1;   // a residual whose size differs from its block's transforms
                 } else if (pre) {
+                    cells.pop_back();
                     continue;   // predicted ahead of the wavefront, nothing to add
                 }
                 Dav1dGpuIntraEdge &e = c.rec;
@@ -693,8 +715,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     if (!cfl) {   // recon_tmpl.c:1252-1266 (blocks up to 64 wide: one 64x64 step)
                         const int x = ox / 4, y = oy / 4;
                         const bool sb_tr = b.flags & DGPU_IE_TOP_HAS_RIGHT, sb_bl = b.flags & DGPU_IE_LEFT_HAS_BOTTOM;
-                        if (!((y > 0 || !sb_tr) && x + tw4 >= bw4)) fl |= DGPU_IE_TOP_HAS_RIGHT;
-                        if (!(x > 0 || (!sb_bl && y + th4 >= bh4))) fl |= DGPU_IE_LEFT_HAS_BOTTOM;
+                        if (!((y > 0 || !sb_tr) && x + tw4 >= bw4c)) fl |= DGPU_IE_TOP_HAS_RIGHT;
+                        if (!(x > 0 || (!sb_bl && y + th4 >= bh4c))) fl |= DGPU_IE_LEFT_HAS_BOTTOM;
                         fl |= b.flags & (DGPU_IE_FILTER_EDGE | DGPU_IE_SMOOTH);
                         e.mode = b.mode;
                         e.angle = b.angle;
@@ -704,6 +726,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         e.mode = DGPU_DC_PRED;   // cfl_pred's DC source (:1395-1410)
                         e.angle = 0;
                         u.p.cfl.alpha = b.cfl_alpha;
+                        u.p.cfl.pad_wh = b.mode;   // cfl_ac's w_pad | h_pad << 4 (:1372-1380)
                         u.p.cfl.luma_off = (2 * uy) * (int)(dst[0].stride / bpp) + 2 * ux;
                     }
                     e.flags = (uint8_t)fl;
@@ -722,8 +745,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 // flush on the same stream: no producer, level 0 for it
                 auto cell = [&](int cx, int cy) {
                     const size_t at = (size_t)cy * w4p + cx;
-                    d = std::max(d, lv[p][at]);
-                    const int32_t o = own[p][at];
+                    d = std::max(d, lvown[p][at].lv);
+                    const int32_t o = lvown[p][at].own;
                     if (o >= 0 && (prod.size() == p0 || prod.back() != o)) prod.push_back(o);
                 };
                 if (nd & 1) {
@@ -750,26 +773,27 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     else if (ht) cell(x4, y4 - 1);
                 }
                 if (cfl) {
-                    const int lw4 = pw[0] / 4;
+                    const int lw4 = mw[0];
                     for (int cy = 2 * y4; cy < 2 * (y4 + th4); cy++)
                         for (int cx = 2 * x4; cx < 2 * (x4 + tw4); cx++) {
                             const size_t at = (size_t)cy * lw4 + cx;
-                            d = std::max(d, lv[0][at]);   // (luma of an earlier flush: no producer)
-                            const int32_t o = own[0][at];
+                            d = std::max(d, lvown[0][at].lv);   // (luma of an earlier flush: no producer)
+                            const int32_t o = lvown[0][at].own;
                             if (o >= 0 && (prod.size() == p0 || prod.back() != o)) prod.push_back(o);
                         }
                 }
-                std::sort(prod.begin() + p0, prod.end());   // duplicate-free
-                prod.erase(std::unique(prod.begin() + p0, prod.end()), prod.end());
+                if (prod.size() - p0 > 1) {   // duplicate-free
+                    std::sort(prod.begin() + p0, prod.end());
+                    prod.erase(std::unique(prod.begin() + p0, prod.end()), prod.end());
+                }
                 prod_start.push_back((int32_t)prod.size());
                 c.level = d + 1;
-                const int ci = (int)cells.size();
+                const int ci = (int)cells.size() - 1;
                 for (int cy = y4; cy < y4 + th4; cy++)
                     for (int cx = x4; cx < x4 + tw4; cx++) {
-                        lv[p][(size_t)cy * w4p + cx] = c.level;
-                        own[p][(size_t)cy * w4p + cx] = ci;
+                        lvown[p][(size_t)cy * w4p + cx] = LvOwn{c.level, ci};
                     }
-                cells.push_back(c);
+                (void)0;   // (c lives in cells already)
             }
     }
     if (n_res_used != r->residuals.size()) return -1;   // a residual outside every block

@@ -184,6 +184,12 @@ class IntraConfig:
     inter_frac: float = 0.0
     mv_range: int = 32
     ref_pad: int = 64
+    # blocks at the right / bottom edge may overhang the picture as AV1's
+    # partition allows (a square block is a leaf when its centre is inside):
+    # the decoder cuts only the part inside into transform blocks, which may
+    # themselves run past the edge (recon_tmpl.c:1208); planes get dst_pad
+    # pixels of padding for them
+    overhang: bool = False
     # recorder kinds with block data (dav1d_gpu_rec_block_aux): this fraction
     # of inter blocks becomes INTER_MASK / WARP / INTER_OBMC / INTER_WMASK /
     # INTER_SCALED, and half as many intra blocks become palette blocks
@@ -435,6 +441,30 @@ class _ExtBuilder:
         raise ValueError(kind)
 
 
+def _partition_overhang(rng, W, H):
+    """Quadtree leaves (x, y, size) over W x H where a block may run past the
+    right / bottom edge: AV1 allows PARTITION_NONE while the block's centre
+    row / column is inside (has_rows / has_cols), else the block splits."""
+    from .workload import _LEVELS
+    ys, xs = np.meshgrid(np.arange(0, H, 64), np.arange(0, W, 64), indexing="ij")
+    xs, ys = xs.ravel(), ys.ravel()
+    out = []
+    for s, p in _LEVELS:
+        ok = (xs + s // 2 < W) & (ys + s // 2 < H)
+        outside = (xs >= W) | (ys >= H)
+        leaf = ok & ((rng.random(len(xs)) < p) | (s == 8))
+        out.append((xs[leaf], ys[leaf], np.full(leaf.sum(), s)))
+        split = ~outside & ~leaf
+        if s == 8:
+            break
+        h = s // 2
+        sx, sy = xs[split], ys[split]
+        xs = np.concatenate([sx, sx + h, sx, sx + h])
+        ys = np.concatenate([sy, sy, sy + h, sy + h])
+    return (np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out]),
+            np.concatenate([o[2] for o in out]))
+
+
 def _morton(x, y):
     r = 0
     for b in range(4):
@@ -461,7 +491,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     planes = [(W, H), (W // 2, H // 2), (W // 2, H // 2)]
     sbl = (cfg.sb_log2, cfg.sb_log2 - 1, cfg.sb_log2 - 1)
     sb = 1 << cfg.sb_log2
-    lx, ly, ls = _partition(rng, W, H)
+    lx, ly, ls = _partition_overhang(rng, W, H) if cfg.overhang else _partition(rng, W, H)
     # uniform tiles of tsw x tsh superblocks, decoded in raster order
     tsw = -(-(-(-W // sb)) // cfg.tile_cols) * sb
     tsh = -(-(-(-H // sb)) // cfg.tile_rows) * sb
@@ -517,7 +547,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     smooth = lambda m: 9 <= m <= 11   # noqa: E731
 
     U = {k: [] for k in ("plane", "x", "y", "tw", "th", "blk", "cfl", "mode", "angle", "flags", "pred", "aux",
-                         "bsz", "weight", "nores")}
+                         "bsz", "weight", "nores", "cflpad")}
     BL = []   # per block and plane, decode order: what recon_b_* hands the recorder
     BLX = []  # per BL entry: its dav1d_gpu_rec_block_aux data (bytes), None, or False (plain block)
     for b in range(nb):
@@ -552,30 +582,39 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
                 bfl |= abi.IE_SMOOTH
             mvs = [(int(bmv[b, k, 0]) >> ss, int(bmv[b, k, 1]) >> ss) for k in range(2)]
             weight = XB.weight(b, kind_)
+            cfl_pad = 0
+            if cfl:   # cfl_ac's w_pad / h_pad (recon_tmpl.c:1372-1380), luma transform units
+                w4l, h4l = min(s, W - x) // 4, min(s, H - y) // 4
+                tw4l, th4l = luma_tx[0] // 4, luma_tx[1] // 4
+                fr_r = ((((w4l + 1) >> 1) << 1) + tw4l - 1) & ~(tw4l - 1)
+                fr_b = ((((h4l + 1) >> 1) << 1) + th4l - 1) & ~(th4l - 1)
+                cfl_pad = max(0, ps_ // 4 - (fr_r >> 1)) | max(0, ps_ // 4 - (fr_b >> 1)) << 4
             BL.append((pl, px_, py_, ps_, ps_, abi.TX_INDEX[(tw, th)], kind_, x0 >> ss, y0 >> ss, x1 >> ss,
                        y1 >> ss, mvs[0][0], mvs[1][0], mvs[0][1], mvs[1][1], 0, 1, int(bfilt[b]), weight,
-                       0 if cfl else int(ymode[b] if pl == 0 else uvmode[b]),
+                       cfl_pad if cfl else int(ymode[b] if pl == 0 else uvmode[b]),
                        0 if cfl else int(yang[b] if pl == 0 else uvang[b]),
                        int(alpha[b, pl - 1]) if cfl else 0, 0 if cfl or is_inter[b] else bfl))
             BLX.append(XB.block_data(b, pl, kind_, px_, py_, ps_, mvs, lx, ly, ls))
             if kind_ in XB.PRE:   # prediction units ahead of the wavefront, <= 32 x 32
                 us = min(ps_, 32)
-                for oy in range(0, ps_, us):
-                    for ox in range(0, ps_, us):
+                for oy in range(0, min(ps_, planes[pl][1] - py_), us):
+                    for ox in range(0, min(ps_, planes[pl][0] - px_), us):
                         rec_ = XB.unit_record(b, pl, kind_, ox, oy, us, us, px_ + ox, py_ + oy)
                         for k_, v_ in (("plane", pl), ("x", px_ + ox), ("y", py_ + oy), ("tw", us), ("th", us),
                                        ("blk", b), ("cfl", False), ("mode", 0), ("angle", 0), ("flags", 0),
                                        ("pred", kind_), ("aux", rec_), ("bsz", ps_), ("weight", weight),
-                                       ("nores", True)):
+                                       ("nores", True), ("cflpad", 0)):
                             U[k_].append(v_)
-            for oy in range(0, ps_, th):
-                for ox in range(0, ps_, tw):
+            # the part of the block inside the grid (w4 / h4, recon_tmpl.c:1208)
+            bwc, bhc = min(ps_, planes[pl][0] - px_), min(ps_, planes[pl][1] - py_)
+            for oy in range(0, bhc, th):
+                for ox in range(0, bwc, tw):
                     x4, y4 = ox // 4, oy // 4
                     fl = 0
                     if not cfl:
-                        if (y4 == 0 and tr) or x4 + tw // 4 < bw4:
+                        if (y4 == 0 and tr) or x4 + tw // 4 < bwc // 4:
                             fl |= abi.IE_TOP_HAS_RIGHT
-                        if x4 == 0 and (bl or y4 + th // 4 < bw4):
+                        if x4 == 0 and (bl or y4 + th // 4 < bhc // 4):
                             fl |= abi.IE_LEFT_HAS_BOTTOM
                         if cfg.filter_edge:
                             fl |= abi.IE_FILTER_EDGE
@@ -596,6 +635,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
                                     if kind_ in (abi.PRED_INTER_MASK, abi.PRED_PAL) else -1)
                     U["bsz"].append(ps_)
                     U["weight"].append(weight)
+                    U["cflpad"].append(cfl_pad)
                     # residual-only units of launch-ahead blocks: some carry none
                     U["nores"].append(kind_ in XB.PRE and XB.rng.random() < 0.3)
     plane_u = np.array(U["plane"], np.int32)
@@ -618,7 +658,8 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
         flags |= np.where((uy > ty0) & (uy % sbh == 0), abi.IE_TOP_SB_EDGE, 0)
 
     units = np.zeros(n, abi.UNIT_DTYPE)   # decode order for now
-    units["dst_off"] = uy * pw[plane_u] + ux
+    dpad = 64 if cfg.overhang else 0   # plane padding right / below for overhanging transform blocks
+    units["dst_off"] = uy * (pw[plane_u] + dpad) + ux
     units["tx"] = tx
     units["plane"] = plane_u
     predu = np.array(U["pred"], np.int32)
@@ -654,8 +695,8 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
         units[interu] = iv
     cu = units[cflu]
     cu["cfl_alpha"] = alpha[blk[cflu], plane_u[cflu] - 1]
-    cu["cfl_pad_wh"] = 0
-    cu["cfl_luma_off"] = (2 * uy[cflu]) * W + 2 * ux[cflu]
+    cu["cfl_pad_wh"] = np.array(U["cflpad"], np.int32)[cflu]
+    cu["cfl_luma_off"] = (2 * uy[cflu]) * (W + dpad) + 2 * ux[cflu]
     units[cflu] = cu
 
     # dependency levels, at 4x4 granularity per plane
@@ -780,6 +821,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
                     refs, dep_start, deps)
     fr.blocks = BL
     fr.block_aux = BLX
+    fr.dst_pad = dpad
     fr.dec_units = dec_units
     fr.aux = aux if XB.used else None
     fr.aux_pool = XB.pool() if XB.used else None
@@ -791,8 +833,9 @@ def frame_batch(fr, dst_ptrs, units, coefs, edges, ref_ptrs=None, aux=None, aux_
     ref_ptrs[r][p]: addresses of the padded reference planes, mixed frames)."""
     bpp = 1 if fr.cfg.bpc == 8 else 2
     b = abi.FrameBatch()
+    pad = getattr(fr, "dst_pad", 0)
     for p, (w, h) in enumerate(fr.plane_wh):
-        b.dst[p].data, b.dst[p].stride, b.dst[p].w, b.dst[p].h = dst_ptrs[p], w * bpp, w, h
+        b.dst[p].data, b.dst[p].stride, b.dst[p].w, b.dst[p].h = dst_ptrs[p], (w + pad) * bpp, w, h
         for r in range(len(ref_ptrs or [])):
             a = fr.refs[r][p]
             b.ref[r][p].data = ref_ptrs[r][p] + fr.ref_origin_offset(p) * bpp
@@ -803,7 +846,7 @@ def frame_batch(fr, dst_ptrs, units, coefs, edges, ref_ptrs=None, aux=None, aux_
     b.coef, b.edges = coefs, edges
     b.bitdepth_max = fr.cfg.bitdepth_max if fr.cfg.bpc == 16 else 255
     W, H = fr.plane_wh[0]
-    b.cfl_luma.data, b.cfl_luma.stride, b.cfl_luma.w, b.cfl_luma.h = dst_ptrs[0], W * bpp, W, H
+    b.cfl_luma.data, b.cfl_luma.stride, b.cfl_luma.w, b.cfl_luma.h = dst_ptrs[0], (W + pad) * bpp, W, H
     b.cfl_ss = 3
     if aux is not None:   # per-unit aux offsets (unit order) and the aux pool
         b.aux, b.aux_pool = aux, aux_pool
@@ -813,8 +856,9 @@ def frame_batch(fr, dst_ptrs, units, coefs, edges, ref_ptrs=None, aux=None, aux_
 def edge_batch(fr, dst_ptrs, top_ptrs, units, edges, recs):
     bpp = 1 if fr.cfg.bpc == 8 else 2
     b = abi.IntraEdgeBatch()
+    pad = getattr(fr, "dst_pad", 0)
     for p, (w, h) in enumerate(fr.plane_wh):
-        b.pic[p].data, b.pic[p].stride, b.pic[p].w, b.pic[p].h = dst_ptrs[p], w * bpp, w, h
+        b.pic[p].data, b.pic[p].stride, b.pic[p].w, b.pic[p].h = dst_ptrs[p], (w + pad) * bpp, w, h
         rows, tw_ = fr.top_rows[p]
         # no top_edge when the frame does not back up superblock rows (the
         # fused launch stores superblock-bottom rows whenever it has one)
@@ -855,7 +899,8 @@ class DeviceIntraFrame:
         self.edges = up(fr.edges.view(np.int16) if hbd else fr.edges)
         self.recs = up(fr.recs.view(np.uint8))
         self.runs = up(fr.runs.view(np.uint8)) if len(fr.runs) else torch.zeros(16, dtype=torch.uint8, device=dev)
-        self.dst = [torch.zeros((h, w), dtype=pdt, device=dev) for (w, h) in fr.plane_wh]
+        pad = getattr(fr, "dst_pad", 0)
+        self.dst = [torch.zeros((h + pad, w + pad), dtype=pdt, device=dev) for (w, h) in fr.plane_wh]
         self.top = [torch.full(s, top_fill, dtype=pdt, device=dev) for s in fr.top_rows]
         self.refs = [[up(a.view(np.int16) if hbd else a) for a in rp] for rp in (fr.refs or [])]
         d = [t.data_ptr() for t in self.dst]
@@ -907,8 +952,9 @@ class DeviceIntraFrame:
 
     def planes_host(self):
         out = []
-        for t in self.dst:
-            a = t.cpu().numpy()
+        for p, t in enumerate(self.dst):
+            w, h = self.fr.plane_wh[p]
+            a = t[:h, :w].cpu().numpy()
             out.append(a if self.fr.cfg.bpc == 8 else a.view(np.uint16))
         return out
 
@@ -1011,7 +1057,7 @@ def replay(rec, fr, rows=None):
     u = fr.dec_units
     for i in np.nonzero(u["txtp"] != abi.NO_RESIDUAL)[0]:
         p = int(u["plane"][i])
-        w = fr.plane_wh[p][0]
+        w = fr.plane_wh[p][0] + getattr(fr, "dst_pad", 0)   # dst_off's row pitch
         y, x = divmod(int(u["dst_off"][i]), w)
         if not inside(p, y):
             continue

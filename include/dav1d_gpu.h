@@ -724,7 +724,8 @@ typedef struct Dav1dGpuRecBlock {
     uint8_t ref[2], filter2d, weight;
     /* intra: the coded mode (DC..PAETH = 0..12, FILTER 13) and angle delta
        (FILTER: the filter index); CFL: alpha (its DC source is prepared
-       from DC_PRED, :1395-1410)                                              */
+       from DC_PRED, :1395-1410), and in `mode` cfl_ac's w_pad | h_pad << 4
+       (4-px units, :1372-1380; non-zero when the block overhangs the grid) */
     uint8_t mode;
     int8_t  angle;
     int8_t  cfl_alpha;
@@ -733,6 +734,15 @@ typedef struct Dav1dGpuRecBlock {
                                 DGPU_IE_SMOOTH                                 */
 } Dav1dGpuRecBlock;
 
+/* width / height: the picture's (f->cur.p.w / .h).  Blocks are recorded at
+ * their full size (bw4 * 4 x bh4 * 4) and must start inside the decoder's
+ * block grid, the picture rounded up to 8 (4 * f->bw x 4 * f->bh); like
+ * recon_b_* the recorder cuts only the part inside the grid into transform
+ * units (w4 / h4, src/recon_tmpl.c:1208), whose transform blocks may run past
+ * it.  dst planes must therefore be writable over the grid plus 64 px (any
+ * picture from dav1d's allocator, 128-aligned, is).  Intra max_w / max_h and
+ * the top-right / bottom-left availability follow the clipped block, as in
+ * recon_b_intra (:1252-1266, :1296-1298). */
 Dav1dGpuRecorder *dav1d_gpu_recorder_new(int bpc, int bitdepth_max, int width, int height, int device);
 void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r);
 /* Record one block / one coded transform block.  coef: the reference's

@@ -291,7 +291,9 @@ class HostIntraFrame:
         abi = _abi()
         self.fr = fr
         pdt = fr.cfg.pixel_dtype
-        self.dst = [np.zeros((h, w), pdt) for (w, h) in fr.plane_wh]
+        pad = getattr(fr, "dst_pad", 0)   # room for transform blocks overhanging the picture
+        self._dst = [np.zeros((h + pad, w + pad), pdt) for (w, h) in fr.plane_wh]
+        self.dst = [a[:h, :w] for a, (w, h) in zip(self._dst, fr.plane_wh)]
         self.top = [np.full(s, top_fill, pdt) for s in fr.top_rows]
         self.units = fr.units.copy()
         self.coefs = fr.coefs.copy()
@@ -300,7 +302,7 @@ class HostIntraFrame:
         self.steps = np.ascontiguousarray(fr.steps, dtype=np.int32)
         self.unit_rec = np.ascontiguousarray(fr.unit_rec, dtype=np.int32)
         self.oruns = np.ascontiguousarray(fr.oracle_runs) if len(fr.oracle_runs) else np.zeros(1, abi.EDGE_BACKUP_DTYPE)
-        d = [a.ctypes.data for a in self.dst]
+        d = [a.ctypes.data for a in self._dst]
         # recorder kinds with block data: per-unit aux offsets and a writable
         # pool (INTER_WMASK units write the seg mask their chroma units read)
         self.aux = None if getattr(fr, "aux", None) is None else np.ascontiguousarray(fr.aux, dtype=np.int32)

@@ -49,14 +49,18 @@ def test_recorder_validation(pkg):
     L = pkg.abi.load_lib()
     abi = pkg.abi
     assert not L.dav1d_gpu_recorder_new(10, 1023, 64, 64, 0)          # bpc 8 or 16
-    assert not L.dav1d_gpu_recorder_new(8, 255, 60, 64, 0)            # 8-px aligned sizes
+    assert not L.dav1d_gpu_recorder_new(8, 255, 0, 64, 0)             # empty picture
+    r60 = L.dav1d_gpu_recorder_new(8, 255, 60, 64, 0)                 # any size: the grid is rounded to 8
+    assert r60
+    L.dav1d_gpu_recorder_free(r60)
     r = L.dav1d_gpu_recorder_new(8, 255, 64, 64, 0)
     assert r
     try:
         rec = lambda **kw: L.dav1d_gpu_rec_block(r, ctypes.byref(_blk(pkg, **kw)))   # noqa: E731
         assert rec() == 0
         assert rec(plane=3) == -1
-        assert rec(x=56) == -1                                        # leaves the plane
+        assert rec(x=56) == 0                                         # overhangs the grid (AV1 allows it)
+        assert rec(x=64) == -1                                        # starts outside the grid
         assert rec(w=12) == -1                                        # not a multiple of the transform
         assert rec(kind=abi.PRED_PAL) == -1                           # not a recordable kind
         assert rec(mode=14) == -1
@@ -68,7 +72,8 @@ def test_recorder_validation(pkg):
         cf = np.zeros(64, np.int16)
         res = lambda *a: L.dav1d_gpu_rec_residual(r, *a, cf.ctypes.data)   # noqa: E731
         assert res(0, 16, 16, abi.TX_INDEX[(8, 8)], 0, 0) == 0
-        assert res(0, 60, 16, abi.TX_INDEX[(8, 8)], 0, 0) == -1          # leaves the plane
+        assert res(0, 60, 16, abi.TX_INDEX[(8, 8)], 0, 0) == 0           # overhangs (starts inside)
+        assert res(0, 64, 16, abi.TX_INDEX[(8, 8)], 0, 0) == -1          # starts outside the grid
         assert res(0, 16, 16, abi.TX_INDEX[(8, 8)], 17, 0) == -1         # no such type
         assert L.dav1d_gpu_rec_residual(r, 0, 16, 16, 1, 0, 0, None) == -1
         n, lv = ctypes.c_int32(), ctypes.c_int32()

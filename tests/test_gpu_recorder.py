@@ -59,7 +59,8 @@ def _setup(fr):
     import torch
     hbd = fr.cfg.bpc != 8
     pdt = torch.int16 if hbd else torch.uint8
-    dst = [torch.zeros((h, w), dtype=pdt, device="cuda:0") for (w, h) in fr.plane_wh]
+    pad = getattr(fr, "dst_pad", 0)   # room for transform blocks overhanging the picture
+    dst = [torch.zeros((h + pad, w + pad), dtype=pdt, device="cuda:0") for (w, h) in fr.plane_wh]
     refs = []
     for rp in fr.refs or []:
         planes = []
@@ -75,7 +76,8 @@ def _compare(fr, dst, oracle):
     ho.run()
     hbd = fr.cfg.bpc != 8
     for p in range(3):
-        got = dst[p].cpu().numpy()
+        w, h = fr.plane_wh[p]
+        got = dst[p][:h, :w].cpu().numpy()
         got = got.view(np.uint16) if hbd else got
         diff = np.argwhere(got != ho.dst[p])
         assert len(diff) == 0, f"plane {p}: {len(diff)} pixels differ, first {diff[:5].tolist()}"
@@ -228,5 +230,29 @@ def test_recorder_block_data_per_superblock_row(oracle):
         rec.flush(dst, refs, s)
     assert rec.status() == 0
     torch.cuda.synchronize()
+    _compare(fr, dst, oracle)
+    rec.close()
+
+
+@pytest.mark.parametrize("kw", [dict(width=1920, height=1080, seed=95, inter_frac=0.4),
+                                dict(width=992, height=552, seed=96, inter_frac=0.3, bpc=16, bitdepth_max=1023),
+                                dict(width=992, height=552, seed=97, inter_frac=0.6, ext_frac=0.6, tile_cols=2)])
+def test_recorder_overhanging_blocks(oracle, kw):
+    """Blocks that run past the right / bottom edge, as AV1's partition allows
+    (ADVICE r2): 1080 rows (not a multiple of 64) and a 992 x 552 picture.
+    The recorder cuts only the part inside the 8-aligned grid into transform
+    blocks (recon_tmpl.c:1208 w4 / h4), which may overhang into the plane's
+    padding; TOP_HAS_RIGHT / LEFT_HAS_BOTTOM follow the clipped block, intra
+    max_w / max_h the grid, CfL's cfl_ac pads the luma past the edge."""
+    import torch
+    import dav1d_mirror_amd.intra as intra
+    fr = intra.make_intra_frame(intra.IntraConfig(overhang=True, sb_edge_backup=False, **kw))
+    assert any(y + s_ > fr.cfg.height or x + s_ > fr.cfg.width for (p, x, y, s_, *_r) in fr.blocks if p == 0)
+    dst, refs = _setup(fr)
+    rec = intra.Recorder(fr.cfg.bpc, fr.cfg.bitdepth_max, fr.cfg.width, fr.cfg.height)
+    intra.replay(rec, fr)
+    rec.flush(dst, refs, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert rec.status() == 0
     _compare(fr, dst, oracle)
     rec.close()
