@@ -1151,7 +1151,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     const int ib = Px<BPC>::ibits(bdmax);
     const int pred = u.pred;
     const bool comp = pred == DGPU_PRED_INTER_AVG || pred == DGPU_PRED_INTER_WAVG || pred == DGPU_PRED_INTER_MASK;
-    const bool ii = WARPK && pred == DGPU_PRED_INTER_INTRA;   // second launch only
+    // inter-intra: the second launch (staged edges) and the wavefront (GATHER:
+    // its edges from the picture, for the recorder); never the main kernel
+    const bool ii = (WARPK || GATHER) && pred == DGPU_PRED_INTER_INTRA;
     const bool inter = pred == DGPU_PRED_INTER || comp || ii;
     const int txtp = u.txtp;
     const bool nores = txtp == DGPU_NO_RESIDUAL;
@@ -1418,7 +1420,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
     };
 
-    if (NW && inter) {
+    if (NW && inter && !ii) {
         if (DGPU_ABL_MC) {
             int pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -1540,15 +1542,38 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
         wave_sync();   // the intermediate tile is free: the edges go there
         // 2. the intra record, its edge array and the edge preparation
+        const Dav1dGpuIntraEdge &rec_in = rec;   // (GATHER: the unit's edge record)
         const u32x4 rec = gld<u32x4>(a.aux_pool + auxo);
         Dav1dGpuUnit ui = u;
         ui.p.intra.edge_off = (int32_t)rec[0];
         ui.p.intra.mode = (uint8_t)(rec[1] & 0xff);
         ui.p.intra.angle = (uint16_t)(rec[1] >> 16);
         ui.p.intra.max_w = ui.p.intra.max_h = 0;
-        Stage<SL::EDGE * (int)sizeof(P), G> est2;
-        est2.load(a.edges + (int)rec[0] - 2 * H, SL::EDGE * (int)sizeof(P), l);
-        const P *tl2 = reinterpret_cast<const P *>(src + est2.commit(src, l)) + 2 * H;
+        const P *tl2;
+        if constexpr (GATHER) {   // dav1d_prepare_intra_edges from the picture, as for INTRA units
+            const PlaneTabIE<BPC> &pti = static_cast<const PlaneTabIE<BPC> &>(pt);
+            IeCtx<P> ie = ie_setup<P>(rec_in, pt.dst[plane], ds, pti.top[plane], pti.top_stride[plane],
+                                      pti.sb_log2[plane], W / 4, H / 4, bdmax);
+            constexpr int NE = 2 * W + 2 * H + 1, EPL = (NE + G - 1) / G;
+            P *tw_ = reinterpret_cast<P *>(src) + 2 * H;
+            int ev[EPL];
+#pragma unroll
+            for (int k = 0; k < EPL; k++) {
+                const int i = -2 * H + l + k * G;
+                bool need;
+                ev[k] = (i <= 2 * W && ie_need(ie, i)) ? ie_value(ie, i, need) : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < EPL; k++)
+                if (ev[k] >= 0) tw_[-2 * H + l + k * G] = (P)ev[k];
+            ui.p.intra.mode = (uint8_t)ie.mode;
+            ui.p.intra.angle = ie_angle_field(rec_in, ie.angle);
+            tl2 = tw_;
+        } else {
+            Stage<SL::EDGE * (int)sizeof(P), G> est2;
+            est2.load(a.edges + (int)rec[0] - 2 * H, SL::EDGE * (int)sizeof(P), l);
+            tl2 = reinterpret_cast<const P *>(src + est2.commit(src, l)) + 2 * H;
+        }
         wave_sync();
         const IntraState is = intra_prep<BPC, TX>(ui, tl2, fe, l, bdmax);
         wave_sync();

@@ -173,7 +173,7 @@ struct Unit {   // a transform cell before sorting
 // are predicted by the launch ahead of the wavefront
 inline bool is_ext_kind(int k) {
     return k == DGPU_PRED_INTER_MASK || k == DGPU_PRED_PAL || k == DGPU_PRED_WARP || k == DGPU_PRED_INTER_WMASK ||
-           k == DGPU_PRED_INTER_OBMC || k == DGPU_PRED_INTER_SCALED;
+           k == DGPU_PRED_INTER_OBMC || k == DGPU_PRED_INTER_SCALED || k == DGPU_PRED_INTER_INTRA;
 }
 inline bool is_prelaunch_kind(int k) {
     return k == DGPU_PRED_WARP || k == DGPU_PRED_INTER_WMASK || k == DGPU_PRED_INTER_OBMC ||
@@ -333,6 +333,12 @@ extern "C" int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlo
         need = w * h;
         break;
     case DGPU_PRED_PAL: need = 8 * bpp + (w / 2) * h; break;
+    case DGPU_PRED_INTER_INTRA:   // the block's ii / wedge mask; the intra mode DC / V / H / SMOOTH in `mode`
+        if (w > 32 || h > 32 || tx_of(b->w, b->h) < 0 ||
+            (b->mode != DGPU_DC_PRED && b->mode != DGPU_VERT_PRED && b->mode != DGPU_HOR_PRED && b->mode != DGPU_SMOOTH_PRED))
+            return -1;
+        need = w * h;
+        break;
     case DGPU_PRED_WARP:
         if ((w & 7) || (h & 7) || (b->x & 7) || (b->y & 7)) return -1;
         need = 16 + (w / 8) * (h / 8) * 8;
@@ -629,19 +635,28 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     xaux.push_back(ao);
                 }
         }
-        for (int oy = 0; oy < bhc; oy += t.h)
-            for (int ox = 0; ox < bwc; ox += t.w) {
+        // the transform cells; an INTER_INTRA block first gets one cell for
+        // the whole block's prediction (recon_b_inter predicts the block,
+        // :1540-1580, then adds the residuals), its transform cells become
+        // residual-only cells that read it
+        const bool iib = b.kind == DGPU_PRED_INTER_INTRA;
+        const int ncx = (bwc + t.w - 1) / t.w, ncy = (bhc + t.h - 1) / t.h;
+        for (int k = iib ? -1 : 0; k < ncx * ncy; k++)
+            {
+                const bool iic = k < 0;
+                const int ox = iic ? 0 : (k % ncx) * t.w, oy = iic ? 0 : (k / ncx) * t.h;
+                const int ctw = iic ? b.w : t.w, cth = iic ? b.h : t.h, ctw4 = ctw / 4, cth4 = cth / 4;
                 cells.emplace_back();   // built in place (popped again when skipped)
                 Unit &c = cells.back();
                 memset(&c, 0, sizeof(c));
                 const int ux = b.x + ox, uy = b.y + oy, x4 = ux / 4, y4 = uy / 4;
                 Dav1dGpuUnit &u = c.u;
                 u.dst_off = uy * ds_px + ux;
-                u.tx = (uint8_t)b.tx;
+                u.tx = (uint8_t)(iic ? tx_of(b.w, b.h) : b.tx);
                 u.plane = (uint8_t)p;
-                u.pred = (uint8_t)(pre ? DGPU_PRED_NONE : b.kind);
+                u.pred = (uint8_t)((pre || (iib && !iic)) ? DGPU_PRED_NONE : b.kind);
                 u.txtp = DGPU_NO_RESIDUAL;
-                const int ri = res_at[p][(size_t)y4 * w4p + x4];
+                const int ri = iic ? -1 : res_at[p][(size_t)y4 * w4p + x4];
                 if (ri >= 0 && r->residuals[ri].tx == b.tx) {
                     const Residual &q = r->residuals[ri];
                     u.txtp = (uint8_t)q.txtp;
@@ -651,9 +666,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     n_res_used++;
                 } else if (ri >= 0) {
                     return -1;   // a residual whose size differs from its block's transforms
-                } else if (pre) {
+                } else if (pre || (iib && !iic)) {
                     cells.pop_back();
-                    continue;   // predicted ahead of the wavefront, nothing to add
+                    continue;   // predicted elsewhere, nothing to add
                 }
                 Dav1dGpuIntraEdge &e = c.rec;
                 e.unit = -1;
@@ -663,7 +678,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 e.h4 = (int16_t)(b.tile_y1 / 4);
                 int nd = 0;
                 bool hl = ux > b.tile_x0, ht = uy > b.tile_y0;
-                if (pre) {   // PRED_NONE: the residual onto the launch-ahead prediction
+                if (pre || (iib && !iic)) {   // PRED_NONE: the residual onto the prediction
                     c.sortmode = 0;
                 } else if (pal) {   // pal_pred: palette, then the unit's rows of the index map
                     const int bw2 = b.w / 2;
@@ -674,35 +689,35 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         memcpy(&auxp[c.aux + 16 + yy * (t.w / 2)], bdata + 8 * bpp + (size_t)(oy + yy) * bw2 + ox / 2,
                                t.w / 2);
                     c.sortmode = 15;
-                } else if (inter) {
+                } else if (inter || iic) {
                     u.bw4 = (uint8_t)bw4;
                     u.bh4 = (uint8_t)bh4;
                     for (int k = 0; k < 2; k++) {
                         const int rr = b.ref[k];
                         // every reference an inter block reads must be given
-                        if (k == 0 || b.kind != DGPU_PRED_INTER)
-                            if (!ref || !ref[rr][p].data) return -1;
+                        const bool used = k == 0 || (b.kind != DGPU_PRED_INTER && !iic);
+                        if (used && (!ref || !ref[rr][p].data)) return -1;
                         const int rs = ref ? (int)(ref[rr][p].stride / bpp) : 0;
                         const int ix = ux + (b.mvx[k] >> 4), iy = uy + (b.mvy[k] >> 4);
                         u.p.inter.src_off[k] = iy * rs + ix;
                         u.p.inter.mx[k] = (uint8_t)(b.mvx[k] & 15);
                         u.p.inter.my[k] = (uint8_t)(b.mvy[k] & 15);
                         u.p.inter.ref[k] = (uint8_t)rr;
-                        if (k == 0 || b.kind != DGPU_PRED_INTER) {
+                        if (used) {
                             // the unit kernel reads the footprint with both
                             // 8-tap margins whatever the fraction, and its
                             // aligned row loads may run up to 16 bytes past
                             // the last pixel: direct only when all of that
                             // stays inside the picture, else a clamped copy
                             const int rw = ref[rr][p].w, rh = ref[rr][p].h;
-                            const bool inside = ix - 3 >= 0 && iy - 3 >= 0 && ix + t.w + 4 <= rw &&
-                                                iy + t.h + 4 <= rh && (iy + t.h + 4 < rh || (ix + t.w + 4) * bpp + 16 <= rs * bpp);
+                            const bool inside = ix - 3 >= 0 && iy - 3 >= 0 && ix + ctw + 4 <= rw &&
+                                                iy + cth + 4 <= rh && (iy + cth + 4 < rh || (ix + ctw + 4) * bpp + 16 <= rs * bpp);
                             if (!inside) {
-                                r->emu.push_back(EmuJob{ix - 3, iy - 3, emu_rows, (uint8_t)(t.w + 7), (uint8_t)(t.h + 7),
+                                r->emu.push_back(EmuJob{ix - 3, iy - 3, emu_rows, (uint8_t)(ctw + 7), (uint8_t)(cth + 7),
                                                         (uint8_t)rr, (uint8_t)p});
                                 u.p.inter.src_off[k] = (emu_rows + 3) * kEmuStride + 3;
                                 u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
-                                emu_rows += t.h + 7;
+                                emu_rows += cth + 7;
                             }
                         }
                     }
@@ -710,6 +725,23 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     u.p.inter.weight = b.kind == DGPU_PRED_INTER_WAVG ? b.weight : 0;
                     if (b.kind == DGPU_PRED_INTER_MASK) c.aux = mask_base + oy * mask_stride + ox;
                     c.sortmode = b.filter2d;
+                    if (iic) {   // the intra half: edges gathered by the wavefront like an INTRA unit's
+                        // record: edge_off (unused when gathered), mode, angle, then the mask offset
+                        c.aux = aux_alloc(16 + (size_t)b.w * b.h);
+                        const int32_t moff = c.aux + 16, zero = 0;
+                        memset(&auxp[c.aux], 0, 16);
+                        memcpy(&auxp[c.aux], &zero, 4);
+                        auxp[c.aux + 4] = b.mode;
+                        memcpy(&auxp[c.aux + 8], &moff, 4);
+                        memcpy(&auxp[moff], bdata, (size_t)b.w * b.h);
+                        // prepare_intra_edges with no edge flags, no edge filter, angle 0 (:1551-1566)
+                        e.mode = b.mode;
+                        e.angle = 0;
+                        e.flags = (uint8_t)((hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0));
+                        const int m = remap_mode(e.mode, 0, hl, ht);
+                        nd = kNeeds[m];
+                        c.sortmode = 16 + m;
+                    }
                 } else {
                     int fl = (hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0);
                     if (!cfl) {   // recon_tmpl.c:1252-1266 (blocks up to 64 wide: one 64x64 step)
@@ -751,22 +783,25 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 };
                 if (nd & 1) {
                     if (hl) {
-                        for (int k = y4; k < std::min(y4 + th4, H4); k++) cell(x4 - 1, k);
-                        if ((nd & 16) && y4 + th4 < H4 && (e.flags & DGPU_IE_LEFT_HAS_BOTTOM))
-                            for (int k = y4 + th4; k < std::min(y4 + 2 * th4, H4); k++) cell(x4 - 1, k);
+                        for (int q = y4; q < std::min(y4 + cth4, H4); q++) cell(x4 - 1, q);
+                        if ((nd & 16) && y4 + cth4 < H4 && (e.flags & DGPU_IE_LEFT_HAS_BOTTOM))
+                            for (int q = y4 + cth4; q < std::min(y4 + 2 * cth4, H4); q++) cell(x4 - 1, q);
                     } else if (ht) {
                         cell(x4, y4 - 1);
                     }
                 }
                 if (nd & 2) {
                     if (ht) {
-                        for (int k = x4; k < std::min(x4 + tw4, W4); k++) cell(k, y4 - 1);
-                        if ((nd & 8) && x4 + tw4 < W4 && (e.flags & DGPU_IE_TOP_HAS_RIGHT))
-                            for (int k = x4 + tw4; k < std::min(x4 + 2 * tw4, W4); k++) cell(k, y4 - 1);
+                        for (int q = x4; q < std::min(x4 + ctw4, W4); q++) cell(q, y4 - 1);
+                        if ((nd & 8) && x4 + ctw4 < W4 && (e.flags & DGPU_IE_TOP_HAS_RIGHT))
+                            for (int q = x4 + ctw4; q < std::min(x4 + 2 * ctw4, W4); q++) cell(q, y4 - 1);
                     } else if (hl) {
                         cell(x4 - 1, y4);
                     }
                 }
+                if (iib && !iic)   // the residual reads the block's inter-intra prediction
+                    for (int cy = y4; cy < y4 + cth4; cy++)
+                        for (int cx = x4; cx < x4 + ctw4; cx++) cell(cx, cy);
                 if (nd & 4) {
                     if (hl && ht) cell(x4 - 1, y4 - 1);
                     else if (hl) cell(x4 - 1, y4);
@@ -789,8 +824,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 prod_start.push_back((int32_t)prod.size());
                 c.level = d + 1;
                 const int ci = (int)cells.size() - 1;
-                for (int cy = y4; cy < y4 + th4; cy++)
-                    for (int cx = x4; cx < x4 + tw4; cx++) {
+                for (int cy = y4; cy < y4 + cth4; cy++)
+                    for (int cx = x4; cx < x4 + ctw4; cx++) {
                         lvown[p][(size_t)cy * w4p + cx] = LvOwn{c.level, ci};
                     }
                 (void)0;   // (c lives in cells already)

@@ -244,6 +244,10 @@ class _ExtBuilder:
     include/dav1d_gpu.h Dav1dGpuPredKind), INTER_MASK / PAL per transform
     unit.  OBMC and scaled geometry as in workload._ext2_records."""
     PRE = (abi.PRED_WARP, abi.PRED_INTER_WMASK, abi.PRED_INTER_OBMC, abi.PRED_INTER_SCALED)
+    # kinds whose prediction is one or more units of their own, the
+    # residuals then residual-only units: the launch-ahead kinds and
+    # inter-intra (one unit for the whole block, recon_tmpl.c:1540-1580)
+    CUT = PRE + (abi.PRED_INTER_INTRA,)
 
     def __init__(self, cfg, rng, bdmax, refs):
         self.cfg, self.rng, self.bdmax, self.refs = cfg, rng, bdmax, refs
@@ -265,6 +269,11 @@ class _ExtBuilder:
     def pool(self):
         return np.concatenate(self.chunks) if self.chunks else np.zeros(16, np.uint8)
 
+    def block_mode(self, b, kind, mode):
+        """Dav1dGpuRecBlock.mode: the inter-intra block's intra mode (DC / V /
+        H / SMOOTH, recon_tmpl.c:1547-1549), else the coded mode given."""
+        return self._block(b)["iimode"] if kind == abi.PRED_INTER_INTRA else mode
+
     @staticmethod
     def plane_kind(k, pl):
         if not k:
@@ -279,6 +288,7 @@ class _ExtBuilder:
         if b not in self.bb:
             r = self.rng
             self.bb[b] = dict(sign=int(r.integers(0, 2)), nref=int(r.integers(1, 3)),
+                              iimode=int((abi.DC_PRED, abi.VERT_PRED, abi.HOR_PRED, abi.SMOOTH_PRED)[r.integers(0, 4)]),
                               wt=int(0 if r.random() < 0.5 else r.integers(1, 16)),
                               steps=r.integers(256, 2049, size=(2, 2)), phase=r.integers(0, 1024, size=(2, 2)),
                               abcd=r.integers(-1024, 1025, 4).astype(np.int16), obmc=None)
@@ -320,6 +330,9 @@ class _ExtBuilder:
             if self._block(b).get("wm") is not None and pl:   # COMPOUND_SEG chroma
                 st["mask_at"], st["mask_stride"] = self._block(b)["wm"], s
                 return None
+            st["mask"] = r.integers(0, 65, (s, s)).astype(np.uint8)
+            return st["mask"].tobytes()
+        if kind == abi.PRED_INTER_INTRA:   # the block's ii / wedge mask
             st["mask"] = r.integers(0, 65, (s, s)).astype(np.uint8)
             return st["mask"].tobytes()
         if kind == abi.PRED_PAL:
@@ -401,6 +414,12 @@ class _ExtBuilder:
             if "mask_at" not in st:
                 st["mask_at"], st["mask_stride"] = self.put(st["mask"]), s
             return st["mask_at"] + oy * st["mask_stride"] + ox
+        if kind == abi.PRED_INTER_INTRA:   # record (its edge slot is patched in later) + mask
+            rec = np.zeros(16 + s * s, np.uint8)
+            rec[4] = self._block(b)["iimode"]
+            rec[8:12] = np.array([self.off + 16], "<i4").view(np.uint8)   # the mask follows the record
+            rec[16:] = st["mask"].ravel()
+            return self.put(rec)
         if kind == abi.PRED_PAL:
             rec = np.zeros(16 + (uw // 2) * uh, np.uint8)
             rec[:8 * bpp] = st["pal"].view(np.uint8)
@@ -531,8 +550,10 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     xr = np.random.default_rng(cfg.seed ^ 0xE7E7)
     if cfg.ext_frac > 0:
         ext_kinds = np.array([abi.PRED_INTER_MASK, abi.PRED_WARP, abi.PRED_INTER_OBMC, abi.PRED_INTER_WMASK,
-                              abi.PRED_INTER_SCALED])
-        xk = np.where(is_inter & (xr.random(nb) < cfg.ext_frac), ext_kinds[xr.integers(0, 5, nb)], 0)
+                              abi.PRED_INTER_SCALED, abi.PRED_INTER_INTRA])
+        xk = np.where(is_inter & (xr.random(nb) < cfg.ext_frac), ext_kinds[xr.integers(0, 6, nb)], 0)
+        # inter-intra exists for blocks up to 32x32 (interintra_allowed_mask)
+        xk = np.where((xk == abi.PRED_INTER_INTRA) & (ls > 32), abi.PRED_INTER_MASK, xk)
         pal_b = ~is_inter & (xr.random(nb) < cfg.ext_frac * 0.5)
         xk = np.where(pal_b, abi.PRED_PAL, xk)
         ymode[pal_b] = abi.DC_PRED     # palette blocks code DC_PRED (no smooth context)
@@ -591,17 +612,18 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
                 cfl_pad = max(0, ps_ // 4 - (fr_r >> 1)) | max(0, ps_ // 4 - (fr_b >> 1)) << 4
             BL.append((pl, px_, py_, ps_, ps_, abi.TX_INDEX[(tw, th)], kind_, x0 >> ss, y0 >> ss, x1 >> ss,
                        y1 >> ss, mvs[0][0], mvs[1][0], mvs[0][1], mvs[1][1], 0, 1, int(bfilt[b]), weight,
-                       cfl_pad if cfl else int(ymode[b] if pl == 0 else uvmode[b]),
+                       cfl_pad if cfl else XB.block_mode(b, kind_, int(ymode[b] if pl == 0 else uvmode[b])),
                        0 if cfl else int(yang[b] if pl == 0 else uvang[b]),
                        int(alpha[b, pl - 1]) if cfl else 0, 0 if cfl or is_inter[b] else bfl))
             BLX.append(XB.block_data(b, pl, kind_, px_, py_, ps_, mvs, lx, ly, ls))
-            if kind_ in XB.PRE:   # prediction units ahead of the wavefront, <= 32 x 32
+            if kind_ in XB.CUT:   # prediction units of their own (<= 32 x 32), residuals apart
                 us = min(ps_, 32)
                 for oy in range(0, min(ps_, planes[pl][1] - py_), us):
                     for ox in range(0, min(ps_, planes[pl][0] - px_), us):
                         rec_ = XB.unit_record(b, pl, kind_, ox, oy, us, us, px_ + ox, py_ + oy)
                         for k_, v_ in (("plane", pl), ("x", px_ + ox), ("y", py_ + oy), ("tw", us), ("th", us),
-                                       ("blk", b), ("cfl", False), ("mode", 0), ("angle", 0), ("flags", 0),
+                                       ("blk", b), ("cfl", False), ("mode", XB.block_mode(b, kind_, 0)),
+                                       ("angle", 0), ("flags", 0),
                                        ("pred", kind_), ("aux", rec_), ("bsz", ps_), ("weight", weight),
                                        ("nores", True), ("cflpad", 0)):
                             U[k_].append(v_)
@@ -630,14 +652,14 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
                     U["mode"].append(abi.DC_PRED if cfl else int(ymode[b] if pl == 0 else uvmode[b]))
                     U["angle"].append(0 if cfl else int(yang[b] if pl == 0 else uvang[b]))
                     U["flags"].append(fl)
-                    U["pred"].append(abi.PRED_NONE if kind_ in XB.PRE else kind_)
+                    U["pred"].append(abi.PRED_NONE if kind_ in XB.CUT else kind_)
                     U["aux"].append(XB.unit_record(b, pl, kind_, ox, oy, tw, th, px_ + ox, py_ + oy)
                                     if kind_ in (abi.PRED_INTER_MASK, abi.PRED_PAL) else -1)
                     U["bsz"].append(ps_)
                     U["weight"].append(weight)
                     U["cflpad"].append(cfl_pad)
                     # residual-only units of launch-ahead blocks: some carry none
-                    U["nores"].append(kind_ in XB.PRE and XB.rng.random() < 0.3)
+                    U["nores"].append(kind_ in XB.CUT and XB.rng.random() < 0.3)
     plane_u = np.array(U["plane"], np.int32)
     ux, uy = np.array(U["x"], np.int32), np.array(U["y"], np.int32)
     tw, th = np.array(U["tw"], np.int32), np.array(U["th"], np.int32)
@@ -666,14 +688,16 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     units["pred"] = predu
     # units that read no picture pixels: inter kinds, palette, residual-only
     interu = ~np.isin(predu, (abi.PRED_INTRA, abi.PRED_CFL))
+    # units that read edges: intra, CfL and the intra half of inter-intra
+    edger = np.isin(predu, (abi.PRED_INTRA, abi.PRED_CFL, abi.PRED_INTER_INTRA))
     bsz = np.array(U["bsz"], np.int32)
     units["bw4"] = units["bh4"] = np.where(interu, bsz // 4, 0)
     txtp, nzw, nzh, coef_off, coefs = make_residuals(rng, tx, tw, th, bdmax, cfg.coef_dtype)
     txtp = np.where(np.array(U["nores"], bool), abi.NO_RESIDUAL, txtp)
     units["txtp"], units["nzw"], units["nzh"], units["coef_off"] = txtp, nzw, nzh, coef_off
-    edge_len = np.where(interu, 0, 2 * th + 2 * tw + 1)
+    edge_len = np.where(edger, 2 * th + 2 * tw + 1, 0)
     edge_start = np.concatenate([[0], np.cumsum(edge_len)[:-1]])
-    units["edge_off"] = np.where(interu, 0, edge_start + 2 * th)
+    units["edge_off"] = np.where(interu, 0, edge_start + 2 * th)   # (inter-intra: in its record)
     iu = ~cflu & ~interu
     units["max_w"] = np.where(iu, pw[plane_u] - ux, 0)
     units["max_h"] = np.where(iu, ph[plane_u] - uy, 0)
@@ -713,7 +737,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
         f = int(flags[i])
         hl, ht = bool(f & abi.IE_HAVE_LEFT), bool(f & abi.IE_HAVE_TOP)
         m, _ = remap_mode(modes[i], angles[i], hl, ht)
-        nd = 0 if interu[i] else _NEEDS[m]   # inter units read only the references
+        nd = _NEEDS[m] if edger[i] else 0   # inter units read only the references
         L, O = lv[p], own[p]
         reads = []   # (plane, rows, cols) regions read
         if nd & _NEED_L:
@@ -735,6 +759,8 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
             reads.append((p, slice(ry, ry + 1), slice(rx, rx + 1)))
         if cflu[i]:
             reads.append((0, slice(2 * y4, 2 * (y4 + t4h)), slice(2 * x4, 2 * (x4 + t4w))))
+        if predu[i] == abi.PRED_NONE:   # the residual reads the prediction under it
+            reads.append((p, slice(y4, y4 + t4h), slice(x4, x4 + t4w)))
         d, pr = -1, set()
         for (q, ry, rx) in reads:
             assert lv[q][ry, rx].min() >= 0     # (a block's luma precedes its chroma)
@@ -804,7 +830,8 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     recs = recs[perm]
     aux = np.array(U["aux"], np.int64)[perm].astype(np.int32)
     rec_start = unit_start.copy()
-    unit_rec = np.where(np.isin(units["pred"], (abi.PRED_INTRA, abi.PRED_CFL)), np.arange(n), -1).astype(np.int32)
+    unit_rec = np.where(np.isin(units["pred"], (abi.PRED_INTRA, abi.PRED_CFL, abi.PRED_INTER_INTRA)),
+                        np.arange(n), -1).astype(np.int32)
     rp = np.argsort(run_lv, kind="stable")
     runs = runs[rp]
     run_start = np.searchsorted(run_lv[rp], np.arange(n_levels + 1)).astype(np.int32)
@@ -825,6 +852,9 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     fr.dec_units = dec_units
     fr.aux = aux if XB.used else None
     fr.aux_pool = XB.pool() if XB.used else None
+    for i in np.nonzero(predu == abi.PRED_INTER_INTRA)[0]:   # inter-intra records: their edge slots
+        o = int(U["aux"][i])
+        fr.aux_pool[o:o + 4] = np.array([edge_start[i] + 2 * th[i]], "<i4").view(np.uint8)
     return fr
 
 

@@ -780,13 +780,20 @@ int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int y, int tx,
  *               int32 n_refs, 12 pad bytes, then per ref 16 B: int32 x, y
  *               (integer source position of block pixel (0, 0): pos >> 10),
  *               uint16 mx, my (pos & 1023), uint16 dx, dy (steps)
+ *   INTER_INTRA (recon_b_inter's inter-intra, recon_tmpl.c:1540-1580; blocks
+ *               up to 32 x 32): uint8 mask[h][w] (the ii or wedge mask), the
+ *               intra mode (DC / VERT / HOR / SMOOTH after the II_ mapping)
+ *               in `mode`, ref[0] / mv[0] / filter2d the put prediction; one
+ *               wavefront unit predicts the whole block (its edges gathered
+ *               from the picture like an intra unit's, no edge flags, no
+ *               filter), its residuals are residual-only units after it
  * INTER_WMASK / OBMC / SCALED / WARP predictions run in a launch of their own
  * ahead of the wavefront (dav1d_gpu_recon_*'s second launch), cut into
  * prediction units of at most 32 x 32; their residuals are added by PRED_NONE
  * units in the wavefront.  Those four kinds read their references directly:
  * the reference planes need the padding the unit batch documents (the
- * emu_edge clamp covers INTER / INTER_AVG / INTER_WAVG / INTER_MASK).
- * INTER_INTRA is not recorded.  0 or -1. */
+ * emu_edge clamp covers INTER / INTER_AVG / INTER_WAVG / INTER_MASK /
+ * INTER_INTRA).  0 or -1. */
 int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, const void *aux, size_t aux_bytes);
 /* Build, upload and launch everything recorded since the last flush on
  * `stream` (the recorder waits for its previous flush before reusing its

@@ -1969,7 +1969,25 @@ int SFX(oracle_recon_intra_frame)(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIn
     for (int i = 0; i < n_steps; i++) {
         const int op = steps[2 * i], a = steps[2 * i + 1];
         if (op == 0) {
-            if (unit_rec[a] >= 0) {
+            if (unit_rec[a] >= 0 && rb->units[a].pred == DGPU_PRED_INTER_INTRA) {
+                /* recon_b_inter's inter-intra (src/recon_tmpl.c:1551-1566):
+                 * dav1d_prepare_intra_edges for the whole block into the
+                 * edge slot of its record, the remapped mode and angle
+                 * into the record (a stand-in INTRA unit carries them) */
+                uint8_t *rec = (uint8_t *)rb->aux_pool + rb->aux[a];
+                Dav1dGpuUnit tmp = rb->units[a];
+                tmp.pred = DGPU_PRED_INTRA;
+                memcpy(&tmp.p.intra.edge_off, rec, 4);
+                Dav1dGpuIntraEdge r1 = eb->recs[unit_rec[a]];
+                r1.unit = 0;
+                Dav1dGpuIntraEdgeBatch ii = *eb;
+                ii.units = &tmp;
+                ii.recs = &r1;
+                ii.n_recs = 1;
+                SFX(oracle_prepare_intra_edges)(&ii);
+                rec[4] = tmp.p.intra.mode;
+                memcpy(rec + 6, &tmp.p.intra.angle, 2);
+            } else if (unit_rec[a] >= 0) {
                 one.recs = eb->recs + unit_rec[a];
                 SFX(oracle_prepare_intra_edges)(&one);
             }

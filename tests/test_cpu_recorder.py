@@ -114,6 +114,10 @@ def test_recorder_block_aux_validation(pkg):
         assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == 0
         sc[0] = 3
         assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == -1
+        assert rec(bytes(256), kind=abi.PRED_INTER_INTRA, mode=abi.SMOOTH_PRED) == 0
+        assert rec(bytes(256), kind=abi.PRED_INTER_INTRA, mode=abi.PAETH_PRED) == -1   # DC / V / H / SMOOTH only
+        assert rec(bytes(64 * 64), kind=abi.PRED_INTER_INTRA, w=64, h=64, x=0, y=0,
+                   tx=abi.TX_INDEX[(16, 16)]) == -1                              # blocks up to 32x32
         assert rec(bytes(16), kind=abi.PRED_INTER) == -1                      # no data kind
         assert L.dav1d_gpu_rec_block(r, ctypes.byref(_blk(pkg, kind=abi.PRED_WARP))) == -1
     finally:

@@ -191,7 +191,8 @@ def test_recorder_unpadded_references(oracle, bpc, bdmax, seed):
 def test_recorder_block_data_kinds(oracle, bpc, bdmax, seed):
     """Blocks recorded with their data (dav1d_gpu_rec_block_aux): INTER_MASK
     (caller masks, and COMPOUND_SEG chroma on the luma's w_mask output),
-    palette, WARP, INTER_WMASK, INTER_OBMC and INTER_SCALED, beside intra /
+    palette, WARP, INTER_WMASK, INTER_OBMC, INTER_SCALED and inter-intra (its
+    intra edges gathered in the wavefront), beside intra /
     CfL / inter blocks whose edges read them.  The recorder cuts the
     launch-ahead kinds into prediction units and adds their residuals in the
     wavefront; the oracle walks its own cut of the same blocks in decoder
@@ -203,7 +204,7 @@ def test_recorder_block_data_kinds(oracle, bpc, bdmax, seed):
     kinds = set(int(k) for k in fr.units["pred"])
     import dav1d_mirror_amd.abi as abi
     assert {abi.PRED_INTER_MASK, abi.PRED_PAL, abi.PRED_WARP, abi.PRED_INTER_WMASK, abi.PRED_INTER_OBMC,
-            abi.PRED_INTER_SCALED} <= kinds
+            abi.PRED_INTER_SCALED, abi.PRED_INTER_INTRA} <= kinds
     dst, refs = _setup(fr)
     rec = intra.Recorder(fr.cfg.bpc, fr.cfg.bitdepth_max, fr.cfg.width, fr.cfg.height)
     intra.replay(rec, fr)
