@@ -316,8 +316,13 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     using C = typename Px<BPC>::coef;
     constexpr int B = BPC / 8;
     if (!b || !e || !s || !b->units || !e->recs || !s->workspace) return -1;
-    for (int p = 0; p < 3; p++)
+    for (int p = 0; p < 3; p++) {
         if (((uintptr_t)b->dst[p].data & 15) || (b->dst[p].stride & 15)) return -4;
+        // row offsets are 24-bit multiplies in the kernels (__mul24): strides in [0, 2^23) bytes
+        if (!stride24(b->dst[p].stride)) return -4;
+        for (int r = 0; r < DGPU_MAX_REFS; r++)
+            if (b->ref[r][p].data && !stride24(b->ref[r][p].stride)) return -4;
+    }
     std::vector<FlowTask> tasks;
     std::vector<int32_t> level_tasks;
     int rc = flow_tasks(s, b->n_units, tasks, level_tasks);
@@ -385,6 +390,7 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     a.coef = (C *)b->coef;
     a.edges = (const P *)b->edges;
     a.cfl_luma = (const P *)b->cfl_luma.data;
+    if (b->cfl_luma.data && !stride24(b->cfl_luma.stride)) return -4;
     a.cfl_luma_stride = (int)(b->cfl_luma.stride / B);
     a.cfl_ss = b->cfl_ss;
     a.aux = b->aux;   // INTER_MASK masks / PAL records (recorder flushes)

@@ -18,8 +18,13 @@ static int launch_ie(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *
     for (int c = 0; c < DGPU_N_RECT_TX_SIZES; c++)
         if (b->class_start[c + 1] < b->class_start[c] || b->class_warp[c]) return -2;
     if (b->class_start[0] != 0 || b->class_start[DGPU_N_RECT_TX_SIZES] != b->n_units) return -2;
-    for (int p = 0; p < 3; p++)
+    for (int p = 0; p < 3; p++) {
         if (((uintptr_t)b->dst[p].data & 15) || (b->dst[p].stride & 15)) return -4;
+        // row offsets are 24-bit multiplies in the kernels (__mul24): strides in [0, 2^23) bytes
+        if (!stride24(b->dst[p].stride)) return -4;
+        for (int r = 0; r < DGPU_MAX_REFS; r++)
+            if (b->ref[r][p].data && !stride24(b->ref[r][p].stride)) return -4;
+    }
     if (b->n_units == 0) return 0;
     ReconArgs<BPC> a;
     memset(&a, 0, sizeof(a));
@@ -41,6 +46,7 @@ static int launch_ie(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *
     a.coef = (C *)b->coef;
     a.edges = (const P *)b->edges;
     a.cfl_luma = (const P *)b->cfl_luma.data;
+    if (b->cfl_luma.data && !stride24(b->cfl_luma.stride)) return -4;
     a.cfl_luma_stride = (int)(b->cfl_luma.stride / B);
     a.cfl_ss = b->cfl_ss;
     a.aux = b->aux;   // INTER_MASK masks / PAL records (recorder flushes)

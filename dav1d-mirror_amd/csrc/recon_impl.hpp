@@ -258,6 +258,10 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     if (b->class_start[0] != 0 || b->class_start[DGPU_N_RECT_TX_SIZES] != b->n_units) return -2;
     for (int p = 0; p < 3; p++) {   // output rows are stored with aligned 4/8-byte stores
         if (((uintptr_t)b->dst[p].data & 15) || (b->dst[p].stride & 15)) return -4;
+        // row offsets are 24-bit multiplies in the kernels (__mul24): strides in [0, 2^23) bytes
+        if (!stride24(b->dst[p].stride)) return -4;
+        for (int r = 0; r < DGPU_MAX_REFS; r++)
+            if (b->ref[r][p].data && !stride24(b->ref[r][p].stride)) return -4;
         for (int r = 0; r < DGPU_MAX_REFS; r++)   // footprint rows are read as aligned dwords
             if (b->ref[r][p].data && (b->ref[r][p].stride & 3)) return -4;
     }
@@ -277,6 +281,7 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     a.coef = (C *)b->coef;
     a.edges = (const P *)b->edges;
     a.cfl_luma = (const P *)b->cfl_luma.data;
+    if (b->cfl_luma.data && !stride24(b->cfl_luma.stride)) return -4;
     a.cfl_luma_stride = (int)(b->cfl_luma.stride / B);
     a.cfl_ss = b->cfl_ss;
     a.aux = b->aux;

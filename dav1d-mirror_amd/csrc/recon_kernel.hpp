@@ -64,6 +64,9 @@
 #ifndef DGPU_ALIGNED_ROWS8
 #define DGPU_ALIGNED_ROWS8 1    // 8bpc footprint rows by aligned loads + v_alignbyte (see HPass)
 #endif
+#ifndef DGPU_VODD_ALIGN
+#define DGPU_VODD_ALIGN 0   // odd vertical rows by realigned pairs (the round-1/2 form) instead of shifted taps
+#endif
 #ifndef DGPU_ALIGNED_ROWS16
 #define DGPU_ALIGNED_ROWS16 0   // 16bpc: register pressure spills with it (measured), off
 #endif
@@ -147,6 +150,8 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// the kernels form row offsets with 24-bit multiplies (__mul24 / __umul24)
+__host__ __device__ constexpr bool stride24(ptrdiff_t s) { return s >= 0 && s < (1 << 23); }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
@@ -321,12 +326,13 @@ __device__ __forceinline__ void hdot4x4(const uint32_t *lo, const uint32_t *hi, 
         : "v"(lo[0]), "v"(lo[1]), "v"(lo[2]), "v"(lo[3]), "v"(hi[0]), "v"(hi[1]), "v"(hi[2]), "v"(hi[3]),
           "v"(tx), "v"(ty));
 }
-// t[i] = (sum_k dot2(a[k][i], tap pair k) + kk) >> sh, k = 0..3
+// t[i] = (sum_k dot2(a[k][i], tap pair k) + kk) >> sh, k = 0..3; the chains
+// start from kk (an SGPR operand), so no separate add
 __device__ __forceinline__ void vdot4x4(const uint32_t (*a)[4], const uint4 &tv, int kk, int sh, int *t) {
-    asm("v_dot2_i32_i16 %0, %4, %20, 0\n\t"
-        "v_dot2_i32_i16 %1, %5, %20, 0\n\t"
-        "v_dot2_i32_i16 %2, %6, %20, 0\n\t"
-        "v_dot2_i32_i16 %3, %7, %20, 0\n\t"
+    asm("v_dot2_i32_i16 %0, %4, %20, %24\n\t"
+        "v_dot2_i32_i16 %1, %5, %20, %24\n\t"
+        "v_dot2_i32_i16 %2, %6, %20, %24\n\t"
+        "v_dot2_i32_i16 %3, %7, %20, %24\n\t"
         "v_dot2_i32_i16 %0, %8, %21, %0\n\t"
         "v_dot2_i32_i16 %1, %9, %21, %1\n\t"
         "v_dot2_i32_i16 %2, %10, %21, %2\n\t"
@@ -339,10 +345,6 @@ __device__ __forceinline__ void vdot4x4(const uint32_t (*a)[4], const uint4 &tv,
         "v_dot2_i32_i16 %1, %17, %23, %1\n\t"
         "v_dot2_i32_i16 %2, %18, %23, %2\n\t"
         "v_dot2_i32_i16 %3, %19, %23, %3\n\t"
-        "v_add_u32 %0, %24, %0\n\t"
-        "v_add_u32 %1, %24, %1\n\t"
-        "v_add_u32 %2, %24, %2\n\t"
-        "v_add_u32 %3, %24, %3\n\t"
         "v_ashrrev_i32 %0, %25, %0\n\t"
         "v_ashrrev_i32 %1, %25, %1\n\t"
         "v_ashrrev_i32 %2, %25, %2\n\t"
@@ -369,6 +371,59 @@ __device__ __forceinline__ uint32_t alb(uint32_t hi, uint32_t lo, int s) {
 // (lo16(lo), lo16(hi)) -- int16 truncation, as the reference's int16_t stores
 __device__ __forceinline__ uint32_t pack16(int lo, int hi) {
     return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+
+// The odd output rows of a 4x2 task from the same (row 2p, row 2p+1) pairs
+// as the even ones: row 2j+1+m needs taps shifted by one row, i.e. pairs
+// (0, t0) (t1, t2) (t3, t4) (t5, t6) (t7, 0) over P[0..4] -- five dot2 per
+// output instead of four on realigned pairs (v_alignbyte) (s: the shifted
+// tap pairs, see vtaps_odd).  Two blocks (operand limit); the first ends
+// with wait states, its outputs being DOT results.
+__device__ __forceinline__ void vtaps_odd(const uint4 &tv, uint32_t *s) {
+    s[0] = tv.x << 16;
+    s[1] = alb(tv.y, tv.x, 2);
+    s[2] = alb(tv.z, tv.y, 2);
+    s[3] = alb(tv.w, tv.z, 2);
+    s[4] = tv.w >> 16;
+}
+__device__ __forceinline__ void vdot5x4(const uint32_t (*a)[4], const uint32_t *s, int kk, int sh, int *t) {
+    int u0, u1, u2, u3;
+    asm("v_dot2_i32_i16 %0, %4, %16, %19\n\t"
+        "v_dot2_i32_i16 %1, %5, %16, %19\n\t"
+        "v_dot2_i32_i16 %2, %6, %16, %19\n\t"
+        "v_dot2_i32_i16 %3, %7, %16, %19\n\t"
+        "v_dot2_i32_i16 %0, %8, %17, %0\n\t"
+        "v_dot2_i32_i16 %1, %9, %17, %1\n\t"
+        "v_dot2_i32_i16 %2, %10, %17, %2\n\t"
+        "v_dot2_i32_i16 %3, %11, %17, %3\n\t"
+        "v_dot2_i32_i16 %0, %12, %18, %0\n\t"
+        "v_dot2_i32_i16 %1, %13, %18, %1\n\t"
+        "v_dot2_i32_i16 %2, %14, %18, %2\n\t"
+        "v_dot2_i32_i16 %3, %15, %18, %3\n\t"
+        "s_nop 2"
+        : "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3)
+        : "v"(a[0][0]), "v"(a[0][1]), "v"(a[0][2]), "v"(a[0][3]), "v"(a[1][0]), "v"(a[1][1]), "v"(a[1][2]),
+          "v"(a[1][3]), "v"(a[2][0]), "v"(a[2][1]), "v"(a[2][2]), "v"(a[2][3]), "v"(s[0]), "v"(s[1]), "v"(s[2]),
+          "s"(kk));
+    asm("v_dot2_i32_i16 %0, %4, %12, %0\n\t"
+        "v_dot2_i32_i16 %1, %5, %12, %1\n\t"
+        "v_dot2_i32_i16 %2, %6, %12, %2\n\t"
+        "v_dot2_i32_i16 %3, %7, %12, %3\n\t"
+        "v_dot2_i32_i16 %0, %8, %13, %0\n\t"
+        "v_dot2_i32_i16 %1, %9, %13, %1\n\t"
+        "v_dot2_i32_i16 %2, %10, %13, %2\n\t"
+        "v_dot2_i32_i16 %3, %11, %13, %3\n\t"
+        "v_ashrrev_i32 %0, %14, %0\n\t"
+        "v_ashrrev_i32 %1, %14, %1\n\t"
+        "v_ashrrev_i32 %2, %14, %2\n\t"
+        "v_ashrrev_i32 %3, %14, %3"
+        : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3)
+        : "v"(a[3][0]), "v"(a[3][1]), "v"(a[3][2]), "v"(a[3][3]), "v"(a[4][0]), "v"(a[4][1]), "v"(a[4][2]),
+          "v"(a[4][3]), "v"(s[3]), "v"(s[4]), "s"(sh));
+    t[0] = u0;
+    t[1] = u1;
+    t[2] = u2;
+    t[3] = u3;
 }
 
 // Copies bytes [src, src + n) into 16-B aligned LDS at their own 16-B skew
@@ -724,7 +779,7 @@ template <int BPC, int TX> struct HPass {
         sb = (unsigned)stride_px * B;
         const int q = l % QW;
         p0 = l / QW;
-        rp = reinterpret_cast<const uint8_t *>(org) + (size_t)(2u * p0 * sb) + 4 * B * q;
+        rp = reinterpret_cast<const uint8_t *>(org) + (size_t)__umul24(2u * p0, sb) + 4 * B * q;
         sh = 0;
         if constexpr (AL) {
             sh = (unsigned)reinterpret_cast<uintptr_t>(rp) & 3u;   // strides are dword multiples (launch check)
@@ -749,7 +804,7 @@ template <int BPC, int TX> struct HPass {
             const bool task = k0 + c < IT && pu < RP;
             const bool n0 = !DGPU_ROWSKIP || (task && 2 * p >= rlo && 2 * p <= rhi);
             const bool n1 = !DGPU_ROWSKIP || (task && 2 * p + 1 >= rlo && 2 * p + 1 <= rhi);
-            const uint8_t *a0 = rp + (size_t)((unsigned)(p - p0) * 2u * sb);
+            const uint8_t *a0 = rp + (size_t)__umul24((unsigned)(p - p0) * 2u, sb);
             // row 2p+1 == H+7 (last pair) is never used: re-read row 2p
             const uint8_t *a1 = 2 * p + 1 < H + 7 ? a0 + sb : a0;
 #ifdef DGPU_FAKE_COALESCE
@@ -864,13 +919,19 @@ __device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, cons
         const uint4 v = *reinterpret_cast<const uint4 *>(mid + (j + k) * W + 4 * q);
         P[k][0] = v.x; P[k][1] = v.y; P[k][2] = v.z; P[k][3] = v.w;
     }
-    uint32_t O[4][4];   // odd rows: (row 2j+1+2k, row 2j+2+2k) pairs
+    vdot4x4(P, tv, kk, sh, t);
+#if DGPU_VODD_ALIGN   // odd rows on realigned pairs (row 2j+1+2k, row 2j+2+2k)
+    uint32_t O[4][4];
 #pragma unroll
     for (int k = 0; k < 4; k++)
 #pragma unroll
         for (int i = 0; i < 4; i++) O[k][i] = alb(P[k + 1][i], P[k][i], 2);
-    vdot4x4(P, tv, kk, sh, t);
     vdot4x4(O, tv, kk, sh, t + 4);
+#else
+    uint32_t so[5];
+    vtaps_odd(tv, so);
+    vdot5x4(P, so, kk, sh, t + 4);
+#endif
 }
 
 // ------------------------------------------------------------------ cfl ---
@@ -902,7 +963,7 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
         if (fast) {   // luma rows 4j..4j+3, columns 8q..8q+7
 #pragma unroll
             for (int rr = 0; rr < 2; rr++) {
-                const P *r0 = yp + (4 * j + 2 * rr) * ys + 8 * q;
+                const P *r0 = yp + __mul24(4 * j + 2 * rr, ys) + 8 * q;
                 if constexpr (BPC == 8) {
                     const u32x2 v0 = gld<u32x2a1>(r0), v1 = gld<u32x2a1>(r0 + ys);
                     // byte pairs summed over both rows: dot4 with 1-masks
@@ -922,7 +983,7 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 const int sx = min(4 * q + (i & 3), vw - 1), sy = min(2 * j + (i >> 2), vh - 1);
-                const P *p = yp + (sy << ssv) * ys + (sx << ssh);
+                const P *p = yp + __mul24(sy << ssv, ys) + (sx << ssh);
                 int v = gld<P>(p);
                 if (ssh) v += gld<P>(p + 1);
                 if (ssv) {
@@ -1404,7 +1465,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
 #pragma unroll
         for (int rr = 0; rr < 2; rr++) {
-            P *row = dstp + (2 * j + rr) * ds + 4 * q;
+            P *row = dstp + __mul24(2 * j + rr, ds) + 4 * q;   // 24-bit: strides < 2^23 px (full-rate multiply)
             const int o0 = clampi(pv[4 * rr + 0] + rv[4 * rr + 0], 0, bdmax);
             const int o1 = clampi(pv[4 * rr + 1] + rv[4 * rr + 1], 0, bdmax);
             const int o2 = clampi(pv[4 * rr + 2] + rv[4 * rr + 2], 0, bdmax);
@@ -1477,7 +1538,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                     for (int i = 0; i < 8; i++)
                         pv[i] = clampi((p0[i] * wt + t1[i] * (16 - wt) + (8 << ib)) >> (ib + 4), 0, bdmax);
                 } else {   // INTER_MASK: mask rows of the block (stride bw), 4 bytes per task row
-                    const uint8_t *mk = a.aux_pool + auxo + (2 * j) * bw + 4 * q;
+                    const uint8_t *mk = a.aux_pool + auxo + __mul24(2 * j, bw) + 4 * q;
                     const uint32_t m0 = gld<uint32_t>(mk), m1 = gld<uint32_t>(mk + bw);
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
@@ -1593,7 +1654,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             } else {
                 intra_task<TX>(is, tl2, fe, 4 * q, 2 * j, pvi);
             }
-            const uint8_t *mk = mkb + (2 * j) * bw + 4 * q;
+            const uint8_t *mk = mkb + __mul24(2 * j, bw) + 4 * q;
             const uint32_t m0 = gld<uint32_t>(mk), m1 = gld<uint32_t>(mk + bw);
 #pragma unroll
             for (int i = 0; i < 8; i++) {
@@ -1640,7 +1701,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             const int j = t / QW, q = t % QW;
             int pv[8];
 #pragma unroll
-            for (int i = 0; i < 8; i++) pv[i] = gld<P>(dstp + (2 * j + (i >> 2)) * ds + 4 * q + (i & 3));
+            for (int i = 0; i < 8; i++) pv[i] = gld<P>(dstp + __mul24(2 * j + (i >> 2), ds) + 4 * q + (i & 3));
             emit(j, q, pv);
         }
     }
@@ -1828,7 +1889,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
                 const int rv = haveres ? (int)res[(4 * q + i) * H + 2 * j + rr] : dcres;
                 o[i] = clampi(pv[4 * rr + i] + rv, 0, bdmax);
             }
-            P *row = dstp + (2 * j + rr) * ds + 4 * q;
+            P *row = dstp + __mul24(2 * j + rr, ds) + 4 * q;   // 24-bit: strides < 2^23 px (full-rate multiply)
             if constexpr (BPC == 8)
                 gst<uint32_t>(row, (uint32_t)o[0] | o[1] << 8 | o[2] << 16 | (uint32_t)o[3] << 24);
             else

@@ -161,6 +161,13 @@ __global__ __launch_bounds__(64) void k_emu_footprints(EmuArgs a) {
     }
 }
 
+// per 4x4 cell of a plane: the level and the decode-order cell that last
+// wrote it, side by side (one cache line per lookup).  `own` is stored as
+// the flush's cell base + the cell index, so the maps are never cleared: an
+// entry whose own is below the current base was written by an earlier flush
+// (no producer, level -1 for the level rule).
+struct LvOwn { int32_t lv, own; };
+
 struct Unit {   // a transform cell before sorting
     Dav1dGpuUnit u;
     Dav1dGpuIntraEdge rec;
@@ -229,6 +236,12 @@ struct Dav1dGpuRecorder {
     std::vector<Dav1dGpuUnit> xunits;   // the launch ahead of the wavefront (class order)
     std::vector<int32_t> xaux;
     std::vector<uint8_t> h_host;   // DAV1D_GPU_REC_HOSTONLY: stands in for the pinned buffer
+    // per-4x4 maps kept across flushes (generation-stamped, see LvOwn):
+    // the residual recorded at each cell (index + res_base) and LvOwn
+    std::vector<int32_t> res_at[3];
+    std::vector<LvOwn> lvown[3];
+    int32_t map_w4[3] = {0, 0, 0}, map_h4[3] = {0, 0, 0};
+    int32_t res_base = 0, cell_base = 0;
     PinnedBuf pin;   // units | recs | coefficients | emu jobs, written in place by the fill
     PinnedBuf flag;  // the last flush's wavefront error word, copied back on its stream
     DevBuf d_units, d_recs, d_coef, d_edges, d_work, d_emu, d_emu_jobs, d_aux, d_auxp, d_xunits, d_xaux;
@@ -471,27 +484,42 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         mw[p] = pw[p] / 4 + kMapPad4;
         mh[p] = ph[p] / 4 + kMapPad4;
     }
+    // the maps, kept across flushes; cleared only when their size changes or
+    // the stamps would overflow
+    size_t ncells = 0;   // an upper bound of this flush's cells (an inter-intra block adds one)
+    for (const Dav1dGpuRecBlock &b : r->blocks) ncells += (size_t)(b.w / kTx[b.tx].w) * (b.h / kTx[b.tx].h) + 1;
+    {
+        bool reset = (int64_t)r->res_base + (int64_t)r->residuals.size() >= INT32_MAX ||
+                     (int64_t)r->cell_base + (int64_t)ncells >= INT32_MAX;
+        for (int p = 0; p < 3; p++) reset |= r->map_w4[p] != mw[p] || r->map_h4[p] != mh[p];
+        if (reset) {
+            for (int p = 0; p < 3; p++) {
+                r->res_at[p].assign((size_t)mw[p] * mh[p], -1);
+                r->lvown[p].assign((size_t)mw[p] * mh[p], LvOwn{-1, -1});
+                r->map_w4[p] = mw[p];
+                r->map_h4[p] = mh[p];
+            }
+            r->res_base = r->cell_base = 0;
+        }
+    }
+    const int32_t res_base = r->res_base, cell_base = r->cell_base;
+    // the stamps of this flush, whatever its outcome, are below the next one's
+    r->res_base += (int32_t)r->residuals.size();
+    r->cell_base += (int32_t)ncells;
     // residual lookup: per plane, the top-left 4x4 cell of each residual
-    std::vector<int32_t> res_at[3];
-    for (int p = 0; p < 3; p++) res_at[p].assign((size_t)mw[p] * mh[p], -1);
+    std::vector<int32_t> *res_at = r->res_at;
     for (size_t i = 0; i < r->residuals.size(); i++) {
         const Residual &q = r->residuals[i];
-        res_at[q.plane][(size_t)(q.y / 4) * mw[q.plane] + q.x / 4] = (int32_t)i;
+        res_at[q.plane][(size_t)(q.y / 4) * mw[q.plane] + q.x / 4] = res_base + (int32_t)i;
     }
 
     // 1-3. transform units in decode order, their edge records and levels
     std::vector<Unit> &cells = r->cells;
     cells.clear();
-    {
-        size_t nc = 0;
-        for (const Dav1dGpuRecBlock &b : r->blocks) nc += (size_t)(b.w / kTx[b.tx].w) * (b.h / kTx[b.tx].h);
-        cells.reserve(nc);
-    }
+    cells.reserve(ncells);
     // per 4x4: level and the decode-order cell writing it, side by side (one
     // cache line per lookup)
-    struct LvOwn { int32_t lv, own; };
-    std::vector<LvOwn> lvown[3];
-    for (int p = 0; p < 3; p++) lvown[p].assign((size_t)mw[p] * mh[p], LvOwn{-1, -1});
+    std::vector<LvOwn> *lvown = r->lvown;
     lap("maps");
     r->emu.clear();
     int32_t emu_rows = 0;
@@ -656,7 +684,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 u.plane = (uint8_t)p;
                 u.pred = (uint8_t)((pre || (iib && !iic)) ? DGPU_PRED_NONE : b.kind);
                 u.txtp = DGPU_NO_RESIDUAL;
-                const int ri = iic ? -1 : res_at[p][(size_t)y4 * w4p + x4];
+                const int32_t rs_ = iic ? -1 : res_at[p][(size_t)y4 * w4p + x4];
+                const int ri = rs_ >= res_base ? rs_ - res_base : -1;   // (an earlier flush's: none)
                 if (ri >= 0 && r->residuals[ri].tx == b.tx) {
                     const Residual &q = r->residuals[ri];
                     u.txtp = (uint8_t)q.txtp;
@@ -776,10 +805,11 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 // a pixel no cell of this flush wrote came from an earlier
                 // flush on the same stream: no producer, level 0 for it
                 auto cell = [&](int cx, int cy) {
-                    const size_t at = (size_t)cy * w4p + cx;
-                    d = std::max(d, lvown[p][at].lv);
-                    const int32_t o = lvown[p][at].own;
-                    if (o >= 0 && (prod.size() == p0 || prod.back() != o)) prod.push_back(o);
+                    const LvOwn m = lvown[p][(size_t)cy * w4p + cx];
+                    if (m.own < cell_base) return;   // an earlier flush's pixel: level -1, no producer
+                    d = std::max(d, m.lv);
+                    const int32_t o = m.own - cell_base;
+                    if (prod.size() == p0 || prod.back() != o) prod.push_back(o);
                 };
                 if (nd & 1) {
                     if (hl) {
@@ -811,10 +841,11 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     const int lw4 = mw[0];
                     for (int cy = 2 * y4; cy < 2 * (y4 + th4); cy++)
                         for (int cx = 2 * x4; cx < 2 * (x4 + tw4); cx++) {
-                            const size_t at = (size_t)cy * lw4 + cx;
-                            d = std::max(d, lvown[0][at].lv);   // (luma of an earlier flush: no producer)
-                            const int32_t o = lvown[0][at].own;
-                            if (o >= 0 && (prod.size() == p0 || prod.back() != o)) prod.push_back(o);
+                            const LvOwn m = lvown[0][(size_t)cy * lw4 + cx];
+                            if (m.own < cell_base) continue;   // luma of an earlier flush: no producer
+                            d = std::max(d, m.lv);
+                            const int32_t o = m.own - cell_base;
+                            if (prod.size() == p0 || prod.back() != o) prod.push_back(o);
                         }
                 }
                 if (prod.size() - p0 > 1) {   // duplicate-free
@@ -826,7 +857,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 const int ci = (int)cells.size() - 1;
                 for (int cy = y4; cy < y4 + cth4; cy++)
                     for (int cx = x4; cx < x4 + ctw4; cx++) {
-                        lvown[p][(size_t)cy * w4p + cx] = LvOwn{c.level, ci};
+                        lvown[p][(size_t)cy * w4p + cx] = LvOwn{c.level, cell_base + ci};
                     }
                 (void)0;   // (c lives in cells already)
             }
@@ -958,6 +989,23 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         r->coefb.clear();
     };
     if ((!n && !nx) || host_only) {
+        // DAV1D_GPU_REC_DUMP=<file> with DAV1D_GPU_REC_HOSTONLY (diagnostics):
+        // the upload image and the schedule, appended, to compare host builds
+        static const char *dump = getenv("DAV1D_GPU_REC_DUMP");
+        if (host_only && dump) {
+            if (FILE *f = fopen(dump, "ab")) {
+                auto put = [&](const void *p, size_t nb) { if (nb) fwrite(p, 1, nb, f); };
+                const int64_t hdr[4] = {n, n_levels, (int64_t)nx, (int64_t)o_end};
+                put(hdr, sizeof(hdr));
+                put(r->h_host.data(), o_end);
+                put(r->unit_start.data(), r->unit_start.size() * 4);
+                put(r->class_start.data(), r->class_start.size() * 4);
+                put(r->dep_start.data(), r->dep_start.size() * 4);
+                put(r->deps.data(), r->deps.size() * 4);
+                put(x_class, sizeof(x_class));
+                fclose(f);
+            }
+        }
         drop_recording();
         return 0;
     }

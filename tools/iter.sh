@@ -1,0 +1,55 @@
+#!/bin/bash
+# One iteration on the GPU box:  bash tools/iter.sh TAG [STEP...]
+#   tests:  the -m gpu parity suite (stops at the first failure)
+#   quick:  headline kernel time (configs 3 / 2 / 4 and families, no other legs)
+#   trace:  rocprofv3 kernel-trace summary of the quick bench
+#   cls:    per-class profile (tools/class_prof.sh)
+#   var:    quick bench per DAV1D_GPU_LIB_VARIANT in $VARIANTS
+# Every step has its own time limit; the script stops at the first failure.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-it}
+shift
+STEPS=${*:-"tests quick"}
+O=$R/gpurun_out/it_$TAG
+mkdir -p "$O"
+cd "$R"
+Q="--no-cpu --steps 30 --warmup 3 --no-tiles --no-intra --no-recorder --no-grain --no-cdef --no-lpf --no-lr"
+for s in $STEPS; do
+    case $s in
+    tests)
+        echo "[it] tests" >&2
+        timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+            > "$O/gputest.log" 2>&1 || { echo "tests failed" >&2; tail -30 "$O/gputest.log"; exit 1; }
+        tail -2 "$O/gputest.log"
+        ;;
+    quick)
+        echo "[it] quick" >&2
+        timeout -k 10 300 python3 bench.py $Q > "$O/quick.json" 2> "$O/quick.err" \
+            || { echo "bench failed" >&2; tail -20 "$O/quick.err"; exit 1; }
+        python3 -c "import json,sys; d=json.load(open('$O/quick.json')); r=d['roofline']; print('4k', r['kernel_us'], r['frac'], {k: v['kernel_us'] for k, v in d.get('configs', {}).items()}, {k: v['kernel_us'] for k, v in d.get('families', {}).items()})"
+        ;;
+    trace)
+        echo "[it] trace" >&2
+        cd /tmp && export TMPDIR=/tmp
+        timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv \
+            -- python3 "$R/bench.py" $Q --no-families > "$O/trace.log" 2>&1 || { echo "trace failed" >&2; exit 1; }
+        cd "$R"
+        head -12 "$O/trace/run_kernel_stats.csv"
+        ;;
+    cls)
+        echo "[it] cls" >&2
+        timeout -k 10 800 bash tools/class_prof.sh "$TAG" > "$O/cls.log" 2>&1 || { echo "cls failed" >&2; tail -20 "$O/cls.log"; exit 1; }
+        cat "$O/cls.log" | tail -60
+        ;;
+    var)
+        for v in base $VARIANTS; do
+            if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
+            timeout -k 10 300 python3 bench.py $Q --no-families --no-configs > "$O/var_$v.json" 2> "$O/var_$v.err" \
+                || { echo "variant $v failed" >&2; tail -5 "$O/var_$v.err"; exit 1; }
+            echo "$v $(grep -o '"kernel_us": [0-9.]*' "$O/var_$v.json" | head -1)"
+        done
+        unset DAV1D_GPU_LIB_VARIANT
+        ;;
+    esac
+done
+echo "[it] done" >&2

@@ -1,0 +1,55 @@
+"""Host-only recorder flushes of several frames with the upload image and
+schedule dumped (DAV1D_GPU_REC_HOSTONLY + DAV1D_GPU_REC_DUMP): compares two
+builds of the recorder's host code byte for byte, no GPU needed.
+
+  python tools/rec_dump.py OUT.bin     (prints one md5 per frame)"""
+import ctypes
+import hashlib
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+FRAMES = [
+    dict(width=3840, height=2160, inter_frac=0.7, sb_edge_backup=False),
+    dict(width=1024, height=512, tile_cols=2, tile_rows=2, cfl_frac=0.6, sb_edge_backup=False),
+    dict(width=992, height=552, inter_frac=0.6, ext_frac=0.5, overhang=True, tile_cols=2, sb_edge_backup=False),
+    dict(width=512, height=256, bpc=16, bitdepth_max=1023, inter_frac=0.5, ext_frac=0.4, sb_edge_backup=False),
+    dict(width=1920, height=1080, inter_frac=0.3, overhang=True, sb_log2=7, sb_edge_backup=False),
+]
+
+
+def main():
+    out = sys.argv[1]
+    os.environ["DAV1D_GPU_REC_HOSTONLY"] = "1"
+    os.environ["DAV1D_GPU_REC_DUMP"] = out
+    import __graft_entry__ as ge
+    ge.load_package()
+    import dav1d_mirror_amd.abi as abi
+    import dav1d_mirror_amd.intra as intra
+    for i, kw in enumerate(FRAMES):
+        if os.path.exists(out):
+            os.remove(out)
+        fr = intra.make_intra_frame(intra.IntraConfig(**kw))
+        rec = intra.Recorder(fr.cfg.bpc, fr.cfg.bitdepth_max, fr.cfg.width, fr.cfg.height)
+        d = (abi.Plane * 3)()
+        for p, (w, h) in enumerate(fr.plane_wh):
+            pad = getattr(fr, "dst_pad", 0)
+            d[p].data, d[p].stride, d[p].w, d[p].h = 0x1000, (w + pad) * (fr.cfg.bpc // 8), w, h
+        r = ((abi.Plane * 3) * abi.MAX_REFS)()
+        for k in range(2):
+            for p, (w, h) in enumerate(fr.plane_wh):
+                st = (w + 2 * fr.cfg.ref_pad) * (fr.cfg.bpc // 8)
+                r[k][p].data, r[k][p].stride, r[k][p].w, r[k][p].h = 0x1000, st, w, h
+        intra.replay(rec, fr)
+        t0 = time.perf_counter()
+        rc = rec.lib.dav1d_gpu_recorder_flush(rec.h, ctypes.byref(d), ctypes.byref(r), None)
+        t1 = time.perf_counter()
+        md5 = hashlib.md5(open(out, "rb").read()).hexdigest() if os.path.exists(out) else None
+        print(f"frame {i} rc {rc} units {rec.stats()[0]} flush {1e3 * (t1 - t0):.2f} ms md5 {md5}", flush=True)
+        rec.close()
+
+
+if __name__ == "__main__":
+    main()
