@@ -86,7 +86,7 @@ __global__ __launch_bounds__(64) void k_itx(typename Px<BPC>::pixel *dst, ptrdif
             int v = x < SW ? (int)coef[lane + x * SH] : 0;
             c[x] = RECT2 ? r8s(v) : v;
         }
-        tx1d<W, 1>(kind_h(txtp), c, rc);
+        tx1d<W, 1, BPC == 8>(kind_h(txtp), c, rc);
 #pragma unroll
         for (int x = 0; x < W; x++) t[lane][x] = cc((c[x] + RND) >> SHIFT);
     }
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(64) void k_itx(typename Px<BPC>::pixel *dst, ptrdif
         int c[H];
 #pragma unroll
         for (int y = 0; y < H; y++) c[y] = y < SH ? t[y][lane] : 0;
-        tx1d<H, 1>(kind_v(txtp), c, cc);
+        tx1d<H, 1, BPC == 8>(kind_v(txtp), c, cc);
 #pragma unroll
         for (int y = 0; y < H; y++) {
             pixel &d = dst[y * ds + lane];

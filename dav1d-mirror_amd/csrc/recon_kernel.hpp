@@ -645,8 +645,8 @@ __device__ __forceinline__ void intra_task(const IntraState &s, const P *tl, con
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int x = x0 + (i & 3), y = y0 + (i >> 2);
-            const int xpos = (y + 1) * s.d1, frac = xpos & 0x3e;
-            const int base = (xpos >> 6) + x * (1 + s.up);
+            const int xpos = __mul24(y + 1, s.d1), frac = xpos & 0x3e;
+            const int base = (xpos >> 6) + (x << s.up);   // s.up is 0 or 1
             pv[i] = base < s.maxb ? (fe[base] * (64 - frac) + fe[base + 1] * frac + 32) >> 6 : fe[s.maxb];
         }
         break;
@@ -654,8 +654,8 @@ __device__ __forceinline__ void intra_task(const IntraState &s, const P *tl, con
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int x = x0 + (i & 3), y = y0 + (i >> 2);
-            const int ypos = (x + 1) * s.d1, frac = ypos & 0x3e;
-            const int base = (ypos >> 6) + y * (1 + s.up);
+            const int ypos = __mul24(x + 1, s.d1), frac = ypos & 0x3e;
+            const int base = (ypos >> 6) + (y << s.up);
             pv[i] = base < s.maxb ? (fe[s.maxb - base] * (64 - frac) + fe[s.maxb - base - 1] * frac + 32) >> 6
                                   : fe[0];
         }
@@ -666,14 +666,14 @@ __device__ __forceinline__ void intra_task(const IntraState &s, const P *tl, con
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int x = x0 + (i & 3), y = y0 + (i >> 2);
-            const int xpos = ((1 + s.up) << 6) - (y + 1) * s.d1;
-            const int bx = (xpos >> 6) + x * (1 + s.up);
+            const int xpos = ((1 + s.up) << 6) - __mul24(y + 1, s.d1);
+            const int bx = (xpos >> 6) + (x << s.up);
             int t;
             if (bx >= 0) {
                 const int fx = xpos & 0x3e;
                 t = c[bx] * (64 - fx) + c[bx + 1] * fx;
             } else {
-                const int ypos = (y << (6 + s.upl)) - (x + 1) * s.d2;
+                const int ypos = (y << (6 + s.upl)) - __mul24(x + 1, s.d2);
                 const int by = ypos >> 6, fy = ypos & 0x3e;
                 t = lft[-by] * (64 - fy) + lft[-(by + 1)] * fy;
             }
@@ -1333,7 +1333,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                         }
                         c[x] = CL::RECT2 ? r8s(v) : v;
                     }
-                    tx1d<W, 1>(kind_h(txtp), c, rc);
+                    tx1d<W, 1, BPC == 8>(kind_h(txtp), c, rc);
                     constexpr int RND = (1 << CL::SHIFT) >> 1;
 #pragma unroll
                     for (int x = 0; x < W; x++) c[x] = cc((c[x] + RND) >> CL::SHIFT);
@@ -1370,7 +1370,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                 int col[H];
 #pragma unroll
                 for (int y = 0; y < H; y++) col[y] = y < SH ? (int)tmp[y * W + x] : 0;
-                tx1d<H, 1>(kind_v(txtp), col, cc);
+                tx1d<H, 1, BPC == 8>(kind_v(txtp), col, cc);
                 TT *rcol = res + x * H;
                 if constexpr (BPC == 8) {
 #pragma unroll
@@ -1536,14 +1536,14 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                     const int wt = u.p.inter.weight;
 #pragma unroll
                     for (int i = 0; i < 8; i++)
-                        pv[i] = clampi((p0[i] * wt + t1[i] * (16 - wt) + (8 << ib)) >> (ib + 4), 0, bdmax);
+                        pv[i] = clampi((__mul24(p0[i], wt) + __mul24(t1[i], 16 - wt) + (8 << ib)) >> (ib + 4), 0, bdmax);
                 } else {   // INTER_MASK: mask rows of the block (stride bw), 4 bytes per task row
                     const uint8_t *mk = a.aux_pool + auxo + __mul24(2 * j, bw) + 4 * q;
                     const uint32_t m0 = gld<uint32_t>(mk), m1 = gld<uint32_t>(mk + bw);
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
                         const int m = (int)(((i < 4 ? m0 : m1) >> (8 * (i & 3))) & 0xff);
-                        pv[i] = clampi((p0[i] * m + t1[i] * (64 - m) + (32 << ib)) >> (ib + 6), 0, bdmax);
+                        pv[i] = clampi((__mul24(p0[i], m) + __mul24(t1[i], 64 - m) + (32 << ib)) >> (ib + 6), 0, bdmax);
                     }
                 }
                 emit(j, q, pv);
@@ -1659,7 +1659,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 const int m = (int)(((i < 4 ? m0 : m1) >> (8 * (i & 3))) & 0xff);
-                pv[i] = (ipv[k][i] * (64 - m) + pvi[i] * m + 32) >> 6;
+                pv[i] = (__mul24(ipv[k][i], 64 - m) + __mul24(pvi[i], m) + 32) >> 6;
             }
             emit(j, q, pv);
         }
@@ -1855,7 +1855,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
                     }
                     c[x] = CL::RECT2 ? r8s(v) : v;
                 }
-                if (r < nzh) tx1d<W, 1>(kind_h(txtp), c, rc);
+                if (r < nzh) tx1d<W, 1, BPC == 8>(kind_h(txtp), c, rc);
                 constexpr int RND = (1 << CL::SHIFT) >> 1;
 #pragma unroll
                 for (int x = 0; x < W; x++) trow[x] = (TT)cc((c[x] + RND) >> CL::SHIFT);
@@ -1871,7 +1871,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
                 int col[H];
 #pragma unroll
                 for (int y = 0; y < H; y++) col[y] = y < SH ? (int)tmp[y * W + x] : 0;
-                tx1d<H, 1>(kind_v(txtp), col, cc);
+                tx1d<H, 1, BPC == 8>(kind_v(txtp), col, cc);
                 TT *rcol = res + x * H;
 #pragma unroll
                 for (int y = 0; y < H; y++) rcol[y] = (TT)((col[y] + 8) >> 4);
@@ -1938,7 +1938,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
             for (int i = 0; i < 8; i++) {   // p = prep + PREP_BIAS: the bias terms cancel
                 const int m = min(38 + ((abs(p0[i] - p1[i]) + mrnd) >> msh), 64);
                 mm[i] = m;
-                pv[i] = clampi((p0[i] * m + p1[i] * (64 - m) + (32 << ib)) >> (ib + 6), 0, bdmax);
+                pv[i] = clampi((__mul24(p0[i], m) + __mul24(p1[i], 64 - m) + (32 << ib)) >> (ib + 6), 0, bdmax);
             }
             if (!ssh) {
 #pragma unroll
@@ -2016,7 +2016,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
                         const int x = 4 * q + (i & 3), y = 2 * j + (i >> 2);
                         if (x >= x0 && x < x1 && y >= y0 && y < y1) {   // blend_px, src/mc_tmpl.c:640
                             const int m = dspt_obmc[moff + (dir ? x : y)];
-                            ipv[k][i] = (ipv[k][i] * (64 - m) + clampi(lap[i], 0, bdmax) * m + 32) >> 6;
+                            ipv[k][i] = (__mul24(ipv[k][i], 64 - m) + __mul24(clampi(lap[i], 0, bdmax), m) + 32) >> 6;
                         }
                     }
                 }
@@ -2092,7 +2092,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
                         const int p1 = (pv[i] + 32) >> 6;
-                        pv[i] = wt ? clampi((q0[kt][i] * wt + p1 * (16 - wt) + (8 << ib)) >> (ib + 4), 0, bdmax)
+                        pv[i] = wt ? clampi((__mul24(q0[kt][i], wt) + __mul24(p1, 16 - wt) + (8 << ib)) >> (ib + 4), 0, bdmax)
                                    : clampi((q0[kt][i] + p1 + (1 << ib)) >> (ib + 1), 0, bdmax);
                     }
                     emit(j, qq, pv);

@@ -30,6 +30,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <numeric>
 #include <thread>
 #include <vector>
@@ -104,21 +108,102 @@ struct PinnedBuf {   // page-locked staging, so the uploads do not wait for the 
     }
 };
 
-// LSD radix sort of 64-bit keys on bits [lo, hi), 16-bit digits (stable, so
-// keys whose low bits hold their input index need not sort those)
-void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int lo, int hi) {
-    tmp.resize(k.size());
-    std::vector<uint32_t> cnt(1 << 16);
-    for (int sh = lo; sh < hi; sh += 16) {
-        std::fill(cnt.begin(), cnt.end(), 0);
-        for (uint64_t v : k) cnt[(v >> sh) & 0xffff]++;
-        uint32_t acc = 0;
-        for (auto &c : cnt) {
-            const uint32_t t = c;
-            c = acc;
-            acc += t;
+// A few host workers kept for a recorder's lifetime: every parallel step of
+// a flush runs on them (no thread start per step).  run(nt, f) calls f(t) for
+// t in [0, nt) and returns when all have; the caller runs t = 0.
+class Pool {
+public:
+    explicit Pool(int n) : n_(std::max(1, n)) {
+        for (int i = 1; i < n_; i++) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            stop_ = true;
         }
-        for (uint64_t v : k) tmp[cnt[(v >> sh) & 0xffff]++] = v;
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return n_; }
+    template <typename F> void run(int nt, F &&f) {
+        nt = std::min(nt, n_);
+        if (nt <= 1) {
+            f(0);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> l(m_);
+            job_ = [&f](int t) { f(t); };
+            nt_ = nt;
+            pending_ = nt - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [this] { return pending_ == 0; });
+    }
+
+private:
+    void loop(int i) {
+        unsigned seen = 0;
+        for (;;) {
+            std::function<void(int)> job;
+            int nt;
+            {
+                std::unique_lock<std::mutex> l(m_);
+                cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                job = job_;
+                nt = nt_;
+            }
+            if (i < nt) {
+                job(i);
+                std::lock_guard<std::mutex> l(m_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    std::function<void(int)> job_;
+    int nt_ = 0, pending_ = 0;
+    unsigned gen_ = 0;
+    bool stop_ = false;
+};
+
+// LSD radix sort of 64-bit keys on bits [lo, hi), digits of at most 13 bits, by up to
+// nt threads (per-thread digit counts over contiguous chunks, so it stays
+// stable: keys whose low bits hold their input index need not sort those)
+void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int lo, int hi, Pool &pool) {
+    int nt = pool.size();
+    const int passes = (hi - lo + 12) / 13, DB = (hi - lo + passes - 1) / std::max(passes, 1), ND = 1 << DB;
+    const size_t n = k.size();
+    tmp.resize(n);
+    nt = n < 65536 ? 1 : nt;
+    std::vector<uint32_t> cnt((size_t)nt * ND);
+    for (int sh = lo; sh < hi; sh += DB) {
+        auto count = [&](int t) {
+            uint32_t *c = &cnt[(size_t)t * ND];
+            std::fill(c, c + ND, 0);
+            for (size_t i = n * t / nt, e = n * (t + 1) / nt; i < e; i++) c[(k[i] >> sh) & (ND - 1)]++;
+        };
+        auto scatter = [&](int t) {
+            uint32_t *c = &cnt[(size_t)t * ND];
+            for (size_t i = n * t / nt, e = n * (t + 1) / nt; i < e; i++) tmp[c[(k[i] >> sh) & (ND - 1)]++] = k[i];
+        };
+        pool.run(nt, count);
+        uint32_t acc = 0;   // digit-major, then thread: every thread's keys of a digit after the earlier threads'
+        for (int d = 0; d < ND; d++)
+            for (int t = 0; t < nt; t++) {
+                const uint32_t v = cnt[(size_t)t * ND + d];
+                cnt[(size_t)t * ND + d] = acc;
+                acc += v;
+            }
+        pool.run(nt, scatter);
         k.swap(tmp);
     }
 }
@@ -176,6 +261,48 @@ struct Unit {   // a transform cell before sorting
     int32_t aux;   // aux_pool offset (INTER_MASK / PAL), else 0
 };
 
+// what the level pass needs of a cell (its geometry in 4x4 units, the edge
+// needs of its remapped mode, the tile end) and which of its offsets are
+// part-local until the parts are joined
+struct LvJob {
+    int16_t x4, y4, W4, H4;
+    uint8_t p, cw4, ch4, nd, fl, fix;
+    enum { HL = 1, HT = 2, TR = 4, BL = 8, CFL = 16, IIRES = 32 };
+};
+
+// one thread's run of blocks, cut into cells with part-local offsets
+struct CellPart {
+    enum { F_AUX = 1, F_EDGE = 2, F_EMU0 = 4, F_EMU1 = 8, F_IIREC = 16 };
+    std::vector<Unit> cells;
+    std::vector<LvJob> jobs;
+    std::vector<uint8_t> auxp;
+    std::vector<EmuJob> emu;
+    std::vector<Dav1dGpuUnit> xunits;
+    std::vector<int32_t> xaux;
+    int32_t emu_rows = 0;
+    size_t edge_px = 0, n_res_used = 0;
+    int32_t wm_off = -1, wm_w = 0, wm_h = 0;   // the last INTER_WMASK block's seg mask (4:2:0)
+    int err = 0;
+    void clear() {
+        cells.clear();
+        jobs.clear();
+        auxp.clear();
+        emu.clear();
+        xunits.clear();
+        xaux.clear();
+        emu_rows = 0;
+        edge_px = n_res_used = 0;
+        wm_off = -1;
+        wm_w = wm_h = 0;
+        err = 0;
+    }
+    int32_t aux_alloc(size_t nbytes) {   // 16-byte aligned records
+        const size_t o = (auxp.size() + 15) & ~(size_t)15;
+        auxp.resize(o + nbytes);
+        return (int32_t)o;
+    }
+};
+
 // kinds recorded with block data (dav1d_gpu_rec_block_aux); the last four
 // are predicted by the launch ahead of the wavefront
 inline bool is_ext_kind(int k) {
@@ -228,6 +355,9 @@ struct Dav1dGpuRecorder {
     // flush products (kept alive while the device may still read them)
     std::vector<int32_t> unit_start, class_start, rec_start, run_start;
     std::vector<Unit> cells;
+    std::vector<LvJob> jobs;
+    std::vector<CellPart> parts;
+    std::unique_ptr<Pool> pool;   // host workers of the flush's parallel steps
     std::vector<uint64_t> keys, keys_tmp;
     std::vector<int32_t> rank;
     std::vector<int32_t> prod_start, prod, dep_start, deps;   // producers: decode order, then level order
@@ -513,36 +643,23 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         res_at[q.plane][(size_t)(q.y / 4) * mw[q.plane] + q.x / 4] = res_base + (int32_t)i;
     }
 
-    // 1-3. transform units in decode order, their edge records and levels
+    // 1-3. transform units in decode order, their edge records and levels.
+    //    The blocks are cut into cells by up to 8 threads, each over a run of
+    //    blocks into its own part (cells, aux pool, emu jobs, launch-ahead
+    //    units, with part-local offsets); the parts are then joined in
+    //    decode order, their offsets rebased (which gives exactly the
+    //    sequential layout), and one sequential pass assigns the levels and
+    //    producers, which follow decode order.
     std::vector<Unit> &cells = r->cells;
-    cells.clear();
-    cells.reserve(ncells);
     // per 4x4: level and the decode-order cell writing it, side by side (one
     // cache line per lookup)
     std::vector<LvOwn> *lvown = r->lvown;
     lap("maps");
-    r->emu.clear();
-    int32_t emu_rows = 0;
-    size_t edge_px = 0;   // the edge pool (the staged path's), decode order
     std::vector<int32_t> &prod_start = r->prod_start, &prod = r->prod;
-    prod_start.assign(1, 0);
-    prod.clear();
-    size_t n_res_used = 0;
-    // the aux pool (16-byte aligned records) and the launch ahead of the
-    // wavefront (WARP / INTER_WMASK / INTER_OBMC / INTER_SCALED predictions)
     std::vector<uint8_t> &auxp = r->auxp;
-    auxp.clear();
     std::vector<Dav1dGpuUnit> &xunits = r->xunits;
     std::vector<int32_t> &xaux = r->xaux;
-    xunits.clear();
-    xaux.clear();
-    auto aux_alloc = [&](size_t nbytes) -> int32_t {
-        const size_t o = (auxp.size() + 15) & ~(size_t)15;
-        auxp.resize(o + nbytes);
-        return (int32_t)o;
-    };
-    int32_t wm_off = -1, wm_w = 0, wm_h = 0;   // the last INTER_WMASK block's seg mask (4:2:0)
-    for (size_t bi = 0; bi < r->blocks.size(); bi++) {
+    auto build = [&](size_t bi, CellPart &P) -> int {
         const Dav1dGpuRecBlock &b = r->blocks[bi];
         const TxDim t = kTx[b.tx];
         const int p = b.plane, w4p = mw[p];
@@ -566,22 +683,22 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         int32_t mask_base = 0, mask_stride = 0;   // INTER_MASK: the block's mask
         if (b.kind == DGPU_PRED_INTER_MASK) {
             if (bdata) {
-                mask_base = aux_alloc((size_t)b.w * b.h);
-                memcpy(&auxp[mask_base], bdata, (size_t)b.w * b.h);
+                mask_base = P.aux_alloc((size_t)b.w * b.h);
+                memcpy(&P.auxp[mask_base], bdata, (size_t)b.w * b.h);
                 mask_stride = b.w;
             } else {   // COMPOUND_SEG chroma: the luma block's w_mask output
-                if (wm_off < 0 || b.w != wm_w || b.h != wm_h) return -1;
-                mask_base = wm_off;
-                mask_stride = wm_w;
+                if (P.wm_off < 0 || b.w != P.wm_w || b.h != P.wm_h) return -1;
+                mask_base = P.wm_off;
+                mask_stride = P.wm_w;
             }
         }
         if (pre) {   // prediction units of at most 32 x 32, no residual
             const int uw = std::min(b.w, 32), uh = std::min(b.h, 32), utx = tx_of(uw, uh);
             if (utx < 0) return -1;
             if (b.kind == DGPU_PRED_INTER_WMASK) {   // its seg mask at the 4:2:0 chroma resolution
-                wm_w = b.w >> 1;
-                wm_h = b.h >> 1;
-                wm_off = aux_alloc((size_t)wm_w * wm_h);
+                P.wm_w = b.w >> 1;
+                P.wm_h = b.h >> 1;
+                P.wm_off = P.aux_alloc((size_t)P.wm_w * P.wm_h);
             }
             for (int oy = 0; oy < bhc; oy += uh)
                 for (int ox = 0; ox < bwc; ox += uw) {
@@ -607,13 +724,13 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     u.p.inter.weight = b.weight;
                     int32_t ao = 0;
                     if (b.kind == DGPU_PRED_INTER_WMASK) {
-                        ao = wm_off + (oy >> 1) * wm_w + (ox >> 1);
+                        ao = P.wm_off + (oy >> 1) * P.wm_w + (ox >> 1);
                     } else if (b.kind == DGPU_PRED_WARP) {   // abcd, then the unit's 8x8s
                         const int gw = b.w / 8, nx = uw / 8, ny = uh / 8;
-                        ao = aux_alloc(16 + 8 * (size_t)nx * ny);
-                        memcpy(&auxp[ao], bdata, 8);
+                        ao = P.aux_alloc(16 + 8 * (size_t)nx * ny);
+                        memcpy(&P.auxp[ao], bdata, 8);
                         for (int sy = 0; sy < ny; sy++)
-                            memcpy(&auxp[ao + 16 + 8 * sy * nx], bdata + 16 + 8 * ((oy / 8 + sy) * gw + ox / 8), 8 * nx);
+                            memcpy(&P.auxp[ao + 16 + 8 * sy * nx], bdata + 16 + 8 * ((oy / 8 + sy) * gw + ox / 8), 8 * nx);
                     } else if (b.kind == DGPU_PRED_INTER_OBMC) {   // the laps overlapping the unit
                         const int n = *(const int32_t *)bdata;
                         const ObmcBlockLap *lb = (const ObmcBlockLap *)(bdata + 16);
@@ -636,17 +753,17 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                             q.mask_off = (uint8_t)(e.mask_off + (e.dir ? ox : oy));
                             ents.push_back(q);
                         }
-                        ao = aux_alloc(16 + 16 * ents.size());
+                        ao = P.aux_alloc(16 + 16 * ents.size());
                         const int32_t ne = (int32_t)ents.size();
-                        memset(&auxp[ao], 0, 16);
-                        memcpy(&auxp[ao], &ne, 4);
-                        if (ne) memcpy(&auxp[ao + 16], ents.data(), 16 * ents.size());
+                        memset(&P.auxp[ao], 0, 16);
+                        memcpy(&P.auxp[ao], &ne, 4);
+                        if (ne) memcpy(&P.auxp[ao + 16], ents.data(), 16 * ents.size());
                     } else {   // INTER_SCALED: the unit's integer position and phase (running sums)
                         const int n = *(const int32_t *)bdata;
                         const ScaledBlockRef *sb = (const ScaledBlockRef *)(bdata + 16);
-                        ao = aux_alloc(16 + 16 * (size_t)n);
-                        memset(&auxp[ao], 0, 16 + 16 * (size_t)n);
-                        memcpy(&auxp[ao], &n, 4);
+                        ao = P.aux_alloc(16 + 16 * (size_t)n);
+                        memset(&P.auxp[ao], 0, 16 + 16 * (size_t)n);
+                        memcpy(&P.auxp[ao], &n, 4);
                         for (int k = 0; k < n; k++) {
                             const int rs = (int)(ref[b.ref[k]][p].stride / bpp);
                             const int px_ = sb[k].mx + ox * sb[k].dx, py_ = sb[k].my + oy * sb[k].dy;
@@ -655,12 +772,12 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                             q.mx = (uint16_t)(px_ & 1023), q.my = (uint16_t)(py_ & 1023);
                             q.dx = sb[k].dx, q.dy = sb[k].dy;
                             q.pad_ = 0;
-                            memcpy(&auxp[ao + 16 + 16 * k], &q, 16);
+                            memcpy(&P.auxp[ao + 16 + 16 * k], &q, 16);
                         }
                         if (n == 1) u.p.inter.weight = 0;
                     }
-                    xunits.push_back(u);
-                    xaux.push_back(ao);
+                    P.xunits.push_back(u);
+                    P.xaux.push_back(ao);
                 }
         }
         // the transform cells; an INTER_INTRA block first gets one cell for
@@ -674,9 +791,10 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 const bool iic = k < 0;
                 const int ox = iic ? 0 : (k % ncx) * t.w, oy = iic ? 0 : (k / ncx) * t.h;
                 const int ctw = iic ? b.w : t.w, cth = iic ? b.h : t.h, ctw4 = ctw / 4, cth4 = cth / 4;
-                cells.emplace_back();   // built in place (popped again when skipped)
-                Unit &c = cells.back();
+                P.cells.emplace_back();   // built in place (popped again when skipped)
+                Unit &c = P.cells.back();
                 memset(&c, 0, sizeof(c));
+                uint8_t fix = 0;   // the part-local offsets this cell holds (CellPart::F_*)
                 const int ux = b.x + ox, uy = b.y + oy, x4 = ux / 4, y4 = uy / 4;
                 Dav1dGpuUnit &u = c.u;
                 u.dst_off = uy * ds_px + ux;
@@ -692,11 +810,11 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     u.nzw = (uint8_t)q.nzw;
                     u.nzh = (uint8_t)q.nzh;
                     u.coef_off = (int32_t)q.coef;   // pool offset fixed below
-                    n_res_used++;
+                    P.n_res_used++;
                 } else if (ri >= 0) {
                     return -1;   // a residual whose size differs from its block's transforms
                 } else if (pre || (iib && !iic)) {
-                    cells.pop_back();
+                    P.cells.pop_back();
                     continue;   // predicted elsewhere, nothing to add
                 }
                 Dav1dGpuIntraEdge &e = c.rec;
@@ -711,11 +829,12 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     c.sortmode = 0;
                 } else if (pal) {   // pal_pred: palette, then the unit's rows of the index map
                     const int bw2 = b.w / 2;
-                    c.aux = aux_alloc(16 + (size_t)(t.w / 2) * t.h);
-                    memset(&auxp[c.aux], 0, 16);
-                    memcpy(&auxp[c.aux], bdata, 8 * (size_t)bpp);
+                    c.aux = P.aux_alloc(16 + (size_t)(t.w / 2) * t.h);
+                    fix |= CellPart::F_AUX;
+                    memset(&P.auxp[c.aux], 0, 16);
+                    memcpy(&P.auxp[c.aux], bdata, 8 * (size_t)bpp);
                     for (int yy = 0; yy < t.h; yy++)
-                        memcpy(&auxp[c.aux + 16 + yy * (t.w / 2)], bdata + 8 * bpp + (size_t)(oy + yy) * bw2 + ox / 2,
+                        memcpy(&P.auxp[c.aux + 16 + yy * (t.w / 2)], bdata + 8 * bpp + (size_t)(oy + yy) * bw2 + ox / 2,
                                t.w / 2);
                     c.sortmode = 15;
                 } else if (inter || iic) {
@@ -742,27 +861,32 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                             const bool inside = ix - 3 >= 0 && iy - 3 >= 0 && ix + ctw + 4 <= rw &&
                                                 iy + cth + 4 <= rh && (iy + cth + 4 < rh || (ix + ctw + 4) * bpp + 16 <= rs * bpp);
                             if (!inside) {
-                                r->emu.push_back(EmuJob{ix - 3, iy - 3, emu_rows, (uint8_t)(ctw + 7), (uint8_t)(cth + 7),
+                                P.emu.push_back(EmuJob{ix - 3, iy - 3, P.emu_rows, (uint8_t)(ctw + 7), (uint8_t)(cth + 7),
                                                         (uint8_t)rr, (uint8_t)p});
-                                u.p.inter.src_off[k] = (emu_rows + 3) * kEmuStride + 3;
+                                u.p.inter.src_off[k] = (P.emu_rows + 3) * kEmuStride + 3;
+                                fix |= k ? CellPart::F_EMU1 : CellPart::F_EMU0;
                                 u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
-                                emu_rows += cth + 7;
+                                P.emu_rows += cth + 7;
                             }
                         }
                     }
                     u.p.inter.filter2d = b.filter2d;
                     u.p.inter.weight = b.kind == DGPU_PRED_INTER_WAVG ? b.weight : 0;
-                    if (b.kind == DGPU_PRED_INTER_MASK) c.aux = mask_base + oy * mask_stride + ox;
+                    if (b.kind == DGPU_PRED_INTER_MASK) {
+                        c.aux = mask_base + oy * mask_stride + ox;
+                        fix |= CellPart::F_AUX;
+                    }
                     c.sortmode = b.filter2d;
                     if (iic) {   // the intra half: edges gathered by the wavefront like an INTRA unit's
                         // record: edge_off (unused when gathered), mode, angle, then the mask offset
-                        c.aux = aux_alloc(16 + (size_t)b.w * b.h);
+                        c.aux = P.aux_alloc(16 + (size_t)b.w * b.h);
+                        fix |= CellPart::F_AUX | CellPart::F_IIREC;
                         const int32_t moff = c.aux + 16, zero = 0;
-                        memset(&auxp[c.aux], 0, 16);
-                        memcpy(&auxp[c.aux], &zero, 4);
-                        auxp[c.aux + 4] = b.mode;
-                        memcpy(&auxp[c.aux + 8], &moff, 4);
-                        memcpy(&auxp[moff], bdata, (size_t)b.w * b.h);
+                        memset(&P.auxp[c.aux], 0, 16);
+                        memcpy(&P.auxp[c.aux], &zero, 4);
+                        P.auxp[c.aux + 4] = b.mode;
+                        memcpy(&P.auxp[c.aux + 8], &moff, 4);
+                        memcpy(&P.auxp[moff], bdata, (size_t)b.w * b.h);
                         // prepare_intra_edges with no edge flags, no edge filter, angle 0 (:1551-1566)
                         e.mode = b.mode;
                         e.angle = 0;
@@ -791,79 +915,198 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         u.p.cfl.luma_off = (2 * uy) * (int)(dst[0].stride / bpp) + 2 * ux;
                     }
                     e.flags = (uint8_t)fl;
-                    u.p.intra.edge_off = (int32_t)(edge_px + 2 * t.h);   // CFL: the same field
-                    edge_px += 2 * t.h + 2 * t.w + 1;
+                    u.p.intra.edge_off = (int32_t)(P.edge_px + 2 * t.h);   // CFL: the same field
+                    P.edge_px += 2 * t.h + 2 * t.w + 1;
+                    fix |= CellPart::F_EDGE;
                     const int m = remap_mode(e.mode, e.angle, hl, ht);
                     nd = kNeeds[m];
                     c.sortmode = 16 + m;
                 }
-                // level: one above every pixel the edges (or CfL luma) read;
-                // producers: the cells that wrote those pixels
-                const int W4 = e.w4, H4 = e.h4;
-                const size_t p0 = prod.size();
-                int d = -1;
-                // a pixel no cell of this flush wrote came from an earlier
-                // flush on the same stream: no producer, level 0 for it
-                auto cell = [&](int cx, int cy) {
-                    const LvOwn m = lvown[p][(size_t)cy * w4p + cx];
-                    if (m.own < cell_base) return;   // an earlier flush's pixel: level -1, no producer
+                // the level pass (below) reads the cell's geometry and edge needs
+                P.jobs.emplace_back();
+                LvJob &j = P.jobs.back();
+                j.x4 = (int16_t)x4;
+                j.y4 = (int16_t)y4;
+                j.W4 = e.w4;
+                j.H4 = e.h4;
+                j.p = (uint8_t)p;
+                j.cw4 = (uint8_t)ctw4;
+                j.ch4 = (uint8_t)cth4;
+                j.nd = (uint8_t)nd;
+                j.fl = (uint8_t)((hl ? LvJob::HL : 0) | (ht ? LvJob::HT : 0) |
+                                 ((e.flags & DGPU_IE_TOP_HAS_RIGHT) ? LvJob::TR : 0) |
+                                 ((e.flags & DGPU_IE_LEFT_HAS_BOTTOM) ? LvJob::BL : 0) | (cfl ? LvJob::CFL : 0) |
+                                 ((iib && !iic) ? LvJob::IIRES : 0));
+                j.fix = fix;
+            }
+        return 0;
+    };
+
+    if (!r->pool) r->pool.reset(new Pool((int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()))));
+    const size_t nb = r->blocks.size();
+    const int nt = nb < 4096 ? 1 : r->pool->size();
+    if (r->parts.size() < (size_t)nt) r->parts.resize(nt);
+    std::vector<size_t> bcut(nt + 1, nb);   // part boundaries on luma blocks (a block's chroma stays with it)
+    bcut[0] = 0;
+    for (int t = 1; t < nt; t++) {
+        size_t c = std::max(bcut[t - 1], nb * t / nt);
+        while (c < nb && r->blocks[c].plane != 0) c++;
+        bcut[t] = c;
+    }
+    auto run_part = [&](int t) {
+        CellPart &P = r->parts[t];
+        P.clear();
+        P.cells.reserve((size_t)((double)ncells * (bcut[t + 1] - bcut[t]) / std::max<size_t>(nb, 1)) + 64);
+        for (size_t bi = bcut[t]; bi < bcut[t + 1] && !P.err; bi++) P.err = build(bi, P);
+    };
+    r->pool->run(nt, run_part);
+    // join: part bases (the aux pool keeps its 16-byte alignment rule)
+    size_t n_cells = 0, n_x = 0, n_emu = 0, aux_end = 0, n_res_used = 0;
+    std::vector<size_t> cb0(nt), xb0(nt), eb0(nt), ab0(nt), pb0(nt);
+    std::vector<int32_t> erow0(nt);
+    int32_t emu_rows = 0;
+    size_t edge_px = 0;
+    for (int t = 0; t < nt; t++) {
+        const CellPart &P = r->parts[t];
+        if (P.err) return P.err;
+        cb0[t] = n_cells;
+        xb0[t] = n_x;
+        eb0[t] = n_emu;
+        erow0[t] = emu_rows;
+        pb0[t] = edge_px;
+        ab0[t] = P.auxp.empty() ? aux_end : (aux_end + 15) & ~(size_t)15;
+        if (!P.auxp.empty()) aux_end = ab0[t] + P.auxp.size();
+        n_cells += P.cells.size();
+        n_x += P.xunits.size();
+        n_emu += P.emu.size();
+        emu_rows += P.emu_rows;
+        edge_px += P.edge_px;
+        n_res_used += P.n_res_used;
+    }
+    if (n_res_used != r->residuals.size()) return -1;   // a residual outside every block
+    cells.resize(n_cells);
+    r->jobs.resize(n_cells);
+    auxp.resize(aux_end);
+    r->emu.resize(n_emu);
+    xunits.resize(n_x);
+    xaux.resize(n_x);
+    auto join_part = [&](int t) {
+        const CellPart &P = r->parts[t];
+        const int32_t ab = (int32_t)ab0[t], er = erow0[t], pb = (int32_t)pb0[t];
+        if (!P.auxp.empty()) memcpy(&auxp[ab0[t]], P.auxp.data(), P.auxp.size());
+        for (size_t i = 0; i < P.cells.size(); i++) {
+            Unit c = P.cells[i];
+            const uint8_t f = P.jobs[i].fix;
+            if (f & CellPart::F_AUX) c.aux += ab;
+            if (f & CellPart::F_EDGE) c.u.p.intra.edge_off += pb;
+            if (f & CellPart::F_EMU0) c.u.p.inter.src_off[0] += er * kEmuStride;
+            if (f & CellPart::F_EMU1) c.u.p.inter.src_off[1] += er * kEmuStride;
+            if (f & CellPart::F_IIREC) {   // the inter-intra record's mask offset
+                int32_t mo;
+                memcpy(&mo, &auxp[(size_t)c.aux + 8], 4);
+                mo += ab;
+                memcpy(&auxp[(size_t)c.aux + 8], &mo, 4);
+            }
+            cells[cb0[t] + i] = c;
+            r->jobs[cb0[t] + i] = P.jobs[i];
+        }
+        for (size_t i = 0; i < P.emu.size(); i++) {
+            EmuJob e = P.emu[i];
+            e.r0 += er;
+            r->emu[eb0[t] + i] = e;
+        }
+        for (size_t i = 0; i < P.xunits.size(); i++) {
+            xunits[xb0[t] + i] = P.xunits[i];
+            xaux[xb0[t] + i] = P.xaux[i] + ab;
+        }
+    };
+    r->pool->run(nt, join_part);
+    lap("cells");
+    // levels and producers, in decode order: a cell sits one level above
+    // every pixel its edges (or CfL luma, or an inter-intra residual's
+    // prediction) read; its producers are the cells that wrote them.  A
+    // pixel no cell of this flush wrote came from an earlier flush on the
+    // same stream: no producer, level 0 for it
+    prod_start.assign(1, 0);
+    prod.clear();
+    prod_start.reserve(n_cells + 1);
+    for (size_t ci = 0; ci < n_cells; ci++) {
+        const LvJob &j = r->jobs[ci];
+        const int p = j.p, w4p = mw[p], x4 = j.x4, y4 = j.y4, cw4 = j.cw4, ch4 = j.ch4, W4 = j.W4, H4 = j.H4;
+        const int nd = j.nd;
+        const bool hl = j.fl & LvJob::HL, ht = j.fl & LvJob::HT;
+        const LvOwn *mp = lvown[p].data();
+        const size_t p0 = prod.size();
+        int d = -1;
+        auto cell = [&](int cx, int cy) {
+            const LvOwn m = mp[(size_t)cy * w4p + cx];
+            if (m.own < cell_base) return;   // an earlier flush's pixel: level -1, no producer
+            d = std::max(d, m.lv);
+            const int32_t o = m.own - cell_base;
+            if (prod.size() == p0 || prod.back() != o) prod.push_back(o);
+        };
+        if (nd & 1) {
+            if (hl) {
+                for (int q = y4; q < std::min(y4 + ch4, H4); q++) cell(x4 - 1, q);
+                if ((nd & 16) && y4 + ch4 < H4 && (j.fl & LvJob::BL))
+                    for (int q = y4 + ch4; q < std::min(y4 + 2 * ch4, H4); q++) cell(x4 - 1, q);
+            } else if (ht) {
+                cell(x4, y4 - 1);
+            }
+        }
+        if (nd & 2) {
+            if (ht) {
+                for (int q = x4; q < std::min(x4 + cw4, W4); q++) cell(q, y4 - 1);
+                if ((nd & 8) && x4 + cw4 < W4 && (j.fl & LvJob::TR))
+                    for (int q = x4 + cw4; q < std::min(x4 + 2 * cw4, W4); q++) cell(q, y4 - 1);
+            } else if (hl) {
+                cell(x4 - 1, y4);
+            }
+        }
+        if (j.fl & LvJob::IIRES)   // the residual reads the block's inter-intra prediction
+            for (int cy = y4; cy < y4 + ch4; cy++)
+                for (int cx = x4; cx < x4 + cw4; cx++) cell(cx, cy);
+        if (nd & 4) {
+            if (hl && ht) cell(x4 - 1, y4 - 1);
+            else if (hl) cell(x4 - 1, y4);
+            else if (ht) cell(x4, y4 - 1);
+        }
+        if (j.fl & LvJob::CFL) {
+            const int lw4 = mw[0];
+            const LvOwn *ml = lvown[0].data();
+            for (int cy = 2 * y4; cy < 2 * (y4 + ch4); cy++)
+                for (int cx = 2 * x4; cx < 2 * (x4 + cw4); cx++) {
+                    const LvOwn m = ml[(size_t)cy * lw4 + cx];
+                    if (m.own < cell_base) continue;   // luma of an earlier flush: no producer
                     d = std::max(d, m.lv);
                     const int32_t o = m.own - cell_base;
                     if (prod.size() == p0 || prod.back() != o) prod.push_back(o);
-                };
-                if (nd & 1) {
-                    if (hl) {
-                        for (int q = y4; q < std::min(y4 + cth4, H4); q++) cell(x4 - 1, q);
-                        if ((nd & 16) && y4 + cth4 < H4 && (e.flags & DGPU_IE_LEFT_HAS_BOTTOM))
-                            for (int q = y4 + cth4; q < std::min(y4 + 2 * cth4, H4); q++) cell(x4 - 1, q);
-                    } else if (ht) {
-                        cell(x4, y4 - 1);
-                    }
                 }
-                if (nd & 2) {
-                    if (ht) {
-                        for (int q = x4; q < std::min(x4 + ctw4, W4); q++) cell(q, y4 - 1);
-                        if ((nd & 8) && x4 + ctw4 < W4 && (e.flags & DGPU_IE_TOP_HAS_RIGHT))
-                            for (int q = x4 + ctw4; q < std::min(x4 + 2 * ctw4, W4); q++) cell(q, y4 - 1);
-                    } else if (hl) {
-                        cell(x4 - 1, y4);
-                    }
-                }
-                if (iib && !iic)   // the residual reads the block's inter-intra prediction
-                    for (int cy = y4; cy < y4 + cth4; cy++)
-                        for (int cx = x4; cx < x4 + ctw4; cx++) cell(cx, cy);
-                if (nd & 4) {
-                    if (hl && ht) cell(x4 - 1, y4 - 1);
-                    else if (hl) cell(x4 - 1, y4);
-                    else if (ht) cell(x4, y4 - 1);
-                }
-                if (cfl) {
-                    const int lw4 = mw[0];
-                    for (int cy = 2 * y4; cy < 2 * (y4 + th4); cy++)
-                        for (int cx = 2 * x4; cx < 2 * (x4 + tw4); cx++) {
-                            const LvOwn m = lvown[0][(size_t)cy * lw4 + cx];
-                            if (m.own < cell_base) continue;   // luma of an earlier flush: no producer
-                            d = std::max(d, m.lv);
-                            const int32_t o = m.own - cell_base;
-                            if (prod.size() == p0 || prod.back() != o) prod.push_back(o);
-                        }
-                }
-                if (prod.size() - p0 > 1) {   // duplicate-free
-                    std::sort(prod.begin() + p0, prod.end());
-                    prod.erase(std::unique(prod.begin() + p0, prod.end()), prod.end());
-                }
-                prod_start.push_back((int32_t)prod.size());
-                c.level = d + 1;
-                const int ci = (int)cells.size() - 1;
-                for (int cy = y4; cy < y4 + cth4; cy++)
-                    for (int cx = x4; cx < x4 + ctw4; cx++) {
-                        lvown[p][(size_t)cy * w4p + cx] = LvOwn{c.level, cell_base + ci};
-                    }
-                (void)0;   // (c lives in cells already)
+        }
+        if (prod.size() - p0 > 1) {   // sorted, duplicate-free (lists are short: insertion sort)
+            int32_t *q = prod.data() + p0;
+            const size_t m = prod.size() - p0;
+            size_t u = 1;
+            for (size_t a = 1; a < m; a++) {
+                const int32_t v = q[a];
+                size_t b = u;
+                while (b > 0 && q[b - 1] > v) b--;
+                if (b > 0 && q[b - 1] == v) continue;   // a duplicate
+                for (size_t c = u; c > b; c--) q[c] = q[c - 1];
+                q[b] = v;
+                u++;
             }
+            prod.resize(p0 + u);
+        }
+        prod_start.push_back((int32_t)prod.size());
+        const int lv = d + 1;
+        cells[ci].level = lv;
+        LvOwn *wp = lvown[p].data();
+        const LvOwn v{lv, cell_base + (int32_t)ci};
+        for (int cy = y4; cy < y4 + ch4; cy++)
+            for (int cx = x4; cx < x4 + cw4; cx++) wp[(size_t)cy * w4p + cx] = v;
     }
-    if (n_res_used != r->residuals.size()) return -1;   // a residual outside every block
-    lap("cells");
+    lap("levels");
     const int n = (int)cells.size();
 
     // 4. level order, size classes inside a level, then kind / mode / type:
@@ -871,6 +1114,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     //    (stable: equal keys stay in decode order).  Key: level | tx (5) |
     //    pred (4) | mode (6) | type (5, NO_RESIDUAL last)
     if (n >= (1 << 21)) return -1;
+    const int nthreads = r->pool->size();
     std::vector<uint64_t> &keys = r->keys;
     keys.resize(n);
     int max_level = 0;
@@ -885,7 +1129,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     {
         int lb = 0;
         while ((1 << lb) <= max_level) lb++;
-        radix_sort(keys, r->keys_tmp, 21, 21 + 20 + lb);
+        radix_sort(keys, r->keys_tmp, 21, 21 + 20 + lb, *r->pool);
     }
     lap("sort");
     const int n_levels = n ? max_level + 1 : 0;
@@ -952,28 +1196,27 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         }
     }
     if (bp) memcpy(img + o_p, r->auxp.data(), bp);
-    {
-        const int nt = n < 32768 ? 1 : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    {   // in rank order: the image is written sequentially, the cells read by index
+        const int nt = n < 32768 ? 1 : nthreads;
+        int32_t *deps = r->deps.data();
+        const int32_t *ds = r->dep_start.data();
         auto work = [&](int t) {
-            const int c0 = (int)((int64_t)n * t / nt), c1 = (int)((int64_t)n * (t + 1) / nt);
-            for (int ci = c0; ci < c1; ci++) {
+            const int i0 = (int)((int64_t)n * t / nt), i1 = (int)((int64_t)n * (t + 1) / nt);
+            for (int i = i0; i < i1; i++) {
+                const int ci = (int)(keys[i] & ((1u << 21) - 1));
                 const Unit &c = cells[ci];
-                const int i = rank[ci];
                 hu[i] = c.u;   // coef_off / edge_off are decode-order pool offsets
                 ha[i] = c.aux;
                 Dav1dGpuIntraEdge e = c.rec;
                 e.unit = i;
                 hr[i] = e;
-                int32_t *o = &r->deps[r->dep_start[i]];
+                int32_t *o = deps + ds[i];
                 for (int k = prod_start[ci]; k < prod_start[ci + 1]; k++) *o++ = rank[prod[k]];
             }
             const size_t b0 = bc * t / nt, b1 = bc * (t + 1) / nt;
             if (b1 > b0) memcpy(img + o_c + b0, r->coefb.data() + b0, b1 - b0);
         };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; t++) th.emplace_back(work, t);
-        work(0);
-        for (auto &x : th) x.join();
+        r->pool->run(nt, work);
         if (be) memcpy(img + o_e, r->emu.data(), be);
     }
     lap("fill");

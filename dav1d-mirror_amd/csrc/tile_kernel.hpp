@@ -138,7 +138,7 @@ __device__ __forceinline__ void tile_row(const typename Px<BPC>::coef *cs, int n
         if (x < SW && x < nzw) v = cs[x * nzh + r];
         c[x] = rect2 ? r8s(v) : v;
     }
-    tx1d<W, 1>(kind, c, rc);
+    tx1d<W, 1, BPC == 8>(kind, c, rc);
     const int rnd = (1 << shift) >> 1;
 #pragma unroll
     for (int x = 0; x < W; x++) c[x] = cc((c[x] + rnd) >> shift);
@@ -160,7 +160,7 @@ __device__ __forceinline__ void tile_col(typename TAcc<BPC>::T *acol, int nzh, i
     int col[H];
 #pragma unroll
     for (int y = 0; y < H; y++) col[y] = (y < SH && y < nzh) ? (int)acol[y * S] : 0;
-    tx1d<H, 1>(kind, col, cc);
+    tx1d<H, 1, BPC == 8>(kind, col, cc);
 #pragma unroll
     for (int y = 0; y < H; y++) acol[y * S] = (col[y] + 8) >> 4;
 }

@@ -15,7 +15,7 @@ build() {
     done
     wait
     local objs=""
-    for s in runtime mc ipred itx recon8 recon16 tile8 tile16 edges recon_ie8 recon_ie16 recorder grain cdef lpf lr; do
+    for s in runtime mc ipred itx recon8 recon16 tile8 tile16 edges recon_ie8 recon_ie16 recorder grain cdef lpf lr picture; do
         if [ -f build/var/$name.$s.o ] && [[ " ${TUS:-recon8 recon16} " == *" $s "* ]]; then objs="$objs build/var/$name.$s.o"; else objs="$objs build/$s.o"; fi
     done
     $HIPCC $F -shared -o libdav1d_gpu.$name.so $objs build/stamp.o
@@ -23,6 +23,7 @@ build() {
 for v in ${VARIANTS:-nomc noitx nointra}; do
     case $v in
         vodd) TUS=recon8 build vodd -DDGPU_VODD_ALIGN=1 ;;
+        nod2) TUS=recon8 build nod2 -DDGPU_ITX_D2=0 ;;
         salu200) build salu200 -DDGPU_PAD_SALU=200 ;;
         al16) build al16 -DDGPU_ALIGNED_ROWS16=1 ;;
         ch16) build ch16 -DDGPU_CH16=1 ;;

@@ -41,6 +41,12 @@ for s in $STEPS; do
         timeout -k 10 800 bash tools/class_prof.sh "$TAG" > "$O/cls.log" 2>&1 || { echo "cls failed" >&2; tail -20 "$O/cls.log"; exit 1; }
         cat "$O/cls.log" | tail -60
         ;;
+    rec)
+        echo "[it] rec" >&2
+        timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 --no-families --no-configs --no-tiles --no-intra \
+            --no-grain --no-cdef --no-lpf --no-lr > "$O/rec.json" 2> "$O/rec.err" || { echo "rec failed" >&2; tail -20 "$O/rec.err"; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/rec.json')); print(json.dumps(d['recorder']))"
+        ;;
     var)
         for v in base $VARIANTS; do
             if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
