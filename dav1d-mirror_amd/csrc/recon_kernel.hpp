@@ -160,9 +160,19 @@ __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 // than the 1-D transform passes can use (max(W, min(H, 32)) lines), 2..64;
 // 32x32 takes a whole wave so its LDS slot (9 KB) does not set the budget
 // of the large group
+#ifndef DGPU_TALL_LANES
+#define DGPU_TALL_LANES 1
+#endif
 __host__ __device__ constexpr int lanes_per_unit(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
     if (w * h >= 1024) return 64;
+    // tall classes: as few lanes as the column pass has lines (or half as
+    // many for 8x32), so the column transforms leave no lane idle, within
+    // the 8 KB-per-wave LDS budget of the main group (round 3; the rule
+    // below gives 16 / 8 / 32 lanes, half of them idle in the column pass)
+    if (DGPU_TALL_LANES && w == 8 && h == 16) return 8;
+    if (DGPU_TALL_LANES && w == 4 && h == 16) return 4;
+    if (DGPU_TALL_LANES && w == 8 && h == 32) return 16;
     return cmin(cmax(cmin(w * h / 8, cmax(w, cmin(h, 32))), 2), 64);
 }
 // class groups, each its own kernel with its own register / LDS budget:

@@ -89,20 +89,52 @@ struct DevBuf {
     }
 };
 
-struct PinnedBuf {   // page-locked staging, so the uploads do not wait for the stream
+// page-locked staging, so the uploads do not wait for the stream.
+// DAV1D_GPU_REC_PIN (tuning): "default" hipHostMalloc, "nc" non-coherent
+// (CPU-cached) hipHostMalloc, "reg" (the default) hipHostRegister of an
+// ordinary aligned allocation: host memory the CPU caches like any other,
+// which the fill writes at memory speed
+static int pin_mode() {
+    static const int m = [] {
+        const char *e = getenv("DAV1D_GPU_REC_PIN");
+        if (!e) return 2;
+        return !strcmp(e, "default") ? 0 : !strcmp(e, "nc") ? 1 : 2;
+    }();
+    return m;
+}
+struct PinnedBuf {
     void *p = nullptr;
     size_t cap = 0;
+    int mode = -1;
     int grow(size_t n) {
         if (n <= cap) return 0;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return -1;
+        release();
+        mode = pin_mode();
+        if (mode == 2) {
+            const size_t sz = (n + 4095) & ~(size_t)4095;
+            void *q = nullptr;
+            if (posix_memalign(&q, 4096, sz)) return -1;
+            if (hipHostRegister(q, sz, hipHostRegisterDefault) != hipSuccess) {
+                free(q);
+                return -1;
+            }
+            p = q;
+        } else if (hipHostMalloc(&p, n, mode ? hipHostMallocNonCoherent : hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return -1;
+        }
         cap = n;
         return 0;
     }
     void release() {
-        if (p) (void)hipHostFree(p);
+        if (p) {
+            if (mode == 2) {
+                (void)hipHostUnregister(p);
+                free(p);
+            } else {
+                (void)hipHostFree(p);
+            }
+        }
         p = nullptr;
         cap = 0;
     }

@@ -367,7 +367,9 @@ typedef struct Dav1dGpuUnit {
 typedef struct Dav1dGpuPlane {
     void    *data;        /* device pointer to pixel (0,0); dst planes must be
                              16-byte aligned with a 16-byte multiple stride */
-    int64_t  stride;      /* bytes                                           */
+    int64_t  stride;      /* bytes; the unit batch and the intra wavefront
+                             take strides in [0, 2^23) (24-bit row offsets),
+                             else -4                                         */
     int32_t  w, h;        /* visible size (reference reads are clamped)      */
 } Dav1dGpuPlane;
 

@@ -24,6 +24,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
     case $v in
         vodd) TUS=recon8 build vodd -DDGPU_VODD_ALIGN=1 ;;
         nod2) TUS=recon8 build nod2 -DDGPU_ITX_D2=0 ;;
+        notall) TUS=recon8 build notall -DDGPU_TALL_LANES=0 ;;
         salu200) build salu200 -DDGPU_PAD_SALU=200 ;;
         al16) build al16 -DDGPU_ALIGNED_ROWS16=1 ;;
         ch16) build ch16 -DDGPU_CH16=1 ;;
