@@ -71,6 +71,13 @@ def test_recon_batch_validation(pkg):
         b = batch(5)
         b.dst[0].data = 8     # not 16-byte aligned
         assert fn(ctypes.byref(b), None) == -4
+        b = batch(5)
+        b.dst[1].stride = 1 << 23   # row offsets are 24-bit multiplies: strides in [0, 2^23)
+        assert fn(ctypes.byref(b), None) == -4
+        b = batch(5)
+        b.ref[0][0].data = 4096
+        b.ref[0][0].stride = -4096   # negative reference strides too
+        assert fn(ctypes.byref(b), None) == -4
     assert L.dav1d_gpu_recon_lds_bytes(8, 3) > L.dav1d_gpu_recon_lds_bytes(8, 2) - 65536
     assert L.dav1d_gpu_recon_lds_bytes(8, 9) == -1
 
