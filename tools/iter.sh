@@ -55,6 +55,16 @@ for s in $STEPS; do
             python3 -c "import json; d=json.load(open('$O/recpin_$m.json'))['recorder']; print('$m', d['flush_host_ms'], d['flush_device_ms'], d['frame_threads']['flush_host_ms_per_frame'], d['bit_exact_vs_oracle'], d['frame_threads']['bit_exact_vs_oracle'])"
         done
         ;;
+    intra)   # the intra wavefront leg for the product build and each of $IVARIANTS
+        for v in base $IVARIANTS; do
+            if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
+            timeout -k 10 400 python3 bench.py --no-cpu --steps 5 --warmup 1 --no-families --no-configs --no-tiles \
+                --no-recorder --no-grain --no-cdef --no-lpf --no-lr > "$O/intra_$v.json" 2> "$O/intra_$v.err" \
+                || { echo "intra $v failed" >&2; tail -5 "$O/intra_$v.err"; exit 1; }
+            python3 -c "import json; d=json.load(open('$O/intra_$v.json'))['intra_wavefront']; print('$v', {k: (x['ms_per_frame'], x['us_per_level'], x['bit_exact_vs_oracle']) for k, x in d.items()})"
+        done
+        unset DAV1D_GPU_LIB_VARIANT
+        ;;
     var)
         for v in base $VARIANTS; do
             if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
