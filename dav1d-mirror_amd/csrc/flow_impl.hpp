@@ -132,7 +132,13 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
                 }
             }
             if (!ok && lane == 0) __hip_atomic_store(&f.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (nd && !DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            // DGPU_FLOW_SC1: every load of a producer's bytes is an sc1 load, so
+            // no L1 invalidate; the wavefront-scope fence only keeps the
+            // compiler from hoisting them above the poll
+            if (nd && !DGPU_FLOW_NOFENCE) {
+                if (DGPU_FLOW_SC1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
         } else if (level > 0) {
             int ok = 1;
             if (lane == 0) {
@@ -153,7 +159,10 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
             }
             __builtin_amdgcn_wave_barrier();
             // the previous levels' picture / top_edge stores are visible from here
-            if (!DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (!DGPU_FLOW_NOFENCE) {
+                if (DGPU_FLOW_SC1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
         }
         if constexpr (DGPU_FLOW_TRACE) tr1 = __builtin_amdgcn_s_memrealtime();
     };
@@ -162,9 +171,10 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
         __builtin_amdgcn_s_waitcnt(0);
         tr2 = __builtin_amdgcn_s_memrealtime();
     }
-    // this task's stores reach agent scope before it is counted
-    if (!DGPU_FLOW_NOFENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    else __builtin_amdgcn_s_waitcnt(0);
+    // this task's stores reach agent scope before it is counted (SC1: they
+    // are write-through, so draining them is the release)
+    if (DGPU_FLOW_SC1 || DGPU_FLOW_NOFENCE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (f.dep_start) {   // (all lanes are live again here)
         for (int i = lane; i < count; i += 64)
             __hip_atomic_store(&f.done[first + i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

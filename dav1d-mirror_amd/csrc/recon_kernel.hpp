@@ -374,6 +374,22 @@ template <typename T> __device__ __forceinline__ T gld(const void *p) {
 template <typename T> __device__ __forceinline__ void gst(void *p, T v) {
     *(__attribute__((address_space(1))) T *)p = v;
 }
+// The intra wavefront's acquire-free hand-off (DGPU_FLOW_SC1, flow_impl.hpp):
+// in GATHER builds every picture / top_edge store is write-through (sc1) and
+// every load of those bytes an sc1 load, the MI355X guide's "Valid forms"
+// row 1 (producer: sc1 stores, vmcnt(0), agent-scope flag; consumer: sc1
+// poll, sc1 loads, no buffer_inv).  Off by default: kept behind the flag
+// until measured and validated under load.
+#ifndef DGPU_FLOW_SC1
+#define DGPU_FLOW_SC1 0
+#endif
+template <typename T> __device__ __forceinline__ void st_sc1(void *p, T v) {
+    __hip_atomic_store((__attribute__((address_space(1))) T *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T> __device__ __forceinline__ T ld_sc1(const void *p) {
+    return __hip_atomic_load((const __attribute__((address_space(1))) T *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ({hi, lo} >> 8s)[31:0]
 __device__ __forceinline__ uint32_t alb(uint32_t hi, uint32_t lo, int s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
@@ -946,11 +962,22 @@ __device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, cons
 
 // ------------------------------------------------------------------ cfl ---
 
+template <bool SC, typename P> __device__ __forceinline__ int cfl_px(const P *p) {
+    if constexpr (SC) return ie_px<true>(p);
+    else return gld<P>(p);
+}
+// 16 bytes as two 8-byte sc1 loads (the hand-off's access sizes)
+__device__ __forceinline__ u32x4 ld_sc1_x4(const void *p) {
+    const u32x2 a = __builtin_bit_cast(u32x2, ld_sc1<uint64_t>(p));
+    const u32x2 b = __builtin_bit_cast(u32x2, ld_sc1<uint64_t>(reinterpret_cast<const uint8_t *>(p) + 8));
+    return u32x4{a.x, a.y, b.x, b.y};
+}
+
 // Chroma-from-luma for one unit (the whole chroma block, square <= 32):
 // cfl_ac on the co-located luma (src/ipred_tmpl.c:657-703), then cfl_pred
 // with the DC of the edge array (:71-84, :103-218), task by task through
 // `emit`.  The 4:2:0 no-padding case sums luma pairs with packed dots.
-template <int BPC, int TX, typename P, typename Emit>
+template <int BPC, int TX, bool SC = false, typename P, typename Emit>
 __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGpuUnit &u, const P *tl, int16_t *fe,
                                           int l, int bdmax, Emit &emit) {
     using CL = Cls<TX>;
@@ -975,14 +1002,28 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
             for (int rr = 0; rr < 2; rr++) {
                 const P *r0 = yp + __mul24(4 * j + 2 * rr, ys) + 8 * q;
                 if constexpr (BPC == 8) {
-                    const u32x2 v0 = gld<u32x2a1>(r0), v1 = gld<u32x2a1>(r0 + ys);
+                    u32x2 v0, v1;
+                    if constexpr (SC) {   // 8-byte aligned (x4 luma columns, 16-byte strides)
+                        v0 = __builtin_bit_cast(u32x2, ld_sc1<uint64_t>(r0));
+                        v1 = __builtin_bit_cast(u32x2, ld_sc1<uint64_t>(r0 + ys));
+                    } else {
+                        v0 = gld<u32x2a1>(r0);
+                        v1 = gld<u32x2a1>(r0 + ys);
+                    }
                     // byte pairs summed over both rows: dot4 with 1-masks
                     ac[k][4 * rr + 0] = (int)__builtin_amdgcn_udot4(v1.x, 0x00000101u, __builtin_amdgcn_udot4(v0.x, 0x00000101u, 0, false), false) << 1;
                     ac[k][4 * rr + 1] = (int)__builtin_amdgcn_udot4(v1.x, 0x01010000u, __builtin_amdgcn_udot4(v0.x, 0x01010000u, 0, false), false) << 1;
                     ac[k][4 * rr + 2] = (int)__builtin_amdgcn_udot4(v1.y, 0x00000101u, __builtin_amdgcn_udot4(v0.y, 0x00000101u, 0, false), false) << 1;
                     ac[k][4 * rr + 3] = (int)__builtin_amdgcn_udot4(v1.y, 0x01010000u, __builtin_amdgcn_udot4(v0.y, 0x01010000u, 0, false), false) << 1;
                 } else {
-                    const u32x4a2 v0 = gld<u32x4a2>(r0), v1 = gld<u32x4a2>(r0 + ys);
+                    u32x4 v0, v1;
+                    if constexpr (SC) {   // 16-byte aligned
+                        v0 = ld_sc1_x4(r0);
+                        v1 = ld_sc1_x4(r0 + ys);
+                    } else {
+                        v0 = gld<u32x4a2>(r0);
+                        v1 = gld<u32x4a2>(r0 + ys);
+                    }
                     const uint32_t d0[4] = {v0.x, v0.y, v0.z, v0.w}, d1[4] = {v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
                     for (int i = 0; i < 4; i++)
@@ -994,11 +1035,11 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
             for (int i = 0; i < 8; i++) {
                 const int sx = min(4 * q + (i & 3), vw - 1), sy = min(2 * j + (i >> 2), vh - 1);
                 const P *p = yp + __mul24(sy << ssv, ys) + (sx << ssh);
-                int v = gld<P>(p);
-                if (ssh) v += gld<P>(p + 1);
+                int v = cfl_px<SC>(p);
+                if (ssh) v += cfl_px<SC>(p + 1);
                 if (ssv) {
-                    v += gld<P>(p + ys);
-                    if (ssh) v += gld<P>(p + ys + 1);
+                    v += cfl_px<SC>(p + ys);
+                    if (ssh) v += cfl_px<SC>(p + ys + 1);
                 }
                 ac[k][i] = v << acsh;
             }
@@ -1424,7 +1465,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             for (int k = 0; k < EPL; k++) {
                 const int i = -2 * H + l + k * G;
                 bool need;
-                ev[k] = (i <= 2 * W && ie_need(iec, i)) ? ie_value(iec, i, need) : -1;
+                ev[k] = (i <= 2 * W && ie_need(iec, i)) ? ie_value<P, DGPU_FLOW_SC1>(iec, i, need) : -1;
             }
 #pragma unroll
             for (int k = 0; k < EPL; k++)
@@ -1483,10 +1524,16 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #if DGPU_ABL_STORE   // cost-model probe: no picture stores (values kept alive)
             asm volatile("" ::"v"((uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24), "v"(row));
 #else
-            if constexpr (BPC == 8)
+            if constexpr (GATHER && DGPU_FLOW_SC1) {   // write-through: the wavefront's acquire-free hand-off
+                if constexpr (BPC == 8)
+                    st_sc1<uint32_t>(row, (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24);
+                else
+                    st_sc1<uint64_t>(row, (uint64_t)((uint32_t)o0 | o1 << 16) | (uint64_t)((uint32_t)o2 | (uint32_t)o3 << 16) << 32);
+            } else if constexpr (BPC == 8) {
                 gst<uint32_t>(row, (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24);
-            else
+            } else {
                 gst<u32x2>(row, u32x2{(uint32_t)o0 | o1 << 16, (uint32_t)o2 | (uint32_t)o3 << 16});
+            }
 #endif
         }
     };
@@ -1632,7 +1679,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             for (int k = 0; k < EPL; k++) {
                 const int i = -2 * H + l + k * G;
                 bool need;
-                ev[k] = (i <= 2 * W && ie_need(ie, i)) ? ie_value(ie, i, need) : -1;
+                ev[k] = (i <= 2 * W && ie_need(ie, i)) ? ie_value<P, DGPU_FLOW_SC1>(ie, i, need) : -1;
             }
 #pragma unroll
             for (int k = 0; k < EPL; k++)
@@ -1702,7 +1749,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             emit(j, q, pv);
         }
     } else if (NW && pred == DGPU_PRED_CFL) {
-        if constexpr (W == H && W <= 32) cfl_units<BPC, TX>(a, u, tl, fe, l, bdmax, emit);
+        if constexpr (W == H && W <= 32) cfl_units<BPC, TX, GATHER && DGPU_FLOW_SC1>(a, u, tl, fe, l, bdmax, emit);
     } else if (NW) {   // PRED_NONE: the residual goes onto the picture
 #pragma unroll
         for (int k = 0; k < TPL; k++) {
@@ -1711,7 +1758,11 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             const int j = t / QW, q = t % QW;
             int pv[8];
 #pragma unroll
-            for (int i = 0; i < 8; i++) pv[i] = gld<P>(dstp + __mul24(2 * j + (i >> 2), ds) + 4 * q + (i & 3));
+            for (int i = 0; i < 8; i++) {
+                const P *pp = dstp + __mul24(2 * j + (i >> 2), ds) + 4 * q + (i & 3);
+                if constexpr (GATHER && DGPU_FLOW_SC1) pv[i] = ie_px<true>(pp);
+                else pv[i] = gld<P>(pp);
+            }
             emit(j, q, pv);
         }
     }
@@ -1719,7 +1770,12 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         if (bkrow) {
             wave_sync();   // this wave's picture stores are visible to its own loads
             const P *last = dstp + (size_t)(H - 1) * ds;
-            for (int x = l; x < W; x += G) bkrow[x] = last[x];
+            if constexpr (DGPU_FLOW_SC1) {   // 4-pixel words, sc1 both ways (the hand-off's access sizes)
+                using WT = std::conditional_t<BPC == 8, uint32_t, uint64_t>;
+                for (int x = 4 * l; x < W; x += 4 * G) st_sc1<WT>(bkrow + x, ld_sc1<WT>(last + x));
+            } else {
+                for (int x = l; x < W; x += G) bkrow[x] = last[x];
+            }
         }
     }
     mark(8);

@@ -36,6 +36,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         ttrace) TUS=tile8 build ttrace -DDGPU_TILE_TRACE=1 ;;
         twpe2|twpe4|twpe5) TUS=tile8 build $v -DDGPU_TILE_WPE=${v#twpe} ;;
         fnofence) TUS="recon_ie8" build fnofence -DDGPU_FLOW_NOFENCE=1 ;;
+        fsc1) TUS="recon_ie8" build fsc1 -DDGPU_FLOW_SC1=1 ;;
         fsleep1) TUS="recon_ie8" build fsleep1 -DDGPU_FLOW_SLEEP=1 ;;
         ftrace) TUS="recon_ie8" build ftrace -DDGPU_FLOW_TRACE=1 ;;
         ftrace127) TUS="recon_ie8" build ftrace127 -DDGPU_FLOW_TRACE=1 -DDGPU_FLOW_SLEEP=127 ;;

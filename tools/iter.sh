@@ -65,6 +65,14 @@ for s in $STEPS; do
         done
         unset DAV1D_GPU_LIB_VARIANT
         ;;
+    vtests)   # the intra wavefront / recorder / chain GPU tests against each of $IVARIANTS
+        for v in $IVARIANTS; do
+            DAV1D_GPU_LIB_VARIANT=$v timeout -k 10 900 python3 -u -m pytest tests/test_gpu_intra_frame.py tests/test_gpu_recorder.py \
+                tests/test_gpu_chain.py -m gpu -x -q --timeout 300 --timeout-method thread > "$O/vtests_$v.log" 2>&1 \
+                || { echo "vtests $v failed" >&2; tail -30 "$O/vtests_$v.log"; exit 1; }
+            echo "$v $(tail -1 "$O/vtests_$v.log")"
+        done
+        ;;
     var)
         for v in base $VARIANTS; do
             if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
