@@ -432,6 +432,39 @@ def cdef_breakdown(cfg, dev, steps):
             "bit_exact_vs_oracle": all(bool(np.array_equal(a, b)) for a, b in zip(d.outputs_host(), want))}
 
 
+def superres_breakdown(cfg, dev, steps):
+    """super-res (dav1d_gpu_resize_frame_*, dav1d_filter_
+    sbrow_resize over a whole frame) of a picture upscaled to the config's
+    size from half its width (denominator 16), 4:2:0: us per frame by HIP
+    events, algorithmic GB/s (source read once, output written once), the
+    oracle's superblock-row walk on one core, bit-exact check."""
+    import torch
+    import dav1d_mirror_amd.superres as sr
+    c = sr.make_case(cfg.width, cfg.height, 16, layout=1, bpc=cfg.bpc, bitdepth_max=cfg.bitdepth_max, seed=11)
+    d = sr.DeviceResize(c, dev)
+    s = torch.cuda.current_stream(dev)
+    for _ in range(3):
+        d.launch(s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = max(steps, 20)
+    e0.record(s)
+    for _ in range(n):
+        d.launch(s)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    us = e0.elapsed_time(e1) * 1e3 / n
+    t0 = time.perf_counter()
+    want = ge.load_oracle().resize_frame(c)
+    cpu = time.perf_counter() - t0
+    nbytes = sr.algorithmic_bytes(c)
+    px = sum(a.shape[0] * c.dst_w[p] for p, a in enumerate(c.ins))
+    return {"frame": f"{c.w}x{cfg.height} -> {cfg.width}x{cfg.height} 4:2:0", "us_per_frame": round(us, 2),
+            "gpix_s": round(px / us / 1e3, 2), "algorithmic_bytes": nbytes,
+            "achieved_gbs": round(nbytes / us / 1e3, 1), "frac_of_hbm_peak": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+            "kernel": f"k_resize_frame<{cfg.bpc}>", "oracle_1core_ms": round(cpu * 1e3, 1),
+            "bit_exact_vs_oracle": all(bool(np.array_equal(a, b)) for a, b in zip(d.outputs_host(), want))}
+
+
 def lpf_breakdown(cfg, dev, steps):
     """the deblocking loop filter (dav1d_gpu_loopfilter_
     frame_*: every column edge, then every row edge) on a synthetic frame of
@@ -523,6 +556,7 @@ def main():
     ap.add_argument("--no-recorder", action="store_true", help="skip the batch-recorder measurement (N=1)")
     ap.add_argument("--no-grain", action="store_true", help="skip the film-grain measurement (N=1)")
     ap.add_argument("--no-cdef", action="store_true", help="skip the CDEF measurement (N=1)")
+    ap.add_argument("--no-superres", action="store_true", help="skip the super-res measurement (N=1)")
     ap.add_argument("--no-lpf", action="store_true", help="skip the deblocking measurement (N=1)")
     ap.add_argument("--no-lr", action="store_true", help="skip the loop-restoration measurement (N=1)")
     args = ap.parse_args()
@@ -668,6 +702,8 @@ def main():
             out["film_grain"] = grain_breakdown(cfg, dev, args.steps)
         if not args.no_cdef and world == 1:
             out["cdef"] = cdef_breakdown(cfg, dev, args.steps)
+        if not args.no_superres and world == 1:
+            out["superres"] = superres_breakdown(cfg, dev, args.steps)
         if not args.no_lpf and world == 1:
             out["loop_filter"] = lpf_breakdown(cfg, dev, args.steps)
         if not args.no_lr and world == 1:

@@ -214,6 +214,12 @@ class LrFrame(ctypes.Structure):
                 ("sb128", ctypes.c_int32), ("restore_planes", ctypes.c_int32)]
 
 
+class ResizeFrame(ctypes.Structure):   # Dav1dGpuResizeFrame
+    _fields_ = [("in_", Plane * 3), ("out", Plane * 3), ("step", ctypes.c_int32 * 2), ("start", ctypes.c_int32 * 2),
+                ("layout", ctypes.c_int32), ("bitdepth_max", ctypes.c_int32), ("sb128", ctypes.c_int32),
+                ("pad_", ctypes.c_int32)]
+
+
 class PictureParameters(ctypes.Structure):
     _fields_ = [("w", ctypes.c_int), ("h", ctypes.c_int), ("layout", ctypes.c_int), ("bpc", ctypes.c_int)]
 
@@ -361,6 +367,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_loop_restoration_dsp_init_8bpc", "dav1d_loop_restoration_dsp_init_16bpc",
     "dav1d_loop_restoration_dsp_init_gpu_8bpc", "dav1d_loop_restoration_dsp_init_gpu_16bpc",
     "dav1d_gpu_lr_frame_8bpc", "dav1d_gpu_lr_frame_16bpc",
+    "dav1d_gpu_resize_frame_8bpc", "dav1d_gpu_resize_frame_16bpc",
 ]
 
 

@@ -299,6 +299,63 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs<BPC> a) {
     a.dst[y * a.ds + x] = (typename Px<BPC>::pixel)clampi((-sum + 64) >> 7, 0, a.bdmax);
 }
 
+// Super-res frame tier (dav1d_filter_sbrow_resize for the whole frame): one
+// launch, blockIdx.z = plane, 64 output columns x 4 rows per workgroup; the
+// same per-pixel filter as k_resize.  The 8 source taps of a lane are
+// consecutive pixels of one row, served by L1 for the neighbouring lanes.
+template <int BPC> struct ResizeFrameArgs {
+    typename Px<BPC>::pixel *dst[3];
+    const typename Px<BPC>::pixel *src[3];
+    int ds[3], ss[3];   // pixels
+    int dst_w[3], src_w[3], h[3], dx[3], mx0[3];
+    int bdmax;
+};
+template <int BPC>
+__global__ __launch_bounds__(256) void k_resize_frame(ResizeFrameArgs<BPC> a) {
+    const int p = blockIdx.z;
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= a.dst_w[p] || y >= a.h[p]) return;
+    const int pos = a.mx0[p] + x * a.dx[p];
+    const int sx = (pos >> 14) - 1, sw = a.src_w[p];
+    const signed char *k = &dspt_resize[((pos & 0x3fff) >> 8) * 8];
+    const auto *s = a.src[p] + (size_t)y * a.ss[p];
+    int sum = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) sum += k[i] * (int)s[clampi(sx + i - 3, 0, sw - 1)];
+    a.dst[p][(size_t)y * a.ds[p] + x] = (typename Px<BPC>::pixel)clampi((-sum + 64) >> 7, 0, a.bdmax);
+}
+
+template <int BPC>
+static int launch_resize_frame(const Dav1dGpuResizeFrame *f, hipStream_t stream) {
+    using P = typename Px<BPC>::pixel;
+    constexpr int B = BPC / 8;
+    if (!f || f->layout < 0 || f->layout > 3) return -1;
+    const int np = f->layout ? 3 : 1;
+    ResizeFrameArgs<BPC> a{};
+    int gw = 0, gh = 0;
+    for (int p = 0; p < np; p++) {
+        const Dav1dGpuPlane &i = f->in[p], &o = f->out[p];
+        if (!i.data || !o.data || i.w <= 0 || o.w <= 0 || i.h <= 0 || o.h < i.h || i.stride < (int64_t)i.w * B ||
+            o.stride < (int64_t)o.w * B || (i.stride % B) || (o.stride % B))
+            return -1;
+        a.src[p] = (const P *)i.data;
+        a.dst[p] = (P *)o.data;
+        a.ss[p] = (int)(i.stride / B);
+        a.ds[p] = (int)(o.stride / B);
+        a.src_w[p] = i.w;
+        a.dst_w[p] = o.w;
+        a.h[p] = i.h;
+        a.dx[p] = f->step[p ? 1 : 0];
+        a.mx0[p] = f->start[p ? 1 : 0];
+        gw = max(gw, (o.w + 63) / 64);
+        gh = max(gh, (i.h + 3) / 4);
+    }
+    a.bdmax = BPC == 8 ? 255 : f->bitdepth_max;
+    k_resize_frame<BPC><<<dim3(gw, gh, np), 256, 0, stream>>>(a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 // ---------------------------------------------------------------------------
 // Host entries with the reference signatures.
 // ---------------------------------------------------------------------------
@@ -603,3 +660,10 @@ extern "C" void dav1d_mc_dsp_init_gpu_16bpc(Dav1dMCDSPContext_16bpc *c) {
 }
 extern "C" void dav1d_mc_dsp_init_8bpc(Dav1dMCDSPContext_8bpc *c) { FILL_MC(8, c); }
 extern "C" void dav1d_mc_dsp_init_16bpc(Dav1dMCDSPContext_16bpc *c) { FILL_MC(16, c); }
+
+extern "C" int dav1d_gpu_resize_frame_8bpc(const Dav1dGpuResizeFrame *f, void *stream) {
+    return launch_resize_frame<8>(f, (hipStream_t)stream);
+}
+extern "C" int dav1d_gpu_resize_frame_16bpc(const Dav1dGpuResizeFrame *f, void *stream) {
+    return launch_resize_frame<16>(f, (hipStream_t)stream);
+}

@@ -1106,6 +1106,32 @@ typedef struct Dav1dGpuLrFrame {
 int dav1d_gpu_lr_frame_8bpc(const Dav1dGpuLrFrame *f, void *stream);
 int dav1d_gpu_lr_frame_16bpc(const Dav1dGpuLrFrame *f, void *stream);
 
+/* Super-res: bytefn(dav1d_filter_sbrow_resize)
+ * (src/recon_tmpl.c:2104-2137) for a whole frame.  Every row of every plane
+ * of the post-CDEF picture is upscaled horizontally by mc.resize (resize_c,
+ * src/mc_tmpl.c:877-903) into the super-res picture.  The reference resizes
+ * one superblock row at a time, 8 rows (>> ss_ver) behind the CDEF; those
+ * row ranges tile the picture and the filter works on one row at a time, so
+ * one launch over the finished picture computes the same pixels.  in[p].w is
+ * the coded width the filter clamps to, (4 * f->bw + ss_hor) >> ss_hor;
+ * out[p].w the upscaled width, (f->sr_cur.p.p.w + ss_hor) >> ss_hor; in[p].h
+ * the plane height.  out must not alias in.  For loop restoration after
+ * super-res, upscale the deblocked picture the same way and hand it to
+ * dav1d_gpu_lr_frame_* as its lpf source (backup_lpf resizes the rows it
+ * keeps, src/lf_apply_tmpl.c:63-80).  Errors: -1 NULL / bad layout / bad
+ * sizes, -3 launch failure. */
+typedef struct Dav1dGpuResizeFrame {
+    Dav1dGpuPlane in[3];          /* device: the coded-width picture, read  */
+    Dav1dGpuPlane out[3];         /* device: the upscaled picture, written  */
+    int32_t step[2], start[2];    /* f->resize_step / resize_start [luma, chroma] */
+    int32_t layout;               /* 0 I400, 1 I420, 2 I422, 3 I444          */
+    int32_t bitdepth_max;
+    int32_t sb128;                /* the superblock-row walk (oracle only)   */
+    int32_t pad_;
+} Dav1dGpuResizeFrame;
+int dav1d_gpu_resize_frame_8bpc(const Dav1dGpuResizeFrame *f, void *stream);
+int dav1d_gpu_resize_frame_16bpc(const Dav1dGpuResizeFrame *f, void *stream);
+
 /* LDS bytes per workgroup of a batch kernel (bpc 8/16; group 0: the main
  * kernel, every size up to 32x32; 1: the large sizes when built with split
  * groups; 2: a 64-point side; 3: the warp kernel; -1 otherwise).

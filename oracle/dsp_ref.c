@@ -3108,3 +3108,42 @@ int oracle_lr_frame_16bpc(const Dav1dGpuLrFrame *F)
     }
     return 0;
 }
+
+/* ============================================================== super-res */
+
+/* bytefn(dav1d_filter_sbrow_resize), src/recon_tmpl.c:2104-2137, driven for
+ * every superblock row of the frame as dav1d_filter_sbrow does
+ * (:2151-2160): per plane, the rows from 8 (>> ss_ver) above the
+ * superblock row to two block rows before its end (the whole rest on the
+ * last row), each through mc.resize with the plane's step and start. */
+#if BITDEPTH == 8
+int oracle_resize_frame_8bpc(const Dav1dGpuResizeFrame *F)
+#else
+int oracle_resize_frame_16bpc(const Dav1dGpuResizeFrame *F)
+#endif
+{
+    if (!F || F->layout < 0 || F->layout > 3) return -1;
+    const int bdmax = BITDEPTH == 8 ? 255 : F->bitdepth_max;
+    const int pic_h = F->in[0].h;                       /* f->cur.p.h */
+    const int sbsz = F->sb128 ? 32 : 16;                /* f->sb_step, 4-px units */
+    const int bh = ((pic_h + 7) >> 3) << 1;             /* f->bh */
+    const int sbh = (bh + sbsz - 1) / sbsz;             /* f->sbh */
+    const int has_chroma = F->layout != 0;
+    for (int sby = 0; sby < sbh; sby++) {
+        const int y = sby * sbsz * 4;
+        for (int pl = 0; pl < 1 + 2 * has_chroma; pl++) {
+            const int ss_ver = pl && F->layout == 1, ss_hor = pl && F->layout != 3;
+            (void)ss_hor;
+            const Dav1dGpuPlane *in = &F->in[pl], *out = &F->out[pl];
+            const ptrdiff_t ss = in->stride, ds = out->stride;
+            const int h_start = 8 * !!sby >> ss_ver;
+            pixel *dst = (pixel *)out->data + (y >> ss_ver) * PX(ds) - h_start * PX(ds);
+            const pixel *src = (const pixel *)in->data + (y >> ss_ver) * PX(ss) - h_start * PX(ss);
+            const int h_end = 4 * (sbsz - 2 * (sby + 1 < sbh)) >> ss_ver;
+            const int img_h = (pic_h - sbsz * 4 * sby + ss_ver) >> ss_ver;
+            const int rows = (img_h < h_end ? img_h : h_end) + h_start;
+            resize(dst, ds, src, ss, out->w, rows, in->w, F->step[!!pl], F->start[!!pl], bdmax);
+        }
+    }
+    return 0;
+}

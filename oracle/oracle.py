@@ -508,3 +508,19 @@ def lr_frame(case):
     fn.restype = ctypes.c_int
     assert fn(ctypes.byref(f)) == 0
     return outs
+
+
+def resize_frame(case):
+    """A superres.ResizeCase through the oracle's dav1d_filter_sbrow_resize
+    walk (per superblock row); returns the upscaled planes."""
+    import dav1d_mirror_amd.superres as sr
+    abi = _abi()
+    L = load()
+    ins = [np.ascontiguousarray(a) for a in case.ins]
+    outs = [np.zeros(sh, dtype=case.dtype) for sh in sr.out_shapes(case)]
+    f = sr.fill(case, [(a.ctypes.data, a.shape[1]) for a in ins], [(a.ctypes.data, a.shape[1]) for a in outs])
+    fn = getattr(L, f"oracle_resize_frame_{8 if case.bpc == 8 else 16}bpc")
+    fn.argtypes = [ctypes.POINTER(abi.ResizeFrame)]
+    fn.restype = ctypes.c_int
+    assert fn(ctypes.byref(f)) == 0
+    return [o[:, :case.dst_w[p]] for p, o in enumerate(outs)]

@@ -13,7 +13,7 @@ STEPS=${*:-"tests quick"}
 O=$R/gpurun_out/it_$TAG
 mkdir -p "$O"
 cd "$R"
-Q="--no-cpu --steps 30 --warmup 3 --no-tiles --no-intra --no-recorder --no-grain --no-cdef --no-lpf --no-lr"
+Q="--no-cpu --steps 30 --warmup 3 --no-tiles --no-intra --no-recorder --no-grain --no-cdef --no-superres --no-lpf --no-lr"
 for s in $STEPS; do
     case $s in
     tests)
@@ -44,14 +44,14 @@ for s in $STEPS; do
     rec)
         echo "[it] rec" >&2
         DAV1D_GPU_REC_TIMING=1 timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 --no-families --no-configs --no-tiles --no-intra \
-            --no-grain --no-cdef --no-lpf --no-lr > "$O/rec.json" 2> "$O/rec.err" || { echo "rec failed" >&2; tail -20 "$O/rec.err"; exit 1; }
+            --no-grain --no-cdef --no-superres --no-lpf --no-lr > "$O/rec.json" 2> "$O/rec.err" || { echo "rec failed" >&2; tail -20 "$O/rec.err"; exit 1; }
         python3 -c "import json; d=json.load(open('$O/rec.json')); print(json.dumps(d['recorder']))"
         grep "^recorder" "$O/rec.err" | tail -14
         ;;
     recpin)   # the recorder's staging allocation (DAV1D_GPU_REC_PIN), bench recorder leg each
         for m in default nc reg; do
             DAV1D_GPU_REC_PIN=$m timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 --no-families --no-configs --no-tiles --no-intra \
-                --no-grain --no-cdef --no-lpf --no-lr > "$O/recpin_$m.json" 2> "$O/recpin_$m.err" || { echo "recpin $m failed" >&2; tail -20 "$O/recpin_$m.err"; exit 1; }
+                --no-grain --no-cdef --no-superres --no-lpf --no-lr > "$O/recpin_$m.json" 2> "$O/recpin_$m.err" || { echo "recpin $m failed" >&2; tail -20 "$O/recpin_$m.err"; exit 1; }
             python3 -c "import json; d=json.load(open('$O/recpin_$m.json'))['recorder']; print('$m', d['flush_host_ms'], d['flush_device_ms'], d['frame_threads']['flush_host_ms_per_frame'], d['bit_exact_vs_oracle'], d['frame_threads']['bit_exact_vs_oracle'])"
         done
         ;;
@@ -59,7 +59,7 @@ for s in $STEPS; do
         for v in base $IVARIANTS; do
             if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
             timeout -k 10 400 python3 bench.py --no-cpu --steps 5 --warmup 1 --no-families --no-configs --no-tiles \
-                --no-recorder --no-grain --no-cdef --no-lpf --no-lr > "$O/intra_$v.json" 2> "$O/intra_$v.err" \
+                --no-recorder --no-grain --no-cdef --no-superres --no-lpf --no-lr > "$O/intra_$v.json" 2> "$O/intra_$v.err" \
                 || { echo "intra $v failed" >&2; tail -5 "$O/intra_$v.err"; exit 1; }
             python3 -c "import json; d=json.load(open('$O/intra_$v.json'))['intra_wavefront']; print('$v', {k: (x['ms_per_frame'], x['us_per_level'], x['bit_exact_vs_oracle']) for k, x in d.items()})"
         done
@@ -72,6 +72,15 @@ for s in $STEPS; do
                 || { echo "vtests $v failed" >&2; tail -30 "$O/vtests_$v.log"; exit 1; }
             echo "$v $(tail -1 "$O/vtests_$v.log")"
         done
+        ;;
+    superres)   # the super-res frame tier's GPU tests and its bench leg
+        timeout -k 10 600 python3 -u -m pytest tests/test_gpu_superres.py -m gpu -x -q --timeout 300 --timeout-method thread \
+            > "$O/superres_tests.log" 2>&1 || { echo "superres tests failed" >&2; tail -30 "$O/superres_tests.log"; exit 1; }
+        tail -1 "$O/superres_tests.log"
+        timeout -k 10 300 python3 bench.py --no-cpu --steps 20 --warmup 2 --no-families --no-configs --no-tiles --no-intra \
+            --no-recorder --no-grain --no-cdef --no-lpf --no-lr > "$O/superres.json" 2> "$O/superres.err" \
+            || { echo "superres bench failed" >&2; tail -20 "$O/superres.err"; exit 1; }
+        python3 -c "import json; print(json.dumps(json.load(open('$O/superres.json'))['superres']))"
         ;;
     var)
         for v in base $VARIANTS; do

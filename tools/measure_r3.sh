@@ -30,7 +30,7 @@ for s in $STEPS; do
         ;;
     prof)
         echo "[m] prof" >&2
-        P="--steps 20 --warmup 3 --no-families --no-configs --no-tiles --no-intra --no-recorder --no-grain --no-cdef --no-lpf --no-lr"
+        P="--steps 20 --warmup 3 --no-families --no-configs --no-tiles --no-intra --no-recorder --no-grain --no-cdef --no-superres --no-lpf --no-lr"
         timeout -k 10 600 bash tools/prof.sh "$TAG" $P || exit 1
         timeout -k 10 600 bash tools/prof.sh "${TAG}_10bit" $P --config 4k-10bit || exit 1
         ;;
