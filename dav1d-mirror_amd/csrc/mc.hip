@@ -300,9 +300,12 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs<BPC> a) {
 }
 
 // Super-res frame tier (dav1d_filter_sbrow_resize for the whole frame): one
-// launch, blockIdx.z = plane, 64 output columns x 4 rows per workgroup; the
-// same per-pixel filter as k_resize.  The 8 source taps of a lane are
-// consecutive pixels of one row, served by L1 for the neighbouring lanes.
+// launch, blockIdx.z = plane.  A wave upscales 256 consecutive output pixels
+// of one row: the source span they read (at most 256 * dx / 2^14 + 8 pixels,
+// dx <= 2^14 since super-res only upscales) is loaded once into LDS with the
+// reference's column clamp applied at load time, then each lane filters
+// four outputs (x0 + lane + 64 k) from LDS with the 8 taps of resize_c.
+constexpr int kRzOut = 256, kRzSpan = kRzOut + 16;
 template <int BPC> struct ResizeFrameArgs {
     typename Px<BPC>::pixel *dst[3];
     const typename Px<BPC>::pixel *src[3];
@@ -312,18 +315,36 @@ template <int BPC> struct ResizeFrameArgs {
 };
 template <int BPC>
 __global__ __launch_bounds__(256) void k_resize_frame(ResizeFrameArgs<BPC> a) {
-    const int p = blockIdx.z;
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= a.dst_w[p] || y >= a.h[p]) return;
-    const int pos = a.mx0[p] + x * a.dx[p];
-    const int sx = (pos >> 14) - 1, sw = a.src_w[p];
-    const signed char *k = &dspt_resize[((pos & 0x3fff) >> 8) * 8];
-    const auto *s = a.src[p] + (size_t)y * a.ss[p];
-    int sum = 0;
+    using P = typename Px<BPC>::pixel;
+    __shared__ P span[4][kRzSpan];
+    const int p = blockIdx.z, w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int y = blockIdx.y * 4 + w, x0 = blockIdx.x * kRzOut;
+    const int dw = a.dst_w[p], sw = a.src_w[p], dx = a.dx[p], mx0 = a.mx0[p];
+    if (y >= a.h[p] || x0 >= dw) return;   // wave-uniform
+    const P *s = a.src[p] + (size_t)y * a.ss[p];
+    const int s0 = ((mx0 + x0 * dx) >> 14) - 4;   // first source column a tap of this run reads
+    P *t = span[w];
 #pragma unroll
-    for (int i = 0; i < 8; i++) sum += k[i] * (int)s[clampi(sx + i - 3, 0, sw - 1)];
-    a.dst[p][(size_t)y * a.ds[p] + x] = (typename Px<BPC>::pixel)clampi((-sum + 64) >> 7, 0, a.bdmax);
+    for (int k = 0; k < kRzSpan / 64 + 1; k++) {
+        const int i = l + 64 * k;
+        if (i < kRzSpan) t[i] = s[clampi(s0 + i, 0, sw - 1)];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    P *d = a.dst[p] + (size_t)y * a.ds[p];
+#pragma unroll
+    for (int k = 0; k < kRzOut / 64; k++) {
+        const int x = x0 + l + 64 * k;
+        if (x < dw) {
+            const int pos = mx0 + x * dx;
+            const P *c = t + ((pos >> 14) - 4 - s0);   // taps c[0..7] = source (pos >> 14) - 4 .. + 3
+            const signed char *f = &dspt_resize[((pos & 0x3fff) >> 8) * 8];
+            int sum = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) sum += f[i] * (int)c[i];
+            d[x] = (P)clampi((-sum + 64) >> 7, 0, a.bdmax);
+        }
+    }
 }
 
 template <int BPC>
@@ -348,7 +369,8 @@ static int launch_resize_frame(const Dav1dGpuResizeFrame *f, hipStream_t stream)
         a.h[p] = i.h;
         a.dx[p] = f->step[p ? 1 : 0];
         a.mx0[p] = f->start[p ? 1 : 0];
-        gw = max(gw, (o.w + 63) / 64);
+        if (f->step[p ? 1 : 0] <= 0 || f->step[p ? 1 : 0] > 1 << 14) return -1;   // super-res upscales
+        gw = max(gw, (o.w + kRzOut - 1) / kRzOut);
         gh = max(gh, (i.h + 3) / 4);
     }
     a.bdmax = BPC == 8 ? 255 : f->bitdepth_max;
