@@ -380,6 +380,20 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
             return -3;
         }
     }
+#if DGPU_BOUNDS
+    {
+        DgpuBndTab t{};
+        for (int p = 0; p < 3; p++) {
+            bnd_add(t, b->dst[p]);
+            bnd_add(t, e->top_edge[p]);
+            for (int r = 0; r < DGPU_MAX_REFS; r++) bnd_add(t, b->ref[r][p]);
+        }
+        bnd_add(t, b->cfl_luma);
+        bnd_print<P>(t, "flow");
+        if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dgpu_bnd), &t, sizeof(t), 0, hipMemcpyHostToDevice, stream) != hipSuccess)
+            return -3;
+    }
+#endif
     ReconArgs<BPC> a;
     memset(&a, 0, sizeof(a));
     for (int p = 0; p < 3; p++) {

@@ -78,13 +78,23 @@ __device__ __forceinline__ IeCtx<P> ie_setup(const Dav1dGpuIntraEdge &r, const P
 // hand-off, flow_impl.hpp DGPU_FLOW_SC1): the aligned 4-byte word holding it,
 // loaded write-through coherent (global_load_dword sc1, bypassing this CU's
 // L1), so no acquire is needed before it.
-template <bool SC, typename P> __device__ __forceinline__ int ie_px(const P *p) {
+#if DGPU_BOUNDS
+__device__ __noinline__ bool bnd_ok(const void *p, int n, int line);
+#endif
+template <bool SC, typename P> __device__ __forceinline__ int ie_px(const P *p
+#if DGPU_BOUNDS
+                                                                    , int line = __builtin_LINE()
+#endif
+) {
     if constexpr (SC) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(p);
         const uint32_t w = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t *)(a & ~(uintptr_t)3),
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return sizeof(P) == 1 ? (int)((w >> (8 * (a & 3))) & 0xff) : (int)((w >> (8 * (a & 2))) & 0xffff);
     } else {
+#if DGPU_BOUNDS
+        if (!bnd_ok(p, (int)sizeof(P), line)) return 0;
+#endif
         return (int)*p;
     }
 }

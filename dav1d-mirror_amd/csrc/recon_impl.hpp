@@ -266,6 +266,20 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
             if (b->ref[r][p].data && (b->ref[r][p].stride & 3)) return -4;
     }
     if (b->n_units == 0) return 0;
+#if DGPU_BOUNDS
+    {
+        DgpuBndTab t{};
+        for (int p = 0; p < 3; p++) {
+            bnd_add(t, b->dst[p]);
+            for (int r = 0; r < DGPU_MAX_REFS; r++) bnd_add(t, b->ref[r][p]);
+        }
+        bnd_add(t, b->cfl_luma);
+        bnd_print<P>(t, "recon");
+        if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dgpu_bnd), &t, sizeof(t), 0, hipMemcpyHostToDevice, stream) != hipSuccess ||
+            hipStreamSynchronize(stream) != hipSuccess)
+            return -3;
+    }
+#endif
 
     ReconArgs<BPC> a;
     memset(&a, 0, sizeof(a));

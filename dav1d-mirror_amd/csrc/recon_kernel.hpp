@@ -368,10 +368,52 @@ __device__ __forceinline__ void vdot4x4(const uint32_t (*a)[4], const uint4 &tv,
 // Global-memory access through pointers that came from LDS (the plane
 // table): tell the compiler the address space so it emits global_*
 // instead of flat_* instructions.
-template <typename T> __device__ __forceinline__ T gld(const void *p) {
+#ifndef DGPU_BOUNDS
+#define DGPU_BOUNDS 0
+#endif
+#if DGPU_BOUNDS
+// Diagnostics builds only (tools/build_variants.sh `bounds`): the planes a
+// launch was given, [data, data + stride * h) each; an access within 4 MiB of
+// one of them but inside none is printed with its source line and skipped.
+struct DgpuBndTab {
+    unsigned long long r[3 * DGPU_MAX_REFS + 8][2];
+    int n;
+};
+static __device__ DgpuBndTab g_dgpu_bnd;
+__device__ __noinline__ bool bnd_ok(const void *p, int n, int line) {
+    const unsigned long long a = (unsigned long long)(uintptr_t)p;
+    bool near = false;
+    for (int i = 0; i < g_dgpu_bnd.n; i++) {
+        const unsigned long long lo = g_dgpu_bnd.r[i][0], hi = g_dgpu_bnd.r[i][1];
+        if (a >= lo && a + n <= hi) return true;
+        if (a + (4ull << 20) > lo && a < hi + (4ull << 20)) near = true;
+    }
+    if (near) printf("DGPU_BOUNDS line %d addr %llx bytes %d\n", line, a, n);
+    return !near;
+}
+static inline void bnd_add(DgpuBndTab &t, const Dav1dGpuPlane &pl) {
+    if (pl.data && t.n < (int)(sizeof(t.r) / sizeof(t.r[0]))) {
+        t.r[t.n][0] = (unsigned long long)(uintptr_t)pl.data;
+        t.r[t.n][1] = t.r[t.n][0] + (unsigned long long)pl.stride * (unsigned long long)pl.h;
+        t.n++;
+    }
+}
+template <typename P>
+static inline void bnd_print(const DgpuBndTab &t, const char *who) {
+    for (int i = 0; i < t.n; i++) fprintf(stderr, "DGPU_BOUNDS %s range %d %llx..%llx\n", who, i, t.r[i][0], t.r[i][1]);
+}
+#define DGPU_LINE , int line = __builtin_LINE()
+#define DGPU_CHK(p, n, fail) if (!bnd_ok(p, n, line)) fail
+#else
+#define DGPU_LINE
+#define DGPU_CHK(p, n, fail)
+#endif
+template <typename T> __device__ __forceinline__ T gld(const void *p DGPU_LINE) {
+    DGPU_CHK(p, (int)sizeof(T), return T{});
     return *(const __attribute__((address_space(1))) T *)p;
 }
-template <typename T> __device__ __forceinline__ void gst(void *p, T v) {
+template <typename T> __device__ __forceinline__ void gst(void *p, T v DGPU_LINE) {
+    DGPU_CHK(p, (int)sizeof(T), return);
     *(__attribute__((address_space(1))) T *)p = v;
 }
 // The intra wavefront's acquire-free hand-off (DGPU_FLOW_SC1, flow_impl.hpp):
@@ -465,7 +507,12 @@ template <int MAXN, int G> struct Stage {
         const uint8_t *s = reinterpret_cast<const uint8_t *>(src) - sk;
         nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
 #pragma unroll
-        for (int k = 0; k < IT; k++) v[k] = gld<u32x4>(s + 16 * min(l + k * G, nch - 1));   // clamped
+        for (int k = 0; k < IT; k++)   // clamped
+#if DGPU_BOUNDS   // coefficient / edge buffers, not planes: unchecked
+            v[k] = *(const __attribute__((address_space(1))) u32x4 *)(s + 16 * min(l + k * G, nch - 1));
+#else
+            v[k] = gld<u32x4>(s + 16 * min(l + k * G, nch - 1));
+#endif
     }
     __device__ __forceinline__ int commit(uint8_t *dst, int l) const {
 #pragma unroll

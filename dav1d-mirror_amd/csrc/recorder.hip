@@ -78,7 +78,10 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        if (hipMalloc(&p, n) != hipSuccess) return -1;
+        // 64 KiB of slack past every buffer, rounded to 64 KiB: a vector
+        // load that runs past a buffer's last element stays mapped
+        const size_t sz = ((n + (64u << 10)) + ((64u << 10) - 1)) & ~(size_t)((64u << 10) - 1);
+        if (hipMalloc(&p, sz) != hipSuccess) return -1;
         cap = n;
         return 0;
     }
