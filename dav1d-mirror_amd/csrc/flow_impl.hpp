@@ -95,31 +95,35 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
     // runs (a loop over tasks would hoist the argument loads out of the
     // whole class code and spill)
     int t = 0;
-    if (lane == 0) t = __hip_atomic_fetch_add(&f.ctr[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        bnd_touch(f.ctr);
+        t = __hip_atomic_fetch_add(&f.ctr[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= f.n_tasks) return;
     unsigned long long tr0 = 0, tr1 = 0, tr2 = 0;
     if constexpr (DGPU_FLOW_TRACE) tr0 = __builtin_amdgcn_s_memrealtime();
-    const FlowTask task = f.tasks[t];
+    const FlowTask task = bld(f.tasks + t);
     const int level = __builtin_amdgcn_readfirstlane(task.level);
     const int cls = __builtin_amdgcn_readfirstlane(task.cls);
     const int first = __builtin_amdgcn_readfirstlane(task.first);
     const int count = __builtin_amdgcn_readfirstlane(task.count);
     const int lg = (int)((kLog2Lanes >> (3 * cls)) & 7);
     const int ui = first + min(lane >> lg, count - 1);
-    const Dav1dGpuUnit u = a.units[ui];
-    const Dav1dGpuIntraEdge rec = a.recs[ui];
+    const Dav1dGpuUnit u = bld(a.units + ui);
+    const Dav1dGpuIntraEdge rec = bld(a.recs + ui);
     // the level wait runs inside the class code, after the coefficient loads
     // and the transforms and before the edge gather (recon_kernel.hpp)
     auto wait = [&]() {
         if (f.dep_start) {   // dataflow: the producers of the task's units, one per lane
-            const int d0 = f.dep_start[first], nd = f.dep_start[first + count] - d0;
+            const int d0 = bld(f.dep_start + first), nd = bld(f.dep_start + first + count) - d0;
             // the class code has let lanes past its units go: the live lanes
             // are a prefix of the wave
             const int nl = __popcll(__ballot(1));
             int ok = 1;
             for (int j0 = 0; j0 < nd; j0 += nl) {
-                const int j = j0 + lane, dep = j < nd ? f.deps[d0 + j] : -1;
+                const int j = j0 + lane, dep = j < nd ? bld(f.deps + d0 + j) : -1;
+                if (dep >= 0) bnd_touch(f.done + dep);
                 for (int it = 0;; it++) {
                     const int v = dep < 0 ? 1 : __hip_atomic_load(&f.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (__all(v != 0)) break;
@@ -142,8 +146,9 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
         } else if (level > 0) {
             int ok = 1;
             if (lane == 0) {
-                const int need = f.level_tasks[level - 1];
+                const int need = bld(f.level_tasks + level - 1);
                 int *done = &f.ctr[kFlowCtrHead + kFlowCtrStride * (level - 1)];
+                bnd_touch(done);
                 for (int it = 0;; it++) {
                     if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
                     if (it >= f.spin_limit ||
@@ -176,9 +181,12 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
     if (DGPU_FLOW_SC1 || DGPU_FLOW_NOFENCE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (f.dep_start) {   // (all lanes are live again here)
-        for (int i = lane; i < count; i += 64)
+        for (int i = lane; i < count; i += 64) {
+            bnd_touch(f.done + first + i);
             __hip_atomic_store(&f.done[first + i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     } else if (lane == 0) {
+        bnd_touch(f.ctr + kFlowCtrHead + kFlowCtrStride * level);
         __hip_atomic_fetch_add(&f.ctr[kFlowCtrHead + kFlowCtrStride * level], 1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -384,11 +392,16 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     {
         DgpuBndTab t{};
         for (int p = 0; p < 3; p++) {
-            bnd_add(t, b->dst[p]);
-            bnd_add(t, e->top_edge[p]);
-            for (int r = 0; r < DGPU_MAX_REFS; r++) bnd_add(t, b->ref[r][p]);
+            bnd_add(t, b->dst[p], BND_DST);
+            bnd_add(t, e->top_edge[p], BND_TOP);
+            for (int r = 0; r < DGPU_MAX_REFS; r++) bnd_add(t, b->ref[r][p], BND_REF);
         }
-        bnd_add(t, b->cfl_luma);
+        bnd_add(t, b->cfl_luma, BND_CFL);
+        bnd_range(t, b->units, (unsigned long long)b->n_units * sizeof(Dav1dGpuUnit), BND_UNITS);
+        bnd_range(t, e->units, (unsigned long long)b->n_units * sizeof(Dav1dGpuUnit), BND_UNITS);
+        bnd_range(t, e->recs, (unsigned long long)b->n_units * sizeof(Dav1dGpuIntraEdge), BND_RECS);
+        bnd_range(t, ws, Lw.total, BND_WORK);
+        bnd_add_extra(t);
         bnd_print<P>(t, "flow");
         if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dgpu_bnd), &t, sizeof(t), 0, hipMemcpyHostToDevice, stream) != hipSuccess)
             return -3;

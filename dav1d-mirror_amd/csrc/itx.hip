@@ -125,7 +125,7 @@ static bool itx_entry(typename Px<BPC>::pixel *dst, ptrdiff_t stride,
 // The caller's entries before dav1d_itx_dsp_init_gpu_* overwrote them (run
 // when the GPU path fails: runtime.hpp's error contract).
 static Dav1dInvTxfmDSPContext_8bpc g_fb8;
-static Dav1dInvTxfmDSPContext_16bpc g_fb16;
+static Dav1dInvTxfmDSPContext_16bpc g_fb16[2];   // 10 bit, 12 bit (fb16_slot)
 
 template <int TX, int TP>
 static void itx8(uint8_t *d, ptrdiff_t s, int16_t *c, int eob) {
@@ -133,7 +133,8 @@ static void itx8(uint8_t *d, ptrdiff_t s, int16_t *c, int eob) {
 }
 template <int TX, int TP>
 static void itx16(uint16_t *d, ptrdiff_t s, int32_t *c, int eob, int bdmax) {
-    DGPU_OR_FALLBACK((itx_entry<16, TX, TP>(d, s, c, eob, bdmax)), g_fb16.itxfm_add[TX][TP], d, s, c, eob, bdmax);
+    DGPU_OR_FALLBACK((itx_entry<16, TX, TP>(d, s, c, eob, bdmax)), g_fb16[fb16_slot_bdmax(bdmax)].itxfm_add[TX][TP], d, s, c, eob,
+                     bdmax);
 }
 
 template <typename Ctx, int TX, int TP>
@@ -161,7 +162,8 @@ using namespace dgpu;
 // bitfn(dav1d_itx_dsp_init) replacement, src/itx_tmpl.c:200-284.  Entries
 // the reference leaves unset stay NULL; `bpc` selects nothing here (one
 // kernel set covers 10 and 12 bit through bitdepth_max).  The _gpu_ hooks
-// keep the caller's previous entries as fallbacks.
+// keep the caller's previous entries as fallbacks, per bit depth for 16bpc
+// (the caller's 10- and 12-bit entries differ).
 extern "C" void dav1d_itx_dsp_init_gpu_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int bpc) {
     (void)bpc;
     Dav1dInvTxfmDSPContext_8bpc g{};
@@ -170,10 +172,9 @@ extern "C" void dav1d_itx_dsp_init_gpu_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int 
     fill_all(c, false, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 extern "C" void dav1d_itx_dsp_init_gpu_16bpc(Dav1dInvTxfmDSPContext_16bpc *c, int bpc) {
-    (void)bpc;
     Dav1dInvTxfmDSPContext_16bpc g{};
     fill_all(&g, true, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
-    save_fallback(&g_fb16, c, &g);
+    save_fallback(&g_fb16[fb16_slot(bpc)], c, &g);
     fill_all(c, true, std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 }
 extern "C" void dav1d_itx_dsp_init_8bpc(Dav1dInvTxfmDSPContext_8bpc *c, int bpc) {

@@ -476,14 +476,16 @@ static bool lr_t(typename Px<BPC>::pixel *p, ptrdiff_t stride, const typename Px
 // contract).  KIND 0 serves both Wiener slots: the 7-tap entry wiener[0]
 // handles any Wiener filter, so it is the fallback for both.
 static Dav1dLoopRestorationDSPContext_8bpc g_fb8;
-static Dav1dLoopRestorationDSPContext_16bpc g_fb16;
+static Dav1dLoopRestorationDSPContext_16bpc g_fb16[2];   // 10 bit, 12 bit (fb16_slot)
+#define LR_FB8 g_fb8
+#define LR_FB16 g_fb16[fb16_slot_bdmax(bitdepth_max)]
 
 #define LR_ENTRIES(BPC, P, BDP, BDV)                                                                      \
 template <int KIND>                                                                                       \
 static void lr_##BPC(P *d, ptrdiff_t s, const P (*l)[4], const P *lpf, int w, int h,                      \
                      const Dav1dGpuLrParams *prm, int edges BDP)                                          \
 { DGPU_OR_FALLBACK((lr_t<BPC>(d, s, l, lpf, w, h, prm, edges, KIND, BDV)),                               \
-                   KIND == 0 ? g_fb##BPC.wiener[0] : g_fb##BPC.sgr[KIND ? KIND - 1 : 0], d, s, l, lpf,    \
+                   KIND == 0 ? LR_FB##BPC.wiener[0] : LR_FB##BPC.sgr[KIND ? KIND - 1 : 0], d, s, l, lpf,  \
                    w, h, prm, edges BDV##_ARG); }
 
 #define BD8_PARAM
@@ -517,10 +519,9 @@ extern "C" void dav1d_loop_restoration_dsp_init_gpu_8bpc(Dav1dLoopRestorationDSP
     FILL_LR(8, c);
 }
 extern "C" void dav1d_loop_restoration_dsp_init_gpu_16bpc(Dav1dLoopRestorationDSPContext_16bpc *c, int bpc) {
-    (void)bpc;
     Dav1dLoopRestorationDSPContext_16bpc g{}, *gp = &g;
     FILL_LR(16, gp);
-    save_fallback(&g_fb16, c, gp);
+    save_fallback(&g_fb16[fb16_slot(bpc)], c, gp);
     FILL_LR(16, c);
 }
 extern "C" int dav1d_gpu_lr_frame_8bpc(const Dav1dGpuLrFrame *f, void *stream) {

@@ -154,9 +154,9 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     // this lane's unit descriptor (lanes past the last unit re-read it)
     const int ui_ = first + min((int)(threadIdx.x & 63) >> lg, count - 1);
     // (a struct load: assembling it from vector loads spilled it to scratch)
-    const Dav1dGpuUnit u = units[ui_];
+    const Dav1dGpuUnit u = bld(units + ui_);
     Dav1dGpuIntraEdge rec{};
-    if constexpr (gathers(GRP)) rec = a.recs[ui_];   // its edge record, in the same round trip
+    if constexpr (gathers(GRP)) rec = bld(a.recs + ui_);   // its edge record, in the same round trip
     // per-wave copy of the plane table: lane-indexed vector loads of the
     // argument segment, in flight together with the descriptor loads (no
     // workgroup barrier: the waves do not wait for each other)
@@ -270,10 +270,12 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
     {
         DgpuBndTab t{};
         for (int p = 0; p < 3; p++) {
-            bnd_add(t, b->dst[p]);
-            for (int r = 0; r < DGPU_MAX_REFS; r++) bnd_add(t, b->ref[r][p]);
+            bnd_add(t, b->dst[p], BND_DST);
+            for (int r = 0; r < DGPU_MAX_REFS; r++) bnd_add(t, b->ref[r][p], BND_REF);
         }
-        bnd_add(t, b->cfl_luma);
+        bnd_add(t, b->cfl_luma, BND_CFL);
+        bnd_range(t, b->units, (unsigned long long)b->n_units * sizeof(Dav1dGpuUnit), BND_UNITS);
+        bnd_add_extra(t);
         bnd_print<P>(t, "recon");
         if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dgpu_bnd), &t, sizeof(t), 0, hipMemcpyHostToDevice, stream) != hipSuccess ||
             hipStreamSynchronize(stream) != hipSuccess)

@@ -30,6 +30,7 @@
 // Every LDS hand-off stays inside one wave (no workgroup barrier).
 #pragma once
 #include "dav1d_gpu.h"
+#include "bounds.hpp"
 #include "dsp_common.hpp"
 #include "intra_edge_dev.hpp"
 
@@ -372,14 +373,22 @@ __device__ __forceinline__ void vdot4x4(const uint32_t (*a)[4], const uint4 &tv,
 #define DGPU_BOUNDS 0
 #endif
 #if DGPU_BOUNDS
-// Diagnostics builds only (tools/build_variants.sh `bounds`): the planes a
-// launch was given, [data, data + stride * h) each; an access within 4 MiB of
-// one of them but inside none is printed with its source line and skipped.
+// Diagnostics builds only (tools/build_variants.sh `bounds`): every device
+// range a launch may touch, [lo, hi) each -- the planes it was given
+// ([data, data + stride * h)) and, when the caller registered them
+// (dgpu::bnd_extra(): the recorder registers every buffer of its flush with
+// its exact byte size), the unit / record / coefficient / edge / aux /
+// workspace / scratch buffers.  Strict tables (any buffer registered): an
+// access inside none of the ranges is printed with its source line and the
+// range table's ids, and skipped.  Otherwise (planes only: direct callers of
+// the batch entries) only an access within 4 MiB of a plane is judged.
 struct DgpuBndTab {
-    unsigned long long r[3 * DGPU_MAX_REFS + 8][2];
-    int n;
+    unsigned long long r[64][2];
+    int id[64];
+    int n, strict;
 };
 static __device__ DgpuBndTab g_dgpu_bnd;
+static __device__ int g_dgpu_bnd_hits;   // printed at most 256 times per process
 __device__ __noinline__ bool bnd_ok(const void *p, int n, int line) {
     const unsigned long long a = (unsigned long long)(uintptr_t)p;
     bool near = false;
@@ -388,19 +397,35 @@ __device__ __noinline__ bool bnd_ok(const void *p, int n, int line) {
         if (a >= lo && a + n <= hi) return true;
         if (a + (4ull << 20) > lo && a < hi + (4ull << 20)) near = true;
     }
-    if (near) printf("DGPU_BOUNDS line %d addr %llx bytes %d\n", line, a, n);
-    return !near;
+    if (!g_dgpu_bnd.strict && !near) return true;
+    if (atomicAdd(&g_dgpu_bnd_hits, 1) < 256)
+        printf("DGPU_BOUNDS line %d addr %llx bytes %d block %d lane %d\n", line, a, n, (int)blockIdx.x,
+               (int)(threadIdx.x & 63));
+    return false;
 }
-static inline void bnd_add(DgpuBndTab &t, const Dav1dGpuPlane &pl) {
-    if (pl.data && t.n < (int)(sizeof(t.r) / sizeof(t.r[0]))) {
-        t.r[t.n][0] = (unsigned long long)(uintptr_t)pl.data;
-        t.r[t.n][1] = t.r[t.n][0] + (unsigned long long)pl.stride * (unsigned long long)pl.h;
+static inline void bnd_range(DgpuBndTab &t, const void *p, unsigned long long bytes, int id) {
+    if (p && bytes && t.n < (int)(sizeof(t.r) / sizeof(t.r[0]))) {
+        t.r[t.n][0] = (unsigned long long)(uintptr_t)p;
+        t.r[t.n][1] = t.r[t.n][0] + bytes;
+        t.id[t.n] = id;
         t.n++;
+    }
+}
+static inline void bnd_add(DgpuBndTab &t, const Dav1dGpuPlane &pl, int id = 0) {
+    if (pl.data) bnd_range(t, pl.data, (unsigned long long)pl.stride * (unsigned long long)pl.h, id);
+}
+// the caller's registered buffers (strict mode when there are any)
+static inline void bnd_add_extra(DgpuBndTab &t) {
+    for (const BndRange &e : bnd_extra()) {
+        bnd_range(t, e.p, e.bytes, e.id);
+        t.strict = 1;
     }
 }
 template <typename P>
 static inline void bnd_print(const DgpuBndTab &t, const char *who) {
-    for (int i = 0; i < t.n; i++) fprintf(stderr, "DGPU_BOUNDS %s range %d %llx..%llx\n", who, i, t.r[i][0], t.r[i][1]);
+    for (int i = 0; i < t.n; i++)
+        fprintf(stderr, "DGPU_BOUNDS %s range %d id %d %llx..%llx%s\n", who, i, t.id[i], t.r[i][0], t.r[i][1],
+                t.strict ? " strict" : "");
 }
 #define DGPU_LINE , int line = __builtin_LINE()
 #define DGPU_CHK(p, n, fail) if (!bnd_ok(p, n, line)) fail
@@ -415,6 +440,20 @@ template <typename T> __device__ __forceinline__ T gld(const void *p DGPU_LINE) 
 template <typename T> __device__ __forceinline__ void gst(void *p, T v DGPU_LINE) {
     DGPU_CHK(p, (int)sizeof(T), return);
     *(__attribute__((address_space(1))) T *)p = v;
+}
+// Plain loads / stores of the descriptor, record, aux-index and workspace
+// arrays: exactly `*p` / `*p = v` in product builds, checked in DGPU_BOUNDS
+// builds; bnd_touch checks the address of an atomic
+template <typename T> __device__ __forceinline__ T bld(const T *p DGPU_LINE) {
+    DGPU_CHK(p, (int)sizeof(T), return T{});
+    return *p;
+}
+template <typename T> __device__ __forceinline__ void bst(T *p, T v DGPU_LINE) {
+    DGPU_CHK(p, (int)sizeof(T), return);
+    *p = v;
+}
+template <typename T> __device__ __forceinline__ void bnd_touch(const T *p DGPU_LINE) {
+    DGPU_CHK(p, (int)sizeof(T), return);
 }
 // The intra wavefront's acquire-free hand-off (DGPU_FLOW_SC1, flow_impl.hpp):
 // in GATHER builds every picture / top_edge store is write-through (sc1) and
@@ -508,11 +547,7 @@ template <int MAXN, int G> struct Stage {
         nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
 #pragma unroll
         for (int k = 0; k < IT; k++)   // clamped
-#if DGPU_BOUNDS   // coefficient / edge buffers, not planes: unchecked
-            v[k] = *(const __attribute__((address_space(1))) u32x4 *)(s + 16 * min(l + k * G, nch - 1));
-#else
             v[k] = gld<u32x4>(s + 16 * min(l + k * G, nch - 1));
-#endif
     }
     __device__ __forceinline__ int commit(uint8_t *dst, int l) const {
 #pragma unroll
@@ -1131,7 +1166,9 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
     const int a0 = (int16_t)(abcd[0] & 0xffff), a1 = (int)abcd[0] >> 16;
     const int a2 = (int16_t)(abcd[1] & 0xffff), a3 = (int)abcd[1] >> 16;
     const int ri = u.p.inter.ref[0] * 3 + u.plane;
-    const P *ref = pt.ref[ri];
+    // src_off[0]: a base the 8x8 positions are relative to (0, or the
+    // recorder's clamped-copy strip in its scratch plane)
+    const P *ref = pt.ref[ri] + u.p.inter.src_off[0];
     const int rs = pt.ref_stride[ri];
     const int ib = Px<BPC>::ibits(bdmax);
     const int hsh = 7 - ib, hrnd = (1 << hsh) >> 1;
@@ -1381,7 +1418,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     }
     // INTER_MASK / PAL: the unit's aux_pool offset (mask / palette record)
     const bool auxed = pred == DGPU_PRED_INTER_MASK || pred == DGPU_PRED_PAL || pred == DGPU_PRED_WARP || ii;
-    const int auxo = auxed ? a.aux[first + g] : 0;
+    const int auxo = auxed ? bld(a.aux + first + g) : 0;
     int cfsk = 0;
     if (ncoef) cfsk = cst.commit(cfl, l);
     const P *tl = nullptr;
@@ -1401,7 +1438,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     // coefficient zeroing (the reference's itx zeroes what it consumed,
     // src/itx_tmpl.c:55/89); loads above completed before the LDS writes
     if (a.zero_coefs && ncoef)
-        for (int i = l; i < ncoef; i += G) cf[i] = 0;
+        for (int i = l; i < ncoef; i += G) bst<C>(cf + i, 0);
 
     // ---------------- P3: row transforms -> tmp [SH][W] ----------------
     int dcres = 0;
@@ -1520,8 +1557,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             ug.p.intra.mode = (uint8_t)iec.mode;   // CFL: its DC source, the same byte
             if (pred != DGPU_PRED_CFL) ug.p.intra.angle = ie_angle_field(rec, iec.angle);
             if (l == 0) {
-                a.units_rw[first + g].p.intra.mode = ug.p.intra.mode;
-                if (pred != DGPU_PRED_CFL) a.units_rw[first + g].p.intra.angle = ug.p.intra.angle;
+                bst(&a.units_rw[first + g].p.intra.mode, ug.p.intra.mode);
+                if (pred != DGPU_PRED_CFL) bst(&a.units_rw[first + g].p.intra.angle, ug.p.intra.angle);
             }
         }
     }
@@ -1899,7 +1936,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
     const bool haveres = !nores && !dconly;
     P *dstp = pt.dst[plane] + u.dst_off;
     const int ds = pt.dst_stride[plane];
-    const int auxo = a.aux[first + g];
+    const int auxo = bld(a.aux + first + g);
 
     // ---- loads: coefficients and the first reference's footprint rows
     C *cf = a.coef + u.coef_off;
@@ -1939,7 +1976,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
     }
     wave_sync();
     if (a.zero_coefs && ncoef)
-        for (int i = l; i < ncoef; i += G) cf[i] = 0;
+        for (int i = l; i < ncoef; i += G) bst<C>(cf + i, 0);
 
     // ---- row, then column transforms into the residual (as recon_units)
     int dcres = 0;

@@ -38,7 +38,12 @@
 #include <thread>
 #include <vector>
 
+#include "bounds.hpp"
 #include "dav1d_gpu.h"
+
+#ifndef DGPU_BOUNDS
+#define DGPU_BOUNDS 0
+#endif
 
 namespace {
 
@@ -243,13 +248,14 @@ void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int lo, in
     }
 }
 
-// emu_edge per transform unit (src/recon_tmpl.c:986-999): a footprint that
-// leaves its reference picture is copied, every read clamped, into a scratch
-// plane of kEmuStride pixels per row, one (H + 7)-row band per copy
+// emu_edge per transform / prediction unit (src/recon_tmpl.c:986-999,
+// scaled :1036-1046, warp :1168-1177): a footprint that leaves its reference
+// picture is copied, every read clamped, into a scratch plane of kEmuStride
+// pixels per row (a band of rows per copy; warp 8x8s side by side)
 constexpr int kEmuStride = 128;
 struct EmuJob {
     int32_t x0, y0;   // the footprint's top-left in the reference (may be outside)
-    int32_t r0;       // its first scratch row
+    int32_t o0;       // its top-left in the scratch plane (pixels)
     uint8_t w, h, slot, plane;
 };
 static_assert(sizeof(EmuJob) == 16, "EmuJob layout");
@@ -260,7 +266,7 @@ struct EmuArgs {
     int32_t w[DGPU_MAX_REFS - 1][3], h[DGPU_MAX_REFS - 1][3];
     void *out;
     const EmuJob *jobs;
-    int32_t n;
+    int32_t n, rows;   // rows: the scratch plane's (diagnostics)
 };
 
 // one 64-lane workgroup per footprint: lanes along the row, clamped reads
@@ -271,7 +277,12 @@ __global__ __launch_bounds__(64) void k_emu_footprints(EmuArgs a) {
     const EmuJob jb = a.jobs[j];
     const P *ref = static_cast<const P *>(a.ref[jb.slot][jb.plane]);
     const int rs = a.stride[jb.slot][jb.plane], rw = a.w[jb.slot][jb.plane], rh = a.h[jb.slot][jb.plane];
-    P *out = static_cast<P *>(a.out) + (size_t)jb.r0 * kEmuStride;
+    P *out = static_cast<P *>(a.out) + jb.o0;
+#if DGPU_BOUNDS   // diagnostics: the job's scratch rows and the clamped reads stay inside their buffers
+    if (threadIdx.x == 0 && (jb.o0 < 0 || jb.o0 + (jb.h - 1) * kEmuStride + jb.w > a.rows * kEmuStride ||
+                             (jb.o0 % kEmuStride) + jb.w > kEmuStride || rw <= 0 || rh <= 0 || !ref))
+        printf("DGPU_BOUNDS emu job %d: at %d, %dx%d of %d rows, ref %dx%d\n", j, jb.o0, jb.w, jb.h, a.rows, rw, rh);
+#endif
     for (int c = threadIdx.x; c < jb.w; c += 64) {
         const int x = min(max(jb.x0 + c, 0), rw - 1);
         for (int i = 0; i < jb.h; i++) {
@@ -314,6 +325,8 @@ struct CellPart {
     std::vector<EmuJob> emu;
     std::vector<Dav1dGpuUnit> xunits;
     std::vector<int32_t> xaux;
+    std::vector<uint8_t> xfix;       // per launch-ahead unit: F_EMU0 / F_EMU1 (part-local src_off)
+    std::vector<int32_t> emu_auxfix; // aux_pool offsets of int32 part-local scratch offsets (OBMC / scaled)
     int32_t emu_rows = 0;
     size_t edge_px = 0, n_res_used = 0;
     int32_t wm_off = -1, wm_w = 0, wm_h = 0;   // the last INTER_WMASK block's seg mask (4:2:0)
@@ -325,6 +338,8 @@ struct CellPart {
         emu.clear();
         xunits.clear();
         xaux.clear();
+        xfix.clear();
+        emu_auxfix.clear();
         emu_rows = 0;
         edge_px = n_res_used = 0;
         wm_off = -1;
@@ -335,6 +350,14 @@ struct CellPart {
         const size_t o = (auxp.size() + 15) & ~(size_t)15;
         auxp.resize(o + nbytes);
         return (int32_t)o;
+    }
+    // a clamped copy of the fw x fh footprint at (x0, y0) of ref slot / plane
+    // in a band of new scratch rows; returns its part-local scratch offset
+    int32_t emu_band(int x0, int y0, int fw, int fh, int slot, int plane) {
+        const int32_t o = emu_rows * kEmuStride;
+        emu.push_back(EmuJob{x0, y0, o, (uint8_t)fw, (uint8_t)fh, (uint8_t)slot, (uint8_t)plane});
+        emu_rows += fh;
+        return o;
     }
 };
 
@@ -538,6 +561,13 @@ extern "C" int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlo
         const int32_t n = *(const int32_t *)aux;
         if (n != 1 && n != 2) return -1;
         need = 16 + 16 * (size_t)n;
+        if (aux_bytes != need) return -1;
+        // steps of a valid reference scale (1/16x .. 2x: dav1d's svc step,
+        // src/decode.c:3365-3369): up to 2048 per pixel; phases below 1024
+        for (int k = 0; k < n; k++) {
+            const ScaledBlockRef *q = (const ScaledBlockRef *)((const uint8_t *)aux + 16) + k;
+            if (q->dx < 1 || q->dx > 2048 || q->dy < 1 || q->dy > 2048 || q->mx > 1023 || q->my > 1023) return -1;
+        }
         break;
     }
     default: return -1;
@@ -735,9 +765,23 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 P.wm_h = b.h >> 1;
                 P.wm_off = P.aux_alloc((size_t)P.wm_w * P.wm_h);
             }
+            // mc()'s emu_edge decision per prediction unit and reference
+            // (src/recon_tmpl.c:986-999): the unit kernel reads a W+7 x H+7
+            // footprint with aligned 16-byte row loads (up to 16 bytes past
+            // it), so a direct read needs all of that inside the reference
+            // picture, else the footprint is read from a clamped copy
+            auto mc_inside = [&](int rr, int ix, int iy) {
+                const int rw = ref[rr][p].w, rh = ref[rr][p].h;
+                return ix - 3 >= 0 && iy - 3 >= 0 && ix + uw + 4 <= rw && iy + uh + 4 <= rh &&
+                       (iy + uh + 4 < rh || (int64_t)(ix + uw + 4) * bpp + 16 <= ref[rr][p].stride);
+            };
+            auto mc_emu = [&](int rr, int ix, int iy) {   // the copy's (0, 0) pixel offset
+                return P.emu_band(ix - 3, iy - 3, uw + 7, uh + 7, rr, p) + 3 * kEmuStride + 3;
+            };
             for (int oy = 0; oy < bhc; oy += uh)
                 for (int ox = 0; ox < bwc; ox += uw) {
                     const int ux = b.x + ox, uy = b.y + oy;
+                    uint8_t xf = 0;   // CellPart::F_EMU0 / F_EMU1: src_off[k] is a part-local scratch offset
                     Dav1dGpuUnit u;
                     memset(&u, 0, sizeof(u));
                     u.dst_off = uy * ds_px + ux;
@@ -757,6 +801,16 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     }
                     u.p.inter.filter2d = b.filter2d;
                     u.p.inter.weight = b.weight;
+                    // WMASK: both refs' footprints; OBMC: the block's own put
+                    const int nmc = b.kind == DGPU_PRED_INTER_WMASK ? 2 : b.kind == DGPU_PRED_INTER_OBMC ? 1 : 0;
+                    for (int k = 0; k < nmc; k++) {
+                        const int rr = b.ref[k], ix = ux + (b.mvx[k] >> 4), iy = uy + (b.mvy[k] >> 4);
+                        if (!mc_inside(rr, ix, iy)) {
+                            u.p.inter.src_off[k] = mc_emu(rr, ix, iy);
+                            u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
+                            xf |= k ? CellPart::F_EMU1 : CellPart::F_EMU0;
+                        }
+                    }
                     int32_t ao = 0;
                     if (b.kind == DGPU_PRED_INTER_WMASK) {
                         ao = P.wm_off + (oy >> 1) * P.wm_w + (ox >> 1);
@@ -766,10 +820,46 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         memcpy(&P.auxp[ao], bdata, 8);
                         for (int sy = 0; sy < ny; sy++)
                             memcpy(&P.auxp[ao + 16 + 8 * sy * nx], bdata + 16 + 8 * ((oy / 8 + sy) * gw + ox / 8), 8 * nx);
+                        // warp_affine's emu_edge (src/recon_tmpl.c:1168-1177): an
+                        // 8x8 reads 15 x 15 pixels at (x - 3, y - 3); the kernel's
+                        // aligned loads reach 16 bytes past column x + 11.  When
+                        // any 8x8 of the unit leaves the picture, every 8x8 of it
+                        // is read from a clamped copy (exact for the ones inside):
+                        // 15-row strips, 8x8s 16 px apart, positions rewritten to
+                        // the copy and the strip base in src_off[0] (the kernel
+                        // adds it); otherwise src_off[0] = 0
+                        const int rr = b.ref[0], rw = ref[rr][p].w, rh = ref[rr][p].h;
+                        bool all_in = true;
+                        for (int i = 0; i < nx * ny && all_in; i++) {
+                            int16_t xy[2];
+                            memcpy(xy, &P.auxp[ao + 16 + 8 * i], 4);
+                            all_in = xy[0] - 3 >= 0 && xy[1] - 3 >= 0 && xy[0] + 12 <= rw && xy[1] + 12 <= rh &&
+                                     (xy[1] + 12 < rh || (int64_t)(xy[0] + 12) * bpp + 16 <= ref[rr][p].stride);
+                        }
+                        u.p.inter.src_off[0] = 0;
+                        if (!all_in) {
+                            const int32_t band = P.emu_rows * kEmuStride;
+                            for (int sy = 0; sy < ny; sy++)
+                                for (int sx = 0; sx < nx; sx++) {
+                                    uint8_t *e8 = &P.auxp[ao + 16 + 8 * (sy * nx + sx)];
+                                    int16_t xy[2];
+                                    memcpy(xy, e8, 4);
+                                    P.emu.push_back(EmuJob{xy[0] - 3, xy[1] - 3, band + 15 * sy * kEmuStride + 16 * sx, 15, 15,
+                                                           (uint8_t)rr, (uint8_t)p});
+                                    const int16_t nxy[2] = {(int16_t)(16 * sx + 3), (int16_t)(15 * sy + 3)};
+                                    memcpy(e8, nxy, 4);
+                                }
+                            P.emu_rows += 15 * ny;
+                            u.p.inter.src_off[0] = band;
+                            u.p.inter.ref[0] = (uint8_t)DGPU_REC_EMU_SLOT;
+                            xf |= CellPart::F_EMU0;
+                        }
                     } else if (b.kind == DGPU_PRED_INTER_OBMC) {   // the laps overlapping the unit
                         const int n = *(const int32_t *)bdata;
                         const ObmcBlockLap *lb = (const ObmcBlockLap *)(bdata + 16);
                         std::vector<ObmcUnitLap> ents;
+                        std::vector<int> emu_ents;   // laps read through the scratch (the lap's
+                                                     // prediction reads the unit's whole footprint)
                         for (int k = 0; k < n; k++) {
                             const ObmcBlockLap &e = lb[k];
                             const int x0 = std::max((int)e.x0 - ox, 0), x1 = std::min((int)e.x1 - ox, uw);
@@ -786,6 +876,12 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                             q.x0 = (uint8_t)x0, q.y0 = (uint8_t)y0, q.x1 = (uint8_t)x1, q.y1 = (uint8_t)y1;
                             q.lap_w4 = e.lap_w4, q.lap_h4 = e.lap_h4, q.dir = e.dir;
                             q.mask_off = (uint8_t)(e.mask_off + (e.dir ? ox : oy));
+                            const int ix = ux + (e.mvx >> 4), iy = uy + (e.mvy >> 4);
+                            if (!mc_inside(e.ref, ix, iy)) {
+                                q.src_off = mc_emu(e.ref, ix, iy);
+                                q.ref = (uint8_t)DGPU_REC_EMU_SLOT;
+                                emu_ents.push_back((int)ents.size());
+                            }
                             ents.push_back(q);
                         }
                         ao = P.aux_alloc(16 + 16 * ents.size());
@@ -793,6 +889,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         memset(&P.auxp[ao], 0, 16);
                         memcpy(&P.auxp[ao], &ne, 4);
                         if (ne) memcpy(&P.auxp[ao + 16], ents.data(), 16 * ents.size());
+                        for (const int k : emu_ents) P.emu_auxfix.push_back(ao + 16 + 16 * k);   // (src_off first)
                     } else {   // INTER_SCALED: the unit's integer position and phase (running sums)
                         const int n = *(const int32_t *)bdata;
                         const ScaledBlockRef *sb = (const ScaledBlockRef *)(bdata + 16);
@@ -800,19 +897,33 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         memset(&P.auxp[ao], 0, 16 + 16 * (size_t)n);
                         memcpy(&P.auxp[ao], &n, 4);
                         for (int k = 0; k < n; k++) {
-                            const int rs = (int)(ref[b.ref[k]][p].stride / bpp);
+                            const int rr = b.ref[k];
+                            const int rs = (int)(ref[rr][p].stride / bpp);
                             const int px_ = sb[k].mx + ox * sb[k].dx, py_ = sb[k].my + oy * sb[k].dy;
+                            const int ix = sb[k].x + (px_ >> 10), iy = sb[k].y + (py_ >> 10);
                             ScaledUnitRef q;
-                            q.src_off = (sb[k].y + (py_ >> 10)) * rs + sb[k].x + (px_ >> 10);
+                            q.src_off = iy * rs + ix;
                             q.mx = (uint16_t)(px_ & 1023), q.my = (uint16_t)(py_ & 1023);
                             q.dx = sb[k].dx, q.dy = sb[k].dy;
                             q.pad_ = 0;
+                            // the scaled mc()'s emu_edge (src/recon_tmpl.c:1036-1046): the
+                            // kernel reads columns ix - 3 .. ((mx + (W - 1) dx) >> 10) + 4
+                            // past ix and rows iy - 3 .. ((my + (H - 1) dy) >> 10) + 4 past iy
+                            // (its row count capped at 2H + 8), pixel by pixel
+                            const int fw = ((q.mx + (uw - 1) * q.dx) >> 10) + 8;
+                            const int fh = std::min(((q.my + (uh - 1) * q.dy) >> 10) + 8, 2 * uh + 8);
+                            if (ix - 3 < 0 || iy - 3 < 0 || ix - 3 + fw > ref[rr][p].w || iy - 3 + fh > ref[rr][p].h) {
+                                q.src_off = P.emu_band(ix - 3, iy - 3, fw, fh, rr, p) + 3 * kEmuStride + 3;
+                                u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
+                                P.emu_auxfix.push_back(ao + 16 + 16 * k);
+                            }
                             memcpy(&P.auxp[ao + 16 + 16 * k], &q, 16);
                         }
                         if (n == 1) u.p.inter.weight = 0;
                     }
                     P.xunits.push_back(u);
                     P.xaux.push_back(ao);
+                    P.xfix.push_back(xf);
                 }
         }
         // the transform cells; an INTER_INTRA block first gets one cell for
@@ -896,12 +1007,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                             const bool inside = ix - 3 >= 0 && iy - 3 >= 0 && ix + ctw + 4 <= rw &&
                                                 iy + cth + 4 <= rh && (iy + cth + 4 < rh || (ix + ctw + 4) * bpp + 16 <= rs * bpp);
                             if (!inside) {
-                                P.emu.push_back(EmuJob{ix - 3, iy - 3, P.emu_rows, (uint8_t)(ctw + 7), (uint8_t)(cth + 7),
-                                                        (uint8_t)rr, (uint8_t)p});
-                                u.p.inter.src_off[k] = (P.emu_rows + 3) * kEmuStride + 3;
+                                u.p.inter.src_off[k] = P.emu_band(ix - 3, iy - 3, ctw + 7, cth + 7, rr, p) + 3 * kEmuStride + 3;
                                 fix |= k ? CellPart::F_EMU1 : CellPart::F_EMU0;
                                 u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
-                                P.emu_rows += cth + 7;
                             }
                         }
                     }
@@ -1047,12 +1155,21 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         }
         for (size_t i = 0; i < P.emu.size(); i++) {
             EmuJob e = P.emu[i];
-            e.r0 += er;
+            e.o0 += er * kEmuStride;
             r->emu[eb0[t] + i] = e;
         }
         for (size_t i = 0; i < P.xunits.size(); i++) {
-            xunits[xb0[t] + i] = P.xunits[i];
+            Dav1dGpuUnit u = P.xunits[i];
+            if (P.xfix[i] & CellPart::F_EMU0) u.p.inter.src_off[0] += er * kEmuStride;
+            if (P.xfix[i] & CellPart::F_EMU1) u.p.inter.src_off[1] += er * kEmuStride;
+            xunits[xb0[t] + i] = u;
             xaux[xb0[t] + i] = P.xaux[i] + ab;
+        }
+        for (const int32_t o : P.emu_auxfix) {   // OBMC laps / scaled refs read through the scratch
+            int32_t v;
+            memcpy(&v, &auxp[(size_t)ab + o], 4);
+            v += er * kEmuStride;
+            memcpy(&auxp[(size_t)ab + o], &v, 4);
         }
     };
     r->pool->run(nt, join_part);
@@ -1311,6 +1428,13 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         (nx && (r->d_xunits.grow(bxu) || r->d_xaux.grow(bxa))))
         return -3;
     const uint8_t *pin = img;
+    // once a copy from the pinned image may be queued, a failure drains the
+    // stream before returning: a retry rewrites that image and may regrow the
+    // device buffers, which the queued copies and kernels still use
+    auto drained = [&](int rc) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    };
     if ((bu && hipMemcpyAsync(r->d_units.p, pin, bu, hipMemcpyHostToDevice, st)) ||
         (br && hipMemcpyAsync(r->d_recs.p, pin + bu, br, hipMemcpyHostToDevice, st)) ||
         (bc && hipMemcpyAsync(r->d_coef.p, pin + o_c, bc, hipMemcpyHostToDevice, st)) ||
@@ -1319,7 +1443,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         (nx && hipMemcpyAsync(r->d_xunits.p, pin + o_xu, bxu, hipMemcpyHostToDevice, st)) ||
         (nx && hipMemcpyAsync(r->d_xaux.p, pin + o_xa, bxa, hipMemcpyHostToDevice, st)) ||
         (bp && hipMemcpyAsync(r->d_auxp.p, pin + o_p, bp, hipMemcpyHostToDevice, st)))
-        return -3;
+        return drained(-3);
     if (be) {   // the clamped footprints, before the wavefront reads them
         EmuArgs ea;
         memset(&ea, 0, sizeof(ea));
@@ -1333,14 +1457,38 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         ea.out = r->d_emu.p;
         ea.jobs = (const EmuJob *)r->d_emu_jobs.p;
         ea.n = (int32_t)r->emu.size();
+        ea.rows = emu_rows;
         if (r->bpc == 8)
             k_emu_footprints<uint8_t><<<dim3(ea.n), 64, 0, st>>>(ea);
         else
             k_emu_footprints<uint16_t><<<dim3(ea.n), 64, 0, st>>>(ea);
-        if (hipGetLastError() != hipSuccess) return -3;
+        if (hipGetLastError() != hipSuccess) return drained(-3);
     }
     s.workspace = r->d_work.p;
     s.workspace_bytes = wsb;
+#if DGPU_BOUNDS
+    {   // every buffer of this flush with its exact byte size (whole 16-B
+        // blocks: Stage reads the 16-B blocks holding a region's first and
+        // last byte), for the launches' range tables
+        auto &bx = dgpu::bnd_extra();
+        bx.clear();
+        auto reg = [&](const void *p, size_t nb, int id) {
+            if (p && nb) bx.push_back(dgpu::BndRange{p, (nb + 15) & ~(size_t)15, id});
+        };
+        reg(r->d_units.p, bu, dgpu::BND_UNITS);
+        reg(r->d_recs.p, br, dgpu::BND_RECS);
+        reg(r->d_coef.p, bc, dgpu::BND_COEF);
+        reg(r->d_edges.p, edge_px * bpp, dgpu::BND_EDGES);
+        reg(r->d_aux.p, ba, dgpu::BND_AUX);
+        reg(r->d_auxp.p, bp, dgpu::BND_AUXPOOL);
+        reg(r->d_work.p, (size_t)wsb, dgpu::BND_WORK);
+        if (be) reg(r->d_emu.p, (size_t)emu_rows * kEmuStride * bpp, dgpu::BND_EMU);
+        if (nx) {
+            reg(r->d_xunits.p, bxu, dgpu::BND_XUNITS);
+            reg(r->d_xaux.p, bxa, dgpu::BND_XAUX);
+        }
+    }
+#endif
     Dav1dGpuFrameBatch fb;
     memset(&fb, 0, sizeof(fb));
     Dav1dGpuIntraEdgeBatch eb;
@@ -1372,7 +1520,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         for (int k = 0; k < NC; k++) xb.class_warp[k] = x_class[k + 1] - x_class[k];
         xb.aux = (const int32_t *)r->d_xaux.p;
         const int xrc = r->bpc == 8 ? dav1d_gpu_recon_8bpc(&xb, stream) : dav1d_gpu_recon_16bpc(&xb, stream);
-        if (xrc) return xrc;
+        if (xrc) return drained(xrc);
     }
     eb.units = (Dav1dGpuUnit *)r->d_units.p;
     eb.edges = r->d_edges.p;
@@ -1384,14 +1532,17 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         const int rc = r->bpc == 8 ? dav1d_gpu_recon_intra_frame_8bpc(&fb, &eb, &s, stream)
                                    : dav1d_gpu_recon_intra_frame_16bpc(&fb, &eb, &s, stream);
         lap("launch");
-        if (rc) return rc;
+        if (rc) return drained(rc);
     }
-    if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return -3;
+#if DGPU_BOUNDS
+    dgpu::bnd_extra().clear();   // this flush's launches have their tables
+#endif
+    if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return drained(-3);
     // the wavefront's error word (workspace int32 [1]) follows on the stream
     if (n && (r->flag.grow(16) ||
               hipMemcpyAsync(r->flag.p, (const int32_t *)r->d_work.p + 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess))
-        return -3;
-    if (hipEventRecord(r->done, st) != hipSuccess) return -3;
+        return drained(-3);
+    if (hipEventRecord(r->done, st) != hipSuccess) return drained(-3);
     r->pending_check = n > 0;
     drop_recording();
     return 0;

@@ -7,9 +7,21 @@
 
 #include <atomic>
 
+#include "bounds.hpp"
 #include "dav1d_gpu.h"
 
 namespace dgpu {
+
+std::mutex &fallback_mutex() {
+    static std::mutex m;
+    return m;
+}
+
+// DGPU_BOUNDS builds: the calling thread's registered device buffers
+std::vector<BndRange> &bnd_extra() {
+    static thread_local std::vector<BndRange> v;
+    return v;
+}
 
 // ---- sticky error ------------------------------------------
 static std::atomic<int> g_error{0};        // first latched error, 0 = none

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+
+#include <mutex>
 #include <vector>
 
 namespace dgpu {
@@ -30,8 +32,19 @@ bool gpu_usable();                             // no error latched
 // The caller's table entries before a _gpu_ hook overwrote them: every slot
 // of `caller` that is not the GPU entry itself (a second hook call must not
 // make the GPU its own fallback).  Contexts are arrays of function pointers.
+// Decoders of one process may run their init hooks on several threads at
+// once: the saves are serialised.  The itx and loop-restoration hooks take
+// the bit depth (the reference's arch code installs different 10- and 12-bit
+// entries, src/x86/itx.h, src/x86/looprestoration.h:62-88), so their 16bpc
+// fallbacks are one table per bit depth, chosen by bitdepth_max at the call;
+// the other hooks have none (the reference installs the same entries for 10
+// and 12 bit).
+std::mutex &fallback_mutex();
+inline int fb16_slot(int bpc) { return bpc == 12; }
+inline int fb16_slot_bdmax(int bitdepth_max) { return bitdepth_max > 1023; }
 template <typename Ctx>
 inline void save_fallback(Ctx *fb, const Ctx *caller, const Ctx *gpu) {
+    std::lock_guard<std::mutex> lock(fallback_mutex());
     constexpr int n = sizeof(Ctx) / sizeof(void *);
     static_assert(sizeof(Ctx) % sizeof(void *) == 0, "function-pointer tables only");
     void *const *c = reinterpret_cast<void *const *>(caller);

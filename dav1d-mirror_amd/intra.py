@@ -710,7 +710,8 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
             mvx = np.where(ip_ > 0, mvx >> 1, mvx)
             mvy = np.where(ip_ > 0, mvy >> 1, mvy)
             sx, sy = ux[interu] + (mvx >> 4), uy[interu] + (mvy >> 4)
-            iv[f"src_off{k}"] = sy * ref_stride[ip_] + sx
+            # WARP: the 8x8 positions are absolute (src_off, their base, 0)
+            iv[f"src_off{k}"] = np.where(predu[interu] == abi.PRED_WARP, 0, sy * ref_stride[ip_] + sx)
             iv[f"mx{k}"] = mvx & 15
             iv[f"my{k}"] = mvy & 15
             iv[f"ref{k}"] = k

@@ -251,9 +251,11 @@ enum Dav1dGpuPredKind {
                                 16-byte aligned record: int16 abcd[4], 8 pad
                                 bytes, then per 8x8 (row-major) int16 x, y
                                 (the warp source position in the ref plane:
-                                dx, dy of recon_tmpl.c:1162-1167), int16
-                                mx >> 6, int16 my >> 6 (warp_affine clears
-                                their low 6 bits, :1163-1167)                */
+                                dx, dy of recon_tmpl.c:1162-1167, relative
+                                to pixel p.inter.src_off[0] of the plane,
+                                normally 0), int16 mx >> 6, int16 my >> 6
+                                (warp_affine clears their low 6 bits,
+                                :1163-1167)                                  */
     DGPU_PRED_INTER_INTRA = 9,/* inter-intra: mc put from ref 0, intra_pred
                                 into a tile, then blend (src/mc_tmpl.c:
                                 641-653, recon_tmpl.c:1540-1580).  aux[unit]
@@ -792,10 +794,11 @@ int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int y, int tx,
  * INTER_WMASK / OBMC / SCALED / WARP predictions run in a launch of their own
  * ahead of the wavefront (dav1d_gpu_recon_*'s second launch), cut into
  * prediction units of at most 32 x 32; their residuals are added by PRED_NONE
- * units in the wavefront.  Those four kinds read their references directly:
- * the reference planes need the padding the unit batch documents (the
- * emu_edge clamp covers INTER / INTER_AVG / INTER_WAVG / INTER_MASK /
- * INTER_INTRA).  0 or -1. */
+ * units in the wavefront.  Their reads are clamped like every other kind's:
+ * mc()'s emu_edge decision per unit and reference (translation footprints
+ * and OBMC laps src/recon_tmpl.c:986-999, scaled :1036-1046 with steps of
+ * 1..2048, warp 15 x 15 per 8x8 :1168-1177), a footprint leaving the
+ * reference being read from a clamped copy.  0 or -1. */
 int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, const void *aux, size_t aux_bytes);
 /* Build, upload and launch everything recorded since the last flush on
  * `stream` (the recorder waits for its previous flush before reusing its

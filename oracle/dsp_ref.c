@@ -1586,7 +1586,9 @@ int SFX(oracle_recon_units)(const Dav1dGpuFrameBatch *b, int u0, int u1)
                     int16_t xy[2], mxy[2];   /* the 8x8's source position, mx >> 6, my >> 6 */
                     memcpy(xy, sb, 4);
                     memcpy(mxy, sb + 4, 4);
-                    const pixel *src = (const pixel *)b->ref[r][pl].data + xy[1] * PX(ss) + xy[0];
+                    /* src_off[0]: the base the positions are relative to (the
+                     * recorder's clamped-copy strip; 0 otherwise) */
+                    const pixel *src = (const pixel *)b->ref[r][pl].data + u->p.inter.src_off[0] + xy[1] * PX(ss) + xy[0];
                     warp8x8(dst + 8 * sy * PX(ds) + 8 * sx, ds, NULL, 0, src, ss, abcd, mxy[0] * 64, mxy[1] * 64,
                             bdmax);
                 }

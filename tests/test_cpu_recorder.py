@@ -111,6 +111,16 @@ def test_recorder_block_aux_validation(pkg):
         assert rec(obmc[:-1].tobytes(), kind=abi.PRED_INTER_OBMC) == -1
         sc = np.zeros(16 + 16 * 2, np.uint8)
         sc[0] = 2
+        st = sc[16:].view("<u2").reshape(2, 8)   # per ref: x, y (int32), mx, my, dx, dy
+        st[:, 6:8] = 1024
+        assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == 0
+        st[1, 6] = 0                                                          # steps 1..2048 (2x at most)
+        assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == -1
+        st[1, 6] = 2049
+        assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == -1
+        st[1, 6], st[1, 4] = 2048, 1024                                       # phases 0..1023
+        assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == -1
+        st[1, 4] = 1023
         assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == 0
         sc[0] = 3
         assert rec(sc.tobytes(), kind=abi.PRED_INTER_SCALED) == -1

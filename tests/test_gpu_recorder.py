@@ -154,18 +154,26 @@ def test_recorder_rejects_missing_reference(oracle):
     rec.close()
 
 
-@pytest.mark.parametrize("bpc,bdmax,seed", [(8, 255, 61), (16, 1023, 62), (16, 4095, 63)])
-def test_recorder_unpadded_references(oracle, bpc, bdmax, seed):
+@pytest.mark.parametrize("bpc,bdmax,seed,ext", [(8, 255, 61, 0.0), (16, 1023, 62, 0.0), (16, 4095, 63, 0.0),
+                                                  (8, 255, 64, 0.8), (16, 1023, 65, 0.8), (16, 4095, 66, 0.8)])
+def test_recorder_unpadded_references(oracle, bpc, bdmax, seed, ext):
     """References without padding and MVs up to 200 px past the picture
     (VERDICT r2): every read is clamped to the picture, as mc()'s emu_edge
     copy makes it (src/recon_tmpl.c:986-999).  The device gets exact-size
     reference planes (stride = width, so an unclamped read lands on another
-    row); the oracle reads edge-replicated copies padded past every MV."""
+    row); the oracle reads edge-replicated copies padded past every MV.
+    With ext: the launch-ahead kinds too: WARP 8x8 origins,
+    INTER_WMASK / OBMC lap MVs and scaled positions up to 200 px outside
+    (scaled :1036-1046, warp :1168-1177)."""
     import torch
+    import dav1d_mirror_amd.abi as abi
     import dav1d_mirror_amd.intra as intra
     fr = intra.make_intra_frame(intra.IntraConfig(seed=seed, width=384, height=256, bpc=bpc, bitdepth_max=bdmax,
-                                                  inter_frac=0.8, mv_range=200, ref_pad=288,
+                                                  inter_frac=0.8, mv_range=200, ref_pad=288, ext_frac=ext,
                                                   sb_edge_backup=False))
+    if ext:
+        kinds = set(int(k) for k in fr.units["pred"])
+        assert {abi.PRED_WARP, abi.PRED_INTER_WMASK, abi.PRED_INTER_OBMC, abi.PRED_INTER_SCALED} <= kinds
     hbd = bpc != 8
     dst = [torch.zeros((h, w), dtype=torch.int16 if hbd else torch.uint8, device="cuda:0") for (w, h) in fr.plane_wh]
     pad = fr.cfg.ref_pad
