@@ -292,12 +292,10 @@ __global__ __launch_bounds__(64) void k_emu_footprints(EmuArgs a) {
     }
 }
 
-// per 4x4 cell of a plane: the level and the decode-order cell that last
-// wrote it, side by side (one cache line per lookup).  `own` is stored as
-// the flush's cell base + the cell index, so the maps are never cleared: an
-// entry whose own is below the current base was written by an earlier flush
-// (no producer, level -1 for the level rule).
-struct LvOwn { int32_t lv, own; };
+// per 4x4 cell of a plane: the decode-order cell that last wrote it, stored
+// as the flush's cell base + the cell index, so the maps are never cleared:
+// an entry below the current base was written by an earlier flush (no
+// producer, level -1 for the level rule).
 
 struct Unit {   // a transform cell before sorting
     Dav1dGpuUnit u;
@@ -313,7 +311,8 @@ struct Unit {   // a transform cell before sorting
 struct LvJob {
     int16_t x4, y4, W4, H4;
     uint8_t p, cw4, ch4, nd, fl, fix;
-    enum { HL = 1, HT = 2, TR = 4, BL = 8, CFL = 16, IIRES = 32 };
+    int32_t link;   // IIRES: its block's inter-intra prediction cell (part-local until the join)
+    enum { HL = 1, HT = 2, TR = 4, BL = 8, CFL = 16, IIRES = 32, IIC = 64 };
 };
 
 // one thread's run of blocks, cut into cells with part-local offsets
@@ -424,10 +423,13 @@ struct Dav1dGpuRecorder {
     std::vector<Dav1dGpuUnit> xunits;   // the launch ahead of the wavefront (class order)
     std::vector<int32_t> xaux;
     std::vector<uint8_t> h_host;   // DAV1D_GPU_REC_HOSTONLY: stands in for the pinned buffer
-    // per-4x4 maps kept across flushes (generation-stamped, see LvOwn):
-    // the residual recorded at each cell (index + res_base) and LvOwn
+    // per-4x4 maps kept across flushes (generation-stamped): the residual
+    // recorded at each cell (index + res_base) and its writer (cell_base + cell)
     std::vector<int32_t> res_at[3];
-    std::vector<LvOwn> lvown[3];
+    std::vector<int32_t> own[3];
+    std::vector<int32_t> lv;                 // per decode-order cell: its level
+    std::vector<int32_t> prod_cnt;           // per decode-order cell: its producer count
+    std::vector<std::vector<int32_t>> tprod; // producers found by each worker (its cell range)
     int32_t map_w4[3] = {0, 0, 0}, map_h4[3] = {0, 0, 0};
     int32_t res_base = 0, cell_base = 0;
     PinnedBuf pin;   // units | recs | coefficients | emu jobs, written in place by the fill
@@ -690,7 +692,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         if (reset) {
             for (int p = 0; p < 3; p++) {
                 r->res_at[p].assign((size_t)mw[p] * mh[p], -1);
-                r->lvown[p].assign((size_t)mw[p] * mh[p], LvOwn{-1, -1});
+                r->own[p].assign((size_t)mw[p] * mh[p], -1);
                 r->map_w4[p] = mw[p];
                 r->map_h4[p] = mh[p];
             }
@@ -716,9 +718,6 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     //    sequential layout), and one sequential pass assigns the levels and
     //    producers, which follow decode order.
     std::vector<Unit> &cells = r->cells;
-    // per 4x4: level and the decode-order cell writing it, side by side (one
-    // cache line per lookup)
-    std::vector<LvOwn> *lvown = r->lvown;
     lap("maps");
     std::vector<int32_t> &prod_start = r->prod_start, &prod = r->prod;
     std::vector<uint8_t> &auxp = r->auxp;
@@ -932,6 +931,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         // residual-only cells that read it
         const bool iib = b.kind == DGPU_PRED_INTER_INTRA;
         const int ncx = (bwc + t.w - 1) / t.w, ncy = (bhc + t.h - 1) / t.h;
+        const int32_t iic_at = (int32_t)P.cells.size();   // the inter-intra block's prediction cell
         for (int k = iib ? -1 : 0; k < ncx * ncy; k++)
             {
                 const bool iic = k < 0;
@@ -1079,8 +1079,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 j.fl = (uint8_t)((hl ? LvJob::HL : 0) | (ht ? LvJob::HT : 0) |
                                  ((e.flags & DGPU_IE_TOP_HAS_RIGHT) ? LvJob::TR : 0) |
                                  ((e.flags & DGPU_IE_LEFT_HAS_BOTTOM) ? LvJob::BL : 0) | (cfl ? LvJob::CFL : 0) |
-                                 ((iib && !iic) ? LvJob::IIRES : 0));
+                                 ((iib && !iic) ? LvJob::IIRES : 0) | (iic ? LvJob::IIC : 0));
                 j.fix = fix;
+                j.link = iib && !iic ? iic_at : -1;
             }
         return 0;
     };
@@ -1151,7 +1152,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 memcpy(&auxp[(size_t)c.aux + 8], &mo, 4);
             }
             cells[cb0[t] + i] = c;
-            r->jobs[cb0[t] + i] = P.jobs[i];
+            LvJob j = P.jobs[i];
+            if (j.link >= 0) j.link += (int32_t)cb0[t];
+            r->jobs[cb0[t] + i] = j;
         }
         for (size_t i = 0; i < P.emu.size(); i++) {
             EmuJob e = P.emu[i];
@@ -1174,89 +1177,123 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     };
     r->pool->run(nt, join_part);
     lap("cells");
-    // levels and producers, in decode order: a cell sits one level above
-    // every pixel its edges (or CfL luma, or an inter-intra residual's
-    // prediction) read; its producers are the cells that wrote them.  A
-    // pixel no cell of this flush wrote came from an earlier flush on the
-    // same stream: no producer, level 0 for it
-    prod_start.assign(1, 0);
-    prod.clear();
-    prod_start.reserve(n_cells + 1);
-    for (size_t ci = 0; ci < n_cells; ci++) {
-        const LvJob &j = r->jobs[ci];
-        const int p = j.p, w4p = mw[p], x4 = j.x4, y4 = j.y4, cw4 = j.cw4, ch4 = j.ch4, W4 = j.W4, H4 = j.H4;
-        const int nd = j.nd;
-        const bool hl = j.fl & LvJob::HL, ht = j.fl & LvJob::HT;
-        const LvOwn *mp = lvown[p].data();
-        const size_t p0 = prod.size();
-        int d = -1;
-        auto cell = [&](int cx, int cy) {
-            const LvOwn m = mp[(size_t)cy * w4p + cx];
-            if (m.own < cell_base) return;   // an earlier flush's pixel: level -1, no producer
-            d = std::max(d, m.lv);
-            const int32_t o = m.own - cell_base;
-            if (prod.size() == p0 || prod.back() != o) prod.push_back(o);
-        };
-        if (nd & 1) {
-            if (hl) {
-                for (int q = y4; q < std::min(y4 + ch4, H4); q++) cell(x4 - 1, q);
-                if ((nd & 16) && y4 + ch4 < H4 && (j.fl & LvJob::BL))
-                    for (int q = y4 + ch4; q < std::min(y4 + 2 * ch4, H4); q++) cell(x4 - 1, q);
-            } else if (ht) {
-                cell(x4, y4 - 1);
-            }
-        }
-        if (nd & 2) {
-            if (ht) {
-                for (int q = x4; q < std::min(x4 + cw4, W4); q++) cell(q, y4 - 1);
-                if ((nd & 8) && x4 + cw4 < W4 && (j.fl & LvJob::TR))
-                    for (int q = x4 + cw4; q < std::min(x4 + 2 * cw4, W4); q++) cell(q, y4 - 1);
-            } else if (hl) {
-                cell(x4 - 1, y4);
-            }
-        }
-        if (j.fl & LvJob::IIRES)   // the residual reads the block's inter-intra prediction
-            for (int cy = y4; cy < y4 + ch4; cy++)
-                for (int cx = x4; cx < x4 + cw4; cx++) cell(cx, cy);
-        if (nd & 4) {
-            if (hl && ht) cell(x4 - 1, y4 - 1);
-            else if (hl) cell(x4 - 1, y4);
-            else if (ht) cell(x4, y4 - 1);
-        }
-        if (j.fl & LvJob::CFL) {
-            const int lw4 = mw[0];
-            const LvOwn *ml = lvown[0].data();
-            for (int cy = 2 * y4; cy < 2 * (y4 + ch4); cy++)
-                for (int cx = 2 * x4; cx < 2 * (x4 + cw4); cx++) {
-                    const LvOwn m = ml[(size_t)cy * lw4 + cx];
-                    if (m.own < cell_base) continue;   // luma of an earlier flush: no producer
-                    d = std::max(d, m.lv);
-                    const int32_t o = m.own - cell_base;
-                    if (prod.size() == p0 || prod.back() != o) prod.push_back(o);
+    // levels and producers: a cell sits one level above every pixel its
+    // edges (or CfL luma, or an inter-intra residual's prediction) read; its
+    // producers are the cells that wrote them.  A pixel no cell of this flush
+    // wrote came from an earlier flush on the same stream: no producer, level
+    // 0 for it.  Three steps, the first two on the worker pool:
+    //   1. every cell stamps its 4x4s in the writer map (the only overlap in a
+    //      flush: an inter-intra block's prediction cell under its residual
+    //      cells, which come after it in decode order and win);
+    //   2. every cell looks its producers up (a writer at or after the cell in
+    //      decode order has not written yet: none), sorted, duplicate-free;
+    //   3. the levels in decode order, from the producers' (decode order is a
+    //      topological order).
+    const int nlv = n_cells < 32768 ? 1 : r->pool->size();
+    {
+        auto stamp = [&](size_t ci, bool iic_pass) {
+            const LvJob &j = r->jobs[ci];
+            const bool iic = j.fl & LvJob::IIC;
+            if (iic != iic_pass) return;
+            int32_t *wp = r->own[j.p].data();
+            const int w4p = mw[j.p];
+            const int32_t v = cell_base + (int32_t)ci;
+            for (int cy = j.y4; cy < j.y4 + j.ch4; cy++)
+                for (int cx = j.x4; cx < j.x4 + j.cw4; cx++) {
+                    int32_t &o = wp[(size_t)cy * w4p + cx];
+                    if (!iic_pass || o < cell_base) o = v;   // (under its residual cells: theirs)
                 }
-        }
-        if (prod.size() - p0 > 1) {   // sorted, duplicate-free (lists are short: insertion sort)
-            int32_t *q = prod.data() + p0;
-            const size_t m = prod.size() - p0;
-            size_t u = 1;
-            for (size_t a = 1; a < m; a++) {
-                const int32_t v = q[a];
-                size_t b = u;
-                while (b > 0 && q[b - 1] > v) b--;
-                if (b > 0 && q[b - 1] == v) continue;   // a duplicate
-                for (size_t c = u; c > b; c--) q[c] = q[c - 1];
-                q[b] = v;
-                u++;
+        };
+        r->pool->run(nlv, [&](int t) {
+            for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) stamp(ci, false);
+        });
+        r->pool->run(nlv, [&](int t) {
+            for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) stamp(ci, true);
+        });
+    }
+    r->prod_cnt.resize(n_cells);
+    if (r->tprod.size() < (size_t)nlv) r->tprod.resize(nlv);
+    r->pool->run(nlv, [&](int t) {
+        std::vector<int32_t> &out = r->tprod[t];
+        out.clear();
+        for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) {
+            const LvJob &j = r->jobs[ci];
+            const int p = j.p, w4p = mw[p], x4 = j.x4, y4 = j.y4, cw4 = j.cw4, ch4 = j.ch4, W4 = j.W4, H4 = j.H4;
+            const int nd = j.nd;
+            const bool hl = j.fl & LvJob::HL, ht = j.fl & LvJob::HT;
+            const int32_t *mp = r->own[p].data();
+            const int32_t lo = cell_base, hi = cell_base + (int32_t)ci;   // this flush, before the cell
+            const size_t p0 = out.size();
+            auto put = [&](int32_t o) {
+                if (o < lo || o >= hi) return;
+                o -= cell_base;
+                if (out.size() == p0 || out.back() != o) out.push_back(o);
+            };
+            auto cell = [&](int cx, int cy) { put(mp[(size_t)cy * w4p + cx]); };
+            if (nd & 1) {
+                if (hl) {
+                    for (int q = y4; q < std::min(y4 + ch4, H4); q++) cell(x4 - 1, q);
+                    if ((nd & 16) && y4 + ch4 < H4 && (j.fl & LvJob::BL))
+                        for (int q = y4 + ch4; q < std::min(y4 + 2 * ch4, H4); q++) cell(x4 - 1, q);
+                } else if (ht) {
+                    cell(x4, y4 - 1);
+                }
             }
-            prod.resize(p0 + u);
+            if (nd & 2) {
+                if (ht) {
+                    for (int q = x4; q < std::min(x4 + cw4, W4); q++) cell(q, y4 - 1);
+                    if ((nd & 8) && x4 + cw4 < W4 && (j.fl & LvJob::TR))
+                        for (int q = x4 + cw4; q < std::min(x4 + 2 * cw4, W4); q++) cell(q, y4 - 1);
+                } else if (hl) {
+                    cell(x4 - 1, y4);
+                }
+            }
+            if (j.fl & LvJob::IIRES) put(cell_base + j.link);   // the block's inter-intra prediction
+            if (nd & 4) {
+                if (hl && ht) cell(x4 - 1, y4 - 1);
+                else if (hl) cell(x4 - 1, y4);
+                else if (ht) cell(x4, y4 - 1);
+            }
+            if (j.fl & LvJob::CFL) {
+                const int lw4 = mw[0];
+                const int32_t *ml = r->own[0].data();
+                for (int cy = 2 * y4; cy < 2 * (y4 + ch4); cy++)
+                    for (int cx = 2 * x4; cx < 2 * (x4 + cw4); cx++) put(ml[(size_t)cy * lw4 + cx]);
+            }
+            if (out.size() - p0 > 1) {   // sorted, duplicate-free (lists are short: insertion sort)
+                int32_t *q = out.data() + p0;
+                const size_t m = out.size() - p0;
+                size_t u = 1;
+                for (size_t a_ = 1; a_ < m; a_++) {
+                    const int32_t v = q[a_];
+                    size_t b_ = u;
+                    while (b_ > 0 && q[b_ - 1] > v) b_--;
+                    if (b_ > 0 && q[b_ - 1] == v) continue;   // a duplicate
+                    for (size_t c_ = u; c_ > b_; c_--) q[c_] = q[c_ - 1];
+                    q[b_] = v;
+                    u++;
+                }
+                out.resize(p0 + u);
+            }
+            r->prod_cnt[ci] = (int32_t)(out.size() - p0);
         }
-        prod_start.push_back((int32_t)prod.size());
-        const int lv = d + 1;
-        cells[ci].level = lv;
-        LvOwn *wp = lvown[p].data();
-        const LvOwn v{lv, cell_base + (int32_t)ci};
-        for (int cy = y4; cy < y4 + ch4; cy++)
-            for (int cx = x4; cx < x4 + cw4; cx++) wp[(size_t)cy * w4p + cx] = v;
+    });
+    // the producer lists in decode order (CSR), then the levels
+    prod_start.resize(n_cells + 1);
+    prod_start[0] = 0;
+    for (size_t ci = 0; ci < n_cells; ci++) prod_start[ci + 1] = prod_start[ci] + r->prod_cnt[ci];
+    prod.resize((size_t)prod_start[n_cells]);
+    r->pool->run(nlv, [&](int t) {
+        const size_t c0 = n_cells * t / nlv;
+        if (!r->tprod[t].empty()) memcpy(&prod[(size_t)prod_start[c0]], r->tprod[t].data(), r->tprod[t].size() * 4);
+    });
+    {
+        const int32_t *ps = prod_start.data(), *pp = prod.data();
+        for (size_t ci = 0; ci < n_cells; ci++) {
+            int d = -1;
+            for (int32_t k = ps[ci]; k < ps[ci + 1]; k++) d = std::max(d, cells[pp[k]].level);
+            cells[ci].level = d + 1;
+        }
     }
     lap("levels");
     const int n = (int)cells.size();

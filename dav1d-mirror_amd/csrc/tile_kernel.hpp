@@ -1054,6 +1054,13 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         }
         for (int i = 0; i < n; i++) pmap[base + i] = (uint8_t)tid;
     }
+    // the cooperative section's padding lanes [lanes_coop_used, lanes_coop)
+    // belong to no prediction but still read one below (P2): give them
+    // record 0, so no lane indexes the record array with stale LDS (an
+    // index up to 255 past the tile's records read past the array's end:
+    // the intermittent illegal-address faults of the round-3 / round-4
+    // GPU runs)
+    for (int i = T.lanes_coop_used + tid; i < T.lanes_coop; i += kTileThreads) pmap[i] = 0;
     // zero the residual tile
     for (int i = tid; i < L::ACC / 16; i += kTileThreads) reinterpret_cast<u32x4 *>(acc)[i] = u32x4{0, 0, 0, 0};
 #pragma unroll
@@ -1092,7 +1099,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         const int lane = base + tid;
         const bool act = lane < T.lanes_tx;
         Dav1dGpuTx tx = {0, 0};
-        if (act) tx = a.txs[T.tx0 + txmap[lane]];
+        if (act) tx = a.txs[T.tx0 + min((int)txmap[lane], T.n_tx - 1)];
         const int txs = (tx.w0 >> 8) & 31, txtp = (tx.w0 >> 13) & 31;
         const int nzw = (tx.w0 >> 18) & 63, nzh = (tx.w0 >> 24) & 63;
         const int l = lane - (int)(tx.w1 >> 16);
@@ -1149,7 +1156,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         const int lane = base + tid;
         const int wlane = base + (tid & ~63);   // wave-uniform: its section
         if (lane < lanes_pred) {
-            const Dav1dGpuPred p = a.preds[T.pred0 + pmap[lane]];
+            const Dav1dGpuPred p = a.preds[T.pred0 + min((int)pmap[lane], T.n_pred - 1)];
             if (wlane < T.lanes_coop) {
                 if (lane < T.lanes_coop_used && !(DGPU_TILE_ABL & 4)) tile_coop<BPC>(a, c, p, lane - p.lane0);
             } else {

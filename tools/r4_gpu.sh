@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-4 GPU check (run through gpurun from the repo root):
+#   bash tools/r4_gpu.sh <tag> [steps...]
+# steps: tests (full -m gpu suite), stests (the same with every kernel
+# serialized, AMD_SERIALIZE_KERNEL=3, so a fault is reported at its launch), bounds (the recorder tests on the
+# DGPU_BOUNDS build, tools/build_variants.sh bounds), smoke, bench (headline
+# line), prof (rocprofv3 kernel trace of the headline), pmc (FETCH / WRITE
+# passes).  Every step has its own time limit; the first failure ends the run.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+T=${1:-r4}
+shift
+O=$R/gpurun_out/$T
+mkdir -p "$O"
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+BENCH_FAST="--no-families --no-configs --no-tiles --no-intra --no-recorder --no-grain --no-cdef --no-superres --no-lpf --no-lr --no-cpu --no-check"
+for s in "${@:-tests}"; do
+    echo "[r4] $s start $(date +%T)"
+    case $s in
+    tests) timeout -k 10 900 $PYT -m gpu -x tests > "$O/gputest.log" 2>&1 || { echo "[r4] tests failed"; exit 1; } ;;
+    stests) AMD_SERIALIZE_KERNEL=3 timeout -k 10 1200 $PYT -m gpu -x tests > "$O/gputest.log" 2>&1 || { echo "[r4] stests failed"; exit 1; } ;;
+    rectests) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_recorder.py tests/test_gpu_batch.py > "$O/rectest.log" 2>&1 || { echo "[r4] rectests failed"; exit 1; } ;;
+    bounds) DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 600 $PYT -m gpu tests/test_gpu_recorder.py > "$O/bounds.log" 2>&1
+            rc=$?; echo "[r4] bounds rc=$rc"; [ $rc -le 1 ] || exit 1 ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "[r4] smoke failed"; exit 1; } ;;
+    bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r4] bench failed"; exit 1; } ;;
+    benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r4] benchfast failed"; exit 1; } ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 50 $BENCH_FAST) > "$O/prof.log" 2>&1 || { echo "[r4] prof failed"; exit 1; } ;;
+    pmc) for c in FETCH_SIZE WRITE_SIZE; do
+             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/pmc_$c" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 $BENCH_FAST) > "$O/pmc_$c.log" 2>&1 || { echo "[r4] pmc $c failed"; exit 1; }
+         done ;;
+    esac
+    echo "[r4] $s done $(date +%T)"
+done
