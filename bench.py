@@ -259,9 +259,11 @@ def tile_breakdown(fd, dev, stream, steps):
 def intra_breakdown(cfg, dev, stream, steps):
     """an all-intra frame of the config's size and
     bitdepth reconstructed on the device by the intra wavefront
-    (dav1d_gpu_recon_intra_frame_*: persistent, one launch per frame whose
-    waves wait on their producers' tasks; levels, the same launch waiting on
-    per-level counters; and fused, one launch per level), one
+    (dav1d_gpu_recon_intra_frame_*: sb -- the headline ms_per_frame -- one
+    launch per frame, a workgroup per superblock (DGPU_IS_SB); persistent,
+    one launch per frame whose waves wait on their producers' tasks; levels,
+    the same launch waiting on per-level counters; and fused, one launch per
+    level), one
     tile and 2x2 tiles; beside it the oracle in the decoder's own order on
     one host core.  Reported beside the headline, not part of it."""
     import dav1d_mirror_amd.intra as intra
@@ -271,28 +273,30 @@ def intra_breakdown(cfg, dev, stream, steps):
         fr = intra.make_intra_frame(intra.IntraConfig(width=cfg.width, height=cfg.height, bpc=cfg.bpc,
                                                       bitdepth_max=cfg.bitdepth_max, tile_cols=tiles[0],
                                                       tile_rows=tiles[1]))
-        ms = {}
-        for mode in ("persistent", "levels", "fused"):
+        ms, got, flow_error = {}, {}, 0
+        for mode in ("sb", "persistent", "levels", "fused"):
             frame = intra.DeviceIntraFrame(fr, dev, mode=mode)
             for _ in range(2):
                 frame.launch(stream)
             ms[mode] = kernel_seconds(frame, stream, max(3, min(steps, 5)))
-            if mode == "persistent":
-                flow_error = frame.flow_error()
-                got = frame.planes_host()
+            if mode in ("sb", "persistent"):
+                flow_error |= frame.flow_error()
+                got[mode] = frame.planes_host()
             del frame
-        ks = ms["persistent"]
+        ks = ms["sb"]
         ho = orc.HostIntraFrame(fr)
         t0 = time.perf_counter()
         ho.run()
         cpu_s = time.perf_counter() - t0
         px = sum(w * h for w, h in fr.plane_wh)
-        out[name] = {"units": int(len(fr.units)), "levels": int(fr.n_levels), "ms_per_frame": round(ks * 1e3, 3),
-                     "gpix_s": round(px / ks / 1e9, 4), "us_per_level": round(ks * 1e6 / fr.n_levels, 2),
+        n_sb = len(intra.sb_schedule(fr)[3]) - 1
+        out[name] = {"units": int(len(fr.units)), "levels": int(fr.n_levels), "superblocks": n_sb,
+                     "ms_per_frame": round(ks * 1e3, 3), "gpix_s": round(px / ks / 1e9, 4),
+                     "persistent_ms_per_frame": round(ms["persistent"] * 1e3, 3),
                      "levels_ms_per_frame": round(ms["levels"] * 1e3, 3),
                      "fused_ms_per_frame": round(ms["fused"] * 1e3, 3),
                      "oracle_1core_ms": round(cpu_s * 1e3, 2), "flow_error": flow_error,
-                     "bit_exact_vs_oracle": all(bool(np.array_equal(g, o)) for g, o in zip(got, ho.dst))}
+                     "bit_exact_vs_oracle": all(bool(np.array_equal(g, o)) for m in got for g, o in zip(got[m], ho.dst))}
     return out
 
 

@@ -126,7 +126,7 @@ class IntraEdgeBatch(ctypes.Structure):
                 ("bitdepth_max", ctypes.c_int32)]
 
 
-IS_FUSED, IS_PERSISTENT = 1, 2
+IS_FUSED, IS_PERSISTENT, IS_SB = 1, 2, 4
 EDGE_BACKUP_DTYPE = np.dtype([("plane", "<i4"), ("sby", "<i4"), ("x0", "<i4"), ("w", "<i4")])
 
 
@@ -141,7 +141,11 @@ class IntraSchedule(ctypes.Structure):
                 ("workspace", ctypes.c_void_p),
                 ("workspace_bytes", ctypes.c_int64),
                 ("dep_start", ctypes.c_void_p),
-                ("deps", ctypes.c_void_p)]
+                ("deps", ctypes.c_void_p),
+                ("n_sb", ctypes.c_int32),
+                ("sb_level_start", ctypes.c_void_p),
+                ("sb_dep_start", ctypes.c_void_p),
+                ("sb_deps", ctypes.c_void_p)]
 
 
 class RecBlock(ctypes.Structure):

@@ -122,12 +122,14 @@ struct CdefTaps {
         const s2 shp = { (short)pri_shift, (short)pri_shift }, shs = { (short)sec_shift, (short)sec_shift };
         s2 sum = zero, mx = p;
         u2 mn = __builtin_bit_cast(u2, p);
+        // constrain(d) = sign(d) * min(|d|, v) with v = max(0, thr - (|d| >> shift))
+        // = median(-v, d, v) since v >= 0; v as a saturating unsigned subtract
         auto cons = [&](s2 t, s2 thr, s2 sh) {
             const s2 d = t - p;
             const s2 ad = __builtin_elementwise_max(d, zero - d);
-            const s2 v = __builtin_elementwise_min(ad, __builtin_elementwise_max(zero, thr - (ad >> sh)));
-            const s2 sg = d >> (s2){ 15, 15 };
-            return (s2)((v ^ sg) - sg);
+            const s2 v = __builtin_bit_cast(s2, __builtin_elementwise_sub_sat(__builtin_bit_cast(u2, thr),
+                                                                                __builtin_bit_cast(u2, (s2)(ad >> sh))));
+            return __builtin_elementwise_min(__builtin_elementwise_max(d, zero - v), v);
         };
 #pragma unroll
         for (int k = 0; k < 2; k++) {
@@ -154,15 +156,30 @@ struct CdefTaps {
 };
 
 // The costs of directions 2Q and 2Q+1 (cdef_find_dir_c, :246-291) from the
-// block's pixels (already (px >> bd8) - 128).
+// block's pixels px >> bd8.  The reference sums px - 128; the partial sums
+// here are of px, and each line's 128 * (its pixel count) comes off after.
 template <int Q>
 __device__ __forceinline__ void cdef_cost_pair(const int (&v)[8][8], unsigned &c0, unsigned &c1) {
     constexpr unsigned div[7] = { 840, 420, 280, 210, 168, 140, 120 };
     int a[15], b[11];
+    constexpr auto na = [](int i) {   // pixels on line i of the a / b sets
+        int n = 0;
+        for (int y = 0; y < 8; y++)
+            for (int x = 0; x < 8; x++)
+                n += (Q == 0 ? y + x : Q == 1 ? y : Q == 2 ? 7 + y - x : x) == i;
+        return n;
+    };
+    constexpr auto nb = [](int i) {
+        int n = 0;
+        for (int y = 0; y < 8; y++)
+            for (int x = 0; x < 8; x++)
+                n += (Q == 0 ? y + (x >> 1) : Q == 1 ? 3 + y - (x >> 1) : Q == 2 ? 3 - (y >> 1) + x : (y >> 1) + x) == i;
+        return n;
+    };
 #pragma unroll
-    for (int i = 0; i < 15; i++) a[i] = 0;
+    for (int i = 0; i < 15; i++) a[i] = -128 * na(i);
 #pragma unroll
-    for (int i = 0; i < 11; i++) b[i] = 0;
+    for (int i = 0; i < 11; i++) b[i] = -128 * nb(i);
 #pragma unroll
     for (int y = 0; y < 8; y++)
 #pragma unroll
@@ -369,7 +386,7 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
     const int idx = a.idx[sb];
     const int ylvl = idx >= 0 ? a.ys[idx] : 0, uvlvl = idx >= 0 && LAYOUT ? a.uvs[idx] : 0;
     const bool active = ylvl || uvlvl;   // :150-156
-    const int bd8 = bits_of(a.bdmax) - 8;
+    const int bd8 = BPC == 8 ? 0 : bits_of(a.bdmax) - 8;
     const int ypri = (ylvl >> 2) << bd8, ysec = ((ylvl & 3) + ((ylvl & 3) == 3)) << bd8;
     const int uvpri = (uvlvl >> 2) << bd8, uvsec = ((uvlvl & 3) + ((uvlvl & 3) == 3)) << bd8;
     const int damping = a.damping + bd8;
@@ -405,9 +422,9 @@ __global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
                 const uint4 r1 = *reinterpret_cast<const uint4 *>(c + y * LS + 4);
                 const uint32_t w[8] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w };
 #pragma unroll
-                for (int x = 0; x < 8; x++) {
-                    v[y][x] = ((int)(w[x] & 0xffff) >> bd8) - 128;
-                    v[y + 1][x] = ((int)(w[x] >> 16) >> bd8) - 128;
+                for (int x = 0; x < 8; x++) {   // (the - 128 is folded into cdef_cost_pair)
+                    v[y][x] = BPC == 8 ? (int)(w[x] & 0xffff) : (int)(w[x] & 0xffff) >> bd8;
+                    v[y + 1][x] = BPC == 8 ? (int)(w[x] >> 16) : (int)(w[x] >> 16) >> bd8;
                 }
             }
             cdef_costs(q, v, &cost[0][blk], 64);

@@ -201,6 +201,146 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// DGPU_IS_SB: the wavefront per superblock.  A task-per-wave kernel pays an
+// agent-scope acquire (L1 invalidate, ~1.7 us and x4 at several workgroups
+// per CU) and release (L2 write-back, 1.7-6.5 us) on every dependency step,
+// and a 4K intra frame's chain is ~1600 steps long.  Here one workgroup of
+// WPB waves owns a superblock (its luma and chroma units): it waits once for
+// the superblocks its units read (left, top, top-right, as the schedule
+// lists them), then runs the superblock's levels one after the other, each
+// level's tasks spread over its waves and the levels separated by workgroup
+// barriers -- the in-superblock hand-offs never leave the CU -- and releases
+// once.  Superblocks are taken by ticket in an order where every one comes
+// after those it waits for, so a workgroup only waits for workgroups that
+// already run (the same progress argument as k_flow); a poll bound turns a
+// stall into the error word.
+struct SbFlowArgs {
+    const FlowTask *tasks;
+    const int32_t *lvl_task_start;   // per group (superblock level): its tasks
+    const int32_t *sb_level_start;   // per superblock: its groups
+    const int32_t *sb_dep_start;     // per superblock: the superblocks it waits for
+    const int32_t *sb_deps;
+    int *ctr;                        // [0] ticket, [1] error
+    int *done;                       // per superblock: reconstructed
+    int n_sb;
+    int spin_limit;
+};
+
+template <int BPC> using KArg = __attribute__((address_space(4))) ReconArgs<BPC>;
+
+template <int BPC> __host__ __device__ constexpr int sb_waves() {
+    // waves per superblock workgroup within the CU's 160 KB of LDS
+    return cmin(4, (160 * 1024) / wave_lds<BPC, GROUP_ALL_IE>());
+}
+
+// one task of the superblock loop, out of line (the launch arguments read
+// from the kernarg segment in the call): with the class code inlined into
+// the loop the compiler hoists the argument loads and address arithmetic out
+// of it and spills ~670 VGPRs; as a call it takes 248 VGPRs and no spills
+template <int BPC>
+__device__ __noinline__ void sb_task(const KArg<BPC> *ka, const PlaneTabIE<BPC> *ptp, FlowTask task, uint8_t *wl) {
+#if defined(__HIP_DEVICE_COMPILE__)   // (the kernarg address space exists only on the device)
+    const int lane = threadIdx.x & 63;
+    const ReconArgs<BPC> ai = *(const ReconArgs<BPC> *)ka;
+    const int cls = __builtin_amdgcn_readfirstlane(task.cls);
+    const int first = __builtin_amdgcn_readfirstlane(task.first);
+    const int count = __builtin_amdgcn_readfirstlane(task.count);
+    const int lg = (int)((kLog2Lanes >> (3 * cls)) & 7);
+    const int ui = first + min(lane >> lg, count - 1);
+    const Dav1dGpuUnit u = bld(ai.units + ui);
+    const Dav1dGpuIntraEdge rec = bld(ai.recs + ui);
+    dispatch<BPC, GROUP_ALL_IE>(ai, *ptp, u, rec, cls, first, count, wl, 0);
+#endif
+}
+
+template <int BPC>
+__global__ __launch_bounds__(64 * sb_waves<BPC>()) void k_flow_sb(ReconArgs<BPC> a, SbFlowArgs f) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    using P = typename Px<BPC>::pixel;
+    constexpr int WPB = sb_waves<BPC>(), WL = wave_lds<BPC, GROUP_ALL_IE>();
+    __shared__ PlaneTabIE<BPC> pt;
+    __shared__ int s_sb;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (wave == 0) {   // plane, reference and top_edge tables, as in k_flow
+        const int tr_ = min(lane, DGPU_MAX_REFS * 3 - 1);
+        const P *rp = (&a.ref[0][0])[tr_];
+        const int rs = (&a.ref_stride[0][0])[tr_];
+        if (lane < DGPU_MAX_REFS * 3) {
+            pt.ref[lane] = rp;
+            pt.ref_stride[lane] = rs;
+        }
+        const int td = min(lane, 2);
+        P *dp = a.dst[td];
+        const int dsd = a.dst_stride[td];
+        P *tp = a.top[td];
+        const int ts = a.top_stride[td], tr = a.top_rows[td], sl = a.sb_log2[td];
+        if (lane < 3) {
+            pt.dst[lane] = dp;
+            pt.dst_stride[lane] = dsd;
+            pt.top[lane] = tp;
+            pt.top_stride[lane] = ts;
+            pt.top_rows[lane] = tr;
+            pt.sb_log2[lane] = sl;
+        }
+        if (lane == 0) {
+            bnd_touch(f.ctr);
+            s_sb = __hip_atomic_fetch_add(&f.ctr[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    const int sb = __builtin_amdgcn_readfirstlane(s_sb);
+    if (sb >= f.n_sb) return;
+    // wait for the superblocks this one reads: one poll per lane of wave 0,
+    // then one agent-scope acquire for the whole workgroup
+    if (wave == 0) {
+        const int d0 = bld(f.sb_dep_start + sb), nd = bld(f.sb_dep_start + sb + 1) - d0;
+        int ok = 1;
+        for (int j0 = 0; j0 < nd; j0 += 64) {
+            const int j = j0 + lane, dep = j < nd ? bld(f.sb_deps + d0 + j) : -1;
+            if (dep >= 0) bnd_touch(f.done + dep);
+            for (int it = 0;; it++) {
+                const int v = dep < 0 ? 1 : __hip_atomic_load(&f.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__all(v != 0)) break;
+                if (it >= f.spin_limit ||
+                    __hip_atomic_load(&f.ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(DGPU_FLOW_SLEEP);
+            }
+        }
+        if (!ok && lane == 0) __hip_atomic_store(&f.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (nd) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    // the superblock's levels: each level's tasks over the waves, a workgroup
+    // barrier after it (its stores drained first, so the next level's loads
+    // on this CU see them)
+    uint8_t *wl = lds + wave * WL;
+    const int l0 = bld(f.sb_level_start + sb), l1 = bld(f.sb_level_start + sb + 1);
+#pragma unroll 1
+    for (int lv = l0; lv < l1; lv++) {
+        const int t0 = bld(f.lvl_task_start + lv), t1 = bld(f.lvl_task_start + lv + 1);
+#pragma unroll 1
+        for (int t = t0 + wave; t < t1; t += WPB) {
+#if defined(__HIP_DEVICE_COMPILE__)
+            sb_task<BPC>((const KArg<BPC> *)__builtin_amdgcn_kernarg_segment_ptr(), &pt, bld(f.tasks + t), wl);
+#endif
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // every wave's stores have completed (the last barrier): one agent-scope
+    // release and the superblock's flag
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        bnd_touch(f.done + sb);
+        __hip_atomic_store(&f.done[sb], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // host: the wave tasks of a schedule (level order, classes largest first)
 static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<FlowTask> &tasks,
                       std::vector<int32_t> &level_tasks) {
@@ -317,11 +457,170 @@ static FlowLayout flow_layout(int n_levels, size_t n_tasks, int n_units, int64_t
     return L;
 }
 
+// DGPU_IS_SB workspace: counters | superblock flags | tasks | per-group task
+// starts | per-superblock group starts | superblock dependency CSR
+struct SbLayout {
+    size_t ctr, done, tasks, lts, sls, sds, sdeps, total;
+};
+static SbLayout sb_layout(int n_levels, size_t n_tasks, int n_sb, int64_t n_sb_deps) {
+    SbLayout L;
+    L.ctr = 0;
+    L.done = kFlowCtrHead * 4;
+    L.tasks = L.done + (((size_t)n_sb * 4 + 15) & ~(size_t)15);
+    L.lts = L.tasks + n_tasks * sizeof(FlowTask);
+    L.sls = L.lts + (size_t)(n_levels + 1) * 4;
+    L.sds = L.sls + (size_t)(n_sb + 1) * 4;
+    L.sdeps = L.sds + (size_t)(n_sb + 1) * 4;
+    L.total = L.sdeps + (size_t)n_sb_deps * 4;
+    return L;
+}
+// host: the superblock schedule's consistency (groups in range and in
+// order, dependencies on earlier superblocks only); -2 if not, else the
+// number of dependency entries
+static int64_t sb_check(const Dav1dGpuIntraSchedule *s) {
+    if (s->n_sb < 0 || (s->n_sb && (!s->sb_level_start || !s->sb_dep_start || !s->sb_deps))) return -2;
+    if (!s->n_sb) return 0;
+    if (s->sb_level_start[0] != 0 || s->sb_level_start[s->n_sb] != s->n_levels || s->sb_dep_start[0] != 0) return -2;
+    for (int b = 0; b < s->n_sb; b++) {
+        if (s->sb_level_start[b + 1] < s->sb_level_start[b] || s->sb_dep_start[b + 1] < s->sb_dep_start[b]) return -2;
+        for (int k = s->sb_dep_start[b]; k < s->sb_dep_start[b + 1]; k++)
+            if ((uint32_t)s->sb_deps[k] >= (uint32_t)b) return -2;   // (negative: huge)
+    }
+    return s->sb_dep_start[s->n_sb];
+}
+// the per-group task starts from the task list (tasks are in group order)
+static void sb_level_tasks(const std::vector<FlowTask> &tasks, int n_levels, std::vector<int32_t> &lts) {
+    lts.assign((size_t)n_levels + 1, 0);
+    for (const FlowTask &t : tasks) lts[t.level + 1]++;
+    for (int l = 0; l < n_levels; l++) lts[l + 1] += lts[l];
+}
+
+template <int BPC>
+static int launch_flow_sb(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, const Dav1dGpuIntraSchedule *s,
+                          const std::vector<FlowTask> &tasks, hipStream_t stream) {
+    using P = typename Px<BPC>::pixel;
+    using C = typename Px<BPC>::coef;
+    constexpr int B = BPC / 8;
+    const int64_t nd = sb_check(s);
+    if (nd < 0) return -2;
+    if (!s->n_sb) return 0;
+    std::vector<int32_t> lts;
+    sb_level_tasks(tasks, s->n_levels, lts);
+    const SbLayout Lw = sb_layout(s->n_levels, tasks.size(), s->n_sb, nd);
+    if ((size_t)s->workspace_bytes < Lw.total || ((uintptr_t)s->workspace & 15)) return -5;
+    uint8_t *ws = (uint8_t *)s->workspace;
+    SbFlowArgs f;
+    f.ctr = (int *)ws;
+    f.done = (int *)(ws + Lw.done);
+    f.tasks = (const FlowTask *)(ws + Lw.tasks);
+    f.lvl_task_start = (const int32_t *)(ws + Lw.lts);
+    f.sb_level_start = (const int32_t *)(ws + Lw.sls);
+    f.sb_dep_start = (const int32_t *)(ws + Lw.sds);
+    f.sb_deps = (const int32_t *)(ws + Lw.sdeps);
+    f.n_sb = s->n_sb;
+    f.spin_limit = DGPU_FLOW_SPIN_LIMIT;
+    if (const char *sl = getenv("DAV1D_GPU_FLOW_SPIN_LIMIT")) f.spin_limit = (int)strtol(sl, nullptr, 0);
+    {   // the task list and the schedule arrays through page-locked staging
+        const size_t up = Lw.total - Lw.tasks;
+        std::lock_guard<std::mutex> lock(g_stage_mu);
+        int device = 0;
+        if (hipGetDevice(&device) != hipSuccess) return -3;
+        FlowStage *sg = flow_stage_get(up, device);
+        if (!sg) return -3;
+        uint8_t *st = (uint8_t *)sg->p;
+        memcpy(st, tasks.data(), tasks.size() * sizeof(FlowTask));
+        memcpy(st + (Lw.lts - Lw.tasks), lts.data(), lts.size() * 4);
+        memcpy(st + (Lw.sls - Lw.tasks), s->sb_level_start, ((size_t)s->n_sb + 1) * 4);
+        memcpy(st + (Lw.sds - Lw.tasks), s->sb_dep_start, ((size_t)s->n_sb + 1) * 4);
+        if (nd) memcpy(st + (Lw.sdeps - Lw.tasks), s->sb_deps, (size_t)nd * 4);
+        if (hipMemsetAsync(ws, 0, Lw.tasks, stream) != hipSuccess) return -3;   // counters and flags
+        if (hipMemcpyAsync(ws + Lw.tasks, sg->p, up, hipMemcpyHostToDevice, stream) != hipSuccess ||
+            hipEventRecord(sg->ev, stream) != hipSuccess) {
+            (void)hipStreamSynchronize(stream);
+            return -3;
+        }
+    }
+#if DGPU_BOUNDS
+    {
+        DgpuBndTab t{};
+        for (int p = 0; p < 3; p++) {
+            bnd_add(t, b->dst[p], BND_DST);
+            bnd_add(t, e->top_edge[p], BND_TOP);
+            for (int r = 0; r < DGPU_MAX_REFS; r++) bnd_add(t, b->ref[r][p], BND_REF);
+        }
+        bnd_add(t, b->cfl_luma, BND_CFL);
+        bnd_range(t, b->units, (unsigned long long)b->n_units * sizeof(Dav1dGpuUnit), BND_UNITS);
+        bnd_range(t, e->units, (unsigned long long)b->n_units * sizeof(Dav1dGpuUnit), BND_UNITS);
+        bnd_range(t, e->recs, (unsigned long long)b->n_units * sizeof(Dav1dGpuIntraEdge), BND_RECS);
+        bnd_range(t, ws, Lw.total, BND_WORK);
+        bnd_add_extra(t);
+        bnd_print<P>(t, "flow_sb");
+        if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dgpu_bnd), &t, sizeof(t), 0, hipMemcpyHostToDevice, stream) != hipSuccess)
+            return -3;
+    }
+#endif
+    ReconArgs<BPC> a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) {
+        a.dst[p] = (P *)b->dst[p].data;
+        a.dst_stride[p] = (int)(b->dst[p].stride / B);
+        for (int r = 0; r < DGPU_MAX_REFS; r++) {
+            a.ref[r][p] = (const P *)b->ref[r][p].data;
+            a.ref_stride[r][p] = (int)(b->ref[r][p].stride / B);
+        }
+        a.top[p] = (P *)e->top_edge[p].data;
+        a.top_stride[p] = (int)(e->top_edge[p].stride / B);
+        a.top_rows[p] = e->top_edge[p].h;
+        a.sb_log2[p] = e->sb_log2[p];
+    }
+    a.units = b->units;
+    a.units_rw = e->units;
+    a.recs = e->recs;
+    a.coef = (C *)b->coef;
+    a.edges = (const P *)b->edges;
+    a.cfl_luma = (const P *)b->cfl_luma.data;
+    if (b->cfl_luma.data && !stride24(b->cfl_luma.stride)) return -4;
+    a.cfl_luma_stride = (int)(b->cfl_luma.stride / B);
+    a.cfl_ss = b->cfl_ss;
+    a.aux = b->aux;
+    a.aux_pool = (const uint8_t *)b->aux_pool;
+    a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
+    a.zero_coefs = b->zero_coefs;
+    constexpr int WPB = sb_waves<BPC>();
+    constexpr int lds = WPB * wave_lds<BPC, GROUP_ALL_IE>();
+    static std::once_flag once;
+    std::call_once(once, [] {
+        (void)hipFuncSetAttribute((const void *)k_flow_sb<BPC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    });
+    k_flow_sb<BPC><<<dim3((unsigned)s->n_sb), 64 * WPB, lds, stream>>>(a, f);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fprintf(stderr, "dav1d-gpu: intra superblock flow launch failed: %s\n", hipGetErrorString(err));
+        return -3;
+    }
+    return 0;
+}
+
+// the superblock launch lives in its own TUs (recon_sb8.hip / recon_sb16.hip:
+// its class code compiles in parallel with the other wavefront kernels)
+int flow_sb_launch8(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, const Dav1dGpuIntraSchedule *s,
+                    const std::vector<FlowTask> &tasks, hipStream_t stream);
+int flow_sb_launch16(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, const Dav1dGpuIntraSchedule *s,
+                     const std::vector<FlowTask> &tasks, hipStream_t stream);
+static inline int flow_sb_launch(int bpc, const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e,
+                                 const Dav1dGpuIntraSchedule *s, const std::vector<FlowTask> &tasks, hipStream_t stream) {
+    return bpc == 8 ? flow_sb_launch8(b, e, s, tasks, stream) : flow_sb_launch16(b, e, s, tasks, stream);
+}
+
 template <int BPC>
 static int64_t flow_workspace_bytes(const Dav1dGpuIntraSchedule *s, int n_units) {
     std::vector<FlowTask> t;
     std::vector<int32_t> lt;
     if (flow_tasks(s, n_units, t, lt)) return -2;
+    if (s->flags & DGPU_IS_SB) {
+        const int64_t nd = sb_check(s);
+        return nd < 0 ? -2 : (int64_t)sb_layout(s->n_levels, t.size(), s->n_sb, nd).total;
+    }
     const int64_t nd = flow_check_deps(s, n_units, t);
     if (nd < 0) return -2;
     return (int64_t)flow_layout(s->n_levels, t.size(), n_units, nd, s->dep_start && s->deps).total;
@@ -346,6 +645,7 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     int rc = flow_tasks(s, b->n_units, tasks, level_tasks);
     if (rc) return rc;
     if (tasks.empty()) return 0;
+    if (s->flags & DGPU_IS_SB) return flow_sb_launch(BPC, b, e, s, tasks, stream);
     const int64_t nd = flow_check_deps(s, b->n_units, tasks);
     if (nd < 0) return -2;
     const bool dataflow = s->dep_start && s->deps;

@@ -83,9 +83,13 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        // 64 KiB of slack past every buffer, rounded to 64 KiB: a vector
-        // load that runs past a buffer's last element stays mapped
-        const size_t sz = ((n + (64u << 10)) + ((64u << 10) - 1)) & ~(size_t)((64u << 10) - 1);
+        // rounded up to 256 bytes: the one read past a buffer's last element
+        // the kernels make by design is Stage's (the 16-byte block holding a
+        // region's last byte, at most 15 bytes further).  (Round 3 padded
+        // every buffer with 64 KiB after an unexplained fault; the DGPU_BOUNDS
+        // build, which checks every access against these buffers' exact
+        // sizes, reports none)
+        const size_t sz = (n + 255) & ~(size_t)255;
         if (hipMalloc(&p, sz) != hipSuccess) return -1;
         cap = n;
         return 0;
@@ -1086,7 +1090,11 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         return 0;
     };
 
-    if (!r->pool) r->pool.reset(new Pool((int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()))));
+    if (!r->pool) {   // DAV1D_GPU_REC_THREADS (diagnostics): the worker count, default min(8, cores)
+        int nthr = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char *e = getenv("DAV1D_GPU_REC_THREADS")) nthr = std::max(1, atoi(e));
+        r->pool.reset(new Pool(nthr));
+    }
     const size_t nb = r->blocks.size();
     const int nt = nb < 4096 ? 1 : r->pool->size();
     if (r->parts.size() < (size_t)nt) r->parts.resize(nt);
@@ -1211,6 +1219,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
             for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) stamp(ci, true);
         });
     }
+    lap("stamp");
     r->prod_cnt.resize(n_cells);
     if (r->tprod.size() < (size_t)nlv) r->tprod.resize(nlv);
     r->pool->run(nlv, [&](int t) {
@@ -1278,6 +1287,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
             r->prod_cnt[ci] = (int32_t)(out.size() - p0);
         }
     });
+    lap("prods");
     // the producer lists in decode order (CSR), then the levels
     prod_start.resize(n_cells + 1);
     prod_start[0] = 0;
@@ -1287,13 +1297,18 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         const size_t c0 = n_cells * t / nlv;
         if (!r->tprod[t].empty()) memcpy(&prod[(size_t)prod_start[c0]], r->tprod[t].data(), r->tprod[t].size() * 4);
     });
-    {
+    {   // (a compact level array: the walk touches 4 bytes per cell)
+        r->lv.resize(n_cells);
+        int32_t *lv = r->lv.data();
         const int32_t *ps = prod_start.data(), *pp = prod.data();
         for (size_t ci = 0; ci < n_cells; ci++) {
             int d = -1;
-            for (int32_t k = ps[ci]; k < ps[ci + 1]; k++) d = std::max(d, cells[pp[k]].level);
-            cells[ci].level = d + 1;
+            for (int32_t k = ps[ci]; k < ps[ci + 1]; k++) d = std::max(d, lv[pp[k]]);
+            lv[ci] = d + 1;
         }
+        r->pool->run(nlv, [&](int t) {
+            for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) cells[ci].level = lv[ci];
+        });
     }
     lap("levels");
     const int n = (int)cells.size();
@@ -1514,7 +1529,11 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         };
         reg(r->d_units.p, bu, dgpu::BND_UNITS);
         reg(r->d_recs.p, br, dgpu::BND_RECS);
-        reg(r->d_coef.p, bc, dgpu::BND_COEF);
+        // DAV1D_GPU_BND_SELFTEST=1: register the coefficient pool 64 bytes
+        // short, so the diagnostics must report the last units' coefficient
+        // reads (the check's positive control)
+        static const bool selftest = getenv("DAV1D_GPU_BND_SELFTEST") != nullptr;
+        reg(r->d_coef.p, selftest && bc > 128 ? bc - 64 : bc, dgpu::BND_COEF);
         reg(r->d_edges.p, edge_px * bpp, dgpu::BND_EDGES);
         reg(r->d_aux.p, ba, dgpu::BND_AUX);
         reg(r->d_auxp.p, bp, dgpu::BND_AUXPOOL);

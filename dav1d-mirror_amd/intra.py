@@ -903,23 +903,97 @@ def edge_batch(fr, dst_ptrs, top_ptrs, units, edges, recs):
     return b
 
 
+def sb_schedule(fr):
+    """The superblock form of an IntraFrame's schedule (DGPU_IS_SB): every
+    unit goes to the superblock holding its top-left pixel (4:2:0 chroma
+    superblocks are the luma ones halved, so a superblock owns its luma and
+    chroma); inside a superblock a unit sits one level above the units of
+    the same superblock it reads (producers elsewhere are awaited once, per
+    superblock); the superblocks in raster order, which puts every
+    superblock after those it reads (left, top, top-right: AV1's intra edges
+    and CfL never reach further).  Returns (perm, unit_start, class_start,
+    sb_level_start, sb_dep_start, sb_deps): perm[k] is the level-order index
+    of the k-th unit of the superblock order."""
+    n = len(fr.units)
+    W, H = fr.plane_wh[0]
+    sb0 = fr.sb_log2[0]
+    nsbx = (W + (1 << sb0) - 1) >> sb0
+    p = fr.units["plane"].astype(np.int64)
+    sbl = np.array(fr.sb_log2, np.int64)[p]
+    sbx = (fr.recs["x4"].astype(np.int64) * 4) >> sbl
+    sby = (fr.recs["y4"].astype(np.int64) * 4) >> sbl
+    sb = sby * nsbx + sbx
+    ds, dp = fr.dep_start, fr.deps
+    lv = np.zeros(n, np.int64)   # level inside the superblock (units are in level order: producers first)
+    sdeps = [set() for _ in range(n)]
+    for i in range(n):
+        d = -1
+        for q in dp[ds[i]:ds[i + 1]]:
+            if sb[q] == sb[i]:
+                d = max(d, lv[q])
+            else:
+                assert sb[q] < sb[i], "a unit reads a superblock after its own in raster order"
+                sdeps[i].add(int(sb[q]))
+        lv[i] = d + 1
+    modes = fr.units["mode"].astype(np.int64)
+    perm = np.lexsort((fr.units["txtp"], modes, fr.units["pred"], fr.units["tx"], lv, sb))
+    sbs = np.unique(sb)
+    sbidx = {int(v): k for k, v in enumerate(sbs)}
+    grp = sb[perm] * 4096 + lv[perm]
+    cut = np.concatenate([[0], np.nonzero(np.diff(grp))[0] + 1, [n]]).astype(np.int32)
+    n_lvl = len(cut) - 1
+    class_start = np.zeros((n_lvl, abi.N_TX + 1), np.int32)
+    tx = fr.units["tx"][perm]
+    for g in range(n_lvl):
+        class_start[g, 1:] = np.cumsum(np.bincount(tx[cut[g]:cut[g + 1]], minlength=abi.N_TX))
+    gsb = sb[perm][cut[:-1]]
+    sb_level_start = np.searchsorted(gsb, sbs).astype(np.int32)
+    sb_level_start = np.concatenate([sb_level_start, [n_lvl]]).astype(np.int32)
+    per_sb = [set() for _ in sbs]
+    for i in range(n):
+        per_sb[sbidx[int(sb[i])]] |= sdeps[i]
+    dep_lists = [sorted(sbidx[d] for d in x) for x in per_sb]
+    sb_dep_start = np.concatenate([[0], np.cumsum([len(x) for x in dep_lists])]).astype(np.int32)
+    sb_deps = np.array([d for x in dep_lists for d in x], np.int32)
+    return perm, cut, class_start, sb_level_start, sb_dep_start, sb_deps
+
+
 class DeviceIntraFrame:
     """An IntraFrame on one GPU; launch() runs the whole wavefront
     (dav1d_gpu_recon_intra_frame_*) on a stream."""
 
-    MODES = ("persistent", "levels", "fused", "staged")
+    MODES = ("persistent", "levels", "fused", "staged", "sb")
 
     def __init__(self, fr, device="cuda:0", top_fill=0x5A, mode="persistent"):
         """mode: persistent -- one launch per frame (DGPU_IS_PERSISTENT), a
         wave waits for the tasks of its units' producers (dataflow); levels --
         the same launch, a wave waits for the whole previous level; fused --
         one launch per level (DGPU_IS_FUSED); staged -- edge stage, unit
-        batch and backup runs per level."""
+        batch and backup runs per level; sb -- one launch per frame, a
+        workgroup per superblock (DGPU_IS_SB, sb_schedule): units, records
+        and the schedule in superblock order (units_frame_order() maps the
+        rewritten units back)."""
         assert mode in self.MODES
         dataflow = mode == "persistent"
-        mode = "persistent" if mode == "levels" else mode
+        self.sb = mode == "sb"
+        mode = "persistent" if mode in ("levels", "sb") else mode
         import torch
-        self.torch, self.fr = torch, fr
+        self.torch = torch
+        self.perm = None
+        if self.sb:   # the same frame in superblock order
+            import copy
+            perm, cut, cls_start, sls, sds, sdeps = sb_schedule(fr)
+            fr = copy.copy(fr)
+            fr.units, fr.recs = fr.units[perm], fr.recs[perm].copy()
+            fr.recs["unit"] = np.arange(len(perm))
+            fr.unit_start, fr.class_start, fr.rec_start = cut, cls_start, cut.copy()
+            fr.run_start = np.zeros(len(cut), np.int32)
+            if getattr(fr, "aux", None) is not None:
+                fr.aux = fr.aux[perm]
+            self.perm = perm
+            self._sb = [np.ascontiguousarray(a, np.int32) for a in (sls, sds, sdeps if len(sdeps) else np.zeros(1))]
+            self.n_sb = len(sls) - 1
+        self.fr = fr
         dev = torch.device(device)
         hbd = fr.cfg.bpc != 8
         pdt = torch.int16 if hbd else torch.uint8
@@ -942,8 +1016,12 @@ class DeviceIntraFrame:
         self._host = [np.ascontiguousarray(a, dtype=np.int32) for a in
                       (fr.unit_start, fr.class_start, fr.rec_start, fr.run_start)]
         s = abi.IntraSchedule()
-        s.n_levels = fr.n_levels
+        s.n_levels = len(fr.unit_start) - 1
         s.flags = {"persistent": abi.IS_FUSED | abi.IS_PERSISTENT, "fused": abi.IS_FUSED, "staged": 0}[mode]
+        if self.sb:
+            s.flags |= abi.IS_SB
+            s.n_sb = self.n_sb
+            s.sb_level_start, s.sb_dep_start, s.sb_deps = (a.ctypes.data for a in self._sb)
         s.unit_start, s.class_start, s.rec_start, s.run_start = (a.ctypes.data for a in self._host)
         s.runs = self.runs.data_ptr()
         if mode == "persistent" and dataflow and fr.dep_start is not None:
@@ -959,6 +1037,15 @@ class DeviceIntraFrame:
                 raise RuntimeError(f"dav1d_gpu_intra_workspace_bytes failed: {nb}")
             self.workspace = torch.zeros(max(int(nb), 16), dtype=torch.uint8, device=dev)
             s.workspace, s.workspace_bytes = self.workspace.data_ptr(), int(nb)
+
+    def units_frame_order(self):
+        """The device's (rewritten) units in the IntraFrame's level order."""
+        u = self.units.cpu().numpy().view(self.fr.units.dtype)
+        if self.perm is None:
+            return u
+        out = np.empty_like(u)
+        out[self.perm] = u
+        return out
 
     def flow_error(self):
         """The persistent kernel's give-up flag (int32 [1] of the workspace)."""

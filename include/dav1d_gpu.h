@@ -650,6 +650,16 @@ int dav1d_gpu_backup_ipred_edge_16bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav
                                   counters in `workspace` instead of launch
                                   boundaries */
 
+#define DGPU_IS_SB 4   /* (with PERSISTENT, round 4) the wavefront per
+                          superblock: one workgroup reconstructs a whole
+                          superblock, its in-superblock levels separated by
+                          workgroup barriers (the hand-offs stay on the CU),
+                          and waits once, for the superblocks its units read
+                          (one agent-scope acquire and release per
+                          superblock instead of per task).  The schedule's
+                          levels are then (superblock, level inside it)
+                          groups, see n_sb below */
+
 typedef struct Dav1dGpuIntraSchedule {
     int32_t n_levels;
     int32_t flags;               /* DGPU_IS_*                                   */
@@ -669,6 +679,15 @@ typedef struct Dav1dGpuIntraSchedule {
        the whole previous level (dataflow); NULL: level barriers.            */
     const int32_t *dep_start;    /* n_units + 1                                */
     const int32_t *deps;
+    /* DGPU_IS_SB: the levels above are (superblock, level inside it)
+       groups, each superblock's groups consecutive and the superblocks in an
+       order where every superblock comes after those it reads (raster order
+       of the frame's superblocks does); dep_start / deps are unused.        */
+    int32_t n_sb;
+    const int32_t *sb_level_start;   /* host, n_sb + 1: each superblock's groups */
+    const int32_t *sb_dep_start;     /* host, n_sb + 1 (CSR)                     */
+    const int32_t *sb_deps;          /* host: the earlier superblocks whose pixels
+                                        or top_edge rows its units read          */
 } Dav1dGpuIntraSchedule;
 
 /* Workspace a DGPU_IS_PERSISTENT schedule needs (bytes), or -2 if the

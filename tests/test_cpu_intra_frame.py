@@ -113,3 +113,45 @@ def test_intra_frame_launch_validation(pkg):
         assert bk(None, None, 0, None) == -1
         assert bk(ctypes.byref(eb), None, 3, None) == -1
         assert bk(ctypes.byref(eb), None, 0, None) == 0
+
+
+@pytest.mark.parametrize("kw", [dict(seed=27), dict(seed=28, sb_log2=7, width=512, height=384),
+                                dict(seed=29, width=640, height=384, tile_cols=3, tile_rows=2, inter_frac=0.3),
+                                dict(seed=30, bpc=16, bitdepth_max=1023, cfl_frac=1.0)])
+def test_sb_schedule(pkg, kw):
+    """The superblock schedule (DGPU_IS_SB, intra.sb_schedule): a
+    permutation whose groups are (superblock, level) runs in superblock
+    order, size classes inside a group; every producer of a unit sits in an
+    earlier superblock the unit's superblock waits for, or in an earlier
+    group of its own superblock."""
+    abi = pkg.abi
+    fr = _frame(**kw)
+    n = len(fr.units)
+    perm, cut, cls, sls, sds, sdeps = pkg.intra.sb_schedule(fr)
+    assert np.array_equal(np.sort(perm), np.arange(n))
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    n_g, n_sb = len(cut) - 1, len(sls) - 1
+    assert cut[0] == 0 and cut[-1] == n and np.all(np.diff(cut) > 0)
+    assert sls[0] == 0 and sls[-1] == n_g and np.all(np.diff(sls) > 0)
+    grp = np.repeat(np.arange(n_g), np.diff(cut))             # group of each position
+    sb_of_g = np.repeat(np.arange(n_sb), np.diff(sls))
+    for g in range(n_g):
+        t = fr.units["tx"][perm[cut[g]:cut[g + 1]]]
+        assert np.all(np.diff(t.astype(int)) >= 0)
+        assert np.array_equal(cls[g], np.concatenate([[0], np.cumsum(np.bincount(t, minlength=abi.N_TX))]))
+    for b in range(n_sb):
+        d = sdeps[sds[b]:sds[b + 1]]
+        assert np.all(d < b) and len(np.unique(d)) == len(d)
+    for u in range(n):
+        gu = grp[inv[u]]
+        for q in fr.deps[fr.dep_start[u]:fr.dep_start[u + 1]]:
+            gq = grp[inv[q]]
+            if sb_of_g[gq] == sb_of_g[gu]:
+                assert gq < gu
+            else:
+                b = sb_of_g[gu]
+                assert sb_of_g[gq] in sdeps[sds[b]:sds[b + 1]]
+    # far fewer steps on the critical path than levels: a superblock waits
+    # for at most its left, top-left, top and top-right neighbours
+    assert np.all(np.diff(sds) <= 4)

@@ -25,8 +25,7 @@ def _check(oracle, fr, mode="persistent"):
         top = dev.top[p].cpu().numpy()
         top = top if fr.cfg.bpc == 8 else top.view(np.uint16)
         assert np.array_equal(top[:-1], ho.top[p][:-1]), p
-    units = dev.units.cpu().numpy().view(fr.units.dtype)
-    assert np.array_equal(units, ho.units)
+    assert np.array_equal(dev.units_frame_order(), ho.units)
     return dev, ho
 
 
@@ -35,11 +34,12 @@ def _frame(**kw):
     return intra.make_intra_frame(intra.IntraConfig(**kw))
 
 
-@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged"])
+@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged", "sb"])
 @pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023), (16, 4095)])
 def test_intra_frame(oracle, bpc, bdmax, mode):
     """persistent: one launch per frame, waves wait on their producers'
-    task flags; levels: the same, waiting on per-level counters; fused: one launch per level (edges gathered in the reconstruction
+    task flags; levels: the same, waiting on per-level counters; sb: one
+    launch per frame, a workgroup per superblock (DGPU_IS_SB); fused: one launch per level (edges gathered in the reconstruction
     kernel, backups with the stores); staged: edge stage, unit batch and
     backup runs as three launches per level."""
     _check(oracle, _frame(seed=31, bpc=bpc, bitdepth_max=bdmax), mode=mode)
@@ -49,11 +49,12 @@ def test_intra_frame(oracle, bpc, bdmax, mode):
                                 dict(seed=34, width=480, height=264), dict(seed=35, sb_log2=7, width=512, height=384),
                                 dict(seed=38, width=640, height=384, tile_cols=3, tile_rows=2),
                                 dict(seed=39, tile_cols=2, sb_edge_backup=False)])
-def test_intra_frame_variants(oracle, kw):
-    _check(oracle, _frame(**kw))
+@pytest.mark.parametrize("mode", ["persistent", "sb"])
+def test_intra_frame_variants(oracle, kw, mode):
+    _check(oracle, _frame(**kw), mode=mode)
 
 
-@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged"])
+@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged", "sb"])
 @pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
 def test_mixed_frame(oracle, mode, bpc, bdmax):
     """Inter blocks (put / compound avg from padded references) among the
@@ -62,10 +63,11 @@ def test_mixed_frame(oracle, mode, bpc, bdmax):
     _check(oracle, _frame(seed=41, inter_frac=0.5, bpc=bpc, bitdepth_max=bdmax, tile_cols=2), mode=mode)
 
 
-def test_intra_frame_relaunch(oracle):
+@pytest.mark.parametrize("mode", ["persistent", "sb"])
+def test_intra_frame_relaunch(oracle, mode):
     """reset() + launch again: the same pixels (the wavefront is repeatable)."""
     import torch
-    dev, ho = _check(oracle, _frame(seed=36))
+    dev, ho = _check(oracle, _frame(seed=36), mode=mode)
     first = [a.copy() for a in dev.planes_host()]
     dev.reset()
     dev.launch()
@@ -74,13 +76,13 @@ def test_intra_frame_relaunch(oracle):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged"])
+@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged", "sb"])
 def test_intra_frame_1080p(oracle, mode):
     """A 1080p intra frame (partial superblock row at the bottom)."""
     _check(oracle, _frame(seed=37, width=1920, height=1080), mode=mode)
 
 
-@pytest.mark.parametrize("mode", ["persistent", "levels"])
+@pytest.mark.parametrize("mode", ["persistent", "levels", "sb"])
 def test_intra_frame_4k_persistent(oracle, mode):
     """A 4K intra frame (1603 levels) through the persistent kernel, twice."""
     import torch

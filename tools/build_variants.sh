@@ -15,7 +15,7 @@ build() {
     done
     wait
     local objs=""
-    for s in runtime mc ipred itx recon8 recon16 tile8 tile16 edges recon_ie8 recon_ie16 recorder grain cdef lpf lr picture; do
+    for s in runtime mc ipred itx recon8 recon16 tile8 tile16 edges recon_ie8 recon_ie16 recon_sb8 recon_sb16 recorder grain cdef lpf lr picture; do
         if [ -f build/var/$name.$s.o ] && [[ " ${TUS:-recon8 recon16} " == *" $s "* ]]; then objs="$objs build/var/$name.$s.o"; else objs="$objs build/$s.o"; fi
     done
     $HIPCC $F -shared -o libdav1d_gpu.$name.so $objs build/stamp.o
@@ -35,7 +35,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         t1|t2|t4|t8|t16|t3|t6|t7|t15|t31) TUS=tile8 build $v -DDGPU_TILE_ABL=${v#t} ;;
         ttrace) TUS=tile8 build ttrace -DDGPU_TILE_TRACE=1 ;;
         twpe2|twpe4|twpe5) TUS=tile8 build $v -DDGPU_TILE_WPE=${v#twpe} ;;
-        bounds) TUS="recon8 recon_ie8 recorder" build bounds -DDGPU_BOUNDS=1 ;;
+        bounds) TUS="recon8 recon_ie8 recon_sb8 recorder" build bounds -DDGPU_BOUNDS=1 ;;
         fnofence) TUS="recon_ie8" build fnofence -DDGPU_FLOW_NOFENCE=1 ;;
         fsc1) TUS="recon_ie8" build fsc1 -DDGPU_FLOW_SC1=1 ;;
         fsleep1) TUS="recon_ie8" build fsleep1 -DDGPU_FLOW_SLEEP=1 ;;

@@ -5,7 +5,8 @@
 # serialized, AMD_SERIALIZE_KERNEL=3, so a fault is reported at its launch), bounds (the recorder tests on the
 # DGPU_BOUNDS build, tools/build_variants.sh bounds), smoke, bench (headline
 # line), prof (rocprofv3 kernel trace of the headline), pmc (FETCH / WRITE
-# passes).  Every step has its own time limit; the first failure ends the run.
+# passes), intra / cdef (those GPU test files), benchpart (the intra,
+# CDEF, LR and recorder bench legs).  Every step has its own time limit; the first failure ends the run.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 T=${1:-r4}
@@ -20,8 +21,19 @@ for s in "${@:-tests}"; do
     tests) timeout -k 10 900 $PYT -m gpu -x tests > "$O/gputest.log" 2>&1 || { echo "[r4] tests failed"; exit 1; } ;;
     stests) AMD_SERIALIZE_KERNEL=3 timeout -k 10 1200 $PYT -m gpu -x tests > "$O/gputest.log" 2>&1 || { echo "[r4] stests failed"; exit 1; } ;;
     rectests) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_recorder.py tests/test_gpu_batch.py > "$O/rectest.log" 2>&1 || { echo "[r4] rectests failed"; exit 1; } ;;
-    bounds) DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 600 $PYT -m gpu tests/test_gpu_recorder.py > "$O/bounds.log" 2>&1
-            rc=$?; echo "[r4] bounds rc=$rc"; [ $rc -le 1 ] || exit 1 ;;
+    bounds) # -s: the device printf reports must not be captured by pytest
+            DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 600 $PYT -s -m gpu tests/test_gpu_recorder.py > "$O/bounds.log" 2>&1
+            rc=$?; echo "[r4] bounds rc=$rc reports=$(grep -c 'DGPU_BOUNDS line' "$O/bounds.log")"; [ $rc -le 1 ] || exit 1
+            # positive control: the coefficient pool registered 64 bytes short must be reported
+            DAV1D_GPU_BND_SELFTEST=1 DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 300 $PYT -s -m gpu \
+                "tests/test_gpu_recorder.py::test_recorder_mixed" > "$O/bounds_selftest.log" 2>&1
+            echo "[r4] bounds selftest rc=$? reports=$(grep -c 'DGPU_BOUNDS line' "$O/bounds_selftest.log")" ;;
+    intra) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_intra_frame.py > "$O/intra.log" 2>&1 || { echo "[r4] intra failed"; exit 1; } ;;
+    cdef) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_cdef.py > "$O/cdef.log" 2>&1 || { echo "[r4] cdef failed"; exit 1; } ;;
+    benchpart) # the intra wavefront, CDEF, LR and recorder legs only (recorder host laps on stderr)
+            DAV1D_GPU_REC_TIMING=1 timeout -k 10 600 python -u bench.py --steps 50 --no-families --no-configs --no-tiles \
+                --no-grain --no-superres --no-lpf --no-cpu --no-check > "$O/benchpart.json" 2> "$O/benchpart.log" \
+                || { echo "[r4] benchpart failed"; exit 1; } ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "[r4] smoke failed"; exit 1; } ;;
     bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r4] bench failed"; exit 1; } ;;
     benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r4] benchfast failed"; exit 1; } ;;
