@@ -6,7 +6,7 @@
 # DGPU_BOUNDS build, tools/build_variants.sh bounds), smoke, bench (headline
 # line), prof (rocprofv3 kernel trace of the headline), pmc (FETCH / WRITE
 # passes), intra / cdef (those GPU test files), benchpart (the intra,
-# CDEF, LR and recorder bench legs).  Every step has its own time limit; the first failure ends the run.
+# CDEF, LR and recorder bench legs), cdefpmc (CDEF / LR counters).  Every step has its own time limit; the first failure ends the run.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 T=${1:-r4}
@@ -40,6 +40,11 @@ for s in "${@:-tests}"; do
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 50 $BENCH_FAST) > "$O/prof.log" 2>&1 || { echo "[r4] prof failed"; exit 1; } ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE; do
              (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/pmc_$c" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 $BENCH_FAST) > "$O/pmc_$c.log" 2>&1 || { echo "[r4] pmc $c failed"; exit 1; }
+         done ;;
+    cdefpmc) # CDEF / LR counters: the bench with only those legs (the headline frame runs too; filter by kernel)
+         for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS"; do
+             n=$(echo $c | cut -d' ' -f1)
+             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/cdefpmc_$n" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-families --no-configs --no-tiles --no-intra --no-recorder --no-grain --no-superres --no-lpf --no-cpu --no-check) > "$O/cdefpmc_$n.log" 2>&1 || { echo "[r4] cdefpmc $n failed"; exit 1; }
          done ;;
     esac
     echo "[r4] $s done $(date +%T)"
