@@ -358,8 +358,14 @@ __device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, co
     else col_out<BPC, BH, false>(dst, ds, c, S, tp);
 }
 
+// DGPU_CDEF_WPE: a minimum of waves per SIMD for the register allocator
+// (0: the compiler's choice, 86 VGPRs = 5 waves)
+#ifndef DGPU_CDEF_WPE
+#define DGPU_CDEF_WPE 0
+#endif
 template <int BPC, int LAYOUT>
-__global__ __launch_bounds__(256) void k_cdef(CdefArgs<BPC> a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DGPU_CDEF_WPE ? DGPU_CDEF_WPE : 1)))
+void k_cdef(CdefArgs<BPC> a) {
     using P = typename Px<BPC>::pixel;
     constexpr int SX = LAYOUT == 1 || LAYOUT == 2, SY = LAYOUT == 1;
     constexpr int LS = 64 + 8;                      // luma tile stride

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
 // stall into the error word.
 struct SbFlowArgs {
     const FlowTask *tasks;
-    const int32_t *lvl_task_start;   // per group (superblock level): its tasks
+    const int32_t *cls_task_start;   // per group (superblock level) and class position (kOrder): its tasks
     const int32_t *sb_level_start;   // per superblock: its groups
     const int32_t *sb_dep_start;     // per superblock: the superblocks it waits for
     const int32_t *sb_deps;
@@ -225,33 +225,65 @@ struct SbFlowArgs {
     int *done;                       // per superblock: reconstructed
     int n_sb;
     int spin_limit;
+    // diagnostics (DAV1D_GPU_SB_TRACE=<host address of page-locked memory>,
+    // DAV1D_GPU_SB_DEBUG=<mode>): per workgroup, the superblock it took and
+    // finished, and per wave the last task it finished, stored to host memory
+    // as it runs; mode 1 skips the class code
+    unsigned *trace;
+    int debug;
 };
-
-template <int BPC> using KArg = __attribute__((address_space(4))) ReconArgs<BPC>;
 
 template <int BPC> __host__ __device__ constexpr int sb_waves() {
     // waves per superblock workgroup within the CU's 160 KB of LDS
     return cmin(4, (160 * 1024) / wave_lds<BPC, GROUP_ALL_IE>());
 }
 
-// one task of the superblock loop, out of line (the launch arguments read
-// from the kernarg segment in the call): with the class code inlined into
-// the loop the compiler hoists the argument loads and address arithmetic out
-// of it and spills ~670 VGPRs; as a call it takes 248 VGPRs and no spills
-template <int BPC>
-__device__ __noinline__ void sb_task(const KArg<BPC> *ka, const PlaneTabIE<BPC> *ptp, FlowTask task, uint8_t *wl) {
-#if defined(__HIP_DEVICE_COMPILE__)   // (the kernarg address space exists only on the device)
+// One class's tasks of a superblock level on this wave (every WPB-th task of
+// the level, counted from its first).  The class code is inlined once per
+// class, each copy inside its own loop: a single loop around the class
+// switch made the compiler hoist argument loads and addresses out of it
+// across all 19 class bodies (~670 VGPRs of spill); one loop per class keeps
+// what is hoisted to one body's working set, as in k_recon.
+template <int BPC, int K>
+__device__ __forceinline__ void sb_class(const ReconArgs<BPC> &a, const PlaneTabIE<BPC> &pt, const SbFlowArgs &f,
+                                         const int32_t *cts, int t0, int wave, uint8_t *wl) {
+    constexpr int WPB = sb_waves<BPC>(), C = kOrder[K];
+    constexpr int LG = (int)((kLog2Lanes >> (3 * C)) & 7);
+    const int tb = bld(cts + K), te = bld(cts + K + 1);
+    if (tb >= te) return;
     const int lane = threadIdx.x & 63;
-    const ReconArgs<BPC> ai = *(const ReconArgs<BPC> *)ka;
-    const int cls = __builtin_amdgcn_readfirstlane(task.cls);
-    const int first = __builtin_amdgcn_readfirstlane(task.first);
-    const int count = __builtin_amdgcn_readfirstlane(task.count);
-    const int lg = (int)((kLog2Lanes >> (3 * cls)) & 7);
-    const int ui = first + min(lane >> lg, count - 1);
-    const Dav1dGpuUnit u = bld(ai.units + ui);
-    const Dav1dGpuIntraEdge rec = bld(ai.recs + ui);
-    dispatch<BPC, GROUP_ALL_IE>(ai, *ptp, u, rec, cls, first, count, wl, 0);
+    // the first task of the range that is this wave's: (t - t0) % WPB == wave
+    int t = tb + (wave - (tb - t0) % WPB + WPB) % WPB;
+#pragma unroll 1
+    for (; t < te; t += WPB) {
+        asm volatile("" ::: "memory");   // (no load is hoisted out of the loop)
+        const FlowTask task = bld(f.tasks + t);
+        const int first = __builtin_amdgcn_readfirstlane(task.first);
+        const int count = __builtin_amdgcn_readfirstlane(task.count);
+        const int ui = first + min(lane >> LG, count - 1);
+#if defined(__HIP_DEVICE_COMPILE__)
+        // the launch arguments re-read through a pointer the compiler cannot
+        // follow (kernel arguments are invariant loads, hoisted otherwise)
+        const __attribute__((address_space(4))) ReconArgs<BPC> *ka4 =
+            (const __attribute__((address_space(4))) ReconArgs<BPC> *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka4));
+        const ReconArgs<BPC> *ka = (const ReconArgs<BPC> *)ka4;
+#else
+        const ReconArgs<BPC> *ka = &a;
 #endif
+        const Dav1dGpuUnit u = bld(ka->units + ui);
+        const Dav1dGpuIntraEdge rec = bld(ka->recs + ui);
+        run_class<BPC, C, GROUP_ALL_IE>(*ka, pt, u, rec, first, count, wl, 0);
+        if (f.trace && lane == 0)
+            __hip_atomic_store(&f.trace[(blockIdx.x * 8 + wave) * 2 + 1], (unsigned)t | 0x80000000u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+template <int BPC, int... K>
+__device__ __forceinline__ void sb_classes(const ReconArgs<BPC> &a, const PlaneTabIE<BPC> &pt, const SbFlowArgs &f,
+                                           const int32_t *cts, int wave, uint8_t *wl, std::integer_sequence<int, K...>) {
+    const int t0 = bld(cts);
+    (sb_class<BPC, K>(a, pt, f, cts, t0, wave, wl), ...);
 }
 
 template <int BPC>
@@ -319,16 +351,15 @@ __global__ __launch_bounds__(64 * sb_waves<BPC>()) void k_flow_sb(ReconArgs<BPC>
     // barrier after it (its stores drained first, so the next level's loads
     // on this CU see them)
     uint8_t *wl = lds + wave * WL;
+    if (f.trace && threadIdx.x == 0)
+        __hip_atomic_store(&f.trace[blockIdx.x * 16 + 8], (unsigned)sb | 0x40000000u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     const int l0 = bld(f.sb_level_start + sb), l1 = bld(f.sb_level_start + sb + 1);
 #pragma unroll 1
     for (int lv = l0; lv < l1; lv++) {
-        const int t0 = bld(f.lvl_task_start + lv), t1 = bld(f.lvl_task_start + lv + 1);
-#pragma unroll 1
-        for (int t = t0 + wave; t < t1; t += WPB) {
-#if defined(__HIP_DEVICE_COMPILE__)
-            sb_task<BPC>((const KArg<BPC> *)__builtin_amdgcn_kernarg_segment_ptr(), &pt, bld(f.tasks + t), wl);
-#endif
-        }
+        if (f.debug != 1)
+            sb_classes<BPC>(a, pt, f, f.cls_task_start + (size_t)lv * (DGPU_N_RECT_TX_SIZES + 1), wave, wl,
+                            std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -338,6 +369,9 @@ __global__ __launch_bounds__(64 * sb_waves<BPC>()) void k_flow_sb(ReconArgs<BPC>
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         bnd_touch(f.done + sb);
         __hip_atomic_store(&f.done[sb], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f.trace)
+            __hip_atomic_store(&f.trace[blockIdx.x * 16 + 9], (unsigned)sb | 0x20000000u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -468,7 +502,7 @@ static SbLayout sb_layout(int n_levels, size_t n_tasks, int n_sb, int64_t n_sb_d
     L.done = kFlowCtrHead * 4;
     L.tasks = L.done + (((size_t)n_sb * 4 + 15) & ~(size_t)15);
     L.lts = L.tasks + n_tasks * sizeof(FlowTask);
-    L.sls = L.lts + (size_t)(n_levels + 1) * 4;
+    L.sls = L.lts + (size_t)(n_levels > 0 ? n_levels : 1) * (DGPU_N_RECT_TX_SIZES + 1) * 4;
     L.sds = L.sls + (size_t)(n_sb + 1) * 4;
     L.sdeps = L.sds + (size_t)(n_sb + 1) * 4;
     L.total = L.sdeps + (size_t)n_sb_deps * 4;
@@ -488,11 +522,22 @@ static int64_t sb_check(const Dav1dGpuIntraSchedule *s) {
     }
     return s->sb_dep_start[s->n_sb];
 }
-// the per-group task starts from the task list (tasks are in group order)
-static void sb_level_tasks(const std::vector<FlowTask> &tasks, int n_levels, std::vector<int32_t> &lts) {
-    lts.assign((size_t)n_levels + 1, 0);
-    for (const FlowTask &t : tasks) lts[t.level + 1]++;
-    for (int l = 0; l < n_levels; l++) lts[l + 1] += lts[l];
+// per group and class position k (kOrder), the first task: flow_tasks emits
+// a level's tasks class by class in kOrder, so [cts[g][k], cts[g][k + 1])
+// are the group's tasks of class kOrder[k]
+static void sb_class_tasks(const std::vector<FlowTask> &tasks, int n_levels, std::vector<int32_t> &cts) {
+    constexpr int NC = DGPU_N_RECT_TX_SIZES;
+    int pos[NC];
+    for (int k = 0; k < NC; k++) pos[kOrder[k]] = k;
+    cts.assign((size_t)(n_levels > 0 ? n_levels : 1) * (NC + 1), 0);
+    std::vector<int32_t> cnt((size_t)(n_levels > 0 ? n_levels : 1) * NC, 0);
+    for (const FlowTask &t : tasks) cnt[(size_t)t.level * NC + pos[t.cls]]++;
+    int32_t run = 0;
+    for (int l = 0; l < n_levels; l++)
+        for (int k = 0; k <= NC; k++) {
+            cts[(size_t)l * (NC + 1) + k] = run;
+            if (k < NC) run += cnt[(size_t)l * NC + k];
+        }
 }
 
 template <int BPC>
@@ -505,7 +550,7 @@ static int launch_flow_sb(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBa
     if (nd < 0) return -2;
     if (!s->n_sb) return 0;
     std::vector<int32_t> lts;
-    sb_level_tasks(tasks, s->n_levels, lts);
+    sb_class_tasks(tasks, s->n_levels, lts);
     const SbLayout Lw = sb_layout(s->n_levels, tasks.size(), s->n_sb, nd);
     if ((size_t)s->workspace_bytes < Lw.total || ((uintptr_t)s->workspace & 15)) return -5;
     uint8_t *ws = (uint8_t *)s->workspace;
@@ -513,13 +558,17 @@ static int launch_flow_sb(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBa
     f.ctr = (int *)ws;
     f.done = (int *)(ws + Lw.done);
     f.tasks = (const FlowTask *)(ws + Lw.tasks);
-    f.lvl_task_start = (const int32_t *)(ws + Lw.lts);
+    f.cls_task_start = (const int32_t *)(ws + Lw.lts);
     f.sb_level_start = (const int32_t *)(ws + Lw.sls);
     f.sb_dep_start = (const int32_t *)(ws + Lw.sds);
     f.sb_deps = (const int32_t *)(ws + Lw.sdeps);
     f.n_sb = s->n_sb;
     f.spin_limit = DGPU_FLOW_SPIN_LIMIT;
     if (const char *sl = getenv("DAV1D_GPU_FLOW_SPIN_LIMIT")) f.spin_limit = (int)strtol(sl, nullptr, 0);
+    f.trace = nullptr;
+    f.debug = 0;
+    if (const char *e = getenv("DAV1D_GPU_SB_TRACE")) f.trace = (unsigned *)(uintptr_t)strtoull(e, nullptr, 0);
+    if (const char *e = getenv("DAV1D_GPU_SB_DEBUG")) f.debug = (int)strtol(e, nullptr, 0);
     {   // the task list and the schedule arrays through page-locked staging
         const size_t up = Lw.total - Lw.tasks;
         std::lock_guard<std::mutex> lock(g_stage_mu);
@@ -586,6 +635,8 @@ static int launch_flow_sb(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBa
     a.aux_pool = (const uint8_t *)b->aux_pool;
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;
+    // DGPU_TRACE builds (diagnostics): the class code's phase marks to host memory
+    if (const char *e = getenv("DAV1D_GPU_SB_PHASES")) a.trace = (unsigned long long *)(uintptr_t)strtoull(e, nullptr, 0);
     constexpr int WPB = sb_waves<BPC>();
     constexpr int lds = WPB * wave_lds<BPC, GROUP_ALL_IE>();
     static std::once_flag once;

@@ -1301,6 +1301,22 @@ struct NoWait {
     __device__ __forceinline__ void operator()() const {}
 };
 
+// DGPU_LANE_OPAQUE (the superblock wavefront's TUs, recon_sb*.hip): the lane
+// id from an asm the compiler cannot move, so nothing lane-derived is hoisted
+// out of their task loops (hoisted across 19 class bodies it spills)
+#ifndef DGPU_LANE_OPAQUE
+#define DGPU_LANE_OPAQUE 0
+#endif
+__device__ __forceinline__ int unit_lane() {
+    if constexpr (DGPU_LANE_OPAQUE) {
+        int l;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+        return l;
+    } else {
+        return threadIdx.x & 63;
+    }
+}
+
 template <int BPC, int TX, bool WARPK, bool GATHER = false, typename WaitT = NoWait>
 __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt,
                                             const Dav1dGpuUnit &u_in, const Dav1dGpuIntraEdge &rec, int first,
@@ -1313,7 +1329,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     using TT = typename Tmp<BPC>::T;
     constexpr int W = CL::W, H = CL::H, SW = CL::SW, SH = CL::SH, G = CL::G, QW = CL::QW, NT = CL::NT;
     constexpr int TPL = CL::TPL;
-    const int lane = threadIdx.x & 63;
+    const int lane = unit_lane();
     const int g = lane / G, l = lane % G;
     if (g >= count) return;
     // DGPU_TRACE: timestamp phase i after draining this wave's memory ops
@@ -1912,7 +1928,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
     using TT = typename Tmp<BPC>::T;
     constexpr int W = CL::W, H = CL::H, SW = CL::SW, SH = CL::SH, G = CL::G, QW = CL::QW, NT = CL::NT;
     constexpr int TPL = CL::TPL;
-    const int lane = threadIdx.x & 63;
+    const int lane = unit_lane();
     const int g = lane / G, l = lane % G;
     if (g >= count) return;
     uint8_t *slot = wave_lds + g * SL::BYTES_W;

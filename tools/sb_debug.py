@@ -30,7 +30,7 @@ n_sb = len(sls) - 1
 trace = torch.zeros(16 * n_sb + 16, dtype=torch.int32, pin_memory=True)
 os.environ["DAV1D_GPU_SB_TRACE"] = str(trace.data_ptr())
 phases = None
-if os.environ.get("DAV1D_GPU_LIB_VARIANT") == "sbtrace":   # DGPU_TRACE marks of the class code (group 8 = ALL_IE)
+if os.environ.get("DAV1D_GPU_SB_PHASE_MARKS"):   # DGPU_TRACE builds: the class code's marks (group 8 = ALL_IE)
     phases = torch.zeros(9 << 20, dtype=torch.int64, pin_memory=True)
     os.environ["DAV1D_GPU_SB_PHASES"] = str(phases.data_ptr())
 
@@ -45,13 +45,8 @@ def show(tag):
         r = tr[b]
         if not r.any():
             continue
-        waves = " ".join("w%d on %s fin %s" % (w, _d(r[2 * w]), _d(r[2 * w + 1])) for w in range(4))
+        waves = " ".join("w%d last task %s" % (w, int(r[2 * w + 1]) & 0xffffff if r[2 * w + 1] else "-") for w in range(4))
         print("wg %3d sb %s done %s | %s" % (b, hex(r[8]), hex(r[9]), waves), flush=True)
-
-
-def _d(v):
-    v = int(v)
-    return "-" if v == 0 else "%d/%d" % ((v >> 16) & 0x7fff, v & 0xffff)
 
 
 def watch():
