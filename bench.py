@@ -259,9 +259,9 @@ def tile_breakdown(fd, dev, stream, steps):
 def intra_breakdown(cfg, dev, stream, steps):
     """an all-intra frame of the config's size and
     bitdepth reconstructed on the device by the intra wavefront
-    (dav1d_gpu_recon_intra_frame_*: sb -- the headline ms_per_frame -- one
-    launch per frame, a workgroup per superblock (DGPU_IS_SB); persistent,
-    one launch per frame whose waves wait on their producers' tasks; levels,
+    (dav1d_gpu_recon_intra_frame_*: persistent -- the headline ms_per_frame --
+    one launch per frame whose waves wait on their producers' tasks; sb, one
+    launch per frame, a workgroup per superblock (DGPU_IS_SB); levels,
     the same launch waiting on per-level counters; and fused, one launch per
     level), one
     tile and 2x2 tiles; beside it the oracle in the decoder's own order on
@@ -283,7 +283,7 @@ def intra_breakdown(cfg, dev, stream, steps):
                 flow_error |= frame.flow_error()
                 got[mode] = frame.planes_host()
             del frame
-        ks = ms["sb"]
+        ks = ms["persistent"]
         ho = orc.HostIntraFrame(fr)
         t0 = time.perf_counter()
         ho.run()
@@ -292,7 +292,8 @@ def intra_breakdown(cfg, dev, stream, steps):
         n_sb = len(intra.sb_schedule(fr)[3]) - 1
         out[name] = {"units": int(len(fr.units)), "levels": int(fr.n_levels), "superblocks": n_sb,
                      "ms_per_frame": round(ks * 1e3, 3), "gpix_s": round(px / ks / 1e9, 4),
-                     "persistent_ms_per_frame": round(ms["persistent"] * 1e3, 3),
+                     "us_per_level": round(ks * 1e6 / fr.n_levels, 2),
+                     "sb_ms_per_frame": round(ms["sb"] * 1e3, 3),
                      "levels_ms_per_frame": round(ms["levels"] * 1e3, 3),
                      "fused_ms_per_frame": round(ms["fused"] * 1e3, 3),
                      "oracle_1core_ms": round(cpu_s * 1e3, 2), "flow_error": flow_error,

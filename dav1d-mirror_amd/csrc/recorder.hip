@@ -1112,6 +1112,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         for (size_t bi = bcut[t]; bi < bcut[t + 1] && !P.err; bi++) P.err = build(bi, P);
     };
     r->pool->run(nt, run_part);
+    lap("cut");
     // join: part bases (the aux pool keeps its 16-byte alignment rule)
     size_t n_cells = 0, n_x = 0, n_emu = 0, aux_end = 0, n_res_used = 0;
     std::vector<size_t> cb0(nt), xb0(nt), eb0(nt), ab0(nt), pb0(nt);
@@ -1184,7 +1185,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         }
     };
     r->pool->run(nt, join_part);
-    lap("cells");
+    lap("join");
     // levels and producers: a cell sits one level above every pixel its
     // edges (or CfL luma, or an inter-intra residual's prediction) read; its
     // producers are the cells that wrote them.  A pixel no cell of this flush
@@ -1319,16 +1320,26 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     //    pred (4) | mode (6) | type (5, NO_RESIDUAL last)
     if (n >= (1 << 21)) return -1;
     const int nthreads = r->pool->size();
+    const int npar = n < 32768 ? 1 : nthreads;   // (the O(n) passes below on the pool)
     std::vector<uint64_t> &keys = r->keys;
     keys.resize(n);
     int max_level = 0;
-    for (int i = 0; i < n; i++) {
-        const Unit &c = cells[i];
-        if (c.level >= (1 << 16)) return -1;
-        max_level = std::max(max_level, c.level);
-        const uint64_t key = (uint64_t)c.level << 20 | (uint64_t)c.u.tx << 15 | (uint64_t)c.u.pred << 11 |
-                             (uint64_t)(c.sortmode & 63) << 5 | (uint64_t)(c.u.txtp == DGPU_NO_RESIDUAL ? 31 : c.u.txtp);
-        keys[i] = key << 21 | (uint64_t)i;
+    {
+        std::vector<int> tmax(npar, 0);
+        r->pool->run(npar, [&](int t) {
+            int m = 0;
+            for (int i = (int)((int64_t)n * t / npar), e = (int)((int64_t)n * (t + 1) / npar); i < e; i++) {
+                const Unit &c = cells[i];
+                m = std::max(m, c.level);
+                const uint64_t key = (uint64_t)c.level << 20 | (uint64_t)c.u.tx << 15 | (uint64_t)c.u.pred << 11 |
+                                     (uint64_t)(c.sortmode & 63) << 5 |
+                                     (uint64_t)(c.u.txtp == DGPU_NO_RESIDUAL ? 31 : c.u.txtp);
+                keys[i] = key << 21 | (uint64_t)i;
+            }
+            tmax[t] = m;
+        });
+        for (int t = 0; t < npar; t++) max_level = std::max(max_level, tmax[t]);
+        if (max_level >= (1 << 16)) return -1;
     }
     {
         int lb = 0;
@@ -1340,19 +1351,38 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     r->unit_start.assign(n_levels + 1, 0);
     r->class_start.assign((size_t)n_levels * (NC + 1), 0);
     const size_t cb = r->bpc == 8 ? 2 : 4;
-    // the rank of every decode-order cell, and the level / class ranges
+    // the rank of every decode-order cell, and the level / class ranges: a
+    // (level, class) run ends where the sorted key's top bits change
     std::vector<int32_t> &rank = r->rank;
     rank.resize(n);
-    for (int i = 0; i < n; i++) {
-        const uint64_t k = keys[i];
-        const int ci = (int)(k & ((1u << 21) - 1)), level = (int)(k >> 41), tx = (int)((k >> 36) & 31);
-        rank[ci] = i;
-        r->unit_start[level + 1] = i + 1;
-        r->class_start[(size_t)level * (NC + 1) + tx + 1]++;
-    }
-    // the producer lists in level order (the persistent kernel's dataflow waits)
     r->dep_start.assign((size_t)n + 1, 0);
-    for (int ci = 0; ci < n; ci++) r->dep_start[rank[ci] + 1] = prod_start[ci + 1] - prod_start[ci];
+    r->pool->run(npar, [&](int t) {
+        for (int i = (int)((int64_t)n * t / npar), e = (int)((int64_t)n * (t + 1) / npar); i < e; i++) {
+            const uint64_t k = keys[i];
+            const int ci = (int)(k & ((1u << 21) - 1));
+            rank[ci] = i;
+            const uint64_t lt = k >> 36;   // level | tx
+            if (i + 1 == n || (keys[i + 1] >> 36) != lt) {   // the last of its (level, class) run
+                const int level = (int)(lt >> 5), tx = (int)(lt & 31);
+                r->class_start[(size_t)level * (NC + 1) + tx + 1] = i + 1;   // an end, made a count below
+                if (i + 1 == n || (int)(keys[i + 1] >> 41) != level) r->unit_start[level + 1] = i + 1;
+            }
+            r->dep_start[i + 1] = prod_start[ci + 1] - prod_start[ci];   // (producer lists in level order)
+        }
+    });
+    {   // run ends -> counts: the runs are in (level, class) order, so a run
+        // starts where the previous non-empty one ended
+        int32_t prev = 0;
+        for (int l = 0; l < n_levels; l++) {
+            int32_t *cs = &r->class_start[(size_t)l * (NC + 1)];
+            for (int k = 1; k <= NC; k++)
+                if (cs[k]) {
+                    const int32_t e = cs[k];
+                    cs[k] = e - prev;
+                    prev = e;
+                }
+        }
+    }
     for (int i = 0; i < n; i++) r->dep_start[i + 1] += r->dep_start[i];
     r->deps.resize(prod.size());
     for (int l = 0; l < n_levels; l++) {

@@ -28,13 +28,16 @@ def main():
     for t, (tw, th) in enumerate(abi.TX_WH):
         # lanes_per_unit, csrc/recon_kernel.hpp
         lanes[t] = 64 if tw * th >= 1024 else min(max(min(tw * th // 8, max(tw, min(th, 32))), 2), 64)
-    levels = []
+    levels, classes, firsts = [], [], []
     for l in range(fr.n_levels):
         cs = fr.class_start[l]
         for c in order:
             n = int(cs[c + 1] - cs[c])
             U = 64 // lanes[c]
-            levels += [l] * ((n + U - 1) // U)
+            nt_ = (n + U - 1) // U
+            levels += [l] * nt_
+            classes += [c] * nt_
+            firsts += [int(fr.unit_start[l] + cs[c] + U * k) for k in range(nt_)]
     nt = len(levels)
     ws = dev.workspace.cpu().numpy()
     base = (32 + 16 * fr.n_levels) * 4 + nt * 16 + fr.n_levels * 4
@@ -58,6 +61,30 @@ def main():
            "task_compute_us_p50": float(np.median(tr[:, 2] - tr[:, 1])) / 100.0,
            "release_us_p50": float(np.median(rel)) / 100.0,
            "ticket_to_ready_us_p50": float(np.median(tr[:, 1] - tr[:, 0])) / 100.0}
+    # per class: the post-wait part (ready -> computed) and how often a task
+    # of the class is its level's slowest; per prediction kind of the
+    # slowest tasks
+    comp = tr[:, 2] - tr[:, 1]
+    cl = np.array(classes)
+    slow = np.zeros(nt, bool)
+    for l in range(fr.n_levels):
+        idx = np.nonzero(lv == l)[0]
+        slow[idx[np.argmax(comp[idx])]] = True
+    per = {}
+    for c in sorted(set(classes)):
+        m = cl == c
+        tw, th = abi.TX_WH[c]
+        per[f"{tw}x{th}"] = {"tasks": int(m.sum()), "p50_us": round(float(np.median(comp[m])) / 100.0, 2),
+                             "p90_us": round(float(np.percentile(comp[m], 90)) / 100.0, 2),
+                             "slowest_of_level": int((slow & m).sum())}
+    out["per_class"] = per
+    kinds = {}
+    fi = np.array(firsts)
+    for t in np.nonzero(slow)[0]:
+        u = fr.units[fi[t]]
+        k = "cfl" if u["pred"] == abi.PRED_CFL else f"mode{int(u['mode']) & 15}"
+        kinds[k] = kinds.get(k, 0) + 1
+    out["slowest_task_kind"] = dict(sorted(kinds.items(), key=lambda kv: -kv[1]))
     print(json.dumps(out))
 
 
