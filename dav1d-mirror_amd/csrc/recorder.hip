@@ -102,15 +102,18 @@ struct DevBuf {
 };
 
 // page-locked staging, so the uploads do not wait for the stream.
-// DAV1D_GPU_REC_PIN (tuning): "default" hipHostMalloc, "nc" non-coherent
-// (CPU-cached) hipHostMalloc, "reg" (the default) hipHostRegister of an
-// ordinary aligned allocation: host memory the CPU caches like any other,
-// which the fill writes at memory speed
+// DAV1D_GPU_REC_PIN (tuning): "default" hipHostMalloc, "nc" (the default)
+// non-coherent hipHostMalloc (CPU-cached: the fill writes it at memory
+// speed), "reg" hipHostRegister of an ordinary aligned allocation.  Round 4
+// made "nc" the default: with "reg", every recorder's lifetime registers
+// and unregisters glibc memory that is later handed to other allocations,
+// and the process's later pageable copies are exactly where the
+// intermittent illegal-address faults of rounds 3-4 surfaced
 static int pin_mode() {
     static const int m = [] {
         const char *e = getenv("DAV1D_GPU_REC_PIN");
-        if (!e) return 2;
-        return !strcmp(e, "default") ? 0 : !strcmp(e, "nc") ? 1 : 2;
+        if (!e) return 1;
+        return !strcmp(e, "default") ? 0 : !strcmp(e, "reg") ? 2 : 1;
     }();
     return m;
 }
