@@ -40,7 +40,10 @@ def main():
             firsts += [int(fr.unit_start[l] + cs[c] + U * k) for k in range(nt_)]
     nt = len(levels)
     ws = dev.workspace.cpu().numpy()
-    base = (32 + 16 * fr.n_levels) * 4 + nt * 16 + fr.n_levels * 4
+    # the trace is the workspace's last part (flow_layout: counters, done
+    # flags, tasks, level counts, producer lists, trace)
+    n, nd = len(fr.units), len(fr.deps)
+    base = (32 + 16 * fr.n_levels) * 4 + ((n * 4 + 15) & ~15) + nt * 16 + fr.n_levels * 4 + (n + 1) * 4 + nd * 4
     base = (base + 15) & ~15
     assert base + nt * 32 == len(ws), (base + nt * 32, len(ws))   # same task list as the library
     tr = ws[base:base + nt * 32].view(np.uint64).reshape(nt, 4).astype(np.int64)
