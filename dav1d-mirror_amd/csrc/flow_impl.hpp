@@ -377,10 +377,29 @@ __global__ __launch_bounds__(64 * sb_waves<BPC>()) void k_flow_sb(ReconArgs<BPC>
     }
 }
 
+// Units per wave task in the wavefront (DAV1D_GPU_FLOW_UNITS overrides, for
+// measurements): a class's full wave (64 / lanes units: 32 for 4x4) puts
+// up to 32 units' edge gathers and several intra modes' code paths on one
+// wave, and the wavefront waits for its slowest task on every dependency
+// step; the flow trace shows the small classes' tasks are those
+// (intra wavefront)
+#ifndef DGPU_FLOW_UNITS
+#define DGPU_FLOW_UNITS 64
+#endif
+static int flow_units_cap() {
+    static const int cap = [] {
+        const char *e = getenv("DAV1D_GPU_FLOW_UNITS");
+        const int v = e ? atoi(e) : DGPU_FLOW_UNITS;
+        return v < 1 ? 1 : v > 64 ? 64 : v;
+    }();
+    return cap;
+}
+
 // host: the wave tasks of a schedule (level order, classes largest first)
 static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<FlowTask> &tasks,
                       std::vector<int32_t> &level_tasks) {
     constexpr int NC = DGPU_N_RECT_TX_SIZES;
+    const int cap = flow_units_cap();
     tasks.clear();
     level_tasks.assign(s->n_levels > 0 ? s->n_levels : 1, 0);
     for (int l = 0; l < s->n_levels; l++) {
@@ -391,7 +410,7 @@ static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<F
         for (int k = 0; k < NC; k++) {
             const int c = kOrder[k];
             if (cs[c + 1] < cs[c]) return -2;
-            const int U = 64 >> (int)((kLog2Lanes >> (3 * c)) & 7);
+            const int U = std::min(64 >> (int)((kLog2Lanes >> (3 * c)) & 7), cap);
             for (int i = cs[c]; i < cs[c + 1]; i += U) {
                 tasks.push_back(FlowTask{l, c, u0 + i, std::min(U, cs[c + 1] - i)});
                 level_tasks[l]++;

@@ -28,12 +28,13 @@ def main():
     for t, (tw, th) in enumerate(abi.TX_WH):
         # lanes_per_unit, csrc/recon_kernel.hpp
         lanes[t] = 64 if tw * th >= 1024 else min(max(min(tw * th // 8, max(tw, min(th, 32))), 2), 64)
+        lanes[t] = {(8, 16): 8, (4, 16): 4, (8, 32): 16}.get((tw, th), lanes[t])   # DGPU_TALL_LANES
     levels, classes, firsts = [], [], []
     for l in range(fr.n_levels):
         cs = fr.class_start[l]
         for c in order:
             n = int(cs[c + 1] - cs[c])
-            U = 64 // lanes[c]
+            U = min(64 // lanes[c], int(os.environ.get("DAV1D_GPU_FLOW_UNITS", "64")))
             nt_ = (n + U - 1) // U
             levels += [l] * nt_
             classes += [c] * nt_
