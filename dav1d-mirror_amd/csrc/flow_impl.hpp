@@ -377,14 +377,15 @@ __global__ __launch_bounds__(64 * sb_waves<BPC>()) void k_flow_sb(ReconArgs<BPC>
     }
 }
 
-// Units per wave task in the wavefront (DAV1D_GPU_FLOW_UNITS overrides, for
-// measurements): a class's full wave (64 / lanes units: 32 for 4x4) puts
-// up to 32 units' edge gathers and several intra modes' code paths on one
-// wave, and the wavefront waits for its slowest task on every dependency
-// step; the flow trace shows the small classes' tasks are those
-// (intra wavefront)
+// Units per wave task in the wavefront's levels above 0 (DAV1D_GPU_FLOW_UNITS
+// overrides, for measurements): a class's full wave (64 / lanes units: 32
+// for 4x4) puts up to 32 units' edge gathers and several intra modes' code
+// paths on one wave, and the wavefront waits for its slowest task on every
+// dependency step; the flow trace shows the small classes' tasks are those
+// (intra wavefront).  Level 0 (inter units, and intra units
+// with no producer) has no chain to shorten and keeps full waves.
 #ifndef DGPU_FLOW_UNITS
-#define DGPU_FLOW_UNITS 64
+#define DGPU_FLOW_UNITS 8   // 4K intra frame: 64 (a class's full wave) 19.6 ms, 16: 18.6, 8: 17.75, 4: 17.75
 #endif
 static int flow_units_cap() {
     static const int cap = [] {
@@ -410,7 +411,7 @@ static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<F
         for (int k = 0; k < NC; k++) {
             const int c = kOrder[k];
             if (cs[c + 1] < cs[c]) return -2;
-            const int U = std::min(64 >> (int)((kLog2Lanes >> (3 * c)) & 7), cap);
+            const int full = 64 >> (int)((kLog2Lanes >> (3 * c)) & 7), U = l ? std::min(full, cap) : full;
             for (int i = cs[c]; i < cs[c + 1]; i += U) {
                 tasks.push_back(FlowTask{l, c, u0 + i, std::min(U, cs[c + 1] - i)});
                 level_tasks[l]++;

@@ -10,8 +10,9 @@ is what pins the oracle beyond its own golden regression file: two
 transcriptions of the reference, written apart (the numpy one uses the
 direct rotation products in int64 where the reference and the C oracle use
 their overflow-free (c - 4096) forms, vectorised over whole batches of
-rows), must agree bit for bit.  Not restated here: the 64-point DCT (the C
-oracle alone covers it).
+rows), must agree bit for bit.  The 64-point DCT, warp8x8, blend*, emu_edge and
+scaled mc are restated in tests/test_cpu_restate_mc2.py, the intra_pred
+table in tests/test_cpu_restate_ipred.py (round 4).
 """
 import ctypes
 import os

@@ -34,7 +34,7 @@ def main():
         cs = fr.class_start[l]
         for c in order:
             n = int(cs[c + 1] - cs[c])
-            U = min(64 // lanes[c], int(os.environ.get("DAV1D_GPU_FLOW_UNITS", "64")))
+            U = min(64 // lanes[c], int(os.environ.get("DAV1D_GPU_FLOW_UNITS", "8"))) if l else 64 // lanes[c]
             nt_ = (n + U - 1) // U
             levels += [l] * nt_
             classes += [c] * nt_
