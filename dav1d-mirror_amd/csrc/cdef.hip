@@ -358,6 +358,15 @@ __device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, co
     else col_out<BPC, BH, false>(dst, ds, c, S, tp);
 }
 
+// DGPU_CDEF_ABL (cost-model probes, wrong output): 1 skips the direction
+// search, 2 the filter (blocks copied).  4K 8-bit frame: 41.6 us whole,
+// 41.0 without the directions, 16.1 without the filter, 13.1 without both
+// (DESIGN.md 4).  (Two superblocks per workgroup with the second one's loads
+// in flight during the first one's filter: 108 VGPRs, 4 waves per SIMD,
+// one round of workgroups instead of 1.6, measured 48.2 us: slower.)
+#ifndef DGPU_CDEF_ABL
+#define DGPU_CDEF_ABL 0
+#endif
 // DGPU_CDEF_WPE: a minimum of waves per SIMD for the register allocator
 // (0: the compiler's choice, 86 VGPRs = 5 waves)
 #ifndef DGPU_CDEF_WPE
@@ -415,7 +424,7 @@ void k_cdef(CdefArgs<BPC> a) {
     __syncthreads();
 
     // directions: wave q, lane = block (8 x 8 blocks of 8x8)
-    const bool need_dir = active && (ypri || uvpri);
+    const bool need_dir = active && (ypri || uvpri) && !(DGPU_CDEF_ABL & 1);
     if (need_dir) {
         const int q = threadIdx.x >> 6, blk = threadIdx.x & 63;
         const int bx8 = blk & 7, by8 = blk >> 3;
@@ -465,7 +474,7 @@ void k_cdef(CdefArgs<BPC> a) {
                 filt = true;
             }
         }
-        col_out<BPC, 8>(dst, a.os[0], c, LS, tp, filt);
+        col_out<BPC, 8>(dst, a.os[0], c, LS, tp, filt && !(DGPU_CDEF_ABL & 2));
     }
     if (!LAYOUT) return;
     __syncthreads();   // the luma tile is free: the chroma tiles go there
@@ -492,7 +501,7 @@ void k_cdef(CdefArgs<BPC> a) {
             tp.init(uvpri, uvsec, dir, damping - 1, bd8, CS);
             filt = true;
         }
-        col_out<BPC, CBH>(dst, a.os[1 + pl], c, CS, tp, filt);
+        col_out<BPC, CBH>(dst, a.os[1 + pl], c, CS, tp, filt && !(DGPU_CDEF_ABL & 2));
     }
 }
 

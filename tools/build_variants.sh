@@ -36,6 +36,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         ttrace) TUS=tile8 build ttrace -DDGPU_TILE_TRACE=1 ;;
         twpe2|twpe4|twpe5) TUS=tile8 build $v -DDGPU_TILE_WPE=${v#twpe} ;;
         cdefw6|cdefw7) TUS=cdef build $v -DDGPU_CDEF_WPE=${v#cdefw} ;;
+        cdefa1|cdefa2|cdefa3) TUS=cdef build $v -DDGPU_CDEF_ABL=${v#cdefa} ;;
         bounds) TUS="recon8 recon_ie8 recon_sb8 recorder" build bounds -DDGPU_BOUNDS=1 ;;
         fnofence) TUS="recon_ie8" build fnofence -DDGPU_FLOW_NOFENCE=1 ;;
         fsc1) TUS="recon_ie8" build fsc1 -DDGPU_FLOW_SC1=1 ;;
