@@ -328,6 +328,11 @@ __device__ __forceinline__ int lr_params(const Dav1dGpuLrUnit &u, bool hbd, Dav1
     return !!s0 + !!s1 * 2;
 }
 
+// DGPU_LR_ABL (cost-model probes, wrong output): 1 copies the self-guided
+// units, 2 the Wiener units
+#ifndef DGPU_LR_ABL
+#define DGPU_LR_ABL 0
+#endif
 // One (plane, stripe, 32-column strip): stripes are 64 rows (the first 8
 // luma rows shorter, :45-46), units unit_size columns (the last takes the
 // rest, :135-166) and a superblock row's unit row is chosen as lr_sbrow does
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     const Dav1dGpuLrUnit &u = f.units[pl][(size_t)urow * f.cols[pl] + ucol];
     const P *src = f.in[pl] + (size_t)y0 * f.is[pl];
     P *dst = f.out[pl] + (size_t)y0 * f.os[pl];
-    if (!f.restore[pl] || u.type == 0) {   // copied
+    if (!f.restore[pl] || u.type == 0 || ((DGPU_LR_ABL & 1) && u.type > 2) || ((DGPU_LR_ABL & 2) && u.type == 2)) {   // copied
         const int sw = min(kLrSW, w - xs), n = (y1 - y0) * kLrSW;   // <= 64 rows x 32
         constexpr int NC = (64 * kLrSW + 255) / 256;
         P cv[NC];

@@ -37,6 +37,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         twpe2|twpe4|twpe5) TUS=tile8 build $v -DDGPU_TILE_WPE=${v#twpe} ;;
         cdefw6|cdefw7) TUS=cdef build $v -DDGPU_CDEF_WPE=${v#cdefw} ;;
         cdefa1|cdefa2|cdefa3) TUS=cdef build $v -DDGPU_CDEF_ABL=${v#cdefa} ;;
+        lra1|lra2|lra3) TUS=lr build $v -DDGPU_LR_ABL=${v#lra} ;;
         bounds) TUS="recon8 recon_ie8 recon_sb8 recorder" build bounds -DDGPU_BOUNDS=1 ;;
         fnofence) TUS="recon_ie8" build fnofence -DDGPU_FLOW_NOFENCE=1 ;;
         fsc1) TUS="recon_ie8" build fsc1 -DDGPU_FLOW_SC1=1 ;;
