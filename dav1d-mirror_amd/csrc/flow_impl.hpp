@@ -171,7 +171,8 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
         }
         if constexpr (DGPU_FLOW_TRACE) tr1 = __builtin_amdgcn_s_memrealtime();
     };
-    dispatch<BPC, GROUP_ALL_IE>(a, pt, u, rec, cls, first, count, lds, 0, wait);
+    // (DGPU_TRACE builds: the class code's phase marks per task, a.trace)
+    dispatch<BPC, GROUP_ALL_IE>(a, pt, u, rec, cls, first, count, lds, DGPU_TRACE ? t : 0, wait);
     if constexpr (DGPU_FLOW_TRACE) {
         __builtin_amdgcn_s_waitcnt(0);
         tr2 = __builtin_amdgcn_s_memrealtime();
@@ -807,6 +808,9 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     a.aux_pool = (const uint8_t *)b->aux_pool;
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;
+    // DGPU_TRACE builds (diagnostics): the class code's phase marks per task,
+    // [group][task][16], to device memory at DAV1D_GPU_FLOW_PHASES
+    if (const char *e = getenv("DAV1D_GPU_FLOW_PHASES")) a.trace = (unsigned long long *)(uintptr_t)strtoull(e, nullptr, 0);
     constexpr int lds = wave_lds<BPC, GROUP_ALL_IE>();
     static std::once_flag once;
     std::call_once(once, [] {

@@ -53,6 +53,9 @@
 #ifndef DGPU_EARLY_REF1
 #define DGPU_EARLY_REF1 0  // issue the second ref's footprint loads up front
 #endif
+#ifndef DGPU_TRACE_RT
+#define DGPU_TRACE_RT 0
+#endif
 #ifndef DGPU_TRACE
 #define DGPU_TRACE 0       // per-wave phase timestamps (tools/wave_trace.py)
 #endif
@@ -1339,7 +1342,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #endif
         if constexpr (DGPU_TRACE) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            // DGPU_TRACE_RT: the 100 MHz clock of the flow trace instead of the core clock
+            const unsigned long long t = DGPU_TRACE_RT ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
             if (lane == 0) a.trace[((size_t)grp << 20) + (size_t)gw * 16 + i] = t;
         }
     };

@@ -19,6 +19,10 @@ def main():
     w, h = (int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "3840x2160").split("x"))
     fr = intra.make_intra_frame(intra.IntraConfig(width=w, height=h))
     dev = intra.DeviceIntraFrame(fr, mode="persistent")
+    phases = None
+    if os.environ.get("DAV1D_GPU_LIB_VARIANT") == "fphase":   # + the class code's marks per task (group 8)
+        phases = torch.zeros(9 << 20, dtype=torch.int64, device="cuda:0")
+        os.environ["DAV1D_GPU_FLOW_PHASES"] = str(phases.data_ptr())
     for _ in range(3):
         dev.launch()
     torch.cuda.synchronize()
@@ -89,6 +93,29 @@ def main():
         k = "cfl" if u["pred"] == abi.PRED_CFL else f"mode{int(u['mode']) & 15}"
         kinds[k] = kinds.get(k, 0) + 1
     out["slowest_task_kind"] = dict(sorted(kinds.items(), key=lambda kv: -kv[1]))
+    if phases is not None:
+        # marks (recon_kernel.hpp mark(i)): 0 entry, 2 loads committed, 4 row
+        # transforms done, 5 after the wait and the edge gather, 8 stored;
+        # tr[:, 1] is the end of the wait (same 100 MHz clock)
+        m = phases.cpu().numpy()[8 << 20:(8 << 20) + nt * 16].reshape(nt, 16).astype(np.int64)
+        ok = (m[:, 0] > 0) & (m[:, 5] > 0) & (m[:, 8] > 0)
+        ph = {}
+        for c in sorted(set(classes)):
+            sel = ok & (cl == c)
+            if not sel.any():
+                continue
+            tw, th = abi.TX_WH[c]
+            f = lambda v: round(float(np.median(v)) / 100.0, 2)   # noqa: E731
+            ph[f"{tw}x{th}"] = {"loads_us": f(m[sel, 2] - m[sel, 0]), "to_row_tx_us": f(m[sel, 4] - m[sel, 2]),
+                                "wait_end_to_gathered_us": f(m[sel, 5] - tr[sel, 1]),
+                                "gathered_to_stored_us": f(m[sel, 8] - m[sel, 5]),
+                                "stored_to_released_us": f(tr[sel, 3] - m[sel, 8])}
+        out["phases_p50"] = ph
+        sl = ok & slow
+        out["slowest_tasks_phases_mean_us"] = {
+            "wait_end_to_gathered": round(float((m[sl, 5] - tr[sl, 1]).mean()) / 100.0, 2),
+            "gathered_to_stored": round(float((m[sl, 8] - m[sl, 5]).mean()) / 100.0, 2),
+            "stored_to_released": round(float((tr[sl, 3] - m[sl, 8]).mean()) / 100.0, 2)}
     print(json.dumps(out))
 
 
