@@ -1638,6 +1638,19 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             } else {
                 gst<u32x2>(row, u32x2{(uint32_t)o0 | o1 << 16, (uint32_t)o2 | (uint32_t)o3 << 16});
             }
+            // GATHER: a superblock-bottom unit's last row also goes to top_edge
+            // (dav1d_backup_ipred_edge for its columns) straight from these
+            // registers: reading it back from the picture after the stores
+            // cost a store-to-load round trip on the wavefront's critical path
+            if constexpr (GATHER && !DGPU_FLOW_SC1) {
+                if (bkrow && 2 * j + rr == H - 1) {
+                    P *b = bkrow + 4 * q;
+                    bst(b + 0, (P)o0);
+                    bst(b + 1, (P)o1);
+                    bst(b + 2, (P)o2);
+                    bst(b + 3, (P)o3);
+                }
+            }
 #endif
         }
     };
@@ -1870,16 +1883,12 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             emit(j, q, pv);
         }
     }
-    if constexpr (GATHER) {   // dav1d_backup_ipred_edge for this unit's columns
+    if constexpr (GATHER && DGPU_FLOW_SC1) {   // dav1d_backup_ipred_edge for this unit's columns (emit does it otherwise)
         if (bkrow) {
             wave_sync();   // this wave's picture stores are visible to its own loads
             const P *last = dstp + (size_t)(H - 1) * ds;
-            if constexpr (DGPU_FLOW_SC1) {   // 4-pixel words, sc1 both ways (the hand-off's access sizes)
-                using WT = std::conditional_t<BPC == 8, uint32_t, uint64_t>;
-                for (int x = 4 * l; x < W; x += 4 * G) st_sc1<WT>(bkrow + x, ld_sc1<WT>(last + x));
-            } else {
-                for (int x = l; x < W; x += G) bkrow[x] = last[x];
-            }
+            using WT = std::conditional_t<BPC == 8, uint32_t, uint64_t>;   // 4-pixel words, sc1 both ways
+            for (int x = 4 * l; x < W; x += 4 * G) st_sc1<WT>(bkrow + x, ld_sc1<WT>(last + x));
         }
     }
     mark(8);
