@@ -145,7 +145,7 @@ class IntraSchedule(ctypes.Structure):
                 ("n_sb", ctypes.c_int32),
                 ("sb_level_start", ctypes.c_void_p),
                 ("sb_dep_start", ctypes.c_void_p),
-                ("sb_deps", ctypes.c_void_p)]
+                ("sb_deps", ctypes.c_void_p), ("task_group", ctypes.c_void_p)]
 
 
 class RecBlock(ctypes.Structure):

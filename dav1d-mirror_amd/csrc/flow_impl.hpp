@@ -413,9 +413,18 @@ static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<F
             const int c = kOrder[k];
             if (cs[c + 1] < cs[c]) return -2;
             const int full = 64 >> (int)((kLog2Lanes >> (3 * c)) & 7), U = l ? std::min(full, cap) : full;
-            for (int i = cs[c]; i < cs[c + 1]; i += U) {
-                tasks.push_back(FlowTask{l, c, u0 + i, std::min(U, cs[c + 1] - i)});
+            const uint8_t *tg = l ? s->task_group : nullptr;   // (one code path per task above level 0)
+            for (int i = cs[c]; i < cs[c + 1];) {
+                int e = std::min(i + U, cs[c + 1]);
+                if (tg)
+                    for (int k = i + 1; k < e; k++)
+                        if (tg[u0 + k] != tg[u0 + i]) {
+                            e = k;
+                            break;
+                        }
+                tasks.push_back(FlowTask{l, c, u0 + i, e - i});
                 level_tasks[l]++;
+                i = e;
             }
         }
     }

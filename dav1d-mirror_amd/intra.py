@@ -903,6 +903,14 @@ def edge_batch(fr, dst_ptrs, top_ptrs, units, edges, recs):
     return b
 
 
+def task_group_bytes(fr):
+    """Dav1dGpuIntraSchedule.task_group for an IntraFrame (schedule order):
+    prediction kind << 4 | coded intra mode, the keys the level sort orders
+    a size class's units by."""
+    return np.ascontiguousarray(((fr.units["pred"].astype(np.uint16) & 15) << 4 |
+                                 (fr.recs["mode"].astype(np.uint16) & 15)).astype(np.uint8))
+
+
 def sb_schedule(fr):
     """The superblock form of an IntraFrame's schedule (DGPU_IS_SB): every
     unit goes to the superblock holding its top-left pixel (4:2:0 chroma
@@ -964,7 +972,7 @@ class DeviceIntraFrame:
 
     MODES = ("persistent", "levels", "fused", "staged", "sb")
 
-    def __init__(self, fr, device="cuda:0", top_fill=0x5A, mode="persistent"):
+    def __init__(self, fr, device="cuda:0", top_fill=0x5A, mode="persistent", task_groups=True):
         """mode: persistent -- one launch per frame (DGPU_IS_PERSISTENT), a
         wave waits for the tasks of its units' producers (dataflow); levels --
         the same launch, a wave waits for the whole previous level; fused --
@@ -972,7 +980,9 @@ class DeviceIntraFrame:
         batch and backup runs per level; sb -- one launch per frame, a
         workgroup per superblock (DGPU_IS_SB, sb_schedule): units, records
         and the schedule in superblock order (units_frame_order() maps the
-        rewritten units back)."""
+        rewritten units back).  task_groups: the schedule's task_group bytes
+        (prediction kind and coded intra mode per unit), so a wave task of the
+        persistent kernels runs one mode's code path."""
         assert mode in self.MODES
         dataflow = mode == "persistent"
         self.sb = mode == "sb"
@@ -1023,6 +1033,9 @@ class DeviceIntraFrame:
             s.n_sb = self.n_sb
             s.sb_level_start, s.sb_dep_start, s.sb_deps = (a.ctypes.data for a in self._sb)
         s.unit_start, s.class_start, s.rec_start, s.run_start = (a.ctypes.data for a in self._host)
+        if task_groups:
+            self._tg = task_group_bytes(fr)
+            s.task_group = self._tg.ctypes.data
         s.runs = self.runs.data_ptr()
         if mode == "persistent" and dataflow and fr.dep_start is not None:
             self._host += [np.ascontiguousarray(fr.dep_start, np.int32),

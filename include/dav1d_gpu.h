@@ -690,6 +690,13 @@ typedef struct Dav1dGpuIntraSchedule {
     const int32_t *sb_dep_start;     /* host, n_sb + 1 (CSR)                     */
     const int32_t *sb_deps;          /* host: the earlier superblocks whose pixels
                                         or top_edge rows its units read          */
+    /* optional (round 4): host, one byte per unit of recon->units; above
+       level 0 a wave task never spans two units with different bytes.  Give
+       the units' prediction kind and coded intra mode ((pred << 4 | mode),
+       the order the schedule sorts them in), and each task runs one mode's
+       code path instead of several one after the other.  NULL: tasks are cut
+       by size only.                                                          */
+    const uint8_t *task_group;
 } Dav1dGpuIntraSchedule;
 
 /* Workspace a DGPU_IS_PERSISTENT schedule needs (bytes), or -2 if the

@@ -155,3 +155,59 @@ def test_sb_schedule(pkg, kw):
     # far fewer steps on the critical path than levels: a superblock waits
     # for at most its left, top-left, top and top-right neighbours
     assert np.all(np.diff(sds) <= 4)
+
+
+def _flow_tasks_py(pkg, fr, groups, cap=8):
+    """The wave tasks flow_impl.hpp's flow_tasks cuts (classes largest first
+    per level; above level 0 at most `cap` units, and with task groups never
+    across a change of the group byte)."""
+    abi = pkg.abi
+    order = [3, 9, 10, 2, 15, 16, 7, 8, 1, 13, 14, 5, 6, 0, 4, 11, 12, 17, 18]
+    tall = {(8, 16): 8, (4, 16): 4, (8, 32): 16}
+    lanes = {}
+    for t, (tw, th) in enumerate(abi.TX_WH):
+        lanes[t] = 64 if tw * th >= 1024 else tall.get((tw, th), min(max(min(tw * th // 8, max(tw, min(th, 32))), 2), 64))
+    n = 0
+    for lv in range(fr.n_levels):
+        cs = fr.class_start[lv]
+        for c in order:
+            full = 64 // lanes[c]
+            U = min(full, cap) if lv else full
+            i, e_ = int(fr.unit_start[lv] + cs[c]), int(fr.unit_start[lv] + cs[c + 1])
+            while i < e_:
+                e = min(i + U, e_)
+                if groups is not None and lv:
+                    k = i + 1
+                    while k < e and groups[k] == groups[i]:
+                        k += 1
+                    e = k
+                n += 1
+                i = e
+    return n
+
+
+def test_flow_task_cut(pkg):
+    """dav1d_gpu_intra_workspace_bytes (host code) sizes the persistent
+    kernel's workspace from the tasks it cuts: with and without the
+    schedule's task_group bytes it matches the Python restatement of the
+    cut (size cap above level 0, then one group per task)."""
+    import ctypes
+    abi = pkg.abi
+    fr = _frame(seed=42, width=512, height=256, inter_frac=0.3)
+    L = abi.load_lib()
+    n, nl = len(fr.units), fr.n_levels
+    keep = [np.ascontiguousarray(a, np.int32) for a in (fr.unit_start, fr.class_start, fr.dep_start, fr.deps)]
+    tg = pkg.intra.task_group_bytes(fr)
+    for groups in (None, tg):
+        s = abi.IntraSchedule()
+        s.n_levels = nl
+        s.flags = abi.IS_FUSED | abi.IS_PERSISTENT
+        s.unit_start, s.class_start = keep[0].ctypes.data, keep[1].ctypes.data
+        s.rec_start, s.run_start = keep[0].ctypes.data, keep[0].ctypes.data
+        s.dep_start, s.deps = keep[2].ctypes.data, keep[3].ctypes.data
+        if groups is not None:
+            s.task_group = groups.ctypes.data
+        nt = _flow_tasks_py(pkg, fr, groups)
+        want = (32 + 16 * nl) * 4 + ((n * 4 + 15) & ~15) + nt * 16 + nl * 4 + (n + 1) * 4 + len(fr.deps) * 4
+        assert L.dav1d_gpu_intra_workspace_bytes(ctypes.byref(s), n) == want, groups is not None
+    assert _flow_tasks_py(pkg, fr, tg) > _flow_tasks_py(pkg, fr, None)

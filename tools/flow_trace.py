@@ -34,15 +34,25 @@ def main():
         lanes[t] = 64 if tw * th >= 1024 else min(max(min(tw * th // 8, max(tw, min(th, 32))), 2), 64)
         lanes[t] = {(8, 16): 8, (4, 16): 4, (8, 32): 16}.get((tw, th), lanes[t])   # DGPU_TALL_LANES
     levels, classes, firsts = [], [], []
+    tg_all = intra.task_group_bytes(fr)
     for l in range(fr.n_levels):
         cs = fr.class_start[l]
         for c in order:
             n = int(cs[c + 1] - cs[c])
             U = min(64 // lanes[c], int(os.environ.get("DAV1D_GPU_FLOW_UNITS", "8"))) if l else 64 // lanes[c]
-            nt_ = (n + U - 1) // U
-            levels += [l] * nt_
-            classes += [c] * nt_
-            firsts += [int(fr.unit_start[l] + cs[c] + U * k) for k in range(nt_)]
+            tg = tg_all if l else None   # (the library's cut: size, then group changes)
+            i, e_ = int(fr.unit_start[l] + cs[c]), int(fr.unit_start[l] + cs[c + 1])
+            while i < e_:
+                e = min(i + U, e_)
+                if tg is not None:
+                    k = i + 1
+                    while k < e and tg[k] == tg[i]:
+                        k += 1
+                    e = k
+                levels.append(l)
+                classes.append(c)
+                firsts.append(i)
+                i = e
     nt = len(levels)
     ws = dev.workspace.cpu().numpy()
     # the trace is the workspace's last part (flow_layout: counters, done
@@ -111,6 +121,24 @@ def main():
                                 "gathered_to_stored_us": f(m[sel, 8] - m[sel, 5]),
                                 "stored_to_released_us": f(tr[sel, 3] - m[sel, 8])}
         out["phases_p50"] = ph
+        # 4x4 tasks by the intra modes of their units (device-rewritten modes:
+        # the remapped mode the prediction ran), the post-gather phase
+        uu = dev.units.cpu().numpy().view(fr.units.dtype)
+        c44 = [c for c in set(classes) if tuple(abi.TX_WH[c]) == (4, 4)][0]
+        cnt = np.array([min(64 // lanes[c_], int(os.environ.get("DAV1D_GPU_FLOW_UNITS", "8"))) if lv[t] else 64 // lanes[c_]
+                        for t, c_ in enumerate(classes)])
+        bym, bynm = {}, {}
+        for t in np.nonzero(ok & (cl == c44))[0]:
+            f0 = fi[t]
+            n_ = min(cnt[t], int(fr.unit_start[lv[t] + 1]) - f0)
+            mset = sorted(set(int(x) for x in (uu["mode"][f0:f0 + n_] & 15)))
+            key = "pal" if uu["pred"][f0] == abi.PRED_PAL else "cfl" if uu["pred"][f0] == abi.PRED_CFL else str(mset[0])
+            bym.setdefault(key, []).append(m[t, 8] - m[t, 5])
+            bynm.setdefault(len(mset), []).append(m[t, 8] - m[t, 5])
+        out["4x4_gathered_to_stored_p50_by_first_mode"] = {k: [len(v), round(float(np.median(v)) / 100.0, 2)]
+                                                           for k, v in sorted(bym.items())}
+        out["4x4_gathered_to_stored_p50_by_modes_in_task"] = {k: [len(v), round(float(np.median(v)) / 100.0, 2)]
+                                                              for k, v in sorted(bynm.items())}
         sl = ok & slow
         out["slowest_tasks_phases_mean_us"] = {
             "wait_end_to_gathered": round(float((m[sl, 5] - tr[sl, 1]).mean()) / 100.0, 2),
