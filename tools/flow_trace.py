@@ -40,7 +40,7 @@ def main():
         for c in order:
             n = int(cs[c + 1] - cs[c])
             U = min(64 // lanes[c], int(os.environ.get("DAV1D_GPU_FLOW_UNITS", "8"))) if l else 64 // lanes[c]
-            tg = tg_all if l else None   # (the library's cut: size, then group changes)
+            tg = tg_all if (l and os.environ.get("FLOW_TASK_GROUPS", "0") == "1") else None   # (the library's cut)
             i, e_ = int(fr.unit_start[l] + cs[c]), int(fr.unit_start[l] + cs[c + 1])
             while i < e_:
                 e = min(i + U, e_)

@@ -18,10 +18,10 @@ def main():
     import dav1d_mirror_amd.intra as intra
     orc = ge.load_oracle()
     out = {"units_cap": int(os.environ.get("DAV1D_GPU_FLOW_UNITS", "8")),
-           "task_groups": os.environ.get("FLOW_TASK_GROUPS", "1") == "1"}
+           "task_groups": os.environ.get("FLOW_TASK_GROUPS", "0") == "1"}
     for name, tiles in (("1_tile", (1, 1)), ("2x2_tiles", (2, 2))):
         fr = intra.make_intra_frame(intra.IntraConfig(width=3840, height=2160, tile_cols=tiles[0], tile_rows=tiles[1]))
-        dev = intra.DeviceIntraFrame(fr, mode="persistent", task_groups=os.environ.get("FLOW_TASK_GROUPS", "1") == "1")
+        dev = intra.DeviceIntraFrame(fr, mode="persistent", task_groups=os.environ.get("FLOW_TASK_GROUPS", "0") == "1")
         s = torch.cuda.current_stream()
         for _ in range(2):
             dev.launch(s)
