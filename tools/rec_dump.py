@@ -2,7 +2,7 @@
 schedule dumped (DAV1D_GPU_REC_HOSTONLY + DAV1D_GPU_REC_DUMP): compares two
 builds of the recorder's host code byte for byte, no GPU needed.
 
-  python tools/rec_dump.py OUT.bin     (prints one md5 per frame)"""
+  python tools/rec_dump.py OUT.bin [--only I]    (prints one md5 per frame)"""
 import ctypes
 import hashlib
 import os
@@ -22,6 +22,7 @@ FRAMES = [
 
 def main():
     out = sys.argv[1]
+    only = int(sys.argv[sys.argv.index("--only") + 1]) if "--only" in sys.argv else None
     os.environ["DAV1D_GPU_REC_HOSTONLY"] = "1"
     os.environ["DAV1D_GPU_REC_DUMP"] = out
     import __graft_entry__ as ge
@@ -29,6 +30,8 @@ def main():
     import dav1d_mirror_amd.abi as abi
     import dav1d_mirror_amd.intra as intra
     for i, kw in enumerate(FRAMES):
+        if only is not None and i != only:
+            continue
         if os.path.exists(out):
             os.remove(out)
         fr = intra.make_intra_frame(intra.IntraConfig(**kw))
