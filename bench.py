@@ -551,6 +551,48 @@ def lr_breakdown(cfg, dev, steps):
             "bit_exact_vs_oracle": all(bool(np.array_equal(a, b)) for a, b in zip(d.outputs_host(), want))}
 
 
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N
+    rank processes of this script with the rank environment torchrun would
+    set (one per GPU, RCCL rendezvous on 127.0.0.1), before this process has
+    touched the GPU, and exit with the first failing rank's status.  Rank 0
+    prints the JSON line; the others' stdout goes to stderr."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        log(f"bench: rank exit codes {codes}")
+    return bad[0] if bad else 0
+
+
+def dry_run(world, rank, local):
+    """--dry-run: the N-rank wiring without a GPU (gloo): every rank joins the
+    process group, passes the barrier and the max-over-ranks reduction the
+    timed region uses; rank 0 prints what it saw.  No bench number."""
+    import torch.distributed as dist
+    import dav1d_mirror_amd.shard as sh
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    got = sh.max_over_ranks(float(rank), dist, "cpu")
+    total = sh.sum_over_ranks(1, dist, "cpu")
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": total, "max_rank": got,
+                          "local_rank": local}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -572,14 +614,30 @@ def main():
     ap.add_argument("--no-superres", action="store_true", help="skip the super-res measurement (N=1)")
     ap.add_argument("--no-lpf", action="store_true", help="skip the deblocking measurement (N=1)")
     ap.add_argument("--no-lr", action="store_true", help="skip the loop-restoration measurement (N=1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="check the N-rank wiring only (gloo, no GPU, no bench number)")
     args = ap.parse_args()
+
+    # --gpus N is honoured: without a launcher this process starts the N
+    # ranks itself (before any GPU call); under a launcher its WORLD_SIZE must
+    # agree.  A 1-rank number is never reported under --gpus N > 1
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N ranks for --gpus N")
+    if args.dry_run:
+        ge.load_package()
+        dry_run(world, rank, local)
+        return
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     torch.cuda.set_device(local)
@@ -635,7 +693,19 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     el = sh.max_over_ranks(time.perf_counter() - t0, dist, dev)
-    kern_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
+    stream_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
+
+    # the kernel's own duration per launch (outside the timed region): an
+    # event pair around each launch, so host gaps between launches do not
+    # count (the stream time above includes them)
+    nk = min(args.steps, 100)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
+    for a, b in evs:
+        a.record(stream)
+        frame.launch(stream)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kern_s = sum(a.elapsed_time(b) for a, b in evs) * 1e-3 / nk
 
     # the timed frame's pixels against the oracle (outside the timed region;
     # the launches are idempotent, so the picture is the last step's)
@@ -688,9 +758,13 @@ def main():
                 "traffic": traffic,
                 "traffic_note": traffic_note,
                 "kernel": f"k_recon<{cfg.bpc},*> (main group: all classes up to 32x32 in one launch; "
-                          "the 64-point group launches only when such units exist; one HIP event pair on the "
-                          "launch stream brackets the K timed launches inside the wall-clock bracket)",
+                          "the 64-point group launches only when such units exist)",
                 "kernel_us": round(kern_s * 1e6, 2),
+                "kernel_us_note": f"mean of {nk} launches, each bracketed by its own HIP event pair on the "
+                                  "launch stream (kernel duration, like rocprofv3's)",
+                "stream_us_per_step": round(stream_s * 1e6, 2),
+                "stream_us_note": "one HIP event pair around the K timed launches inside the wall-clock "
+                                  "bracket, / K (includes any gap between launches)",
                 "rocprof_kernel_us": rocprof_kernel_us(cfg.bpc) if args.config != "1080p-mc" else None,
                 "frac_rocprof": (round(bytes_launch / (rocprof_kernel_us(cfg.bpc) * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
                                  if args.config != "1080p-mc" and rocprof_kernel_us(cfg.bpc) else None),

@@ -32,6 +32,14 @@
 #ifndef DGPU_FLOW_TRACE
 #define DGPU_FLOW_TRACE 0     // probe only: per-task s_memrealtime stamps after the task list
 #endif
+// Diagnostics builds only (tools/build_variants.sh sbdiag / fphase): the
+// superblock kernel's progress trace and the class code's phase marks are
+// written to addresses taken from the environment.  Product builds never read
+// those variables, so no environment can make the library store to an
+// arbitrary address
+#ifndef DGPU_DIAG
+#define DGPU_DIAG (DGPU_TRACE || DGPU_FLOW_TRACE)
+#endif
 #ifndef DGPU_FLOW_SLEEP
 #define DGPU_FLOW_SLEEP 8     // s_sleep between polls (x64 cycles)
 #endif
@@ -599,8 +607,10 @@ static int launch_flow_sb(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBa
     if (const char *sl = getenv("DAV1D_GPU_FLOW_SPIN_LIMIT")) f.spin_limit = (int)strtol(sl, nullptr, 0);
     f.trace = nullptr;
     f.debug = 0;
+#if DGPU_DIAG
     if (const char *e = getenv("DAV1D_GPU_SB_TRACE")) f.trace = (unsigned *)(uintptr_t)strtoull(e, nullptr, 0);
     if (const char *e = getenv("DAV1D_GPU_SB_DEBUG")) f.debug = (int)strtol(e, nullptr, 0);
+#endif
     {   // the task list and the schedule arrays through page-locked staging
         const size_t up = Lw.total - Lw.tasks;
         std::lock_guard<std::mutex> lock(g_stage_mu);
@@ -668,7 +678,9 @@ static int launch_flow_sb(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBa
     a.bdmax = BPC == 8 ? 255 : b->bitdepth_max;
     a.zero_coefs = b->zero_coefs;
     // DGPU_TRACE builds (diagnostics): the class code's phase marks to host memory
+#if DGPU_DIAG
     if (const char *e = getenv("DAV1D_GPU_SB_PHASES")) a.trace = (unsigned long long *)(uintptr_t)strtoull(e, nullptr, 0);
+#endif
     constexpr int WPB = sb_waves<BPC>();
     constexpr int lds = WPB * wave_lds<BPC, GROUP_ALL_IE>();
     static std::once_flag once;
@@ -819,7 +831,9 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     a.zero_coefs = b->zero_coefs;
     // DGPU_TRACE builds (diagnostics): the class code's phase marks per task,
     // [group][task][16], to device memory at DAV1D_GPU_FLOW_PHASES
+#if DGPU_DIAG
     if (const char *e = getenv("DAV1D_GPU_FLOW_PHASES")) a.trace = (unsigned long long *)(uintptr_t)strtoull(e, nullptr, 0);
+#endif
     constexpr int lds = wave_lds<BPC, GROUP_ALL_IE>();
     static std::once_flag once;
     std::call_once(once, [] {

@@ -102,39 +102,25 @@ struct DevBuf {
 };
 
 // page-locked staging, so the uploads do not wait for the stream.
-// DAV1D_GPU_REC_PIN (tuning): "default" hipHostMalloc, "nc" (the default)
-// non-coherent hipHostMalloc (CPU-cached: the fill writes it at memory
-// speed), "reg" hipHostRegister of an ordinary aligned allocation.  Round 4
-// made "nc" the default: with "reg", every recorder's lifetime registers
-// and unregisters glibc memory that is later handed to other allocations,
-// and the process's later pageable copies are exactly where the
-// intermittent illegal-address faults of rounds 3-4 surfaced
+// DAV1D_GPU_REC_PIN (tuning): "default" hipHostMalloc, otherwise (the
+// default) non-coherent hipHostMalloc (CPU-cached: the fill writes it at
+// memory speed).  Nothing in the library registers ordinary host memory:
+// round 5 removed the hipHostRegister mode that rounds 3-4 suspected of the
+// intermittent illegal-address faults
 static int pin_mode() {
     static const int m = [] {
         const char *e = getenv("DAV1D_GPU_REC_PIN");
-        if (!e) return 1;
-        return !strcmp(e, "default") ? 0 : !strcmp(e, "reg") ? 2 : 1;
+        return (e && !strcmp(e, "default")) ? 0 : 1;
     }();
     return m;
 }
 struct PinnedBuf {
     void *p = nullptr;
     size_t cap = 0;
-    int mode = -1;
     int grow(size_t n) {
         if (n <= cap) return 0;
         release();
-        mode = pin_mode();
-        if (mode == 2) {
-            const size_t sz = (n + 4095) & ~(size_t)4095;
-            void *q = nullptr;
-            if (posix_memalign(&q, 4096, sz)) return -1;
-            if (hipHostRegister(q, sz, hipHostRegisterDefault) != hipSuccess) {
-                free(q);
-                return -1;
-            }
-            p = q;
-        } else if (hipHostMalloc(&p, n, mode ? hipHostMallocNonCoherent : hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc(&p, n, pin_mode() ? hipHostMallocNonCoherent : hipHostMallocDefault) != hipSuccess) {
             p = nullptr;
             return -1;
         }
@@ -142,14 +128,7 @@ struct PinnedBuf {
         return 0;
     }
     void release() {
-        if (p) {
-            if (mode == 2) {
-                (void)hipHostUnregister(p);
-                free(p);
-            } else {
-                (void)hipHostFree(p);
-            }
-        }
+        if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
     }
@@ -1120,7 +1099,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     size_t n_cells = 0, n_x = 0, n_emu = 0, aux_end = 0, n_res_used = 0;
     std::vector<size_t> cb0(nt), xb0(nt), eb0(nt), ab0(nt), pb0(nt);
     std::vector<int32_t> erow0(nt);
-    int32_t emu_rows = 0;
+    int64_t emu_rows64 = 0;
     size_t edge_px = 0;
     for (int t = 0; t < nt; t++) {
         const CellPart &P = r->parts[t];
@@ -1128,17 +1107,25 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         cb0[t] = n_cells;
         xb0[t] = n_x;
         eb0[t] = n_emu;
-        erow0[t] = emu_rows;
+        erow0[t] = (int32_t)std::min<int64_t>(emu_rows64, INT32_MAX);
         pb0[t] = edge_px;
         ab0[t] = P.auxp.empty() ? aux_end : (aux_end + 15) & ~(size_t)15;
         if (!P.auxp.empty()) aux_end = ab0[t] + P.auxp.size();
         n_cells += P.cells.size();
         n_x += P.xunits.size();
         n_emu += P.emu.size();
-        emu_rows += P.emu_rows;
+        emu_rows64 += P.emu_rows;
         edge_px += P.edge_px;
         n_res_used += P.n_res_used;
     }
+    // every emulated-edge offset (a job's o0, a unit's src_off into the
+    // scratch, the kernels' row * kEmuStride) is int32 pixels: a flush whose
+    // scratch would pass 2^31 pixels fails instead of wrapping (a hostile
+    // stream of all-compound, all-outside cells reaches that below the 2^21
+    // cell limit).  The cut's part-local offsets may have wrapped
+    // already; none of them is used past this point
+    if ((emu_rows64 + 1) * kEmuStride + 256 > (int64_t)INT32_MAX) return -1;
+    const int32_t emu_rows = (int32_t)emu_rows64;
     if (n_res_used != r->residuals.size()) return -1;   // a residual outside every block
     cells.resize(n_cells);
     r->jobs.resize(n_cells);

@@ -178,3 +178,63 @@ def test_recorder_host_flush_repeatable(pkg, tmp_path):
     r = subprocess.run(["python3", "-c", _STAMP_CHILD, ROOT, str(tmp_path / "dump.bin")], env=env,
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
+_EMU_LIMIT_CHILD = r"""
+import ctypes, os, sys
+sys.path.insert(0, sys.argv[1])
+import __graft_entry__ as ge
+ge.load_package()
+import dav1d_mirror_amd.abi as abi
+L = abi.load_lib()
+W, H = 4096, 2304
+pw = [(W, H), (W // 2, H // 2), (W // 2, H // 2)]
+d = (abi.Plane * 3)()
+r = ((abi.Plane * 3) * abi.MAX_REFS)()
+for p, (w, h) in enumerate(pw):
+    d[p].data, d[p].stride, d[p].w, d[p].h = 0x1000, w, w, h
+    for k in range(2):
+        r[k][p].data, r[k][p].stride, r[k][p].w, r[k][p].h = 0x1000, w, w, h
+rec = L.dav1d_gpu_recorder_new(8, 255, W, H, 0)
+assert rec
+
+
+def record(planes):
+    b = abi.RecBlock()
+    b.kind, b.tx, b.filter2d = abi.PRED_INTER_AVG, abi.TX_INDEX[(4, 4)], 0
+    b.ref[0], b.ref[1] = 0, 1
+    for p in planes:
+        s = 16 if p == 0 else 8
+        w, h = pw[p]
+        b.plane, b.w, b.h = p, s, s
+        b.tile_x0, b.tile_y0, b.tile_x1, b.tile_y1 = 0, 0, w, h
+        for y in range(0, h, s):
+            for x in range(0, w, s):
+                b.x, b.y = x, y
+                # both references 3000 px left and above the picture, sub-pel:
+                # every 4x4 cell gets two clamped 11x11 footprints
+                b.mvx[0], b.mvy[0], b.mvx[1], b.mvy[1] = -48007, -48009, -48005, -48003
+                assert L.dav1d_gpu_rec_block(rec, ctypes.byref(b)) == 0
+
+
+record([0])   # 589824 cells, ~13.0 M scratch rows: below 2^31 pixels
+print("luma", L.dav1d_gpu_recorder_flush(rec, ctypes.byref(d), ctypes.byref(r), None), flush=True)
+record([0, 1, 2])   # 884736 cells, ~19.5 M rows: the offsets would wrap
+print("all", L.dav1d_gpu_recorder_flush(rec, ctypes.byref(d), ctypes.byref(r), None), flush=True)
+L.dav1d_gpu_recorder_free(rec)
+print("ok")
+"""
+
+
+def test_recorder_emu_scratch_limit(pkg):
+    """A flush whose emulated-edge scratch would pass 2^31 pixels (every
+    offset into it is int32) fails with -1 instead of wrapping:
+    all-compound 4x4 cells with both references outside a 4096x2304 picture,
+    host-only (no device).  The luma alone stays below the limit and flushes."""
+    env = dict(os.environ, DAV1D_GPU_REC_HOSTONLY="1")
+    env.pop("DAV1D_GPU_REC_DUMP", None)
+    r = subprocess.run(["python3", "-c", _EMU_LIMIT_CHILD, ROOT], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+    lines = dict(line.split() for line in r.stdout.splitlines() if line.split()[0] in ("luma", "all"))
+    assert lines == {"luma": "0", "all": "-1"}, r.stdout

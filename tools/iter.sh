@@ -49,7 +49,7 @@ for s in $STEPS; do
         grep "^recorder" "$O/rec.err" | tail -14
         ;;
     recpin)   # the recorder's staging allocation (DAV1D_GPU_REC_PIN), bench recorder leg each
-        for m in default nc reg; do
+        for m in default nc; do
             DAV1D_GPU_REC_PIN=$m timeout -k 10 300 python3 bench.py --no-cpu --steps 5 --warmup 1 --no-families --no-configs --no-tiles --no-intra \
                 --no-grain --no-cdef --no-superres --no-lpf --no-lr > "$O/recpin_$m.json" 2> "$O/recpin_$m.err" || { echo "recpin $m failed" >&2; tail -20 "$O/recpin_$m.err"; exit 1; }
             python3 -c "import json; d=json.load(open('$O/recpin_$m.json'))['recorder']; print('$m', d['flush_host_ms'], d['flush_device_ms'], d['frame_threads']['flush_host_ms_per_frame'], d['bit_exact_vs_oracle'], d['frame_threads']['bit_exact_vs_oracle'])"

@@ -1,0 +1,57 @@
+#!/bin/bash
+# Round-5 GPU check (run through gpurun from the repo root):
+#   bash tools/r5_gpu.sh <tag> [steps...]
+# steps: tests (full -m gpu suite), stests (the same with every kernel
+# serialized, AMD_SERIALIZE_KERNEL=3, so a fault is reported at its launch), bounds (the recorder tests on the
+# DGPU_BOUNDS build, tools/build_variants.sh bounds), smoke, bench (headline
+# line), prof (rocprofv3 kernel trace of the headline), pmc (FETCH / WRITE
+# passes), intra / cdef (those GPU test files), benchpart (the intra,
+# CDEF, LR and recorder bench legs), cdefpmc (CDEF / LR counters).  Every step has its own time limit; the first failure ends the run.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+T=${1:-r5}
+shift
+O=$R/gpurun_out/$T
+mkdir -p "$O"
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+BENCH_FAST="--no-families --no-configs --no-tiles --no-intra --no-recorder --no-grain --no-cdef --no-superres --no-lpf --no-lr --no-cpu --no-check"
+for s in "${@:-tests}"; do
+    echo "[r5] $s start $(date +%T)"
+    case $s in
+    tests) timeout -k 10 900 $PYT -m gpu -x tests > "$O/gputest.log" 2>&1 || { echo "[r5] tests failed"; exit 1; } ;;
+    stests) AMD_SERIALIZE_KERNEL=3 timeout -k 10 1200 $PYT -m gpu -x tests > "$O/gputest.log" 2>&1 || { echo "[r5] stests failed"; exit 1; } ;;
+    rectests) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_recorder.py tests/test_gpu_batch.py > "$O/rectest.log" 2>&1 || { echo "[r5] rectests failed"; exit 1; } ;;
+    bounds) # -s: the device printf reports must not be captured by pytest
+            DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 600 $PYT -s -m gpu tests/test_gpu_recorder.py > "$O/bounds.log" 2>&1
+            rc=$?; echo "[r5] bounds rc=$rc reports=$(grep -c 'DGPU_BOUNDS line' "$O/bounds.log")"; [ $rc -le 1 ] || exit 1
+            # positive control: the coefficient pool registered 64 bytes short must be reported
+            DAV1D_GPU_BND_SELFTEST=1 DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 300 $PYT -s -m gpu \
+                "tests/test_gpu_recorder.py::test_recorder_mixed" > "$O/bounds_selftest.log" 2>&1
+            echo "[r5] bounds selftest rc=$? reports=$(grep -c 'DGPU_BOUNDS line' "$O/bounds_selftest.log")" ;;
+    intra) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_intra_frame.py > "$O/intra.log" 2>&1 || { echo "[r5] intra failed"; exit 1; } ;;
+    cdef) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_cdef.py > "$O/cdef.log" 2>&1 || { echo "[r5] cdef failed"; exit 1; } ;;
+    benchpart) # the intra wavefront, CDEF, LR and recorder legs only (recorder host laps on stderr)
+            DAV1D_GPU_REC_TIMING=1 timeout -k 10 600 python -u bench.py --steps 50 --no-families --no-configs --no-tiles \
+                --no-grain --no-superres --no-lpf --no-cpu --no-check > "$O/benchpart.json" 2> "$O/benchpart.log" \
+                || { echo "[r5] benchpart failed"; exit 1; } ;;
+    checkasm) # the full checkasm-style space (no --quick), one pass per table and bitdepth
+            for t in mc ipred itx; do for b in 8 16; do
+                timeout -k 10 1200 ./tests/checkasm_gpu --test=$t --bpc=$b --seed=1 > "$O/checkasm_full_${t}_${b}.log" 2>&1 \
+                    || { echo "[r5] checkasm $t $b failed"; tail -5 "$O/checkasm_full_${t}_${b}.log"; exit 1; }
+                tail -1 "$O/checkasm_full_${t}_${b}.log"
+            done; done ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "[r5] smoke failed"; exit 1; } ;;
+    bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r5] bench failed"; exit 1; } ;;
+    benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r5] benchfast failed"; exit 1; } ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 50 $BENCH_FAST) > "$O/prof.log" 2>&1 || { echo "[r5] prof failed"; exit 1; } ;;
+    pmc) for c in FETCH_SIZE WRITE_SIZE; do
+             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/pmc_$c" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 $BENCH_FAST) > "$O/pmc_$c.log" 2>&1 || { echo "[r5] pmc $c failed"; exit 1; }
+         done ;;
+    cdefpmc) # CDEF / LR counters: the bench with only those legs (the headline frame runs too; filter by kernel)
+         for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS"; do
+             n=$(echo $c | cut -d' ' -f1)
+             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/cdefpmc_$n" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-families --no-configs --no-tiles --no-intra --no-recorder --no-grain --no-superres --no-lpf --no-cpu --no-check) > "$O/cdefpmc_$n.log" 2>&1 || { echo "[r5] cdefpmc $n failed"; exit 1; }
+         done ;;
+    esac
+    echo "[r5] $s done $(date +%T)"
+done

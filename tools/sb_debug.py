@@ -1,6 +1,8 @@
 """Diagnostics for the superblock wavefront (DGPU_IS_SB): one small frame,
 a short poll bound, then the error word, the superblock done flags and the
-pixel mismatches against the oracle.  Run on the GPU box under a timeout."""
+pixel mismatches against the oracle.  Run on the GPU box under a timeout,
+with the diagnostics build (tools/build_variants.sh sbdiag,
+DAV1D_GPU_LIB_VARIANT=sbdiag): product builds ignore DAV1D_GPU_SB_TRACE."""
 import os
 import sys
 import time
