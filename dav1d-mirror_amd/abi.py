@@ -278,6 +278,8 @@ def load_lib():
         L.dav1d_gpu_device_count.restype = ctypes.c_int
         L.dav1d_gpu_version.restype = ctypes.c_char_p
         L.dav1d_gpu_source_hash.restype = ctypes.c_char_p
+        L.dav1d_gpu_debug_register_buffer.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.dav1d_gpu_debug_register_buffer.restype = ctypes.c_int
         for bpc in (8, 16):
             f = getattr(L, f"dav1d_gpu_recon_tiles_{bpc}bpc")
             f.argtypes = [ctypes.POINTER(TileBatch), ctypes.c_void_p]
@@ -351,7 +353,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_intra_pred_dsp_init_gpu_8bpc", "dav1d_intra_pred_dsp_init_gpu_16bpc",
     "dav1d_itx_dsp_init_gpu_8bpc", "dav1d_itx_dsp_init_gpu_16bpc",
     "dav1d_gpu_device_count", "dav1d_gpu_set_device", "dav1d_gpu_version", "dav1d_gpu_source_hash",
-    "dav1d_gpu_get_error", "dav1d_gpu_clear_error",
+    "dav1d_gpu_get_error", "dav1d_gpu_clear_error", "dav1d_gpu_debug_register_buffer",
     "dav1d_gpu_pic_allocator_init", "dav1d_gpu_pic_allocator_close", "dav1d_gpu_picture_plane",
     "dav1d_gpu_recon_8bpc", "dav1d_gpu_recon_16bpc", "dav1d_gpu_recon_lds_bytes",
     "dav1d_gpu_recon_tiles_8bpc", "dav1d_gpu_recon_tiles_16bpc",

@@ -5,6 +5,7 @@ produced by libdav1d_gpu.so's HIP kernels through the C ABI
 (dav1d_gpu_recon_{8,16}bpc, include/dav1d_gpu.h).
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -183,6 +184,13 @@ class DeviceTiles:
         torch = self.torch
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         fn = self.lib.dav1d_gpu_recon_tiles_8bpc if self.fd.cfg.bpc == 8 else self.lib.dav1d_gpu_recon_tiles_16bpc
+        if os.environ.get("DAV1D_GPU_LIB_VARIANT") == "bounds":
+            # the diagnostics build checks every access against these exact
+            # buffers (ids: include/dav1d_gpu.h, csrc/bounds.hpp)
+            for t, bid in ((self.tiles, 21), (self.preds, 22), (self.txs, 23), (self.coefs, 12), (self.edges, 13),
+                           (self.aux_pool, 15)):
+                if t is not None and t.numel():
+                    self.lib.dav1d_gpu_debug_register_buffer(t.data_ptr(), t.numel() * t.element_size(), bid)
         rc = fn(ctypes.byref(self.batch), ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"dav1d_gpu_recon_tiles failed: {rc}")

@@ -16,6 +16,7 @@ enum BndId {
     BND_DST = 0, BND_REF = 1, BND_TOP = 2, BND_CFL = 3,
     BND_UNITS = 10, BND_RECS = 11, BND_COEF = 12, BND_EDGES = 13, BND_AUX = 14, BND_AUXPOOL = 15,
     BND_WORK = 16, BND_EMU = 17, BND_EMUJOBS = 18, BND_XUNITS = 19, BND_XAUX = 20,
+    BND_TILES = 21, BND_PREDS = 22, BND_TXS = 23,   // the tile batch (dav1d_gpu_debug_register_buffer)
 };
 struct BndRange {
     const void *p;

@@ -208,6 +208,17 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     dispatch<BPC, GRP>(a, pt, u, rec, cls, first, count, lds + wave * WL, gw);
 }
 
+// DGPU_PERSIST (round 5 experiment): the main group as
+// resident waves walking the wave schedule (csrc/recon_persist.hpp); measured
+// slower, so product builds leave it out
+#ifndef DGPU_PERSIST
+#define DGPU_PERSIST 0
+#endif
+#if DGPU_PERSIST
+template <int BPC, int GRP> __global__ void k_recon_p(ReconArgs<BPC> a);
+template <int BPC, int GRP> static int persist_blocks(int lds);
+#endif
+
 template <int BPC, int GRP>
 static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned classmask, hipStream_t stream) {
     constexpr int NC = DGPU_N_RECT_TX_SIZES;
@@ -237,7 +248,25 @@ static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned
     static std::once_flag once;
     std::call_once(once, [] {
         (void)hipFuncSetAttribute((const void *)k_recon<BPC, GRP>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+#if DGPU_PERSIST
+        if constexpr (GRP == GROUP_SMALL)
+            (void)hipFuncSetAttribute((const void *)k_recon_p<BPC, GRP>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+#endif
     });
+#if DGPU_PERSIST
+    if constexpr (GRP == GROUP_SMALL) {
+        const int res = persist_blocks<BPC, GRP>(lds);
+        if (res >= 8) {
+            k_recon_p<BPC, GRP><<<dim3(min(nblk, res)), 64 * WPB, lds, stream>>>(a);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) {
+                fprintf(stderr, "dav1d-gpu: recon launch failed: %s\n", hipGetErrorString(e));
+                return -3;
+            }
+            return 0;
+        }
+    }
+#endif
     k_recon<BPC, GRP><<<dim3(nblk), 64 * WPB, lds, stream>>>(a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -348,3 +377,7 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
 }
 
 }  // namespace dgpu
+
+#if DGPU_PERSIST
+#include "recon_persist.hpp"
+#endif

@@ -540,6 +540,9 @@ __device__ __forceinline__ void vdot5x4(const uint32_t (*a)[4], const uint32_t *
 // with 16-byte loads, in two steps so other loads can be issued in between:
 // load() issues the global loads, commit() writes LDS and returns the skew.
 // Reads stay inside the 16-B blocks holding the first and last byte.
+#ifndef DGPU_NT_STREAM
+#define DGPU_NT_STREAM 0   // experiment: read-once streams (coefficients, edges) by nontemporal loads
+#endif
 template <int MAXN, int G> struct Stage {
     static constexpr int IT = ((MAXN + 30) / 16 + G - 1) / G;
     u32x4 v[IT];
@@ -549,8 +552,13 @@ template <int MAXN, int G> struct Stage {
         const uint8_t *s = reinterpret_cast<const uint8_t *>(src) - sk;
         nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
 #pragma unroll
-        for (int k = 0; k < IT; k++)   // clamped
+        for (int k = 0; k < IT; k++) {   // clamped
+#if DGPU_NT_STREAM
+            v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(s + 16 * min(l + k * G, nch - 1)));
+#else
             v[k] = gld<u32x4>(s + 16 * min(l + k * G, nch - 1));
+#endif
+        }
     }
     __device__ __forceinline__ int commit(uint8_t *dst, int l) const {
 #pragma unroll

@@ -26,6 +26,24 @@ static int launch_tiles(const Dav1dGpuTileBatch *b, hipStream_t stream) {
     if (b->n_tiles == 0) return 0;
     TileArgs<BPC> a;
     memset(&a, 0, sizeof(a));
+#if DGPU_BOUNDS
+    {   // diagnostics: the planes and the buffers the caller registered
+        // (dav1d_gpu_debug_register_buffer, exact sizes); strict when any
+        DgpuBndTab t{};
+        for (int p = 0; p < 3; p++) {
+            bnd_add(t, b->dst[p], BND_DST);
+            for (int r = 0; r < DGPU_MAX_REFS; r++) bnd_add(t, b->ref[r][p], BND_REF);
+        }
+        bnd_add(t, b->cfl_luma, BND_CFL);
+        bnd_add_extra(t);
+        bnd_extra().clear();
+        bnd_print<P>(t, "tiles");
+        if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dgpu_bnd), &t, sizeof(t), 0, hipMemcpyHostToDevice, stream) != hipSuccess ||
+            hipStreamSynchronize(stream) != hipSuccess)
+            return -3;
+        a.bnd_noclamp = getenv("DAV1D_GPU_BND_NOCLAMP") != nullptr;
+    }
+#endif
     for (int p = 0; p < 3; p++) {
         a.dst[p] = (P *)b->dst[p].data;
         a.dst_stride[p] = (int)(b->dst[p].stride / B);

@@ -99,7 +99,27 @@ template <int BPC> struct TileArgs {
     int tile0, n_tiles;   // this launch's tile range
     int bdmax;
     int zero_coefs;
+#if DGPU_BOUNDS
+    int bnd_noclamp;   // DAV1D_GPU_BND_NOCLAMP self-test: the round-3 lane maps (no padding init, raw indices)
+#endif
 };
+
+// A record index read from the tile's LDS lane maps (pmap / txmap), clamped
+// to the tile's record count.  DGPU_BOUNDS builds report every index at or
+// past the count before clamping it (the stale-map mechanism of the round-3 /
+// round-4 faults), and with the NOCLAMP self-test use it raw, so the range
+// table sees where such a read would have landed.
+#if DGPU_BOUNDS
+__device__ __noinline__ int tile_index(int i, int n, int noclamp, int which, int line) {
+    if (i >= n && atomicAdd(&g_dgpu_bnd_hits, 1) < 256)
+        printf("DGPU_TILE_INDEX %s line %d index %d of %d block %d lane %d\n", which ? "pred" : "tx", line, i, n,
+               (int)blockIdx.x, (int)(threadIdx.x & 63));
+    return noclamp ? i : min(i, n - 1);
+}
+#define DGPU_TILE_INDEX(i, n, which) tile_index(i, n, a.bnd_noclamp, which, __LINE__)
+#else
+#define DGPU_TILE_INDEX(i, n, which) min(i, (n) - 1)
+#endif
 
 // the reference planes of a workgroup in LDS (lane-varying ref slots index it)
 template <int BPC> struct TileRefTab {
@@ -991,7 +1011,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         }
     };
     mark(0);
-    const Dav1dGpuTile T = a.tiles[a.tile0 + lb];
+    const Dav1dGpuTile T = bld(a.tiles + a.tile0 + lb);
     const int plane = T.plane;
     const int TW = T.w4 * 4, TH = T.h4 * 4;
 
@@ -1035,12 +1055,12 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
     if (haswarp && tid < 193) wv = reinterpret_cast<const uint2 *>(dspt_warp)[tid];
     // lane maps: each record writes its index over its lanes
     if (tid < T.n_tx) {
-        const Dav1dGpuTx tx = a.txs[T.tx0 + tid];
+        const Dav1dGpuTx tx = bld(a.txs + T.tx0 + tid);
         const int n = tile_tx_lanes((tx.w0 >> 8) & 31), l0 = tx.w1 >> 16;   // n >= 4, l0 a multiple of n
         for (int i = 0; i < n; i += 4) *reinterpret_cast<uint32_t *>(txmap + l0 + i) = 0x01010101u * (uint32_t)tid;
     }
     if (tid < T.n_pred) {
-        const uint4 ph = *reinterpret_cast<const uint4 *>(a.preds + T.pred0 + tid);   // kind .. lane0
+        const uint4 ph = bld(reinterpret_cast<const uint4 *>(a.preds + T.pred0 + tid));   // kind .. lane0
         const int kind = ph.x & 0xff, w4 = (ph.x >> 24) & 0xff, h4 = ph.y & 0xff, lg = (ph.y >> 24) & 0xff;
         const int l0 = ph.z & 0xffff;
         int n, base;
@@ -1060,6 +1080,9 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
     // index up to 255 past the tile's records read past the array's end:
     // the intermittent illegal-address faults of the round-3 / round-4
     // GPU runs)
+#if DGPU_BOUNDS
+    if (!a.bnd_noclamp)
+#endif
     for (int i = T.lanes_coop_used + tid; i < T.lanes_coop; i += kTileThreads) pmap[i] = 0;
     // zero the residual tile
     for (int i = tid; i < L::ACC / 16; i += kTileThreads) reinterpret_cast<u32x4 *>(acc)[i] = u32x4{0, 0, 0, 0};
@@ -1080,7 +1103,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
     // the coefficient-zeroing contract (src/itx_tmpl.c:55/89): every load of
     // the range completed before the barrier
     if (a.zero_coefs)
-        for (int i = tid; i < T.n_coef; i += kTileThreads) a.coef[T.coef0 + i] = 0;
+        for (int i = tid; i < T.n_coef; i += kTileThreads) bst<C>(a.coef + T.coef0 + i, 0);
 
     TileCtx<BPC> c;
     c.acc = acc;
@@ -1099,7 +1122,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         const int lane = base + tid;
         const bool act = lane < T.lanes_tx;
         Dav1dGpuTx tx = {0, 0};
-        if (act) tx = a.txs[T.tx0 + min((int)txmap[lane], T.n_tx - 1)];
+        if (act) tx = bld(a.txs + T.tx0 + DGPU_TILE_INDEX((int)txmap[lane], T.n_tx, 0));
         const int txs = (tx.w0 >> 8) & 31, txtp = (tx.w0 >> 13) & 31;
         const int nzw = (tx.w0 >> 18) & 63, nzh = (tx.w0 >> 24) & 63;
         const int l = lane - (int)(tx.w1 >> 16);
@@ -1156,7 +1179,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         const int lane = base + tid;
         const int wlane = base + (tid & ~63);   // wave-uniform: its section
         if (lane < lanes_pred) {
-            const Dav1dGpuPred p = a.preds[T.pred0 + min((int)pmap[lane], T.n_pred - 1)];
+            const Dav1dGpuPred p = bld(a.preds + T.pred0 + DGPU_TILE_INDEX((int)pmap[lane], T.n_pred, 1));
             if (wlane < T.lanes_coop) {
                 if (lane < T.lanes_coop_used && !(DGPU_TILE_ABL & 4)) tile_coop<BPC>(a, c, p, lane - p.lane0);
             } else {

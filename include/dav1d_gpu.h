@@ -211,6 +211,13 @@ const char *dav1d_gpu_source_hash(void);
  * variable DAV1D_GPU_FAIL_AFTER=n fails the (n+1)-th HIP call of the tier. */
 int dav1d_gpu_get_error(void);
 int dav1d_gpu_clear_error(void);
+/* Diagnostics (the DGPU_BOUNDS build, tools/build_variants.sh bounds): add
+ * one device buffer the calling thread's next tile-batch launch may touch,
+ * with its exact size in bytes; that launch then checks every record,
+ * coefficient, edge and aux access against the registered buffers and its
+ * planes, and clears the list.  Product builds never read the list: callers
+ * register only when they run the diagnostics build.  Returns 0. */
+int dav1d_gpu_debug_register_buffer(const void *p, size_t bytes, int id);
 
 /* ---- batch tier ----------------------------------------------------------
  * A batch is an array of transform-block "units" (one per inv_txfm_add call

@@ -38,7 +38,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         cdefw6|cdefw7) TUS=cdef build $v -DDGPU_CDEF_WPE=${v#cdefw} ;;
         cdefa1|cdefa2|cdefa3) TUS=cdef build $v -DDGPU_CDEF_ABL=${v#cdefa} ;;
         lra1|lra2|lra3) TUS=lr build $v -DDGPU_LR_ABL=${v#lra} ;;
-        bounds) TUS="recon8 recon_ie8 recon_sb8 recorder" build bounds -DDGPU_BOUNDS=1 ;;
+        bounds) TUS="recon8 recon_ie8 recon_sb8 recorder tile8 tile16" build bounds -DDGPU_BOUNDS=1 ;;
         fnofence) TUS="recon_ie8" build fnofence -DDGPU_FLOW_NOFENCE=1 ;;
         fsc1) TUS="recon_ie8" build fsc1 -DDGPU_FLOW_SC1=1 ;;
         fsleep1) TUS="recon_ie8" build fsleep1 -DDGPU_FLOW_SLEEP=1 ;;
@@ -58,6 +58,12 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         seg64) build seg64 -DDGPU_SEGMENTS=64 ;;
         seg1) build seg1 -DDGPU_SEGMENTS=1 ;;
         trace) build trace -DDGPU_TRACE=1 ;;
+        persist) TUS=recon8 build persist -DDGPU_PERSIST=1 -DDGPU_LANE_OPAQUE=1 ;;
+        persist2) TUS=recon8 build persist2 -DDGPU_PERSIST=2 -DDGPU_LANE_OPAQUE=1 ;;
+        persistn) TUS=recon8 build persistn -DDGPU_PERSIST=1 ;;
+        persist3) TUS=recon8 build persist3 -DDGPU_PERSIST=3 -DDGPU_LANE_OPAQUE=1 ;;
+        persist3n) TUS=recon8 build persist3n -DDGPU_PERSIST=3 ;;
+        ntload) TUS=recon8 build ntload -DDGPU_NT_STREAM=1 ;;
         merge) build merge -DDGPU_MERGE_GROUPS=1 ;;
         sl2) build sl2 -DDGPU_SEG_INNER=2 ;;
         early1) build early1 -DDGPU_EARLY_REF1=1 ;;

@@ -28,6 +28,15 @@ for s in "${@:-tests}"; do
             DAV1D_GPU_BND_SELFTEST=1 DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 300 $PYT -s -m gpu \
                 "tests/test_gpu_recorder.py::test_recorder_mixed" > "$O/bounds_selftest.log" 2>&1
             echo "[r5] bounds selftest rc=$? reports=$(grep -c 'DGPU_BOUNDS line' "$O/bounds_selftest.log")" ;;
+    tbounds) # the tile batch under the bounds build: every record / coefficient / edge / aux access against the
+             # exact buffers, record indices against the tile's counts; then the round-3 lane maps restored
+             # (DAV1D_GPU_BND_NOCLAMP: no padding init, raw indices) as the positive control
+            DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 600 $PYT -s -m gpu tests/test_gpu_tiles.py > "$O/tbounds.log" 2>&1
+            rc=$?; echo "[r5] tbounds rc=$rc range=$(grep -c 'DGPU_BOUNDS line' "$O/tbounds.log") index=$(grep -c 'DGPU_TILE_INDEX' "$O/tbounds.log")"
+            [ $rc -le 1 ] || exit 1
+            DAV1D_GPU_BND_NOCLAMP=1 DAV1D_GPU_LIB_VARIANT=bounds timeout -k 10 600 $PYT -s -m gpu tests/test_gpu_tiles.py > "$O/tbounds_noclamp.log" 2>&1
+            rc=$?; echo "[r5] tbounds noclamp rc=$rc range=$(grep -c 'DGPU_BOUNDS line' "$O/tbounds_noclamp.log") index=$(grep -c 'DGPU_TILE_INDEX' "$O/tbounds_noclamp.log")"
+            [ $rc -le 1 ] || exit 1 ;;
     intra) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_intra_frame.py > "$O/intra.log" 2>&1 || { echo "[r5] intra failed"; exit 1; } ;;
     cdef) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_cdef.py > "$O/cdef.log" 2>&1 || { echo "[r5] cdef failed"; exit 1; } ;;
     benchpart) # the intra wavefront, CDEF, LR and recorder legs only (recorder host laps on stderr)
@@ -40,6 +49,15 @@ for s in "${@:-tests}"; do
                     || { echo "[r5] checkasm $t $b failed"; tail -5 "$O/checkasm_full_${t}_${b}.log"; exit 1; }
                 tail -1 "$O/checkasm_full_${t}_${b}.log"
             done; done ;;
+    ab) # headline-frame A/B of variant libraries (ABV="persist persist2"): kernel us per variant, bit-exact check on
+        for v in base $ABV; do
+            if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
+            timeout -k 10 300 python -u bench.py --no-families --no-configs --no-tiles --no-intra --no-recorder --no-grain \
+                --no-cdef --no-superres --no-lpf --no-lr --no-cpu --steps ${ABSTEPS:-200} > "$O/ab_$v.json" 2> "$O/ab_$v.log" \
+                || { echo "[r5] ab $v failed"; tail -5 "$O/ab_$v.log"; exit 1; }
+            python3 -c "import json; d=json.load(open('$O/ab_$v.json')); r=d['roofline']; print('ab $v', r['kernel_us'], r.get('stream_us_per_step'), d['ms_per_step'], d['config'].get('bit_exact_vs_oracle'))"
+        done
+        unset DAV1D_GPU_LIB_VARIANT ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "[r5] smoke failed"; exit 1; } ;;
     bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r5] bench failed"; exit 1; } ;;
     benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r5] benchfast failed"; exit 1; } ;;
