@@ -99,7 +99,13 @@ class DeviceFrame:
         torch = self.torch
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         fn = self.lib.dav1d_gpu_recon_8bpc if self.fd.cfg.bpc == 8 else self.lib.dav1d_gpu_recon_16bpc
+        # (the unit batch reads references with their edge-replicated
+        # borders: the whole padded allocation is the reference's range)
+        _bounds_buffers(self.lib, [(self.units, 10), (self.coefs, 12), (self.edges, 13)] +
+                        [(t, 14 if i == 0 else 15) for i, t in enumerate((self.aux, self.aux_pool))] +
+                        [(t, 1) for planes in self.refs for t in planes])
         rc = fn(ctypes.byref(self.batch), ctypes.c_void_p(s.cuda_stream))
+        _bounds_buffers(self.lib, None)
         if rc != 0:
             raise RuntimeError(f"dav1d_gpu_recon failed: {rc}")
 
@@ -117,6 +123,22 @@ class DeviceFrame:
         ts = [self.units, self.coefs, self.edges, self.cfl_luma] + list(self.dst)
         ts += [t for planes in self.refs for t in planes]
         return ts + [t for t in (self.aux, self.aux_pool) if t is not None]
+
+
+def _bounds_buffers(lib, bufs):
+    """The diagnostics build (DAV1D_GPU_LIB_VARIANT=bounds): register the
+    batch's own device buffers for its next launch (ids: csrc/bounds.hpp),
+    each up to the end of the 16-byte block holding its last byte (the
+    kernels read coefficients, edges and records as aligned 16-byte blocks;
+    include/dav1d_gpu.h states the contract).  bufs=None clears the list."""
+    if os.environ.get("DAV1D_GPU_LIB_VARIANT") != "bounds":
+        return
+    lib.dav1d_gpu_debug_register_buffer(None, 0, 0)   # clear
+    for t, bid in bufs or ():
+        if t is not None and t.numel():
+            n = t.numel() * t.element_size()
+            n += (-(t.data_ptr() + n)) & 15
+            lib.dav1d_gpu_debug_register_buffer(t.data_ptr(), n, bid)
 
 
 class DeviceTiles:
@@ -184,14 +206,10 @@ class DeviceTiles:
         torch = self.torch
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         fn = self.lib.dav1d_gpu_recon_tiles_8bpc if self.fd.cfg.bpc == 8 else self.lib.dav1d_gpu_recon_tiles_16bpc
-        if os.environ.get("DAV1D_GPU_LIB_VARIANT") == "bounds":
-            # the diagnostics build checks every access against these exact
-            # buffers (ids: include/dav1d_gpu.h, csrc/bounds.hpp)
-            for t, bid in ((self.tiles, 21), (self.preds, 22), (self.txs, 23), (self.coefs, 12), (self.edges, 13),
-                           (self.aux_pool, 15)):
-                if t is not None and t.numel():
-                    self.lib.dav1d_gpu_debug_register_buffer(t.data_ptr(), t.numel() * t.element_size(), bid)
+        _bounds_buffers(self.lib, ((self.tiles, 21), (self.preds, 22), (self.txs, 23), (self.coefs, 12),
+                                   (self.edges, 13), (self.aux_pool, 15)))
         rc = fn(ctypes.byref(self.batch), ctypes.c_void_p(s.cuda_stream))
+        _bounds_buffers(self.lib, None)
         if rc != 0:
             raise RuntimeError(f"dav1d_gpu_recon_tiles failed: {rc}")
 

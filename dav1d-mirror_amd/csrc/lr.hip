@@ -9,10 +9,12 @@
 // rows (0, 0, 1 above; 6, 7, 7 below) or the first / last row, columns left
 // of the unit from `left` or replicated, right of it from the picture or
 // replicated.  Wiener: the horizontal 7-tap pass into LDS (uint16 range
-// clip), then the vertical one.  Self-guided: A / B (box sums, the
-// dav1d_sgr_x_by_x lookup and the inversion, with the reference's unsigned
-// arithmetic) at every position the 6- / 8-neighbour weighting reads, then
-// the weighting and the w0 / w1 blend.  Latency-bound per call like the
+// clip), then the vertical one.  Self-guided (round 5: both radii in one
+// pass): A / B of the 5x5 and 3x3 boxes from horizontal sums slid down each
+// column in registers (the reference's boxsum5 / boxsum3, the
+// dav1d_sgr_x_by_x lookup and the inversion, with its unsigned arithmetic),
+// one barrier, then both weightings and the w0 / w1 blend per pixel.
+// Latency-bound per call like the
 // other per-call entries.
 //
 // Frame tier, k_lr_frame: bytefn(dav1d_lr_sbrow) (lr_apply_tmpl.c:169-202)
@@ -46,57 +48,14 @@ template <int BPC> struct LrArgs {
     Dav1dGpuLrParams prm;
 };
 
-// Vertical box sums of radius R for selfguided_filter's box_sum (:373-376):
-// VS[jj][c] = sum of tile column c over the 2R + 1 rows around unit row
-// jj - 1, VQ the same of the squares, for jj = 0..h + 1 and every tile
-// column.  A thread runs down a chunk of one column with a running sum (two
-// reads per row instead of 2R + 1).
-constexpr int kLrVH = 66;   // rows of the vertical sums: unit rows -1..64
-template <int R>
-__device__ __forceinline__ void lr_vsums(const int16_t (*T)[kLrTW], int16_t (*VS)[kLrTW], int (*VQ)[kLrTW], int h,
-                                         int sw) {
-    constexpr int CH = 11;   // rows per chunk
-    // (every index below is divided by a compile-time stride: a division by
-    // a runtime strip width cost ~40 VALU per use and dominated the kernel)
-    const int nrow = h + 2, nchunk = (nrow + CH - 1) / CH;
-    for (int t = threadIdx.x; t < kLrTW * nchunk; t += 256) {
-        const int ck = t / kLrTW, c = t - ck * kLrTW;
-        if (c >= sw + 6) continue;
-        const int jj0 = ck * CH, jj1 = min(jj0 + CH, nrow);
-        int s = 0, q = 0;   // tile rows jj + 2 - R .. jj + 2 + R (unit row jj - 1 is tile row jj + 2)
-#pragma unroll
-        for (int d = -R; d <= R; d++) {
-            const int v = T[jj0 + 2 + d][c];
-            s += v;
-            q += v * v;
-        }
-        VS[jj0][c] = (int16_t)s;   // <= 5 x 4095
-        VQ[jj0][c] = q;
-        for (int jj = jj0 + 1; jj < jj1; jj++) {
-            const int vi = T[jj + 2 + R][c], vo = T[jj + 1 - R][c];
-            s += vi - vo;
-            q += vi * vi - vo * vo;
-            VS[jj][c] = (int16_t)s;
-            VQ[jj][c] = q;
-        }
-    }
-}
+constexpr int kLrVH = 66;   // A / B rows: unit rows -1..64
 
-// A / B of selfguided_filter (:373-392) at unit position (jj - 1, ii - 1)
-// for box radius R (n = 25 or 9): the horizontal sum of the vertical sums
-// (a register-sliding variant, a thread per row segment, measured slower:
-// fewer busy lanes and a longer dependent chain per thread)
-template <int R>
-__device__ __forceinline__ void lr_ab(const int16_t (*VS)[kLrTW], const int (*VQ)[kLrTW], int jj, int ii, unsigned s,
-                                     int bd8, const uint8_t *x_by_x, int &A, int &B) {
-    constexpr int n = (2 * R + 1) * (2 * R + 1);
+// A / B of selfguided_filter (:373-392) from one position's box sum and sum
+// of squares (n = 25 or 9), with the reference's unsigned arithmetic
+template <int n>
+__device__ __forceinline__ void lr_ab_sums(int sum, int sumsq, unsigned s, int bd8, const uint8_t *x_by_x, int &A,
+                                           int &B) {
     constexpr unsigned one_by_x = n == 25 ? 164 : 455;
-    int sum = 0, sumsq = 0;
-#pragma unroll
-    for (int dx = -R; dx <= R; dx++) {
-        sum += VS[jj][ii + 2 + dx];
-        sumsq += VQ[jj][ii + 2 + dx];
-    }
     const int a = (sumsq + ((1 << (2 * bd8)) >> 1)) >> (2 * bd8);
     const int b = (sum + ((1 << bd8) >> 1)) >> bd8;
     const unsigned p = (unsigned)max(a * n - b * b, 0);
@@ -115,18 +74,19 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     // horizontal sums, 5-row box sums, B = x_by_x <= 255): 31.8 KB, five
     // workgroups per CU
     __shared__ int16_t T[kLrTH][kLrTW];
-    __shared__ int AA[66][kLrSW + 2];        // A at unit rows -1..h, strip columns -1..sw
-    __shared__ uint8_t BB[66][kLrSW + 2];    // B
-    // Wiener's horizontal pass, or the self-guided vertical box sums
-    __shared__ int SCR[kLrVH * kLrTW + (kLrVH * kLrTW + 1) / 2];
+    // 3x3 A / B at unit rows -1..h (every row), strip columns -1..sw; the
+    // Wiener units' horizontal pass reuses the A array
+    __shared__ int AA[kLrVH][kLrSW + 2];
+    __shared__ uint8_t BB[kLrVH][kLrSW + 2];
+    // 5x5 A / B at unit rows -1, 1, .. (row jj at jj / 2)
+    __shared__ int AA5[kLrVH / 2][kLrSW + 2];
+    __shared__ uint8_t BB5[kLrVH / 2][kLrSW + 2];
     // sgr_x_by_x in LDS: a global-memory lookup per A / B position put one
     // memory round trip per loop iteration on the block's critical path
     __shared__ uint8_t XBX[256];
     if (a.kind) XBX[threadIdx.x] = dspt_sgr_x_by_x[threadIdx.x];
-    int16_t(*HOR)[kLrSW] = reinterpret_cast<int16_t(*)[kLrSW]>(SCR);
-    int(*VQ)[kLrTW] = reinterpret_cast<int(*)[kLrTW]>(SCR);
-    int16_t(*VS)[kLrTW] = reinterpret_cast<int16_t(*)[kLrTW]>(SCR + kLrVH * kLrTW);
-    static_assert(kLrTH * kLrSW * 2 <= (int)sizeof(SCR), "HOR fits the scratch");
+    int16_t(*HOR)[kLrSW] = reinterpret_cast<int16_t(*)[kLrSW]>(&AA[0][0]);
+    static_assert(kLrTH * kLrSW * 2 <= (int)sizeof(AA), "HOR fits the A array");
     const int sw = min(kLrSW, a.w - x0), h = a.h;
     const int bd8 = bits_of(a.bdmax) - 8;
     {   // a thread per tile column and sixth of the rows: the column's
@@ -205,81 +165,125 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
         }
         return;
     }
-    int v[8];
-#pragma unroll
-    for (int m = 0; m < 8; m++) v[m] = 0;
-    for (int pass = 0; pass < 2; pass++) {
-        const bool five = pass == 0;
-        if (five ? a.kind == 2 : a.kind == 1) continue;
-        if (five) lr_vsums<2>(T, VS, VQ, h, sw);
-        else lr_vsums<1>(T, VS, VQ, h, sw);
-        __syncthreads();
-        // A / B at unit rows -1..h (every other row from -1 for 5x5, :375)
-        // (5x5: only the odd unit rows, jj = 0, 2, .. <= h + 1)
-        const int nab = five ? (h + 1) / 2 + 1 : h + 2;
-        for (int k = threadIdx.x; k < nab * (kLrSW + 2); k += 256) {
-            const int q = k / (kLrSW + 2), ii = k - q * (kLrSW + 2), jj = five ? 2 * q : q;
-            if (ii >= sw + 2) continue;
-            int A, B;
-            if (five) lr_ab<2>(VS, VQ, jj, ii, a.prm.sgr.s0, bd8, XBX, A, B);
-            else lr_ab<1>(VS, VQ, jj, ii, a.prm.sgr.s1, bd8, XBX, A, B);
-            AA[jj][ii] = A;
-            BB[jj][ii] = (uint8_t)B;
-        }
-        __syncthreads();
-        const int wgt = five ? a.prm.sgr.w0 : a.prm.sgr.w1;
-        // the weighting (:397-439), a thread per column and run of RPT rows
-        // sliding down it: each A / B row is read once per thread as a
-        // (sum over columns ii-1..ii+1, centre) pair, from which the 6/5 and
-        // 4/3 neighbour weights follow:
-        //   EIGHT: 4 s1 + 3 (s0 + s2) + c0 + c2;  SIX (even j): 5 (s0 + s2) +
-        //   c0 + c2;  odd j: 5 s1 + c1  (rows 0/1/2 = unit rows j-1, j, j+1)
-        if (wj0 < h && wi < sw) {
-            const int ii = wi + 1;
-            int s0a = 0, c0a = 0, s0b = 0, c0b = 0, s1a = 0, c1a = 0, s1b = 0, c1b = 0;
-            auto row = [&](int k, int &sa, int &ca, int &sb, int &cb) {
-                const int a0 = AA[k][ii - 1], a1 = AA[k][ii], a2 = AA[k][ii + 1];
-                const int b0 = BB[k][ii - 1], b1 = BB[k][ii], b2 = BB[k][ii + 1];
-                sa = a0 + a1 + a2;
-                ca = a1;
-                sb = b0 + b1 + b2;
-                cb = b1;
+    // ---- self-guided (selfguided_filter, :349-440), both radii in one pass ----
+    // A / B: a thread per A / B column ii (unit column ii - 1) and run of
+    // rows, sliding down the tile: per new tile row the 5- and 3-wide
+    // horizontal sums and sums of squares (the 3-wide ones are the middle of
+    // the 5-wide window), kept for the last five rows in registers, give the
+    // 5x5 box (rows jj .. jj + 4) and the 3x3 box (jj + 1 .. jj + 3) around
+    // unit row jj - 1 -- the reference's boxsum5 / boxsum3 (:211-347) at
+    // every position its A / B loop reads, with no vertical-sum array and no
+    // barrier between the radii.  5x5 A / B exist on every other row from -1
+    // (:375), stored at jj / 2.
+    const bool do5 = a.kind != 2, do3 = a.kind != 1;
+    {
+        constexpr int NCOL = kLrSW + 2, NCH = 256 / NCOL, CH = (kLrVH + NCH - 1) / NCH;   // 34 columns, 7 runs of 10 rows
+        const int t = threadIdx.x, ii = t % NCOL, ck = t / NCOL;
+        const int nrow = h + 2, jj0 = ck * CH, jj1 = min(jj0 + CH, nrow);
+        if (ck < NCH && ii < sw + 2 && jj0 < jj1) {
+            const int c = ii + 2;   // tile column of unit column ii - 1
+            int h5[5], q5[5], h3[5], q3[5];
+            auto hrow = [&](int r, int &s5, int &sq5, int &s3, int &sq3) {
+                const int p0 = T[r][c - 2], p1 = T[r][c - 1], p2 = T[r][c], p3 = T[r][c + 1], p4 = T[r][c + 2];
+                s3 = p1 + p2 + p3;
+                sq3 = p1 * p1 + p2 * p2 + p3 * p3;
+                s5 = s3 + p0 + p4;
+                sq5 = sq3 + p0 * p0 + p4 * p4;
             };
-            // (5x5: only even A / B rows exist; odd ones are never read)
-            if (!five || !(wj0 & 1)) row(wj0, s0a, c0a, s0b, c0b);
-            if (!five || (wj0 & 1)) row(wj0 + 1, s1a, c1a, s1b, c1b);
+            // the window of unit row jj0 - 1: tile rows jj0 .. jj0 + 3 now, jj0 + 4 in the loop
+#pragma unroll
+            for (int k = 0; k < 4; k++) hrow(jj0 + k, h5[k + 1], q5[k + 1], h3[k + 1], q3[k + 1]);
+            const unsigned s0 = a.prm.sgr.s0, s1 = a.prm.sgr.s1;
+            for (int jj = jj0; jj < jj1; jj++) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    h5[k] = h5[k + 1], q5[k] = q5[k + 1], h3[k] = h3[k + 1], q3[k] = q3[k + 1];
+                }
+                hrow(jj + 4, h5[4], q5[4], h3[4], q3[4]);
+                if (do3) {   // n = 9: rows jj + 1 .. jj + 3 of the window
+                    const int sum = h3[1] + h3[2] + h3[3], sumsq = q3[1] + q3[2] + q3[3];
+                    int A, B;
+                    lr_ab_sums<9>(sum, sumsq, s1, bd8, XBX, A, B);
+                    AA[jj][ii] = A;
+                    BB[jj][ii] = (uint8_t)B;
+                }
+                if (do5 && !(jj & 1)) {   // n = 25: rows jj .. jj + 4
+                    const int sum = h5[0] + h5[1] + h5[2] + h5[3] + h5[4];
+                    const int sumsq = q5[0] + q5[1] + q5[2] + q5[3] + q5[4];
+                    int A, B;
+                    lr_ab_sums<25>(sum, sumsq, s0, bd8, XBX, A, B);
+                    AA5[jj >> 1][ii] = A;
+                    BB5[jj >> 1][ii] = (uint8_t)B;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // the weighting (:397-439), both radii, a thread per column and run of
+    // rows sliding down it: each A / B row is read once per thread as a
+    // (sum over columns ii-1..ii+1, centre) pair, from which the 6/5 and 4/3
+    // neighbour weights follow:
+    //   EIGHT: 4 s1 + 3 (s0 + s2) + c0 + c2;  SIX (even j): 5 (s0 + s2) +
+    //   c0 + c2;  odd j: 5 s1 + c1  (rows 0/1/2 = unit rows j-1, j, j+1)
+    if (wj0 < h && wi < sw) {
+        const int ii = wi + 1;
+        int v[8];
+#pragma unroll
+        for (int m = 0; m < 8; m++) v[m] = 0;
+        auto row = [&](const int *ar, const uint8_t *br, int &sa, int &ca, int &sb, int &cb) {
+            const int a0 = ar[ii - 1], a1 = ar[ii], a2 = ar[ii + 1];
+            const int b0 = br[ii - 1], b1 = br[ii], b2 = br[ii + 1];
+            sa = a0 + a1 + a2;
+            ca = a1;
+            sb = b0 + b1 + b2;
+            cb = b1;
+        };
+        if (do5) {   // 5x5: A / B rows at unit rows -1, 1, 3, .. (jj even, stored at jj / 2)
+            const int w0 = a.prm.sgr.w0;
+            // unit row j reads jj = j (even j: rows j - 1 and j + 1 are jj = j, j + 2) or jj = j + 1 (odd j)
+            // held: A / B row jj = wj0 (wj0 even: its row j - 1) or wj0 + 1 (odd: its only row)
+            int sA = 0, cA = 0, sB = 0, cB = 0;
+            row(AA5[(wj0 + 1) >> 1], BB5[(wj0 + 1) >> 1], sA, cA, sB, cB);
 #pragma unroll
             for (int r = 0; r < 8; r++) {
                 const int j = wj0 + r;
                 if (r >= wrpt || j >= h) break;
-                int s2a = 0, c2a = 0, s2b = 0, c2b = 0;
-                if (!five || !(j & 1)) row(j + 2, s2a, c2a, s2b, c2b);
                 int aa, bb, sh;
-                if (five) {
-                    if (!(j & 1)) {
-                        aa = 5 * (s0b + s2b) + c0b + c2b;
-                        bb = 5 * (s0a + s2a) + c0a + c2a;
-                        sh = 9;
-                    } else {
-                        aa = 5 * s1b + c1b;
-                        bb = 5 * s1a + c1a;
-                        sh = 8;
-                    }
-                } else {
-                    aa = 4 * s1b + 3 * (s0b + s2b) + c0b + c2b;
-                    bb = 4 * s1a + 3 * (s0a + s2a) + c0a + c2a;
+                if (!(j & 1)) {   // rows jj = j (held) and j + 2
+                    int s2a, c2a, s2b, c2b;
+                    row(AA5[(j >> 1) + 1], BB5[(j >> 1) + 1], s2a, c2a, s2b, c2b);
+                    aa = 5 * (sB + s2b) + cB + c2b;
+                    bb = 5 * (sA + s2a) + cA + c2a;
                     sh = 9;
+                    sA = s2a, cA = c2a, sB = s2b, cB = c2b;   // row j + 2 == jj of j + 1
+                } else {          // row jj = j + 1 (held)
+                    aa = 5 * sB + cB;
+                    bb = 5 * sA + cA;
+                    sh = 8;
                 }
                 const int px = T[j + 3][wi + 3];
-                const int d = (int)(C)((bb - aa * px + (1 << (sh - 1))) >> sh);   // stored as coef
-                v[r] += wgt * d;
+                v[r] += w0 * (int)(C)((bb - aa * px + (1 << (sh - 1))) >> sh);   // stored as coef
+            }
+        }
+        if (do3) {   // 3x3: A / B on every row, jj = j .. j + 2
+            const int w1 = a.prm.sgr.w1;
+            int s0a, c0a, s0b, c0b, s1a, c1a, s1b, c1b;
+            row(AA[wj0], BB[wj0], s0a, c0a, s0b, c0b);
+            row(AA[wj0 + 1], BB[wj0 + 1], s1a, c1a, s1b, c1b);
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const int j = wj0 + r;
+                if (r >= wrpt || j >= h) break;
+                int s2a, c2a, s2b, c2b;
+                row(AA[j + 2], BB[j + 2], s2a, c2a, s2b, c2b);
+                const int aa = 4 * s1b + 3 * (s0b + s2b) + c0b + c2b;
+                const int bb = 4 * s1a + 3 * (s0a + s2a) + c0a + c2a;
+                const int px = T[j + 3][wi + 3];
+                v[r] += w1 * (int)(C)((bb - aa * px + (1 << 8)) >> 9);
                 s0a = s1a, c0a = c1a, s0b = s1b, c0b = c1b;
                 s1a = s2a, c1a = c2a, s1b = s2b, c1b = c2b;
             }
         }
-        __syncthreads();
-    }
-    if (wj0 < h && wi < sw) {
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const int j = wj0 + r;
@@ -303,6 +307,7 @@ template <int BPC> struct LrFrameArgs {
     P *out[3];
     const Dav1dGpuLrUnit *units[3];
     int is[3], ls[3], os[3], w[3], h[3], rows[3], cols[3], log2[3], restore[3], ss_ver[3];
+    int xb0, xb01;   // strip blocks of plane 0, of planes 0 + 1 (the grid has no empty chroma columns)
     int sb128, bdmax;
 };
 
@@ -340,8 +345,9 @@ __device__ __forceinline__ int lr_params(const Dav1dGpuLrUnit &u, bool hbd, Dav1
 template <int BPC>
 __global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     using P = typename Px<BPC>::pixel;
-    const int pl = blockIdx.z, w = f.w[pl], h = f.h[pl], sv = f.ss_ver[pl];
-    const int xs = blockIdx.x * kLrSW;
+    const int bx = blockIdx.x, pl = bx < f.xb0 ? 0 : bx < f.xb01 ? 1 : 2;
+    const int w = f.w[pl], h = f.h[pl], sv = f.ss_ver[pl];
+    const int xs = (bx - (pl == 0 ? 0 : pl == 1 ? f.xb0 : f.xb01)) * kLrSW;
     if (xs >= w) return;
     const int S64 = 64 >> sv, S8 = 8 >> sv, k = blockIdx.y;
     const int y0 = k ? k * S64 - S8 : 0, y1 = min((k + 1) * S64 - S8, h);
@@ -403,7 +409,7 @@ static int launch_lr_frame(const Dav1dGpuLrFrame *F, hipStream_t stream) {
     const int np = F->layout ? 3 : 1;
     LrFrameArgs<BPC> f;
     memset(&f, 0, sizeof(f));
-    int maxw = 0, maxh = 0;
+    int maxh = 0;
     for (int p = 0; p < np; p++) {
         if (!F->in[p].data || !F->out[p].data || F->in[p].data == F->out[p].data) return -1;
         f.restore[p] = (F->restore_planes >> p) & 1;
@@ -424,13 +430,16 @@ static int launch_lr_frame(const Dav1dGpuLrFrame *F, hipStream_t stream) {
         f.cols[p] = F->unit_cols[p];
         f.log2[p] = l2;
         f.ss_ver[p] = p && F->layout == 1;
-        maxw = max(maxw, f.w[p]);
         maxh = max(maxh, f.h[p]);
     }
     f.sb128 = F->sb128;
     f.bdmax = BPC == 8 ? 255 : F->bitdepth_max;
     const int stripes = (maxh + 8 + 63) / 64 + 1;
-    const dim3 grid((unsigned)((maxw + kLrSW - 1) / kLrSW), (unsigned)stripes, (unsigned)np);
+    int xb[3] = {0, 0, 0};
+    for (int p = 0; p < np; p++) xb[p] = (f.w[p] + kLrSW - 1) / kLrSW;
+    f.xb0 = xb[0];
+    f.xb01 = xb[0] + xb[1];
+    const dim3 grid((unsigned)(xb[0] + xb[1] + xb[2]), (unsigned)stripes, 1);
     k_lr_frame<BPC><<<grid, 256, 0, stream>>>(f);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

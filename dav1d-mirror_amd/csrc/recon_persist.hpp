@@ -51,12 +51,17 @@ __device__ __forceinline__ ItemSched<BPC> item_sched(const ReconArgs<BPC> *ka, i
     return s;
 }
 
-#if DGPU_PERSIST == 3
-static __device__ int g_persist_ctr[16];   // [0..7] per-XCD tickets, [8] finished waves
+#if DGPU_PERSIST >= 3
+// [0..7] per-XCD tickets (3), [8] finished waves, [16 + 16 * shard + xcd]
+// sharded tickets (4: 16 shards per XCD, each on its own 64-B line)
+static __device__ int g_persist_ctr[16 + 16 * 16 * 8];
+#endif
+#ifndef DGPU_PERSIST_WPE
+#define DGPU_PERSIST_WPE 5
 #endif
 template <int BPC, int GRP>
 __global__ __launch_bounds__((64 * waves_per_block<BPC, GRP>()))
-__attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon_p(ReconArgs<BPC> a) {
+__attribute__((amdgpu_waves_per_eu(DGPU_PERSIST_WPE))) void k_recon_p(ReconArgs<BPC> a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int WL = wave_lds<BPC, GRP>();
     constexpr int WPB = waves_per_block<BPC, GRP>();
@@ -93,7 +98,47 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon_
     const __attribute__((address_space(4))) ReconArgs<BPC> *ka40 =
         (const __attribute__((address_space(4))) ReconArgs<BPC> *)__builtin_amdgcn_kernarg_segment_ptr();
 #endif
-    if constexpr (DGPU_PERSIST == 3) {
+    if constexpr (DGPU_PERSIST == 4) {
+        // sharded tickets: the waves of launched block b take the items of
+        // XCD x that are congruent to shard (b >> 3) % 16 (a uniform sample
+        // of the XCD's schedule), one counter per (shard, XCD) on its own line
+        const int items = NBX * WPB, base = x * items;
+        const int sh = k0 & 15;
+        int *ctr = &g_persist_ctr[16 + (sh * 8 + x) * 16];
+        const int lane = unit_lane();
+        int t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __builtin_amdgcn_readfirstlane(t);
+#pragma unroll 1
+        while (sh + 16 * t < items && base + sh + 16 * t < nwaves) {
+            asm volatile("" ::: "memory");
+            int tn = 0;
+            if (lane == 0) tn = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if defined(__HIP_DEVICE_COMPILE__)
+            const __attribute__((address_space(4))) ReconArgs<BPC> *ka4 = ka40;
+            asm volatile("" : "+s"(ka4));
+            const ReconArgs<BPC> *ka = (const ReconArgs<BPC> *)ka4;
+#else
+            const ReconArgs<BPC> *ka = &a;
+#endif
+            const int gw = base + sh + 16 * t;
+            const ItemSched<BPC> s = item_sched<BPC, GRP>(ka, gw);
+            if (s.count > 0) {
+                const Dav1dGpuUnit u =
+                    bld(ka->units + s.first + min(lane >> (int)((kLog2Lanes >> (3 * s.cls)) & 7), s.count - 1));
+                dispatch<BPC, GRP>(*ka, pt, u, rec, s.cls, s.first, s.count, wl, gw);
+            }
+            t = __builtin_amdgcn_readfirstlane(tn);
+        }
+        if (lane == 0) {
+            const int total = (int)gridDim.x * WPB;
+            if (__hip_atomic_fetch_add(&g_persist_ctr[8], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+                for (int i = 0; i < 16 * 8; i++)
+                    __hip_atomic_store(&g_persist_ctr[16 + i * 16], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&g_persist_ctr[8], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    } else if constexpr (DGPU_PERSIST == 3) {
         // dynamic: the waves of an XCD take that XCD's wave items in schedule
         // order from a ticket counter (the next ticket is fetched before the
         // current item's class code runs); the last wave to finish resets the

@@ -206,13 +206,14 @@ extern "C" int dav1d_gpu_set_device(int device) {
     return 0;
 }
 
-extern "C" const char *dav1d_gpu_version(void) { return "dav1d-gpu gfx950 r4"; }
+extern "C" const char *dav1d_gpu_version(void) { return "dav1d-gpu gfx950 r5"; }
 
 extern "C" int dav1d_gpu_get_error(void) { return dgpu::g_error.load(); }
 
 extern "C" int dav1d_gpu_clear_error(void) { return dgpu::g_error.exchange(0); }
 
 extern "C" int dav1d_gpu_debug_register_buffer(const void *p, size_t bytes, int id) {
-    if (p && bytes) dgpu::bnd_extra().push_back(dgpu::BndRange{p, bytes, id});
+    if (!p) dgpu::bnd_extra().clear();
+    else if (bytes) dgpu::bnd_extra().push_back(dgpu::BndRange{p, bytes, id});
     return 0;
 }

@@ -36,7 +36,6 @@ static int launch_tiles(const Dav1dGpuTileBatch *b, hipStream_t stream) {
         }
         bnd_add(t, b->cfl_luma, BND_CFL);
         bnd_add_extra(t);
-        bnd_extra().clear();
         bnd_print<P>(t, "tiles");
         if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dgpu_bnd), &t, sizeof(t), 0, hipMemcpyHostToDevice, stream) != hipSuccess ||
             hipStreamSynchronize(stream) != hipSuccess)

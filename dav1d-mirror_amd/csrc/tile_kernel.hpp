@@ -110,8 +110,9 @@ template <int BPC> struct TileArgs {
 // round-4 faults), and with the NOCLAMP self-test use it raw, so the range
 // table sees where such a read would have landed.
 #if DGPU_BOUNDS
+static __device__ int g_dgpu_tile_index_hits;   // printed at most 256 times per process (its own count)
 __device__ __noinline__ int tile_index(int i, int n, int noclamp, int which, int line) {
-    if (i >= n && atomicAdd(&g_dgpu_bnd_hits, 1) < 256)
+    if (i >= n && atomicAdd(&g_dgpu_tile_index_hits, 1) < 256)
         printf("DGPU_TILE_INDEX %s line %d index %d of %d block %d lane %d\n", which ? "pred" : "tx", line, i, n,
                (int)blockIdx.x, (int)(threadIdx.x & 63));
     return noclamp ? i : min(i, n - 1);

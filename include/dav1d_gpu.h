@@ -212,11 +212,15 @@ const char *dav1d_gpu_source_hash(void);
 int dav1d_gpu_get_error(void);
 int dav1d_gpu_clear_error(void);
 /* Diagnostics (the DGPU_BOUNDS build, tools/build_variants.sh bounds): add
- * one device buffer the calling thread's next tile-batch launch may touch,
- * with its exact size in bytes; that launch then checks every record,
- * coefficient, edge and aux access against the registered buffers and its
- * planes, and clears the list.  Product builds never read the list: callers
- * register only when they run the diagnostics build.  Returns 0. */
+ * one device buffer the calling thread's next batch launches (unit and tile
+ * batches) may touch, with its size in bytes; those launches then check every
+ * record, coefficient, edge and aux access against the registered buffers
+ * and their planes (strict mode).  p = NULL clears the calling thread's list.
+ * Product builds never read the list: callers register only when they run
+ * the diagnostics build.  Returns 0.
+ * (Both batch tiers read coefficient, edge and record arrays as aligned
+ * 16-byte blocks: the 16-byte block holding an array's last byte must be
+ * readable, as every device allocation's granularity makes it.) */
 int dav1d_gpu_debug_register_buffer(const void *p, size_t bytes, int id);
 
 /* ---- batch tier ----------------------------------------------------------

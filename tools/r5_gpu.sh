@@ -58,6 +58,20 @@ for s in "${@:-tests}"; do
             python3 -c "import json; d=json.load(open('$O/ab_$v.json')); r=d['roofline']; print('ab $v', r['kernel_us'], r.get('stream_us_per_step'), d['ms_per_step'], d['config'].get('bit_exact_vs_oracle'))"
         done
         unset DAV1D_GPU_LIB_VARIANT ;;
+    abpmc) # FETCH_SIZE / WRITE_SIZE of the headline kernel per variant library (ABV)
+        for v in base $ABV; do
+            if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
+            for c in FETCH_SIZE WRITE_SIZE; do
+                (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/abpmc_${v}_$c" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 $BENCH_FAST) > "$O/abpmc_${v}_$c.log" 2>&1 || { echo "[r5] abpmc $v $c failed"; exit 1; }
+            done
+        done
+        unset DAV1D_GPU_LIB_VARIANT ;;
+    lr) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_lr.py "tests/test_gpu_checkasm.py::test_checkasm[lr]" tests/test_gpu_chain.py > "$O/lr.log" 2>&1 || { echo "[r5] lr failed"; tail -5 "$O/lr.log"; exit 1; }
+        tail -1 "$O/lr.log"
+        timeout -k 10 300 python -u bench.py --steps 50 --no-families --no-configs --no-tiles --no-intra --no-recorder \
+            --no-grain --no-cdef --no-superres --no-lpf --no-cpu --no-check > "$O/lrbench.json" 2> "$O/lrbench.log" \
+            || { echo "[r5] lr bench failed"; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/lrbench.json'))['loop_restoration']; print('lr', d['us_per_frame'], d['bit_exact_vs_oracle'])" ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "[r5] smoke failed"; exit 1; } ;;
     bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r5] bench failed"; exit 1; } ;;
     benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r5] benchfast failed"; exit 1; } ;;
