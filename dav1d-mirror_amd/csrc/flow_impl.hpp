@@ -37,6 +37,9 @@
 // written to addresses taken from the environment.  Product builds never read
 // those variables, so no environment can make the library store to an
 // arbitrary address
+#ifndef DGPU_FLOW_PRIO
+#define DGPU_FLOW_PRIO 0   // raise a wave's issue priority once its level wait is over
+#endif
 #ifndef DGPU_DIAG
 #define DGPU_DIAG (DGPU_TRACE || DGPU_FLOW_TRACE)
 #endif
@@ -177,6 +180,10 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
                 else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             }
         }
+        // the wave is on the dependency chain from here (its level's edges
+        // are ready): issue priority over the waves still running their
+        // pre-wait loads and transforms for later levels
+        if constexpr (DGPU_FLOW_PRIO) __builtin_amdgcn_s_setprio(3);
         if constexpr (DGPU_FLOW_TRACE) tr1 = __builtin_amdgcn_s_memrealtime();
     };
     // (DGPU_TRACE builds: the class code's phase marks per task, a.trace)
