@@ -113,6 +113,11 @@ struct CdefTaps {
     // rows r and r + 1 of column c: a tap of the pair is one 32-bit LDS read.
     // Every value and difference fits int16 with the kNone marker, the sums
     // too (|sum| <= 12 taps * 4 * 240).
+    // PRI / SEC: whether the primary / secondary taps run (a strength of 0
+    // makes every constrain() of its taps 0, and the min / max clamp applies
+    // only when both are set: :163-164), so a wave whose filtering lanes all
+    // have sec == 0 (or pri == 0) runs the 4-tap (8-tap) form, exactly
+    template <bool PRI = true, bool SEC = true>
     __device__ __forceinline__ void px2(const uint32_t *c, int &o0, int &o1) const {
         typedef short s2 __attribute__((ext_vector_type(2)));
         typedef unsigned short u2 __attribute__((ext_vector_type(2)));
@@ -133,23 +138,33 @@ struct CdefTaps {
         };
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            const s2 a = __builtin_bit_cast(s2, c[o[k][0]]), b = __builtin_bit_cast(s2, c[-o[k][0]]);
-            const s2 s0 = __builtin_bit_cast(s2, c[o[k][1]]), s1 = __builtin_bit_cast(s2, c[-o[k][1]]);
-            const s2 s2_ = __builtin_bit_cast(s2, c[o[k][2]]), s3 = __builtin_bit_cast(s2, c[-o[k][2]]);
-            const short wp = (short)(k ? tap1 : tap0), ws = (short)(2 - k);
-            sum += (s2){ wp, wp } * (cons(a, tp, shp) + cons(b, tp, shp));
-            sum += (s2){ ws, ws } * (cons(s0, ts, shs) + cons(s1, ts, shs) + cons(s2_, ts, shs) + cons(s3, ts, shs));
-            mn = __builtin_elementwise_min(mn, __builtin_elementwise_min(
-                     __builtin_elementwise_min(__builtin_bit_cast(u2, a), __builtin_bit_cast(u2, b)),
-                     __builtin_elementwise_min(__builtin_elementwise_min(__builtin_bit_cast(u2, s0), __builtin_bit_cast(u2, s1)),
-                                               __builtin_elementwise_min(__builtin_bit_cast(u2, s2_), __builtin_bit_cast(u2, s3)))));
-            mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(
-                     __builtin_elementwise_max(a, b),
-                     __builtin_elementwise_max(__builtin_elementwise_max(s0, s1), __builtin_elementwise_max(s2_, s3))));
+            if constexpr (PRI) {
+                const s2 a = __builtin_bit_cast(s2, c[o[k][0]]), b = __builtin_bit_cast(s2, c[-o[k][0]]);
+                const short wp = (short)(k ? tap1 : tap0);
+                sum += (s2){ wp, wp } * (cons(a, tp, shp) + cons(b, tp, shp));
+                if constexpr (SEC) {
+                    mn = __builtin_elementwise_min(mn, __builtin_elementwise_min(__builtin_bit_cast(u2, a),
+                                                                                 __builtin_bit_cast(u2, b)));
+                    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(a, b));
+                }
+            }
+            if constexpr (SEC) {
+                const s2 s0 = __builtin_bit_cast(s2, c[o[k][1]]), s1 = __builtin_bit_cast(s2, c[-o[k][1]]);
+                const s2 s2_ = __builtin_bit_cast(s2, c[o[k][2]]), s3 = __builtin_bit_cast(s2, c[-o[k][2]]);
+                const short ws = (short)(2 - k);
+                sum += (s2){ ws, ws } * (cons(s0, ts, shs) + cons(s1, ts, shs) + cons(s2_, ts, shs) + cons(s3, ts, shs));
+                if constexpr (PRI) {
+                    mn = __builtin_elementwise_min(mn, __builtin_elementwise_min(
+                             __builtin_elementwise_min(__builtin_bit_cast(u2, s0), __builtin_bit_cast(u2, s1)),
+                             __builtin_elementwise_min(__builtin_bit_cast(u2, s2_), __builtin_bit_cast(u2, s3))));
+                    mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(__builtin_elementwise_max(s0, s1),
+                                                                                 __builtin_elementwise_max(s2_, s3)));
+                }
+            }
         }
         const s2 neg = (s2)(sum < zero) & (s2){ 1, 1 };
         s2 v = p + ((sum - neg + (s2){ 8, 8 }) >> (s2){ 4, 4 });
-        if (pri && sec) v = __builtin_elementwise_min(__builtin_elementwise_max(v, __builtin_bit_cast(s2, mn)), mx);
+        if (PRI && SEC && pri && sec) v = __builtin_elementwise_min(__builtin_elementwise_max(v, __builtin_bit_cast(s2, mn)), mx);
         o0 = v.x;
         o1 = v.y;
     }
@@ -339,23 +354,32 @@ struct Stage {
 };
 
 // Filter (FILT) or copy one column of BH pixels of a block from its pair tile.
-template <int BPC, int BH, bool FILT>
+template <int BPC, int BH, bool FILT, bool PRI = true, bool SEC = true>
 __device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const uint32_t *c, int S,
                                         const CdefTaps &tp) {
     using P = typename Px<BPC>::pixel;
 #pragma unroll
     for (int y = 0; y < BH; y += 2) {
         int v0 = (int)(c[y * S] & 0xffff), v1 = (int)(c[y * S] >> 16);
-        if (FILT) tp.px2(c + y * S, v0, v1);
+        if (FILT) tp.px2<PRI, SEC>(c + y * S, v0, v1);
         dst[y * ds] = (P)v0;
         dst[(y + 1) * ds] = (P)v1;
     }
 }
+#ifndef DGPU_CDEF_SPLIT
+#define DGPU_CDEF_SPLIT 1   // the primary-only / secondary-only forms for waves that need only one
+#endif
 template <int BPC, int BH>
 __device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const uint32_t *c, int S,
                                         const CdefTaps &tp, bool filt) {
-    if (filt) col_out<BPC, BH, true>(dst, ds, c, S, tp);
-    else col_out<BPC, BH, false>(dst, ds, c, S, tp);
+    if (filt) {
+        // (the votes run over the filtering lanes: the copying ones are masked off here)
+        if (DGPU_CDEF_SPLIT && __all(tp.sec == 0)) col_out<BPC, BH, true, true, false>(dst, ds, c, S, tp);
+        else if (DGPU_CDEF_SPLIT && __all(tp.pri == 0)) col_out<BPC, BH, true, false, true>(dst, ds, c, S, tp);
+        else col_out<BPC, BH, true>(dst, ds, c, S, tp);
+    } else {
+        col_out<BPC, BH, false>(dst, ds, c, S, tp);
+    }
 }
 
 // DGPU_CDEF_ABL (cost-model probes, wrong output): 1 skips the direction

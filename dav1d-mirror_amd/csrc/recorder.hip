@@ -33,6 +33,7 @@
 #include <condition_variable>
 #include <functional>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <numeric>
 #include <thread>
@@ -1206,6 +1207,32 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         r->pool->run(nlv, [&](int t) {
             for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) stamp(ci, false);
         });
+        // the contract (include/dav1d_gpu.h, dav1d_gpu_recorder_flush): the
+        // cells of one flush do not overlap, an inter-intra prediction under
+        // its own residual cells excepted.  Checked after the parallel stamp:
+        // two overlapping cells leave one stamp on a shared 4x4, so the other
+        // finds a stamp not its own whatever order the workers ran in; the
+        // flush then fails instead of scheduling reads before writes
+        // 
+        std::atomic<int> overlap{0};
+        r->pool->run(nlv, [&](int t) {
+            int bad = 0;
+            for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e && !bad; ci++) {
+                const LvJob &j = r->jobs[ci];
+                if (j.fl & LvJob::IIC) continue;
+                const int32_t *wp = r->own[j.p].data();
+                const int w4p = mw[j.p];
+                const int32_t v = cell_base + (int32_t)ci;
+                for (int cy = j.y4; cy < j.y4 + j.ch4 && !bad; cy++)
+                    for (int cx = j.x4; cx < j.x4 + j.cw4; cx++)
+                        if (wp[(size_t)cy * w4p + cx] != v) {
+                            bad = 1;
+                            break;
+                        }
+            }
+            if (bad) overlap.store(1, std::memory_order_relaxed);
+        });
+        if (overlap.load()) return -1;
         r->pool->run(nlv, [&](int t) {
             for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) stamp(ci, true);
         });

@@ -238,3 +238,53 @@ def test_recorder_emu_scratch_limit(pkg):
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
     lines = dict(line.split() for line in r.stdout.splitlines() if line.split()[0] in ("luma", "all"))
     assert lines == {"luma": "0", "all": "-1"}, r.stdout
+
+
+_OVERLAP_CHILD = r"""
+import ctypes, os, sys
+sys.path.insert(0, sys.argv[1])
+import __graft_entry__ as ge
+ge.load_package()
+import dav1d_mirror_amd.abi as abi
+L = abi.load_lib()
+W, H = 256, 128
+d = (abi.Plane * 3)()
+r = ((abi.Plane * 3) * abi.MAX_REFS)()
+for p in range(3):
+    w, h = (W, H) if p == 0 else (W // 2, H // 2)
+    d[p].data, d[p].stride, d[p].w, d[p].h = 0x1000, w, w, h
+    r[0][p].data, r[0][p].stride, r[0][p].w, r[0][p].h = 0x1000, w, w, h
+
+
+def blk(x, y, s):
+    b = abi.RecBlock()
+    b.plane, b.x, b.y, b.w, b.h, b.tx, b.kind = 0, x, y, s, s, abi.TX_INDEX[(8, 8)], abi.PRED_INTER
+    b.tile_x0, b.tile_y0, b.tile_x1, b.tile_y1 = 0, 0, W, H
+    b.ref[0], b.ref[1] = 0, 0
+    return b
+
+
+rec = L.dav1d_gpu_recorder_new(8, 255, W, H, 0)
+for case, blocks in (("disjoint", [(0, 0, 16), (16, 0, 16), (0, 16, 16)]),
+                     ("overlap", [(0, 0, 16), (8, 8, 16)]),
+                     ("same", [(32, 32, 8), (32, 32, 8)])):
+    for x, y, s in blocks:
+        assert L.dav1d_gpu_rec_block(rec, ctypes.byref(blk(x, y, s))) == 0
+    print(case, L.dav1d_gpu_recorder_flush(rec, ctypes.byref(d), ctypes.byref(r), None), flush=True)
+L.dav1d_gpu_recorder_free(rec)
+print("ok")
+"""
+
+
+def test_recorder_rejects_overlapping_blocks(pkg):
+    """Blocks of one flush must not overlap (each pixel predicted by one
+    block, an inter-intra prediction under its own residuals excepted): a
+    flush with overlapping cells fails with -1 whatever order the worker pool
+    stamped them in, instead of scheduling a read before its write (ADVICE
+    r4).  Host-only flushes, no device."""
+    env = dict(os.environ, DAV1D_GPU_REC_HOSTONLY="1")
+    env.pop("DAV1D_GPU_REC_DUMP", None)
+    r = subprocess.run(["python3", "-c", _OVERLAP_CHILD, ROOT], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+    got = dict(line.split() for line in r.stdout.splitlines() if len(line.split()) == 2)
+    assert got == {"disjoint": "0", "overlap": "-1", "same": "-1"}, r.stdout

@@ -38,7 +38,6 @@ for s in "${@:-tests}"; do
             rc=$?; echo "[r5] tbounds noclamp rc=$rc range=$(grep -c 'DGPU_BOUNDS line' "$O/tbounds_noclamp.log") index=$(grep -c 'DGPU_TILE_INDEX' "$O/tbounds_noclamp.log")"
             [ $rc -le 1 ] || exit 1 ;;
     intra) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_intra_frame.py > "$O/intra.log" 2>&1 || { echo "[r5] intra failed"; exit 1; } ;;
-    cdef) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_cdef.py > "$O/cdef.log" 2>&1 || { echo "[r5] cdef failed"; exit 1; } ;;
     benchpart) # the intra wavefront, CDEF, LR and recorder legs only (recorder host laps on stderr)
             DAV1D_GPU_REC_TIMING=1 timeout -k 10 600 python -u bench.py --steps 50 --no-families --no-configs --no-tiles \
                 --no-grain --no-superres --no-lpf --no-cpu --no-check > "$O/benchpart.json" 2> "$O/benchpart.log" \
@@ -72,6 +71,21 @@ for s in "${@:-tests}"; do
             --no-grain --no-cdef --no-superres --no-lpf --no-cpu --no-check > "$O/lrbench.json" 2> "$O/lrbench.log" \
             || { echo "[r5] lr bench failed"; exit 1; }
         python3 -c "import json; d=json.load(open('$O/lrbench.json'))['loop_restoration']; print('lr', d['us_per_frame'], d['bit_exact_vs_oracle'])" ;;
+    abintra) # the intra wavefront bench leg per variant library (ABV): 1-tile / 2x2 ms per 4K frame, bit-exact
+        for v in base $ABV; do
+            if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
+            timeout -k 10 400 python -u bench.py --steps 20 --no-families --no-configs --no-tiles --no-recorder --no-grain \
+                --no-cdef --no-superres --no-lpf --no-lr --no-cpu --no-check > "$O/abintra_$v.json" 2> "$O/abintra_$v.log" \
+                || { echo "[r5] abintra $v failed"; tail -5 "$O/abintra_$v.log"; exit 1; }
+            python3 -c "import json; d=json.load(open('$O/abintra_$v.json'))['intra_wavefront']; print('abintra $v', d['1_tile']['ms_per_frame'], d['1_tile']['bit_exact_vs_oracle'], d['2x2_tiles']['ms_per_frame'], d['2x2_tiles']['bit_exact_vs_oracle'])"
+        done
+        unset DAV1D_GPU_LIB_VARIANT ;;
+    cdef) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_cdef.py "tests/test_gpu_checkasm.py::test_checkasm[cdef]" > "$O/cdef.log" 2>&1 || { echo "[r5] cdef failed"; tail -5 "$O/cdef.log"; exit 1; }
+        tail -1 "$O/cdef.log"
+        timeout -k 10 300 python -u bench.py --steps 50 --no-families --no-configs --no-tiles --no-intra --no-recorder \
+            --no-grain --no-lr --no-superres --no-lpf --no-cpu --no-check > "$O/cdefbench.json" 2> "$O/cdefbench.log" \
+            || { echo "[r5] cdef bench failed"; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/cdefbench.json'))['cdef']; print('cdef', d['us_per_frame'], d['bit_exact_vs_oracle'])" ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "[r5] smoke failed"; exit 1; } ;;
     bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r5] bench failed"; exit 1; } ;;
     benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r5] benchfast failed"; exit 1; } ;;
