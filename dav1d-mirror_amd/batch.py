@@ -19,7 +19,7 @@ def _ptr(t):
 class DeviceFrame:
     """A FrameData uploaded to one GPU, plus its output planes."""
 
-    def __init__(self, fd, device="cuda:0", zero_coefs=False, dst_planes=None):
+    def __init__(self, fd, device="cuda:0", zero_coefs=False, dst_planes=None, exact_refs=None):
         """dst_planes: optional device tensors to reconstruct into, (rows >=
         h, stride in pixels >= w) each -- e.g. a frame chain's 128-aligned
         pictures -- instead of exact-size planes of its own."""
@@ -35,7 +35,10 @@ class DeviceFrame:
         ed = fd.edges if fd.cfg.bpc == 8 else fd.edges.view(np.int16)
         self.edges = torch.from_numpy(ed.copy()).to(dev)
         self.refs = []
-        for rp in fd.refs:
+        # exact_refs (workload.clamp_units): unpadded [ref][plane] arrays read
+        # at their own origin and stride, DGPU_MX_CLAMP units clamping to them
+        self.exact = exact_refs is not None
+        for rp in (exact_refs if self.exact else fd.refs):
             planes = []
             for a in rp:
                 src = a if fd.cfg.bpc == 8 else a.view(np.int16)
@@ -70,7 +73,7 @@ class DeviceFrame:
             for r in range(len(self.refs)):
                 t = self.refs[r][p]
                 stride = t.shape[1]
-                b.ref[r][p].data = t.data_ptr() + fd.ref_origin_offset(p) * bpp
+                b.ref[r][p].data = t.data_ptr() + (0 if self.exact else fd.ref_origin_offset(p)) * bpp
                 b.ref[r][p].stride = stride * bpp
                 b.ref[r][p].w, b.ref[r][p].h = w, h
         b.units = self.units.data_ptr()

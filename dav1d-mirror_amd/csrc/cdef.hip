@@ -113,10 +113,11 @@ struct CdefTaps {
     // rows r and r + 1 of column c: a tap of the pair is one 32-bit LDS read.
     // Every value and difference fits int16 with the kNone marker, the sums
     // too (|sum| <= 12 taps * 4 * 240).
-    // PRI / SEC: whether the primary / secondary taps run (a strength of 0
-    // makes every constrain() of its taps 0, and the min / max clamp applies
-    // only when both are set: :163-164), so a wave whose filtering lanes all
-    // have sec == 0 (or pri == 0) runs the 4-tap (8-tap) form, exactly
+    // PRI / SEC: whether the primary / secondary taps run -- the reference's
+    // three paths (:119-214: both, primary only, secondary only; a strength
+    // of 0 makes every constrain() of its taps 0 and the min / max clamp
+    // belongs to the first only), so a wave whose filtering lanes all have
+    // sec == 0 (or pri == 0) runs the 4-tap (8-tap) form, exactly
     template <bool PRI = true, bool SEC = true>
     __device__ __forceinline__ void px2(const uint32_t *c, int &o0, int &o1) const {
         typedef short s2 __attribute__((ext_vector_type(2)));

@@ -301,11 +301,17 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs<BPC> a) {
 
 // Super-res frame tier (dav1d_filter_sbrow_resize for the whole frame): one
 // launch, blockIdx.z = plane.  A wave upscales 256 consecutive output pixels
-// of one row: the source span they read (at most 256 * dx / 2^14 + 8 pixels,
-// dx <= 2^14 since super-res only upscales) is loaded once into LDS with the
-// reference's column clamp applied at load time, then each lane filters
-// four outputs (x0 + lane + 64 k) from LDS with the 8 taps of resize_c.
+// of kRzRows rows: the source spans they read (at most 256 * dx / 2^14 + 8
+// pixels per row, dx <= 2^14 since super-res only upscales) are loaded once
+// into LDS with the reference's column clamp applied at load time -- every
+// row's loads in flight together (round 5: two rows per wave, 26.8 -> see
+// DESIGN.md 7) -- then each lane filters four outputs (x0 + lane + 64 k) per
+// row from LDS with the 8 taps of resize_c.
 constexpr int kRzOut = 256, kRzSpan = kRzOut + 16;
+#ifndef DGPU_RZ_ROWS
+#define DGPU_RZ_ROWS 2
+#endif
+constexpr int kRzRows = DGPU_RZ_ROWS;   // rows per wave
 template <int BPC> struct ResizeFrameArgs {
     typename Px<BPC>::pixel *dst[3];
     const typename Px<BPC>::pixel *src[3];
@@ -316,33 +322,49 @@ template <int BPC> struct ResizeFrameArgs {
 template <int BPC>
 __global__ __launch_bounds__(256) void k_resize_frame(ResizeFrameArgs<BPC> a) {
     using P = typename Px<BPC>::pixel;
-    __shared__ P span[4][kRzSpan];
+    __shared__ P span[4][kRzRows][kRzSpan];
     const int p = blockIdx.z, w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int y = blockIdx.y * 4 + w, x0 = blockIdx.x * kRzOut;
-    const int dw = a.dst_w[p], sw = a.src_w[p], dx = a.dx[p], mx0 = a.mx0[p];
-    if (y >= a.h[p] || x0 >= dw) return;   // wave-uniform
-    const P *s = a.src[p] + (size_t)y * a.ss[p];
+    const int y0 = (blockIdx.y * 4 + w) * kRzRows, x0 = blockIdx.x * kRzOut;
+    const int dw = a.dst_w[p], sw = a.src_w[p], dx = a.dx[p], mx0 = a.mx0[p], hh = a.h[p];
+    if (y0 >= hh || x0 >= dw) return;   // wave-uniform
     const int s0 = ((mx0 + x0 * dx) >> 14) - 4;   // first source column a tap of this run reads
-    P *t = span[w];
+    constexpr int NK = kRzSpan / 64 + 1;
+    P v[kRzRows][NK];
 #pragma unroll
-    for (int k = 0; k < kRzSpan / 64 + 1; k++) {
-        const int i = l + 64 * k;
-        if (i < kRzSpan) t[i] = s[clampi(s0 + i, 0, sw - 1)];
+    for (int r = 0; r < kRzRows; r++) {   // every row's loads first
+        const P *s = a.src[p] + (size_t)min(y0 + r, hh - 1) * a.ss[p];
+#pragma unroll
+        for (int k = 0; k < NK; k++) {
+            const int i = l + 64 * k;
+            if (i < kRzSpan) v[r][k] = s[clampi(s0 + i, 0, sw - 1)];
+        }
     }
+#pragma unroll
+    for (int r = 0; r < kRzRows; r++)
+#pragma unroll
+        for (int k = 0; k < NK; k++) {
+            const int i = l + 64 * k;
+            if (i < kRzSpan) span[w][r][i] = v[r][k];
+        }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    P *d = a.dst[p] + (size_t)y * a.ds[p];
 #pragma unroll
-    for (int k = 0; k < kRzOut / 64; k++) {
-        const int x = x0 + l + 64 * k;
-        if (x < dw) {
-            const int pos = mx0 + x * dx;
-            const P *c = t + ((pos >> 14) - 4 - s0);   // taps c[0..7] = source (pos >> 14) - 4 .. + 3
-            const signed char *f = &dspt_resize[((pos & 0x3fff) >> 8) * 8];
-            int sum = 0;
+    for (int r = 0; r < kRzRows; r++) {
+        if (y0 + r >= hh) break;
+        const P *t = span[w][r];
+        P *d = a.dst[p] + (size_t)(y0 + r) * a.ds[p];
 #pragma unroll
-            for (int i = 0; i < 8; i++) sum += f[i] * (int)c[i];
-            d[x] = (P)clampi((-sum + 64) >> 7, 0, a.bdmax);
+        for (int k = 0; k < kRzOut / 64; k++) {
+            const int x = x0 + l + 64 * k;
+            if (x < dw) {
+                const int pos = mx0 + x * dx;
+                const P *c = t + ((pos >> 14) - 4 - s0);   // taps c[0..7] = source (pos >> 14) - 4 .. + 3
+                const signed char *f = &dspt_resize[((pos & 0x3fff) >> 8) * 8];
+                int sum = 0;
+#pragma unroll
+                for (int i = 0; i < 8; i++) sum += f[i] * (int)c[i];
+                d[x] = (P)clampi((-sum + 64) >> 7, 0, a.bdmax);
+            }
         }
     }
 }
@@ -371,7 +393,7 @@ static int launch_resize_frame(const Dav1dGpuResizeFrame *f, hipStream_t stream)
         a.mx0[p] = f->start[p ? 1 : 0];
         if (f->step[p ? 1 : 0] <= 0 || f->step[p ? 1 : 0] > 1 << 14) return -1;   // super-res upscales
         gw = max(gw, (o.w + kRzOut - 1) / kRzOut);
-        gh = max(gh, (i.h + 3) / 4);
+        gh = max(gh, (i.h + 4 * kRzRows - 1) / (4 * kRzRows));
     }
     a.bdmax = BPC == 8 ? 255 : f->bitdepth_max;
     k_resize_frame<BPC><<<dim3(gw, gh, np), 256, 0, stream>>>(a);

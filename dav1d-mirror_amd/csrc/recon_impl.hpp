@@ -320,6 +320,8 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
         for (int r = 0; r < DGPU_MAX_REFS; r++) {
             a.ref[r][p] = (const P *)b->ref[r][p].data;
             a.ref_stride[r][p] = (int)(b->ref[r][p].stride / B);
+            a.ref_w[r][p] = b->ref[r][p].w;
+            a.ref_h[r][p] = b->ref[r][p].h;
         }
     }
     a.units = b->units;

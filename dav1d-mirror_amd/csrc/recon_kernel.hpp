@@ -34,6 +34,8 @@
 #include "dsp_common.hpp"
 #include "intra_edge_dev.hpp"
 
+#include <stddef.h>
+
 #include <utility>
 
 // Profiling-only phase ablations (tools/build_variants.sh); all 0 in the
@@ -127,6 +129,9 @@ template <int BPC> struct ReconArgs {
     int top_stride[3];   // pixels
     int top_rows[3];
     int sb_log2[3];
+    // the reference planes' visible sizes: DGPU_MX_CLAMP units (second
+    // launch) clamp every footprint pixel to them (emu_edge)
+    int ref_w[DGPU_MAX_REFS][3], ref_h[DGPU_MAX_REFS][3];
 };
 
 // Plane pointers and strides, copied once per workgroup into LDS so the
@@ -862,7 +867,7 @@ __device__ __forceinline__ int mc_bank(int type, bool bil, int len) {
 // and its row pairs advance by G / QW.  Split in steps so the loads of the
 // first chunk (all of them below the 64-point classes) are issued together
 // with the unit's other loads: init + load(0) ... compute(0) + rest().
-template <int BPC, int TX> struct HPass {
+template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
     using CL = Cls<TX>;
     static constexpr int W = CL::W, H = CL::H, G = CL::G, QW = CL::QW, NH = CL::NH, RP = CL::RP;
     static constexpr int IT = (NH + G - 1) / G;
@@ -891,6 +896,64 @@ template <int BPC, int TX> struct HPass {
     uint4 th;            // taps: 8bpc .x/.y int8 x4, 16bpc int16 pairs
 
     int rlo, rhi;        // footprint rows the vertical taps read (others are not loaded)
+    // CLAMPABLE (the second launch): a DGPU_MX_CLAMP reference, every
+    // footprint pixel read at its position clamped to the plane, as
+    // emu_edge_c provides them (src/mc_tmpl.c:827-875, src/recon_tmpl.c:
+    // 986-999): each of a lane's 12 columns is read at its clamped column,
+    // each row at its clamped row (such units are rare: only footprints
+    // that leave the picture are flagged).
+    bool cl = false;
+    int cy0, cxs, cw, chh;   // first footprint row (y - 3), this lane's first column, plane size
+    const uint8_t *cbase;    // the plane's (0, 0)
+    __device__ __forceinline__ void init_clamp(const typename Px<BPC>::pixel *plane, int stride_px, int w, int h,
+                                               int x, int y, uint32_t *mid, int bank, int m, int l) {
+        init(plane, stride_px, mid, bank, m, l, 0, H + 7);
+        cl = true;
+        const int q = l % QW;
+        cbase = reinterpret_cast<const uint8_t *>(plane);
+        cy0 = y - 3;
+        cxs = x - 3 + 4 * q;
+        cw = w;
+        chh = h;
+        sh = 0;   // the rows are gathered already aligned
+    }
+    __device__ __forceinline__ void load_clamp(int k0) {
+#pragma unroll
+        for (int c = 0; c < CH; c++) {
+            const int p = cmin(p0 + (k0 + c) * PS, RP - 1);
+#pragma unroll
+            for (int rr = 0; rr < 2; rr++) {
+                const int yy = clampi(cy0 + cmin(2 * p + rr, H + 6), 0, chh - 1);
+                const uint8_t *row = cbase + (size_t)yy * sb;
+                uint32_t w[6];
+#pragma unroll
+                for (int i = 0; i < (BPC == 8 ? 3 : 6); i++) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int j = 0; j < 4 / B; j++) {
+                        const int x = clampi(cxs + (4 / B) * i + j, 0, cw - 1);
+                        const uint32_t px = BPC == 8 ? (uint32_t)gld<uint8_t>(row + x)
+                                                     : (uint32_t)gld<uint16_t>(row + 2 * x);
+                        v |= px << (8 * B * j);
+                    }
+                    w[i] = v;
+                }
+                if constexpr (BPC == 8) {
+                    ra[c][rr][0] = w[0];
+                    ra[c][rr][1] = w[1];
+                    ra[c][rr][2] = w[2];
+                    ra[c][rr][3] = 0;
+                } else {
+                    ra[c][rr][0] = w[0];
+                    ra[c][rr][1] = w[1];
+                    ra[c][rr][2] = w[2];
+                    ra[c][rr][3] = w[3];
+                    rb[c][rr][0] = w[4];
+                    rb[c][rr][1] = w[5];
+                }
+            }
+        }
+    }
     __device__ __forceinline__ void init(const typename Px<BPC>::pixel *org, int stride_px, uint32_t *mid, int bank,
                                          int m, int l, int rlo_, int rhi_) {
         rlo = rlo_;
@@ -913,6 +976,12 @@ template <int BPC, int TX> struct HPass {
         }
     }
     __device__ __forceinline__ void load(int k0) {
+        if constexpr (CLAMPABLE) {
+            if (cl) {
+                load_clamp(k0);
+                return;
+            }
+        }
 #pragma unroll
         for (int c = 0; c < CH; c++) {   // clamped: the loads stay inside the footprint
             const int pu = p0 + (k0 + c) * PS;
@@ -1412,26 +1481,50 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                             : make_uint4(0, 0, 0, 0);
     const uint4 tv1 = comp ? reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[1]]
                            : make_uint4(0, 0, 0, 0);
-    auto hinit = [&](HPass<BPC, TX> &hp, int k) {
+    using HP = HPass<BPC, TX, WARPK>;   // the second launch also runs DGPU_MX_CLAMP units
+    auto hinit = [&](HP &hp, int k) {
         const int r = k ? u.p.inter.ref[1] : u.p.inter.ref[0];
         const int rs = pt.ref_stride[r * 3 + plane];
+        if constexpr (WARPK) {
+            const int mx = k ? u.p.inter.mx[1] : u.p.inter.mx[0];
+            if (mx & DGPU_MX_CLAMP) {   // src_off = x | y << 16 (int16 each), the unit's top-left in the plane
+                const int so = k ? u.p.inter.src_off[1] : u.p.inter.src_off[0];
+                // the plane size by a lane-varying index straight from the
+                // kernel-argument segment (indexing the by-value argument
+                // would copy all of it to scratch); WARPK code runs only in
+                // k_recon, whose argument `a` is
+                int rw = 0, rh = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+                {
+                    const __attribute__((address_space(4))) int *ka =
+                        (const __attribute__((address_space(4))) int *)__builtin_amdgcn_kernarg_segment_ptr();
+                    rw = ka[(offsetof(ReconArgs<BPC>, ref_w) >> 2) + r * 3 + plane];
+                    rh = ka[(offsetof(ReconArgs<BPC>, ref_h) >> 2) + r * 3 + plane];
+                }
+#endif
+                hp.init_clamp(pt.ref[r * 3 + plane], rs, rw, rh, (int)(int16_t)(so & 0xffff), so >> 16,
+                              k ? mid1 : mid0, bank_h, mx & 15, l);
+                return;
+            }
+        }
         const P *org = pt.ref[r * 3 + plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
         // footprint rows the vertical taps read: m == 0 is the identity (tap
         // 3), bilinear taps 3..4, the 4-tap banks 2..5, 8-tap 0..7
         const int my = k ? u.p.inter.my[1] : u.p.inter.my[0];
         const int tf = my == 0 ? 3 : bil ? 3 : bank_v >= 3 ? 2 : 0;
         const int tl = my == 0 ? 3 : bil ? 4 : bank_v >= 3 ? 5 : 7;
-        hp.init(org, rs, k ? mid1 : mid0, bank_h, k ? u.p.inter.mx[1] : u.p.inter.mx[0], l, tf, H - 1 + tl);
+        hp.init(org, rs, k ? mid1 : mid0, bank_h, (k ? u.p.inter.mx[1] : u.p.inter.mx[0]) & (WARPK ? 15 : 255), l, tf,
+                H - 1 + tl);
     };
     auto hpass = [&](int k) {   // the whole h-pass of ref k
-        HPass<BPC, TX> hp;
+        HP hp;
         hinit(hp, k);
         hp.load(0);
         hp.compute(0, ib);
         hp.rest(ib);
     };
-    const bool do_mc = (NW ? inter : ii) && !DGPU_ABL_MC;
-    HPass<BPC, TX> hp0;
+    const bool do_mc = inter && !DGPU_ABL_MC;   // (WARPK: inter-intra and DGPU_MX_CLAMP inter units)
+    HP hp0;
     if (do_mc) {
         hinit(hp0, 0);
         hp0.load(0);
@@ -1439,7 +1532,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     // DGPU_EARLY_REF1: the second ref's first load chunk goes out with the
     // first's (held in registers until its h-pass after the first ref's
     // vertical pass); otherwise it is issued when needed
-    HPass<BPC, TX> hp1;
+    HP hp1;
     if (DGPU_EARLY_REF1 && CL::SEQREF && do_mc && comp) {
         hinit(hp1, 1);
         hp1.load(0);
@@ -1663,7 +1756,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         }
     };
 
-    if (NW && inter && !ii) {
+    if (inter && !ii) {   // (WARPK: DGPU_MX_CLAMP units)
         if (DGPU_ABL_MC) {
             int pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll

@@ -18,6 +18,7 @@ config 2: inter only, prediction-only units (one per block, no residual).
 
 Everything here is host-side numpy; nothing is timed.
 """
+import dataclasses
 import os
 from dataclasses import dataclass, field
 
@@ -759,3 +760,55 @@ def algorithmic_bytes(fd: FrameData):
         "n_inter_intra": int(ii.sum()),
         "n_nopred": int(nopred.sum()),
     }
+
+
+def clamp_units(fd: FrameData):
+    """The frame for exact-size (unpadded) reference planes, as a decoder
+    with dav1d's own pictures would hand it to the unit batch: every inter
+    unit's footprint is tested against its reference plane the way
+    recon_tmpl.c's mc() decides emu_edge (src/recon_tmpl.c:986-999), here with
+    the unit batch's load margins (the rectangle -3 / +4 pixels, plus the 3
+    bytes before and 5 after each row its aligned loads touch).  A unit
+    whose footprint stays inside reads the plane with its src_off
+    re-expressed in the exact plane's stride; a unit whose footprint leaves
+    it gets DGPU_MX_CLAMP on that reference with src_off = x | y << 16 and
+    moves to the end of its class range (the class_warp sub-range of the
+    second launch, which clamps every footprint pixel).  Returns (frame,
+    exact reference planes [ref][plane]).  Frames with the launch-ahead kinds
+    (WARP, INTER_INTRA, INTER_WMASK, INTER_OBMC, INTER_SCALED) still need
+    padded references and are refused."""
+    u = fd.units.copy()
+    if np.isin(u["pred"], abi.SECOND_LAUNCH_KINDS).any():
+        raise ValueError("launch-ahead kinds read unclamped footprints: padded references only")
+    pad = fd.cfg.ref_pad
+    exact = [[np.ascontiguousarray(a[pad:pad + h, pad:pad + w]) for a, (w, h) in zip(rp, fd.plane_wh)]
+             for rp in fd.refs]
+    for (w, h) in fd.plane_wh:
+        assert (w * np.dtype(fd.cfg.pixel_dtype).itemsize) % 4 == 0, "reference rows are read as aligned dwords"
+    tw = np.array([abi.TX_WH[t][0] for t in u["tx"]])
+    th = np.array([abi.TX_WH[t][1] for t in u["tx"]])
+    pw = np.array([wh[0] for wh in fd.plane_wh])[u["plane"]]
+    ph = np.array([wh[1] for wh in fd.plane_wh])[u["plane"]]
+    comp = np.isin(u["pred"], (abi.PRED_INTER_AVG, abi.PRED_INTER_WAVG, abi.PRED_INTER_MASK))
+    inter = np.isin(u["pred"], abi.INTER_KINDS)
+    clamp_any = np.zeros(len(u), bool)
+    for k in range(2):
+        used = inter & (comp if k else True)
+        x = fd.src_xy[:, k, 0].astype(np.int64)
+        y = fd.src_xy[:, k, 1].astype(np.int64)
+        inside = (x - 6 >= 0) & (x + tw + 12 <= pw) & (y - 3 >= 0) & (y + th + 4 <= ph - 1)
+        cl = used & ~inside
+        clamp_any |= cl
+        off = np.where(cl, (x & 0xffff) | ((y & 0xffff) << 16), (y * pw + x) & 0xffffffff)
+        u[f"src_off{k}"] = np.where(used, off.astype(np.uint32).view(np.int32), u[f"src_off{k}"])
+        u[f"mx{k}"] = np.where(cl, u[f"mx{k}"] | 0x80, u[f"mx{k}"])
+    # clamped units last inside their class (stable), the class_warp sub-range
+    order = np.lexsort((np.arange(len(u)), clamp_any, u["tx"]))
+    u = u[order]
+    class_warp = np.bincount(u["tx"][clamp_any[order]], minlength=abi.N_TX).astype(np.int32)
+    out = dataclasses.replace(fd, units=u, class_warp=class_warp, refs=None,
+                              blk=None if fd.blk is None else fd.blk[order],
+                              aux=None if fd.aux is None else fd.aux[order],
+                              src_xy=None if fd.src_xy is None else fd.src_xy[order])
+    out.stats = dict(fd.stats, clamped_units=int(clamp_any.sum()))
+    return out, exact

@@ -413,22 +413,39 @@ typedef struct Dav1dGpuFrameBatch {
     const void *aux_pool; /* device pool of masks (u8) / palette records;
                              INTER_WMASK units write their masks into it    */
     int32_t  class_warp[DGPU_N_RECT_TX_SIZES]; /* WARP, INTER_INTRA, INTER_
-                             WMASK, INTER_OBMC and INTER_SCALED units
-                             at the end of each class range (units sorted
-                             so); they run in a second launch whose kernel
+                             WMASK, INTER_OBMC and INTER_SCALED units, and
+                             INTER / INTER_AVG / INTER_WAVG / INTER_MASK
+                             units with a DGPU_MX_CLAMP reference, at the
+                             end of each class range (units sorted so);
+                             they run in a second launch whose kernel
                              keeps their registers out of the main kernel.
                              64-point classes must have none; WARP units
                              need both sides >= 8                           */
 } Dav1dGpuFrameBatch;
 
+/* Per-unit emu_edge (round 5): an INTER / INTER_AVG / INTER_WAVG /
+ * INTER_MASK unit sets DGPU_MX_CLAMP in mx[k] (the fraction stays in the low
+ * 4 bits) when the footprint of its reference k leaves that reference plane,
+ * as recon_tmpl.c's mc() decides emu_edge (src/recon_tmpl.c:986-999); its
+ * src_off[k] then holds the integer position of the unit's top-left in the
+ * plane as (x & 0xffff) | (y << 16), both int16, and every footprint pixel is
+ * read at its position clamped to the plane's visible w x h (emu_edge_c,
+ * src/mc_tmpl.c:827-875), so unpadded pictures work.  Such units go in the
+ * class_warp sub-range.  A unit without the flag is read as it stands: its
+ * footprint -- the unit's rectangle -3 / +4 pixels, plus up to 3 pixels
+ * before and 5 after each row for the aligned row loads -- must then lie
+ * inside the plane (or inside readable edge-replicated padding). */
+#define DGPU_MX_CLAMP 0x80
+
 /* Launch one frame batch on `stream` (a hipStream_t, NULL = default).
  * Returns 0 or a negative error.  Asynchronous w.r.t. the host.
- * Reference footprints are read straight from the reference planes: the
- * unit batch does NOT emulate edges, so every footprint (the unit's
- * rectangle -3 / +4 pixels) must lie inside readable, edge-replicated
- * memory (e.g. planes padded by >= 80 px with dav1d's own border
- * extension).  Blocks whose footprint leaves the picture belong in the
- * tile batch below, which clamps (emu_edge semantics). */
+ * Reference footprints are read straight from the reference planes, except
+ * for DGPU_MX_CLAMP units (above), which clamp every pixel to the plane:
+ * a caller either pads its reference planes (>= 80 px, dav1d's own border
+ * extension) or flags the units whose footprint leaves them.  WARP,
+ * INTER_INTRA, INTER_WMASK, INTER_OBMC and INTER_SCALED units still read
+ * unclamped footprints (the recorder and the tile batch emulate edges for
+ * them). */
 int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream);
 int dav1d_gpu_recon_16bpc(const Dav1dGpuFrameBatch *b, void *stream);
 

@@ -325,3 +325,35 @@ def test_ext2_kinds_cut_invariant(pkg, oracle, bpc, bdmax):
     hb.run()
     for p in range(3):
         assert np.array_equal(ha.dst[p], hb.dst[p]), f"plane {p}"
+
+
+def test_clamp_units_conversion(pkg):
+    """workload.clamp_units (the unit batch on exact-size references): flags
+    exactly the inter units whose footprint (with the aligned-load margins)
+    leaves the plane, packs their position as x | y << 16, re-expresses the
+    others' src_off in the exact stride, and moves the flagged units to the
+    end of their class (class_warp); every other field is untouched."""
+    import dav1d_mirror_amd.workload as wl
+    import dav1d_mirror_amd.abi as abi
+    fd = wl.make_frame(wl.FrameConfig(width=256, height=128, seed=3, mv_range=100))
+    fdc, exact = wl.clamp_units(fd)
+    assert [a.shape for a in exact[0]] == [(h, w) for (w, h) in fd.plane_wh]
+    assert np.array_equal(fdc.class_start, fd.class_start)
+    u, c = fdc.units, fdc.class_start
+    flagged = ((u["mx0"] | u["mx1"]) & 0x80) != 0
+    assert flagged.sum() == fdc.stats["clamped_units"] > 0
+    for t in range(abi.N_TX):   # flagged units form the tail of each class range
+        seg = flagged[c[t]:c[t + 1]]
+        assert seg.sum() == fdc.class_warp[t] and not seg[:len(seg) - seg.sum()].any()
+    for i in np.flatnonzero(flagged)[:200]:
+        for k in range(2):
+            if u[f"mx{k}"][i] & 0x80:
+                so = int(u[f"src_off{k}"][i])
+                x, y = (so & 0xffff) - ((so & 0x8000) << 1), so >> 16
+                assert (x, y) == tuple(fdc.src_xy[i, k])
+    # (the intra / CfL views alias the inter fields in the union)
+    keep = ["dst_off", "coef_off", "tx", "txtp", "plane", "pred", "nzw", "nzh", "bw4", "bh4", "my0", "my1",
+            "filter2d", "ref0", "ref1", "weight"]
+    a = np.sort(fd.units[keep], order=keep)
+    b = np.sort(u[keep], order=keep)
+    assert np.array_equal(a, b)

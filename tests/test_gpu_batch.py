@@ -190,3 +190,31 @@ def test_batch_ext2_masks_and_cut(pkg, oracle, bpc, bdmax, seed):
         torch.cuda.synchronize()
         pics.append(d.planes_host())
     assert all(np.array_equal(a, b) for a, b in zip(*pics))
+
+
+@pytest.mark.parametrize("bpc,bdmax,kind,mv,size", [
+    (8, 255, "full", 64, (512, 256)), (8, 255, "full", 200, (512, 256)), (8, 255, "mc", 200, (512, 256)),
+    (16, 1023, "full", 200, (512, 256)), (16, 4095, "full", 64, (512, 256)), (8, 255, "full", 64, (3840, 2160))])
+def test_batch_unpadded_refs(pkg, oracle, bpc, bdmax, kind, mv, size):
+    """emu_edge in the unit batch (round 5): exact-size reference planes
+    (stride = width), the units whose footprint leaves them flagged
+    DGPU_MX_CLAMP and run in the second launch with every footprint pixel
+    clamped, the rest read in place; the picture equals the oracle's walk of
+    the same blocks on edge-replicated padded references (what emu_edge_c
+    reads, src/mc_tmpl.c:827-875).  MVs up to 200 px outside the picture."""
+    import torch
+    import dav1d_mirror_amd.batch as bt
+    import dav1d_mirror_amd.workload as wl
+    fd = _frame(pkg, width=size[0], height=size[1], bpc=bpc, bitdepth_max=bdmax, kind=kind, seed=21, mv_range=mv)
+    fdc, exact = wl.clamp_units(fd)
+    n_inter = int(np.isin(fd.units["pred"], (1, 2, 5, 6)).sum())
+    assert 0 < fdc.stats["clamped_units"] < n_inter
+    dev = bt.DeviceFrame(fdc, "cuda:0", exact_refs=exact)
+    dev.launch()
+    torch.cuda.synchronize()
+    got = dev.planes_host()
+    hf = oracle.HostFrame(fd)
+    hf.run(threads=8)
+    for p in range(3):
+        diff = np.argwhere(got[p] != hf.dst[p])
+        assert len(diff) == 0, f"plane {p}: {len(diff)} pixels differ, first {diff[:5].tolist()}"

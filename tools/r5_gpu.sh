@@ -65,6 +65,10 @@ for s in "${@:-tests}"; do
             done
         done
         unset DAV1D_GPU_LIB_VARIANT ;;
+    post) # CDEF, LR, super-res and deblocking bench legs (the headline leg runs too)
+        timeout -k 10 400 python -u bench.py --steps 50 --no-families --no-configs --no-tiles --no-intra --no-recorder \
+            --no-grain --no-cpu --no-check > "$O/post.json" 2> "$O/post.log" || { echo "[r5] post failed"; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/post.json')); print('post', {k: (d[k]['us_per_frame'], d[k]['bit_exact_vs_oracle']) for k in ('cdef','loop_restoration','superres','loop_filter')})" ;;
     lr) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_lr.py "tests/test_gpu_checkasm.py::test_checkasm[lr]" tests/test_gpu_chain.py > "$O/lr.log" 2>&1 || { echo "[r5] lr failed"; tail -5 "$O/lr.log"; exit 1; }
         tail -1 "$O/lr.log"
         timeout -k 10 300 python -u bench.py --steps 50 --no-families --no-configs --no-tiles --no-intra --no-recorder \
@@ -90,6 +94,12 @@ for s in "${@:-tests}"; do
     bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r5] bench failed"; exit 1; } ;;
     benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r5] benchfast failed"; exit 1; } ;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 50 $BENCH_FAST) > "$O/prof.log" 2>&1 || { echo "[r5] prof failed"; exit 1; } ;;
+    prof10) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof10" -o run --output-format csv -- python3 "$R/bench.py" --config 4k-10bit --steps 50 $BENCH_FAST) > "$O/prof10.log" 2>&1 || { echo "[r5] prof10 failed"; exit 1; }
+            for c in FETCH_SIZE WRITE_SIZE; do
+                (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/pmc10_$c" -o run --output-format csv -- python3 "$R/bench.py" --config 4k-10bit --steps 10 --warmup 2 $BENCH_FAST) > "$O/pmc10_$c.log" 2>&1 || { echo "[r5] pmc10 $c failed"; exit 1; }
+            done ;;
+    sqpmc) # SQ counters of the headline kernel (one pass: 8 SQ counters at most)
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE -d "$O/sqpmc" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 $BENCH_FAST) > "$O/sqpmc.log" 2>&1 || { echo "[r5] sqpmc failed"; exit 1; } ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE; do
              (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/pmc_$c" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 $BENCH_FAST) > "$O/pmc_$c.log" 2>&1 || { echo "[r5] pmc $c failed"; exit 1; }
          done ;;
