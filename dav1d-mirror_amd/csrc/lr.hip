@@ -26,6 +26,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
 #include "runtime.hpp"
@@ -76,10 +78,13 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     __shared__ int16_t T[kLrTH][kLrTW];
     // 3x3 A / B at unit rows -1..h (every row), strip columns -1..sw; the
     // Wiener units' horizontal pass reuses the A array
-    __shared__ int AA[kLrVH][kLrSW + 2];
+    // (8-bit: A <= (255 * 25 * 255 * 164 + 2^11) >> 12 = 65089 -- and the
+    // 3x3 bound is lower -- fits 16 bits: 15.7 KB per workgroup, ten per CU)
+    using AT = std::conditional_t<BPC == 8, uint16_t, int>;
+    __shared__ AT AA[kLrVH][kLrSW + 2];
     __shared__ uint8_t BB[kLrVH][kLrSW + 2];
     // 5x5 A / B at unit rows -1, 1, .. (row jj at jj / 2)
-    __shared__ int AA5[kLrVH / 2][kLrSW + 2];
+    __shared__ AT AA5[kLrVH / 2][kLrSW + 2];
     __shared__ uint8_t BB5[kLrVH / 2][kLrSW + 2];
     // sgr_x_by_x in LDS: a global-memory lookup per A / B position put one
     // memory round trip per loop iteration on the block's critical path
@@ -204,7 +209,7 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
                     const int sum = h3[1] + h3[2] + h3[3], sumsq = q3[1] + q3[2] + q3[3];
                     int A, B;
                     lr_ab_sums<9>(sum, sumsq, s1, bd8, XBX, A, B);
-                    AA[jj][ii] = A;
+                    AA[jj][ii] = (AT)A;
                     BB[jj][ii] = (uint8_t)B;
                 }
                 if (do5 && !(jj & 1)) {   // n = 25: rows jj .. jj + 4
@@ -212,7 +217,7 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
                     const int sumsq = q5[0] + q5[1] + q5[2] + q5[3] + q5[4];
                     int A, B;
                     lr_ab_sums<25>(sum, sumsq, s0, bd8, XBX, A, B);
-                    AA5[jj >> 1][ii] = A;
+                    AA5[jj >> 1][ii] = (AT)A;
                     BB5[jj >> 1][ii] = (uint8_t)B;
                 }
             }
@@ -230,7 +235,7 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
         int v[8];
 #pragma unroll
         for (int m = 0; m < 8; m++) v[m] = 0;
-        auto row = [&](const int *ar, const uint8_t *br, int &sa, int &ca, int &sb, int &cb) {
+        auto row = [&](const AT *ar, const uint8_t *br, int &sa, int &ca, int &sb, int &cb) {
             const int a0 = ar[ii - 1], a1 = ar[ii], a2 = ar[ii + 1];
             const int b0 = br[ii - 1], b1 = br[ii], b2 = br[ii + 1];
             sa = a0 + a1 + a2;

@@ -303,13 +303,12 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs<BPC> a) {
 // launch, blockIdx.z = plane.  A wave upscales 256 consecutive output pixels
 // of kRzRows rows: the source spans they read (at most 256 * dx / 2^14 + 8
 // pixels per row, dx <= 2^14 since super-res only upscales) are loaded once
-// into LDS with the reference's column clamp applied at load time -- every
-// row's loads in flight together (round 5: two rows per wave, 26.8 -> see
-// DESIGN.md 7) -- then each lane filters four outputs (x0 + lane + 64 k) per
-// row from LDS with the 8 taps of resize_c.
+// into LDS with the reference's column clamp applied at load time (every
+// row's loads in flight together), then each lane filters four outputs
+// (x0 + lane + 64 k) per row from LDS with the 8 taps of resize_c.
 constexpr int kRzOut = 256, kRzSpan = kRzOut + 16;
 #ifndef DGPU_RZ_ROWS
-#define DGPU_RZ_ROWS 2
+#define DGPU_RZ_ROWS 1   // 2 rows per wave measured 27.6 against 26.8 us: no gain
 #endif
 constexpr int kRzRows = DGPU_RZ_ROWS;   // rows per wave
 template <int BPC> struct ResizeFrameArgs {

@@ -73,6 +73,9 @@
 #ifndef DGPU_VODD_ALIGN
 #define DGPU_VODD_ALIGN 0   // odd vertical rows by realigned pairs (the round-1/2 form) instead of shifted taps
 #endif
+#ifndef DGPU_RES_PAD
+#define DGPU_RES_PAD 0   // experiment: padded residual columns (Slot::RS)
+#endif
 #ifndef DGPU_ALIGNED_ROWS16
 #define DGPU_ALIGNED_ROWS16 0   // 16bpc: register pressure spills with it (measured), off
 #endif
@@ -260,7 +263,13 @@ template <int BPC, int TX> struct Slot {
     static constexpr int CB = sizeof(typename Px<BPC>::coef);
     static constexpr int TB = sizeof(typename Tmp<BPC>::T);
     static constexpr int CF = a16(CL::SW * CL::SH * CB + 16);   // compact coefs at their 16-B skew
-    static constexpr int RES = W * H * TB;                       // residual, column-major [x][y]
+    // residual, column-major [x][y] with a column stride of RS elements:
+    // DGPU_RES_PAD pads the 8-bit columns of 8 and more rows by 4, so the
+    // column pass's 8-byte writes and the tasks' 4-byte reads of one lane
+    // group fall on distinct banks (a 16-row column is 8 dwords: 4-way
+    // conflicts; 32 rows: 8-way)
+    static constexpr int RS = H + ((DGPU_RES_PAD && BPC == 8 && H >= 8) ? 4 : 0);
+    static constexpr int RES = W * RS * TB;
     static constexpr int CFR = a16(cmax(CF, RES));
     static constexpr int TMP = a16(CL::SH * W * TB);             // row-pass output [y][x]
     static constexpr int MID = CL::RP * W * 4;                   // one ref: [row pair][x] int16 x2
@@ -1627,7 +1636,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #pragma unroll
                 for (int y = 0; y < H; y++) col[y] = y < SH ? (int)tmp[y * W + x] : 0;
                 tx1d<H, 1, BPC == 8>(kind_v(txtp), col, cc);
-                TT *rcol = res + x * H;
+                TT *rcol = res + x * SL::RS;
                 if constexpr (BPC == 8) {
 #pragma unroll
                     for (int y = 0; y < H; y += 4) {
@@ -1704,7 +1713,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         if (haveres) {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const TT *rp = res + (4 * q + i) * H + 2 * j;
+                const TT *rp = res + (4 * q + i) * SL::RS + 2 * j;
                 if constexpr (BPC == 8) {
                     const uint32_t v = *reinterpret_cast<const uint32_t *>(rp);
                     rv[i] = (int)(int16_t)(v & 0xffff);
@@ -2152,7 +2161,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
 #pragma unroll
                 for (int y = 0; y < H; y++) col[y] = y < SH ? (int)tmp[y * W + x] : 0;
                 tx1d<H, 1, BPC == 8>(kind_v(txtp), col, cc);
-                TT *rcol = res + x * H;
+                TT *rcol = res + x * SL::RS;
 #pragma unroll
                 for (int y = 0; y < H; y++) rcol[y] = (TT)((col[y] + 8) >> 4);
             }
@@ -2166,7 +2175,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
             int o[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int rv = haveres ? (int)res[(4 * q + i) * H + 2 * j + rr] : dcres;
+                const int rv = haveres ? (int)res[(4 * q + i) * SL::RS + 2 * j + rr] : dcres;
                 o[i] = clampi(pv[4 * rr + i] + rv, 0, bdmax);
             }
             P *row = dstp + __mul24(2 * j + rr, ds) + 4 * q;   // 24-bit: strides < 2^23 px (full-rate multiply)

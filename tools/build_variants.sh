@@ -65,6 +65,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         persist3) TUS=recon8 build persist3 -DDGPU_PERSIST=3 -DDGPU_LANE_OPAQUE=1 ;;
         persist3n) TUS=recon8 build persist3n -DDGPU_PERSIST=3 ;;
         ntload) TUS=recon8 build ntload -DDGPU_NT_STREAM=1 ;;
+        respad) TUS=recon8 build respad -DDGPU_RES_PAD=1 ;;
         persist4) TUS=recon8 build persist4 -DDGPU_PERSIST=4 -DDGPU_LANE_OPAQUE=1 -DDGPU_PERSIST_WPE=4 ;;
         merge) build merge -DDGPU_MERGE_GROUPS=1 ;;
         sl2) build sl2 -DDGPU_SEG_INNER=2 ;;
