@@ -78,9 +78,10 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     __shared__ int16_t T[kLrTH][kLrTW];
     // 3x3 A / B at unit rows -1..h (every row), strip columns -1..sw; the
     // Wiener units' horizontal pass reuses the A array
-    // (8-bit: A <= (255 * 25 * 255 * 164 + 2^11) >> 12 = 65089 -- and the
-    // 3x3 bound is lower -- fits 16 bits: 15.7 KB per workgroup, ten per CU)
-    using AT = std::conditional_t<BPC == 8, uint16_t, int>;
+    // (32-bit A: 16-bit A arrays at 8 bit -- A <= 65089 fits -- gave 15.7 KB
+    // per workgroup and 8 waves per SIMD but measured 60.9 against 50.9 us:
+    // the 2-byte LDS accesses of neighbouring lanes share dwords)
+    using AT = int;
     __shared__ AT AA[kLrVH][kLrSW + 2];
     __shared__ uint8_t BB[kLrVH][kLrSW + 2];
     // 5x5 A / B at unit rows -1, 1, .. (row jj at jj / 2)
