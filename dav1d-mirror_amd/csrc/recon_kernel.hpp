@@ -175,8 +175,16 @@ __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 #ifndef DGPU_TALL_LANES
 #define DGPU_TALL_LANES 1
 #endif
+#ifndef DGPU_IE_SMALL_LANES
+// experiment (the intra wavefront TUs only, tools/build_variants.sh ielanes):
+// lanes per unit of the 4x4 / 4x8 / 8x4 classes.  Above level 0 a wavefront
+// task holds at most 8 units, so at 2-4 lanes per unit most of its wave idles
+// while the small units' edge preparation and prediction run per lane
+#define DGPU_IE_SMALL_LANES 0
+#endif
 __host__ __device__ constexpr int lanes_per_unit(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
+    if (DGPU_IE_SMALL_LANES && w * h <= 32) return DGPU_IE_SMALL_LANES;
     if (w * h >= 1024) return 64;
     // tall classes: as few lanes as the column pass has lines (or half as
     // many for 8x32), so the column transforms leave no lane idle, within
@@ -902,6 +910,7 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
     uint32_t *mp;
     unsigned sb;
     int p0;
+    int prow;            // the row pair rp points at (p0, or the last one, see init)
     uint4 th;            // taps: 8bpc .x/.y int8 x4, 16bpc int16 pairs
 
     int rlo, rhi;        // footprint rows the vertical taps read (others are not loaded)
@@ -970,7 +979,15 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
         sb = (unsigned)stride_px * B;
         const int q = l % QW;
         p0 = l / QW;
-        rp = reinterpret_cast<const uint8_t *>(org) + (size_t)__umul24(2u * p0, sb) + 4 * B * q;
+        // a lane's first row pair; with more lanes than row pairs (PS > RP:
+        // DGPU_IE_SMALL_LANES builds) the lanes past the footprint load (and
+        // discard) its last pair: load() forms each row as (p - base) * 2
+        // rows from rp in unsigned 24-bit arithmetic, which must not go
+        // negative (it did, and faulted, before this guard)
+        int pb = p0;
+        if constexpr (PS > RP) pb = cmin(p0, RP - 1);
+        prow = pb;
+        rp = reinterpret_cast<const uint8_t *>(org) + (size_t)__umul24(2u * pb, sb) + 4 * B * q;
         sh = 0;
         if constexpr (AL) {
             sh = (unsigned)reinterpret_cast<uintptr_t>(rp) & 3u;   // strides are dword multiples (launch check)
@@ -1001,7 +1018,7 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
             const bool task = k0 + c < IT && pu < RP;
             const bool n0 = !DGPU_ROWSKIP || (task && 2 * p >= rlo && 2 * p <= rhi);
             const bool n1 = !DGPU_ROWSKIP || (task && 2 * p + 1 >= rlo && 2 * p + 1 <= rhi);
-            const uint8_t *a0 = rp + (size_t)__umul24((unsigned)(p - p0) * 2u, sb);
+            const uint8_t *a0 = rp + (size_t)__umul24((unsigned)(p - (PS > RP ? prow : p0)) * 2u, sb);
             // row 2p+1 == H+7 (last pair) is never used: re-read row 2p
             const uint8_t *a1 = 2 * p + 1 < H + 7 ? a0 + sb : a0;
 #ifdef DGPU_FAKE_COALESCE

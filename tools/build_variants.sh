@@ -44,6 +44,8 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         fsleep1) TUS="recon_ie8" build fsleep1 -DDGPU_FLOW_SLEEP=1 ;;
         ftrace) TUS="recon_ie8" build ftrace -DDGPU_FLOW_TRACE=1 ;;
         fprio) TUS="recon_ie8" build fprio -DDGPU_FLOW_PRIO=1 ;;
+        ielanes) TUS="recon_ie8" build ielanes -DDGPU_IE_SMALL_LANES=8 ;;
+        ielanes16) TUS="recon_ie8" build ielanes16 -DDGPU_IE_SMALL_LANES=16 ;;
         sbdiag) TUS="recon_sb8" build sbdiag -DDGPU_DIAG=1 ;;   # tools/sb_debug.py
         fphase) TUS="recon_ie8" build fphase -DDGPU_FLOW_TRACE=1 -DDGPU_TRACE=1 -DDGPU_TRACE_RT=1 ;;
         ftrace127) TUS="recon_ie8" build ftrace127 -DDGPU_FLOW_TRACE=1 -DDGPU_FLOW_SLEEP=127 ;;

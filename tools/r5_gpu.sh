@@ -75,6 +75,12 @@ for s in "${@:-tests}"; do
             --no-grain --no-cdef --no-superres --no-lpf --no-cpu --no-check > "$O/lrbench.json" 2> "$O/lrbench.log" \
             || { echo "[r5] lr bench failed"; exit 1; }
         python3 -c "import json; d=json.load(open('$O/lrbench.json'))['loop_restoration']; print('lr', d['us_per_frame'], d['bit_exact_vs_oracle'])" ;;
+    varintra) # the intra-frame and recorder GPU tests on each variant library (ABV)
+        for v in $ABV; do
+            DAV1D_GPU_LIB_VARIANT=$v timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_intra_frame.py tests/test_gpu_recorder.py > "$O/varintra_$v.log" 2>&1 \
+                || { echo "[r5] varintra $v failed"; tail -5 "$O/varintra_$v.log"; exit 1; }
+            echo "varintra $v $(tail -1 "$O/varintra_$v.log")"
+        done ;;
     abintra) # the intra wavefront bench leg per variant library (ABV): 1-tile / 2x2 ms per 4K frame, bit-exact
         for v in base $ABV; do
             if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
