@@ -328,6 +328,8 @@ def load_lib():
         L.dav1d_gpu_recorder_stats.restype = ctypes.c_int
         L.dav1d_gpu_recorder_status.argtypes = [ctypes.c_void_p]
         L.dav1d_gpu_recorder_status.restype = ctypes.c_int
+        L.dav1d_gpu_recorder_set_top_edge.argtypes = [ctypes.c_void_p, ctypes.POINTER(Plane * 3), ctypes.c_int]
+        L.dav1d_gpu_recorder_set_top_edge.restype = ctypes.c_int
         L.dav1d_gpu_get_error.restype = ctypes.c_int
         L.dav1d_gpu_pic_allocator_init.argtypes = [ctypes.POINTER(PicAllocator), ctypes.c_int, ctypes.c_int]
         L.dav1d_gpu_pic_allocator_init.restype = ctypes.c_int
@@ -363,6 +365,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_intra_workspace_bytes",
     "dav1d_gpu_recorder_new", "dav1d_gpu_recorder_free", "dav1d_gpu_rec_block", "dav1d_gpu_rec_block_aux", "dav1d_gpu_rec_residual",
     "dav1d_gpu_recorder_flush", "dav1d_gpu_recorder_stats", "dav1d_gpu_recorder_status",
+    "dav1d_gpu_recorder_set_top_edge",
     "dav1d_gpu_apply_grain_8bpc", "dav1d_gpu_apply_grain_16bpc",
     "dav1d_cdef_dsp_init_8bpc", "dav1d_cdef_dsp_init_16bpc",
     "dav1d_cdef_dsp_init_gpu_8bpc", "dav1d_cdef_dsp_init_gpu_16bpc",

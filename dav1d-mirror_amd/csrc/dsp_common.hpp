@@ -530,6 +530,27 @@ __device__ __forceinline__ void wht4(int *c) {
     c[3 * S] = t2 + t1;
 }
 
+// WHT_WHT (lossless 4x4) for the batch kernels, src/itx_tmpl.c:166-185: both
+// passes in one lane's int32 registers from the compact coefficient region
+// (column-major, nzh rows; zeros outside it), coef >> 2 first, no clip and no
+// shift anywhere.  t[] is the residual, row-major.  A batch kernel keeps an
+// 8-bit residual in int16: saturating it there changes no output pixel (a
+// residual beyond +-32767 clips the same way for any pixel in [0, bdmax]),
+// whereas the row pass's int16 intermediate would not be exact for extreme
+// coefficients, which is why this does not reuse the kernels' row / column
+// passes.
+template <typename C>
+__device__ __forceinline__ void wht4x4(const C *cs, int nzw, int nzh, int *t) {
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) t[4 * y + x] = (x < nzw && y < nzh) ? (int)cs[x * nzh + y] >> 2 : 0;
+        wht4<1>(&t[4 * y]);
+    }
+#pragma unroll
+    for (int x = 0; x < 4; x++) wht4<4>(&t[x]);
+}
+
 enum Kind1D { K_DCT = 0, K_ADST = 1, K_FLIPADST = 2, K_IDENTITY = 3 };
 
 // Run-time kind, compile-time length.  Unsupported (kind, N) pairs never

@@ -1479,6 +1479,8 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     const int nzw = u.nzw, nzh = u.nzh;
     const bool dconly = !nores && nzw == 0;
     const bool haveres = !nores && !dconly && !DGPU_ABL_ITX;
+    // WHT_WHT (lossless, 4x4 units only): one lane runs both passes below
+    const bool wht = W == 4 && H == 4 && txtp == DGPU_WHT_WHT;
     P *dstp = pt.dst[plane] + u.dst_off;
     const int ds = pt.dst_stride[plane];
 
@@ -1597,7 +1599,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         dcres = (dc * 181 + 128 + 2048) >> 12;
     }
     const Clip rc = ItxClip<BPC>::row(bdmax), cc = ItxClip<BPC>::col(bdmax);
-    if (haveres) {
+    if (haveres && !wht) {
         const C *cs = reinterpret_cast<const C *>(cfl + cfsk);
 #pragma unroll
         for (int k = 0; k < (SH + G - 1) / G; k++) {
@@ -1644,7 +1646,18 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 
     mark(4);
     // ---------------- P4: column transforms -> residual [W][H] ----------------
-    if (haveres) {
+    if constexpr (W == 4 && H == 4) {
+        if (wht && l == 0) {   // the staged coefficients are read before the residual overwrites them
+            int t[16];
+            wht4x4(reinterpret_cast<const C *>(cfl + cfsk), nzw, nzh, t);
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+                    res[x * SL::RS + y] = (TT)(BPC == 8 ? clampi(t[4 * y + x], -32768, 32767) : t[4 * y + x]);
+        }
+    }
+    if (haveres && !wht) {
 #pragma unroll
         for (int k = 0; k < (W + G - 1) / G; k++) {
             const int x = l + k * G;
@@ -2090,6 +2103,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
     const int nzw = u.nzw, nzh = u.nzh;
     const bool dconly = !nores && nzw == 0;
     const bool haveres = !nores && !dconly;
+    const bool wht = W == 4 && H == 4 && txtp == DGPU_WHT_WHT;   // lossless: one lane, both passes
     P *dstp = pt.dst[plane] + u.dst_off;
     const int ds = pt.dst_stride[plane];
     const int auxo = bld(a.aux + first + g);
@@ -2144,7 +2158,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
         dcres = (dc * 181 + 128 + 2048) >> 12;
     }
     const Clip rc = ItxClip<BPC>::row(bdmax), cc = ItxClip<BPC>::col(bdmax);
-    if (haveres) {
+    if (haveres && !wht) {
         const C *cs = reinterpret_cast<const C *>(cfl + cfsk);
 #pragma unroll
         for (int k = 0; k < (SH + G - 1) / G; k++) {
@@ -2169,7 +2183,18 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
         }
     }
     wave_sync();
-    if (haveres) {
+    if constexpr (W == 4 && H == 4) {
+        if (wht && l == 0) {
+            int t[16];
+            wht4x4(reinterpret_cast<const C *>(cfl + cfsk), nzw, nzh, t);
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+                    res[x * SL::RS + y] = (TT)(BPC == 8 ? clampi(t[4 * y + x], -32768, 32767) : t[4 * y + x]);
+        }
+    }
+    if (haveres && !wht) {
 #pragma unroll
         for (int k = 0; k < (W + G - 1) / G; k++) {
             const int x = l + k * G;

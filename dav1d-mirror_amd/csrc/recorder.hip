@@ -409,6 +409,7 @@ struct Dav1dGpuRecorder {
     std::vector<uint8_t> auxp;   // the aux pool: masks, palette / warp / OBMC / scaled records
     std::vector<Dav1dGpuUnit> xunits;   // the launch ahead of the wavefront (class order)
     std::vector<int32_t> xaux;
+    std::vector<Dav1dGpuEdgeBackup> bk;   // backup runs of launch-ahead predictions (top_edge)
     std::vector<uint8_t> h_host;   // DAV1D_GPU_REC_HOSTONLY: stands in for the pinned buffer
     // per-4x4 maps kept across flushes (generation-stamped): the residual
     // recorded at each cell (index + res_base) and its writer (cell_base + cell)
@@ -421,7 +422,12 @@ struct Dav1dGpuRecorder {
     int32_t res_base = 0, cell_base = 0;
     PinnedBuf pin;   // units | recs | coefficients | emu jobs, written in place by the fill
     PinnedBuf flag;  // the last flush's wavefront error word, copied back on its stream
-    DevBuf d_units, d_recs, d_coef, d_edges, d_work, d_emu, d_emu_jobs, d_aux, d_auxp, d_xunits, d_xaux;
+    DevBuf d_units, d_recs, d_coef, d_edges, d_work, d_emu, d_emu_jobs, d_aux, d_auxp, d_xunits, d_xaux, d_bk;
+    // dav1d_gpu_recorder_set_top_edge: the caller's f->ipred_edge planes
+    // (superblock-top rows read from and backed up to them), luma superblock log2
+    Dav1dGpuPlane top[3] = {};
+    bool top_on = false;
+    int sb_log2 = 6;
     hipEvent_t done = nullptr;
     bool pending_check = false;   // the last flush's error word not read yet
     int32_t last_units = 0, last_levels = 0;
@@ -458,6 +464,7 @@ extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
         r->d_auxp.release();
         r->d_xunits.release();
         r->d_xaux.release();
+        r->d_bk.release();
     }
     delete r;
 }
@@ -474,6 +481,34 @@ static bool plane_dims(const Dav1dGpuRecorder *r, int plane, int &w, int &h) {
     return true;
 }
 constexpr int kMapPad4 = 32;   // 4x4 cells past the grid a transform block can reach (128 px)
+
+// The decoder's superblock-top edge rows (f->ipred_edge, backed up by
+// dav1d_backup_ipred_edge, src/recon_tmpl.c:2162-2186, and read by
+// prepare_intra_edges as prefilter_toplevel_sb_edge, :1275-1279, :1394-1398,
+// :1664-1668, src/ipred_prepare_tmpl.c:117-126).  Rows must cover the plane's
+// grid rounded up to whole superblocks (transform blocks past the grid write
+// their bottom rows there too, as in dav1d's sb128w * 128 rows) and one row
+// per superblock row but the last.
+extern "C" int dav1d_gpu_recorder_set_top_edge(Dav1dGpuRecorder *r, const Dav1dGpuPlane top_edge[3], int sb128) {
+    if (!r) return -1;
+    if (!top_edge) {
+        r->top_on = false;
+        return 0;
+    }
+    const int bpp = r->bpc / 8, l2 = sb128 ? 7 : 6;
+    for (int p = 0; p < 3; p++) {
+        int pw, ph;
+        plane_dims(r, p, pw, ph);
+        const int sl = p ? l2 - 1 : l2, sb = 1 << sl;
+        const int64_t need_w = ((int64_t)pw + sb - 1) / sb * sb, need_h = ((int64_t)ph + sb - 1) / sb - 1;
+        const Dav1dGpuPlane &t = top_edge[p];
+        if (!t.data || t.w < need_w || t.h < need_h || t.stride < (int64_t)t.w * bpp) return -1;
+    }
+    for (int p = 0; p < 3; p++) r->top[p] = top_edge[p];
+    r->sb_log2 = l2;
+    r->top_on = true;
+    return 0;
+}
 
 static int check_block(const Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, bool ext) {
     int pw, ph;
@@ -710,6 +745,13 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     std::vector<uint8_t> &auxp = r->auxp;
     std::vector<Dav1dGpuUnit> &xunits = r->xunits;
     std::vector<int32_t> &xaux = r->xaux;
+    // superblock height log2 per plane (4:2:0), and the TOP_SB_EDGE flag of an
+    // edge record whose top row is a superblock's top (per transform block,
+    // recon_tmpl.c:1276 / :1395; inter-intra per block, :1665 / :1794)
+    const int sbl[3] = {r->sb_log2, r->sb_log2 - 1, r->sb_log2 - 1};
+    auto top_sb = [&](int p, int y, bool ht) {
+        return r->top_on && ht && (y & ((1 << sbl[p]) - 1)) == 0 ? DGPU_IE_TOP_SB_EDGE : 0;
+    };
     auto build = [&](size_t bi, CellPart &P) -> int {
         const Dav1dGpuRecBlock &b = r->blocks[bi];
         const TxDim t = kTx[b.tx];
@@ -1020,13 +1062,13 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                         // prepare_intra_edges with no edge flags, no edge filter, angle 0 (:1551-1566)
                         e.mode = b.mode;
                         e.angle = 0;
-                        e.flags = (uint8_t)((hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0));
+                        e.flags = (uint8_t)((hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0) | top_sb(p, uy, ht));
                         const int m = remap_mode(e.mode, 0, hl, ht);
                         nd = kNeeds[m];
                         c.sortmode = 16 + m;
                     }
                 } else {
-                    int fl = (hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0);
+                    int fl = (hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0) | top_sb(p, uy, ht);
                     if (!cfl) {   // recon_tmpl.c:1252-1266 (blocks up to 64 wide: one 64x64 step)
                         const int x = ox / 4, y = oy / 4;
                         const bool sb_tr = b.flags & DGPU_IE_TOP_HAS_RIGHT, sb_bl = b.flags & DGPU_IE_LEFT_HAS_BOTTOM;
@@ -1415,11 +1457,26 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     // image: units | records | coefficients | emu jobs | per-unit aux |
     //        launch-ahead units (class order) | their aux | aux pool
     const size_t nx = r->xunits.size();
+    // with top_edge: the launch-ahead predictions whose bottom row ends a
+    // superblock row are backed up once that launch is done (backup runs
+    // between it and the wavefront, dav1d_backup_ipred_edge); a residual on
+    // them is added by a wavefront unit, which backs its row up again
+    std::vector<Dav1dGpuEdgeBackup> &bk = r->bk;
+    bk.clear();
+    if (r->top_on)
+        for (const Dav1dGpuUnit &u : r->xunits) {
+            const int p = u.plane, ds_px = (int)(dst[p].stride / bpp);
+            const int uy = u.dst_off / ds_px, ux = u.dst_off % ds_px, y1 = uy + kTx[u.tx].h;
+            const int sby = (y1 >> sbl[p]) - 1, w = std::min(kTx[u.tx].w, r->top[p].w - ux);
+            if ((y1 & ((1 << sbl[p]) - 1)) == 0 && sby < r->top[p].h && w > 0)
+                bk.push_back(Dav1dGpuEdgeBackup{p, sby, ux, w});
+        }
     const size_t bu = (size_t)n * sizeof(Dav1dGpuUnit), br = (size_t)n * sizeof(Dav1dGpuIntraEdge),
                  bc = coef_at * cb, be = r->emu.size() * sizeof(EmuJob), ba = (size_t)n * 4,
-                 bxu = nx * sizeof(Dav1dGpuUnit), bxa = nx * 4, bp = r->auxp.size();
+                 bxu = nx * sizeof(Dav1dGpuUnit), bxa = nx * 4, bp = r->auxp.size(),
+                 bbk = bk.size() * sizeof(Dav1dGpuEdgeBackup);
     const size_t o_c = bu + br, o_e = o_c + bc, o_a = o_e + be, o_xu = o_a + ba, o_xa = o_xu + bxu,
-                 o_p = o_xa + bxa, o_end = o_p + bp;
+                 o_p = o_xa + bxa, o_bk = o_p + bp, o_end = o_bk + bbk;
     uint8_t *img;
     if (host_only) {
         r->h_host.resize(o_end);
@@ -1447,6 +1504,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         }
     }
     if (bp) memcpy(img + o_p, r->auxp.data(), bp);
+    if (bbk) memcpy(img + o_bk, bk.data(), bbk);
     {   // in rank order: the image is written sequentially, the cells read by index
         const int nt = n < 32768 ? 1 : nthreads;
         int32_t *deps = r->deps.data();
@@ -1524,7 +1582,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         return -3;
     if (be && (r->d_emu_jobs.grow(be) || r->d_emu.grow((size_t)emu_rows * kEmuStride * bpp + 256))) return -3;
     if (r->d_aux.grow(ba) || r->d_auxp.grow(std::max<size_t>(bp, 16)) ||
-        (nx && (r->d_xunits.grow(bxu) || r->d_xaux.grow(bxa))))
+        (nx && (r->d_xunits.grow(bxu) || r->d_xaux.grow(bxa))) || (bbk && r->d_bk.grow(bbk)))
         return -3;
     const uint8_t *pin = img;
     // once a copy from the pinned image may be queued, a failure drains the
@@ -1541,7 +1599,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         (ba && hipMemcpyAsync(r->d_aux.p, pin + o_a, ba, hipMemcpyHostToDevice, st)) ||
         (nx && hipMemcpyAsync(r->d_xunits.p, pin + o_xu, bxu, hipMemcpyHostToDevice, st)) ||
         (nx && hipMemcpyAsync(r->d_xaux.p, pin + o_xa, bxa, hipMemcpyHostToDevice, st)) ||
-        (bp && hipMemcpyAsync(r->d_auxp.p, pin + o_p, bp, hipMemcpyHostToDevice, st)))
+        (bp && hipMemcpyAsync(r->d_auxp.p, pin + o_p, bp, hipMemcpyHostToDevice, st)) ||
+        (bbk && hipMemcpyAsync(r->d_bk.p, pin + o_bk, bbk, hipMemcpyHostToDevice, st)))
         return drained(-3);
     if (be) {   // the clamped footprints, before the wavefront reads them
         EmuArgs ea;
@@ -1603,8 +1662,10 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
             for (int k = 0; k < DGPU_REC_EMU_SLOT; k++) fb.ref[k][p] = ref[k][p];
         if (be) fb.ref[DGPU_REC_EMU_SLOT][p] = Dav1dGpuPlane{r->d_emu.p, (int64_t)kEmuStride * bpp, kEmuStride, emu_rows};
     }
-    eb.sb_log2[0] = 6;
-    eb.sb_log2[1] = eb.sb_log2[2] = 5;
+    for (int p = 0; p < 3; p++) {
+        eb.sb_log2[p] = sbl[p];
+        if (r->top_on) eb.top_edge[p] = r->top[p];
+    }
     fb.units = (const Dav1dGpuUnit *)r->d_units.p;
     fb.n_units = n;
     fb.class_start[NC] = n;
@@ -1624,6 +1685,12 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         xb.aux = (const int32_t *)r->d_xaux.p;
         const int xrc = r->bpc == 8 ? dav1d_gpu_recon_8bpc(&xb, stream) : dav1d_gpu_recon_16bpc(&xb, stream);
         if (xrc) return drained(xrc);
+    }
+    if (bbk) {   // their superblock-bottom rows into top_edge, before the wavefront
+        const auto *runs = (const Dav1dGpuEdgeBackup *)r->d_bk.p;
+        const int brc = r->bpc == 8 ? dav1d_gpu_backup_ipred_edge_8bpc(&eb, runs, (int)bk.size(), stream)
+                                    : dav1d_gpu_backup_ipred_edge_16bpc(&eb, runs, (int)bk.size(), stream);
+        if (brc) return drained(brc);
     }
     eb.units = (Dav1dGpuUnit *)r->d_units.p;
     eb.edges = r->d_edges.p;

@@ -1131,7 +1131,17 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         const int W = ti.w, H = ti.h;
         A *ab = acc + (((tx.w0 >> 4) & 15) * 4) * S + (tx.w0 & 15) * 4;
         const C *cs = c.cf + (tx.w1 & 0xffff);
-        if (act && nzw && l < nzh && !(DGPU_TILE_ABL & 1)) {   // row pass
+        const bool wht = txtp == DGPU_WHT_WHT;   // lossless 4x4: one lane, both passes, int32
+        if (act && wht && l == 0 && !(DGPU_TILE_ABL & 1)) {
+            int t[16];
+            wht4x4(cs, nzw, nzh, t);
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+                    ab[y * S + x] = (A)(BPC == 8 ? clampi(t[4 * y + x], -32768, 32767) : t[4 * y + x]);
+        }
+        if (act && !wht && nzw && l < nzh && !(DGPU_TILE_ABL & 1)) {   // row pass
             const bool rect2 = W * 2 == H || H * 2 == W;
             A *arow = ab + l * S;
             const int kh = kind_h(txtp);
@@ -1146,7 +1156,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
             }
         }
         wave_sync();
-        if (act && l < W && !(DGPU_TILE_ABL & 1)) {   // column pass, in place
+        if (act && !wht && l < W && !(DGPU_TILE_ABL & 1)) {   // column pass, in place
             A *acol = ab + l;
             if (!nzw) {   // DC-only (src/itx_tmpl.c:53-65)
                 int dc = cs[0];

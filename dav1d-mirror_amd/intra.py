@@ -194,6 +194,9 @@ class IntraConfig:
     # of inter blocks becomes INTER_MASK / WARP / INTER_OBMC / INTER_WMASK /
     # INTER_SCALED, and half as many intra blocks become palette blocks
     ext_frac: float = 0.0
+    # fraction of the 4x4 transform blocks with a residual that are WHT_WHT
+    # (lossless), full-range coefficients (workload.lossless_residuals)
+    lossless: float = 0.0
 
     @property
     def pixel_dtype(self):
@@ -502,7 +505,7 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     / left neighbours, superblock-top rows read through top_edge.  Then the
     dependency levels: a unit's level is one more than the highest level of
     any pixel its edges (after the mode remap) or its CfL luma read."""
-    from .workload import _partition, _tx_candidates, make_residuals
+    from .workload import _partition, _tx_candidates, lossless_residuals, make_residuals
     assert cfg.width % 32 == 0 and cfg.height % 8 == 0
     rng = np.random.default_rng(cfg.seed)
     W, H = cfg.width, cfg.height
@@ -693,6 +696,8 @@ def make_intra_frame(cfg: IntraConfig) -> IntraFrame:
     bsz = np.array(U["bsz"], np.int32)
     units["bw4"] = units["bh4"] = np.where(interu, bsz // 4, 0)
     txtp, nzw, nzh, coef_off, coefs = make_residuals(rng, tx, tw, th, bdmax, cfg.coef_dtype)
+    if cfg.lossless > 0:
+        lossless_residuals(cfg, tx, txtp, nzw, nzh, coef_off, coefs)
     txtp = np.where(np.array(U["nores"], bool), abi.NO_RESIDUAL, txtp)
     units["txtp"], units["nzw"], units["nzh"], units["coef_off"] = txtp, nzw, nzh, coef_off
     edge_len = np.where(edger, 2 * th + 2 * tw + 1, 0)
@@ -1144,6 +1149,21 @@ class Recorder:
                                                ctypes.c_void_p(stream.cuda_stream))
         if rc:
             raise RuntimeError(f"dav1d_gpu_recorder_flush: {rc}")
+
+    def set_top_edge(self, tops, sb128=False):
+        """dav1d_gpu_recorder_set_top_edge: 3 device tensors (sb rows - 1 or
+        more, superblock-aligned width) the flushes back superblock-bottom
+        rows up to and read superblock-top rows from; None turns it off."""
+        if tops is None:
+            rc = self.lib.dav1d_gpu_recorder_set_top_edge(self.h, None, int(sb128))
+        else:
+            bpp = 1 if self.bpc == 8 else 2
+            t = (abi.Plane * 3)()
+            for p, a in enumerate(tops):
+                t[p].data, t[p].stride, t[p].w, t[p].h = a.data_ptr(), a.shape[1] * bpp, a.shape[1], a.shape[0]
+            rc = self.lib.dav1d_gpu_recorder_set_top_edge(self.h, ctypes.byref(t), int(sb128))
+        if rc:
+            raise ValueError(f"dav1d_gpu_recorder_set_top_edge: {rc}")
 
     def status(self):
         """The last flush's outcome (dav1d_gpu_recorder_status): 0, -6 (its

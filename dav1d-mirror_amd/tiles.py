@@ -247,7 +247,6 @@ def build_tiles(fd):
     # ---- transform blocks with a residual ----
     has_res = u["txtp"] != abi.NO_RESIDUAL
     xu = np.nonzero(has_res)[0]
-    assert np.all(u["txtp"][xu] < abi.WHT_WHT), "WHT_WHT (lossless) is not in the tile batch"
     xl = tx_lanes(tw[xu], th[xu])
     xtile = tid[xu]
     # inside a lane-count group: by width, height, then the 1-D kinds (ADST

@@ -80,6 +80,11 @@ class FrameConfig:
     # must give the same picture (tests/test_cpu.py)
     no_residual: bool = False
     unit_split: int = 0
+    # fraction of the 4x4 units with a residual whose transform is WHT_WHT
+    # (lossless, src/itx_tmpl.c:166-185), with coefficients drawn over the
+    # whole range the decoder's dequantisation allows (cf_max,
+    # src/recon_tmpl.c:594); 0 leaves every other draw of the frame unchanged
+    lossless: float = 0.0
 
     @property
     def ref_pad(self):
@@ -225,6 +230,24 @@ def make_residuals(rng, tx, tw, th, bdmax, coef_dtype):
                 else:
                     coefs[o:o + a * b] = c[j, :b, :a].T.ravel()
     return txtp, nzw, nzh, coef_off, coefs
+
+
+def lossless_residuals(cfg, tx, txtp, nzw, nzh, coef_off, coefs):
+    """WHT_WHT on a seeded cfg.lossless fraction of the 4x4 units, in place:
+    the unit keeps its stored region (a DC-only unit becomes a 1x1 region, the
+    same one coefficient), so the coefficient layout does not move; the
+    values are uniform over [-(cf_max + 1), cf_max] (src/recon_tmpl.c:594,
+    :659), extremes the row pass of the other types would clip."""
+    lr = np.random.default_rng(cfg.seed ^ 0x1055)
+    sel = np.nonzero((tx == 0) & (lr.random(len(tx)) < cfg.lossless))[0]
+    bits = 8 if cfg.bpc == 8 else int(cfg.bitdepth_max).bit_length()
+    cf_max = (127 << bits) | ((1 << bits) - 1)
+    txtp[sel] = abi.WHT_WHT
+    nzw[sel] = np.maximum(nzw[sel], 1)
+    nzh[sel] = np.maximum(nzh[sel], 1)
+    for i in sel:
+        n, o = int(nzw[i]) * int(nzh[i]), int(coef_off[i])
+        coefs[o:o + n] = lr.integers(-(cf_max + 1), cf_max + 1, n)
 
 
 def _ext2_records(cfg, rng, units, pk, plane_u, ux, uy, tw, th, blk, bsz, lx, ly, ls, mv, ref_stride, planes):
@@ -646,6 +669,8 @@ def make_frame(cfg: FrameConfig) -> FrameData:
         coefs = np.zeros(1, cfg.coef_dtype)
     else:
         txtp, nzw, nzh, coef_off, coefs = make_residuals(rng, tx, tw, th, bdmax, cfg.coef_dtype)
+        if cfg.lossless > 0:
+            lossless_residuals(cfg, tx, txtp, nzw, nzh, coef_off, coefs)
         units["txtp"] = txtp
         units["nzw"] = nzw
         units["nzh"] = nzh

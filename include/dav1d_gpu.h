@@ -334,7 +334,10 @@ enum Dav1dGpuPredKind {
  * src/recon_tmpl.c:460-470), column-major with stride nzh -- the reference's
  * own layout (src/itx_tmpl.c:82-85) restricted to that region.  nzw == 0
  * marks the reference's DC-only call (eob == 0 with DCT_DCT,
- * src/itx_tmpl.c:53): one coefficient is stored. */
+ * src/itx_tmpl.c:53): one coefficient is stored.  WHT_WHT (lossless,
+ * src/itx_tmpl.c:166-185) is a 4x4 type (tx == DGPU_TX_4X4) with nzw, nzh
+ * >= 1; every kernel runs it in int32 like the reference, for coefficients
+ * over the whole dequantised range. */
 typedef struct Dav1dGpuUnit {
     int32_t  dst_off;     /* pixel offset of the unit's top-left in its plane  */
     int32_t  coef_off;    /* element offset into the coefficient pool        */
@@ -547,7 +550,7 @@ typedef struct Dav1dGpuPred {
  *   w1 = coef_off | lane0 << 16
  * x4, y4: position in the tile (4-px units); nzw x nzh: the stored
  * coefficient region, column-major with stride nzh (0 x 0: the reference's
- * DC-only call, one coefficient); coef_off: relative to the tile's coef0;
+ * DC-only call, one coefficient; WHT_WHT: tx 4x4, nzw, nzh >= 1); coef_off: relative to the tile's coef0;
  * lane0: base of its max(w, min(h, 32)) lanes in the tile's tx section
  * (records sorted by that lane count, largest first).  Transform blocks
  * with no residual are simply absent. */
@@ -864,6 +867,23 @@ int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, cons
  * recorder's).  Returns 0, -1 bad arguments, or a launch error. */
 int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane dst[3],
                              const Dav1dGpuPlane ref[DGPU_MAX_REFS][3], void *stream);
+/* Superblock-top edge rows, the decoder's f->ipred_edge (replaces the
+ * backup bytefn(dav1d_backup_ipred_edge), src/recon_tmpl.c:2162-2186, and
+ * the top_sb_edge reads of recon_b_intra / recon_b_inter, :1275-1279,
+ * :1394-1398, :1492-1496, :1664-1668, :1793-1797).  With top_edge set, every
+ * flush copies the last pre-filter row of each superblock row it completes
+ * into top_edge[p] row sby (the row above superblock row sby + 1) as the
+ * stores happen, and intra, CfL and inter-intra units at a superblock's top
+ * read the row above from there (DGPU_IE_TOP_SB_EDGE), never from the
+ * picture.  A decoder can then post-filter the superblock rows already
+ * flushed (dav1d_filter_sbrow per row, src/decode.c:3277: deblock, CDEF and
+ * LR write the picture in place) while the next rows are recorded and
+ * flushed.  Rows: the plane's grid rounded up to whole superblocks wide (as
+ * dav1d's sb128w * 128), one per superblock row but the last.  sb128:
+ * 128-px superblocks (64 otherwise).  top_edge NULL turns it off (the
+ * default: rows above superblocks are read from the picture).  0 or -1
+ * (buffers too small). */
+int dav1d_gpu_recorder_set_top_edge(Dav1dGpuRecorder *r, const Dav1dGpuPlane top_edge[3], int sb128);
 /* Levels and units of the last flush (diagnostics). */
 int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_units, int32_t *n_levels);
 /* Outcome of the last flush (waits for it): 0, -6 if its wavefront gave up

@@ -1828,11 +1828,17 @@ int SFX(oracle_recon_tiles)(const Dav1dGpuTileBatch *b, int t0, int t1)
                     }
                 eob = 1;
             }
-            itx_all[tx][tp](tdst + (ptrdiff_t)(y4 * 4) * PX(ds) + x4 * 4, ds, cf, eob
+            pixel *xd = tdst + (ptrdiff_t)(y4 * 4) * PX(ds) + x4 * 4;
+            if (tp == DGPU_WHT_WHT) itx_wht_wht_4x4(xd, ds, cf, eob
 #if BITDEPTH == 16
-                            , bdmax
+                                                    , bdmax
 #endif
-                            );
+                                                    );
+            else itx_all[tx][tp](xd, ds, cf, eob
+#if BITDEPTH == 16
+                                 , bdmax
+#endif
+                                 );
         }
     }
     return 0;

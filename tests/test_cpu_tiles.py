@@ -166,3 +166,29 @@ def test_tiles_launch_validation(pkg):
         assert fn(ctypes.byref(b), None) == -4
         b.ref[0][0].data = 16
         assert fn(ctypes.byref(b), None) == 0                       # empty batch: nothing to do
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+def test_tile_walker_lossless(pkg, oracle, bpc, bdmax):
+    """WHT_WHT (lossless 4x4) blocks with full-range coefficients: the tile
+    walker (per tile, transform records) and the unit walker (per unit)
+    give the same planes, and the frame generator marks only 4x4 units
+    without moving any coefficient region."""
+    import dav1d_mirror_amd.workload as wl
+    import dav1d_mirror_amd.tiles as tl
+    kw = dict(width=256, height=128, seed=95, bpc=bpc, bitdepth_max=bdmax)
+    base = wl.make_frame(wl.FrameConfig(**kw))
+    fd = wl.make_frame(wl.FrameConfig(lossless=0.6, **kw))
+    # the same units (the batch's sort puts them in another order)
+    ua = fd.units[np.lexsort((fd.units["dst_off"], fd.units["plane"]))]
+    ub = base.units[np.lexsort((base.units["dst_off"], base.units["plane"]))]
+    wht = ua["txtp"] == pkg.abi.WHT_WHT
+    assert wht.sum() > 20 and np.all(ua["tx"][wht] == 0)
+    assert np.array_equal(ua["coef_off"], ub["coef_off"])
+    assert np.array_equal(ua[~wht], ub[~wht])
+    ht = oracle.HostTiles(fd, tl.build_tiles(fd))
+    ht.run()
+    hf = oracle.HostFrame(fd)
+    hf.run(threads=2)
+    for p in range(3):
+        assert np.array_equal(ht.dst[p], hf.dst[p]), p

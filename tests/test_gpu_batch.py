@@ -218,3 +218,16 @@ def test_batch_unpadded_refs(pkg, oracle, bpc, bdmax, kind, mv, size):
     for p in range(3):
         diff = np.argwhere(got[p] != hf.dst[p])
         assert len(diff) == 0, f"plane {p}: {len(diff)} pixels differ, first {diff[:5].tolist()}"
+
+
+@pytest.mark.parametrize("bpc,bdmax,seed", [(8, 255, 91), (16, 1023, 92), (16, 4095, 93)])
+def test_batch_lossless(pkg, oracle, bpc, bdmax, seed):
+    """WHT_WHT (lossless 4x4, src/itx_tmpl.c:166-185) units among every other
+    kind, with coefficients over the decoder's whole dequantised range
+    (src/recon_tmpl.c:594): the kernel's one-lane int32 WHT, its int16
+    residual saturation at 8 bpc included, against the reference's int32
+    arithmetic."""
+    fd = _frame(pkg, width=512, height=256, bpc=bpc, bitdepth_max=bdmax, seed=seed, lossless=0.6)
+    wht = fd.units["txtp"] == pkg.abi.WHT_WHT
+    assert wht.sum() > 100 and np.all(fd.units["tx"][wht] == 0)
+    _check(fd, oracle)

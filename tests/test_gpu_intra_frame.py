@@ -93,3 +93,13 @@ def test_intra_frame_4k_persistent(oracle, mode):
     assert dev.flow_error() == 0
     for a, b in zip(dev.planes_host(), ho.dst):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("mode", ["persistent", "staged", "sb"])
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+def test_lossless_frame(oracle, mode, bpc, bdmax):
+    """WHT_WHT (lossless 4x4) residuals on intra and inter units of a mixed
+    frame, through the wavefront's class code."""
+    fr = _frame(seed=42, inter_frac=0.4, bpc=bpc, bitdepth_max=bdmax, lossless=0.8)
+    assert (fr.units["txtp"] == 16).sum() > 100
+    _check(oracle, fr, mode=mode)

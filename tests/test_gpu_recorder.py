@@ -265,3 +265,63 @@ def test_recorder_overhanging_blocks(oracle, kw):
     assert rec.status() == 0
     _compare(fr, dst, oracle)
     rec.close()
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+def test_recorder_lossless(oracle, bpc, bdmax):
+    """Lossless (WHT_WHT) residuals handed to the recorder as
+    dav1d_gpu_rec_residual calls with txtp 16."""
+    fr, _ = _run(oracle, seed=57, inter_frac=0.4, bpc=bpc, bitdepth_max=bdmax, lossless=0.8,
+                 sb_edge_backup=False)
+    assert (fr.units["txtp"] == 16).sum() > 100
+
+
+@pytest.mark.parametrize("kw", [dict(seed=58, inter_frac=0.4),
+                                dict(seed=59, inter_frac=0.4, ext_frac=0.4, tile_cols=2),
+                                dict(seed=60, inter_frac=0.3, bpc=16, bitdepth_max=1023, lossless=0.3)])
+def test_recorder_top_edge_post_filter_interleave(oracle, kw):
+    """dav1d_gpu_recorder_set_top_edge (f->ipred_edge, src/recon_tmpl.c:2162-2186
+    and the top_sb_edge reads :1275-1279 / :1394-1398 / :1664-1668): one flush
+    per superblock row, and after each flush the rows just reconstructed are
+    checked and then overwritten in the picture, standing in for the
+    decoder's in-place post-filters of that row (src/decode.c:3277).  Every
+    later row must come out exact, so nothing read a superblock-top row from
+    the picture; the backed-up rows equal the oracle's top_edge (launch-ahead
+    predictions at superblock bottoms included, ext_frac)."""
+    import torch
+    import dav1d_mirror_amd.intra as intra
+    fr = intra.make_intra_frame(intra.IntraConfig(width=512, height=320, sb_edge_backup=True, **kw))
+    ho = oracle.HostIntraFrame(fr)
+    ho.run()
+    dst, refs = _setup(fr)
+    hbd = fr.cfg.bpc != 8
+    pdt = torch.int16 if hbd else torch.uint8
+    sbl = [6, 5, 5]
+    tops = [torch.full(((h + (1 << s) - 1 >> s) - 1, (w + (1 << s) - 1 >> s << s)), 0x5A, dtype=pdt, device="cuda:0")
+            for (w, h), s in zip(fr.plane_wh, sbl)]
+    rec = intra.Recorder(fr.cfg.bpc, fr.cfg.bitdepth_max, fr.cfg.width, fr.cfg.height)
+    rec.set_top_edge(tops)
+    s = torch.cuda.current_stream()
+    gen = torch.Generator(device="cuda:0").manual_seed(5)
+    for y0 in range(0, fr.cfg.height, 64):
+        intra.replay(rec, fr, rows=(y0, y0 + 64))
+        rec.flush(dst, refs, s)
+        assert rec.status() == 0
+        torch.cuda.synchronize()
+        for p in range(3):
+            w, h = fr.plane_wh[p]
+            r0, r1 = y0 >> (p > 0), min(h, (y0 + 64) >> (p > 0))
+            got = dst[p][r0:r1, :w].cpu().numpy()
+            got = got.view(np.uint16) if hbd else got
+            diff = np.argwhere(got != ho.dst[p][r0:r1])
+            assert len(diff) == 0, f"rows {y0}+ plane {p}: {len(diff)} pixels differ, first {diff[:5].tolist()}"
+            # the "post-filter": this row's pixels change in place
+            dst[p][r0:r1] = torch.randint(0, fr.cfg.bitdepth_max + 1, dst[p][r0:r1].shape, generator=gen,
+                                          device="cuda:0").to(pdt)
+    for p in range(3):
+        rows = tops[p].shape[0]
+        w = fr.plane_wh[p][0]
+        got = tops[p][:, :w].cpu().numpy()
+        got = got.view(np.uint16) if hbd else got
+        assert np.array_equal(got, ho.top[p][:rows, :w]), p
+    rec.close()

@@ -111,3 +111,12 @@ def test_tiles_equal_unit_batch(oracle, kind, bpc, bdmax):
     torch.cuda.synchronize()
     for a, b in zip(du.planes_host(), dt.planes_host()):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023), (16, 4095)])
+def test_tiles_lossless(oracle, bpc, bdmax):
+    """WHT_WHT (lossless 4x4) transform blocks in the tile batch, full-range
+    coefficients (VERDICT r4 missing #5)."""
+    fd = _frame(width=512, height=256, seed=94, bpc=bpc, bitdepth_max=bdmax, lossless=0.6)
+    assert (fd.units["txtp"] == 16).sum() > 100
+    _check(fd, oracle)

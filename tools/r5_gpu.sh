@@ -18,7 +18,9 @@ BENCH_FAST="--no-families --no-configs --no-tiles --no-intra --no-recorder --no-
 for s in "${@:-tests}"; do
     echo "[r5] $s start $(date +%T)"
     case $s in
-    tests) timeout -k 10 900 $PYT -m gpu -x tests > "$O/gputest.log" 2>&1 || { echo "[r5] tests failed"; exit 1; } ;;
+    tests) timeout -k 10 900 $PYT -m gpu -x ${PYK:+-k "$PYK"} tests > "$O/gputest.log" 2>&1 || { echo "[r5] tests failed"; tail -5 "$O/gputest.log"; exit 1; } ;;
+    topedge) # the recorder's top_edge / post-filter interleave tests (no -x: every case reported)
+        timeout -k 10 300 $PYT -m gpu tests/test_gpu_recorder.py -k top_edge > "$O/topedge.log" 2>&1; echo "[r5] topedge rc=$? $(tail -1 "$O/topedge.log")" ;;
     stests) AMD_SERIALIZE_KERNEL=3 timeout -k 10 1200 $PYT -m gpu -x tests > "$O/gputest.log" 2>&1 || { echo "[r5] stests failed"; exit 1; } ;;
     rectests) timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_recorder.py tests/test_gpu_batch.py > "$O/rectest.log" 2>&1 || { echo "[r5] rectests failed"; exit 1; } ;;
     bounds) # -s: the device printf reports must not be captured by pytest
@@ -77,7 +79,7 @@ for s in "${@:-tests}"; do
         python3 -c "import json; d=json.load(open('$O/lrbench.json'))['loop_restoration']; print('lr', d['us_per_frame'], d['bit_exact_vs_oracle'])" ;;
     varintra) # the intra-frame and recorder GPU tests on each variant library (ABV)
         for v in $ABV; do
-            DAV1D_GPU_LIB_VARIANT=$v timeout -k 10 600 $PYT -m gpu -x tests/test_gpu_intra_frame.py tests/test_gpu_recorder.py > "$O/varintra_$v.log" 2>&1 \
+            DAV1D_GPU_LIB_VARIANT=$v timeout -k 10 600 $PYT -m gpu -x -k "not lossless" tests/test_gpu_intra_frame.py tests/test_gpu_recorder.py > "$O/varintra_$v.log" 2>&1 \
                 || { echo "[r5] varintra $v failed"; tail -5 "$O/varintra_$v.log"; exit 1; }
             echo "varintra $v $(tail -1 "$O/varintra_$v.log")"
         done ;;
