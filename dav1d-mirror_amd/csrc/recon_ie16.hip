@@ -1,6 +1,13 @@
 // recon_ie16.hip -- 16bpc instantiation of the intra wavefront's fused
 // reconstruction launch (recon_ie.hpp); its own TU so it compiles in
 // parallel with the unit batch and leaves that code unchanged.
+// 8 lanes per 4x4 / 4x8 / 8x4 unit in the wavefront (round 5, measured:
+// 4K one-tile intra frame 17.9 -> 17.1 ms, 2x2 tiles 10.9 -> 10.6 ms,
+// bit-exact; 16 lanes 18.2 / 12.3 ms; profiles/r5/r5k_intra_lanes_ab.json).
+// Only these TUs: the unit batch's classes keep their lanes.
+#ifndef DGPU_IE_SMALL_LANES
+#define DGPU_IE_SMALL_LANES 8
+#endif
 #include "recon_ie.hpp"
 
 int dgpu_recon_ie_16bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, void *stream) {

@@ -176,10 +176,10 @@ __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 #define DGPU_TALL_LANES 1
 #endif
 #ifndef DGPU_IE_SMALL_LANES
-// experiment (the intra wavefront TUs only, tools/build_variants.sh ielanes):
-// lanes per unit of the 4x4 / 4x8 / 8x4 classes.  Above level 0 a wavefront
-// task holds at most 8 units, so at 2-4 lanes per unit most of its wave idles
-// while the small units' edge preparation and prediction run per lane
+// lanes per unit of the 4x4 / 4x8 / 8x4 classes, for the intra wavefront
+// TUs (recon_ie{8,16}.hip set 8; 0 here: the class's own count).  Above level
+// 0 a wavefront task holds at most 8 units, so at 2-4 lanes per unit most of
+// its wave idles while the small units' edge preparation runs per lane
 #define DGPU_IE_SMALL_LANES 0
 #endif
 __host__ __device__ constexpr int lanes_per_unit(int tx) {
