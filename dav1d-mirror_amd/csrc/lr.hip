@@ -47,10 +47,20 @@ template <int BPC> struct LrArgs {
     const P *left;    // [h][4]; null: the columns left of the unit are src's
     int ss, ds, ts, bs;
     int w, h, edges, kind, bdmax;   // kind: 0 wiener, 1 sgr 5x5, 2 sgr 3x3, 3 mix
+    int vec;                        // every pointer and pitch 16-byte aligned (DGPU_LR_VEC)
     Dav1dGpuLrParams prm;
 };
 
 constexpr int kLrVH = 66;   // A / B rows: unit rows -1..64
+
+// DGPU_LR_VEC (bits): full 32-column strips on 16-byte-aligned planes move
+// their pixels in 16-byte pieces instead of one pixel per lane: 1 the copied
+// (unrestored) strips, 2 the tile's 32 interior columns (the 3 + 3 padding
+// columns keep the per-pixel padding() code), 4 the outputs (staged in LDS,
+// then stored whole rows)
+#ifndef DGPU_LR_VEC
+#define DGPU_LR_VEC 0
+#endif
 
 // A / B of selfguided_filter (:373-392) from one position's box sum and sum
 // of squares (n = 25 or 9), with the reference's unsigned arithmetic
@@ -67,6 +77,20 @@ __device__ __forceinline__ void lr_ab_sums(int sum, int sumsq, unsigned s, int b
     B = (int)x;
 }
 
+// DGPU_LR_VEC & 4: the strip's h x 32 outputs, staged in LDS at a 32-pixel
+// pitch by every thread, to the picture in 16-byte pieces
+template <int BPC>
+__device__ __forceinline__ void lr_store_rows(const LrArgs<BPC> &a, int x0, const typename Px<BPC>::pixel *o) {
+    using P = typename Px<BPC>::pixel;
+    constexpr int N = 16 / (int)sizeof(P), PR = kLrSW / N;
+    __syncthreads();
+    for (int t = threadIdx.x; t < a.h * PR; t += 256) {
+        const int j = t / PR, k = t % PR;
+        *reinterpret_cast<uint4 *>(a.dst + (size_t)j * a.ds + x0 + k * N) =
+            reinterpret_cast<const uint4 *>(o + j * kLrSW)[k];
+    }
+}
+
 // One 32-column strip (columns x0.. of the unit) of one stripe.
 template <int BPC>
 __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
@@ -75,7 +99,7 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     // 16-bit tiles and scratch where the values fit (pixels, Wiener's clipped
     // horizontal sums, 5-row box sums, B = x_by_x <= 255): 31.8 KB, five
     // workgroups per CU
-    __shared__ int16_t T[kLrTH][kLrTW];
+    __shared__ __attribute__((aligned(16))) int16_t T[kLrTH][kLrTW];
     // 3x3 A / B at unit rows -1..h (every row), strip columns -1..sw; the
     // Wiener units' horizontal pass reuses the A array
     // (32-bit A: 16-bit A arrays at 8 bit -- A <= 65089 fits -- gave 15.7 KB
@@ -95,7 +119,59 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     static_assert(kLrTH * kLrSW * 2 <= (int)sizeof(AA), "HOR fits the A array");
     const int sw = min(kLrSW, a.w - x0), h = a.h;
     const int bd8 = bits_of(a.bdmax) - 8;
-    {   // a thread per tile column and sixth of the rows: the column's
+    // a full strip on aligned planes (workgroup-uniform)
+    const bool vec = a.vec && sw == kLrSW;
+    if ((DGPU_LR_VEC & 2) && vec) {   // the 32 interior columns read no padding: 16-byte row pieces
+        constexpr int PR = kLrSW * (int)sizeof(P) / 16, NV = (kLrTH * PR + 255) / 256;   // pieces per row
+        const bool ht = a.edges & DGPU_LR_HAVE_TOP, hb = a.edges & DGPU_LR_HAVE_BOTTOM;
+        uint4 pv[NV];
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            const int t = threadIdx.x + 256 * i, r = t / PR, k = t % PR;
+            if (r < h + 6) {
+                const int j = min(max(r - 3, 0), h - 1);
+                const P *p = a.src + (ptrdiff_t)j * a.ss + x0;
+                if (r < 3 && ht) p = a.top + (r == 2) * a.ts + x0;
+                if (r >= h + 3 && hb) p = a.bot + (r > h + 3) * a.bs + x0;
+                pv[i] = *reinterpret_cast<const uint4 *>(p + k * (16 / (int)sizeof(P)));
+            }
+        }
+        // the padding columns 0-2 and 35-37, a thread per (row, column)
+        constexpr int NH = (kLrTH * 6 + 255) / 256;
+        const bool hl = a.edges & DGPU_LR_HAVE_LEFT, hr = a.edges & DGPU_LR_HAVE_RIGHT;
+        int hv[NH];
+#pragma unroll
+        for (int i = 0; i < NH; i++) {
+            const int t = threadIdx.x + 256 * i, r = t / 6, e = t % 6, c = e < 3 ? e : kLrSW + e;
+            int cc = x0 + c;
+            if (!hr && cc >= a.w + 3) cc = a.w + 2;
+            if (!hl && cc < 3) cc = 3;
+            const int x = cc - 3;
+            hv[i] = 0;
+            if (r < h + 6) {
+                const int j = min(max(r - 3, 0), h - 1);
+                const P *p = x < 0 && a.left ? a.left + j * 4 + x + 4 : a.src + (ptrdiff_t)j * a.ss + x;
+                if (r < 3 && ht) p = a.top + (r == 2) * a.ts + x;
+                if (r >= h + 3 && hb) p = a.bot + (r > h + 3) * a.bs + x;
+                hv[i] = *p;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            const int t = threadIdx.x + 256 * i, r = t / PR, k = t % PR;
+            if (r < h + 6) {
+                constexpr int N = 16 / (int)sizeof(P);
+                const P *q = reinterpret_cast<const P *>(&pv[i]);
+#pragma unroll
+                for (int m = 0; m < N; m++) T[r][3 + k * N + m] = (int16_t)q[m];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NH; i++) {
+            const int t = threadIdx.x + 256 * i, r = t / 6, e = t % 6, c = e < 3 ? e : kLrSW + e;
+            if (r < h + 6) T[r][c] = (int16_t)hv[i];
+        }
+    } else {   // a thread per tile column and sixth of the rows: the column's
         // padding() case once, then per row only the row's source; every
         // load first, then the LDS writes
         constexpr int RG = 256 / kLrTW, NR = (kLrTH + RG - 1) / RG;   // 6 row groups, 12 rows each
@@ -164,11 +240,14 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
                 int sum = -round_offset;
 #pragma unroll
                 for (int t = 0; t < 7; t++) sum += hv[t] * a.prm.filter[1][t];
-                a.dst[(size_t)j * a.ds + x0 + wi] = (P)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, a.bdmax);
+                const P o = (P)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, a.bdmax);
+                if ((DGPU_LR_VEC & 4) && vec) reinterpret_cast<P *>(&T[0][0])[j * kLrSW + wi] = o;   // T is free here
+                else a.dst[(size_t)j * a.ds + x0 + wi] = o;
 #pragma unroll
                 for (int t = 0; t < 6; t++) hv[t] = hv[t + 1];
             }
         }
+        if ((DGPU_LR_VEC & 4) && vec) lr_store_rows<BPC>(a, x0, reinterpret_cast<const P *>(&T[0][0]));
         return;
     }
     // ---- self-guided (selfguided_filter, :349-440), both radii in one pass ----
@@ -231,11 +310,11 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     // neighbour weights follow:
     //   EIGHT: 4 s1 + 3 (s0 + s2) + c0 + c2;  SIX (even j): 5 (s0 + s2) +
     //   c0 + c2;  odd j: 5 s1 + c1  (rows 0/1/2 = unit rows j-1, j, j+1)
+    int v[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) v[m] = 0;
     if (wj0 < h && wi < sw) {
         const int ii = wi + 1;
-        int v[8];
-#pragma unroll
-        for (int m = 0; m < 8; m++) v[m] = 0;
         auto row = [&](const AT *ar, const uint8_t *br, int &sa, int &ca, int &sb, int &cb) {
             const int a0 = ar[ii - 1], a1 = ar[ii], a2 = ar[ii + 1];
             const int b0 = br[ii - 1], b1 = br[ii], b2 = br[ii + 1];
@@ -294,9 +373,21 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
         for (int r = 0; r < 8; r++) {
             const int j = wj0 + r;
             if (r >= wrpt || j >= h) break;
-            a.dst[(size_t)j * a.ds + x0 + wi] =
-                (P)clampi(T[j + 3][wi + 3] + ((v[r] + (1 << 10)) >> 11), 0, a.bdmax);
+            v[r] = clampi(T[j + 3][wi + 3] + ((v[r] + (1 << 10)) >> 11), 0, a.bdmax);
+            if (!((DGPU_LR_VEC & 4) && vec)) a.dst[(size_t)j * a.ds + x0 + wi] = (P)v[r];
         }
+    }
+    if ((DGPU_LR_VEC & 4) && vec) {   // through T once every thread has read its pixels from it
+        __syncthreads();
+        if (wj0 < h && wi < sw) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const int j = wj0 + r;
+                if (r >= wrpt || j >= h) break;
+                reinterpret_cast<P *>(&T[0][0])[j * kLrSW + wi] = (P)v[r];
+            }
+        }
+        lr_store_rows<BPC>(a, x0, reinterpret_cast<const P *>(&T[0][0]));
     }
 }
 
@@ -315,6 +406,7 @@ template <int BPC> struct LrFrameArgs {
     int is[3], ls[3], os[3], w[3], h[3], rows[3], cols[3], log2[3], restore[3], ss_ver[3];
     int xb0, xb01;   // strip blocks of plane 0, of planes 0 + 1 (the grid has no empty chroma columns)
     int sb128, bdmax;
+    int vec;         // every plane pointer and pitch 16-byte aligned (DGPU_LR_VEC)
 };
 
 // lr_stripe's filter parameters (src/lr_apply_tmpl.c:51-80); kind 0 wiener,
@@ -371,6 +463,22 @@ __global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     P *dst = f.out[pl] + (size_t)y0 * f.os[pl];
     if (!f.restore[pl] || u.type == 0 || ((DGPU_LR_ABL & 1) && u.type > 2) || ((DGPU_LR_ABL & 2) && u.type == 2)) {   // copied
         const int sw = min(kLrSW, w - xs), n = (y1 - y0) * kLrSW;   // <= 64 rows x 32
+        if ((DGPU_LR_VEC & 1) && f.vec && sw == kLrSW) {   // 16-byte pieces, loads first
+            constexpr int N = 16 / (int)sizeof(P), PR = kLrSW / N, NV = (64 * PR + 255) / 256;
+            const int nv = (y1 - y0) * PR;
+            uint4 cv[NV];
+#pragma unroll
+            for (int m = 0; m < NV; m++) {
+                const int t = threadIdx.x + 256 * m;
+                if (t < nv) cv[m] = *reinterpret_cast<const uint4 *>(src + (size_t)(t / PR) * f.is[pl] + xs + (t % PR) * N);
+            }
+#pragma unroll
+            for (int m = 0; m < NV; m++) {
+                const int t = threadIdx.x + 256 * m;
+                if (t < nv) *reinterpret_cast<uint4 *>(dst + (size_t)(t / PR) * f.os[pl] + xs + (t % PR) * N) = cv[m];
+            }
+            return;
+        }
         constexpr int NC = (64 * kLrSW + 255) / 256;
         P cv[NC];
 #pragma unroll
@@ -403,6 +511,7 @@ __global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     a.w = ux1 - ux0;
     a.h = y1 - y0;
     a.bdmax = f.bdmax;
+    a.vec = f.vec;
     a.kind = lr_params(u, BPC != 8, a.prm);
     lr_strip<BPC>(a, xs - ux0);
 }
@@ -440,6 +549,12 @@ static int launch_lr_frame(const Dav1dGpuLrFrame *F, hipStream_t stream) {
     }
     f.sb128 = F->sb128;
     f.bdmax = BPC == 8 ? 255 : F->bitdepth_max;
+    f.vec = 1;
+    for (int p = 0; p < np; p++) {
+        auto al = [](const void *q, int64_t pitch) { return q && !((uintptr_t)q & 15) && !(pitch & 15); };
+        f.vec &= al(F->in[p].data, F->in[p].stride) && al(F->out[p].data, F->out[p].stride) &&
+                 (!f.restore[p] || al(F->lpf[p].data, F->lpf[p].stride));
+    }
     const int stripes = (maxh + 8 + 63) / 64 + 1;
     int xb[3] = {0, 0, 0};
     for (int p = 0; p < np; p++) xb[p] = (f.w[p] + kLrSW - 1) / kLrSW;

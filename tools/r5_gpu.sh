@@ -83,6 +83,17 @@ for s in "${@:-tests}"; do
                 || { echo "[r5] varintra $v failed"; tail -5 "$O/varintra_$v.log"; exit 1; }
             echo "varintra $v $(tail -1 "$O/varintra_$v.log")"
         done ;;
+    ablr) # the LR frame tests and bench leg per variant library (ABV), base first
+        for v in base $ABV; do
+            if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
+            timeout -k 10 400 $PYT -m gpu -x tests/test_gpu_lr.py tests/test_gpu_chain.py > "$O/ablr_test_$v.log" 2>&1 \
+                || { echo "[r5] ablr tests $v failed"; tail -5 "$O/ablr_test_$v.log"; exit 1; }
+            timeout -k 10 300 python -u bench.py --steps 100 --no-families --no-configs --no-tiles --no-intra --no-recorder \
+                --no-grain --no-cdef --no-superres --no-lpf --no-cpu > "$O/ablr_$v.json" 2> "$O/ablr_$v.log" \
+                || { echo "[r5] ablr bench $v failed"; exit 1; }
+            python3 -c "import json; d=json.load(open('$O/ablr_$v.json'))['loop_restoration']; print('ablr $v', d['us_per_frame'], d['bit_exact_vs_oracle'], '$(tail -1 "$O/ablr_test_$v.log" | tr -d =)')"
+        done
+        unset DAV1D_GPU_LIB_VARIANT ;;
     abintra) # the intra wavefront bench leg per variant library (ABV): 1-tile / 2x2 ms per 4K frame, bit-exact
         for v in base $ABV; do
             if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
