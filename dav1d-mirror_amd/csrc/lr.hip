@@ -59,7 +59,13 @@ constexpr int kLrVH = 66;   // A / B rows: unit rows -1..64
 // columns keep the per-pixel padding() code), 4 the outputs (staged in LDS,
 // then stored whole rows)
 #ifndef DGPU_LR_VEC
-#define DGPU_LR_VEC 0
+#define DGPU_LR_VEC 3   // (4, the LDS-staged outputs, measured slower: two more barriers)
+#endif
+// DGPU_LR_PF (bits, experiment): the self-guided A / B loop 1 issues the
+// next tile row's LDS reads before the current row's arithmetic, 2 is
+// unrolled by two
+#ifndef DGPU_LR_PF
+#define DGPU_LR_PF 0
 #endif
 
 // A / B of selfguided_filter (:373-392) from one position's box sum and sum
@@ -279,12 +285,30 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
 #pragma unroll
             for (int k = 0; k < 4; k++) hrow(jj0 + k, h5[k + 1], q5[k + 1], h3[k + 1], q3[k + 1]);
             const unsigned s0 = a.prm.sgr.s0, s1 = a.prm.sgr.s1;
+            int nx[5];   // DGPU_LR_PF & 1: tile row jj + 4, read one iteration ahead
+            if (DGPU_LR_PF & 1)
+#pragma unroll
+                for (int k = 0; k < 5; k++) nx[k] = T[jj0 + 4][c - 2 + k];
+#if DGPU_LR_PF & 2
+#pragma unroll 2
+#endif
             for (int jj = jj0; jj < jj1; jj++) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     h5[k] = h5[k + 1], q5[k] = q5[k + 1], h3[k] = h3[k + 1], q3[k] = q3[k + 1];
                 }
-                hrow(jj + 4, h5[4], q5[4], h3[4], q3[4]);
+                if (DGPU_LR_PF & 1) {
+                    const int p0 = nx[0], p1 = nx[1], p2 = nx[2], p3 = nx[3], p4 = nx[4];
+                    if (jj + 1 < jj1)
+#pragma unroll
+                        for (int k = 0; k < 5; k++) nx[k] = T[jj + 5][c - 2 + k];
+                    h3[4] = p1 + p2 + p3;
+                    q3[4] = p1 * p1 + p2 * p2 + p3 * p3;
+                    h5[4] = h3[4] + p0 + p4;
+                    q5[4] = q3[4] + p0 * p0 + p4 * p4;
+                } else {
+                    hrow(jj + 4, h5[4], q5[4], h3[4], q3[4]);
+                }
                 if (do3) {   // n = 9: rows jj + 1 .. jj + 3 of the window
                     const int sum = h3[1] + h3[2] + h3[3], sumsq = q3[1] + q3[2] + q3[3];
                     int A, B;
