@@ -35,7 +35,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         t1|t2|t4|t8|t16|t3|t6|t7|t15|t31) TUS=tile8 build $v -DDGPU_TILE_ABL=${v#t} ;;
         ttrace) TUS=tile8 build ttrace -DDGPU_TILE_TRACE=1 ;;
         twpe2|twpe4|twpe5) TUS=tile8 build $v -DDGPU_TILE_WPE=${v#twpe} ;;
-        cdefw6|cdefw7) TUS=cdef build $v -DDGPU_CDEF_WPE=${v#cdefw} ;;
+        cdefw6|cdefw7|cdefw8) TUS=cdef build $v -DDGPU_CDEF_WPE=${v#cdefw} ;;
         cdefa1|cdefa2|cdefa3) TUS=cdef build $v -DDGPU_CDEF_ABL=${v#cdefa} ;;
         lra1|lra2|lra3) TUS=lr build $v -DDGPU_LR_ABL=${v#lra} ;;
         lrv1|lrv2|lrv3|lrv4|lrv5|lrv6|lrv7) TUS=lr build $v -DDGPU_LR_VEC=${v#lrv} ;;

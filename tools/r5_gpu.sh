@@ -94,6 +94,24 @@ for s in "${@:-tests}"; do
             python3 -c "import json; d=json.load(open('$O/ablr_$v.json'))['loop_restoration']; print('ablr $v', d['us_per_frame'], d['bit_exact_vs_oracle'], '$(tail -1 "$O/ablr_test_$v.log" | tr -d =)')"
         done
         unset DAV1D_GPU_LIB_VARIANT ;;
+    abcdef) # the CDEF frame tests and bench leg per variant library (ABV), base first
+        for v in base $ABV; do
+            if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
+            timeout -k 10 400 $PYT -m gpu -x tests/test_gpu_cdef.py > "$O/abcdef_test_$v.log" 2>&1 \
+                || { echo "[r5] abcdef tests $v failed"; tail -5 "$O/abcdef_test_$v.log"; exit 1; }
+            timeout -k 10 300 python -u bench.py --steps 100 --no-families --no-configs --no-tiles --no-intra --no-recorder \
+                --no-grain --no-lr --no-superres --no-lpf --no-cpu > "$O/abcdef_$v.json" 2> "$O/abcdef_$v.log" \
+                || { echo "[r5] abcdef bench $v failed"; exit 1; }
+            python3 -c "import json; d=json.load(open('$O/abcdef_$v.json'))['cdef']; print('abcdef $v', d['us_per_frame'], d['bit_exact_vs_oracle'], '$(tail -1 "$O/abcdef_test_$v.log" | tr -d =)')"
+        done
+        unset DAV1D_GPU_LIB_VARIANT ;;
+    flowunits) # the wavefront's units-per-task cap above level 0 (DAV1D_GPU_FLOW_UNITS), 4K intra frames
+        for U in ${FLOWU:-4 8 16}; do
+            DAV1D_GPU_FLOW_UNITS=$U timeout -k 10 300 python -u bench.py --steps 20 --no-families --no-configs --no-tiles --no-recorder --no-grain \
+                --no-cdef --no-superres --no-lpf --no-lr --no-cpu --no-check > "$O/flowunits_$U.json" 2> "$O/flowunits_$U.log" \
+                || { echo "[r5] flowunits $U failed"; exit 1; }
+            python3 -c "import json; d=json.load(open('$O/flowunits_$U.json'))['intra_wavefront']; print('flowunits $U', d['1_tile']['ms_per_frame'], d['1_tile']['bit_exact_vs_oracle'], d['2x2_tiles']['ms_per_frame'], d['2x2_tiles']['bit_exact_vs_oracle'])"
+        done ;;
     abintra) # the intra wavefront bench leg per variant library (ABV): 1-tile / 2x2 ms per 4K frame, bit-exact
         for v in base $ABV; do
             if [ "$v" = base ]; then unset DAV1D_GPU_LIB_VARIANT; else export DAV1D_GPU_LIB_VARIANT=$v; fi
