@@ -175,6 +175,9 @@ __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 #ifndef DGPU_TALL_LANES
 #define DGPU_TALL_LANES 1
 #endif
+#ifndef DGPU_ST8
+#define DGPU_ST8 0
+#endif
 #ifndef DGPU_IE_SMALL_LANES
 // lanes per unit of the 4x4 / 4x8 / 8x4 classes, for the intra wavefront
 // TUs (recon_ie{8,16}.hip set 8; 0 here: the class's own count).  Above level
@@ -1738,6 +1741,9 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         if (pti.top[plane] && (y1 & ((1 << sbl) - 1)) == 0 && sby < pti.top_rows[plane])
             bkrow = pti.top[plane] + (size_t)sby * pti.top_stride[plane] + rec.x4 * 4;
     }
+    // DGPU_ST8 (experiment): neighbouring lanes (quads q, q + 1 of one task
+    // row pair) trade halves so each stores one 8-byte row piece
+    constexpr bool ST8 = DGPU_ST8 && !GATHER && !WARPK && BPC == 8 && QW >= 2 && G % 2 == 0 && !DGPU_ABL_STORE;
     auto emit = [&](int j, int q, const int *pv) {   // + residual, clip, store 2 rows of 4
         int rv[8];
         if (haveres) {
@@ -1757,6 +1763,25 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         } else {
 #pragma unroll
             for (int i = 0; i < 8; i++) rv[i] = dcres;
+        }
+        if constexpr (ST8) {   // DGPU_ST8: one 8-byte row piece per lane of a (q, q + 1) pair
+            uint32_t d[2];
+#pragma unroll
+            for (int rr = 0; rr < 2; rr++) {
+                const int o0 = clampi(pv[4 * rr + 0] + rv[4 * rr + 0], 0, bdmax);
+                const int o1 = clampi(pv[4 * rr + 1] + rv[4 * rr + 1], 0, bdmax);
+                const int o2 = clampi(pv[4 * rr + 2] + rv[4 * rr + 2], 0, bdmax);
+                const int o3 = clampi(pv[4 * rr + 3] + rv[4 * rr + 3], 0, bdmax);
+                d[rr] = (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24;
+            }
+            // q and l have the same parity (QW and G even): the even lane
+            // stores row 2j of both quads, the odd lane row 2j + 1; each
+            // sends the other the half it stores (DPP quad_perm [1, 0, 3, 2])
+            const bool odd = l & 1;
+            const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? d[0] : d[1]), 0xB1, 0xF, 0xF, false);
+            P *row = dstp + __mul24(2 * j + (int)odd, ds) + 4 * (q & ~1);
+            gst<u32x2>(row, odd ? u32x2{got, d[1]} : u32x2{d[0], got});
+            return;
         }
 #pragma unroll
         for (int rr = 0; rr < 2; rr++) {
