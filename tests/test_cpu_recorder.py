@@ -288,3 +288,77 @@ def test_recorder_rejects_overlapping_blocks(pkg):
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
     got = dict(line.split() for line in r.stdout.splitlines() if len(line.split()) == 2)
     assert got == {"disjoint": "0", "overlap": "-1", "same": "-1"}, r.stdout
+
+
+_TOP_EDGE_CHILD = r"""
+import ctypes, os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import __graft_entry__ as ge
+ge.load_package()
+import dav1d_mirror_amd.abi as abi
+import dav1d_mirror_amd.intra as intra
+out = sys.argv[2]
+L = abi.load_lib()
+res = []
+for kw in (dict(seed=71, width=512, height=320, inter_frac=0.4, tile_cols=2, tile_rows=2),
+           dict(seed=72, width=640, height=384, sb_log2=7, cfl_frac=1.0)):
+    fr = intra.make_intra_frame(intra.IntraConfig(sb_edge_backup=True, **kw))
+    rec = intra.Recorder(8, 255, fr.cfg.width, fr.cfg.height)
+    d = (abi.Plane * 3)()
+    r = ((abi.Plane * 3) * abi.MAX_REFS)()
+    for p, (w, h) in enumerate(fr.plane_wh):
+        d[p].data, d[p].stride, d[p].w, d[p].h = 0x1000, w + 64, w + 64, h + 64
+        for k in range(2):
+            r[k][p].data, r[k][p].stride, r[k][p].w, r[k][p].h = 0x1000, w, w, h
+    sbl = fr.cfg.sb_log2
+    t = (abi.Plane * 3)()
+    for p, (w, h) in enumerate(fr.plane_wh):
+        s = sbl - (p > 0)
+        t[p].data, t[p].w, t[p].h = 0x1000, ((w + (1 << s) - 1) >> s) << s, ((h + (1 << s) - 1) >> s) - 1
+        t[p].stride = t[p].w
+    small = (abi.Plane * 3)(*t)
+    small[1].h = t[1].h - 1
+    assert L.dav1d_gpu_recorder_set_top_edge(rec.h, ctypes.byref(small), int(sbl == 7)) == -1   # too few rows
+    for on in (False, True):
+        assert L.dav1d_gpu_recorder_set_top_edge(rec.h, ctypes.byref(t) if on else None, int(sbl == 7)) == 0
+        if os.path.exists(out):
+            os.remove(out)
+        intra.replay(rec, fr)
+        assert L.dav1d_gpu_recorder_flush(rec.h, ctypes.byref(d), ctypes.byref(r), None) == 0
+        b = open(out, "rb").read()
+        n = int(np.frombuffer(b[:8], "<i8")[0])
+        units = np.frombuffer(b[32:32 + 32 * n], abi.UNIT_DTYPE)
+        recs = np.frombuffer(b[32 + 32 * n:32 + 48 * n], abi.INTRA_EDGE_DTYPE)
+        edged = np.isin(units["pred"], (abi.PRED_INTRA, abi.PRED_CFL, abi.PRED_INTER_INTRA))
+        got = {(int(p), int(x), int(y)): int(f) for p, x, y, f in
+               zip(units["plane"][edged], recs["x4"][edged], recs["y4"][edged], recs["flags"][edged])}
+        pe = np.isin(fr.units["pred"], (abi.PRED_INTRA, abi.PRED_CFL, abi.PRED_INTER_INTRA))
+        pr = fr.recs[np.argsort(fr.recs["unit"])]   # by unit index
+        want = {(int(p), int(x), int(y)): int(f) for p, x, y, f in
+                zip(fr.units["plane"][pe], pr["x4"][pe], pr["y4"][pe], pr["flags"][pe])}
+        assert set(got) == set(want), (len(got), len(want))
+        top = abi.IE_TOP_SB_EDGE
+        bad = [k for k in want if (got[k] & top) != ((want[k] & top) if on else 0)]
+        assert not bad, (on, bad[:5])
+        res.append((on, sum(1 for k in got if got[k] & top)))
+    rec.close()
+print(res)
+assert all(c > 0 for on, c in res if on) and all(c == 0 for on, c in res if not on)
+print("ok")
+"""
+
+
+def test_recorder_top_edge_flags(pkg, tmp_path):
+    """dav1d_gpu_recorder_set_top_edge: host-only flushes (no device) of
+    mixed and all-CfL frames, 64- and 128-px superblocks, 2x2 tiles; every
+    intra, CfL and inter-intra edge record of the upload image carries
+    DGPU_IE_TOP_SB_EDGE exactly where the frame generator's model of
+    recon_tmpl.c:1276 / :1395 / :1665 puts it (a transform block at a
+    superblock's top with a top neighbour in its tile), and none without top
+    edges; a top_edge plane with too few rows is refused."""
+    out = tmp_path / "dump.bin"
+    env = dict(os.environ, DAV1D_GPU_REC_HOSTONLY="1", DAV1D_GPU_REC_DUMP=str(out))
+    r = subprocess.run(["python3", "-c", _TOP_EDGE_CHILD, ROOT, str(out)], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
