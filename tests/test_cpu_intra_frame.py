@@ -167,6 +167,8 @@ def _flow_tasks_py(pkg, fr, groups, cap=8):
     lanes = {}
     for t, (tw, th) in enumerate(abi.TX_WH):
         lanes[t] = 64 if tw * th >= 1024 else tall.get((tw, th), min(max(min(tw * th // 8, max(tw, min(th, 32))), 2), 64))
+        if tw * th <= 32:   # the wavefront TUs give 4x4 / 4x8 / 8x4 units 8 lanes (recon_ie{8,16}.hip)
+            lanes[t] = 8
     n = 0
     for lv in range(fr.n_levels):
         cs = fr.class_start[lv]
