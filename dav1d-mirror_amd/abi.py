@@ -181,7 +181,8 @@ class CdefFrame(ctypes.Structure):
     """Dav1dGpuCdefFrame: one frame of bytefn(dav1d_cdef_brow) work."""
     _fields_ = [("in_", Plane * 3), ("out", Plane * 3), ("cdef_idx", ctypes.c_void_p), ("noskip", ctypes.c_void_p),
                 ("layout", ctypes.c_int32), ("bitdepth_max", ctypes.c_int32), ("damping", ctypes.c_int32),
-                ("pad_", ctypes.c_int32), ("y_strength", ctypes.c_uint8 * 8), ("uv_strength", ctypes.c_uint8 * 8)]
+                ("pad_", ctypes.c_int32), ("y_strength", ctypes.c_uint8 * 8), ("uv_strength", ctypes.c_uint8 * 8),
+                ("row_start", ctypes.c_int32), ("row_end", ctypes.c_int32)]
 
 
 class FilterLUT(ctypes.Structure):
@@ -193,7 +194,8 @@ class LoopFilterFrame(ctypes.Structure):
     """Dav1dGpuLoopFilterFrame: one frame of deblocking."""
     _fields_ = [("pic", Plane * 3), ("masks", ctypes.c_void_p), ("level", ctypes.c_void_p),
                 ("b4_stride", ctypes.c_int64), ("lut", FilterLUT), ("layout", ctypes.c_int32),
-                ("bitdepth_max", ctypes.c_int32), ("filter_uv", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("bitdepth_max", ctypes.c_int32), ("filter_uv", ctypes.c_int32), ("row_start", ctypes.c_int32),
+                ("row_end", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
 class _LrSgr(ctypes.Structure):
@@ -215,7 +217,8 @@ class LrFrame(ctypes.Structure):
     _fields_ = [("in_", Plane * 3), ("lpf", Plane * 3), ("out", Plane * 3), ("units", ctypes.c_void_p * 3),
                 ("unit_rows", ctypes.c_int32 * 3), ("unit_cols", ctypes.c_int32 * 3),
                 ("unit_size_log2", ctypes.c_int32 * 2), ("layout", ctypes.c_int32), ("bitdepth_max", ctypes.c_int32),
-                ("sb128", ctypes.c_int32), ("restore_planes", ctypes.c_int32)]
+                ("sb128", ctypes.c_int32), ("restore_planes", ctypes.c_int32), ("row_start", ctypes.c_int32),
+                ("row_end", ctypes.c_int32)]
 
 
 class ResizeFrame(ctypes.Structure):   # Dav1dGpuResizeFrame

@@ -304,6 +304,7 @@ template <int BPC> struct CdefArgs {
     const uint8_t *noskip;
     int gw, gh;                // luma grid (8x8 blocks) in pixels
     int sbw, sbh, b8w, b8h;
+    int sby0, sbr;             // the superblock rows run: [sby0, sby0 + sbr)
     int bdmax, damping;
     uint8_t ys[8], uvs[8];
 };
@@ -419,11 +420,11 @@ void k_cdef(CdefArgs<BPC> a) {
     // XCD-contiguous superblock order: workgroups are dealt round-robin over
     // the 8 XCDs, so logical superblock (b % 8) * (n / 8) + b / 8 keeps a run
     // of neighbours (which share their border lines) in one L2
-    const int nsb = a.sbw * a.sbh, nb8 = (int)gridDim.x >> 3, b = blockIdx.x;
+    const int nsb = a.sbw * a.sbr, nb8 = (int)gridDim.x >> 3, b = blockIdx.x;
     const int sb = (b & 7) * nb8 + (b >> 3);
     if (sb >= nsb) return;
-    const int sbx = sb % a.sbw, sby = sb / a.sbw;
-    const int idx = a.idx[sb];
+    const int sbx = sb % a.sbw, sby = a.sby0 + sb / a.sbw;
+    const int idx = a.idx[sby * a.sbw + sbx];   // (the frame's superblock index, row ranges included)
     const int ylvl = idx >= 0 ? a.ys[idx] : 0, uvlvl = idx >= 0 && LAYOUT ? a.uvs[idx] : 0;
     const bool active = ylvl || uvlvl;   // :150-156
     const int bd8 = BPC == 8 ? 0 : bits_of(a.bdmax) - 8;
@@ -566,7 +567,13 @@ static int launch_cdef(const Dav1dGpuCdefFrame *f, hipStream_t stream) {
     a.damping = f->damping;
     memcpy(a.ys, f->y_strength, 8);
     memcpy(a.uvs, f->uv_strength, 8);
-    const dim3 grid((unsigned)((a.sbw * a.sbh + 7) & ~7));
+    // a row range (luma rows, multiples of 64): its superblock rows
+    const int r0 = f->row_start, r1 = f->row_end;
+    if (r0 < 0 || r1 < 0 || (r0 & 63) || (r1 & 63) || (r1 && r1 <= r0)) return -1;
+    a.sby0 = r0 >> 6;
+    a.sbr = min(a.sbh, r1 ? r1 >> 6 : a.sbh) - a.sby0;
+    if (a.sbr <= 0) return 0;   // (a range past the picture)
+    const dim3 grid((unsigned)((a.sbw * a.sbr + 7) & ~7));
     switch (f->layout) {
     case 0: k_cdef<BPC, 0><<<grid, 256, 0, stream>>>(a); break;
     case 1: k_cdef<BPC, 1><<<grid, 256, 0, stream>>>(a); break;

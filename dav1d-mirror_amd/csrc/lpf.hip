@@ -128,6 +128,7 @@ template <int BPC> struct LpfArgs {
     int b4s, sb128w;
     int w4, h4;                     // luma 4x4 units
     int cw[3], ch[3];               // per plane: 4x4 cells walked
+    int cy0[3];                     // per plane: the first cell row walked (row ranges)
     int cells0, cells1;             // cumulative cell counts (plane 0, 0+1)
     int ssx, ssy, bdmax;
     Dav1dGpuFilterLUT lut;
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(256) void k_lpf(LpfArgs<BPC> a) {
     else if (t < a.cells1) { pl = 1; cell = t - a.cells0; }
     else if (t < a.cells1 + (a.cells1 - a.cells0)) { pl = 2; cell = t - a.cells1; }
     else return;
-    const int cy = cell / a.cw[pl], cx = cell - cy * a.cw[pl];
+    const int cyr = cell / a.cw[pl], cx = cell - cyr * a.cw[pl], cy = a.cy0[pl] + cyr;
     if (ROWS ? cy == 0 : cx == 0) return;   // picture edges (have_top / have_left)
     const int sx = pl ? a.ssx : 0, sy = pl ? a.ssy : 0;
     const int cpx = 32 >> sx, cpy = 32 >> sy;   // cells per 128x128 area
@@ -212,22 +213,29 @@ static int launch_lpf(const Dav1dGpuLoopFilterFrame *f, hipStream_t stream) {
     // edges: rows below h4 (the y loop, :226, :295), every column of the
     // 128-wide areas (the C loops over all mask bits).
     const int halves = (a.h4 + 15) >> 4;
-    int cw[2][3], ch[2][3];
+    // a row range (luma rows, superblock multiples): the cell rows in it
+    const int r0 = f->row_start, r1 = f->row_end;
+    if (r0 < 0 || r1 < 0 || (r0 & 63) || (r1 & 63) || (r1 && r1 <= r0)) return -1;
+    const int y40 = r0 >> 2, y41 = r1 ? r1 >> 2 : 1 << 30;
+    int cw[2][3], ch[2][3], c0[3];
     for (int p = 0; p < 3; p++) {
         const int sx = p ? a.ssx : 0, sy = p ? a.ssy : 0;
+        c0[p] = y40 >> sy;
         cw[0][p] = (a.w4 + sx) >> sx;
-        ch[0][p] = (halves * 16) >> sy;
+        ch[0][p] = max(0, min(halves * 16, y41) - y40) >> sy;
         cw[1][p] = (a.sb128w * 32) >> sx;
-        ch[1][p] = (a.h4 + sy) >> sy;
+        ch[1][p] = max(0, min((a.h4 + sy) >> sy << sy, y41) - y40 + sy) >> sy;
     }
     for (int pass = 0; pass < 2; pass++) {
         for (int p = 0; p < 3; p++) {
             a.cw[p] = cw[pass][p];
             a.ch[p] = ch[pass][p];
+            a.cy0[p] = c0[p];
         }
         a.cells0 = a.cw[0] * a.ch[0];
         a.cells1 = a.cells0 + (np == 3 ? a.cw[1] * a.ch[1] : 0);
         const int total = a.cells1 + (np == 3 ? a.cw[2] * a.ch[2] : 0);
+        if (!total) continue;   // (a range past the picture)
         const dim3 grid((unsigned)((total + 255) / 256));
         if (pass == 0) k_lpf<BPC, 0><<<grid, 256, 0, stream>>>(a);
         else k_lpf<BPC, 1><<<grid, 256, 0, stream>>>(a);

@@ -431,6 +431,7 @@ template <int BPC> struct LrFrameArgs {
     int xb0, xb01;   // strip blocks of plane 0, of planes 0 + 1 (the grid has no empty chroma columns)
     int sb128, bdmax;
     int vec;         // every plane pointer and pitch 16-byte aligned (DGPU_LR_VEC)
+    int k0;          // the first stripe run (row ranges): stripe = k0 + blockIdx.y
 };
 
 // lr_stripe's filter parameters (src/lr_apply_tmpl.c:51-80); kind 0 wiener,
@@ -471,7 +472,7 @@ __global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     const int w = f.w[pl], h = f.h[pl], sv = f.ss_ver[pl];
     const int xs = (bx - (pl == 0 ? 0 : pl == 1 ? f.xb0 : f.xb01)) * kLrSW;
     if (xs >= w) return;
-    const int S64 = 64 >> sv, S8 = 8 >> sv, k = blockIdx.y;
+    const int S64 = 64 >> sv, S8 = 8 >> sv, k = f.k0 + (int)blockIdx.y;
     const int y0 = k ? k * S64 - S8 : 0, y1 = min((k + 1) * S64 - S8, h);
     if (y0 >= h) return;
     const int us = 1 << f.log2[pl];
@@ -579,7 +580,13 @@ static int launch_lr_frame(const Dav1dGpuLrFrame *F, hipStream_t stream) {
         f.vec &= al(F->in[p].data, F->in[p].stride) && al(F->out[p].data, F->out[p].stride) &&
                  (!f.restore[p] || al(F->lpf[p].data, F->lpf[p].stride));
     }
-    const int stripes = (maxh + 8 + 63) / 64 + 1;
+    int stripes = (maxh + 8 + 63) / 64 + 1;
+    // a row range (luma rows, multiples of 64): stripes start / 64 .. end / 64 - 1
+    const int r0 = F->row_start, r1 = F->row_end;
+    if (r0 < 0 || r1 < 0 || (r0 & 63) || (r1 & 63) || (r1 && r1 <= r0)) return -1;
+    f.k0 = r0 >> 6;
+    stripes = min(stripes, r1 ? r1 >> 6 : stripes) - f.k0;
+    if (stripes <= 0) return 0;   // (a range past the picture)
     int xb[3] = {0, 0, 0};
     for (int p = 0; p < np; p++) xb[p] = (f.w[p] + kLrSW - 1) / kLrSW;
     f.xb0 = xb[0];

@@ -129,10 +129,14 @@ class DeviceLr:
                                 [(t.data_ptr(), t.shape[1]) for t in self.outs], [t.data_ptr() for t in self.units])
         self.lib = abi.load_lib()
 
-    def launch(self, stream=None):
+    def launch(self, stream=None, rows=None):
+        """rows=(start, end): luma rows, multiples of 64 (a superblock-row
+        range: the frame struct's row_start / row_end); None: the frame."""
         s = stream if stream is not None else self.torch.cuda.current_stream()
         fn = getattr(self.lib, f"dav1d_gpu_lr_frame_{8 if self.case.bpc == 8 else 16}bpc")
+        self.frame.row_start, self.frame.row_end = rows if rows is not None else (0, 0)
         rc = fn(ctypes.byref(self.frame), ctypes.c_void_p(s.cuda_stream))
+        self.frame.row_start = self.frame.row_end = 0
         if rc:
             raise RuntimeError(f"dav1d_gpu_lr_frame failed: {rc}")
 

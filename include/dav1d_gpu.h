@@ -1050,9 +1050,15 @@ typedef struct Dav1dGpuCdefFrame {
     int32_t pad_;
     uint8_t y_strength[8];        /* frame_hdr->cdef.y_strength / uv_strength */
     uint8_t uv_strength[8];
+    int32_t row_start, row_end;   /* round 5: luma rows [start, end), multiples
+                                     of 64: the 64x64 filter blocks of those
+                                     rows only (dav1d_cdef_brow per row);
+                                     0, 0: the whole frame                   */
 } Dav1dGpuCdefFrame;
-/* Errors: -1 NULL / bad layout / in == out / bad damping or strength,
- * -3 launch failure, -4 misaligned planes. */
+/* Errors: -1 NULL / bad layout / in == out / bad damping or strength / bad
+ * row range, -3 launch failure, -4 misaligned planes.  in is read-only, so
+ * a range may run as soon as the deblocked rows it reads exist (its rows
+ * plus 2 below, 64 + 2 per superblock row). */
 int dav1d_gpu_cdef_frame_8bpc(const Dav1dGpuCdefFrame *f, void *stream);
 int dav1d_gpu_cdef_frame_16bpc(const Dav1dGpuCdefFrame *f, void *stream);
 
@@ -1112,9 +1118,16 @@ typedef struct Dav1dGpuLoopFilterFrame {
     int32_t layout;               /* 0 I400, 1 I420, 2 I422, 3 I444          */
     int32_t bitdepth_max;
     int32_t filter_uv;            /* loopfilter.level_u || level_v           */
+    int32_t row_start, row_end;   /* round 5: luma rows [start, end), multiples
+                                     of 64 -- the superblock rows of
+                                     dav1d_filter_sbrow_deblock_cols / _rows
+                                     (src/recon_tmpl.c:2037-2069), chroma
+                                     rows >> ss_ver; 0, 0: the whole frame   */
     int32_t pad_;
 } Dav1dGpuLoopFilterFrame;
-/* Errors: -1 NULL / bad layout, -3 launch failure. */
+/* Errors: -1 NULL / bad layout / bad row range, -3 launch failure.  Row
+ * ranges run in increasing order give the whole-frame result (a superblock
+ * row's row edges never reach pixels the next row's column edges read). */
 int dav1d_gpu_loopfilter_frame_8bpc(const Dav1dGpuLoopFilterFrame *f, void *stream);
 int dav1d_gpu_loopfilter_frame_16bpc(const Dav1dGpuLoopFilterFrame *f, void *stream);
 
@@ -1180,8 +1193,16 @@ typedef struct Dav1dGpuLrFrame {
     int32_t bitdepth_max;
     int32_t sb128;
     int32_t restore_planes;       /* LR_RESTORE_Y 1 | U 2 | V 4              */
+    int32_t row_start, row_end;   /* round 5: luma rows [start, end), multiples
+                                     of 64: the restoration stripes k =
+                                     start / 64 .. end / 64 - 1 (rows
+                                     64k - 8 .. 64k + 55, >> ss_ver), what
+                                     dav1d_lr_sbrow filters per superblock
+                                     row (src/lr_apply_tmpl.c:169-202);
+                                     0, 0: the whole frame                   */
 } Dav1dGpuLrFrame;
-/* Errors: -1 NULL / bad layout / bad unit grid, -3 launch failure. */
+/* Errors: -1 NULL / bad layout / bad unit grid / bad row range, -3 launch
+ * failure. */
 int dav1d_gpu_lr_frame_8bpc(const Dav1dGpuLrFrame *f, void *stream);
 int dav1d_gpu_lr_frame_16bpc(const Dav1dGpuLrFrame *f, void *stream);
 

@@ -8,11 +8,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _check(oracle, c, sb128=0):
+def _check(oracle, c, sb128=0, step=None):
     import torch
     import dav1d_mirror_amd.cdef as cdef
     dev = cdef.DeviceCdef(c)
-    dev.launch()
+    if step is None:
+        dev.launch()
+    else:   # one call per superblock row, last row first (the input is read-only), and one past the picture
+        for y in reversed(range(0, c.height + step, step)):
+            dev.launch(rows=(y, y + step))
     torch.cuda.synchronize()
     want = oracle.cdef_frame(c, sb128)
     for p, (a, b) in enumerate(zip(dev.outputs_host(), want)):
@@ -70,3 +74,17 @@ def test_cdef_1080p(oracle):
 def test_cdef_4k_10bit(oracle):
     import dav1d_mirror_amd.cdef as cdef
     _check(oracle, cdef.make_cdef_case(seed=8, width=3840, height=2160, bpc=16, bitdepth_max=1023))
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+@pytest.mark.parametrize("layout", [1, 2])
+@pytest.mark.parametrize("sb128", [0, 1])
+def test_cdef_per_superblock_row(oracle, bpc, bdmax, layout, sb128):
+    """Row ranges (round 5): one call per superblock row (dav1d_cdef_brow
+    per row), in reverse order, equal the oracle's frame walk."""
+    import dav1d_mirror_amd.cdef as cdef
+    c = cdef.make_cdef_case(seed=90 + layout + bpc, width=328, height=264, bpc=bpc, bitdepth_max=bdmax,
+                            layout=layout)
+    dev = _check(oracle, c, sb128=sb128, step=64 << sb128)
+    with pytest.raises(RuntimeError):
+        dev.launch(rows=(64, 64))

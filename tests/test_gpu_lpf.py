@@ -9,11 +9,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _check(oracle, c):
+def _check(oracle, c, step=None):
     import torch
     import dav1d_mirror_amd.lpf as lpf
     dev = lpf.DeviceLpf(c)
-    dev.launch()
+    if step is None:
+        dev.launch()
+    else:   # one call per superblock row, in decoding order (row_start / row_end), and one past the picture
+        for y in range(0, c.height + step, step):
+            dev.launch(rows=(y, y + step))
     torch.cuda.synchronize()
     want = oracle.loopfilter_frame(c)
     for p, (a, b) in enumerate(zip(dev.outputs_host(), want)):
@@ -52,3 +56,20 @@ def test_lpf_paths(oracle, kw):
 def test_lpf_1080p(oracle):
     import dav1d_mirror_amd.lpf as lpf
     _check(oracle, lpf.make_lpf_case(seed=5, width=1920, height=1080))
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+@pytest.mark.parametrize("layout", [1, 3])
+@pytest.mark.parametrize("sb128", [0, 1])
+def test_lpf_per_superblock_row(oracle, bpc, bdmax, layout, sb128):
+    """Row ranges (round 5): one call per superblock row, in order, as
+    dav1d_filter_sbrow_deblock_cols / _rows run (src/recon_tmpl.c:2037-2069),
+    equal the oracle's frame walk; a range past the picture does nothing and
+    a range off the 64-row grid is refused."""
+    import ctypes
+    import dav1d_mirror_amd.lpf as lpf
+    c = lpf.make_lpf_case(seed=77 + layout + sb128, width=328, height=264, bpc=bpc, bitdepth_max=bdmax,
+                          layout=layout, sb128=sb128)
+    dev = _check(oracle, c, step=64 << sb128)
+    with pytest.raises(RuntimeError):
+        dev.launch(rows=(32, 96))

@@ -7,11 +7,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _check(oracle, c):
+def _check(oracle, c, step=None):
     import torch
     import dav1d_mirror_amd.lr as lr
     dev = lr.DeviceLr(c)
-    dev.launch()
+    if step is None:
+        dev.launch()
+    else:   # one call per superblock row, last row first (in, lpf read-only), and one past the picture
+        for y in reversed(range(0, c.height + step, step)):
+            dev.launch(rows=(y, y + step))
     torch.cuda.synchronize()
     want = oracle.lr_frame(c)
     for p, (a, b) in enumerate(zip(dev.outputs_host(), want)):
@@ -43,3 +47,16 @@ def test_lr_random(oracle, seed):
 def test_lr_1080p(oracle):
     import dav1d_mirror_amd.lr as lr
     _check(oracle, lr.make_lr_case(seed=9, width=1920, height=1080, unit_log2=(6, 5)))
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+@pytest.mark.parametrize("layout", [1, 3])
+@pytest.mark.parametrize("sb128", [0, 1])
+def test_lr_per_superblock_row(oracle, bpc, bdmax, layout, sb128):
+    """Row ranges (round 5): one call per superblock row, the stripes
+    dav1d_lr_sbrow filters for it (src/lr_apply_tmpl.c:169-202), in reverse
+    order, equal the oracle's frame walk."""
+    import dav1d_mirror_amd.lr as lr
+    c = lr.make_lr_case(seed=120 + layout + sb128 + bpc, width=336, height=264, bpc=bpc, bitdepth_max=bdmax,
+                        layout=layout, sb128=sb128, unit_log2=(6 + sb128, 5 + sb128 if layout == 1 else 6 + sb128))
+    _check(oracle, c, step=64 << sb128)
