@@ -84,6 +84,25 @@ class DeviceChain:
         self.lr.launch(s)
         self.grain.launch(s)
 
+    def launch_per_row(self, stream=None, step=64):
+        """The same chain with the post-filters interleaved per superblock
+        row as a decoder runs them behind its flushes (round 5 row ranges,
+        INTEGRATION.md 2d): deblock row k, then CDEF and LR of row k - 1 --
+        CDEF reads two deblocked rows below its own, which row k's
+        deblocking finishes, and LR's stripes of row k - 1 end 8 rows above
+        its bottom -- then the last row's CDEF and LR, then grain."""
+        s = stream if stream is not None else self.torch.cuda.current_stream()
+        self.recon.launch(s)
+        rows = list(range(0, self.fd.cfg.height, step))
+        for k, y in enumerate(rows):
+            self.lpf.launch(s, rows=(y, y + step))
+            if k:
+                self.cdef.launch(s, rows=(y - step, y))
+                self.lr.launch(s, rows=(y - step, y))
+        self.cdef.launch(s, rows=(rows[-1], rows[-1] + step))
+        self.lr.launch(s, rows=(rows[-1], rows[-1] + step))
+        self.grain.launch(s)
+
     def stage_host(self, P):
         out = []
         for p, t in enumerate(P):

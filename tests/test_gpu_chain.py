@@ -9,15 +9,23 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("w,h,bpc,bdmax", [(1920, 1080, 8, 255), (3840, 2160, 8, 255), (1920, 1080, 16, 1023)])
-def test_chain_recon_postfilters_grain(pkg, oracle, w, h, bpc, bdmax):
+@pytest.mark.parametrize("w,h,bpc,bdmax,per_row", [(1920, 1080, 8, 255, False), (3840, 2160, 8, 255, False),
+                                                   (1920, 1080, 16, 1023, False), (1920, 1080, 8, 255, True),
+                                                   (1920, 1080, 16, 1023, True)])
+def test_chain_recon_postfilters_grain(pkg, oracle, w, h, bpc, bdmax, per_row):
+    """per_row: the post-filters run per superblock row, interleaved as a
+    decoder runs them (DeviceChain.launch_per_row), against the same
+    whole-frame oracle chain."""
     import torch
     import dav1d_mirror_amd.chain as ch
     import dav1d_mirror_amd.workload as wl
     fd = wl.make_frame(wl.FrameConfig(width=w, height=h, bpc=bpc, bitdepth_max=bdmax, seed=81))
     cases = ch.make_cases(fd, seed=17)
     dev = ch.DeviceChain(fd, cases, "cuda:0")
-    dev.launch(torch.cuda.current_stream())
+    if per_row:
+        dev.launch_per_row(torch.cuda.current_stream())
+    else:
+        dev.launch(torch.cuda.current_stream())
     torch.cuda.synchronize()
     got = [dev.stage_host(P) for P in (dev.A, dev.B, dev.C, dev.D)]
     want = ch.host_chain(fd, cases, oracle, threads=8)
