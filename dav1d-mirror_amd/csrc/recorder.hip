@@ -23,6 +23,7 @@
 //      waves wait for their producers only.
 // Host code only; the device work runs on the caller's stream.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -433,8 +434,20 @@ struct Dav1dGpuRecorder {
     int32_t last_units = 0, last_levels = 0;
 };
 
+// recorders alive in the process: a decoder with frame threads owns one per
+// frame, and each sizes its worker pool to its share of the CPUs the process
+// may run on (four recorders of 8 workers each oversubscribed
+// the host)
+static std::atomic<int> g_live_recorders{0};
+static int rec_cpu_budget() {
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) return std::max(1, CPU_COUNT(&set));
+    return (int)std::max(1u, std::thread::hardware_concurrency());
+}
+
 extern "C" Dav1dGpuRecorder *dav1d_gpu_recorder_new(int bpc, int bitdepth_max, int width, int height, int device) {
     if ((bpc != 8 && bpc != 16) || width <= 0 || height <= 0) return nullptr;
+    g_live_recorders.fetch_add(1, std::memory_order_relaxed);
     Dav1dGpuRecorder *r = new Dav1dGpuRecorder();
     r->bpc = bpc;
     r->bdmax = bpc == 8 ? 255 : bitdepth_max;
@@ -446,6 +459,7 @@ extern "C" Dav1dGpuRecorder *dav1d_gpu_recorder_new(int bpc, int bitdepth_max, i
 
 extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
     if (!r) return;
+    g_live_recorders.fetch_sub(1, std::memory_order_relaxed);
     if (hipSetDevice(r->device) == hipSuccess) {
         if (r->done) {
             (void)hipEventSynchronize(r->done);
@@ -1115,8 +1129,10 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         return 0;
     };
 
-    if (!r->pool) {   // DAV1D_GPU_REC_THREADS (diagnostics): the worker count, default min(8, cores)
-        int nthr = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    if (!r->pool) {   // DAV1D_GPU_REC_THREADS (diagnostics): the worker count; default this
+                      // recorder's share of the process's CPUs, at most 8
+        const int live = std::max(1, g_live_recorders.load(std::memory_order_relaxed));
+        int nthr = std::max(1, std::min(8, rec_cpu_budget() / live));
         if (const char *e = getenv("DAV1D_GPU_REC_THREADS")) nthr = std::max(1, atoi(e));
         r->pool.reset(new Pool(nthr));
     }
