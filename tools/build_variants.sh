@@ -42,6 +42,7 @@ for v in ${VARIANTS:-nomc noitx nointra}; do
         lrpf1|lrpf2|lrpf3) TUS=lr build $v -DDGPU_LR_PF=${v#lrpf} ;;
         st8) TUS=recon8 build st8 -DDGPU_ST8=1 ;;
         lpfb) TUS=lpf build lpfb -DDGPU_LPF_BATCH=1 ;;
+        rzvec) TUS=mc build rzvec -DDGPU_RZ_VEC=1 ;;
         bounds) TUS="recon8 recon_ie8 recon_sb8 recorder tile8 tile16" build bounds -DDGPU_BOUNDS=1 ;;
         fnofence) TUS="recon_ie8" build fnofence -DDGPU_FLOW_NOFENCE=1 ;;
         fsc1) TUS="recon_ie8" build fsc1 -DDGPU_FLOW_SC1=1 ;;
