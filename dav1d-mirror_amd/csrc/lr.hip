@@ -61,11 +61,12 @@ constexpr int kLrVH = 66;   // A / B rows: unit rows -1..64
 #ifndef DGPU_LR_VEC
 #define DGPU_LR_VEC 3   // (4, the LDS-staged outputs, measured slower: two more barriers)
 #endif
-// DGPU_LR_PF (bits, experiment): the self-guided A / B loop 1 issues the
-// next tile row's LDS reads before the current row's arithmetic, 2 is
-// unrolled by two
+// DGPU_LR_PF (bits): the self-guided A / B loop 1 issues the next tile
+// row's LDS reads before the current row's arithmetic (measured slower), 2
+// is unrolled by two (the default: 47.8-48.0 against 48.8-49.3 us on three
+// boxes, profiles/r5/r5z_lr_unroll_ab.json)
 #ifndef DGPU_LR_PF
-#define DGPU_LR_PF 0
+#define DGPU_LR_PF 2
 #endif
 
 // A / B of selfguided_filter (:373-392) from one position's box sum and sum
