@@ -576,11 +576,43 @@ def spawn_ranks(n, argv):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
                                       stdout=None if r == 0 else sys.stderr))
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    if bad:
-        log(f"bench: rank exit codes {codes}")
-    return bad[0] if bad else 0
+    return wait_ranks(procs)
+
+
+def wait_ranks(procs, poll_s=0.2):
+    """Poll every rank (waiting in rank order blocks forever when a
+    later rank dies while rank 0 sits in a rendezvous or barrier).  On the
+    first non-zero exit the other ranks are terminated (then killed) and that
+    status is returned; 0 when every rank exits cleanly."""
+    import time as _t
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            log(f"bench: rank exit codes {codes}: stopping the others")
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            t_end = _t.time() + 10
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.1, t_end - _t.time()))
+                except Exception:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(c == 0 for c in codes):
+            return 0
+        _t.sleep(poll_s)
+
+
+def per_rank_fields(kernel_us, ms_per_step):
+    """The N>1 line's per-rank view: each rank's kernel time
+    and time per step, in rank order, with the max over ranks (the rank that
+    sets the aggregate's clock)."""
+    return {"kernel_us": [round(v, 2) for v in kernel_us], "kernel_us_max": round(max(kernel_us), 2),
+            "ms_per_step": [round(v, 4) for v in ms_per_step], "ms_per_step_max": round(max(ms_per_step), 4),
+            "slowest_rank": int(np.argmax(ms_per_step))}
 
 
 def dry_run(world, rank, local):
@@ -594,9 +626,10 @@ def dry_run(world, rank, local):
         dist.barrier()
     got = sh.max_over_ranks(float(rank), dist, "cpu")
     total = sh.sum_over_ranks(1, dist, "cpu")
+    per_rank = sh.gather_over_ranks(10.0 + rank, dist, "cpu")   # stands in for each rank's kernel_us
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": total, "max_rank": got,
-                          "local_rank": local}), flush=True)
+                          "local_rank": local, "per_rank": per_rank_fields(per_rank, per_rank)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -687,9 +720,10 @@ def main():
 
     # timed region: exactly K steps, barrier + synchronize on both sides.
     # One HIP event pair on the launch stream brackets the same K launches
-    # inside it, so the per-launch kernel time and the wall clock per step
-    # come from one run (the events sit inside the wall-clock bracket: the
-    # kernel time can never exceed the time per step)
+    # inside it; the kernel time per launch is that stream time / K, which
+    # sits inside the wall-clock bracket and so never exceeds the time per
+    # step (frac comes from it; the launches are back to back,
+    # so it matches rocprofv3's per-launch duration)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize(dev)
@@ -700,12 +734,14 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     barrier()
-    el = sh.max_over_ranks(time.perf_counter() - t0, dist, dev)
+    my_el = time.perf_counter() - t0
+    el = sh.max_over_ranks(my_el, dist, dev)
     stream_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
+    kern_s = stream_s
+    assert kern_s <= my_el / args.steps * (1 + 1e-6), (kern_s, my_el / args.steps)
 
-    # the kernel's own duration per launch (outside the timed region): an
-    # event pair around each launch, so host gaps between launches do not
-    # count (the stream time above includes them)
+    # diagnostic only (outside the timed region, not used for frac): an event
+    # pair around each launch; the pairs add their own packets' latency
     nk = min(args.steps, 100)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
     for a, b in evs:
@@ -713,7 +749,11 @@ def main():
         frame.launch(stream)
         b.record(stream)
     torch.cuda.synchronize(dev)
-    kern_s = sum(a.elapsed_time(b) for a, b in evs) * 1e-3 / nk
+    pair_s = sum(a.elapsed_time(b) for a, b in evs) * 1e-3 / nk
+    per_rank = None
+    if world > 1:
+        per_rank = per_rank_fields([v * 1e6 for v in sh.gather_over_ranks(kern_s, dist, dev)],
+                                   [v * 1e3 / args.steps for v in sh.gather_over_ranks(my_el, dist, dev)])
 
     # the timed frame's pixels against the oracle (outside the timed region;
     # the launches are idempotent, so the picture is the last step's)
@@ -768,11 +808,11 @@ def main():
                 "kernel": f"k_recon<{cfg.bpc},*> (main group: all classes up to 32x32 in one launch; "
                           "the 64-point group launches only when such units exist)",
                 "kernel_us": round(kern_s * 1e6, 2),
-                "kernel_us_note": f"mean of {nk} launches, each bracketed by its own HIP event pair on the "
-                                  "launch stream (kernel duration, like rocprofv3's)",
-                "stream_us_per_step": round(stream_s * 1e6, 2),
-                "stream_us_note": "one HIP event pair around the K timed launches inside the wall-clock "
-                                  "bracket, / K (includes any gap between launches)",
+                "kernel_us_note": "one HIP event pair on the launch stream around the K timed launches "
+                                  "(inside the wall-clock bracket, so <= ms_per_step), / K; frac uses it",
+                "event_pair_us_diag": round(pair_s * 1e6, 2),
+                "event_pair_note": f"diagnostic only: mean of {nk} launches each bracketed by its own event "
+                                   "pair (adds the event packets' latency; not used for frac)",
                 "rocprof_kernel_us": rocprof_kernel_us(cfg.bpc) if args.config != "1080p-mc" else None,
                 "frac_rocprof": (round(bytes_launch / (rocprof_kernel_us(cfg.bpc) * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
                                  if args.config != "1080p-mc" and rocprof_kernel_us(cfg.bpc) else None),
@@ -791,6 +831,8 @@ def main():
             out["config"]["bit_exact_vs_oracle"] = check
         if feed is not None:
             out["feed"] = feed
+        if per_rank is not None:
+            out["per_rank"] = per_rank
         if not args.no_configs and world == 1 and args.config == "4k":
             out["configs"] = config_legs(dev, stream, args.steps)
         if not args.no_configs and world == 1 and args.config == "4k":
@@ -815,6 +857,7 @@ def main():
             out["loop_restoration"] = lr_breakdown(cfg, dev, args.steps)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
+        assert out["roofline"]["kernel_us"] <= out["ms_per_step"] * 1e3, "kernel time exceeds the step time"
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -368,38 +368,27 @@ __device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, co
         dst[(y + 1) * ds] = (P)v1;
     }
 }
-#ifndef DGPU_CDEF_SPLIT
-#define DGPU_CDEF_SPLIT 1   // the primary-only / secondary-only forms for waves that need only one
-#endif
 template <int BPC, int BH>
 __device__ __forceinline__ void col_out(typename Px<BPC>::pixel *dst, int ds, const uint32_t *c, int S,
                                         const CdefTaps &tp, bool filt) {
     if (filt) {
         // (the votes run over the filtering lanes: the copying ones are masked off here)
-        if (DGPU_CDEF_SPLIT && __all(tp.sec == 0)) col_out<BPC, BH, true, true, false>(dst, ds, c, S, tp);
-        else if (DGPU_CDEF_SPLIT && __all(tp.pri == 0)) col_out<BPC, BH, true, false, true>(dst, ds, c, S, tp);
+        // (the primary-only / secondary-only forms for waves that need only one)
+        if (__all(tp.sec == 0)) col_out<BPC, BH, true, true, false>(dst, ds, c, S, tp);
+        else if (__all(tp.pri == 0)) col_out<BPC, BH, true, false, true>(dst, ds, c, S, tp);
         else col_out<BPC, BH, true>(dst, ds, c, S, tp);
     } else {
         col_out<BPC, BH, false>(dst, ds, c, S, tp);
     }
 }
 
-// DGPU_CDEF_ABL (cost-model probes, wrong output): 1 skips the direction
-// search, 2 the filter (blocks copied).  4K 8-bit frame: 41.6 us whole,
-// 41.0 without the directions, 16.1 without the filter, 13.1 without both
-// (DESIGN.md 4).  (Two superblocks per workgroup with the second one's loads
-// in flight during the first one's filter: 108 VGPRs, 4 waves per SIMD,
-// one round of workgroups instead of 1.6, measured 48.2 us: slower.)
-#ifndef DGPU_CDEF_ABL
-#define DGPU_CDEF_ABL 0
-#endif
-// DGPU_CDEF_WPE: a minimum of waves per SIMD for the register allocator
-// (0: the compiler's choice, 86 VGPRs = 5 waves)
-#ifndef DGPU_CDEF_WPE
-#define DGPU_CDEF_WPE 0
-#endif
+// Measured: the round-4 ablations (41.6 us whole, 41.0 without
+// the direction search, 16.1 without the filter); two superblocks per
+// workgroup with the second one's loads in flight (48.2 us) and a forced 6 /
+// 7 waves per SIMD (42.5 / 46.8, then 38.2 against 36.1 us with a spill)
+// were slower; the register allocator keeps its own choice.
 template <int BPC, int LAYOUT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DGPU_CDEF_WPE ? DGPU_CDEF_WPE : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void k_cdef(CdefArgs<BPC> a) {
     using P = typename Px<BPC>::pixel;
     constexpr int SX = LAYOUT == 1 || LAYOUT == 2, SY = LAYOUT == 1;
@@ -450,7 +439,7 @@ void k_cdef(CdefArgs<BPC> a) {
     __syncthreads();
 
     // directions: wave q, lane = block (8 x 8 blocks of 8x8)
-    const bool need_dir = active && (ypri || uvpri) && !(DGPU_CDEF_ABL & 1);
+    const bool need_dir = active && (ypri || uvpri);
     if (need_dir) {
         const int q = threadIdx.x >> 6, blk = threadIdx.x & 63;
         const int bx8 = blk & 7, by8 = blk >> 3;
@@ -500,7 +489,7 @@ void k_cdef(CdefArgs<BPC> a) {
                 filt = true;
             }
         }
-        col_out<BPC, 8>(dst, a.os[0], c, LS, tp, filt && !(DGPU_CDEF_ABL & 2));
+        col_out<BPC, 8>(dst, a.os[0], c, LS, tp, filt);
     }
     if (!LAYOUT) return;
     __syncthreads();   // the luma tile is free: the chroma tiles go there
@@ -527,7 +516,7 @@ void k_cdef(CdefArgs<BPC> a) {
             tp.init(uvpri, uvsec, dir, damping - 1, bd8, CS);
             filt = true;
         }
-        col_out<BPC, CBH>(dst, a.os[1 + pl], c, CS, tp, filt && !(DGPU_CDEF_ABL & 2));
+        col_out<BPC, CBH>(dst, a.os[1 + pl], c, CS, tp, filt);
     }
 }
 

@@ -65,10 +65,7 @@ __device__ __forceinline__ int r8s(int v) { return (v * 181 + 128) >> 8; }
 // 2^15).  drN<SH, K...>(v...) = (sum K_i v_i + (1 << SH >> 1)) >> SH; the
 // reference's '- 4096' overflow-free forms (10/12-bit) fold back in
 // (tools/gen_itx_d2.py wrote each D2SEL next to its original expression).
-#ifndef DGPU_ITX_D2
-#define DGPU_ITX_D2 1   // 0: the 8-bit path keeps the scalar forms too (A/B builds)
-#endif
-#define D2SEL(d2, orig) ((D2 && DGPU_ITX_D2) ? (d2) : (orig))
+#define D2SEL(d2, orig) (D2 ? (d2) : (orig))
 typedef short dgpu_v2i16 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int dot2c(uint32_t v, uint32_t k, int acc) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(dgpu_v2i16, v), __builtin_bit_cast(dgpu_v2i16, k), acc, false);

@@ -13,7 +13,7 @@
 // Progress: tickets go out in level order to waves that already run, and a
 // wave waits only for tasks with smaller tickets, so every awaited task is
 // held by a resident wave that itself waits only on earlier ones.  A poll
-// bound (DGPU_FLOW_SPIN_LIMIT) turns any unexpected stall into an error
+// bound (kFlowSpinLimit) turns any unexpected stall into an error
 // flag; a wave that gives up still counts itself done, so the grid drains.
 #pragma once
 #include <algorithm>
@@ -22,13 +22,6 @@
 
 #include "recon_impl.hpp"
 
-#ifndef DGPU_FLOW_SPIN_LIMIT
-#define DGPU_FLOW_SPIN_LIMIT (1 << 21)   // polls of ~0.25 us: ~0.5 s
-#endif
-
-#ifndef DGPU_FLOW_NOFENCE
-#define DGPU_FLOW_NOFENCE 0   // probe only: no agent-scope fences (unsafe)
-#endif
 #ifndef DGPU_FLOW_TRACE
 #define DGPU_FLOW_TRACE 0     // probe only: per-task s_memrealtime stamps after the task list
 #endif
@@ -37,17 +30,14 @@
 // written to addresses taken from the environment.  Product builds never read
 // those variables, so no environment can make the library store to an
 // arbitrary address
-#ifndef DGPU_FLOW_PRIO
-#define DGPU_FLOW_PRIO 0   // raise a wave's issue priority once its level wait is over
-#endif
 #ifndef DGPU_DIAG
 #define DGPU_DIAG (DGPU_TRACE || DGPU_FLOW_TRACE)
 #endif
-#ifndef DGPU_FLOW_SLEEP
-#define DGPU_FLOW_SLEEP 8     // s_sleep between polls (x64 cycles)
-#endif
 
 namespace dgpu {
+
+constexpr int kFlowSpinLimit = 1 << 21;   // polls of ~0.25 us before a wave gives up: ~0.5 s
+constexpr int kFlowSleep = 8;             // s_sleep between polls (x64 cycles; 32 / 127 changed nothing)
 
 struct FlowTask {   // 16 B
     int32_t level, cls, first, count;
@@ -69,7 +59,7 @@ struct FlowArgs {
     const int32_t *dep_start;     // dataflow: per unit, its producer units (CSR); NULL: levels
     const int32_t *deps;
     unsigned long long *trace;    // DGPU_FLOW_TRACE: [ticket][4] start, ready, computed, released
-    int spin_limit;               // polls before a wave gives up (DGPU_FLOW_SPIN_LIMIT)
+    int spin_limit;               // polls before a wave gives up (kFlowSpinLimit)
 };
 
 template <int BPC>
@@ -143,17 +133,11 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
                         ok = 0;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(DGPU_FLOW_SLEEP);
+                    __builtin_amdgcn_s_sleep(kFlowSleep);
                 }
             }
             if (!ok && lane == 0) __hip_atomic_store(&f.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // DGPU_FLOW_SC1: every load of a producer's bytes is an sc1 load, so
-            // no L1 invalidate; the wavefront-scope fence only keeps the
-            // compiler from hoisting them above the poll
-            if (nd && !DGPU_FLOW_NOFENCE) {
-                if (DGPU_FLOW_SC1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            }
+            if (nd) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         } else if (level > 0) {
             int ok = 1;
             if (lane == 0) {
@@ -167,7 +151,7 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
                         ok = 0;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(DGPU_FLOW_SLEEP);
+                    __builtin_amdgcn_s_sleep(kFlowSleep);
                 }
                 // a wave that gives up flags the error and carries on (its
                 // pixels are then wrong, but every wave still finishes)
@@ -175,15 +159,8 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
             }
             __builtin_amdgcn_wave_barrier();
             // the previous levels' picture / top_edge stores are visible from here
-            if (!DGPU_FLOW_NOFENCE) {
-                if (DGPU_FLOW_SC1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
-        // the wave is on the dependency chain from here (its level's edges
-        // are ready): issue priority over the waves still running their
-        // pre-wait loads and transforms for later levels
-        if constexpr (DGPU_FLOW_PRIO) __builtin_amdgcn_s_setprio(3);
         if constexpr (DGPU_FLOW_TRACE) tr1 = __builtin_amdgcn_s_memrealtime();
     };
     // (DGPU_TRACE builds: the class code's phase marks per task, a.trace)
@@ -192,10 +169,8 @@ __global__ __launch_bounds__(64) void k_flow(ReconArgs<BPC> a, FlowArgs f) {
         __builtin_amdgcn_s_waitcnt(0);
         tr2 = __builtin_amdgcn_s_memrealtime();
     }
-    // this task's stores reach agent scope before it is counted (SC1: they
-    // are write-through, so draining them is the release)
-    if (DGPU_FLOW_SC1 || DGPU_FLOW_NOFENCE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // this task's stores reach agent scope before it is counted
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (f.dep_start) {   // (all lanes are live again here)
         for (int i = lane; i < count; i += 64) {
             bnd_touch(f.done + first + i);
@@ -358,7 +333,7 @@ __global__ __launch_bounds__(64 * sb_waves<BPC>()) void k_flow_sb(ReconArgs<BPC>
                     ok = 0;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(DGPU_FLOW_SLEEP);
+                __builtin_amdgcn_s_sleep(kFlowSleep);
             }
         }
         if (!ok && lane == 0) __hip_atomic_store(&f.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -400,13 +375,12 @@ __global__ __launch_bounds__(64 * sb_waves<BPC>()) void k_flow_sb(ReconArgs<BPC>
 // dependency step; the flow trace shows the small classes' tasks are those
 // (intra wavefront).  Level 0 (inter units, and intra units
 // with no producer) has no chain to shorten and keeps full waves.
-#ifndef DGPU_FLOW_UNITS
-#define DGPU_FLOW_UNITS 8   // 4K intra frame: 64 (a class's full wave) 19.6 ms, 16: 18.6, 8: 17.75, 4: 17.75
-#endif
+// 4K intra frame: 64 (a class's full wave) 19.6 ms, 16: 18.6, 8: 17.75, 4: 17.75
+constexpr int kFlowUnits = 8;
 static int flow_units_cap() {
     static const int cap = [] {
-        const char *e = getenv("DAV1D_GPU_FLOW_UNITS");
-        const int v = e ? atoi(e) : DGPU_FLOW_UNITS;
+        const char *e = getenv("DAV1D_GPU_FLOW_UNITS");   // (tuning)
+        const int v = e ? atoi(e) : kFlowUnits;
         return v < 1 ? 1 : v > 64 ? 64 : v;
     }();
     return cap;
@@ -610,7 +584,7 @@ static int launch_flow_sb(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBa
     f.sb_dep_start = (const int32_t *)(ws + Lw.sds);
     f.sb_deps = (const int32_t *)(ws + Lw.sdeps);
     f.n_sb = s->n_sb;
-    f.spin_limit = DGPU_FLOW_SPIN_LIMIT;
+    f.spin_limit = kFlowSpinLimit;
     if (const char *sl = getenv("DAV1D_GPU_FLOW_SPIN_LIMIT")) f.spin_limit = (int)strtol(sl, nullptr, 0);
     f.trace = nullptr;
     f.debug = 0;
@@ -765,7 +739,7 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     f.trace = (unsigned long long *)(ws + Lw.trace);
     // DAV1D_GPU_FLOW_SPIN_LIMIT (tests): a smaller poll bound makes waves give
     // up early, to exercise the error word's reporting
-    f.spin_limit = DGPU_FLOW_SPIN_LIMIT;
+    f.spin_limit = kFlowSpinLimit;
     if (const char *sl = getenv("DAV1D_GPU_FLOW_SPIN_LIMIT")) f.spin_limit = (int)strtol(sl, nullptr, 0);
     {   // the task list and producer lists through page-locked staging (asynchronous copy)
         const size_t up = Lw.deps + (size_t)nd * 4 - Lw.tasks;

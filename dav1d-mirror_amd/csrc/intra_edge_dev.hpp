@@ -74,35 +74,25 @@ __device__ __forceinline__ IeCtx<P> ie_setup(const Dav1dGpuIntraEdge &r, const P
     return c;
 }
 
-// One pixel of the picture / top_edge.  SC (the intra wavefront's sc1
-// hand-off, flow_impl.hpp DGPU_FLOW_SC1): the aligned 4-byte word holding it,
-// loaded write-through coherent (global_load_dword sc1, bypassing this CU's
-// L1), so no acquire is needed before it.
+// One pixel of the picture / top_edge (checked in the bounds build).
 #if DGPU_BOUNDS
 __device__ __noinline__ bool bnd_ok(const void *p, int n, int line);
 #endif
-template <bool SC, typename P> __device__ __forceinline__ int ie_px(const P *p
+template <typename P> __device__ __forceinline__ int ie_px(const P *p
 #if DGPU_BOUNDS
                                                                     , int line = __builtin_LINE()
 #endif
 ) {
-    if constexpr (SC) {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-        const uint32_t w = __hip_atomic_load((const __attribute__((address_space(1))) uint32_t *)(a & ~(uintptr_t)3),
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return sizeof(P) == 1 ? (int)((w >> (8 * (a & 3))) & 0xff) : (int)((w >> (8 * (a & 2))) & 0xffff);
-    } else {
 #if DGPU_BOUNDS
-        if (!bnd_ok(p, (int)sizeof(P), line)) return 0;
+    if (!bnd_ok(p, (int)sizeof(P), line)) return 0;
 #endif
-        return (int)*p;
-    }
+    return (int)*p;
 }
-template <typename P, bool SC = false> __device__ __forceinline__ int ie_left(const IeCtx<P> &c, int k) {
-    return c.hl ? ie_px<SC>(c.dst + (size_t)min(k, c.nl - 1) * c.ps - 1) : c.ht ? ie_px<SC>(c.top) : c.half + 1;
+template <typename P> __device__ __forceinline__ int ie_left(const IeCtx<P> &c, int k) {
+    return c.hl ? ie_px(c.dst + (size_t)min(k, c.nl - 1) * c.ps - 1) : c.ht ? ie_px(c.top) : c.half + 1;
 }
-template <typename P, bool SC = false> __device__ __forceinline__ int ie_top(const IeCtx<P> &c, int k) {
-    return c.ht ? ie_px<SC>(c.top + min(k, c.nt - 1)) : c.hl ? ie_px<SC>(c.dst - 1) : c.half - 1;
+template <typename P> __device__ __forceinline__ int ie_top(const IeCtx<P> &c, int k) {
+    return c.ht ? ie_px(c.top + min(k, c.nt - 1)) : c.hl ? ie_px(c.dst - 1) : c.half - 1;
 }
 
 // whether the remapped mode reads topleft[i]
@@ -112,29 +102,29 @@ template <typename P> __device__ __forceinline__ bool ie_need(const IeCtx<P> &c,
 }
 
 // topleft[i]; `needed` false for entries the remapped mode does not read
-template <typename P, bool SC = false> __device__ __forceinline__ int ie_value(const IeCtx<P> &c, int i, bool &needed) {
+template <typename P> __device__ __forceinline__ int ie_value(const IeCtx<P> &c, int i, bool &needed) {
     if (i < -c.szl) {           // bottom-left (:135-154)
         needed = c.nd & 16;
         const int k = -i - c.szl - 1;
-        return c.hbl ? ie_px<SC>(c.dst + (size_t)(c.szl + min(k, c.nbl - 1)) * c.ps - 1) : ie_left<P, SC>(c, c.szl - 1);
+        return c.hbl ? ie_px(c.dst + (size_t)(c.szl + min(k, c.nbl - 1)) * c.ps - 1) : ie_left<P>(c, c.szl - 1);
     }
     if (i < 0) {                // left (:124-133)
         needed = c.nd & 1;
-        return ie_left<P, SC>(c, -i - 1);
+        return ie_left<P>(c, -i - 1);
     }
     if (i == 0) {               // top-left (:187-201)
         needed = c.nd & 4;
-        int v = c.hl ? (c.ht ? ie_px<SC>(c.top - 1) : ie_px<SC>(c.dst - 1)) : (c.ht ? ie_px<SC>(c.top) : c.half);
-        if (c.z2f) v = ((ie_left<P, SC>(c, 0) + ie_top<P, SC>(c, 0)) * 5 + v * 6 + 8) >> 4;
+        int v = c.hl ? (c.ht ? ie_px(c.top - 1) : ie_px(c.dst - 1)) : (c.ht ? ie_px(c.top) : c.half);
+        if (c.z2f) v = ((ie_left<P>(c, 0) + ie_top<P>(c, 0)) * 5 + v * 6 + 8) >> 4;
         return v;
     }
     if (i <= c.szt) {           // top (:156-166)
         needed = c.nd & 2;
-        return ie_top<P, SC>(c, i - 1);
+        return ie_top<P>(c, i - 1);
     }
     needed = c.nd & 8;          // top-right (:168-185)
     const int k = i - c.szt - 1;
-    return c.htr ? ie_px<SC>(c.top + c.szt + min(k, c.ntr - 1)) : ie_top<P, SC>(c, c.szt - 1);
+    return c.htr ? ie_px(c.top + c.szt + min(k, c.ntr - 1)) : ie_top<P>(c, c.szt - 1);
 }
 
 // the unit's rewritten angle field: angle | smooth << 9 | edge filter << 10

@@ -24,6 +24,7 @@
 // right columns from the pre-LR picture (what lr_sbrow backs up).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -47,27 +48,20 @@ template <int BPC> struct LrArgs {
     const P *left;    // [h][4]; null: the columns left of the unit are src's
     int ss, ds, ts, bs;
     int w, h, edges, kind, bdmax;   // kind: 0 wiener, 1 sgr 5x5, 2 sgr 3x3, 3 mix
-    int vec;                        // every pointer and pitch 16-byte aligned (DGPU_LR_VEC)
+    int vec;                        // every pointer and pitch 16-byte aligned
     Dav1dGpuLrParams prm;
 };
 
 constexpr int kLrVH = 66;   // A / B rows: unit rows -1..64
 
-// DGPU_LR_VEC (bits): full 32-column strips on 16-byte-aligned planes move
-// their pixels in 16-byte pieces instead of one pixel per lane: 1 the copied
-// (unrestored) strips, 2 the tile's 32 interior columns (the 3 + 3 padding
-// columns keep the per-pixel padding() code), 4 the outputs (staged in LDS,
-// then stored whole rows)
-#ifndef DGPU_LR_VEC
-#define DGPU_LR_VEC 3   // (4, the LDS-staged outputs, measured slower: two more barriers)
-#endif
-// DGPU_LR_PF (bits): the self-guided A / B loop 1 issues the next tile
-// row's LDS reads before the current row's arithmetic (measured slower), 2
-// is unrolled by two (the default: 47.8-48.0 against 48.8-49.3 us on three
-// boxes, profiles/r5/r5z_lr_unroll_ab.json)
-#ifndef DGPU_LR_PF
-#define DGPU_LR_PF 2
-#endif
+// Full 32-column strips on 16-byte-aligned planes (`vec`) move their pixels
+// in 16-byte pieces instead of one pixel per lane: the copied (unrestored)
+// strips and the tile's 32 interior columns (the 3 + 3 padding columns keep
+// the per-pixel padding() code).  Measured and deleted in round 6: outputs
+// staged in LDS and stored as whole rows (two more barriers, slower), the
+// next tile row's LDS reads issued one A / B iteration ahead (slower); the
+// A / B loop stays unrolled by two (47.8-48.0 against 48.8-49.3 us,
+// profiles/r5/r5z_lr_unroll_ab.json).
 
 // A / B of selfguided_filter (:373-392) from one position's box sum and sum
 // of squares (n = 25 or 9), with the reference's unsigned arithmetic
@@ -82,20 +76,6 @@ __device__ __forceinline__ void lr_ab_sums(int sum, int sumsq, unsigned s, int b
     const unsigned x = x_by_x[min(z, 255u)];   // the block's LDS copy
     A = (int)((x * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
     B = (int)x;
-}
-
-// DGPU_LR_VEC & 4: the strip's h x 32 outputs, staged in LDS at a 32-pixel
-// pitch by every thread, to the picture in 16-byte pieces
-template <int BPC>
-__device__ __forceinline__ void lr_store_rows(const LrArgs<BPC> &a, int x0, const typename Px<BPC>::pixel *o) {
-    using P = typename Px<BPC>::pixel;
-    constexpr int N = 16 / (int)sizeof(P), PR = kLrSW / N;
-    __syncthreads();
-    for (int t = threadIdx.x; t < a.h * PR; t += 256) {
-        const int j = t / PR, k = t % PR;
-        *reinterpret_cast<uint4 *>(a.dst + (size_t)j * a.ds + x0 + k * N) =
-            reinterpret_cast<const uint4 *>(o + j * kLrSW)[k];
-    }
 }
 
 // One 32-column strip (columns x0.. of the unit) of one stripe.
@@ -128,7 +108,7 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     const int bd8 = bits_of(a.bdmax) - 8;
     // a full strip on aligned planes (workgroup-uniform)
     const bool vec = a.vec && sw == kLrSW;
-    if ((DGPU_LR_VEC & 2) && vec) {   // the 32 interior columns read no padding: 16-byte row pieces
+    if (vec) {   // the 32 interior columns read no padding: 16-byte row pieces
         constexpr int PR = kLrSW * (int)sizeof(P) / 16, NV = (kLrTH * PR + 255) / 256;   // pieces per row
         const bool ht = a.edges & DGPU_LR_HAVE_TOP, hb = a.edges & DGPU_LR_HAVE_BOTTOM;
         uint4 pv[NV];
@@ -248,13 +228,11 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
 #pragma unroll
                 for (int t = 0; t < 7; t++) sum += hv[t] * a.prm.filter[1][t];
                 const P o = (P)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, a.bdmax);
-                if ((DGPU_LR_VEC & 4) && vec) reinterpret_cast<P *>(&T[0][0])[j * kLrSW + wi] = o;   // T is free here
-                else a.dst[(size_t)j * a.ds + x0 + wi] = o;
+                a.dst[(size_t)j * a.ds + x0 + wi] = o;
 #pragma unroll
                 for (int t = 0; t < 6; t++) hv[t] = hv[t + 1];
             }
         }
-        if ((DGPU_LR_VEC & 4) && vec) lr_store_rows<BPC>(a, x0, reinterpret_cast<const P *>(&T[0][0]));
         return;
     }
     // ---- self-guided (selfguided_filter, :349-440), both radii in one pass ----
@@ -286,30 +264,13 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
 #pragma unroll
             for (int k = 0; k < 4; k++) hrow(jj0 + k, h5[k + 1], q5[k + 1], h3[k + 1], q3[k + 1]);
             const unsigned s0 = a.prm.sgr.s0, s1 = a.prm.sgr.s1;
-            int nx[5];   // DGPU_LR_PF & 1: tile row jj + 4, read one iteration ahead
-            if (DGPU_LR_PF & 1)
-#pragma unroll
-                for (int k = 0; k < 5; k++) nx[k] = T[jj0 + 4][c - 2 + k];
-#if DGPU_LR_PF & 2
 #pragma unroll 2
-#endif
             for (int jj = jj0; jj < jj1; jj++) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     h5[k] = h5[k + 1], q5[k] = q5[k + 1], h3[k] = h3[k + 1], q3[k] = q3[k + 1];
                 }
-                if (DGPU_LR_PF & 1) {
-                    const int p0 = nx[0], p1 = nx[1], p2 = nx[2], p3 = nx[3], p4 = nx[4];
-                    if (jj + 1 < jj1)
-#pragma unroll
-                        for (int k = 0; k < 5; k++) nx[k] = T[jj + 5][c - 2 + k];
-                    h3[4] = p1 + p2 + p3;
-                    q3[4] = p1 * p1 + p2 * p2 + p3 * p3;
-                    h5[4] = h3[4] + p0 + p4;
-                    q5[4] = q3[4] + p0 * p0 + p4 * p4;
-                } else {
-                    hrow(jj + 4, h5[4], q5[4], h3[4], q3[4]);
-                }
+                hrow(jj + 4, h5[4], q5[4], h3[4], q3[4]);
                 if (do3) {   // n = 9: rows jj + 1 .. jj + 3 of the window
                     const int sum = h3[1] + h3[2] + h3[3], sumsq = q3[1] + q3[2] + q3[3];
                     int A, B;
@@ -399,20 +360,8 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
             const int j = wj0 + r;
             if (r >= wrpt || j >= h) break;
             v[r] = clampi(T[j + 3][wi + 3] + ((v[r] + (1 << 10)) >> 11), 0, a.bdmax);
-            if (!((DGPU_LR_VEC & 4) && vec)) a.dst[(size_t)j * a.ds + x0 + wi] = (P)v[r];
+            a.dst[(size_t)j * a.ds + x0 + wi] = (P)v[r];
         }
-    }
-    if ((DGPU_LR_VEC & 4) && vec) {   // through T once every thread has read its pixels from it
-        __syncthreads();
-        if (wj0 < h && wi < sw) {
-#pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const int j = wj0 + r;
-                if (r >= wrpt || j >= h) break;
-                reinterpret_cast<P *>(&T[0][0])[j * kLrSW + wi] = (P)v[r];
-            }
-        }
-        lr_store_rows<BPC>(a, x0, reinterpret_cast<const P *>(&T[0][0]));
     }
 }
 
@@ -431,8 +380,10 @@ template <int BPC> struct LrFrameArgs {
     int is[3], ls[3], os[3], w[3], h[3], rows[3], cols[3], log2[3], restore[3], ss_ver[3];
     int xb0, xb01;   // strip blocks of plane 0, of planes 0 + 1 (the grid has no empty chroma columns)
     int sb128, bdmax;
-    int vec;         // every plane pointer and pitch 16-byte aligned (DGPU_LR_VEC)
-    int k0;          // the first stripe run (row ranges): stripe = k0 + blockIdx.y
+    int vec;         // every plane pointer and pitch 16-byte aligned
+    int k0;          // the first stripe run (row ranges): stripe = k0 + the grid row
+    int nx, nwg;     // strips per stripe (all planes), workgroups (nx x stripes)
+    int linear;      // A/B only: the dispatcher's own order (DAV1D_GPU_LR_ORDER=linear)
 };
 
 // lr_stripe's filter parameters (src/lr_apply_tmpl.c:51-80); kind 0 wiener,
@@ -457,11 +408,6 @@ __device__ __forceinline__ int lr_params(const Dav1dGpuLrUnit &u, bool hbd, Dav1
     return !!s0 + !!s1 * 2;
 }
 
-// DGPU_LR_ABL (cost-model probes, wrong output): 1 copies the self-guided
-// units, 2 the Wiener units
-#ifndef DGPU_LR_ABL
-#define DGPU_LR_ABL 0
-#endif
 // One (plane, stripe, 32-column strip): stripes are 64 rows (the first 8
 // luma rows shorter, :45-46), units unit_size columns (the last takes the
 // rest, :135-166) and a superblock row's unit row is chosen as lr_sbrow does
@@ -469,11 +415,20 @@ __device__ __forceinline__ int lr_params(const Dav1dGpuLrUnit &u, bool hbd, Dav1
 template <int BPC>
 __global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     using P = typename Px<BPC>::pixel;
-    const int bx = blockIdx.x, pl = bx < f.xb0 ? 0 : bx < f.xb01 ? 1 : 2;
+    // XCD-contiguous order (the frame read 3.0x its picture):
+    // workgroups are dealt round-robin over the 8 XCDs, so logical workgroup
+    // (b % 8) * (nb / 8) + b / 8 gives each XCD a contiguous run of stripes;
+    // the 4-5 strips that share a 128-B picture line (32 px, plus the 3 + 3
+    // halo columns) and the rows stripes share then meet in one L2 instead
+    // of being fetched once per XCD
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int lb = f.linear ? b : (b & 7) * (nb >> 3) + (b >> 3);   // (A/B: DAV1D_GPU_LR_ORDER=linear)
+    if (lb >= f.nwg) return;
+    const int by = lb / f.nx, bx = lb - by * f.nx, pl = bx < f.xb0 ? 0 : bx < f.xb01 ? 1 : 2;
     const int w = f.w[pl], h = f.h[pl], sv = f.ss_ver[pl];
     const int xs = (bx - (pl == 0 ? 0 : pl == 1 ? f.xb0 : f.xb01)) * kLrSW;
     if (xs >= w) return;
-    const int S64 = 64 >> sv, S8 = 8 >> sv, k = f.k0 + (int)blockIdx.y;
+    const int S64 = 64 >> sv, S8 = 8 >> sv, k = f.k0 + by;
     const int y0 = k ? k * S64 - S8 : 0, y1 = min((k + 1) * S64 - S8, h);
     if (y0 >= h) return;
     const int us = 1 << f.log2[pl];
@@ -487,9 +442,9 @@ __global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     const Dav1dGpuLrUnit &u = f.units[pl][(size_t)urow * f.cols[pl] + ucol];
     const P *src = f.in[pl] + (size_t)y0 * f.is[pl];
     P *dst = f.out[pl] + (size_t)y0 * f.os[pl];
-    if (!f.restore[pl] || u.type == 0 || ((DGPU_LR_ABL & 1) && u.type > 2) || ((DGPU_LR_ABL & 2) && u.type == 2)) {   // copied
+    if (!f.restore[pl] || u.type == 0) {   // copied
         const int sw = min(kLrSW, w - xs), n = (y1 - y0) * kLrSW;   // <= 64 rows x 32
-        if ((DGPU_LR_VEC & 1) && f.vec && sw == kLrSW) {   // 16-byte pieces, loads first
+        if (f.vec && sw == kLrSW) {   // 16-byte pieces, loads first
             constexpr int N = 16 / (int)sizeof(P), PR = kLrSW / N, NV = (64 * PR + 255) / 256;
             const int nv = (y1 - y0) * PR;
             uint4 cv[NV];
@@ -586,14 +541,24 @@ static int launch_lr_frame(const Dav1dGpuLrFrame *F, hipStream_t stream) {
     const int r0 = F->row_start, r1 = F->row_end;
     if (r0 < 0 || r1 < 0 || (r0 & 63) || (r1 & 63) || (r1 && r1 <= r0)) return -1;
     f.k0 = r0 >> 6;
-    stripes = min(stripes, r1 ? r1 >> 6 : stripes) - f.k0;
+    // the range holding the last superblock row filters down to the picture's
+    // bottom (dav1d_lr_sbrow: not_last = 0, row_h = h, src/lr_apply_tmpl.c:
+    // 174-191), i.e. every stripe from k0 on, also the one starting 8 rows
+    // above a 64-row multiple (h % 64 in {0, 57..63})
+    const bool last = r1 && r1 >= ((f.h[0] + 63) & ~63);
+    stripes = min(stripes, r1 && !last ? r1 >> 6 : stripes) - f.k0;
     if (stripes <= 0) return 0;   // (a range past the picture)
     int xb[3] = {0, 0, 0};
     for (int p = 0; p < np; p++) xb[p] = (f.w[p] + kLrSW - 1) / kLrSW;
     f.xb0 = xb[0];
     f.xb01 = xb[0] + xb[1];
-    const dim3 grid((unsigned)(xb[0] + xb[1] + xb[2]), (unsigned)stripes, 1);
-    k_lr_frame<BPC><<<grid, 256, 0, stream>>>(f);
+    f.nx = xb[0] + xb[1] + xb[2];
+    {
+        const char *e = getenv("DAV1D_GPU_LR_ORDER");
+        f.linear = e && !strcmp(e, "linear");
+    }
+    f.nwg = f.nx * stripes;
+    k_lr_frame<BPC><<<(unsigned)((f.nwg + 7) & ~7), 256, 0, stream>>>(f);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         fprintf(stderr, "dav1d-gpu: loop restoration launch failed: %s\n", hipGetErrorString(e));

@@ -307,22 +307,16 @@ __global__ __launch_bounds__(256) void k_resize(ResizeArgs<BPC> a) {
 // row's loads in flight together), then each lane filters four outputs
 // (x0 + lane + 64 k) per row from LDS with the 8 taps of resize_c.
 constexpr int kRzOut = 256, kRzSpan = kRzOut + 16;
-#ifndef DGPU_RZ_ROWS
-#define DGPU_RZ_ROWS 1   // 2 rows per wave measured 27.6 against 26.8 us: no gain
-#endif
-constexpr int kRzRows = DGPU_RZ_ROWS;   // rows per wave
-// DGPU_RZ_VEC (experiment): a lane computes 4 neighbouring outputs and stores
-// them as one 4-pixel word (one store instruction per row instead of four)
-#ifndef DGPU_RZ_VEC
-#define DGPU_RZ_VEC 0
-#endif
+// Rows per wave: 2 measured 27.6 against 26.8 us; 4 neighbouring outputs
+// per lane stored as one 4-pixel word 27.3 against 27.2 (both deleted in
+// round 6).
+constexpr int kRzRows = 1;
 template <int BPC> struct ResizeFrameArgs {
     typename Px<BPC>::pixel *dst[3];
     const typename Px<BPC>::pixel *src[3];
     int ds[3], ss[3];   // pixels
     int dst_w[3], src_w[3], h[3], dx[3], mx0[3];
     int bdmax;
-    int vec;            // every output plane and pitch 4-pixel aligned (DGPU_RZ_VEC)
 };
 template <int BPC>
 __global__ __launch_bounds__(256) void k_resize_frame(ResizeFrameArgs<BPC> a) {
@@ -358,32 +352,6 @@ __global__ __launch_bounds__(256) void k_resize_frame(ResizeFrameArgs<BPC> a) {
         if (y0 + r >= hh) break;
         const P *t = span[w][r];
         P *d = a.dst[p] + (size_t)(y0 + r) * a.ds[p];
-        if (DGPU_RZ_VEC && a.vec) {
-            const int xb = x0 + 4 * l;
-            int o[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int pos = mx0 + (xb + j) * dx;
-                const P *c = t + ((pos >> 14) - 4 - s0);
-                const signed char *f = &dspt_resize[((pos & 0x3fff) >> 8) * 8];
-                int sum = 0;
-#pragma unroll
-                for (int i = 0; i < 8; i++) sum += f[i] * (int)c[i];
-                o[j] = clampi((-sum + 64) >> 7, 0, a.bdmax);
-            }
-            if (xb + 3 < dw) {
-                if constexpr (BPC == 8)
-                    *reinterpret_cast<uint32_t *>(d + xb) = (uint32_t)o[0] | o[1] << 8 | o[2] << 16 | (uint32_t)o[3] << 24;
-                else
-                    *reinterpret_cast<uint2 *>(d + xb) = make_uint2((uint32_t)o[0] | (uint32_t)o[1] << 16,
-                                                                     (uint32_t)o[2] | (uint32_t)o[3] << 16);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (xb + j < dw) d[xb + j] = (P)o[j];
-            }
-            continue;
-        }
 #pragma unroll
         for (int k = 0; k < kRzOut / 64; k++) {
             const int x = x0 + l + 64 * k;
@@ -427,8 +395,6 @@ static int launch_resize_frame(const Dav1dGpuResizeFrame *f, hipStream_t stream)
         gh = max(gh, (i.h + 4 * kRzRows - 1) / (4 * kRzRows));
     }
     a.bdmax = BPC == 8 ? 255 : f->bitdepth_max;
-    a.vec = 1;
-    for (int p = 0; p < np; p++) a.vec &= !((uintptr_t)a.dst[p] & (4 * B - 1)) && !(f->out[p].stride & (4 * B - 1));
     k_resize_frame<BPC><<<dim3(gw, gh, np), 256, 0, stream>>>(a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -39,15 +39,11 @@ template <int... TX> constexpr uint64_t pack_log2_lanes(std::integer_sequence<in
 }
 constexpr uint64_t kLog2Lanes = pack_log2_lanes(std::make_integer_sequence<int, DGPU_N_RECT_TX_SIZES>());
 
-#ifndef DGPU_ONLY_CLASS
-#define DGPU_ONLY_CLASS -1   // build-time probe: compile a single class (resource studies)
-#endif
 template <int BPC, int TX, int GRP, typename WaitT = NoWait>
 __device__ __forceinline__ void run_class(const ReconArgs<BPC> &a, const PlaneTab<BPC> &pt, const Dav1dGpuUnit &u,
                                           const Dav1dGpuIntraEdge &rec, int first, int count, uint8_t *lds, int gw,
                                           const WaitT &wait = WaitT()) {
-    if constexpr (TX < DGPU_N_RECT_TX_SIZES && in_group(TX, GRP) &&
-                  (DGPU_ONLY_CLASS < 0 || TX == DGPU_ONLY_CLASS)) {
+    if constexpr (TX < DGPU_N_RECT_TX_SIZES && in_group(TX, GRP)) {
         if constexpr (GRP == GROUP_WARP) {
             // the second launch: w_mask / OBMC / scaled units in their own
             // function, warp and inter-intra in recon_units (per unit: a wave
@@ -85,11 +81,8 @@ static_assert(DGPU_N_RECT_TX_SIZES == 19, "dispatch switch lists 19 classes");
 // and group: 5 for the 8-bit main group (small + large classes) fits in 96
 // VGPRs without spills (left alone it takes ~102, 4 waves: measured 2 us
 // slower); the others are left to the compiler (forcing them spills).
-#ifndef DGPU_WPE_SMALL8
-#define DGPU_WPE_SMALL8 5
-#endif
 template <int BPC, int GRP> constexpr int min_waves_per_eu() {
-    return (BPC == 8 && GRP == GROUP_SMALL) ? DGPU_WPE_SMALL8 : 1;
+    return (BPC == 8 && GRP == GROUP_SMALL) ? 5 : 1;
 }
 
 template <int BPC, int GRP>
@@ -208,16 +201,8 @@ __attribute__((amdgpu_waves_per_eu(min_waves_per_eu<BPC, GRP>()))) void k_recon(
     dispatch<BPC, GRP>(a, pt, u, rec, cls, first, count, lds + wave * WL, gw);
 }
 
-// DGPU_PERSIST (round 5 experiment): the main group as
-// resident waves walking the wave schedule (csrc/recon_persist.hpp); measured
-// slower, so product builds leave it out
-#ifndef DGPU_PERSIST
-#define DGPU_PERSIST 0
-#endif
-#if DGPU_PERSIST
-template <int BPC, int GRP> __global__ void k_recon_p(ReconArgs<BPC> a);
-template <int BPC, int GRP> static int persist_blocks(int lds);
-#endif
+// (round 5: the main group as resident waves walking this schedule measured
+// 84-477 us against 56; deleted in round 6)
 
 template <int BPC, int GRP>
 static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned classmask, hipStream_t stream) {
@@ -248,25 +233,7 @@ static int launch_group(ReconArgs<BPC> &a, const Dav1dGpuFrameBatch *b, unsigned
     static std::once_flag once;
     std::call_once(once, [] {
         (void)hipFuncSetAttribute((const void *)k_recon<BPC, GRP>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-#if DGPU_PERSIST
-        if constexpr (GRP == GROUP_SMALL)
-            (void)hipFuncSetAttribute((const void *)k_recon_p<BPC, GRP>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-#endif
     });
-#if DGPU_PERSIST
-    if constexpr (GRP == GROUP_SMALL) {
-        const int res = persist_blocks<BPC, GRP>(lds);
-        if (res >= 8) {
-            k_recon_p<BPC, GRP><<<dim3(min(nblk, res)), 64 * WPB, lds, stream>>>(a);
-            const hipError_t e = hipGetLastError();
-            if (e != hipSuccess) {
-                fprintf(stderr, "dav1d-gpu: recon launch failed: %s\n", hipGetErrorString(e));
-                return -3;
-            }
-            return 0;
-        }
-    }
-#endif
     k_recon<BPC, GRP><<<dim3(nblk), 64 * WPB, lds, stream>>>(a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -380,6 +347,3 @@ static int launch(const Dav1dGpuFrameBatch *b, hipStream_t stream) {
 
 }  // namespace dgpu
 
-#if DGPU_PERSIST
-#include "recon_persist.hpp"
-#endif

@@ -38,61 +38,22 @@
 
 #include <utility>
 
-// Profiling-only phase ablations (tools/build_variants.sh); all 0 in the
-// product build.  Outputs are wrong when any is set.
-#ifndef DGPU_ABL_MC
-#define DGPU_ABL_MC 0      // skip the mc h/v passes
-#endif
-#ifndef DGPU_ABL_ITX
-#define DGPU_ABL_ITX 0     // skip the row/column transforms
-#endif
-#ifndef DGPU_ABL_INTRA
-#define DGPU_ABL_INTRA 0   // skip intra edge preparation and prediction
-#endif
-#ifndef DGPU_ABL_STORE
-#define DGPU_ABL_STORE 0   // skip the picture stores (probe)
-#endif
-#ifndef DGPU_EARLY_REF1
-#define DGPU_EARLY_REF1 0  // issue the second ref's footprint loads up front
+#ifndef DGPU_TRACE
+#define DGPU_TRACE 0       // diagnostics: per-wave phase timestamps (tools/wave_trace.py)
 #endif
 #ifndef DGPU_TRACE_RT
-#define DGPU_TRACE_RT 0
-#endif
-#ifndef DGPU_TRACE
-#define DGPU_TRACE 0       // per-wave phase timestamps (tools/wave_trace.py)
-#endif
-#ifndef DGPU_ROWSKIP
-// skip footprint rows no vertical tap reads (HPass::load): measured slower
-// at both bitdepths (60 -> 63 us 8-bit with a 20 B/lane spill, 83.5 -> 86
-// us 10-bit), so off; kept as a knob
-#define DGPU_ROWSKIP 0
-#endif
-#ifndef DGPU_ALIGNED_ROWS8
-#define DGPU_ALIGNED_ROWS8 1    // 8bpc footprint rows by aligned loads + v_alignbyte (see HPass)
-#endif
-#ifndef DGPU_VODD_ALIGN
-#define DGPU_VODD_ALIGN 0   // odd vertical rows by realigned pairs (the round-1/2 form) instead of shifted taps
-#endif
-#ifndef DGPU_RES_PAD
-#define DGPU_RES_PAD 0   // experiment: padded residual columns (Slot::RS)
-#endif
-#ifndef DGPU_ALIGNED_ROWS16
-#define DGPU_ALIGNED_ROWS16 0   // 16bpc: register pressure spills with it (measured), off
+#define DGPU_TRACE_RT 0    // diagnostics: the trace in the 100 MHz clock of the flow trace
 #endif
 
 namespace dgpu {
 
-#ifndef DGPU_SEGMENTS
-#define DGPU_SEGMENTS 16
-#endif
-#ifndef DGPU_SEQREF_MAX_TPL
-#define DGPU_SEQREF_MAX_TPL 2
-#endif
-#ifndef DGPU_SEG_INNER
-#define DGPU_SEG_INNER 1
-#endif
-constexpr int kSegments = DGPU_SEGMENTS;   // spatial segments per class (task ordering)
-constexpr int kSegInner = DGPU_SEG_INNER;  // segments whose classes are scheduled as one group
+// Measured variants of this kernel that lost (phase ablations, row skipping,
+// realigned odd rows, padded residual columns, aligned 16bpc rows, paired
+// 8-byte stores, nontemporal streams, resident waves) were deleted in round
+// 6; their A/B results stay under profiles/r3..r5 and in DESIGN.md.
+constexpr int kSegments = 16;      // spatial segments per class (task ordering; 8 / 32: 67 / 64 us)
+constexpr int kSegInner = 1;       // segments whose classes are scheduled as one group
+constexpr int kSeqRefMaxTpl = 2;   // compound refs one after the other through one tile up to this many tasks per lane
 
 template <int BPC> struct ReconArgs {
     using P = typename Px<BPC>::pixel;
@@ -172,12 +133,6 @@ __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 // than the 1-D transform passes can use (max(W, min(H, 32)) lines), 2..64;
 // 32x32 takes a whole wave so its LDS slot (9 KB) does not set the budget
 // of the large group
-#ifndef DGPU_TALL_LANES
-#define DGPU_TALL_LANES 1
-#endif
-#ifndef DGPU_ST8
-#define DGPU_ST8 0
-#endif
 #ifndef DGPU_IE_SMALL_LANES
 // lanes per unit of the 4x4 / 4x8 / 8x4 classes, for the intra wavefront
 // TUs (recon_ie{8,16}.hip set 8; 0 here: the class's own count).  Above level
@@ -193,22 +148,31 @@ __host__ __device__ constexpr int lanes_per_unit(int tx) {
     // many for 8x32), so the column transforms leave no lane idle, within
     // the 8 KB-per-wave LDS budget of the main group (round 3; the rule
     // below gives 16 / 8 / 32 lanes, half of them idle in the column pass)
-    if (DGPU_TALL_LANES && w == 8 && h == 16) return 8;
-    if (DGPU_TALL_LANES && w == 4 && h == 16) return 4;
-    if (DGPU_TALL_LANES && w == 8 && h == 32) return 16;
+    if (w == 8 && h == 16) return 8;
+    if (w == 4 && h == 16) return 4;
+    if (w == 8 && h == 32) return 16;
     return cmin(cmax(cmin(w * h / 8, cmax(w, cmin(h, 32))), 2), 64);
 }
+// HPass advances a lane's row pairs by G / QW from a first pair l / QW: every
+// class a product kernel runs has at most as many lane rows as footprint row
+// pairs (G / QW <= RP), so no lane starts past the footprint (the r5j fault:
+// a negative row-pair offset through an unsigned 24-bit multiply).  Only the
+// wavefront TUs' small-unit lanes (DGPU_IE_SMALL_LANES) exceed it, and HPass
+// clamps their base pair at compile time for exactly that case.
+__host__ __device__ constexpr bool lanes_fit_row_pairs() {
+    for (int tx = 0; tx < DGPU_N_RECT_TX_SIZES; tx++) {
+        const int w = tx_info(tx).w, h = tx_info(tx).h;
+        if (DGPU_IE_SMALL_LANES && w * h <= 32) continue;
+        if (lanes_per_unit(tx) % (w / 4) || lanes_per_unit(tx) / (w / 4) > (h + 8) / 2) return false;
+    }
+    return true;
+}
+static_assert(lanes_fit_row_pairs(), "a product class gives a unit more lane rows than footprint row pairs");
 // class groups, each its own kernel with its own register / LDS budget:
 // small (w*h <= 128), large (up to 32x32), huge (the 64-point sides).
-// By default (DGPU_MERGE_GROUPS) small and large are one launch: the large
-// classes' long-latency waves then overlap the small classes' work
-// (measured 76 -> 64 us per 4K frame against two launches back to back).
-#ifndef DGPU_MERGE_GROUPS
-#define DGPU_MERGE_GROUPS 1
-#endif
-#ifndef DGPU_IE_NOGATHER
-#define DGPU_IE_NOGATHER 0   // probe only: no edge gather in the intra wavefront kernels
-#endif
+// Small and large are one launch: the large classes' long-latency waves
+// then overlap the small classes' work (measured 76 -> 64 us per 4K frame
+// against two launches back to back); GROUP_LARGE stays as a name only.
 enum { GROUP_SMALL = 0, GROUP_LARGE = 1, GROUP_HUGE = 2, GROUP_WARP = 3, N_GROUPS = 4,
        // the intra wavefront's variants of SMALL / HUGE: edges gathered in
        // the kernel (intra_edge_dev.hpp) instead of read from the edge pool
@@ -222,7 +186,7 @@ __host__ __device__ constexpr bool gathers(int grp) { return grp >= N_GROUPS; }
 __host__ __device__ constexpr int class_group(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
     return (w == 64 || h == 64) ? GROUP_HUGE
-         : (w * h <= 128 || DGPU_MERGE_GROUPS) ? GROUP_SMALL : GROUP_LARGE;
+         : GROUP_SMALL;
 }
 // Order of the classes inside one schedule segment: largest first, so
 // their long-latency waves start early.  kOrder[position] = class.
@@ -260,7 +224,7 @@ template <int TX> struct Cls {
     static constexpr int TPL = (NT + G - 1) / G;  // output tasks per lane
     // compound refs run one after the other through one intermediate tile,
     // the first ref's predictions held in registers across the second
-    static constexpr bool SEQREF = TPL <= DGPU_SEQREF_MAX_TPL;
+    static constexpr bool SEQREF = TPL <= kSeqRefMaxTpl;
 };
 
 template <int BPC> struct Tmp { using T = int32_t; };
@@ -274,12 +238,10 @@ template <int BPC, int TX> struct Slot {
     static constexpr int CB = sizeof(typename Px<BPC>::coef);
     static constexpr int TB = sizeof(typename Tmp<BPC>::T);
     static constexpr int CF = a16(CL::SW * CL::SH * CB + 16);   // compact coefs at their 16-B skew
-    // residual, column-major [x][y] with a column stride of RS elements:
-    // DGPU_RES_PAD pads the 8-bit columns of 8 and more rows by 4, so the
-    // column pass's 8-byte writes and the tasks' 4-byte reads of one lane
-    // group fall on distinct banks (a 16-row column is 8 dwords: 4-way
-    // conflicts; 32 rows: 8-way)
-    static constexpr int RS = H + ((DGPU_RES_PAD && BPC == 8 && H >= 8) ? 4 : 0);
+    // residual, column-major [x][y] with a column stride of RS elements
+    // (padding the columns against the 4/8-way bank conflicts measured no
+    // gain: 56.0 against 56.1 us, profiles/r5/r5c_krecon_ab.json)
+    static constexpr int RS = H;
     static constexpr int RES = W * RS * TB;
     static constexpr int CFR = a16(cmax(CF, RES));
     static constexpr int TMP = a16(CL::SH * W * TB);             // row-pass output [y][x]
@@ -483,21 +445,6 @@ template <typename T> __device__ __forceinline__ void bst(T *p, T v DGPU_LINE) {
 template <typename T> __device__ __forceinline__ void bnd_touch(const T *p DGPU_LINE) {
     DGPU_CHK(p, (int)sizeof(T), return);
 }
-// The intra wavefront's acquire-free hand-off (DGPU_FLOW_SC1, flow_impl.hpp):
-// in GATHER builds every picture / top_edge store is write-through (sc1) and
-// every load of those bytes an sc1 load, the MI355X guide's "Valid forms"
-// row 1 (producer: sc1 stores, vmcnt(0), agent-scope flag; consumer: sc1
-// poll, sc1 loads, no buffer_inv).  Off by default: kept behind the flag
-// until measured and validated under load.
-#ifndef DGPU_FLOW_SC1
-#define DGPU_FLOW_SC1 0
-#endif
-template <typename T> __device__ __forceinline__ void st_sc1(void *p, T v) {
-    __hip_atomic_store((__attribute__((address_space(1))) T *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T> __device__ __forceinline__ T ld_sc1(const void *p) {
-    return __hip_atomic_load((const __attribute__((address_space(1))) T *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // ({hi, lo} >> 8s)[31:0]
 __device__ __forceinline__ uint32_t alb(uint32_t hi, uint32_t lo, int s) {
@@ -565,9 +512,6 @@ __device__ __forceinline__ void vdot5x4(const uint32_t (*a)[4], const uint32_t *
 // with 16-byte loads, in two steps so other loads can be issued in between:
 // load() issues the global loads, commit() writes LDS and returns the skew.
 // Reads stay inside the 16-B blocks holding the first and last byte.
-#ifndef DGPU_NT_STREAM
-#define DGPU_NT_STREAM 0   // experiment: read-once streams (coefficients, edges) by nontemporal loads
-#endif
 template <int MAXN, int G> struct Stage {
     static constexpr int IT = ((MAXN + 30) / 16 + G - 1) / G;
     u32x4 v[IT];
@@ -577,13 +521,8 @@ template <int MAXN, int G> struct Stage {
         const uint8_t *s = reinterpret_cast<const uint8_t *>(src) - sk;
         nch = (sk + n + 15) >> 4;   // >= 1 for n >= 1
 #pragma unroll
-        for (int k = 0; k < IT; k++) {   // clamped
-#if DGPU_NT_STREAM
-            v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(s + 16 * min(l + k * G, nch - 1)));
-#else
+        for (int k = 0; k < IT; k++)   // clamped
             v[k] = gld<u32x4>(s + 16 * min(l + k * G, nch - 1));
-#endif
-        }
     }
     __device__ __forceinline__ int commit(uint8_t *dst, int l) const {
 #pragma unroll
@@ -894,15 +833,13 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
     static constexpr int PS = G / QW;   // row-pair step per task
     static_assert(G % QW == 0, "lane quads must be fixed");
     static constexpr int B = BPC / 8;
-#ifndef DGPU_CH16
-#define DGPU_CH16 2
-#endif
-    static constexpr int CH = cmin(IT, BPC == 8 ? 3 : DGPU_CH16);   // tasks whose loads are in flight together
+    static constexpr int CH = cmin(IT, BPC == 8 ? 3 : 2);   // tasks whose loads are in flight together
     // 8bpc rows are read with dword-aligned loads from the row's dword and
     // realigned in registers (v_alignbyte by the byte skew): the texture
     // path splits an unaligned multi-dword load, measured 2.4-3.3x the cost
-    // of an aligned one (tools/probe/ta_rate.hip)
-    static constexpr bool AL = BPC == 8 ? DGPU_ALIGNED_ROWS8 : DGPU_ALIGNED_ROWS16;
+    // of an aligned one (tools/probe/ta_rate.hip); 16bpc rows the same way
+    // spilled (measured), so they stay unaligned 24-byte loads
+    static constexpr bool AL = BPC == 8;
     typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
     using Raw = typename std::conditional<AL, u32x4, typename std::conditional<BPC == 8, u32x3a1, u32x4a2>::type>::type;
     using RawB = typename std::conditional<AL, u32x3, u32x2a2>::type;   // 16bpc: the row's tail
@@ -916,7 +853,6 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
     int prow;            // the row pair rp points at (p0, or the last one, see init)
     uint4 th;            // taps: 8bpc .x/.y int8 x4, 16bpc int16 pairs
 
-    int rlo, rhi;        // footprint rows the vertical taps read (others are not loaded)
     // CLAMPABLE (the second launch): a DGPU_MX_CLAMP reference, every
     // footprint pixel read at its position clamped to the plane, as
     // emu_edge_c provides them (src/mc_tmpl.c:827-875, src/recon_tmpl.c:
@@ -928,7 +864,7 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
     const uint8_t *cbase;    // the plane's (0, 0)
     __device__ __forceinline__ void init_clamp(const typename Px<BPC>::pixel *plane, int stride_px, int w, int h,
                                                int x, int y, uint32_t *mid, int bank, int m, int l) {
-        init(plane, stride_px, mid, bank, m, l, 0, H + 7);
+        init(plane, stride_px, mid, bank, m, l);
         cl = true;
         const int q = l % QW;
         cbase = reinterpret_cast<const uint8_t *>(plane);
@@ -976,9 +912,7 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
         }
     }
     __device__ __forceinline__ void init(const typename Px<BPC>::pixel *org, int stride_px, uint32_t *mid, int bank,
-                                         int m, int l, int rlo_, int rhi_) {
-        rlo = rlo_;
-        rhi = rhi_;
+                                         int m, int l) {
         sb = (unsigned)stride_px * B;
         const int q = l % QW;
         p0 = l / QW;
@@ -1015,49 +949,17 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
         for (int c = 0; c < CH; c++) {   // clamped: the loads stay inside the footprint
             const int pu = p0 + (k0 + c) * PS;
             const int p = cmin(pu, RP - 1);
-            // a row is loaded only when its task exists and a vertical tap
-            // reads it (4-tap and bilinear banks, m == 0, the unused row
-            // H+7): skipped rows are zero, and meet zero taps
-            const bool task = k0 + c < IT && pu < RP;
-            const bool n0 = !DGPU_ROWSKIP || (task && 2 * p >= rlo && 2 * p <= rhi);
-            const bool n1 = !DGPU_ROWSKIP || (task && 2 * p + 1 >= rlo && 2 * p + 1 <= rhi);
+            // every footprint row is loaded, also those no vertical tap reads
+            // (skipping them measured slower: 60 -> 63 us with a spill)
             const uint8_t *a0 = rp + (size_t)__umul24((unsigned)(p - (PS > RP ? prow : p0)) * 2u, sb);
             // row 2p+1 == H+7 (last pair) is never used: re-read row 2p
             const uint8_t *a1 = 2 * p + 1 < H + 7 ? a0 + sb : a0;
-#ifdef DGPU_FAKE_COALESCE
-            (void)a1;
-#endif
-#ifdef DGPU_FAKE_COALESCE   // cost-model probe: every lane reads lane 0's rows (wrong output)
-            {
-                const uint64_t av = reinterpret_cast<uint64_t>(a0);
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)av);
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(av >> 32));
-                a0 = reinterpret_cast<const uint8_t *>(((uint64_t)hi << 32) | (uint64_t)lo);
-            }
-            a1 = a0;
-#endif
-#ifndef DGPU_FAKE_COALESCE
-            // zero first, then an exec-masked load into the same registers
-            ra[c][0] = Raw{};
-            ra[c][1] = Raw{};
-            if (n0) ra[c][0] = gld<Raw>(a0);
-            if (n1) ra[c][1] = gld<Raw>(a1);
-            if constexpr (BPC == 16) {
-                rb[c][0] = RawB{};
-                rb[c][1] = RawB{};
-                if (n0) rb[c][0] = gld<RawB>(a0 + 16);
-                if (n1) rb[c][1] = gld<RawB>(a1 + 16);
-            }
-#else
-            (void)n0;
-            (void)n1;
             ra[c][0] = gld<Raw>(a0);
             ra[c][1] = gld<Raw>(a1);
             if constexpr (BPC == 16) {
                 rb[c][0] = gld<RawB>(a0 + 16);
                 rb[c][1] = gld<RawB>(a1 + 16);
             }
-#endif
         }
     }
     __device__ __forceinline__ void compute(int k0, int ib) {
@@ -1137,38 +1039,19 @@ __device__ __forceinline__ void mc_vtask(const uint32_t *mid, int j, int q, cons
         P[k][0] = v.x; P[k][1] = v.y; P[k][2] = v.z; P[k][3] = v.w;
     }
     vdot4x4(P, tv, kk, sh, t);
-#if DGPU_VODD_ALIGN   // odd rows on realigned pairs (row 2j+1+2k, row 2j+2+2k)
-    uint32_t O[4][4];
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) O[k][i] = alb(P[k + 1][i], P[k][i], 2);
-    vdot4x4(O, tv, kk, sh, t + 4);
-#else
-    uint32_t so[5];
+    uint32_t so[5];   // odd rows: the same pairs with shifted taps (vtaps_odd)
     vtaps_odd(tv, so);
     vdot5x4(P, so, kk, sh, t + 4);
-#endif
 }
 
 // ------------------------------------------------------------------ cfl ---
 
-template <bool SC, typename P> __device__ __forceinline__ int cfl_px(const P *p) {
-    if constexpr (SC) return ie_px<true>(p);
-    else return gld<P>(p);
-}
-// 16 bytes as two 8-byte sc1 loads (the hand-off's access sizes)
-__device__ __forceinline__ u32x4 ld_sc1_x4(const void *p) {
-    const u32x2 a = __builtin_bit_cast(u32x2, ld_sc1<uint64_t>(p));
-    const u32x2 b = __builtin_bit_cast(u32x2, ld_sc1<uint64_t>(reinterpret_cast<const uint8_t *>(p) + 8));
-    return u32x4{a.x, a.y, b.x, b.y};
-}
 
 // Chroma-from-luma for one unit (the whole chroma block, square <= 32):
 // cfl_ac on the co-located luma (src/ipred_tmpl.c:657-703), then cfl_pred
 // with the DC of the edge array (:71-84, :103-218), task by task through
 // `emit`.  The 4:2:0 no-padding case sums luma pairs with packed dots.
-template <int BPC, int TX, bool SC = false, typename P, typename Emit>
+template <int BPC, int TX, typename P, typename Emit>
 __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGpuUnit &u, const P *tl, int16_t *fe,
                                           int l, int bdmax, Emit &emit) {
     using CL = Cls<TX>;
@@ -1193,28 +1076,14 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
             for (int rr = 0; rr < 2; rr++) {
                 const P *r0 = yp + __mul24(4 * j + 2 * rr, ys) + 8 * q;
                 if constexpr (BPC == 8) {
-                    u32x2 v0, v1;
-                    if constexpr (SC) {   // 8-byte aligned (x4 luma columns, 16-byte strides)
-                        v0 = __builtin_bit_cast(u32x2, ld_sc1<uint64_t>(r0));
-                        v1 = __builtin_bit_cast(u32x2, ld_sc1<uint64_t>(r0 + ys));
-                    } else {
-                        v0 = gld<u32x2a1>(r0);
-                        v1 = gld<u32x2a1>(r0 + ys);
-                    }
+                    const u32x2 v0 = gld<u32x2a1>(r0), v1 = gld<u32x2a1>(r0 + ys);
                     // byte pairs summed over both rows: dot4 with 1-masks
                     ac[k][4 * rr + 0] = (int)__builtin_amdgcn_udot4(v1.x, 0x00000101u, __builtin_amdgcn_udot4(v0.x, 0x00000101u, 0, false), false) << 1;
                     ac[k][4 * rr + 1] = (int)__builtin_amdgcn_udot4(v1.x, 0x01010000u, __builtin_amdgcn_udot4(v0.x, 0x01010000u, 0, false), false) << 1;
                     ac[k][4 * rr + 2] = (int)__builtin_amdgcn_udot4(v1.y, 0x00000101u, __builtin_amdgcn_udot4(v0.y, 0x00000101u, 0, false), false) << 1;
                     ac[k][4 * rr + 3] = (int)__builtin_amdgcn_udot4(v1.y, 0x01010000u, __builtin_amdgcn_udot4(v0.y, 0x01010000u, 0, false), false) << 1;
                 } else {
-                    u32x4 v0, v1;
-                    if constexpr (SC) {   // 16-byte aligned
-                        v0 = ld_sc1_x4(r0);
-                        v1 = ld_sc1_x4(r0 + ys);
-                    } else {
-                        v0 = gld<u32x4a2>(r0);
-                        v1 = gld<u32x4a2>(r0 + ys);
-                    }
+                    const u32x4 v0 = gld<u32x4a2>(r0), v1 = gld<u32x4a2>(r0 + ys);
                     const uint32_t d0[4] = {v0.x, v0.y, v0.z, v0.w}, d1[4] = {v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
                     for (int i = 0; i < 4; i++)
@@ -1226,11 +1095,11 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
             for (int i = 0; i < 8; i++) {
                 const int sx = min(4 * q + (i & 3), vw - 1), sy = min(2 * j + (i >> 2), vh - 1);
                 const P *p = yp + __mul24(sy << ssv, ys) + (sx << ssh);
-                int v = cfl_px<SC>(p);
-                if (ssh) v += cfl_px<SC>(p + 1);
+                int v = gld<P>(p);
+                if (ssh) v += gld<P>(p + 1);
                 if (ssv) {
-                    v += cfl_px<SC>(p + ys);
-                    if (ssh) v += cfl_px<SC>(p + ys + 1);
+                    v += gld<P>(p + ys);
+                    if (ssh) v += gld<P>(p + ys + 1);
                 }
                 ac[k][i] = v << acsh;
             }
@@ -1258,6 +1127,28 @@ __device__ __forceinline__ void cfl_units(const ReconArgs<BPC> &a, const Dav1dGp
     }
 }
 
+// The visible size of reference plane (r, plane), by a lane-varying index
+// straight from the kernel-argument segment (indexing the by-value argument
+// would copy all of it to scratch).  Only for code that runs in k_recon,
+// whose argument is the ReconArgs (the second launch's kinds).
+template <int BPC> __device__ __forceinline__ void ref_plane_wh(int r, int plane, int &rw, int &rh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __attribute__((address_space(4))) int *ka =
+        (const __attribute__((address_space(4))) int *)__builtin_amdgcn_kernarg_segment_ptr();
+    rw = ka[(offsetof(ReconArgs<BPC>, ref_w) >> 2) + r * 3 + plane];
+    rh = ka[(offsetof(ReconArgs<BPC>, ref_h) >> 2) + r * 3 + plane];
+#else
+    rw = rh = 1;
+#endif
+}
+// A pixel of a plane at (x, y) clamped to its visible w x h (emu_edge_c,
+// src/mc_tmpl.c:827-875); `base` is the plane's (0, 0), `sb` its pitch in bytes
+template <typename P>
+__device__ __forceinline__ uint32_t clamped_px(const uint8_t *base, unsigned sb, int x, int y, int w, int h) {
+    return (uint32_t)gld<P>(reinterpret_cast<const P *>(base + (size_t)__umul24((unsigned)clampi(y, 0, h - 1), sb)) +
+                            clampi(x, 0, w - 1));
+}
+
 // ----------------------------------------------------------------- warp ---
 
 // One WARP unit (w, h multiples of 8): warp_affine_8x8_c (src/mc_tmpl.c:
@@ -1276,9 +1167,15 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
     const int a2 = (int16_t)(abcd[1] & 0xffff), a3 = (int)abcd[1] >> 16;
     const int ri = u.p.inter.ref[0] * 3 + u.plane;
     // src_off[0]: a base the 8x8 positions are relative to (0, or the
-    // recorder's clamped-copy strip in its scratch plane)
-    const P *ref = pt.ref[ri] + u.p.inter.src_off[0];
+    // recorder's clamped-copy strip in its scratch plane); with
+    // DGPU_MX_CLAMP in mx[0] (round 6) the positions are the plane's own and
+    // every footprint pixel is read clamped to it, as warp_affine's
+    // emu_edge call provides it (src/recon_tmpl.c:1168-1177)
+    const bool clamp = u.p.inter.mx[0] & DGPU_MX_CLAMP;
+    const P *ref = pt.ref[ri] + (clamp ? 0 : u.p.inter.src_off[0]);
     const int rs = pt.ref_stride[ri];
+    int cw = 1, ch = 1;
+    if (clamp) ref_plane_wh<BPC>(u.p.inter.ref[0], u.plane, cw, ch);
     const int ib = Px<BPC>::ibits(bdmax);
     const int hsh = 7 - ib, hrnd = (1 << hsh) >> 1;
     constexpr int NHT = 15 * QW, NVT = 4 * QW;
@@ -1300,7 +1197,27 @@ __device__ __forceinline__ void warp_unit(const ReconArgs<BPC> &a, const PlaneTa
             mxs[k] = (int)(int16_t)(sb[1] & 0xffff) * 64;
             const int wx = (int16_t)(sb[0] & 0xffff), wy = (int)sb[0] >> 16;   // the 8x8's source position
             const P *s = ref + (wy + row - 3) * rs + wx + x0 - 3;   // columns x0-3 .. x0+7
-            if constexpr (BPC == 8) {
+            if (clamp) {   // the 12 pixels gathered at clamped positions, already aligned
+                const uint8_t *b = reinterpret_cast<const uint8_t *>(ref);
+                const unsigned sbb = (unsigned)rs * sizeof(P);
+                const int yy = wy + row - 3, xx = wx + x0 - 3;
+                uint32_t w[6];
+#pragma unroll
+                for (int i = 0; i < (BPC == 8 ? 3 : 6); i++) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int j = 0; j < 4 / (int)sizeof(P); j++)
+                        v |= clamped_px<P>(b, sbb, xx + (4 / (int)sizeof(P)) * i + j, yy, cw, ch) << (8 * sizeof(P) * j);
+                    w[i] = v;
+                }
+                shs[k] = 0;
+                if constexpr (BPC == 8) {
+                    raw[k] = u32x4{w[0], w[1], w[2], 0};
+                } else {
+                    raw[k] = u32x4a2{w[0], w[1], w[2], w[3]};
+                    raw2[k] = u32x2a2{w[4], w[5]};
+                }
+            } else if constexpr (BPC == 8) {
                 shs[k] = (unsigned)reinterpret_cast<uintptr_t>(s) & 3u;
                 raw[k] = gld<u32x4>(reinterpret_cast<const uint8_t *>(s) - shs[k]);
             } else {
@@ -1443,9 +1360,6 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     if (g >= count) return;
     // DGPU_TRACE: timestamp phase i after draining this wave's memory ops
     auto mark = [&](int i) {
-#ifdef DGPU_ASM_MARKS   // static per-phase instruction counts (tools/phase_isa.py)
-        asm volatile(";DGPU_MARK %0" ::"n"(i));
-#endif
         if constexpr (DGPU_TRACE) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             // DGPU_TRACE_RT: the 100 MHz clock of the flow trace instead of the core clock
@@ -1481,7 +1395,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
     const bool nores = txtp == DGPU_NO_RESIDUAL;
     const int nzw = u.nzw, nzh = u.nzh;
     const bool dconly = !nores && nzw == 0;
-    const bool haveres = !nores && !dconly && !DGPU_ABL_ITX;
+    const bool haveres = !nores && !dconly;
     // WHT_WHT (lossless, 4x4 units only): one lane runs both passes below
     const bool wht = W == 4 && H == 4 && txtp == DGPU_WHT_WHT;
     P *dstp = pt.dst[plane] + u.dst_off;
@@ -1539,13 +1453,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             }
         }
         const P *org = pt.ref[r * 3 + plane] + (k ? u.p.inter.src_off[1] : u.p.inter.src_off[0]) - 3 * rs - 3;
-        // footprint rows the vertical taps read: m == 0 is the identity (tap
-        // 3), bilinear taps 3..4, the 4-tap banks 2..5, 8-tap 0..7
-        const int my = k ? u.p.inter.my[1] : u.p.inter.my[0];
-        const int tf = my == 0 ? 3 : bil ? 3 : bank_v >= 3 ? 2 : 0;
-        const int tl = my == 0 ? 3 : bil ? 4 : bank_v >= 3 ? 5 : 7;
-        hp.init(org, rs, k ? mid1 : mid0, bank_h, (k ? u.p.inter.mx[1] : u.p.inter.mx[0]) & (WARPK ? 15 : 255), l, tf,
-                H - 1 + tl);
+        hp.init(org, rs, k ? mid1 : mid0, bank_h, (k ? u.p.inter.mx[1] : u.p.inter.mx[0]) & (WARPK ? 15 : 255), l);
     };
     auto hpass = [&](int k) {   // the whole h-pass of ref k
         HP hp;
@@ -1554,19 +1462,11 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         hp.compute(0, ib);
         hp.rest(ib);
     };
-    const bool do_mc = inter && !DGPU_ABL_MC;   // (WARPK: inter-intra and DGPU_MX_CLAMP inter units)
+    const bool do_mc = inter;   // (WARPK: inter-intra and DGPU_MX_CLAMP inter units)
     HP hp0;
     if (do_mc) {
         hinit(hp0, 0);
         hp0.load(0);
-    }
-    // DGPU_EARLY_REF1: the second ref's first load chunk goes out with the
-    // first's (held in registers until its h-pass after the first ref's
-    // vertical pass); otherwise it is issued when needed
-    HP hp1;
-    if (DGPU_EARLY_REF1 && CL::SEQREF && do_mc && comp) {
-        hinit(hp1, 1);
-        hp1.load(0);
     }
     // INTER_MASK / PAL: the unit's aux_pool offset (mask / palette record)
     const bool auxed = pred == DGPU_PRED_INTER_MASK || pred == DGPU_PRED_PAL || pred == DGPU_PRED_WARP || ii;
@@ -1698,7 +1598,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         wait();
     }
     IeCtx<P> iec;
-    if constexpr (GATHER && !DGPU_IE_NOGATHER) {   // dav1d_prepare_intra_edges, every entry straight into LDS
+    if constexpr (GATHER) {   // dav1d_prepare_intra_edges, every entry straight into LDS
         if (edged) {
             const PlaneTabIE<BPC> &pti = static_cast<const PlaneTabIE<BPC> &>(pt);
             iec = ie_setup<P>(rec, pt.dst[plane], ds, pti.top[plane], pti.top_stride[plane], pti.sb_log2[plane],
@@ -1712,7 +1612,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             for (int k = 0; k < EPL; k++) {
                 const int i = -2 * H + l + k * G;
                 bool need;
-                ev[k] = (i <= 2 * W && ie_need(iec, i)) ? ie_value<P, DGPU_FLOW_SC1>(iec, i, need) : -1;
+                ev[k] = (i <= 2 * W && ie_need(iec, i)) ? ie_value<P>(iec, i, need) : -1;
             }
 #pragma unroll
             for (int k = 0; k < EPL; k++)
@@ -1741,9 +1641,6 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
         if (pti.top[plane] && (y1 & ((1 << sbl) - 1)) == 0 && sby < pti.top_rows[plane])
             bkrow = pti.top[plane] + (size_t)sby * pti.top_stride[plane] + rec.x4 * 4;
     }
-    // DGPU_ST8 (experiment): neighbouring lanes (quads q, q + 1 of one task
-    // row pair) trade halves so each stores one 8-byte row piece
-    constexpr bool ST8 = DGPU_ST8 && !GATHER && !WARPK && BPC == 8 && QW >= 2 && G % 2 == 0 && !DGPU_ABL_STORE;
     auto emit = [&](int j, int q, const int *pv) {   // + residual, clip, store 2 rows of 4
         int rv[8];
         if (haveres) {
@@ -1764,25 +1661,6 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
 #pragma unroll
             for (int i = 0; i < 8; i++) rv[i] = dcres;
         }
-        if constexpr (ST8) {   // DGPU_ST8: one 8-byte row piece per lane of a (q, q + 1) pair
-            uint32_t d[2];
-#pragma unroll
-            for (int rr = 0; rr < 2; rr++) {
-                const int o0 = clampi(pv[4 * rr + 0] + rv[4 * rr + 0], 0, bdmax);
-                const int o1 = clampi(pv[4 * rr + 1] + rv[4 * rr + 1], 0, bdmax);
-                const int o2 = clampi(pv[4 * rr + 2] + rv[4 * rr + 2], 0, bdmax);
-                const int o3 = clampi(pv[4 * rr + 3] + rv[4 * rr + 3], 0, bdmax);
-                d[rr] = (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24;
-            }
-            // q and l have the same parity (QW and G even): the even lane
-            // stores row 2j of both quads, the odd lane row 2j + 1; each
-            // sends the other the half it stores (DPP quad_perm [1, 0, 3, 2])
-            const bool odd = l & 1;
-            const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? d[0] : d[1]), 0xB1, 0xF, 0xF, false);
-            P *row = dstp + __mul24(2 * j + (int)odd, ds) + 4 * (q & ~1);
-            gst<u32x2>(row, odd ? u32x2{got, d[1]} : u32x2{d[0], got});
-            return;
-        }
 #pragma unroll
         for (int rr = 0; rr < 2; rr++) {
             P *row = dstp + __mul24(2 * j + rr, ds) + 4 * q;   // 24-bit: strides < 2^23 px (full-rate multiply)
@@ -1790,15 +1668,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             const int o1 = clampi(pv[4 * rr + 1] + rv[4 * rr + 1], 0, bdmax);
             const int o2 = clampi(pv[4 * rr + 2] + rv[4 * rr + 2], 0, bdmax);
             const int o3 = clampi(pv[4 * rr + 3] + rv[4 * rr + 3], 0, bdmax);
-#if DGPU_ABL_STORE   // cost-model probe: no picture stores (values kept alive)
-            asm volatile("" ::"v"((uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24), "v"(row));
-#else
-            if constexpr (GATHER && DGPU_FLOW_SC1) {   // write-through: the wavefront's acquire-free hand-off
-                if constexpr (BPC == 8)
-                    st_sc1<uint32_t>(row, (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24);
-                else
-                    st_sc1<uint64_t>(row, (uint64_t)((uint32_t)o0 | o1 << 16) | (uint64_t)((uint32_t)o2 | (uint32_t)o3 << 16) << 32);
-            } else if constexpr (BPC == 8) {
+            if constexpr (BPC == 8) {
                 gst<uint32_t>(row, (uint32_t)o0 | o1 << 8 | o2 << 16 | (uint32_t)o3 << 24);
             } else {
                 gst<u32x2>(row, u32x2{(uint32_t)o0 | o1 << 16, (uint32_t)o2 | (uint32_t)o3 << 16});
@@ -1807,7 +1677,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             // (dav1d_backup_ipred_edge for its columns) straight from these
             // registers: reading it back from the picture after the stores
             // cost a store-to-load round trip on the wavefront's critical path
-            if constexpr (GATHER && !DGPU_FLOW_SC1) {
+            if constexpr (GATHER) {
                 if (bkrow && 2 * j + rr == H - 1) {
                     P *b = bkrow + 4 * q;
                     bst(b + 0, (P)o0);
@@ -1816,19 +1686,11 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                     bst(b + 3, (P)o3);
                 }
             }
-#endif
         }
     };
 
     if (inter && !ii) {   // (WARPK: DGPU_MX_CLAMP units)
-        if (DGPU_ABL_MC) {
-            int pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < TPL; k++) {
-                const int t = l + k * G;
-                if (t < NT) emit(t / QW, t % QW, pv);
-            }
-        } else if (comp) {   // prep x2 (rnd_sh(t, 6) - PB) then avg_c, src/mc_tmpl.c:587-602
+        if (comp) {   // prep x2 (rnd_sh(t, 6) - PB) then avg_c, src/mc_tmpl.c:587-602
             constexpr int KP = kMidBias<BPC> + 32;
             int q0[CL::SEQREF ? TPL : 1][8];
             if constexpr (CL::SEQREF) {
@@ -1843,12 +1705,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
                 }
                 wave_sync();
                 mark(6);
-                if (DGPU_EARLY_REF1) {
-                    hp1.compute(0, ib);
-                    hp1.rest(ib);
-                } else {
-                    hpass(1);
-                }
+                hpass(1);
                 wave_sync();
                 mark(7);
             }
@@ -1902,23 +1759,17 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             }
         }
     } else if (NW && pred == DGPU_PRED_INTRA) {
-        IntraState is{};
-        if (!DGPU_ABL_INTRA) {
-            is = intra_prep<BPC, TX>(u, tl, fe, l, bdmax);
-            wave_sync();
-            if (is.mode == DGPU_FILTER_PRED) filter_intra<TX>(u, tl, ptile, l, bdmax);
-            wave_sync();
-        }
+        const IntraState is = intra_prep<BPC, TX>(u, tl, fe, l, bdmax);
+        wave_sync();
+        if (is.mode == DGPU_FILTER_PRED) filter_intra<TX>(u, tl, ptile, l, bdmax);
+        wave_sync();
 #pragma unroll
         for (int k = 0; k < TPL; k++) {
             const int t = l + k * G;
             if (t >= NT) break;
             const int j = t / QW, q = t % QW;
             int pv[8];
-            if (DGPU_ABL_INTRA) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) pv[i] = 0;
-            } else if (is.mode == DGPU_FILTER_PRED) {
+            if (is.mode == DGPU_FILTER_PRED) {
 #pragma unroll
                 for (int i = 0; i < 8; i++) pv[i] = ptile[(2 * j + (i >> 2)) * W + 4 * q + (i & 3)];
             } else {
@@ -1961,7 +1812,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             for (int k = 0; k < EPL; k++) {
                 const int i = -2 * H + l + k * G;
                 bool need;
-                ev[k] = (i <= 2 * W && ie_need(ie, i)) ? ie_value<P, DGPU_FLOW_SC1>(ie, i, need) : -1;
+                ev[k] = (i <= 2 * W && ie_need(ie, i)) ? ie_value<P>(ie, i, need) : -1;
             }
 #pragma unroll
             for (int k = 0; k < EPL; k++)
@@ -2031,7 +1882,7 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             emit(j, q, pv);
         }
     } else if (NW && pred == DGPU_PRED_CFL) {
-        if constexpr (W == H && W <= 32) cfl_units<BPC, TX, GATHER && DGPU_FLOW_SC1>(a, u, tl, fe, l, bdmax, emit);
+        if constexpr (W == H && W <= 32) cfl_units<BPC, TX>(a, u, tl, fe, l, bdmax, emit);
     } else if (NW) {   // PRED_NONE: the residual goes onto the picture
 #pragma unroll
         for (int k = 0; k < TPL; k++) {
@@ -2041,51 +1892,12 @@ __device__ __forceinline__ void recon_units(const ReconArgs<BPC> &a, const Plane
             int pv[8];
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                const P *pp = dstp + __mul24(2 * j + (i >> 2), ds) + 4 * q + (i & 3);
-                if constexpr (GATHER && DGPU_FLOW_SC1) pv[i] = ie_px<true>(pp);
-                else pv[i] = gld<P>(pp);
+                pv[i] = gld<P>(dstp + __mul24(2 * j + (i >> 2), ds) + 4 * q + (i & 3));
             }
             emit(j, q, pv);
         }
     }
-    if constexpr (GATHER && DGPU_FLOW_SC1) {   // dav1d_backup_ipred_edge for this unit's columns (emit does it otherwise)
-        if (bkrow) {
-            wave_sync();   // this wave's picture stores are visible to its own loads
-            const P *last = dstp + (size_t)(H - 1) * ds;
-            using WT = std::conditional_t<BPC == 8, uint32_t, uint64_t>;   // 4-pixel words, sc1 both ways
-            for (int x = 4 * l; x < W; x += 4 * G) st_sc1<WT>(bkrow + x, ld_sc1<WT>(last + x));
-        }
-    }
     mark(8);
-#if defined(DGPU_PAD_SALU) || defined(DGPU_PAD_VALU) || defined(DGPU_PAD_VMEM) || defined(DGPU_PAD_VMEM1)   // cost-model probes (tools/build_variants.sh)
-    {
-        int p0 = first, p1 = count, p2 = gw, p3 = grp;
-#ifdef DGPU_PAD_SALU
-#pragma unroll
-        for (int i = 0; i < DGPU_PAD_SALU / 4; i++)
-            asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1"
-                         : "+s"(p0), "+s"(p1), "+s"(p2), "+s"(p3));
-#endif
-        int v0 = lane, v1 = lane + 1, v2 = lane + 2, v3 = lane + 3;
-#ifdef DGPU_PAD_VALU
-#pragma unroll
-        for (int i = 0; i < DGPU_PAD_VALU / 4; i++)
-            asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1"
-                         : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
-#endif
-#ifdef DGPU_PAD_VMEM
-#pragma unroll
-        for (int i = 0; i < DGPU_PAD_VMEM; i++)
-            v0 += gld<int>(pt.ref[0] + ((uint32_t)(u.dst_off * 7 + lane * 4099 + i * 131) % (1u << 22)));
-#endif
-#ifdef DGPU_PAD_VMEM1   // the same line for every lane: the per-instruction floor
-#pragma unroll
-        for (int i = 0; i < DGPU_PAD_VMEM1; i++)
-            v0 += gld<int>(pt.ref[0] + 4 * (lane & 15) + 64 * i);
-#endif
-        asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(p3), "v"(v0), "v"(v1), "v"(v2), "v"(v3));
-    }
-#endif
 }
 
 
@@ -2145,13 +1957,25 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
     const int bank_h = mc_bank(ftype & 3, bil, bw), bank_v = mc_bank(ftype >> 2, bil, bh);
     const uint4 tv0 = reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[0]];
     const uint4 tv1 = reinterpret_cast<const uint4 *>(dspt_mc16)[bank_v * 16 + u.p.inter.my[1]];
-    auto hinit = [&](HPass<BPC, TX> &hp, int k) {
+    // DGPU_MX_CLAMP (round 6, as the first launch's inter units): src_off[k]
+    // = x | y << 16 and every footprint pixel clamped to the plane
+    using HPC = HPass<BPC, TX, true>;
+    auto hinit = [&](HPC &hp, int k) {
         const int r = u.p.inter.ref[k];
         const int rs = pt.ref_stride[r * 3 + plane];
+        const int mx = u.p.inter.mx[k];
+        if (mx & DGPU_MX_CLAMP) {
+            int rw, rh;
+            ref_plane_wh<BPC>(r, plane, rw, rh);
+            const int so = u.p.inter.src_off[k];
+            hp.init_clamp(pt.ref[r * 3 + plane], rs, rw, rh, (int)(int16_t)(so & 0xffff), so >> 16, k ? mid1 : mid0,
+                          bank_h, mx & 15, l);
+            return;
+        }
         const P *org = pt.ref[r * 3 + plane] + u.p.inter.src_off[k] - 3 * rs - 3;
-        hp.init(org, rs, k ? mid1 : mid0, bank_h, u.p.inter.mx[k], l, 0, H + 7);
+        hp.init(org, rs, k ? mid1 : mid0, bank_h, mx, l);
     };
-    HPass<BPC, TX> hp0;
+    HPC hp0;
     if (wm || ob) {
         hinit(hp0, 0);
         hp0.load(0);
@@ -2162,7 +1986,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
         hp0.compute(0, ib);
         hp0.rest(ib);
         if (!CL::SEQREF && wm) {
-            HPass<BPC, TX> hp1;
+            HPC hp1;
             hinit(hp1, 1);
             hp1.load(0);
             hp1.compute(0, ib);
@@ -2264,7 +2088,7 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
                 if (t < NT) mc_vtask<W>(mid0, t / QW, t % QW, tv0, KP, 6, q0[k]);
             }
             wave_sync();
-            HPass<BPC, TX> hp1;
+            HPC hp1;
             hinit(hp1, 1);
             hp1.load(0);
             hp1.compute(0, ib);
@@ -2348,10 +2172,18 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
             const int ebh = mc_bank(eft & 3, ebil, (int)(er[3] & 0xff) * 4);
             const int ebv = mc_bank(eft >> 2, ebil, (int)((er[3] >> 8) & 0xff) * 4);
             if (has) {
-                HPass<BPC, TX> hp;
+                HPC hp;
                 const int rs = pt.ref_stride[eref * 3 + plane];
-                const P *org = pt.ref[eref * 3 + plane] + (int)er[0] - 3 * rs - 3;
-                hp.init(org, rs, mid0, ebh, (int)(er[1] & 0xff), l, 0, H + 7);
+                const int emx = (int)(er[1] & 0xff);
+                if (emx & DGPU_MX_CLAMP) {   // this lap's footprint clamped: er[0] = x | y << 16
+                    int rw, rh;
+                    ref_plane_wh<BPC>(eref, plane, rw, rh);
+                    hp.init_clamp(pt.ref[eref * 3 + plane], rs, rw, rh, (int)(int16_t)(er[0] & 0xffff),
+                                  (int)er[0] >> 16, mid0, ebh, emx & 15, l);
+                } else {
+                    const P *org = pt.ref[eref * 3 + plane] + (int)er[0] - 3 * rs - 3;
+                    hp.init(org, rs, mid0, ebh, emx, l);
+                }
                 hp.load(0);
                 hp.compute(0, ib);
                 hp.rest(ib);
@@ -2396,11 +2228,17 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
             wave_sync();
             const bool act = k < nref;
             const u32x4 rr = act ? gld<u32x4>(rec + 16 + 16 * k) : u32x4{0, 0, 0, 0};
-            const int smx = (int)(rr[1] & 0xffff), smy = (int)(rr[1] >> 16);
+            // bit 15 of the x phase: this reference's footprint clamped to the
+            // plane (round 6), rr[0] = x | y << 16 of the integer origin
+            const bool scl = rr[1] & 0x8000u;
+            const int smx = (int)(rr[1] & 0x7fff), smy = (int)(rr[1] >> 16);
             const int sdx = (int)(rr[2] & 0xffff), sdy = (int)(rr[2] >> 16);
             const int r = u.p.inter.ref[k];
             const int rs = pt.ref_stride[r * 3 + plane];
-            const P *org = pt.ref[r * 3 + plane] + (int)rr[0] - 3 * rs - 3;
+            const P *org = pt.ref[r * 3 + plane] + (scl ? 0 : (int)rr[0] - 3 * rs - 3);
+            int cw = 1, chh = 1;
+            if (scl) ref_plane_wh<BPC>(r, plane, cw, chh);
+            const int cx0 = (int)(int16_t)(rr[0] & 0xffff) - 3, cy0 = ((int)rr[0] >> 16) - 3;
             const int rows = min((((H - 1) * sdy + smy) >> 10) + 8, 2 * H + 8);   // (bound: the LDS area)
             const int hsh = 6 - ib, hrnd = (1 << hsh) >> 1;
             if (act) {
@@ -2411,9 +2249,17 @@ __device__ __forceinline__ void recon_units_ext(const ReconArgs<BPC> &a, const P
                     const P *sp = org + row * rs + (pos >> 10);
                     const uint2 tp = reinterpret_cast<const uint2 *>(dspt_mc8)[fb_h * 16 + ((pos & 1023) >> 6)];
                     int acc = 0;
+                    if (scl) {
 #pragma unroll
-                    for (int i = 0; i < 8; i++)
-                        acc += __builtin_amdgcn_sbfe((int)(i < 4 ? tp.x : tp.y), 8 * (i & 3), 8) * (int)gld<P>(sp + i);
+                        for (int i = 0; i < 8; i++)
+                            acc += __builtin_amdgcn_sbfe((int)(i < 4 ? tp.x : tp.y), 8 * (i & 3), 8) *
+                                   (int)clamped_px<P>(reinterpret_cast<const uint8_t *>(org), (unsigned)rs * sizeof(P),
+                                                      cx0 + (pos >> 10) + i, cy0 + row, cw, chh);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 8; i++)
+                            acc += __builtin_amdgcn_sbfe((int)(i < 4 ? tp.x : tp.y), 8 * (i & 3), 8) * (int)gld<P>(sp + i);
+                    }
                     mids[row * W + x] = (int16_t)((acc + hrnd) >> hsh);
                 }
             }

@@ -1129,12 +1129,15 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         return 0;
     };
 
-    if (!r->pool) {   // DAV1D_GPU_REC_THREADS (diagnostics): the worker count; default this
-                      // recorder's share of the process's CPUs, at most 8
+    {   // DAV1D_GPU_REC_THREADS (diagnostics): the worker count; default this
+        // recorder's share of the process's CPUs, at most 8, taken from the
+        // live recorders at EACH flush (a pool sized at the first
+        // flush kept 8 workers when the other frame threads' recorders came
+        // later); the pool is rebuilt between flushes when the share changes
         const int live = std::max(1, g_live_recorders.load(std::memory_order_relaxed));
         int nthr = std::max(1, std::min(8, rec_cpu_budget() / live));
         if (const char *e = getenv("DAV1D_GPU_REC_THREADS")) nthr = std::max(1, atoi(e));
-        r->pool.reset(new Pool(nthr));
+        if (!r->pool || r->pool->size() != nthr) r->pool.reset(new Pool(nthr));
     }
     const size_t nb = r->blocks.size();
     const int nt = nb < 4096 ? 1 : r->pool->size();

@@ -31,13 +31,6 @@
 
 namespace dgpu {
 
-// Profiling-only phase ablations (tools/build_variants.sh tile variants);
-// 0 in the product build, outputs are wrong when set:
-//   1 skip the transforms, 2 skip the mc tasks, 4 skip the cooperative
-//   groups, 8 skip the other tasks, 16 skip the store
-#ifndef DGPU_TILE_ABL
-#define DGPU_TILE_ABL 0
-#endif
 // DGPU_TILE_TRACE builds: per tile and wave, s_memtime at the phase
 // boundaries into TileArgs::trace ([tile][wave][8]; tools/tile_trace.py)
 #ifndef DGPU_TILE_TRACE
@@ -925,14 +918,12 @@ __device__ __forceinline__ void tile_task(const TileArgs<BPC> &a, const TileCtx<
     case DGPU_PRED_INTER_AVG:
     case DGPU_PRED_INTER_WAVG:
     case DGPU_PRED_INTER_MASK:
-        if (!(DGPU_TILE_ABL & 2)) tile_mc<BPC, R>(a, c, p, x0, y0, ab);
+        tile_mc<BPC, R>(a, c, p, x0, y0, ab);
         break;
     case DGPU_PRED_INTER_INTRA:
-        if (DGPU_TILE_ABL & 8) break;
         tile_ii<BPC, R>(a, c, p, x0, y0, ab);
         break;
     case DGPU_PRED_WARP:
-        if (DGPU_TILE_ABL & 8) break;
         tile_warp<BPC, R>(a, c, p, x0, y0, ab);
         break;
     case DGPU_PRED_PAL: {   // pal_pred (src/ipred_tmpl.c:717-730): record = 8 entries, then
@@ -983,11 +974,9 @@ __device__ __forceinline__ void tile_task(const TileArgs<BPC> &a, const TileCtx<
 // HUGE: the launch over the tiles with 64-point transforms (the 64-point
 // row / column code is compiled only there: its registers would otherwise
 // set the occupancy of every tile)
-#ifndef DGPU_TILE_WPE
-#define DGPU_TILE_WPE 3   // waves per SIMD the register allocator must allow
-#endif
+// (3 waves per SIMD the register allocator must allow; 4 spilled: 165 us)
 template <int BPC, bool HUGE>
-__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DGPU_TILE_WPE))) void k_tiles(
+__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_tiles(
     TileArgs<BPC> a) {
     using P = typename Px<BPC>::pixel;
     using C = typename Px<BPC>::coef;
@@ -1132,7 +1121,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         A *ab = acc + (((tx.w0 >> 4) & 15) * 4) * S + (tx.w0 & 15) * 4;
         const C *cs = c.cf + (tx.w1 & 0xffff);
         const bool wht = txtp == DGPU_WHT_WHT;   // lossless 4x4: one lane, both passes, int32
-        if (act && wht && l == 0 && !(DGPU_TILE_ABL & 1)) {
+        if (act && wht && l == 0) {
             int t[16];
             wht4x4(cs, nzw, nzh, t);
 #pragma unroll
@@ -1141,7 +1130,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
                 for (int x = 0; x < 4; x++)
                     ab[y * S + x] = (A)(BPC == 8 ? clampi(t[4 * y + x], -32768, 32767) : t[4 * y + x]);
         }
-        if (act && !wht && nzw && l < nzh && !(DGPU_TILE_ABL & 1)) {   // row pass
+        if (act && !wht && nzw && l < nzh) {   // row pass
             const bool rect2 = W * 2 == H || H * 2 == W;
             A *arow = ab + l * S;
             const int kh = kind_h(txtp);
@@ -1156,7 +1145,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
             }
         }
         wave_sync();
-        if (act && !wht && l < W && !(DGPU_TILE_ABL & 1)) {   // column pass, in place
+        if (act && !wht && l < W) {   // column pass, in place
             A *acol = ab + l;
             if (!nzw) {   // DC-only (src/itx_tmpl.c:53-65)
                 int dc = cs[0];
@@ -1192,7 +1181,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
         if (lane < lanes_pred) {
             const Dav1dGpuPred p = bld(a.preds + T.pred0 + DGPU_TILE_INDEX((int)pmap[lane], T.n_pred, 1));
             if (wlane < T.lanes_coop) {
-                if (lane < T.lanes_coop_used && !(DGPU_TILE_ABL & 4)) tile_coop<BPC>(a, c, p, lane - p.lane0);
+                if (lane < T.lanes_coop_used) tile_coop<BPC>(a, c, p, lane - p.lane0);
             } else {
                 const int t = lane - T.lanes_coop - p.lane0;
                 const int R = (BPC == 8 && p.h4 >= 2) ? 8 : 4;
@@ -1212,7 +1201,6 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(DG
     mark(6);
 
     // ---- P3: store the tile, whole rows ----
-    if (DGPU_TILE_ABL & 16) return;
     P *dp = a.dst[plane] + (size_t)T.y * a.dst_stride[plane] + T.x;
     const int ds = a.dst_stride[plane];
     if constexpr (BPC == 8) {

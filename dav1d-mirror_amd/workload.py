@@ -116,6 +116,7 @@ class FrameData:
     class_warp: np.ndarray = None # WARP units at the end of each class range
     src_xy: np.ndarray = None     # [unit][ref][x|y]: integer source position of the unit's
                                   # top-left in the reference plane (visible coordinates)
+    deferred: object = None       # clamp_units: a second batch to launch after this one
     stats: dict = field(default_factory=dict)
 
     @property
@@ -787,6 +788,17 @@ def algorithmic_bytes(fd: FrameData):
     }
 
 
+def _decode_off(off, rs, pad):
+    """(x, y) of a padded-plane offset y * rs + x (x in [-pad, rs - pad))."""
+    off = np.asarray(off, np.int64)
+    y = (off + pad) // rs
+    return off - y * rs, y
+
+
+def _xy16(x, y):
+    return ((np.asarray(x, np.int64) & 0xffff) | ((np.asarray(y, np.int64) & 0xffff) << 16)).astype(np.uint32).view(np.int32)
+
+
 def clamp_units(fd: FrameData):
     """The frame for exact-size (unpadded) reference planes, as a decoder
     with dav1d's own pictures would hand it to the unit batch: every inter
@@ -798,13 +810,21 @@ def clamp_units(fd: FrameData):
     re-expressed in the exact plane's stride; a unit whose footprint leaves
     it gets DGPU_MX_CLAMP on that reference with src_off = x | y << 16 and
     moves to the end of its class range (the class_warp sub-range of the
-    second launch, which clamps every footprint pixel).  Returns (frame,
-    exact reference planes [ref][plane]).  Frames with the launch-ahead kinds
-    (WARP, INTER_INTRA, INTER_WMASK, INTER_OBMC, INTER_SCALED) still need
-    padded references and are refused."""
+    second launch, which clamps every footprint pixel).
+
+    Round 6: the launch-ahead kinds clamp too, each of them
+    flagged whatever its footprint (they already run in the second launch,
+    and a clamped read of an inside pixel is that pixel):
+      * INTER_WMASK / INTER_OBMC / INTER_SCALED / INTER_INTRA: DGPU_MX_CLAMP
+        in mx[k] and src_off[k] = x | y << 16, as above;
+      * OBMC lap records (aux_pool): DGPU_MX_CLAMP in the lap's mx byte and
+        its source offset as x | y << 16 (src/recon_tmpl.c:1071-1133);
+      * INTER_SCALED records: bit 15 of the x phase and the integer origin as
+        x | y << 16 (:1036-1046);
+      * WARP: DGPU_MX_CLAMP in mx[0] and src_off[0] = 0, the per-8x8 source
+        positions then being the plane's own (:1168-1177).
+    Returns (frame, exact reference planes [ref][plane])."""
     u = fd.units.copy()
-    if np.isin(u["pred"], abi.SECOND_LAUNCH_KINDS).any():
-        raise ValueError("launch-ahead kinds read unclamped footprints: padded references only")
     pad = fd.cfg.ref_pad
     exact = [[np.ascontiguousarray(a[pad:pad + h, pad:pad + w]) for a, (w, h) in zip(rp, fd.plane_wh)]
              for rp in fd.refs]
@@ -827,13 +847,172 @@ def clamp_units(fd: FrameData):
         off = np.where(cl, (x & 0xffff) | ((y & 0xffff) << 16), (y * pw + x) & 0xffffffff)
         u[f"src_off{k}"] = np.where(used, off.astype(np.uint32).view(np.int32), u[f"src_off{k}"])
         u[f"mx{k}"] = np.where(cl, u[f"mx{k}"] | 0x80, u[f"mx{k}"])
+    # the launch-ahead kinds, every one flagged
+    aux_pool = None if fd.aux_pool is None else fd.aux_pool.copy()
+    rs = np.array([fd.refs[0][p].shape[1] for p in range(3)])
+    ext = np.isin(u["pred"], (abi.PRED_INTER_WMASK, abi.PRED_INTER_OBMC, abi.PRED_INTER_SCALED,
+                              abi.PRED_INTER_INTRA))
+    for k in range(2):
+        used = ext & ((u["pred"] == abi.PRED_INTER_WMASK) if k else True)
+        xy = _xy16(fd.src_xy[:, k, 0], fd.src_xy[:, k, 1])
+        u[f"src_off{k}"] = np.where(used, xy, u[f"src_off{k}"])
+        u[f"mx{k}"] = np.where(used, u[f"mx{k}"] | 0x80, u[f"mx{k}"])
+    clamp_any |= ext
+    warp = u["pred"] == abi.PRED_WARP
+    u["src_off0"] = np.where(warp, 0, u["src_off0"])
+    u["mx0"] = np.where(warp, u["mx0"] | 0x80, u["mx0"])
+    clamp_any |= warp
+    if aux_pool is not None:
+        ap32 = aux_pool.view(np.int32)
+        for i in np.nonzero(u["pred"] == abi.PRED_INTER_OBMC)[0]:
+            o = int(fd.aux[i])
+            n = int(ap32[o // 4])
+            for e in range(n):
+                b = o + 16 + 16 * e
+                x, y = _decode_off(ap32[b // 4], rs[u["plane"][i]], pad)
+                ap32[b // 4] = _xy16(x, y)
+                aux_pool[b + 4] |= 0x80
+        for i in np.nonzero(u["pred"] == abi.PRED_INTER_SCALED)[0]:
+            o = int(fd.aux[i])
+            n = int(ap32[o // 4]) & 3
+            for e in range(n):
+                b = o + 16 + 16 * e
+                x, y = _decode_off(ap32[b // 4], rs[u["plane"][i]], pad)
+                ap32[b // 4] = _xy16(x, y)
+                aux_pool[b + 5] |= 0x80   # bit 15 of the u16 x phase
+    # A clamped INTER_MASK unit on the seg mask an INTER_WMASK unit of this
+    # batch writes (COMPOUND_SEG chroma, src/recon_tmpl.c:1900) would run in
+    # the same launch as its writer: it goes into a second batch, launched
+    # after this one (out.deferred), as a decoder's next flush would run it
+    dep = np.zeros(len(u), bool)
+    if fd.blk is not None:
+        wm_blk = np.unique(fd.blk[u["pred"] == abi.PRED_INTER_WMASK] // 3)
+        dep = (u["pred"] == abi.PRED_INTER_MASK) & np.isin(fd.blk // 3, wm_blk) & clamp_any
+
+    def build(sel):
+        idx = np.nonzero(sel)[0]
+        order = idx[np.lexsort((idx, clamp_any[idx], u["tx"][idx]))]
+        uu = u[order]
+        counts = np.bincount(uu["tx"], minlength=abi.N_TX)
+        cs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+        cw = np.bincount(uu["tx"][clamp_any[order]], minlength=abi.N_TX).astype(np.int32)
+        f = dataclasses.replace(fd, units=uu, class_start=cs, class_warp=cw, refs=None, aux_pool=aux_pool,
+                                blk=None if fd.blk is None else fd.blk[order],
+                                aux=None if fd.aux is None else fd.aux[order],
+                                src_xy=None if fd.src_xy is None else fd.src_xy[order])
+        f.stats = dict(fd.stats, clamped_units=int(clamp_any[order].sum()))
+        return f
+
     # clamped units last inside their class (stable), the class_warp sub-range
-    order = np.lexsort((np.arange(len(u)), clamp_any, u["tx"]))
-    u = u[order]
-    class_warp = np.bincount(u["tx"][clamp_any[order]], minlength=abi.N_TX).astype(np.int32)
-    out = dataclasses.replace(fd, units=u, class_warp=class_warp, refs=None,
-                              blk=None if fd.blk is None else fd.blk[order],
-                              aux=None if fd.aux is None else fd.aux[order],
-                              src_xy=None if fd.src_xy is None else fd.src_xy[order])
-    out.stats = dict(fd.stats, clamped_units=int(clamp_any.sum()))
+    out = build(~dep)
+    out.deferred = build(dep) if dep.any() else None
     return out, exact
+
+
+def _class_sorted(units, keys_minor, planes, blk=None):
+    """units sorted as make_frame sorts a batch: (class, picture band, pred
+    kind, minor); returns (units, class_start, blk)."""
+    pw = np.array([p[0] for p in planes])
+    ph = np.array([p[1] for p in planes])
+    pl = units["plane"].astype(np.int64)
+    uy = units["dst_off"].astype(np.int64) // pw[pl]
+    band = (uy * SORT_BANDS) // ph[pl]
+    order = np.lexsort((keys_minor, units["pred"], band, units["tx"]))
+    units = units[order]
+    counts = np.bincount(units["tx"], minlength=abi.N_TX)
+    class_start = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    return units, class_start, (None if blk is None else blk[order])
+
+
+def split_frame(fd: FrameData, piece: int = 32):
+    """The two-pass form of a frame: the reference's own
+    order of work, mc() once per prediction block and reference
+    (src/recon_tmpl.c:957-1060, compound :1845-1866) writing the block's
+    prediction into the picture, then inv_txfm_add of each transform block
+    adding its residual to what is there (src/itx_tmpl.c:40-100, the
+    `dst` read + clip of every entry).
+
+    Returns (pred_fd, res_fd), both run by the unchanged unit batch on the
+    same picture, pred_fd first:
+      * pred_fd: one prediction-only unit (txtp NO_RESIDUAL) per inter block
+        and plane, blocks wider than `piece` cut into piece x piece units
+        (mc is pointwise in the block call and the filter bank follows the
+        block size carried in bw4 / bh4, as for the "mc" frames); sorted by
+        (class, band, kind, filter), so a wave runs one block shape and
+        filter and each footprint row is read once per block, not once per
+        transform unit;
+      * res_fd: the intra / CfL units unchanged (prediction + residual, they
+        do not share footprints) and every inter transform unit with a
+        residual as PRED_NONE (residual onto the predicted picture).
+    pred + residual then clip is the fused kernel's arithmetic and the
+    reference's, so the picture is bit-identical (tests/test_gpu_batch.py).
+    Kinds whose prediction needs per-unit block data (mask, palette, warp,
+    the second launch's) are refused."""
+    u = fd.units
+    ok = (abi.PRED_INTER, abi.PRED_INTER_AVG, abi.PRED_INTER_WAVG, abi.PRED_INTRA, abi.PRED_CFL, abi.PRED_NONE)
+    if not np.isin(u["pred"], ok).all():
+        raise ValueError("split_frame: only put / avg / w_avg inter, intra, CfL and residual-only units")
+    planes = fd.plane_wh
+    pw = np.array([p[0] for p in planes])
+    pl = u["plane"].astype(np.int64)
+    ux = u["dst_off"].astype(np.int64) % pw[pl]
+    uy = u["dst_off"].astype(np.int64) // pw[pl]
+    inter = np.isin(u["pred"], (abi.PRED_INTER, abi.PRED_INTER_AVG, abi.PRED_INTER_WAVG))
+    s = u["bw4"].astype(np.int64) * 4
+    if inter.any() and not np.array_equal(u["bw4"][inter], u["bh4"][inter]):
+        raise ValueError("split_frame: square prediction blocks only")
+    bx0, by0 = ux // np.maximum(s, 1) * s, uy // np.maximum(s, 1) * s
+    key = (pl * (1 << 40)) + by0 * (1 << 20) + bx0
+    idx = np.nonzero(inter)[0]
+    _, first = np.unique(key[idx], return_index=True)
+    heads = idx[first]
+    ref_stride = np.array([fd.refs[0][p].shape[1] for p in range(3)])
+    # prediction pieces
+    rows = []
+    for i in heads:
+        bs = int(s[i])
+        t = min(bs, piece)
+        dx, dy = int(ux[i] - bx0[i]), int(uy[i] - by0[i])
+        for oy in range(0, bs, t):
+            for ox in range(0, bs, t):
+                rows.append((i, ox - dx, oy - dy, t))
+    src = np.array([r[0] for r in rows], np.int64)
+    ox = np.array([r[1] for r in rows], np.int64)
+    oy = np.array([r[2] for r in rows], np.int64)
+    tsz = np.array([r[3] for r in rows], np.int64)
+    pu = u[src].copy()
+    pl_p = pl[src]
+    pu["dst_off"] = (uy[src] + oy) * pw[pl_p] + ux[src] + ox
+    pu["tx"] = np.array([abi.TX_INDEX[(int(a), int(a))] for a in tsz], np.uint8)
+    rs = ref_stride[pl_p]
+    comp = pu["pred"] != abi.PRED_INTER
+    for k in range(2):
+        use = np.ones(len(pu), bool) if k == 0 else comp
+        so = pu[f"src_off{k}"].astype(np.int64) + oy * rs + ox
+        pu[f"src_off{k}"] = np.where(use, so, pu[f"src_off{k}"]).astype(np.int32)
+    pu["txtp"] = abi.NO_RESIDUAL
+    pu["nzw"] = 0
+    pu["nzh"] = 0
+    pu["coef_off"] = 0
+    pblk = None if fd.blk is None else fd.blk[src]
+    pu, pcs, pblk = _class_sorted(pu, pu["filter2d"].astype(np.int64), planes, pblk)
+    pred_fd = dataclasses.replace(fd, units=pu, class_start=pcs, blk=pblk, aux=None,
+                                  class_warp=np.zeros(abi.N_TX, np.int32), src_xy=None)
+    # residual pass: intra / CfL / residual-only as they are, inter units with
+    # a residual as PRED_NONE
+    keep = ~inter | (u["txtp"] != abi.NO_RESIDUAL)
+    ru = u[keep].copy()
+    rin = inter[keep]
+    ru["pred"] = np.where(rin, abi.PRED_NONE, ru["pred"])
+    for f in ("src_off0", "src_off1", "mx0", "mx1", "my0", "my1", "filter2d", "weight"):
+        ru[f] = np.where(rin, 0, ru[f])
+    # minor key: the transform type for the residual-only units, the original
+    # rank (already (filter / mode, type) ordered) for the others
+    minor = np.where(ru["pred"] == abi.PRED_NONE, ru["txtp"].astype(np.int64), np.arange(len(ru)) + 256)
+    rblk = None if fd.blk is None else fd.blk[keep]
+    ru, rcs, rblk = _class_sorted(ru, minor, planes, rblk)
+    res_fd = dataclasses.replace(fd, units=ru, class_start=rcs, blk=rblk, aux=None,
+                                 class_warp=np.zeros(abi.N_TX, np.int32), src_xy=None)
+    pred_fd.stats = algorithmic_bytes(pred_fd)
+    res_fd.stats = algorithmic_bytes(res_fd)
+    return pred_fd, res_fd

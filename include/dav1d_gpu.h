@@ -437,7 +437,18 @@ typedef struct Dav1dGpuFrameBatch {
  * class_warp sub-range.  A unit without the flag is read as it stands: its
  * footprint -- the unit's rectangle -3 / +4 pixels, plus up to 3 pixels
  * before and 5 after each row for the aligned row loads -- must then lie
- * inside the plane (or inside readable edge-replicated padding). */
+ * inside the plane (or inside readable edge-replicated padding).
+ * Round 6: the second launch's kinds take the same flag.  INTER_WMASK,
+ * INTER_OBMC (its own prediction) and INTER_INTRA: DGPU_MX_CLAMP in mx[k],
+ * src_off[k] = x | y << 16 as above.  An INTER_OBMC lap entry: DGPU_MX_CLAMP
+ * in its mx byte and its source offset as x | y << 16.  An INTER_SCALED
+ * reference record: bit 15 of its x phase, its integer origin as
+ * x | y << 16.  WARP: DGPU_MX_CLAMP in mx[0] with src_off[0] = 0, the per-8x8
+ * source positions being the plane's own.  Every footprint pixel is then
+ * read clamped to the plane (src/recon_tmpl.c:1036-1046, :1071-1133,
+ * :1168-1177).  A clamped INTER_MASK unit reading a mask an INTER_WMASK unit
+ * writes must be in a later batch than its writer (both would be in the
+ * second launch). */
 #define DGPU_MX_CLAMP 0x80
 
 /* Launch one frame batch on `stream` (a hipStream_t, NULL = default).
@@ -445,10 +456,8 @@ typedef struct Dav1dGpuFrameBatch {
  * Reference footprints are read straight from the reference planes, except
  * for DGPU_MX_CLAMP units (above), which clamp every pixel to the plane:
  * a caller either pads its reference planes (>= 80 px, dav1d's own border
- * extension) or flags the units whose footprint leaves them.  WARP,
- * INTER_INTRA, INTER_WMASK, INTER_OBMC and INTER_SCALED units still read
- * unclamped footprints (the recorder and the tile batch emulate edges for
- * them). */
+ * extension) or flags the units whose footprint leaves them (every kind,
+ * since round 6). */
 int dav1d_gpu_recon_8bpc(const Dav1dGpuFrameBatch *b, void *stream);
 int dav1d_gpu_recon_16bpc(const Dav1dGpuFrameBatch *b, void *stream);
 
@@ -1198,8 +1207,13 @@ typedef struct Dav1dGpuLrFrame {
                                      start / 64 .. end / 64 - 1 (rows
                                      64k - 8 .. 64k + 55, >> ss_ver), what
                                      dav1d_lr_sbrow filters per superblock
-                                     row (src/lr_apply_tmpl.c:169-202);
-                                     0, 0: the whole frame                   */
+                                     row (src/lr_apply_tmpl.c:169-202); a
+                                     range with end >= the luma height
+                                     rounded up to 64 holds the last
+                                     superblock row and, as there, runs
+                                     every stripe from start / 64 to the
+                                     picture's bottom; 0, 0: the whole
+                                     frame                                   */
 } Dav1dGpuLrFrame;
 /* Errors: -1 NULL / bad layout / bad unit grid / bad row range, -3 launch
  * failure. */

@@ -357,3 +357,40 @@ def test_clamp_units_conversion(pkg):
     a = np.sort(fd.units[keep], order=keep)
     b = np.sort(u[keep], order=keep)
     assert np.array_equal(a, b)
+
+
+def test_clamp_units_launch_ahead_kinds(pkg):
+    """Round 6: clamp_units flags every launch-ahead unit
+    (WARP / INTER_INTRA / INTER_WMASK / INTER_OBMC / INTER_SCALED), rewrites
+    the OBMC lap and scaled-reference records to x | y << 16 with their clamp
+    bits, and defers the clamped COMPOUND_SEG chroma units to a second batch."""
+    import dav1d_mirror_amd.workload as wl
+    import dav1d_mirror_amd.abi as abi
+    for kind in ("ext", "ext2"):
+        fd = wl.make_frame(wl.FrameConfig(width=256, height=128, seed=5, kind=kind, mv_range=200))
+        fdc, _ = wl.clamp_units(fd)
+        parts = [fdc] + ([fdc.deferred] if fdc.deferred is not None else [])
+        assert sum(f.n_units for f in parts) == fd.n_units
+        for f in parts:
+            u = f.units
+            la = np.isin(u["pred"], abi.SECOND_LAUNCH_KINDS)
+            assert ((u["mx0"][la] & 0x80) != 0).all()
+            assert (u["src_off0"][u["pred"] == abi.PRED_WARP] == 0).all()
+            for t in range(abi.N_TX):   # flagged units form each class's tail
+                c0, c1 = f.class_start[t], f.class_start[t + 1]
+                assert not la[c0:c1 - f.class_warp[t]].any()
+        ap = fdc.aux_pool.view(np.int32)
+        pad, u = fd.cfg.ref_pad, fdc.units
+        for i in np.nonzero(u["pred"] == abi.PRED_INTER_OBMC)[0][:50]:
+            o = int(fdc.aux[i])
+            for e in range(int(ap[o // 4])):
+                b = o + 16 + 16 * e
+                assert fdc.aux_pool[b + 4] & 0x80
+                old = int(fd.aux_pool.view(np.int32)[b // 4])
+                rs = fd.refs[0][u["plane"][i]].shape[1]
+                x, y = wl._decode_off(old, rs, pad)
+                v = int(ap[b // 4])
+                assert ((v & 0xffff) - ((v & 0x8000) << 1), v >> 16) == (int(x), int(y))
+        if kind == "ext2":
+            assert fdc.deferred is not None
+            assert (fdc.deferred.units["pred"] == abi.PRED_INTER_MASK).all()

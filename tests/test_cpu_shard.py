@@ -101,3 +101,23 @@ def test_rccl_feed_scatter_gloo():
             assert p.exitcode == 0
         assert all(r[1] for r in res), res
         assert res[0][2] > 0 and all(r[2] > 0 for r in res[1:])
+
+
+def test_pack_frame_one_buffer():
+    """The feed's flat image: every array at a 16-byte
+    aligned offset of one buffer, and unpacking gives the frame back."""
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    ge.load_package()
+    import dav1d_mirror_amd.workload as wl
+    import dav1d_mirror_amd.shard as sh
+    for kind in ("full", "ext", "itx"):
+        fd = wl.make_frame(wl.FrameConfig(width=256, height=128, kind=kind))
+        h, flat = sh.pack_frame(fd)
+        n = h[0]
+        offs = [h[1 + sh._HDR * i + 5] for i in range(n)]
+        assert all(o % 16 == 0 for o in offs) and offs == sorted(offs)
+        back = sh.unpack_frame(h, flat.numpy(), fd.cfg)
+        assert back.units.tobytes() == fd.units.tobytes() and np.array_equal(back.coefs, fd.coefs)
+        assert all(np.array_equal(back.refs[k][p], fd.refs[k][p]) for k in range(2) for p in range(3))
+        assert back.stats == fd.stats

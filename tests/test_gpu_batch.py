@@ -194,23 +194,38 @@ def test_batch_ext2_masks_and_cut(pkg, oracle, bpc, bdmax, seed):
 
 @pytest.mark.parametrize("bpc,bdmax,kind,mv,size", [
     (8, 255, "full", 64, (512, 256)), (8, 255, "full", 200, (512, 256)), (8, 255, "mc", 200, (512, 256)),
-    (16, 1023, "full", 200, (512, 256)), (16, 4095, "full", 64, (512, 256)), (8, 255, "full", 64, (3840, 2160))])
+    (16, 1023, "full", 200, (512, 256)), (16, 4095, "full", 64, (512, 256)), (8, 255, "full", 64, (3840, 2160)),
+    (8, 255, "ext", 200, (512, 256)), (16, 1023, "ext", 200, (512, 256)), (16, 4095, "ext", 200, (512, 256)),
+    (8, 255, "ext2", 200, (512, 256)), (16, 1023, "ext2", 200, (512, 256)), (16, 4095, "ext2", 200, (512, 256))])
 def test_batch_unpadded_refs(pkg, oracle, bpc, bdmax, kind, mv, size):
     """emu_edge in the unit batch (round 5): exact-size reference planes
     (stride = width), the units whose footprint leaves them flagged
     DGPU_MX_CLAMP and run in the second launch with every footprint pixel
     clamped, the rest read in place; the picture equals the oracle's walk of
     the same blocks on edge-replicated padded references (what emu_edge_c
-    reads, src/mc_tmpl.c:827-875).  MVs up to 200 px outside the picture."""
+    reads, src/mc_tmpl.c:827-875).  MVs up to 200 px outside the picture.
+    Round 6: the launch-ahead kinds too -- warp, inter-intra
+    ("ext"), w_mask, OBMC laps and scaled references ("ext2") -- with their
+    mask-reading chroma in a second batch where it reads a clamped footprint
+    (workload.clamp_units' `deferred`)."""
     import torch
     import dav1d_mirror_amd.batch as bt
     import dav1d_mirror_amd.workload as wl
     fd = _frame(pkg, width=size[0], height=size[1], bpc=bpc, bitdepth_max=bdmax, kind=kind, seed=21, mv_range=mv)
     fdc, exact = wl.clamp_units(fd)
     n_inter = int(np.isin(fd.units["pred"], (1, 2, 5, 6)).sum())
-    assert 0 < fdc.stats["clamped_units"] < n_inter
+    if kind in ("full", "mc"):
+        assert 0 < fdc.stats["clamped_units"] < n_inter
+    else:
+        ext = np.isin(fd.units["pred"], pkg.abi.SECOND_LAUNCH_KINDS)
+        assert ext.sum() > 0 and fdc.stats["clamped_units"] >= ext.sum()
     dev = bt.DeviceFrame(fdc, "cuda:0", exact_refs=exact)
     dev.launch()
+    if fdc.deferred is not None:   # after the batch whose w_mask units write the masks it reads
+        dev2 = bt.DeviceFrame(fdc.deferred, "cuda:0", exact_refs=exact, dst_planes=dev.dst)
+        dev2.aux_pool = dev.aux_pool   # the masks the first batch wrote
+        dev2.batch = dev2._make_batch()
+        dev2.launch()
     torch.cuda.synchronize()
     got = dev.planes_host()
     hf = oracle.HostFrame(fd)
@@ -231,3 +246,28 @@ def test_batch_lossless(pkg, oracle, bpc, bdmax, seed):
     wht = fd.units["txtp"] == pkg.abi.WHT_WHT
     assert wht.sum() > 100 and np.all(fd.units["tx"][wht] == 0)
     _check(fd, oracle)
+
+
+@pytest.mark.parametrize("w,h,bpc,bdmax", [(512, 256, 8, 255), (512, 256, 16, 1023), (3840, 2160, 8, 255),
+                                           (3840, 2160, 16, 1023)])
+def test_batch_split_two_pass(pkg, oracle, w, h, bpc, bdmax):
+    """The two-pass form (workload.split_frame): the unit
+    batch run on the prediction blocks, then on the residuals onto the
+    predicted picture, equals the oracle's fused walk of the frame."""
+    import torch
+    import dav1d_mirror_amd.batch as bt
+    import dav1d_mirror_amd.workload as wl
+    fd = _frame(pkg, width=w, height=h, bpc=bpc, bitdepth_max=bdmax, seed=0x5EED0001)
+    pf, rf = wl.split_frame(fd)
+    a = bt.DeviceFrame(pf, "cuda:0")
+    b = bt.DeviceFrame(rf, "cuda:0", dst_planes=a.dst)
+    for _ in range(2):   # idempotent: the prediction pass rewrites every inter pixel
+        a.launch()
+        b.launch()
+    torch.cuda.synchronize()
+    got = b.planes_host()
+    hf = oracle.HostFrame(fd)
+    hf.run(threads=8)
+    for p in range(3):
+        diff = np.argwhere(got[p] != hf.dst[p])
+        assert len(diff) == 0, f"plane {p}: {len(diff)} pixels differ, first {diff[:5].tolist()}"

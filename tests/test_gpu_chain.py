@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("w,h,bpc,bdmax,per_row", [(1920, 1080, 8, 255, False), (3840, 2160, 8, 255, False),
                                                    (1920, 1080, 16, 1023, False), (1920, 1080, 8, 255, True),
-                                                   (1920, 1080, 16, 1023, True)])
+                                                   (1920, 1080, 16, 1023, True),
+                                                   (1920, 1024, 8, 255, True), (1280, 256, 8, 255, True)])
 def test_chain_recon_postfilters_grain(pkg, oracle, w, h, bpc, bdmax, per_row):
     """per_row: the post-filters run per superblock row, interleaved as a
     decoder runs them (DeviceChain.launch_per_row), against the same

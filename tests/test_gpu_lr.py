@@ -7,12 +7,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _check(oracle, c, step=None):
+def _check(oracle, c, step=None, exact=False):
     import torch
     import dav1d_mirror_amd.lr as lr
     dev = lr.DeviceLr(c)
     if step is None:
         dev.launch()
+    elif exact:   # sby = 0 .. sbh - 1 only, in decoding order, as dav1d_filter_sbrow_lr calls it
+        for y in range(0, (c.height + step - 1) // step * step, step):
+            dev.launch(rows=(y, y + step))
     else:   # one call per superblock row, last row first (in, lpf read-only), and one past the picture
         for y in reversed(range(0, c.height + step, step)):
             dev.launch(rows=(y, y + step))
@@ -60,3 +63,18 @@ def test_lr_per_superblock_row(oracle, bpc, bdmax, layout, sb128):
     c = lr.make_lr_case(seed=120 + layout + sb128 + bpc, width=336, height=264, bpc=bpc, bitdepth_max=bdmax,
                         layout=layout, sb128=sb128, unit_log2=(6 + sb128, 5 + sb128 if layout == 1 else 6 + sb128))
     _check(oracle, c, step=64 << sb128)
+
+
+@pytest.mark.parametrize("height", [256, 1024, 250, 1080])
+@pytest.mark.parametrize("sb128", [0, 1])
+@pytest.mark.parametrize("layout", [1, 3])
+def test_lr_per_row_last_stripe(oracle, height, sb128, layout):
+    """the call for the last superblock row filters down to
+    the picture's bottom (dav1d_lr_sbrow: not_last = 0, row_h = h,
+    src/lr_apply_tmpl.c:174-191), also when h % 64 is 0 or 57..63 and the
+    last stripe starts 8 rows above a 64-row multiple.  Only sby = 0 ..
+    sbh - 1 are called, no range past the picture."""
+    import dav1d_mirror_amd.lr as lr
+    c = lr.make_lr_case(seed=300 + height + sb128 + layout, width=200, height=height, bpc=8, layout=layout,
+                        sb128=sb128, unit_log2=(6 + sb128, 5 + sb128 if layout == 1 else 6 + sb128))
+    _check(oracle, c, step=64 << sb128, exact=True)
