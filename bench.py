@@ -86,7 +86,7 @@ def cpu_baseline(fd, budget_s=12.0):
 def _latest_profile(fmt):
     """The newest round's committed summary (profiles/rN/rN_<fmt>), so a line
     never cites an older kernel's profile once the current one is in."""
-    for rnd in ("r5", "r4", "r3"):
+    for rnd in ("r6", "r5", "r4", "r3"):
         path = os.path.join(ROOT, "profiles", rnd, f"{rnd}_{fmt}")
         if os.path.exists(path):
             return path

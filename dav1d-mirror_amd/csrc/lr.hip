@@ -38,6 +38,7 @@ namespace dgpu {
 constexpr int kLrSW = 32;              // strip width
 constexpr int kLrTW = kLrSW + 6;       // tile width
 constexpr int kLrTH = 64 + 6;          // tile height
+constexpr int kLrGroup = 8;            // frame tier: consecutive strips per XCD run
 
 template <int BPC> struct LrArgs {
     using P = typename Px<BPC>::pixel;
@@ -383,7 +384,6 @@ template <int BPC> struct LrFrameArgs {
     int vec;         // every plane pointer and pitch 16-byte aligned
     int k0;          // the first stripe run (row ranges): stripe = k0 + the grid row
     int nx, nwg;     // strips per stripe (all planes), workgroups (nx x stripes)
-    int linear;      // A/B only: the dispatcher's own order (DAV1D_GPU_LR_ORDER=linear)
 };
 
 // lr_stripe's filter parameters (src/lr_apply_tmpl.c:51-80); kind 0 wiener,
@@ -415,14 +415,16 @@ __device__ __forceinline__ int lr_params(const Dav1dGpuLrUnit &u, bool hbd, Dav1
 template <int BPC>
 __global__ __launch_bounds__(256, 5) void k_lr_frame(LrFrameArgs<BPC> f) {
     using P = typename Px<BPC>::pixel;
-    // XCD-contiguous order (the frame read 3.0x its picture):
-    // workgroups are dealt round-robin over the 8 XCDs, so logical workgroup
-    // (b % 8) * (nb / 8) + b / 8 gives each XCD a contiguous run of stripes;
-    // the 4-5 strips that share a 128-B picture line (32 px, plus the 3 + 3
-    // halo columns) and the rows stripes share then meet in one L2 instead
-    // of being fetched once per XCD
-    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
-    const int lb = f.linear ? b : (b & 7) * (nb >> 3) + (b >> 3);   // (A/B: DAV1D_GPU_LR_ORDER=linear)
+    // Workgroup order (the frame read 3.0x its picture): the
+    // hardware deals workgroups round-robin over the 8 XCDs, which put the
+    // 4-5 strips sharing a 128-B line of 8-bit pixels (32 px, plus the 3 + 3
+    // halo columns) on different XCDs, each fetching the line.  Runs of
+    // kLrGroup consecutive strips go to one XCD instead: FETCH 36.9 -> 12.0
+    // MB per 4K frame.  The time hardly moves with the order (every order
+    // within 45.6-48.9 us on one box; an XCD-contiguous run of whole stripes
+    // 6.8 MB but slower on another; profiles/r6/r6c_lr_order_ab.json)
+    const int b = (int)blockIdx.x, i8 = b >> 3, x8 = b & 7;
+    const int lb = ((i8 / kLrGroup) * 8 + x8) * kLrGroup + i8 % kLrGroup;
     if (lb >= f.nwg) return;
     const int by = lb / f.nx, bx = lb - by * f.nx, pl = bx < f.xb0 ? 0 : bx < f.xb01 ? 1 : 2;
     const int w = f.w[pl], h = f.h[pl], sv = f.ss_ver[pl];
@@ -553,12 +555,10 @@ static int launch_lr_frame(const Dav1dGpuLrFrame *F, hipStream_t stream) {
     f.xb0 = xb[0];
     f.xb01 = xb[0] + xb[1];
     f.nx = xb[0] + xb[1] + xb[2];
-    {
-        const char *e = getenv("DAV1D_GPU_LR_ORDER");
-        f.linear = e && !strcmp(e, "linear");
-    }
     f.nwg = f.nx * stripes;
-    k_lr_frame<BPC><<<(unsigned)((f.nwg + 7) & ~7), 256, 0, stream>>>(f);
+    // (a grid of whole groups per XCD, so every logical workgroup has a block)
+    constexpr int per = 8 * kLrGroup;
+    k_lr_frame<BPC><<<(unsigned)((f.nwg + per - 1) / per * per), 256, 0, stream>>>(f);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         fprintf(stderr, "dav1d-gpu: loop restoration launch failed: %s\n", hipGetErrorString(e));

@@ -140,9 +140,17 @@ __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 // its wave idles while the small units' edge preparation runs per lane
 #define DGPU_IE_SMALL_LANES 0
 #endif
+#ifndef DGPU_IE_WIDE_LANES
+// the intra wavefront TUs (A/B, round 6): one 4x2 output task per lane for
+// every class (W*H/8, at most 64), not the unit batch's LDS-bound counts --
+// a wavefront task holds at most 8 units above level 0, and the flow trace
+// shows the tall classes (4x16: 4 lanes, 8x16: 8) as the levels' slowest
+#define DGPU_IE_WIDE_LANES 0
+#endif
 __host__ __device__ constexpr int lanes_per_unit(int tx) {
     const int w = tx_info(tx).w, h = tx_info(tx).h;
     if (DGPU_IE_SMALL_LANES && w * h <= 32) return DGPU_IE_SMALL_LANES;
+    if (DGPU_IE_WIDE_LANES) return cmin(cmax(w * h / 8, 2), 64);
     if (w * h >= 1024) return 64;
     // tall classes: as few lanes as the column pass has lines (or half as
     // many for 8x32), so the column transforms leave no lane idle, within

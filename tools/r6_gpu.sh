@@ -143,14 +143,13 @@ for s in "${@:-tests}"; do
                 (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/splitpmc_${f}_$n" -o run --output-format csv -- python3 "$R/tools/split_ab.py" --only $f --steps 10 --rounds 1) > "$O/splitpmc_${f}_$n.log" 2>&1 || { echo "[r6] splitpmc $f $n failed"; exit 1; }
             done
         done ;;
-    lrab) # LR workgroup order A/B (XCD-contiguous vs the dispatcher's), time + FETCH / WRITE per order
-        timeout -k 10 300 python -u tools/lr_ab.py --steps 100 --rounds 3 > "$O/lrab.json" 2> "$O/lrab.log" || { echo "[r6] lrab failed"; tail -5 "$O/lrab.log"; exit 1; }
-        cat "$O/lrab.json"
-        for m in xcd linear; do
-            for c in FETCH_SIZE WRITE_SIZE; do
-                (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/lrpmc_${m}_$c" -o run --output-format csv -- python3 "$R/tools/lr_ab.py" --only $m --steps 10 --rounds 1) > "$O/lrpmc_${m}_$c.log" 2>&1 || { echo "[r6] lrpmc $m $c failed"; exit 1; }
-            done
-        done ;;
+    fam) # the headline plus the per-family legs (mc / ipred / itx / ext) and configs 2 / 4
+        timeout -k 10 400 python -u bench.py --steps 100 --no-tiles --no-intra --no-recorder --no-grain --no-cdef --no-superres \
+            --no-lpf --no-lr --no-cpu > "$O/fam.json" 2> "$O/fam.log" || { echo "[r6] fam failed"; tail -5 "$O/fam.log"; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/fam.json')); print('fam', d['roofline']['kernel_us'], {k: v['kernel_us'] for k, v in d['families'].items()}, {k: v['kernel_us'] for k, v in d['configs'].items()}, d['config'].get('bit_exact_vs_oracle'))" ;;
+    fphase) # the intra wavefront's per-task / per-phase trace (diagnostics library fphase)
+        DAV1D_GPU_LIB_VARIANT=${FTV:-fphase} timeout -k 10 300 python -u tools/flow_trace.py > "$O/fphase_${FTV:-fphase}.json" 2> "$O/fphase.log" || { echo "[r6] fphase failed"; tail -5 "$O/fphase.log"; exit 1; }
+        head -c 3000 "$O/fphase_${FTV:-fphase}.json"; echo ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "[r6] smoke failed"; exit 1; } ;;
     bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r6] bench failed"; exit 1; } ;;
     benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r6] benchfast failed"; exit 1; } ;;
