@@ -8,6 +8,14 @@
 #ifndef DGPU_IE_SMALL_LANES
 #define DGPU_IE_SMALL_LANES 8
 #endif
+// Round 6: every other class one 4x2 output task per lane (W*H/8, at most
+// 64) instead of the unit batch's LDS-bound counts: the flow trace had the
+// tall classes (4x16: 4 lanes, 8x16: 8) as most levels' slowest task; 4K
+// one-tile intra frame 16.95 -> 15.55 ms, 2x2 tiles 10.42 -> 9.52 ms,
+// bit-exact (profiles/r6/r6e_intra_lanes_ab.json).
+#ifndef DGPU_IE_WIDE_LANES
+#define DGPU_IE_WIDE_LANES 1
+#endif
 #include "recon_ie.hpp"
 
 int dgpu_recon_ie_16bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, void *stream) {

@@ -29,8 +29,7 @@ for v in ${VARIANTS:-bounds}; do
         bounds) TUS="recon8 recon_ie8 recon_sb8 recorder tile8 tile16" build bounds -DDGPU_BOUNDS=1 ;;
         ftrace) TUS="recon_ie8" build ftrace -DDGPU_FLOW_TRACE=1 ;;
         ielanes16) TUS="recon_ie8" build ielanes16 -DDGPU_IE_SMALL_LANES=16 ;;
-        iewide) TUS="recon_ie8" build iewide -DDGPU_IE_WIDE_LANES=1 ;;
-        iewidef) TUS="recon_ie8" build iewidef -DDGPU_IE_WIDE_LANES=1 -DDGPU_FLOW_TRACE=1 ;;
+        ienarrow) TUS="recon_ie8" build ienarrow -DDGPU_IE_WIDE_LANES=0 ;;   # the round-5 lanes
         sbdiag) TUS="recon_sb8" build sbdiag -DDGPU_DIAG=1 ;;   # tools/sb_debug.py
         fphase) TUS="recon_ie8" build fphase -DDGPU_FLOW_TRACE=1 -DDGPU_TRACE=1 -DDGPU_TRACE_RT=1 ;;
         trace) build trace -DDGPU_TRACE=1 ;;

@@ -33,7 +33,7 @@ def main():
         # lanes_per_unit, csrc/recon_kernel.hpp
         lanes[t] = 64 if tw * th >= 1024 else min(max(min(tw * th // 8, max(tw, min(th, 32))), 2), 64)
         lanes[t] = {(8, 16): 8, (4, 16): 4, (8, 32): 16}.get((tw, th), lanes[t])   # the tall classes
-        if os.environ.get("DGPU_IE_WIDE_LANES", "0") == "1":   # (variant iewide / iewidef)
+        if os.environ.get("DGPU_IE_WIDE_LANES", "1") == "1":   # the wavefront TUs since round 6
             lanes[t] = min(max(tw * th // 8, 2), 64)
         if tw * th <= 32:   # the wavefront TUs: DGPU_IE_SMALL_LANES (recon_ie{8,16}.hip)
             lanes[t] = int(os.environ.get("DGPU_IE_SMALL_LANES", "8"))

@@ -45,7 +45,7 @@ for s in "${@:-tests}"; do
                 --no-grain --no-superres --no-lpf --no-cpu --no-check > "$O/benchpart.json" 2> "$O/benchpart.log" \
                 || { echo "[r6] benchpart failed"; exit 1; } ;;
     checkasm) # the full checkasm-style space (no --quick), one pass per table and bitdepth
-            for t in mc ipred itx; do for b in 8 16; do
+            for t in ${CKT:-mc ipred itx cdef lpf lr}; do for b in 8 16; do
                 timeout -k 10 1200 ./tests/checkasm_gpu --test=$t --bpc=$b --seed=1 > "$O/checkasm_full_${t}_${b}.log" 2>&1 \
                     || { echo "[r6] checkasm $t $b failed"; tail -5 "$O/checkasm_full_${t}_${b}.log"; exit 1; }
                 tail -1 "$O/checkasm_full_${t}_${b}.log"
