@@ -206,7 +206,7 @@ extern "C" int dav1d_gpu_set_device(int device) {
     return 0;
 }
 
-extern "C" const char *dav1d_gpu_version(void) { return "dav1d-gpu gfx950 r5"; }
+extern "C" const char *dav1d_gpu_version(void) { return "dav1d-gpu gfx950 r6"; }
 
 extern "C" int dav1d_gpu_get_error(void) { return dgpu::g_error.load(); }
 

@@ -150,6 +150,12 @@ for s in "${@:-tests}"; do
     fphase) # the intra wavefront's per-task / per-phase trace (diagnostics library fphase)
         DAV1D_GPU_LIB_VARIANT=${FTV:-fphase} timeout -k 10 300 python -u tools/flow_trace.py > "$O/fphase_${FTV:-fphase}.json" 2> "$O/fphase.log" || { echo "[r6] fphase failed"; tail -5 "$O/fphase.log"; exit 1; }
         head -c 3000 "$O/fphase_${FTV:-fphase}.json"; echo ;;
+    flowab) # the wavefront's units-per-task cap x coded-mode task groups (tools/flow_units_ab.py, one process each)
+        for U in ${FLOWU:-4 8 16}; do for TG in 0 1; do
+            DAV1D_GPU_FLOW_UNITS=$U FLOW_TASK_GROUPS=$TG timeout -k 10 300 python -u tools/flow_units_ab.py >> "$O/flowab.jsonl" 2>> "$O/flowab.log" \
+                || { echo "[r6] flowab $U $TG failed"; tail -5 "$O/flowab.log"; exit 1; }
+        done; done
+        cat "$O/flowab.jsonl" ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "[r6] smoke failed"; exit 1; } ;;
     bench) timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { echo "[r6] bench failed"; exit 1; } ;;
     benchfast) timeout -k 10 300 python -u bench.py $BENCH_FAST > "$O/benchfast.json" 2> "$O/benchfast.log" || { echo "[r6] benchfast failed"; exit 1; } ;;
