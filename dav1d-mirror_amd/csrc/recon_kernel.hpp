@@ -52,8 +52,12 @@ namespace dgpu {
 // 8-byte stores, nontemporal streams, resident waves) were deleted in round
 // 6; their A/B results stay under profiles/r3..r5 and in DESIGN.md.
 constexpr int kSegments = 16;      // spatial segments per class (task ordering; 8 / 32: 67 / 64 us)
-constexpr int kSegInner = 1;       // segments whose classes are scheduled as one group
-constexpr int kSeqRefMaxTpl = 2;   // compound refs one after the other through one tile up to this many tasks per lane
+// segments whose classes are scheduled as one group (2 / 4 / 16: 58.9 / 59.2
+// / 67.4 against 56.9 us, profiles/r6/r6j_krecon_seg_group_ab.json)
+constexpr int kSegInner = 1;
+// compound refs one after the other through one tile up to this many tasks
+// per lane (0: 60.2 against 56.8 us; profiles/r6/r6k_krecon_seqref_ch_ab.json)
+constexpr int kSeqRefMaxTpl = 2;
 
 template <int BPC> struct ReconArgs {
     using P = typename Px<BPC>::pixel;
@@ -841,7 +845,7 @@ template <int BPC, int TX, bool CLAMPABLE = false> struct HPass {
     static constexpr int PS = G / QW;   // row-pair step per task
     static_assert(G % QW == 0, "lane quads must be fixed");
     static constexpr int B = BPC / 8;
-    static constexpr int CH = cmin(IT, BPC == 8 ? 3 : 2);   // tasks whose loads are in flight together
+    static constexpr int CH = cmin(IT, BPC == 8 ? 3 : 2);   // tasks whose loads are in flight together (2-6: within noise)
     // 8bpc rows are read with dword-aligned loads from the row's dword and
     // realigned in registers (v_alignbyte by the byte skew): the texture
     // path splits an unaligned multi-dword load, measured 2.4-3.3x the cost
