@@ -106,7 +106,9 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
     int16_t(*HOR)[kLrSW] = reinterpret_cast<int16_t(*)[kLrSW]>(&AA[0][0]);
     static_assert(kLrTH * kLrSW * 2 <= (int)sizeof(AA), "HOR fits the A array");
     const int sw = min(kLrSW, a.w - x0), h = a.h;
-    const int bd8 = bits_of(a.bdmax) - 8;
+    // 8 bpc: compile-time bitdepth (the shifts and roundings of the A / B
+    // sums and both filters fold away)
+    const int bdmax = BPC == 8 ? 255 : a.bdmax, bd8 = BPC == 8 ? 0 : bits_of(a.bdmax) - 8;
     // a full strip on aligned planes (workgroup-uniform)
     const bool vec = a.vec && sw == kLrSW;
     if (vec) {   // the 32 interior columns read no padding: 16-byte row pieces
@@ -228,7 +230,7 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
                 int sum = -round_offset;
 #pragma unroll
                 for (int t = 0; t < 7; t++) sum += hv[t] * a.prm.filter[1][t];
-                const P o = (P)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, a.bdmax);
+                const P o = (P)clampi((sum + (1 << (rbv - 1))) >> rbv, 0, bdmax);
                 a.dst[(size_t)j * a.ds + x0 + wi] = o;
 #pragma unroll
                 for (int t = 0; t < 6; t++) hv[t] = hv[t + 1];
@@ -360,7 +362,7 @@ __device__ __forceinline__ void lr_strip(const LrArgs<BPC> &a, const int x0) {
         for (int r = 0; r < 8; r++) {
             const int j = wj0 + r;
             if (r >= wrpt || j >= h) break;
-            v[r] = clampi(T[j + 3][wi + 3] + ((v[r] + (1 << 10)) >> 11), 0, a.bdmax);
+            v[r] = clampi(T[j + 3][wi + 3] + ((v[r] + (1 << 10)) >> 11), 0, bdmax);
             a.dst[(size_t)j * a.ds + x0 + wi] = (P)v[r];
         }
     }
