@@ -780,7 +780,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "ms_per_step": round(el / args.steps * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -857,7 +857,8 @@ def main():
             out["loop_restoration"] = lr_breakdown(cfg, dev, args.steps)
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(fd)
-        assert out["roofline"]["kernel_us"] <= out["ms_per_step"] * 1e3, "kernel time exceeds the step time"
+        # (on the unrounded values: the stream events sit inside the wall-clock bracket)
+        assert kern_s <= el / args.steps * (1 + 1e-6), "kernel time exceeds the step time"
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -37,7 +37,10 @@
 namespace dgpu {
 
 constexpr int kFlowSpinLimit = 1 << 21;   // polls of ~0.25 us before a wave gives up: ~0.5 s
-constexpr int kFlowSleep = 8;             // s_sleep between polls (x64 cycles; 32 / 127 changed nothing)
+// s_sleep between polls (x64 cycles; 32 / 127 changed nothing, 1 loses 0.5-0.8
+// ms per 4K frame; issue priority after the wait is within noise:
+// profiles/r6/r6m_flow_prio_sleep_ab.json)
+constexpr int kFlowSleep = 8;
 
 struct FlowTask {   // 16 B
     int32_t level, cls, first, count;
