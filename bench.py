@@ -304,9 +304,12 @@ def intra_breakdown(cfg, dev, stream, steps):
 def recorder_breakdown(cfg, dev):
     """a 4K mixed frame (70% inter blocks) handed to the
     native batch recorder block by block and residual by residual
-    (dav1d_gpu_rec_*), then one flush: the flush's host time (units, edge
-    records, level schedule, upload) and its device time (HIP events with
-    the GPU kept busy while the host builds), checked against the oracle."""
+    (dav1d_gpu_rec_*), then one flush: the flush's host time (the call's wall
+    time: uploading the recording and waiting for the device-side cut and
+    schedule on the recorder's stream, then the launches), the device time
+    of that prep (HIP events on the recorder's stream) and of the picture's
+    work on the caller's stream (HIP events with the GPU kept busy while the
+    host builds), checked against the oracle."""
     import torch
     import dav1d_mirror_amd.intra as intra
     fr = intra.make_intra_frame(intra.IntraConfig(width=cfg.width, height=cfg.height, bpc=cfg.bpc,
@@ -319,7 +322,7 @@ def recorder_breakdown(cfg, dev):
               fr.plane_wh[p][0], fr.plane_wh[p][1]) for p, x in enumerate(rp)] for rp in fr.refs]
     rec = intra.Recorder(cfg.bpc, cfg.bitdepth_max, cfg.width, cfg.height, dev.index or 0)
     s = torch.cuda.current_stream(dev)
-    host, devt = [], []
+    host, devt, prep = [], [], []
     for _ in range(2):
         intra.replay(rec, fr)
         torch.cuda.synchronize(dev)
@@ -332,6 +335,7 @@ def recorder_breakdown(cfg, dev):
         e1.record(s)
         torch.cuda.synchronize(dev)
         devt.append(e0.elapsed_time(e1) * 1e-3)
+        prep.append(rec.prep_ms() * 1e-3)
     n_units, n_levels = rec.stats()
     rec.close()
     ho = ge.load_oracle().HostIntraFrame(fr)
@@ -379,6 +383,8 @@ def recorder_breakdown(cfg, dev):
         r_.close()
     return {"frame": f"{cfg.width}x{cfg.height}, 70% inter blocks", "units": n_units, "levels": n_levels,
             "flush_host_ms": round(host[-1] * 1e3, 2), "flush_device_ms": round(devt[-1] * 1e3, 3),
+            "flush_prep_device_ms": round(prep[-1] * 1e3, 3),
+            "flush_device_total_ms": round((devt[-1] + prep[-1]) * 1e3, 3),
             "device_gpix_s": round(px / devt[-1] / 1e9, 3), "bit_exact_vs_oracle": ok,
             "frame_threads": {"frames": nf, "host_threads": nf, "wall_ms": round(wall * 1e3, 2), "warm": True,
                               "flush_host_ms_per_frame": round(wall * 1e3 / nf, 2), "bit_exact_vs_oracle": ok_par}}

@@ -126,7 +126,7 @@ class IntraEdgeBatch(ctypes.Structure):
                 ("bitdepth_max", ctypes.c_int32)]
 
 
-IS_FUSED, IS_PERSISTENT, IS_SB = 1, 2, 4
+IS_FUSED, IS_PERSISTENT, IS_SB, IS_DEVICE_DEPS = 1, 2, 4, 8
 EDGE_BACKUP_DTYPE = np.dtype([("plane", "<i4"), ("sby", "<i4"), ("x0", "<i4"), ("w", "<i4")])
 
 
@@ -329,6 +329,8 @@ def load_lib():
         L.dav1d_gpu_recorder_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
                                                ctypes.POINTER(ctypes.c_int32)]
         L.dav1d_gpu_recorder_stats.restype = ctypes.c_int
+        L.dav1d_gpu_recorder_prep_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
+        L.dav1d_gpu_recorder_prep_ms.restype = ctypes.c_int
         L.dav1d_gpu_recorder_status.argtypes = [ctypes.c_void_p]
         L.dav1d_gpu_recorder_status.restype = ctypes.c_int
         L.dav1d_gpu_recorder_set_top_edge.argtypes = [ctypes.c_void_p, ctypes.POINTER(Plane * 3), ctypes.c_int]
@@ -368,6 +370,7 @@ EXPORTED_SYMBOLS = [
     "dav1d_gpu_intra_workspace_bytes",
     "dav1d_gpu_recorder_new", "dav1d_gpu_recorder_free", "dav1d_gpu_rec_block", "dav1d_gpu_rec_block_aux", "dav1d_gpu_rec_residual",
     "dav1d_gpu_recorder_flush", "dav1d_gpu_recorder_stats", "dav1d_gpu_recorder_status",
+    "dav1d_gpu_recorder_prep_ms",
     "dav1d_gpu_recorder_set_top_edge",
     "dav1d_gpu_apply_grain_8bpc", "dav1d_gpu_apply_grain_16bpc",
     "dav1d_cdef_dsp_init_8bpc", "dav1d_cdef_dsp_init_16bpc",

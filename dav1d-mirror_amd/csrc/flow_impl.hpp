@@ -705,7 +705,9 @@ static int64_t flow_workspace_bytes(const Dav1dGpuIntraSchedule *s, int n_units)
         const int64_t nd = sb_check(s);
         return nd < 0 ? -2 : (int64_t)sb_layout(s->n_levels, t.size(), s->n_sb, nd).total;
     }
-    const int64_t nd = flow_check_deps(s, n_units, t);
+    // DGPU_IS_DEVICE_DEPS: the producer lists stay where they are (device
+    // memory), nothing of them is copied into the workspace
+    const int64_t nd = (s->flags & DGPU_IS_DEVICE_DEPS) ? 0 : flow_check_deps(s, n_units, t);
     if (nd < 0) return -2;
     return (int64_t)flow_layout(s->n_levels, t.size(), n_units, nd, s->dep_start && s->deps).total;
 }
@@ -730,7 +732,8 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     if (rc) return rc;
     if (tasks.empty()) return 0;
     if (s->flags & DGPU_IS_SB) return flow_sb_launch(BPC, b, e, s, tasks, stream);
-    const int64_t nd = flow_check_deps(s, b->n_units, tasks);
+    const bool devdeps = s->flags & DGPU_IS_DEVICE_DEPS;
+    const int64_t nd = devdeps ? 0 : flow_check_deps(s, b->n_units, tasks);
     if (nd < 0) return -2;
     const bool dataflow = s->dep_start && s->deps;
     const FlowLayout Lw = flow_layout(s->n_levels, tasks.size(), b->n_units, nd, dataflow);
@@ -742,8 +745,8 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     f.tasks = (const FlowTask *)(ws + Lw.tasks);
     f.n_tasks = (int)tasks.size();
     f.level_tasks = (const int32_t *)(ws + Lw.level);
-    f.dep_start = dataflow ? (const int32_t *)(ws + Lw.dstart) : nullptr;
-    f.deps = (const int32_t *)(ws + Lw.deps);
+    f.dep_start = !dataflow ? nullptr : devdeps ? s->dep_start : (const int32_t *)(ws + Lw.dstart);
+    f.deps = devdeps ? s->deps : (const int32_t *)(ws + Lw.deps);
     f.trace = (unsigned long long *)(ws + Lw.trace);
     // DAV1D_GPU_FLOW_SPIN_LIMIT (tests): a smaller poll bound makes waves give
     // up early, to exercise the error word's reporting
@@ -759,7 +762,7 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
         uint8_t *st = (uint8_t *)sg->p;
         memcpy(st, tasks.data(), tasks.size() * sizeof(FlowTask));
         memcpy(st + (Lw.level - Lw.tasks), level_tasks.data(), level_tasks.size() * 4);
-        if (dataflow) {
+        if (dataflow && !devdeps) {
             memcpy(st + (Lw.dstart - Lw.tasks), s->dep_start, ((size_t)b->n_units + 1) * 4);
             memcpy(st + (Lw.deps - Lw.tasks), s->deps, (size_t)nd * 4);
         }

@@ -4,26 +4,31 @@
 // A decoder's recon_b_inter / recon_b_intra (src/recon_tmpl.c:1598, :1195)
 // hand over, per block and plane, what they would have passed to the DSP
 // (one Dav1dGpuRecBlock) and, per coded transform block, what they would
-// have passed to inv_txfm_add (dav1d_gpu_rec_residual).  A flush turns the
-// record into the device's work:
-//   1. transform units in decode order: every transform cell of every block
+// have passed to inv_txfm_add (dav1d_gpu_rec_residual).  The recording goes
+// straight into page-locked staging; a flush uploads it as recorded and
+// builds the device's work on the device, on the recorder's own stream:
+//   1. the cut (rec_cut.hpp): every transform cell of every block
 //      (recon_b_* iterate the block's transform grid, :1258-1262), carrying
-//      the block's prediction and the cell's residual if one was recorded;
-//   2. per intra / CfL unit the dav1d_prepare_intra_edges record exactly as
-//      recon_b_intra derives it: have_left / have_top against the tile start,
-//      the tile end as (w, h), and the per-transform edge flags of
-//      :1252-1266 from the block's intra_edge_flags;
-//   3. dependency levels at 4x4 granularity: inter units read only their
-//      references (level 0); an intra unit sits one level above every unit
-//      whose pixels the edges of its remapped mode read (CfL: also the
-//      co-located luma), and those units are its producers;
-//   4. units sorted by (level, size class, kind, mode, type), records in the
-//      same order, coefficients compacted to the stored region, and one
-//      persistent wavefront launch (dav1d_gpu_recon_intra_frame_*) whose
-//      waves wait for their producers only.
-// Host code only; the device work runs on the caller's stream.
+//      the block's prediction and the cell's residual if one was recorded,
+//      the dav1d_prepare_intra_edges record of each intra / CfL cell, the
+//      clamped footprint copies (emu_edge) and the launch-ahead units -- a
+//      count pass per block, an exclusive scan, a write pass per block;
+//   2. dependency levels at 4x4 granularity: every cell stamps its 4x4s in a
+//      writer map, looks up the writers of the pixels its edges (CfL: the
+//      co-located luma; an inter-intra residual: its block's prediction)
+//      read, and takes one level above the highest of them (a dataflow
+//      kernel in decode order, which is a topological order);
+//   3. one radix sort of (level, size class, kind, mode, type, decode
+//      index), the cells and their producer lists scattered to their ranks;
+//   4. the launch-ahead units in class order, and their superblock-bottom
+//      backup runs.
+// The host reads back three small results (the totals after the count, the
+// level count and class ranges at the end) and launches the persistent
+// wavefront (dav1d_gpu_recon_intra_frame_*) on the caller's stream, behind
+// the prep.  With DAV1D_GPU_REC_HOSTONLY (diagnostics, no device) the same
+// step functions run serially on the host.
 #include <hip/hip_runtime.h>
-#include <sched.h>
+#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -31,223 +36,110 @@
 
 #include <algorithm>
 #include <chrono>
-#include <condition_variable>
-#include <functional>
-#include <memory>
-#include <atomic>
-#include <mutex>
-#include <numeric>
-#include <thread>
 #include <vector>
 
 #include "bounds.hpp"
 #include "dav1d_gpu.h"
+#include "rec_cut.hpp"
 
 #ifndef DGPU_BOUNDS
 #define DGPU_BOUNDS 0
 #endif
 
+using namespace rec;
+
 namespace {
 
-struct TxDim { int w, h; };
-constexpr TxDim kTx[DGPU_N_RECT_TX_SIZES] = {
-    {4, 4}, {8, 8}, {16, 16}, {32, 32}, {64, 64}, {4, 8}, {8, 4}, {8, 16}, {16, 8}, {16, 32},
-    {32, 16}, {32, 64}, {64, 32}, {4, 16}, {16, 4}, {8, 32}, {32, 8}, {16, 64}, {64, 16}};
-
-// av1_intra_prediction_edges needs (src/ipred_prepare_tmpl.c:50-75):
-// bit0 left, 1 top, 2 top-left, 3 top-right, 4 bottom-left
-constexpr uint8_t kNeeds[14] = {3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7};
-
-// the mode remap of dav1d_prepare_intra_edges (:83-104)
-int remap_mode(int mode, int angle, bool hl, bool ht) {
-    static const int dir[8] = {90, 180, 45, 135, 113, 157, 203, 67};
-    if (mode >= 1 && mode <= 8) {
-        const int a = dir[mode - 1] + 3 * angle;
-        if (a <= 90) return a < 90 && ht ? DGPU_Z1_PRED : DGPU_VERT_PRED;
-        if (a < 180) return DGPU_Z2_PRED;
-        return a > 180 && hl ? DGPU_Z3_PRED : DGPU_HOR_PRED;
-    }
-    if (mode == 0) return hl ? (ht ? DGPU_DC_PRED : DGPU_LEFT_DC_PRED) : (ht ? DGPU_TOP_DC_PRED : DGPU_DC_128_PRED);
-    if (mode == 12) return hl ? (ht ? DGPU_PAETH_PRED : DGPU_HOR_PRED) : (ht ? DGPU_VERT_PRED : DGPU_DC_128_PRED);
-    return mode;
+static bool host_only() {   // DAV1D_GPU_REC_HOSTONLY=1 (diagnostics, no device needed)
+    static const bool v = getenv("DAV1D_GPU_REC_HOSTONLY") != nullptr;
+    return v;
 }
 
-struct Residual {
-    int plane, x, y, tx, txtp, nzw, nzh;
-    size_t coef;   // offset into the recorder's compact pool
-};
-
-struct DevBuf {
+// device buffers (host memory for host-only flushes), grown as needed
+struct Mem {
     void *p = nullptr;
     size_t cap = 0;
+    template <typename T> T *as() const { return (T *)p; }
     int grow(size_t n) {
-        if (n <= cap) return 0;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
+        if (n <= cap && p) return 0;
+        release();
         // rounded up to 256 bytes: the one read past a buffer's last element
         // the kernels make by design is Stage's (the 16-byte block holding a
-        // region's last byte, at most 15 bytes further).  (Round 3 padded
-        // every buffer with 64 KiB after an unexplained fault; the DGPU_BOUNDS
-        // build, which checks every access against these buffers' exact
-        // sizes, reports none)
-        const size_t sz = (n + 255) & ~(size_t)255;
-        if (hipMalloc(&p, sz) != hipSuccess) return -1;
-        cap = n;
-        return 0;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
-
-// page-locked staging, so the uploads do not wait for the stream.
-// DAV1D_GPU_REC_PIN (tuning): "default" hipHostMalloc, otherwise (the
-// default) non-coherent hipHostMalloc (CPU-cached: the fill writes it at
-// memory speed).  Nothing in the library registers ordinary host memory:
-// round 5 removed the hipHostRegister mode that rounds 3-4 suspected of the
-// intermittent illegal-address faults
-static int pin_mode() {
-    static const int m = [] {
-        const char *e = getenv("DAV1D_GPU_REC_PIN");
-        return (e && !strcmp(e, "default")) ? 0 : 1;
-    }();
-    return m;
-}
-struct PinnedBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    int grow(size_t n) {
-        if (n <= cap) return 0;
-        release();
-        if (hipHostMalloc(&p, n, pin_mode() ? hipHostMallocNonCoherent : hipHostMallocDefault) != hipSuccess) {
+        // region's last byte, at most 15 bytes further)
+        const size_t sz = (std::max<size_t>(n, 16) + 255) & ~(size_t)255;
+        if (host_only()) {
+            p = malloc(sz);
+            if (!p) return -1;
+        } else if (hipMalloc(&p, sz) != hipSuccess) {
             p = nullptr;
             return -1;
         }
-        cap = n;
+        cap = sz;
         return 0;
     }
     void release() {
-        if (p) (void)hipHostFree(p);
+        if (p) {
+            if (host_only()) free(p);
+            else (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
 };
 
-// A few host workers kept for a recorder's lifetime: every parallel step of
-// a flush runs on them (no thread start per step).  run(nt, f) calls f(t) for
-// t in [0, nt) and returns when all have; the caller runs t = 0.
-class Pool {
-public:
-    explicit Pool(int n) : n_(std::max(1, n)) {
-        for (int i = 1; i < n_; i++) th_.emplace_back([this, i] { loop(i); });
+// The recording: page-locked (portable, CPU-cached unless
+// DAV1D_GPU_REC_PIN=default) so the flush's uploads are asynchronous copies
+// of it, or ordinary memory for host-only flushes.  Nothing in the library
+// registers ordinary host memory.
+struct Stage {
+    uint8_t *p = nullptr;
+    size_t n = 0, cap = 0;
+    bool pinned = false;
+    void *append(size_t m) {
+        if (n + m > cap && reserve(n + m)) return nullptr;
+        void *q = p + n;
+        n += m;
+        return q;
     }
-    ~Pool() {
-        {
-            std::lock_guard<std::mutex> l(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto &t : th_) t.join();
-    }
-    int size() const { return n_; }
-    template <typename F> void run(int nt, F &&f) {
-        nt = std::min(nt, n_);
-        if (nt <= 1) {
-            f(0);
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> l(m_);
-            job_ = [&f](int t) { f(t); };
-            nt_ = nt;
-            pending_ = nt - 1;
-            gen_++;
-        }
-        cv_.notify_all();
-        f(0);
-        std::unique_lock<std::mutex> l(m_);
-        done_.wait(l, [this] { return pending_ == 0; });
-    }
-
-private:
-    void loop(int i) {
-        unsigned seen = 0;
-        for (;;) {
-            std::function<void(int)> job;
-            int nt;
-            {
-                std::unique_lock<std::mutex> l(m_);
-                cv_.wait(l, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                job = job_;
-                nt = nt_;
-            }
-            if (i < nt) {
-                job(i);
-                std::lock_guard<std::mutex> l(m_);
-                if (--pending_ == 0) done_.notify_one();
+    int reserve(size_t m) {
+        const size_t nc = std::max(m, std::max<size_t>(2 * cap, 1 << 16));
+        void *q = nullptr;
+        bool pin = !host_only();
+        if (pin) {
+            static const bool coherent = [] {
+                const char *e = getenv("DAV1D_GPU_REC_PIN");
+                return e && !strcmp(e, "default");
+            }();
+            // (no device in this process yet, or none at all: ordinary
+            // memory, uploaded through the runtime's staging)
+            if (hipHostMalloc(&q, nc, hipHostMallocPortable | (coherent ? 0 : hipHostMallocNonCoherent)) != hipSuccess) {
+                q = nullptr;
+                pin = false;
             }
         }
+        if (!q && !(q = malloc(nc))) return -1;
+        if (n) memcpy(q, p, n);
+        release_mem();
+        p = (uint8_t *)q;
+        cap = nc;
+        pinned = pin;
+        return 0;
     }
-    int n_;
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    std::function<void(int)> job_;
-    int nt_ = 0, pending_ = 0;
-    unsigned gen_ = 0;
-    bool stop_ = false;
+    void release_mem() {
+        if (p) {
+            if (pinned) (void)hipHostFree(p);
+            else free(p);
+        }
+        p = nullptr;
+        cap = 0;
+    }
+    void release() {
+        release_mem();
+        n = 0;
+    }
 };
 
-// LSD radix sort of 64-bit keys on bits [lo, hi), digits of at most 13 bits, by up to
-// nt threads (per-thread digit counts over contiguous chunks, so it stays
-// stable: keys whose low bits hold their input index need not sort those)
-void radix_sort(std::vector<uint64_t> &k, std::vector<uint64_t> &tmp, int lo, int hi, Pool &pool) {
-    int nt = pool.size();
-    const int passes = (hi - lo + 12) / 13, DB = (hi - lo + passes - 1) / std::max(passes, 1), ND = 1 << DB;
-    const size_t n = k.size();
-    tmp.resize(n);
-    nt = n < 65536 ? 1 : nt;
-    std::vector<uint32_t> cnt((size_t)nt * ND);
-    for (int sh = lo; sh < hi; sh += DB) {
-        auto count = [&](int t) {
-            uint32_t *c = &cnt[(size_t)t * ND];
-            std::fill(c, c + ND, 0);
-            for (size_t i = n * t / nt, e = n * (t + 1) / nt; i < e; i++) c[(k[i] >> sh) & (ND - 1)]++;
-        };
-        auto scatter = [&](int t) {
-            uint32_t *c = &cnt[(size_t)t * ND];
-            for (size_t i = n * t / nt, e = n * (t + 1) / nt; i < e; i++) tmp[c[(k[i] >> sh) & (ND - 1)]++] = k[i];
-        };
-        pool.run(nt, count);
-        uint32_t acc = 0;   // digit-major, then thread: every thread's keys of a digit after the earlier threads'
-        for (int d = 0; d < ND; d++)
-            for (int t = 0; t < nt; t++) {
-                const uint32_t v = cnt[(size_t)t * ND + d];
-                cnt[(size_t)t * ND + d] = acc;
-                acc += v;
-            }
-        pool.run(nt, scatter);
-        k.swap(tmp);
-    }
-}
-
-// emu_edge per transform / prediction unit (src/recon_tmpl.c:986-999,
-// scaled :1036-1046, warp :1168-1177): a footprint that leaves its reference
-// picture is copied, every read clamped, into a scratch plane of kEmuStride
-// pixels per row (a band of rows per copy; warp 8x8s side by side)
-constexpr int kEmuStride = 128;
-struct EmuJob {
-    int32_t x0, y0;   // the footprint's top-left in the reference (may be outside)
-    int32_t o0;       // its top-left in the scratch plane (pixels)
-    uint8_t w, h, slot, plane;
-};
-static_assert(sizeof(EmuJob) == 16, "EmuJob layout");
-
+// one 64-lane workgroup per footprint: lanes along the row, clamped reads
 struct EmuArgs {
     const void *ref[DGPU_MAX_REFS - 1][3];
     int32_t stride[DGPU_MAX_REFS - 1][3];   // pixels
@@ -256,8 +148,6 @@ struct EmuArgs {
     const EmuJob *jobs;
     int32_t n, rows;   // rows: the scratch plane's (diagnostics)
 };
-
-// one 64-lane workgroup per footprint: lanes along the row, clamped reads
 template <typename P>
 __global__ __launch_bounds__(64) void k_emu_footprints(EmuArgs a) {
     const int j = blockIdx.x;
@@ -280,150 +170,196 @@ __global__ __launch_bounds__(64) void k_emu_footprints(EmuArgs a) {
     }
 }
 
-// per 4x4 cell of a plane: the decode-order cell that last wrote it, stored
-// as the flush's cell base + the cell index, so the maps are never cleared:
-// an entry below the current base was written by an earlier flush (no
-// producer, level -1 for the level rule).
+template <typename F>
+__global__ __launch_bounds__(256) void k_each(int n, F f) {
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i < n) f(i);
+}
 
-struct Unit {   // a transform cell before sorting
-    Dav1dGpuUnit u;
-    Dav1dGpuIntraEdge rec;
-    int level;
-    int sortmode;
-    int32_t aux;   // aux_pool offset (INTER_MASK / PAL), else 0
+// the sort key of a cell: level | tx (5) | pred (4) | mode (6) | type (5,
+// NO_RESIDUAL last), then the decode index in the low 21 bits (the sort is
+// then a stable one by the key)
+__host__ __device__ inline uint64_t level_key(const Dav1dGpuUnit &u, int sortmode, int level, int ci) {
+    const uint64_t key = (uint64_t)level << 20 | (uint64_t)u.tx << 15 | (uint64_t)u.pred << 11 |
+                         (uint64_t)(sortmode & 63) << 5 | (uint64_t)(u.txtp == DGPU_NO_RESIDUAL ? 31 : u.txtp);
+    return key << 21 | (uint64_t)ci;
+}
+
+struct LevelArgs {
+    const int32_t *pstart, *prod, *csort;
+    const Dav1dGpuUnit *cu;
+    int32_t *lv;
+    uint64_t *keys;
+    Hdr *hdr;
+    int n, spin_limit;
 };
+constexpr int kLevelSpinLimit = 1 << 22;
+// The levels in decode order: one wave per 64 consecutive cells, taken by
+// ticket, so every cell a wave waits for is held by a wave that already
+// runs (producers come earlier in decode order).  A cell's level is one above
+// its producers' highest; producers inside the wave are read from LDS, the
+// others from the level array at agent scope (the level is the datum, no
+// fence needed).  The loop is wave-uniform: a lane whose producers are not
+// all known yet tries again on the next pass.
+__global__ __launch_bounds__(64) void k_levels(LevelArgs a) {
+    __shared__ int32_t slv[64];
+    const int lane = threadIdx.x;
+    int t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(&a.hdr->ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __shfl(t, 0);
+    const int c0 = t * 64, ci = c0 + lane;
+    const bool live = ci < a.n;
+    slv[lane] = -1;
+    __syncthreads();
+    int k = live ? a.pstart[ci] : 0;
+    const int k1 = live ? a.pstart[ci + 1] : 0;
+    int d = -1, level = 0;
+    bool done = !live;
+    for (int it = 0;; it++) {
+        if (!done) {
+            for (; k < k1; k++) {
+                const int q = a.prod[k];
+                const int v = q >= c0 ? slv[q - c0]
+                                      : __hip_atomic_load(&a.lv[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v < 0) break;
+                d = max(d, v);
+            }
+            if (k >= k1) {
+                level = d + 1;
+                done = true;
+                slv[lane] = level;
+                __hip_atomic_store(&a.lv[ci], level, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        if (__all(done)) break;
+        if (it >= a.spin_limit) {   // never expected: the flush fails instead of hanging
+            if (lane == 0) aor(&a.hdr->err, E_STALL);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    int m = 0;
+    if (live) {
+        const Dav1dGpuUnit u = a.cu[ci];
+        a.keys[ci] = level_key(u, a.csort[ci], level, ci);
+        m = level;
+    }
+    for (int o = 32; o; o >>= 1) m = max(m, __shfl_xor(m, o));
+    if (lane == 0) amax(&a.hdr->max_level, m);
+}
 
-// what the level pass needs of a cell (its geometry in 4x4 units, the edge
-// needs of its remapped mode, the tile end) and which of its offsets are
-// part-local until the parts are joined
-struct LvJob {
-    int16_t x4, y4, W4, H4;
-    uint8_t p, cw4, ch4, nd, fl, fix;
-    int32_t link;   // IIRES: its block's inter-intra prediction cell (part-local until the join)
-    enum { HL = 1, HT = 2, TR = 4, BL = 8, CFL = 16, IIRES = 32, IIC = 64 };
-};
-
-// one thread's run of blocks, cut into cells with part-local offsets
-struct CellPart {
-    enum { F_AUX = 1, F_EDGE = 2, F_EMU0 = 4, F_EMU1 = 8, F_IIREC = 16 };
-    std::vector<Unit> cells;
-    std::vector<LvJob> jobs;
-    std::vector<uint8_t> auxp;
-    std::vector<EmuJob> emu;
-    std::vector<Dav1dGpuUnit> xunits;
-    std::vector<int32_t> xaux;
-    std::vector<uint8_t> xfix;       // per launch-ahead unit: F_EMU0 / F_EMU1 (part-local src_off)
-    std::vector<int32_t> emu_auxfix; // aux_pool offsets of int32 part-local scratch offsets (OBMC / scaled)
-    int32_t emu_rows = 0;
-    size_t edge_px = 0, n_res_used = 0;
-    int32_t wm_off = -1, wm_w = 0, wm_h = 0;   // the last INTER_WMASK block's seg mask (4:2:0)
+// The flush's steps on the device (the recorder's stream) or serially on the
+// host (host-only flushes)
+struct Exec {
+    bool host;
+    hipStream_t st;
+    Mem *tmp;   // hipcub temporary storage
     int err = 0;
-    void clear() {
-        cells.clear();
-        jobs.clear();
-        auxp.clear();
-        emu.clear();
-        xunits.clear();
-        xaux.clear();
-        xfix.clear();
-        emu_auxfix.clear();
-        emu_rows = 0;
-        edge_px = n_res_used = 0;
-        wm_off = -1;
-        wm_w = wm_h = 0;
-        err = 0;
+    template <typename F> void each(long long n, F f) {
+        if (n <= 0 || err) return;
+        if (host) {
+            for (long long i = 0; i < n; i++) f((int)i);
+            return;
+        }
+        k_each<<<dim3((unsigned)((n + 255) / 256)), 256, 0, st>>>((int)n, f);
+        if (hipGetLastError() != hipSuccess) err = -3;
     }
-    int32_t aux_alloc(size_t nbytes) {   // 16-byte aligned records
-        const size_t o = (auxp.size() + 15) & ~(size_t)15;
-        auxp.resize(o + nbytes);
-        return (int32_t)o;
+    void memset(void *p, int v, size_t n) {
+        if (!n || err) return;
+        if (host) ::memset(p, v, n);
+        else if (hipMemsetAsync(p, v, n, st) != hipSuccess) err = -3;
     }
-    // a clamped copy of the fw x fh footprint at (x0, y0) of ref slot / plane
-    // in a band of new scratch rows; returns its part-local scratch offset
-    int32_t emu_band(int x0, int y0, int fw, int fh, int slot, int plane) {
-        const int32_t o = emu_rows * kEmuStride;
-        emu.push_back(EmuJob{x0, y0, o, (uint8_t)fw, (uint8_t)fh, (uint8_t)slot, (uint8_t)plane});
-        emu_rows += fh;
-        return o;
+    void upload(void *d, const void *h, size_t n) {
+        if (!n || err) return;
+        if (host) memcpy(d, h, n);
+        else if (hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st) != hipSuccess) err = -3;
+    }
+    void fetch(void *h, const void *d, size_t n) {   // queued; complete after sync()
+        if (!n || err) return;
+        if (host) memcpy(h, d, n);
+        else if (hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st) != hipSuccess) err = -3;
+    }
+    void sync() {
+        if (!host && !err && hipStreamSynchronize(st) != hipSuccess) err = -3;
+    }
+    // exclusive sum of n1 int32 (in[n1 - 1] = 0 gives the total in out[n1 - 1])
+    void scan(const int32_t *in, int32_t *out, int n1) {
+        if (n1 <= 0 || err) return;
+        if (host) {
+            int32_t acc = 0;
+            for (int i = 0; i < n1; i++) {
+                const int32_t v = in[i];
+                out[i] = acc;
+                acc += v;
+            }
+            return;
+        }
+        size_t b = 0;
+        if (hipcub::DeviceScan::ExclusiveSum(nullptr, b, in, out, n1, st) != hipSuccess || tmp->grow(b) ||
+            hipcub::DeviceScan::ExclusiveSum(tmp->p, b, in, out, n1, st) != hipSuccess)
+            err = -3;
+    }
+    void scan_blocks(const BlockCnt *in, BlockCnt *out, int n) {
+        if (n <= 0 || err) return;
+        if (host) {
+            BlockCnt acc{};
+            for (int i = 0; i < n; i++) {
+                const BlockCnt v = in[i];
+                out[i] = acc;
+                acc = BlockCntSum()(acc, v);
+            }
+            return;
+        }
+        size_t b = 0;
+        const BlockCnt z{};
+        if (hipcub::DeviceScan::ExclusiveScan(nullptr, b, in, out, BlockCntSum(), z, n, st) != hipSuccess ||
+            tmp->grow(b) || hipcub::DeviceScan::ExclusiveScan(tmp->p, b, in, out, BlockCntSum(), z, n, st) != hipSuccess)
+            err = -3;
+    }
+    void sort(const uint64_t *in, uint64_t *out, int n, int lo, int hi) {   // keys are distinct
+        if (n <= 0 || err) return;
+        if (host) {
+            memcpy(out, in, (size_t)n * 8);
+            std::sort(out, out + n);
+            return;
+        }
+        size_t b = 0;
+        if (hipcub::DeviceRadixSort::SortKeys(nullptr, b, in, out, n, lo, hi, st) != hipSuccess || tmp->grow(b) ||
+            hipcub::DeviceRadixSort::SortKeys(tmp->p, b, in, out, n, lo, hi, st) != hipSuccess)
+            err = -3;
     }
 };
-
-// kinds recorded with block data (dav1d_gpu_rec_block_aux); the last four
-// are predicted by the launch ahead of the wavefront
-inline bool is_ext_kind(int k) {
-    return k == DGPU_PRED_INTER_MASK || k == DGPU_PRED_PAL || k == DGPU_PRED_WARP || k == DGPU_PRED_INTER_WMASK ||
-           k == DGPU_PRED_INTER_OBMC || k == DGPU_PRED_INTER_SCALED || k == DGPU_PRED_INTER_INTRA;
-}
-inline bool is_prelaunch_kind(int k) {
-    return k == DGPU_PRED_WARP || k == DGPU_PRED_INTER_WMASK || k == DGPU_PRED_INTER_OBMC ||
-           k == DGPU_PRED_INTER_SCALED;
-}
-inline bool is_mc_kind(int k) {   // the flow kinds that read references through src_off
-    return k == DGPU_PRED_INTER || k == DGPU_PRED_INTER_AVG || k == DGPU_PRED_INTER_WAVG ||
-           k == DGPU_PRED_INTER_MASK;
-}
-inline int tx_of(int w, int h) {
-    for (int t = 0; t < DGPU_N_RECT_TX_SIZES; t++)
-        if (kTx[t].w == w && kTx[t].h == h) return t;
-    return -1;
-}
-
-struct ObmcBlockLap {   // dav1d_gpu_rec_block_aux INTER_OBMC entry (24 B)
-    int32_t mvx, mvy;
-    uint8_t filter2d, ref, x0, y0, x1, y1, lap_w4, lap_h4, dir, mask_off, pad_[6];
-};
-struct ObmcUnitLap {    // Dav1dGpuPredKind INTER_OBMC unit entry (16 B)
-    int32_t src_off;
-    uint8_t mx, my, filter2d, ref, x0, y0, x1, y1, lap_w4, lap_h4, dir, mask_off;
-};
-struct ScaledBlockRef {   // INTER_SCALED block record, per ref
-    int32_t x, y;
-    uint16_t mx, my, dx, dy;
-};
-struct ScaledUnitRef {
-    int32_t src_off;
-    uint16_t mx, my, dx, dy;
-    uint32_t pad_;
-};
-static_assert(sizeof(ObmcBlockLap) == 24 && sizeof(ObmcUnitLap) == 16 && sizeof(ScaledBlockRef) == 16 &&
-              sizeof(ScaledUnitRef) == 16, "aux record layouts");
 
 }  // namespace
 
 struct Dav1dGpuRecorder {
     int bpc, bdmax, width, height, device;
-    std::vector<Dav1dGpuRecBlock> blocks;
-    std::vector<int64_t> block_aux;   // per block: offset into baux, -1 none
-    std::vector<uint8_t> baux;        // dav1d_gpu_rec_block_aux data
-    std::vector<Residual> residuals;
-    std::vector<uint8_t> coefb;    // compact regions in the ABI's coefficient type (int16 / int32)
-    // flush products (kept alive while the device may still read them)
-    std::vector<int32_t> unit_start, class_start, rec_start, run_start;
-    std::vector<Unit> cells;
-    std::vector<LvJob> jobs;
-    std::vector<CellPart> parts;
-    std::unique_ptr<Pool> pool;   // host workers of the flush's parallel steps
-    std::vector<uint64_t> keys, keys_tmp;
-    std::vector<int32_t> rank;
-    std::vector<int32_t> prod_start, prod, dep_start, deps;   // producers: decode order, then level order
-    std::vector<EmuJob> emu;     // clamped footprint copies of this flush
-    std::vector<uint8_t> auxp;   // the aux pool: masks, palette / warp / OBMC / scaled records
-    std::vector<Dav1dGpuUnit> xunits;   // the launch ahead of the wavefront (class order)
-    std::vector<int32_t> xaux;
-    std::vector<Dav1dGpuEdgeBackup> bk;   // backup runs of launch-ahead predictions (top_edge)
-    std::vector<uint8_t> h_host;   // DAV1D_GPU_REC_HOSTONLY: stands in for the pinned buffer
+    // the recording
+    Stage blocks, baux_off, baux, res, coefb;
+    int32_t last_wmask = -1;   // the last INTER_WMASK block (COMPOUND_SEG chroma masks read it)
+    int64_t cell_bound = 0;    // an upper bound of the recording's cells
     // per-4x4 maps kept across flushes (generation-stamped): the residual
     // recorded at each cell (index + res_base) and its writer (cell_base + cell)
-    std::vector<int32_t> res_at[3];
-    std::vector<int32_t> own[3];
-    std::vector<int32_t> lv;                 // per decode-order cell: its level
-    std::vector<int32_t> prod_cnt;           // per decode-order cell: its producer count
-    std::vector<std::vector<int32_t>> tprod; // producers found by each worker (its cell range)
+    Mem res_at, own;
+    size_t map_off[3] = {0, 0, 0};
     int32_t map_w4[3] = {0, 0, 0}, map_h4[3] = {0, 0, 0};
     int32_t res_base = 0, cell_base = 0;
-    PinnedBuf pin;   // units | recs | coefficients | emu jobs, written in place by the fill
-    PinnedBuf flag;  // the last flush's wavefront error word, copied back on its stream
-    DevBuf d_units, d_recs, d_coef, d_edges, d_work, d_emu, d_emu_jobs, d_aux, d_auxp, d_xunits, d_xaux, d_bk;
+    // the flush's buffers
+    Mem d_blocks, d_baux_off, d_baux, d_res, d_coef;
+    Mem d_hdr, d_cnt, d_base, d_auxend;
+    Mem d_cu, d_crec, d_caux, d_csort, d_jobs, d_rawc, d_raws, d_raw, d_pcnt, d_pstart, d_prod, d_lv;
+    Mem d_keys, d_keys2, d_rank, d_ends, d_lend, d_dcnt, d_dstart, d_deps;
+    Mem d_units, d_recs, d_aux, d_auxp, d_emu_jobs, d_xu0, d_xa0, d_xk, d_xk2, d_xunits, d_xaux, d_xends;
+    Mem d_bkf, d_bks, d_bk, d_edges, d_work, d_emu, d_tmp;
+    std::vector<int32_t> unit_start, class_start, rec_start, run_start;
+    hipStream_t pst = nullptr;    // the recorder's stream (the prep)
+    hipEvent_t prep = nullptr;    // the prep done, for the caller's stream
+    hipEvent_t pt0 = nullptr, pt1 = nullptr;   // the prep's span (timing events)
+    float prep_ms = 0;
+    void *rb = nullptr;           // page-locked readback
+    size_t rb_cap = 0;
+    void *flag = nullptr;         // the last flush's wavefront error word, copied back on its stream
     // dav1d_gpu_recorder_set_top_edge: the caller's f->ipred_edge planes
     // (superblock-top rows read from and backed up to them), luma superblock log2
     Dav1dGpuPlane top[3] = {};
@@ -432,22 +368,17 @@ struct Dav1dGpuRecorder {
     hipEvent_t done = nullptr;
     bool pending_check = false;   // the last flush's error word not read yet
     int32_t last_units = 0, last_levels = 0;
+    void drop_recording() {
+        blocks.n = baux_off.n = baux.n = res.n = coefb.n = 0;
+        last_wmask = -1;
+        cell_bound = 0;
+    }
+    size_t nblocks() const { return blocks.n / sizeof(Dav1dGpuRecBlock); }
+    size_t nres() const { return res.n / sizeof(RecRes); }
 };
-
-// recorders alive in the process: a decoder with frame threads owns one per
-// frame, and each sizes its worker pool to its share of the CPUs the process
-// may run on (four recorders of 8 workers each oversubscribed
-// the host)
-static std::atomic<int> g_live_recorders{0};
-static int rec_cpu_budget() {
-    cpu_set_t set;
-    if (sched_getaffinity(0, sizeof(set), &set) == 0) return std::max(1, CPU_COUNT(&set));
-    return (int)std::max(1u, std::thread::hardware_concurrency());
-}
 
 extern "C" Dav1dGpuRecorder *dav1d_gpu_recorder_new(int bpc, int bitdepth_max, int width, int height, int device) {
     if ((bpc != 8 && bpc != 16) || width <= 0 || height <= 0) return nullptr;
-    g_live_recorders.fetch_add(1, std::memory_order_relaxed);
     Dav1dGpuRecorder *r = new Dav1dGpuRecorder();
     r->bpc = bpc;
     r->bdmax = bpc == 8 ? 255 : bitdepth_max;
@@ -459,26 +390,28 @@ extern "C" Dav1dGpuRecorder *dav1d_gpu_recorder_new(int bpc, int bitdepth_max, i
 
 extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
     if (!r) return;
-    g_live_recorders.fetch_sub(1, std::memory_order_relaxed);
-    if (hipSetDevice(r->device) == hipSuccess) {
+    if (host_only() || hipSetDevice(r->device) == hipSuccess) {
         if (r->done) {
             (void)hipEventSynchronize(r->done);
             (void)hipEventDestroy(r->done);
         }
-        r->pin.release();
-        r->flag.release();
-        r->d_units.release();
-        r->d_recs.release();
-        r->d_coef.release();
-        r->d_edges.release();
-        r->d_work.release();
-        r->d_emu.release();
-        r->d_emu_jobs.release();
-        r->d_aux.release();
-        r->d_auxp.release();
-        r->d_xunits.release();
-        r->d_xaux.release();
-        r->d_bk.release();
+        if (r->pst) {
+            (void)hipStreamSynchronize(r->pst);
+            (void)hipStreamDestroy(r->pst);
+        }
+        for (hipEvent_t e : {r->prep, r->pt0, r->pt1})
+            if (e) (void)hipEventDestroy(e);
+        if (r->rb) (void)hipHostFree(r->rb);
+        if (r->flag) (void)hipHostFree(r->flag);
+        for (Stage *s : {&r->blocks, &r->baux_off, &r->baux, &r->res, &r->coefb}) s->release();
+        for (Mem *m : {&r->res_at, &r->own, &r->d_blocks, &r->d_baux_off, &r->d_baux, &r->d_res, &r->d_coef, &r->d_hdr,
+                       &r->d_cnt, &r->d_base, &r->d_auxend, &r->d_cu, &r->d_crec, &r->d_caux, &r->d_csort, &r->d_jobs,
+                       &r->d_rawc, &r->d_raws, &r->d_raw, &r->d_pcnt, &r->d_pstart, &r->d_prod, &r->d_lv, &r->d_keys,
+                       &r->d_keys2, &r->d_rank, &r->d_ends, &r->d_lend, &r->d_dcnt, &r->d_dstart, &r->d_deps,
+                       &r->d_units, &r->d_recs, &r->d_aux, &r->d_auxp, &r->d_emu_jobs, &r->d_xu0, &r->d_xa0, &r->d_xk,
+                       &r->d_xk2, &r->d_xunits, &r->d_xaux, &r->d_xends, &r->d_bkf, &r->d_bks, &r->d_bk, &r->d_edges,
+                       &r->d_work, &r->d_emu, &r->d_tmp})
+            m->release();
     }
     delete r;
 }
@@ -494,7 +427,6 @@ static bool plane_dims(const Dav1dGpuRecorder *r, int plane, int &w, int &h) {
     h = plane ? gh >> 1 : gh;
     return true;
 }
-constexpr int kMapPad4 = 32;   // 4x4 cells past the grid a transform block can reach (128 px)
 
 // The decoder's superblock-top edge rows (f->ipred_edge, backed up by
 // dav1d_backup_ipred_edge, src/recon_tmpl.c:2162-2186, and read by
@@ -528,15 +460,15 @@ static int check_block(const Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, boo
     int pw, ph;
     if (!r || !b || !plane_dims(r, b->plane, pw, ph)) return -1;
     if (b->tx < 0 || b->tx >= DGPU_N_RECT_TX_SIZES) return -1;
-    const TxDim t = kTx[b->tx];
+    const int tw = tx_w(b->tx), th = tx_h(b->tx);
     if (b->x < 0 || b->y < 0 || b->w <= 0 || b->h <= 0 || b->x >= pw || b->y >= ph || b->w > 128 || b->h > 128)
         return -1;
-    if ((b->x & 3) || (b->y & 3) || b->w % t.w || b->h % t.h) return -1;
+    if ((b->x & 3) || (b->y & 3) || b->w % tw || b->h % th) return -1;
     if (ext != is_ext_kind(b->kind)) return -1;
     const bool inter = b->kind == DGPU_PRED_INTER || b->kind == DGPU_PRED_INTER_AVG ||
                        b->kind == DGPU_PRED_INTER_WAVG || (ext && b->kind != DGPU_PRED_PAL);
     if (!inter && b->kind != DGPU_PRED_INTRA && b->kind != DGPU_PRED_CFL && b->kind != DGPU_PRED_PAL) return -1;
-    if (b->kind == DGPU_PRED_CFL && (b->plane == 0 || b->w != t.w || b->h != t.h || t.w != t.h || t.w > 32))
+    if (b->kind == DGPU_PRED_CFL && (b->plane == 0 || b->w != tw || b->h != th || tw != th || tw > 32))
         return -1;   // CfL: one unit per chroma block (cfl_ac + cfl_pred, :1372-1414)
     if (b->kind == DGPU_PRED_CFL ? ((b->mode & 15) >= b->w / 4 || (b->mode >> 4) >= b->h / 4)
                                  : (!inter && b->mode > 13))
@@ -549,11 +481,22 @@ static int check_block(const Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, boo
     return 0;
 }
 
+// appends the block with its data offset (or -1, or -2 - the INTER_WMASK
+// block a COMPOUND_SEG chroma mask reads)
+static int push_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, int32_t aux_off) {
+    if (r->nblocks() >= (size_t)INT32_MAX / 2) return -1;
+    void *q = r->blocks.append(sizeof(*b));
+    int32_t *o = (int32_t *)r->baux_off.append(4);
+    if (!q || !o) return -1;
+    memcpy(q, b, sizeof(*b));
+    *o = aux_off;
+    r->cell_bound += (int64_t)(b->w / tx_w(b->tx)) * (b->h / tx_h(b->tx)) + 1;   // (an inter-intra block adds one)
+    return 0;
+}
+
 extern "C" int dav1d_gpu_rec_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b) {
     if (check_block(r, b, false)) return -1;
-    r->blocks.push_back(*b);
-    r->block_aux.push_back(-1);
-    return 0;
+    return push_block(r, b, -1);
 }
 
 extern "C" int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, const void *aux,
@@ -565,9 +508,7 @@ extern "C" int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlo
     case DGPU_PRED_INTER_MASK:
         if (!aux) {   // a COMPOUND_SEG chroma block: the last INTER_WMASK block's mask
             if (b->plane == 0) return -1;
-            r->blocks.push_back(*b);
-            r->block_aux.push_back(-1);
-            return 0;
+            return push_block(r, b, r->last_wmask >= 0 ? -2 - r->last_wmask : -1);
         }
         need = w * h;
         break;
@@ -582,11 +523,13 @@ extern "C" int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlo
         if ((w & 7) || (h & 7) || (b->x & 7) || (b->y & 7)) return -1;
         need = 16 + (w / 8) * (h / 8) * 8;
         break;
-    case DGPU_PRED_INTER_WMASK:
+    case DGPU_PRED_INTER_WMASK: {
         if (b->plane != 0 || b->weight > 1) return -1;
-        r->blocks.push_back(*b);
-        r->block_aux.push_back(-1);
+        const int32_t bi = (int32_t)r->nblocks();
+        if (push_block(r, b, -1)) return -1;
+        r->last_wmask = bi;
         return 0;
+    }
     case DGPU_PRED_INTER_OBMC: {
         if (!aux || aux_bytes < 16) return -1;
         const int32_t n = *(const int32_t *)aux;
@@ -611,9 +554,16 @@ extern "C" int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlo
     default: return -1;
     }
     if (!aux || aux_bytes != need) return -1;
-    r->blocks.push_back(*b);
-    r->block_aux.push_back((int64_t)r->baux.size());
-    r->baux.insert(r->baux.end(), (const uint8_t *)aux, (const uint8_t *)aux + aux_bytes);
+    const size_t o = r->baux.n, pad = (16 - (aux_bytes & 15)) & 15;   // entries 16-byte aligned
+    if (o + aux_bytes + pad > (size_t)INT32_MAX) return -1;
+    uint8_t *q = (uint8_t *)r->baux.append(aux_bytes + pad);
+    if (!q) return -1;
+    memcpy(q, aux, aux_bytes);
+    memset(q + aux_bytes, 0, pad);
+    if (push_block(r, b, (int32_t)o)) {
+        r->baux.n = o;
+        return -1;
+    }
     return 0;
 }
 
@@ -622,35 +572,31 @@ extern "C" int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int
     int pw, ph;
     if (!r || !coef || !plane_dims(r, plane, pw, ph) || tx < 0 || tx >= DGPU_N_RECT_TX_SIZES) return -1;
     if (txtp < 0 || txtp >= DGPU_N_TX_TYPES_PLUS_LL || eob < 0) return -1;
-    const TxDim t = kTx[tx];
     if (x < 0 || y < 0 || x >= pw || y >= ph || (x & 3) || (y & 3)) return -1;   // starts inside the grid
-    const int sw = std::min(t.w, 32), sh = std::min(t.h, 32);
+    const int sw = std::min(tx_w(tx), 32), sh = std::min(tx_h(tx), 32);
     const size_t cb = r->bpc == 8 ? 2 : 4;
-    Residual res{plane, x, y, tx, txtp, 0, 0, r->coefb.size() / cb};
+    if (r->coefb.n / cb + (size_t)sw * sh > (size_t)INT32_MAX || r->nres() >= (size_t)INT32_MAX / 2) return -1;
+    RecRes q{plane, x, y, tx, txtp, 0, 0, (int32_t)(r->coefb.n / cb)};
     auto at = [&](int cx, int cy) -> int32_t {   // the reference's layout: coef[cy + cx * sh]
         return r->bpc == 8 ? ((const int16_t *)coef)[cy + cx * sh] : ((const int32_t *)coef)[cy + cx * sh];
     };
-    auto put = [&](int cx, int cy) {   // appended in the ABI's coefficient type
-        const size_t o = r->coefb.size();
-        r->coefb.resize(o + cb);
-        memcpy(&r->coefb[o], (const uint8_t *)coef + (size_t)(cy + cx * sh) * cb, cb);
-    };
-    if (eob == 0 && txtp == DGPU_DCT_DCT) {   // the DC-only call (src/itx_tmpl.c:53)
-        put(0, 0);
-    } else {   // the stored region: the bounding box of the non-zero coefficients
-        int nzw = 1, nzh = 1;
+    int nzw = 1, nzh = 1;
+    if (!(eob == 0 && txtp == DGPU_DCT_DCT)) {   // the stored region: the bounding box of the non-zero coefficients
         for (int cx = 0; cx < sw; cx++)
             for (int cy = 0; cy < sh; cy++)
                 if (at(cx, cy)) {
                     nzw = std::max(nzw, cx + 1);
                     nzh = std::max(nzh, cy + 1);
                 }
-        res.nzw = nzw;
-        res.nzh = nzh;
-        for (int cx = 0; cx < nzw; cx++)
-            for (int cy = 0; cy < nzh; cy++) put(cx, cy);
-    }
-    r->residuals.push_back(res);
+        q.nzw = nzw;
+        q.nzh = nzh;
+    }   // else the DC-only call (src/itx_tmpl.c:53): one coefficient, nzw = nzh = 0
+    uint8_t *d = (uint8_t *)r->coefb.append((size_t)nzw * nzh * cb);
+    void *qq = r->res.append(sizeof(q));
+    if (!d || !qq) return -1;
+    for (int cx = 0; cx < nzw; cx++)   // appended in the ABI's coefficient type, column by column
+        memcpy(d + (size_t)cx * nzh * cb, (const uint8_t *)coef + (size_t)cx * sh * cb, (size_t)nzh * cb);
+    memcpy(qq, &q, sizeof(q));
     return 0;
 }
 
@@ -663,7 +609,7 @@ static int recorder_poll(Dav1dGpuRecorder *r) {
     r->pending_check = false;
     // the flush copied its error word to page-locked memory before `done`
     if (hipEventSynchronize(r->done) != hipSuccess) return -3;
-    return *(volatile int32_t *)r->flag.p ? -6 : 0;
+    return *(volatile int32_t *)r->flag ? -6 : 0;
 }
 
 extern "C" int dav1d_gpu_recorder_status(Dav1dGpuRecorder *r) {
@@ -679,14 +625,17 @@ extern "C" int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_un
     return 0;
 }
 
+extern "C" int dav1d_gpu_recorder_prep_ms(const Dav1dGpuRecorder *r, float *ms) {
+    if (!r || !ms) return -1;
+    *ms = r->prep_ms;
+    return 0;
+}
+
 extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane dst[3],
                                         const Dav1dGpuPlane ref[DGPU_MAX_REFS][3], void *stream) {
-    constexpr int NC = DGPU_N_RECT_TX_SIZES;
     if (!r || !dst) return -1;
-    // DAV1D_GPU_REC_HOSTONLY=1 (diagnostics, no device needed): run the host
-    // phases only and drop the recording before the upload
-    static const bool host_only = getenv("DAV1D_GPU_REC_HOSTONLY") != nullptr;
-    if (!host_only) {
+    const bool host = host_only();
+    if (!host) {
         if (hipSetDevice(r->device) != hipSuccess) return -3;
         if (r->done && hipEventSynchronize(r->done) != hipSuccess) return -3;   // buffers free for reuse
     }
@@ -699,6 +648,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     }
     // DAV1D_GPU_REC_TIMING=1: host phase times on stderr (diagnostics)
     static const bool timing = getenv("DAV1D_GPU_REC_TIMING") != nullptr;
+    // DAV1D_GPU_REC_DUMP=<file> (diagnostics): the upload image and the
+    // schedule, appended, to compare builds; nothing is launched on the picture
+    static const char *dump = getenv("DAV1D_GPU_REC_DUMP");
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto t_0 = now();
     auto lap = [&](const char *what) {
@@ -707,747 +659,428 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         fprintf(stderr, "recorder %-8s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_0).count());
         t_0 = t;
     };
+    if (!host && !r->pst) {
+        if (hipStreamCreateWithFlags(&r->pst, hipStreamNonBlocking) != hipSuccess) return -3;
+        if (hipEventCreateWithFlags(&r->prep, hipEventDisableTiming) != hipSuccess || hipEventCreate(&r->pt0) != hipSuccess ||
+            hipEventCreate(&r->pt1) != hipSuccess)
+            return -3;
+    }
+    Exec X{host, r->pst, &r->d_tmp};
+    // once a step may be queued, a failure drains the recorder's stream
+    // before returning: a retry regrows buffers the queued steps still use
+    auto fail = [&](int rc) {
+        if (!host && r->pst) (void)hipStreamSynchronize(r->pst);
+        return rc;
+    };
     const int bpp = r->bpc / 8;
-    int pw[3], ph[3];
-    for (int p = 0; p < 3; p++) plane_dims(r, p, pw[p], ph[p]);
-
-    // per-4x4 maps over the grid plus the overhang transform blocks can reach
-    int mw[3], mh[3];
+    const size_t cb = r->bpc == 8 ? 2 : 4;
+    int pw[3], ph[3], mw[3], mh[3];
     for (int p = 0; p < 3; p++) {
-        mw[p] = pw[p] / 4 + kMapPad4;
+        plane_dims(r, p, pw[p], ph[p]);
+        mw[p] = pw[p] / 4 + kMapPad4;   // per-4x4 maps over the grid plus the overhang transform blocks reach
         mh[p] = ph[p] / 4 + kMapPad4;
     }
+    const int nb = (int)r->nblocks(), nres = (int)r->nres();
     // the maps, kept across flushes; cleared only when their size changes or
     // the stamps would overflow
-    size_t ncells = 0;   // an upper bound of this flush's cells (an inter-intra block adds one)
-    for (const Dav1dGpuRecBlock &b : r->blocks) ncells += (size_t)(b.w / kTx[b.tx].w) * (b.h / kTx[b.tx].h) + 1;
-    {
-        bool reset = (int64_t)r->res_base + (int64_t)r->residuals.size() >= INT32_MAX ||
-                     (int64_t)r->cell_base + (int64_t)ncells >= INT32_MAX;
-        for (int p = 0; p < 3; p++) reset |= r->map_w4[p] != mw[p] || r->map_h4[p] != mh[p];
-        if (reset) {
-            for (int p = 0; p < 3; p++) {
-                r->res_at[p].assign((size_t)mw[p] * mh[p], -1);
-                r->own[p].assign((size_t)mw[p] * mh[p], -1);
-                r->map_w4[p] = mw[p];
-                r->map_h4[p] = mh[p];
-            }
-            r->res_base = r->cell_base = 0;
+    bool reset = (int64_t)r->res_base + nres >= INT32_MAX || (int64_t)r->cell_base + r->cell_bound >= INT32_MAX;
+    for (int p = 0; p < 3; p++) reset |= r->map_w4[p] != mw[p] || r->map_h4[p] != mh[p];
+    if (reset) {
+        size_t tot = 0;
+        for (int p = 0; p < 3; p++) {
+            r->map_off[p] = tot;
+            tot += (size_t)mw[p] * mh[p];
+            r->map_w4[p] = mw[p];
+            r->map_h4[p] = mh[p];
         }
+        if (r->res_at.grow(tot * 4) || r->own.grow(tot * 4)) return -3;
+        X.memset(r->res_at.p, 0xff, tot * 4);
+        X.memset(r->own.p, 0xff, tot * 4);
+        r->res_base = r->cell_base = 0;
     }
     const int32_t res_base = r->res_base, cell_base = r->cell_base;
     // the stamps of this flush, whatever its outcome, are below the next one's
-    r->res_base += (int32_t)r->residuals.size();
-    r->cell_base += (int32_t)ncells;
-    // residual lookup: per plane, the top-left 4x4 cell of each residual
-    std::vector<int32_t> *res_at = r->res_at;
-    for (size_t i = 0; i < r->residuals.size(); i++) {
-        const Residual &q = r->residuals[i];
-        res_at[q.plane][(size_t)(q.y / 4) * mw[q.plane] + q.x / 4] = res_base + (int32_t)i;
+    r->res_base += nres;
+    r->cell_base += (int32_t)r->cell_bound;
+    int32_t *res_at[3], *own[3];
+    for (int p = 0; p < 3; p++) {
+        res_at[p] = r->res_at.as<int32_t>() + r->map_off[p];
+        own[p] = r->own.as<int32_t>() + r->map_off[p];
     }
 
-    // 1-3. transform units in decode order, their edge records and levels.
-    //    The blocks are cut into cells by up to 8 threads, each over a run of
-    //    blocks into its own part (cells, aux pool, emu jobs, launch-ahead
-    //    units, with part-local offsets); the parts are then joined in
-    //    decode order, their offsets rebased (which gives exactly the
-    //    sequential layout), and one sequential pass assigns the levels and
-    //    producers, which follow decode order.
-    std::vector<Unit> &cells = r->cells;
-    lap("maps");
-    std::vector<int32_t> &prod_start = r->prod_start, &prod = r->prod;
-    std::vector<uint8_t> &auxp = r->auxp;
-    std::vector<Dav1dGpuUnit> &xunits = r->xunits;
-    std::vector<int32_t> &xaux = r->xaux;
-    // superblock height log2 per plane (4:2:0), and the TOP_SB_EDGE flag of an
-    // edge record whose top row is a superblock's top (per transform block,
-    // recon_tmpl.c:1276 / :1395; inter-intra per block, :1665 / :1794)
-    const int sbl[3] = {r->sb_log2, r->sb_log2 - 1, r->sb_log2 - 1};
-    auto top_sb = [&](int p, int y, bool ht) {
-        return r->top_on && ht && (y & ((1 << sbl[p]) - 1)) == 0 ? DGPU_IE_TOP_SB_EDGE : 0;
-    };
-    auto build = [&](size_t bi, CellPart &P) -> int {
-        const Dav1dGpuRecBlock &b = r->blocks[bi];
-        const TxDim t = kTx[b.tx];
-        const int p = b.plane, w4p = mw[p];
-        // the part of the block the decoder iterates: w4 / h4 clipped to the
-        // grid (recon_tmpl.c:1208); transform blocks start inside it
-        const bool inter = is_mc_kind(b.kind);
-        const bool cfl = b.kind == DGPU_PRED_CFL, pal = b.kind == DGPU_PRED_PAL;
-        const bool pre = is_prelaunch_kind(b.kind);
-        const uint8_t *bdata = r->block_aux[bi] >= 0 ? &r->baux[(size_t)r->block_aux[bi]] : nullptr;
-        const int bw4 = b.w / 4, bh4 = b.h / 4, tw4 = t.w / 4, th4 = t.h / 4;
-        const int bwc = std::min(b.w, pw[p] - b.x), bhc = std::min(b.h, ph[p] - b.y);
-        const int bw4c = bwc / 4, bh4c = bhc / 4;
-        const int ds_px = (int)(dst[p].stride / bpp);
-        // every reference an inter block reads must be given
-        if (inter || pre) {
-            const int nref = b.kind == DGPU_PRED_INTER || b.kind == DGPU_PRED_WARP || b.kind == DGPU_PRED_INTER_OBMC ? 1
-                             : b.kind == DGPU_PRED_INTER_SCALED ? *(const int32_t *)bdata : 2;
-            for (int k = 0; k < nref; k++)
-                if (!ref || !ref[b.ref[k]][p].data) return -1;
-        }
-        int32_t mask_base = 0, mask_stride = 0;   // INTER_MASK: the block's mask
-        if (b.kind == DGPU_PRED_INTER_MASK) {
-            if (bdata) {
-                mask_base = P.aux_alloc((size_t)b.w * b.h);
-                memcpy(&P.auxp[mask_base], bdata, (size_t)b.w * b.h);
-                mask_stride = b.w;
-            } else {   // COMPOUND_SEG chroma: the luma block's w_mask output
-                if (P.wm_off < 0 || b.w != P.wm_w || b.h != P.wm_h) return -1;
-                mask_base = P.wm_off;
-                mask_stride = P.wm_w;
-            }
-        }
-        if (pre) {   // prediction units of at most 32 x 32, no residual
-            const int uw = std::min(b.w, 32), uh = std::min(b.h, 32), utx = tx_of(uw, uh);
-            if (utx < 0) return -1;
-            if (b.kind == DGPU_PRED_INTER_WMASK) {   // its seg mask at the 4:2:0 chroma resolution
-                P.wm_w = b.w >> 1;
-                P.wm_h = b.h >> 1;
-                P.wm_off = P.aux_alloc((size_t)P.wm_w * P.wm_h);
-            }
-            // mc()'s emu_edge decision per prediction unit and reference
-            // (src/recon_tmpl.c:986-999): the unit kernel reads a W+7 x H+7
-            // footprint with aligned 16-byte row loads (up to 16 bytes past
-            // it), so a direct read needs all of that inside the reference
-            // picture, else the footprint is read from a clamped copy
-            auto mc_inside = [&](int rr, int ix, int iy) {
-                const int rw = ref[rr][p].w, rh = ref[rr][p].h;
-                return ix - 3 >= 0 && iy - 3 >= 0 && ix + uw + 4 <= rw && iy + uh + 4 <= rh &&
-                       (iy + uh + 4 < rh || (int64_t)(ix + uw + 4) * bpp + 16 <= ref[rr][p].stride);
-            };
-            auto mc_emu = [&](int rr, int ix, int iy) {   // the copy's (0, 0) pixel offset
-                return P.emu_band(ix - 3, iy - 3, uw + 7, uh + 7, rr, p) + 3 * kEmuStride + 3;
-            };
-            for (int oy = 0; oy < bhc; oy += uh)
-                for (int ox = 0; ox < bwc; ox += uw) {
-                    const int ux = b.x + ox, uy = b.y + oy;
-                    uint8_t xf = 0;   // CellPart::F_EMU0 / F_EMU1: src_off[k] is a part-local scratch offset
-                    Dav1dGpuUnit u;
-                    memset(&u, 0, sizeof(u));
-                    u.dst_off = uy * ds_px + ux;
-                    u.tx = (uint8_t)utx;
-                    u.plane = (uint8_t)p;
-                    u.pred = (uint8_t)b.kind;
-                    u.txtp = DGPU_NO_RESIDUAL;
-                    u.bw4 = (uint8_t)bw4;
-                    u.bh4 = (uint8_t)bh4;
-                    for (int k = 0; k < 2; k++) {
-                        const int rr = b.ref[k];
-                        const int rs = ref && ref[rr][p].data ? (int)(ref[rr][p].stride / bpp) : 0;
-                        u.p.inter.src_off[k] = (uy + (b.mvy[k] >> 4)) * rs + ux + (b.mvx[k] >> 4);
-                        u.p.inter.mx[k] = (uint8_t)(b.mvx[k] & 15);
-                        u.p.inter.my[k] = (uint8_t)(b.mvy[k] & 15);
-                        u.p.inter.ref[k] = (uint8_t)rr;
-                    }
-                    u.p.inter.filter2d = b.filter2d;
-                    u.p.inter.weight = b.weight;
-                    // WMASK: both refs' footprints; OBMC: the block's own put
-                    const int nmc = b.kind == DGPU_PRED_INTER_WMASK ? 2 : b.kind == DGPU_PRED_INTER_OBMC ? 1 : 0;
-                    for (int k = 0; k < nmc; k++) {
-                        const int rr = b.ref[k], ix = ux + (b.mvx[k] >> 4), iy = uy + (b.mvy[k] >> 4);
-                        if (!mc_inside(rr, ix, iy)) {
-                            u.p.inter.src_off[k] = mc_emu(rr, ix, iy);
-                            u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
-                            xf |= k ? CellPart::F_EMU1 : CellPart::F_EMU0;
-                        }
-                    }
-                    int32_t ao = 0;
-                    if (b.kind == DGPU_PRED_INTER_WMASK) {
-                        ao = P.wm_off + (oy >> 1) * P.wm_w + (ox >> 1);
-                    } else if (b.kind == DGPU_PRED_WARP) {   // abcd, then the unit's 8x8s
-                        const int gw = b.w / 8, nx = uw / 8, ny = uh / 8;
-                        ao = P.aux_alloc(16 + 8 * (size_t)nx * ny);
-                        memcpy(&P.auxp[ao], bdata, 8);
-                        for (int sy = 0; sy < ny; sy++)
-                            memcpy(&P.auxp[ao + 16 + 8 * sy * nx], bdata + 16 + 8 * ((oy / 8 + sy) * gw + ox / 8), 8 * nx);
-                        // warp_affine's emu_edge (src/recon_tmpl.c:1168-1177): an
-                        // 8x8 reads 15 x 15 pixels at (x - 3, y - 3); the kernel's
-                        // aligned loads reach 16 bytes past column x + 11.  When
-                        // any 8x8 of the unit leaves the picture, every 8x8 of it
-                        // is read from a clamped copy (exact for the ones inside):
-                        // 15-row strips, 8x8s 16 px apart, positions rewritten to
-                        // the copy and the strip base in src_off[0] (the kernel
-                        // adds it); otherwise src_off[0] = 0
-                        const int rr = b.ref[0], rw = ref[rr][p].w, rh = ref[rr][p].h;
-                        bool all_in = true;
-                        for (int i = 0; i < nx * ny && all_in; i++) {
-                            int16_t xy[2];
-                            memcpy(xy, &P.auxp[ao + 16 + 8 * i], 4);
-                            all_in = xy[0] - 3 >= 0 && xy[1] - 3 >= 0 && xy[0] + 12 <= rw && xy[1] + 12 <= rh &&
-                                     (xy[1] + 12 < rh || (int64_t)(xy[0] + 12) * bpp + 16 <= ref[rr][p].stride);
-                        }
-                        u.p.inter.src_off[0] = 0;
-                        if (!all_in) {
-                            const int32_t band = P.emu_rows * kEmuStride;
-                            for (int sy = 0; sy < ny; sy++)
-                                for (int sx = 0; sx < nx; sx++) {
-                                    uint8_t *e8 = &P.auxp[ao + 16 + 8 * (sy * nx + sx)];
-                                    int16_t xy[2];
-                                    memcpy(xy, e8, 4);
-                                    P.emu.push_back(EmuJob{xy[0] - 3, xy[1] - 3, band + 15 * sy * kEmuStride + 16 * sx, 15, 15,
-                                                           (uint8_t)rr, (uint8_t)p});
-                                    const int16_t nxy[2] = {(int16_t)(16 * sx + 3), (int16_t)(15 * sy + 3)};
-                                    memcpy(e8, nxy, 4);
-                                }
-                            P.emu_rows += 15 * ny;
-                            u.p.inter.src_off[0] = band;
-                            u.p.inter.ref[0] = (uint8_t)DGPU_REC_EMU_SLOT;
-                            xf |= CellPart::F_EMU0;
-                        }
-                    } else if (b.kind == DGPU_PRED_INTER_OBMC) {   // the laps overlapping the unit
-                        const int n = *(const int32_t *)bdata;
-                        const ObmcBlockLap *lb = (const ObmcBlockLap *)(bdata + 16);
-                        std::vector<ObmcUnitLap> ents;
-                        std::vector<int> emu_ents;   // laps read through the scratch (the lap's
-                                                     // prediction reads the unit's whole footprint)
-                        for (int k = 0; k < n; k++) {
-                            const ObmcBlockLap &e = lb[k];
-                            const int x0 = std::max((int)e.x0 - ox, 0), x1 = std::min((int)e.x1 - ox, uw);
-                            const int y0 = std::max((int)e.y0 - oy, 0), y1 = std::min((int)e.y1 - oy, uh);
-                            if (x0 >= x1 || y0 >= y1) continue;
-                            if (e.ref >= DGPU_REC_EMU_SLOT || !ref || !ref[e.ref][p].data || e.filter2d > 9) return -1;
-                            const int rs = (int)(ref[e.ref][p].stride / bpp);
-                            ObmcUnitLap q;
-                            q.src_off = (uy + (e.mvy >> 4)) * rs + ux + (e.mvx >> 4);
-                            q.mx = (uint8_t)(e.mvx & 15);
-                            q.my = (uint8_t)(e.mvy & 15);
-                            q.filter2d = e.filter2d;
-                            q.ref = e.ref;
-                            q.x0 = (uint8_t)x0, q.y0 = (uint8_t)y0, q.x1 = (uint8_t)x1, q.y1 = (uint8_t)y1;
-                            q.lap_w4 = e.lap_w4, q.lap_h4 = e.lap_h4, q.dir = e.dir;
-                            q.mask_off = (uint8_t)(e.mask_off + (e.dir ? ox : oy));
-                            const int ix = ux + (e.mvx >> 4), iy = uy + (e.mvy >> 4);
-                            if (!mc_inside(e.ref, ix, iy)) {
-                                q.src_off = mc_emu(e.ref, ix, iy);
-                                q.ref = (uint8_t)DGPU_REC_EMU_SLOT;
-                                emu_ents.push_back((int)ents.size());
-                            }
-                            ents.push_back(q);
-                        }
-                        ao = P.aux_alloc(16 + 16 * ents.size());
-                        const int32_t ne = (int32_t)ents.size();
-                        memset(&P.auxp[ao], 0, 16);
-                        memcpy(&P.auxp[ao], &ne, 4);
-                        if (ne) memcpy(&P.auxp[ao + 16], ents.data(), 16 * ents.size());
-                        for (const int k : emu_ents) P.emu_auxfix.push_back(ao + 16 + 16 * k);   // (src_off first)
-                    } else {   // INTER_SCALED: the unit's integer position and phase (running sums)
-                        const int n = *(const int32_t *)bdata;
-                        const ScaledBlockRef *sb = (const ScaledBlockRef *)(bdata + 16);
-                        ao = P.aux_alloc(16 + 16 * (size_t)n);
-                        memset(&P.auxp[ao], 0, 16 + 16 * (size_t)n);
-                        memcpy(&P.auxp[ao], &n, 4);
-                        for (int k = 0; k < n; k++) {
-                            const int rr = b.ref[k];
-                            const int rs = (int)(ref[rr][p].stride / bpp);
-                            const int px_ = sb[k].mx + ox * sb[k].dx, py_ = sb[k].my + oy * sb[k].dy;
-                            const int ix = sb[k].x + (px_ >> 10), iy = sb[k].y + (py_ >> 10);
-                            ScaledUnitRef q;
-                            q.src_off = iy * rs + ix;
-                            q.mx = (uint16_t)(px_ & 1023), q.my = (uint16_t)(py_ & 1023);
-                            q.dx = sb[k].dx, q.dy = sb[k].dy;
-                            q.pad_ = 0;
-                            // the scaled mc()'s emu_edge (src/recon_tmpl.c:1036-1046): the
-                            // kernel reads columns ix - 3 .. ((mx + (W - 1) dx) >> 10) + 4
-                            // past ix and rows iy - 3 .. ((my + (H - 1) dy) >> 10) + 4 past iy
-                            // (its row count capped at 2H + 8), pixel by pixel
-                            const int fw = ((q.mx + (uw - 1) * q.dx) >> 10) + 8;
-                            const int fh = std::min(((q.my + (uh - 1) * q.dy) >> 10) + 8, 2 * uh + 8);
-                            if (ix - 3 < 0 || iy - 3 < 0 || ix - 3 + fw > ref[rr][p].w || iy - 3 + fh > ref[rr][p].h) {
-                                q.src_off = P.emu_band(ix - 3, iy - 3, fw, fh, rr, p) + 3 * kEmuStride + 3;
-                                u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
-                                P.emu_auxfix.push_back(ao + 16 + 16 * k);
-                            }
-                            memcpy(&P.auxp[ao + 16 + 16 * k], &q, 16);
-                        }
-                        if (n == 1) u.p.inter.weight = 0;
-                    }
-                    P.xunits.push_back(u);
-                    P.xaux.push_back(ao);
-                    P.xfix.push_back(xf);
-                }
-        }
-        // the transform cells; an INTER_INTRA block first gets one cell for
-        // the whole block's prediction (recon_b_inter predicts the block,
-        // :1540-1580, then adds the residuals), its transform cells become
-        // residual-only cells that read it
-        const bool iib = b.kind == DGPU_PRED_INTER_INTRA;
-        const int ncx = (bwc + t.w - 1) / t.w, ncy = (bhc + t.h - 1) / t.h;
-        const int32_t iic_at = (int32_t)P.cells.size();   // the inter-intra block's prediction cell
-        for (int k = iib ? -1 : 0; k < ncx * ncy; k++)
-            {
-                const bool iic = k < 0;
-                const int ox = iic ? 0 : (k % ncx) * t.w, oy = iic ? 0 : (k / ncx) * t.h;
-                const int ctw = iic ? b.w : t.w, cth = iic ? b.h : t.h, ctw4 = ctw / 4, cth4 = cth / 4;
-                P.cells.emplace_back();   // built in place (popped again when skipped)
-                Unit &c = P.cells.back();
-                memset(&c, 0, sizeof(c));
-                uint8_t fix = 0;   // the part-local offsets this cell holds (CellPart::F_*)
-                const int ux = b.x + ox, uy = b.y + oy, x4 = ux / 4, y4 = uy / 4;
-                Dav1dGpuUnit &u = c.u;
-                u.dst_off = uy * ds_px + ux;
-                u.tx = (uint8_t)(iic ? tx_of(b.w, b.h) : b.tx);
-                u.plane = (uint8_t)p;
-                u.pred = (uint8_t)((pre || (iib && !iic)) ? DGPU_PRED_NONE : b.kind);
-                u.txtp = DGPU_NO_RESIDUAL;
-                const int32_t rs_ = iic ? -1 : res_at[p][(size_t)y4 * w4p + x4];
-                const int ri = rs_ >= res_base ? rs_ - res_base : -1;   // (an earlier flush's: none)
-                if (ri >= 0 && r->residuals[ri].tx == b.tx) {
-                    const Residual &q = r->residuals[ri];
-                    u.txtp = (uint8_t)q.txtp;
-                    u.nzw = (uint8_t)q.nzw;
-                    u.nzh = (uint8_t)q.nzh;
-                    u.coef_off = (int32_t)q.coef;   // pool offset fixed below
-                    P.n_res_used++;
-                } else if (ri >= 0) {
-                    return -1;   // a residual whose size differs from its block's transforms
-                } else if (pre || (iib && !iic)) {
-                    P.cells.pop_back();
-                    continue;   // predicted elsewhere, nothing to add
-                }
-                Dav1dGpuIntraEdge &e = c.rec;
-                e.unit = -1;
-                e.x4 = (int16_t)x4;
-                e.y4 = (int16_t)y4;
-                e.w4 = (int16_t)(b.tile_x1 / 4);
-                e.h4 = (int16_t)(b.tile_y1 / 4);
-                int nd = 0;
-                bool hl = ux > b.tile_x0, ht = uy > b.tile_y0;
-                if (pre || (iib && !iic)) {   // PRED_NONE: the residual onto the prediction
-                    c.sortmode = 0;
-                } else if (pal) {   // pal_pred: palette, then the unit's rows of the index map
-                    const int bw2 = b.w / 2;
-                    c.aux = P.aux_alloc(16 + (size_t)(t.w / 2) * t.h);
-                    fix |= CellPart::F_AUX;
-                    memset(&P.auxp[c.aux], 0, 16);
-                    memcpy(&P.auxp[c.aux], bdata, 8 * (size_t)bpp);
-                    for (int yy = 0; yy < t.h; yy++)
-                        memcpy(&P.auxp[c.aux + 16 + yy * (t.w / 2)], bdata + 8 * bpp + (size_t)(oy + yy) * bw2 + ox / 2,
-                               t.w / 2);
-                    c.sortmode = 15;
-                } else if (inter || iic) {
-                    u.bw4 = (uint8_t)bw4;
-                    u.bh4 = (uint8_t)bh4;
-                    for (int k = 0; k < 2; k++) {
-                        const int rr = b.ref[k];
-                        // every reference an inter block reads must be given
-                        const bool used = k == 0 || (b.kind != DGPU_PRED_INTER && !iic);
-                        if (used && (!ref || !ref[rr][p].data)) return -1;
-                        const int rs = ref ? (int)(ref[rr][p].stride / bpp) : 0;
-                        const int ix = ux + (b.mvx[k] >> 4), iy = uy + (b.mvy[k] >> 4);
-                        u.p.inter.src_off[k] = iy * rs + ix;
-                        u.p.inter.mx[k] = (uint8_t)(b.mvx[k] & 15);
-                        u.p.inter.my[k] = (uint8_t)(b.mvy[k] & 15);
-                        u.p.inter.ref[k] = (uint8_t)rr;
-                        if (used) {
-                            // the unit kernel reads the footprint with both
-                            // 8-tap margins whatever the fraction, and its
-                            // aligned row loads may run up to 16 bytes past
-                            // the last pixel: direct only when all of that
-                            // stays inside the picture, else a clamped copy
-                            const int rw = ref[rr][p].w, rh = ref[rr][p].h;
-                            const bool inside = ix - 3 >= 0 && iy - 3 >= 0 && ix + ctw + 4 <= rw &&
-                                                iy + cth + 4 <= rh && (iy + cth + 4 < rh || (ix + ctw + 4) * bpp + 16 <= rs * bpp);
-                            if (!inside) {
-                                u.p.inter.src_off[k] = P.emu_band(ix - 3, iy - 3, ctw + 7, cth + 7, rr, p) + 3 * kEmuStride + 3;
-                                fix |= k ? CellPart::F_EMU1 : CellPart::F_EMU0;
-                                u.p.inter.ref[k] = (uint8_t)DGPU_REC_EMU_SLOT;
-                            }
-                        }
-                    }
-                    u.p.inter.filter2d = b.filter2d;
-                    u.p.inter.weight = b.kind == DGPU_PRED_INTER_WAVG ? b.weight : 0;
-                    if (b.kind == DGPU_PRED_INTER_MASK) {
-                        c.aux = mask_base + oy * mask_stride + ox;
-                        fix |= CellPart::F_AUX;
-                    }
-                    c.sortmode = b.filter2d;
-                    if (iic) {   // the intra half: edges gathered by the wavefront like an INTRA unit's
-                        // record: edge_off (unused when gathered), mode, angle, then the mask offset
-                        c.aux = P.aux_alloc(16 + (size_t)b.w * b.h);
-                        fix |= CellPart::F_AUX | CellPart::F_IIREC;
-                        const int32_t moff = c.aux + 16, zero = 0;
-                        memset(&P.auxp[c.aux], 0, 16);
-                        memcpy(&P.auxp[c.aux], &zero, 4);
-                        P.auxp[c.aux + 4] = b.mode;
-                        memcpy(&P.auxp[c.aux + 8], &moff, 4);
-                        memcpy(&P.auxp[moff], bdata, (size_t)b.w * b.h);
-                        // prepare_intra_edges with no edge flags, no edge filter, angle 0 (:1551-1566)
-                        e.mode = b.mode;
-                        e.angle = 0;
-                        e.flags = (uint8_t)((hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0) | top_sb(p, uy, ht));
-                        const int m = remap_mode(e.mode, 0, hl, ht);
-                        nd = kNeeds[m];
-                        c.sortmode = 16 + m;
-                    }
-                } else {
-                    int fl = (hl ? DGPU_IE_HAVE_LEFT : 0) | (ht ? DGPU_IE_HAVE_TOP : 0) | top_sb(p, uy, ht);
-                    if (!cfl) {   // recon_tmpl.c:1252-1266 (blocks up to 64 wide: one 64x64 step)
-                        const int x = ox / 4, y = oy / 4;
-                        const bool sb_tr = b.flags & DGPU_IE_TOP_HAS_RIGHT, sb_bl = b.flags & DGPU_IE_LEFT_HAS_BOTTOM;
-                        if (!((y > 0 || !sb_tr) && x + tw4 >= bw4c)) fl |= DGPU_IE_TOP_HAS_RIGHT;
-                        if (!(x > 0 || (!sb_bl && y + th4 >= bh4c))) fl |= DGPU_IE_LEFT_HAS_BOTTOM;
-                        fl |= b.flags & (DGPU_IE_FILTER_EDGE | DGPU_IE_SMOOTH);
-                        e.mode = b.mode;
-                        e.angle = b.angle;
-                        u.p.intra.max_w = (uint16_t)(pw[p] - ux);
-                        u.p.intra.max_h = (uint16_t)(ph[p] - uy);
-                    } else {
-                        e.mode = DGPU_DC_PRED;   // cfl_pred's DC source (:1395-1410)
-                        e.angle = 0;
-                        u.p.cfl.alpha = b.cfl_alpha;
-                        u.p.cfl.pad_wh = b.mode;   // cfl_ac's w_pad | h_pad << 4 (:1372-1380)
-                        u.p.cfl.luma_off = (2 * uy) * (int)(dst[0].stride / bpp) + 2 * ux;
-                    }
-                    e.flags = (uint8_t)fl;
-                    u.p.intra.edge_off = (int32_t)(P.edge_px + 2 * t.h);   // CFL: the same field
-                    P.edge_px += 2 * t.h + 2 * t.w + 1;
-                    fix |= CellPart::F_EDGE;
-                    const int m = remap_mode(e.mode, e.angle, hl, ht);
-                    nd = kNeeds[m];
-                    c.sortmode = 16 + m;
-                }
-                // the level pass (below) reads the cell's geometry and edge needs
-                P.jobs.emplace_back();
-                LvJob &j = P.jobs.back();
-                j.x4 = (int16_t)x4;
-                j.y4 = (int16_t)y4;
-                j.W4 = e.w4;
-                j.H4 = e.h4;
-                j.p = (uint8_t)p;
-                j.cw4 = (uint8_t)ctw4;
-                j.ch4 = (uint8_t)cth4;
-                j.nd = (uint8_t)nd;
-                j.fl = (uint8_t)((hl ? LvJob::HL : 0) | (ht ? LvJob::HT : 0) |
-                                 ((e.flags & DGPU_IE_TOP_HAS_RIGHT) ? LvJob::TR : 0) |
-                                 ((e.flags & DGPU_IE_LEFT_HAS_BOTTOM) ? LvJob::BL : 0) | (cfl ? LvJob::CFL : 0) |
-                                 ((iib && !iic) ? LvJob::IIRES : 0) | (iic ? LvJob::IIC : 0));
-                j.fix = fix;
-                j.link = iib && !iic ? iic_at : -1;
-            }
-        return 0;
-    };
-
-    {   // DAV1D_GPU_REC_THREADS (diagnostics): the worker count; default this
-        // recorder's share of the process's CPUs, at most 8, taken from the
-        // live recorders at EACH flush (a pool sized at the first
-        // flush kept 8 workers when the other frame threads' recorders came
-        // later); the pool is rebuilt between flushes when the share changes
-        const int live = std::max(1, g_live_recorders.load(std::memory_order_relaxed));
-        int nthr = std::max(1, std::min(8, rec_cpu_budget() / live));
-        if (const char *e = getenv("DAV1D_GPU_REC_THREADS")) nthr = std::max(1, atoi(e));
-        if (!r->pool || r->pool->size() != nthr) r->pool.reset(new Pool(nthr));
+    // 0. the recording, as recorded
+    if (r->d_blocks.grow(r->blocks.n) || r->d_baux_off.grow(r->baux_off.n) || r->d_baux.grow(r->baux.n) ||
+        r->d_res.grow(r->res.n) || r->d_coef.grow(r->coefb.n) || r->d_hdr.grow(sizeof(Hdr)) ||
+        r->d_cnt.grow((size_t)nb * sizeof(BlockCnt)) || r->d_base.grow((size_t)nb * sizeof(BlockCnt)) ||
+        r->d_auxend.grow((size_t)nb * 4))
+        return fail(-3);
+    if (!host && !r->rb) {
+        if (hipHostMalloc(&r->rb, 1 << 16, 0) != hipSuccess) return fail(-3);
+        r->rb_cap = 1 << 16;
     }
-    const size_t nb = r->blocks.size();
-    const int nt = nb < 4096 ? 1 : r->pool->size();
-    if (r->parts.size() < (size_t)nt) r->parts.resize(nt);
-    std::vector<size_t> bcut(nt + 1, nb);   // part boundaries on luma blocks (a block's chroma stays with it)
-    bcut[0] = 0;
-    for (int t = 1; t < nt; t++) {
-        size_t c = std::max(bcut[t - 1], nb * t / nt);
-        while (c < nb && r->blocks[c].plane != 0) c++;
-        bcut[t] = c;
+    if (!host && hipEventRecord(r->pt0, r->pst) != hipSuccess) return fail(-3);
+    X.upload(r->d_blocks.p, r->blocks.p, r->blocks.n);
+    X.upload(r->d_baux_off.p, r->baux_off.p, r->baux_off.n);
+    X.upload(r->d_baux.p, r->baux.p, r->baux.n);
+    X.upload(r->d_res.p, r->res.p, r->res.n);
+    Hdr *hdr = r->d_hdr.as<Hdr>();
+    X.memset(hdr, 0, sizeof(Hdr));
+    {   // residual lookup: per plane, the top-left 4x4 cell of each residual
+        const RecRes *rs = r->d_res.as<RecRes>();
+        struct { int32_t *m[3]; int32_t w[3]; } ra = {{res_at[0], res_at[1], res_at[2]}, {mw[0], mw[1], mw[2]}};
+        X.each(nres, [=] __host__ __device__(int i) {
+            const RecRes q = rs[i];
+            ra.m[q.plane][(size_t)(q.y / 4) * ra.w[q.plane] + q.x / 4] = res_base + i;
+        });
     }
-    auto run_part = [&](int t) {
-        CellPart &P = r->parts[t];
-        P.clear();
-        P.cells.reserve((size_t)((double)ncells * (bcut[t + 1] - bcut[t]) / std::max<size_t>(nb, 1)) + 64);
-        for (size_t bi = bcut[t]; bi < bcut[t + 1] && !P.err; bi++) P.err = build(bi, P);
-    };
-    r->pool->run(nt, run_part);
+    // 1. the cut: count, scan, totals
+    CutCtx c;
+    memset(&c, 0, sizeof(c));
+    c.blocks = r->d_blocks.as<Dav1dGpuRecBlock>();
+    c.baux_off = r->d_baux_off.as<int32_t>();
+    c.baux = r->d_baux.as<uint8_t>();
+    c.res = r->d_res.as<RecRes>();
+    for (int p = 0; p < 3; p++) {
+        c.res_at[p] = res_at[p];
+        c.mw[p] = mw[p];
+        c.pw[p] = pw[p];
+        c.ph[p] = ph[p];
+        c.ds_px[p] = (int32_t)(dst[p].stride / bpp);
+        c.sbl[p] = p ? r->sb_log2 - 1 : r->sb_log2;
+        for (int k = 0; k < DGPU_MAX_REFS; k++) {
+            RefInfo &ri = c.ref[k][p];
+            if (!ref) continue;
+            ri.stride_b = ref[k][p].stride;
+            ri.stride_px = (int32_t)(ref[k][p].stride / bpp);
+            ri.w = ref[k][p].w;
+            ri.h = ref[k][p].h;
+            ri.ok = ref[k][p].data != nullptr;
+        }
+    }
+    c.res_base = res_base;
+    c.bpp = bpp;
+    c.top_on = r->top_on;
+    c.hdr = hdr;
+    c.cnt = r->d_cnt.as<BlockCnt>();
+    c.auxend = r->d_auxend.as<int32_t>();
+    c.base = r->d_base.as<BlockCnt>();
+    X.each(1, [=] __host__ __device__(int) { hdr->last_aux = -1; });
+    X.each(nb, [=] __host__ __device__(int i) {
+        const int e = cut_block<false>(c, i);
+        if (e) aor(&hdr->err, e);
+    });
+    X.scan_blocks(c.cnt, r->d_base.as<BlockCnt>(), nb);
+    {
+        const BlockCnt *cnt = c.cnt, *base = c.base;
+        const int32_t *auxend = c.auxend;
+        X.each(1, [=] __host__ __device__(int) {
+            if (nb) hdr->tot = BlockCntSum()(base[nb - 1], cnt[nb - 1]);
+            hdr->aux_end = hdr->last_aux >= 0 ? base[hdr->last_aux].v[C_AUX] + auxend[hdr->last_aux] : 0;
+        });
+    }
+    Hdr h1;
+    {
+        Hdr *hh = host ? hdr : (Hdr *)r->rb;
+        X.fetch(hh, hdr, sizeof(Hdr));
+        X.sync();
+        if (X.err) return fail(X.err);
+        h1 = *hh;
+    }
     lap("cut");
-    // join: part bases (the aux pool keeps its 16-byte alignment rule)
-    size_t n_cells = 0, n_x = 0, n_emu = 0, aux_end = 0, n_res_used = 0;
-    std::vector<size_t> cb0(nt), xb0(nt), eb0(nt), ab0(nt), pb0(nt);
-    std::vector<int32_t> erow0(nt);
-    int64_t emu_rows64 = 0;
-    size_t edge_px = 0;
-    for (int t = 0; t < nt; t++) {
-        const CellPart &P = r->parts[t];
-        if (P.err) return P.err;
-        cb0[t] = n_cells;
-        xb0[t] = n_x;
-        eb0[t] = n_emu;
-        erow0[t] = (int32_t)std::min<int64_t>(emu_rows64, INT32_MAX);
-        pb0[t] = edge_px;
-        ab0[t] = P.auxp.empty() ? aux_end : (aux_end + 15) & ~(size_t)15;
-        if (!P.auxp.empty()) aux_end = ab0[t] + P.auxp.size();
-        n_cells += P.cells.size();
-        n_x += P.xunits.size();
-        n_emu += P.emu.size();
-        emu_rows64 += P.emu_rows;
-        edge_px += P.edge_px;
-        n_res_used += P.n_res_used;
-    }
+    if (h1.err) return fail(-1);
+    if (h1.tot.v[C_RES] != nres) return fail(-1);   // a residual outside every block
     // every emulated-edge offset (a job's o0, a unit's src_off into the
     // scratch, the kernels' row * kEmuStride) is int32 pixels: a flush whose
     // scratch would pass 2^31 pixels fails instead of wrapping (a hostile
     // stream of all-compound, all-outside cells reaches that below the 2^21
-    // cell limit).  The cut's part-local offsets may have wrapped
-    // already; none of them is used past this point
-    if ((emu_rows64 + 1) * kEmuStride + 256 > (int64_t)INT32_MAX) return -1;
-    const int32_t emu_rows = (int32_t)emu_rows64;
-    if (n_res_used != r->residuals.size()) return -1;   // a residual outside every block
-    cells.resize(n_cells);
-    r->jobs.resize(n_cells);
-    auxp.resize(aux_end);
-    r->emu.resize(n_emu);
-    xunits.resize(n_x);
-    xaux.resize(n_x);
-    auto join_part = [&](int t) {
-        const CellPart &P = r->parts[t];
-        const int32_t ab = (int32_t)ab0[t], er = erow0[t], pb = (int32_t)pb0[t];
-        if (!P.auxp.empty()) memcpy(&auxp[ab0[t]], P.auxp.data(), P.auxp.size());
-        for (size_t i = 0; i < P.cells.size(); i++) {
-            Unit c = P.cells[i];
-            const uint8_t f = P.jobs[i].fix;
-            if (f & CellPart::F_AUX) c.aux += ab;
-            if (f & CellPart::F_EDGE) c.u.p.intra.edge_off += pb;
-            if (f & CellPart::F_EMU0) c.u.p.inter.src_off[0] += er * kEmuStride;
-            if (f & CellPart::F_EMU1) c.u.p.inter.src_off[1] += er * kEmuStride;
-            if (f & CellPart::F_IIREC) {   // the inter-intra record's mask offset
-                int32_t mo;
-                memcpy(&mo, &auxp[(size_t)c.aux + 8], 4);
-                mo += ab;
-                memcpy(&auxp[(size_t)c.aux + 8], &mo, 4);
-            }
-            cells[cb0[t] + i] = c;
-            LvJob j = P.jobs[i];
-            if (j.link >= 0) j.link += (int32_t)cb0[t];
-            r->jobs[cb0[t] + i] = j;
-        }
-        for (size_t i = 0; i < P.emu.size(); i++) {
-            EmuJob e = P.emu[i];
-            e.o0 += er * kEmuStride;
-            r->emu[eb0[t] + i] = e;
-        }
-        for (size_t i = 0; i < P.xunits.size(); i++) {
-            Dav1dGpuUnit u = P.xunits[i];
-            if (P.xfix[i] & CellPart::F_EMU0) u.p.inter.src_off[0] += er * kEmuStride;
-            if (P.xfix[i] & CellPart::F_EMU1) u.p.inter.src_off[1] += er * kEmuStride;
-            xunits[xb0[t] + i] = u;
-            xaux[xb0[t] + i] = P.xaux[i] + ab;
-        }
-        for (const int32_t o : P.emu_auxfix) {   // OBMC laps / scaled refs read through the scratch
-            int32_t v;
-            memcpy(&v, &auxp[(size_t)ab + o], 4);
-            v += er * kEmuStride;
-            memcpy(&auxp[(size_t)ab + o], &v, 4);
-        }
-    };
-    r->pool->run(nt, join_part);
-    lap("join");
-    // levels and producers: a cell sits one level above every pixel its
-    // edges (or CfL luma, or an inter-intra residual's prediction) read; its
-    // producers are the cells that wrote them.  A pixel no cell of this flush
-    // wrote came from an earlier flush on the same stream: no producer, level
-    // 0 for it.  Three steps, the first two on the worker pool:
-    //   1. every cell stamps its 4x4s in the writer map (the only overlap in a
-    //      flush: an inter-intra block's prediction cell under its residual
-    //      cells, which come after it in decode order and win);
-    //   2. every cell looks its producers up (a writer at or after the cell in
-    //      decode order has not written yet: none), sorted, duplicate-free;
-    //   3. the levels in decode order, from the producers' (decode order is a
-    //      topological order).
-    const int nlv = n_cells < 32768 ? 1 : r->pool->size();
-    {
-        auto stamp = [&](size_t ci, bool iic_pass) {
-            const LvJob &j = r->jobs[ci];
-            const bool iic = j.fl & LvJob::IIC;
-            if (iic != iic_pass) return;
-            int32_t *wp = r->own[j.p].data();
-            const int w4p = mw[j.p];
-            const int32_t v = cell_base + (int32_t)ci;
-            for (int cy = j.y4; cy < j.y4 + j.ch4; cy++)
-                for (int cx = j.x4; cx < j.x4 + j.cw4; cx++) {
-                    int32_t &o = wp[(size_t)cy * w4p + cx];
-                    if (!iic_pass || o < cell_base) o = v;   // (under its residual cells: theirs)
-                }
-        };
-        r->pool->run(nlv, [&](int t) {
-            for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) stamp(ci, false);
-        });
-        // the contract (include/dav1d_gpu.h, dav1d_gpu_recorder_flush): the
-        // cells of one flush do not overlap, an inter-intra prediction under
-        // its own residual cells excepted.  Checked after the parallel stamp:
-        // two overlapping cells leave one stamp on a shared 4x4, so the other
-        // finds a stamp not its own whatever order the workers ran in; the
-        // flush then fails instead of scheduling reads before writes
-        // 
-        std::atomic<int> overlap{0};
-        r->pool->run(nlv, [&](int t) {
-            int bad = 0;
-            for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e && !bad; ci++) {
-                const LvJob &j = r->jobs[ci];
-                if (j.fl & LvJob::IIC) continue;
-                const int32_t *wp = r->own[j.p].data();
-                const int w4p = mw[j.p];
-                const int32_t v = cell_base + (int32_t)ci;
-                for (int cy = j.y4; cy < j.y4 + j.ch4 && !bad; cy++)
-                    for (int cx = j.x4; cx < j.x4 + j.cw4; cx++)
-                        if (wp[(size_t)cy * w4p + cx] != v) {
-                            bad = 1;
-                            break;
-                        }
-            }
-            if (bad) overlap.store(1, std::memory_order_relaxed);
-        });
-        if (overlap.load()) return -1;
-        r->pool->run(nlv, [&](int t) {
-            for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) stamp(ci, true);
-        });
-    }
-    lap("stamp");
-    r->prod_cnt.resize(n_cells);
-    if (r->tprod.size() < (size_t)nlv) r->tprod.resize(nlv);
-    r->pool->run(nlv, [&](int t) {
-        std::vector<int32_t> &out = r->tprod[t];
-        out.clear();
-        for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) {
-            const LvJob &j = r->jobs[ci];
-            const int p = j.p, w4p = mw[p], x4 = j.x4, y4 = j.y4, cw4 = j.cw4, ch4 = j.ch4, W4 = j.W4, H4 = j.H4;
-            const int nd = j.nd;
-            const bool hl = j.fl & LvJob::HL, ht = j.fl & LvJob::HT;
-            const int32_t *mp = r->own[p].data();
-            const int32_t lo = cell_base, hi = cell_base + (int32_t)ci;   // this flush, before the cell
-            const size_t p0 = out.size();
-            auto put = [&](int32_t o) {
-                if (o < lo || o >= hi) return;
-                o -= cell_base;
-                if (out.size() == p0 || out.back() != o) out.push_back(o);
-            };
-            auto cell = [&](int cx, int cy) { put(mp[(size_t)cy * w4p + cx]); };
-            if (nd & 1) {
-                if (hl) {
-                    for (int q = y4; q < std::min(y4 + ch4, H4); q++) cell(x4 - 1, q);
-                    if ((nd & 16) && y4 + ch4 < H4 && (j.fl & LvJob::BL))
-                        for (int q = y4 + ch4; q < std::min(y4 + 2 * ch4, H4); q++) cell(x4 - 1, q);
-                } else if (ht) {
-                    cell(x4, y4 - 1);
-                }
-            }
-            if (nd & 2) {
-                if (ht) {
-                    for (int q = x4; q < std::min(x4 + cw4, W4); q++) cell(q, y4 - 1);
-                    if ((nd & 8) && x4 + cw4 < W4 && (j.fl & LvJob::TR))
-                        for (int q = x4 + cw4; q < std::min(x4 + 2 * cw4, W4); q++) cell(q, y4 - 1);
-                } else if (hl) {
-                    cell(x4 - 1, y4);
-                }
-            }
-            if (j.fl & LvJob::IIRES) put(cell_base + j.link);   // the block's inter-intra prediction
-            if (nd & 4) {
-                if (hl && ht) cell(x4 - 1, y4 - 1);
-                else if (hl) cell(x4 - 1, y4);
-                else if (ht) cell(x4, y4 - 1);
-            }
-            if (j.fl & LvJob::CFL) {
-                const int lw4 = mw[0];
-                const int32_t *ml = r->own[0].data();
-                for (int cy = 2 * y4; cy < 2 * (y4 + ch4); cy++)
-                    for (int cx = 2 * x4; cx < 2 * (x4 + cw4); cx++) put(ml[(size_t)cy * lw4 + cx]);
-            }
-            if (out.size() - p0 > 1) {   // sorted, duplicate-free (lists are short: insertion sort)
-                int32_t *q = out.data() + p0;
-                const size_t m = out.size() - p0;
-                size_t u = 1;
-                for (size_t a_ = 1; a_ < m; a_++) {
-                    const int32_t v = q[a_];
-                    size_t b_ = u;
-                    while (b_ > 0 && q[b_ - 1] > v) b_--;
-                    if (b_ > 0 && q[b_ - 1] == v) continue;   // a duplicate
-                    for (size_t c_ = u; c_ > b_; c_--) q[c_] = q[c_ - 1];
-                    q[b_] = v;
-                    u++;
-                }
-                out.resize(p0 + u);
-            }
-            r->prod_cnt[ci] = (int32_t)(out.size() - p0);
-        }
+    // cell limit)
+    if ((h1.tot.v[C_EROWS] + 1) * kEmuStride + 256 > (long long)INT32_MAX) return fail(-1);
+    if (h1.tot.v[C_CELLS] >= (1 << 21) || h1.tot.v[C_RAW] >= INT32_MAX || h1.tot.v[C_EDGE] >= INT32_MAX ||
+        h1.aux_end >= INT32_MAX)
+        return fail(-1);
+    const int n = (int)h1.tot.v[C_CELLS], nx = (int)h1.tot.v[C_XU], n_emu = (int)h1.tot.v[C_EJOBS];
+    const int32_t emu_rows = (int32_t)h1.tot.v[C_EROWS];
+    const size_t edge_px = (size_t)h1.tot.v[C_EDGE], aux_end = (size_t)h1.aux_end;
+    const int64_t n_raw = h1.tot.v[C_RAW];
+    if (r->d_cu.grow((size_t)n * sizeof(Dav1dGpuUnit)) || r->d_crec.grow((size_t)n * sizeof(Dav1dGpuIntraEdge)) ||
+        r->d_caux.grow((size_t)n * 4) || r->d_csort.grow((size_t)n * 4) || r->d_jobs.grow((size_t)n * sizeof(LvJob)) ||
+        r->d_rawc.grow((size_t)(n + 1) * 4) || r->d_raws.grow((size_t)(n + 1) * 4) || r->d_raw.grow((size_t)n_raw * 4) ||
+        r->d_pcnt.grow((size_t)(n + 1) * 4) || r->d_pstart.grow((size_t)(n + 1) * 4) ||
+        r->d_prod.grow((size_t)n_raw * 4) || r->d_lv.grow((size_t)n * 4) || r->d_keys.grow((size_t)n * 8) ||
+        r->d_keys2.grow((size_t)n * 8) || r->d_rank.grow((size_t)n * 4) || r->d_dcnt.grow((size_t)(n + 1) * 4) ||
+        r->d_dstart.grow((size_t)(n + 1) * 4) || r->d_deps.grow((size_t)n_raw * 4) ||
+        r->d_auxp.grow(aux_end) || r->d_emu_jobs.grow((size_t)n_emu * sizeof(EmuJob)) ||
+        r->d_xu0.grow((size_t)nx * sizeof(Dav1dGpuUnit)) || r->d_xa0.grow((size_t)nx * 4) ||
+        r->d_units.grow((size_t)n * sizeof(Dav1dGpuUnit)) || r->d_recs.grow((size_t)n * sizeof(Dav1dGpuIntraEdge)) ||
+        r->d_aux.grow((size_t)n * 4))
+        return fail(-3);
+    // 2. the write pass (the aux pool zero-filled first: its alignment gaps
+    //    and unwritten record bytes are zero)
+    c.cu = r->d_cu.as<Dav1dGpuUnit>();
+    c.crec = r->d_crec.as<Dav1dGpuIntraEdge>();
+    c.caux = r->d_caux.as<int32_t>();
+    c.csort = r->d_csort.as<int32_t>();
+    c.rawc = r->d_rawc.as<int32_t>();
+    c.jobs = r->d_jobs.as<LvJob>();
+    c.auxp = r->d_auxp.as<uint8_t>();
+    c.emu = r->d_emu_jobs.as<EmuJob>();
+    c.xu = r->d_xu0.as<Dav1dGpuUnit>();
+    c.xa = r->d_xa0.as<int32_t>();
+    X.memset(c.auxp, 0, aux_end);
+    X.memset(c.rawc + n, 0, 4);
+    X.upload(r->d_coef.p, r->coefb.p, r->coefb.n);
+    X.each(nb, [=] __host__ __device__(int i) { (void)cut_block<true>(c, i); });
+    // 3. levels and producers: a cell sits one level above every pixel its
+    //    edges (or CfL luma, or an inter-intra residual's prediction) read;
+    //    its producers are the cells that wrote them.  A pixel no cell of this
+    //    flush wrote came from an earlier flush on the same stream: no
+    //    producer, level 0 for it.
+    struct Maps {
+        int32_t *own[3];
+        int32_t w[3];
+    } mp = {{own[0], own[1], own[2]}, {mw[0], mw[1], mw[2]}};
+    const LvJob *jobs = c.jobs;
+    //    every cell stamps its 4x4s in the writer map (the only overlap in a
+    //    flush: an inter-intra block's prediction cell under its residual
+    //    cells, which come after it in decode order and win)
+    X.each(n, [=] __host__ __device__(int ci) {
+        const LvJob j = jobs[ci];
+        if (j.fl & LvJob::IIC) return;
+        int32_t *wp = mp.own[j.p];
+        for (int cy = j.y4; cy < j.y4 + j.ch4; cy++)
+            for (int cx = j.x4; cx < j.x4 + j.cw4; cx++) wp[(size_t)cy * mp.w[j.p] + cx] = cell_base + ci;
     });
-    lap("prods");
-    // the producer lists in decode order (CSR), then the levels
-    prod_start.resize(n_cells + 1);
-    prod_start[0] = 0;
-    for (size_t ci = 0; ci < n_cells; ci++) prod_start[ci + 1] = prod_start[ci] + r->prod_cnt[ci];
-    prod.resize((size_t)prod_start[n_cells]);
-    r->pool->run(nlv, [&](int t) {
-        const size_t c0 = n_cells * t / nlv;
-        if (!r->tprod[t].empty()) memcpy(&prod[(size_t)prod_start[c0]], r->tprod[t].data(), r->tprod[t].size() * 4);
+    // the contract (include/dav1d_gpu.h, dav1d_gpu_recorder_flush): the
+    // cells of one flush do not overlap, an inter-intra prediction under its
+    // own residual cells excepted.  Two overlapping cells leave one stamp on
+    // a shared 4x4, so the other finds a stamp not its own whatever order
+    // they ran in; the flush then fails instead of scheduling reads before
+    // writes
+    X.each(n, [=] __host__ __device__(int ci) {
+        const LvJob j = jobs[ci];
+        if (j.fl & LvJob::IIC) return;
+        const int32_t *wp = mp.own[j.p];
+        for (int cy = j.y4; cy < j.y4 + j.ch4; cy++)
+            for (int cx = j.x4; cx < j.x4 + j.cw4; cx++)
+                if (wp[(size_t)cy * mp.w[j.p] + cx] != cell_base + ci) {
+                    aor(&hdr->err, E_OVERLAP);
+                    return;
+                }
     });
-    {   // (a compact level array: the walk touches 4 bytes per cell)
-        r->lv.resize(n_cells);
-        int32_t *lv = r->lv.data();
-        const int32_t *ps = prod_start.data(), *pp = prod.data();
-        for (size_t ci = 0; ci < n_cells; ci++) {
-            int d = -1;
-            for (int32_t k = ps[ci]; k < ps[ci + 1]; k++) d = std::max(d, lv[pp[k]]);
-            lv[ci] = d + 1;
-        }
-        r->pool->run(nlv, [&](int t) {
-            for (size_t ci = n_cells * t / nlv, e = n_cells * (t + 1) / nlv; ci < e; ci++) cells[ci].level = lv[ci];
+    X.each(n, [=] __host__ __device__(int ci) {
+        const LvJob j = jobs[ci];
+        if (!(j.fl & LvJob::IIC)) return;
+        int32_t *wp = mp.own[j.p];
+        for (int cy = j.y4; cy < j.y4 + j.ch4; cy++)
+            for (int cx = j.x4; cx < j.x4 + j.cw4; cx++) {
+                int32_t &o = wp[(size_t)cy * mp.w[j.p] + cx];
+                if (o < cell_base) o = cell_base + ci;   // (under its residual cells: theirs)
+            }
+    });
+    //    every cell looks its producers up (a writer at or after the cell in
+    //    decode order has not written yet: none), sorted, duplicate-free
+    int32_t *raws = r->d_raws.as<int32_t>(), *raw = r->d_raw.as<int32_t>(), *pcnt = r->d_pcnt.as<int32_t>();
+    int32_t *pstart = r->d_pstart.as<int32_t>(), *prod = r->d_prod.as<int32_t>();
+    X.scan(c.rawc, raws, n + 1);
+    X.memset(pcnt + n, 0, 4);
+    X.each(n, [=] __host__ __device__(int ci) {
+        const LvJob j = jobs[ci];
+        int32_t *seg = raw + raws[ci];
+        int m = 0;
+        const int32_t lo = cell_base, hi = cell_base + ci;   // this flush, before the cell
+        lookups<true>(j, mp.own[j.p], mp.w[j.p], mp.own[0], mp.w[0], [&](int32_t o) {
+            if (o <= -2) {   // the inter-intra prediction cell, by index
+                seg[m++] = -2 - o;
+            } else if (o >= lo && o < hi) {
+                seg[m++] = o - cell_base;
+            }
         });
+        int u = 0;   // sorted, duplicate-free (lists are short: insertion sort in place)
+        for (int a = 0; a < m; a++) {
+            const int32_t v = seg[a];
+            int b = u;
+            while (b > 0 && seg[b - 1] > v) b--;
+            if (b > 0 && seg[b - 1] == v) continue;
+            for (int k = u; k > b; k--) seg[k] = seg[k - 1];
+            seg[b] = v;
+            u++;
+        }
+        pcnt[ci] = u;
+    });
+    X.scan(pcnt, pstart, n + 1);
+    X.each(n, [=] __host__ __device__(int ci) {
+        const int32_t *s = raw + raws[ci];
+        int32_t *d = prod + pstart[ci];
+        for (int k = 0, e = pstart[ci + 1] - pstart[ci]; k < e; k++) d[k] = s[k];
+    });
+    //    the levels in decode order, from the producers' (decode order is a
+    //    topological order), and the sort keys
+    int32_t *lv = r->d_lv.as<int32_t>();
+    uint64_t *keys = r->d_keys.as<uint64_t>(), *keys2 = r->d_keys2.as<uint64_t>();
+    if (n) {
+        LevelArgs la{pstart, prod, c.csort, c.cu, lv, keys, hdr, n, kLevelSpinLimit};
+        if (host) {
+            for (int ci = 0; ci < n; ci++) {
+                int d = -1;
+                for (int k = pstart[ci]; k < pstart[ci + 1]; k++) d = std::max(d, lv[prod[k]]);
+                lv[ci] = d + 1;
+                keys[ci] = level_key(c.cu[ci], c.csort[ci], d + 1, ci);
+                hdr->max_level = std::max(hdr->max_level, d + 1);
+            }
+        } else if (!X.err) {
+            X.memset(lv, 0xff, (size_t)n * 4);
+            k_levels<<<dim3((unsigned)((n + 63) / 64)), 64, 0, r->pst>>>(la);
+            if (hipGetLastError() != hipSuccess) X.err = -3;
+        }
     }
-    lap("levels");
-    const int n = (int)cells.size();
-
     // 4. level order, size classes inside a level, then kind / mode / type:
-    //    one LSD radix sort of (key << 21 | decode index) on the key bits only
-    //    (stable: equal keys stay in decode order).  Key: level | tx (5) |
-    //    pred (4) | mode (6) | type (5, NO_RESIDUAL last)
-    if (n >= (1 << 21)) return -1;
-    const int nthreads = r->pool->size();
-    const int npar = n < 32768 ? 1 : nthreads;   // (the O(n) passes below on the pool)
-    std::vector<uint64_t> &keys = r->keys;
-    keys.resize(n);
-    int max_level = 0;
+    //    one radix sort of the keys (distinct: they hold the decode index)
+    X.sort(keys, keys2, n, 21, 21 + 20 + 16);
+    // the rank of every decode-order cell, and the level / class ranges: a
+    // (level, class) run ends where the sorted key's top bits change (levels
+    // past 2^16 fail the flush below)
+    const int lb = std::min(n, 1 << 16);
+    if (r->d_ends.grow((size_t)lb * (NC + 1) * 4) || r->d_lend.grow((size_t)(lb + 1) * 4)) return fail(-3);
+    int32_t *ends = r->d_ends.as<int32_t>(), *lend = r->d_lend.as<int32_t>(), *rank = r->d_rank.as<int32_t>();
+    int32_t *dcnt = r->d_dcnt.as<int32_t>(), *dstart = r->d_dstart.as<int32_t>(), *deps = r->d_deps.as<int32_t>();
+    X.memset(ends, 0, (size_t)lb * (NC + 1) * 4);
+    X.memset(lend, 0, (size_t)(lb + 1) * 4);
+    X.memset(dcnt + n, 0, 4);
+    X.each(n, [=] __host__ __device__(int i) {
+        const uint64_t k = keys2[i];
+        const int ci = (int)(k & ((1u << 21) - 1));
+        rank[ci] = i;
+        const uint64_t lt = k >> 36;   // level | tx
+        const int level = (int)(lt >> 5), tx = (int)(lt & 31);
+        if (level < lb && (i + 1 == n || (keys2[i + 1] >> 36) != lt)) {   // the last of its (level, class) run
+            ends[(size_t)level * (NC + 1) + tx + 1] = i + 1;
+            if (i + 1 == n || (int)(keys2[i + 1] >> 41) != level) lend[level + 1] = i + 1;
+        }
+        dcnt[i] = pcnt[ci];   // (producer lists in level order)
+    });
+    X.scan(dcnt, dstart, n + 1);
+    // 5. the image: units and records at their ranks, producers as ranks
+    Dav1dGpuUnit *units = r->d_units.as<Dav1dGpuUnit>();
+    Dav1dGpuIntraEdge *recs = r->d_recs.as<Dav1dGpuIntraEdge>();
+    int32_t *aux = r->d_aux.as<int32_t>();
     {
-        std::vector<int> tmax(npar, 0);
-        r->pool->run(npar, [&](int t) {
-            int m = 0;
-            for (int i = (int)((int64_t)n * t / npar), e = (int)((int64_t)n * (t + 1) / npar); i < e; i++) {
-                const Unit &c = cells[i];
-                m = std::max(m, c.level);
-                const uint64_t key = (uint64_t)c.level << 20 | (uint64_t)c.u.tx << 15 | (uint64_t)c.u.pred << 11 |
-                                     (uint64_t)(c.sortmode & 63) << 5 |
-                                     (uint64_t)(c.u.txtp == DGPU_NO_RESIDUAL ? 31 : c.u.txtp);
-                keys[i] = key << 21 | (uint64_t)i;
-            }
-            tmax[t] = m;
+        const Dav1dGpuUnit *cu = c.cu;
+        const Dav1dGpuIntraEdge *crec = c.crec;
+        const int32_t *caux = c.caux;
+        X.each(n, [=] __host__ __device__(int i) {
+            const int ci = (int)(keys2[i] & ((1u << 21) - 1));
+            memcpy(&units[i], &cu[ci], sizeof(Dav1dGpuUnit));   // coef_off / edge_off are decode-order pool offsets
+            aux[i] = caux[ci];
+            Dav1dGpuIntraEdge e;
+            memcpy(&e, &crec[ci], sizeof(e));
+            e.unit = i;
+            memcpy(&recs[i], &e, sizeof(e));
+            int32_t *o = deps + dstart[i];
+            for (int k = pstart[ci]; k < pstart[ci + 1]; k++) *o++ = rank[prod[k]];
         });
-        for (int t = 0; t < npar; t++) max_level = std::max(max_level, tmax[t]);
-        if (max_level >= (1 << 16)) return -1;
     }
+    // 6. the launch-ahead units in class order (a stable sort by size class)
+    //    and, with top_edge, the backup runs of those whose bottom row ends a
+    //    superblock row (decode order; dav1d_backup_ipred_edge, run between
+    //    that launch and the wavefront; a residual on them is added by a
+    //    wavefront unit, which backs its row up again)
+    if (r->d_xk.grow((size_t)nx * 8) || r->d_xk2.grow((size_t)nx * 8) ||
+        r->d_xunits.grow((size_t)nx * sizeof(Dav1dGpuUnit)) || r->d_xaux.grow((size_t)nx * 4) ||
+        r->d_xends.grow((NC + 1) * 4) || r->d_bkf.grow((size_t)(nx + 1) * 4) || r->d_bks.grow((size_t)(nx + 1) * 4) ||
+        r->d_bk.grow((size_t)nx * sizeof(Dav1dGpuEdgeBackup)))
+        return fail(-3);
+    uint64_t *xk = r->d_xk.as<uint64_t>(), *xk2 = r->d_xk2.as<uint64_t>();
+    Dav1dGpuUnit *xunits = r->d_xunits.as<Dav1dGpuUnit>();
+    int32_t *xaux = r->d_xaux.as<int32_t>(), *xends = r->d_xends.as<int32_t>();
+    int32_t *bkf = r->d_bkf.as<int32_t>(), *bks = r->d_bks.as<int32_t>();
+    Dav1dGpuEdgeBackup *bk = r->d_bk.as<Dav1dGpuEdgeBackup>();
     {
-        int lb = 0;
-        while ((1 << lb) <= max_level) lb++;
-        radix_sort(keys, r->keys_tmp, 21, 21 + 20 + lb, *r->pool);
+        const Dav1dGpuUnit *xu0 = c.xu;
+        const int32_t *xa0 = c.xa;
+        X.memset(xends, 0, (NC + 1) * 4);
+        X.each(nx, [=] __host__ __device__(int i) { xk[i] = (uint64_t)xu0[i].tx << 32 | (uint64_t)i; });
+        X.sort(xk, xk2, nx, 32, 37);
+        X.each(nx, [=] __host__ __device__(int k) {
+            const int i = (int)(xk2[k] & 0xffffffffu), tx = (int)(xk2[k] >> 32);
+            memcpy(&xunits[k], &xu0[i], sizeof(Dav1dGpuUnit));
+            xaux[k] = xa0[i];
+            if (k + 1 == nx || (int)(xk2[k + 1] >> 32) != tx) xends[tx + 1] = k + 1;
+        });
+        if (r->top_on && nx) {
+            struct Tops {
+                int32_t ds[3], tw[3], th[3], sbl[3];
+            } tp;
+            for (int p = 0; p < 3; p++) {
+                tp.ds[p] = c.ds_px[p];
+                tp.tw[p] = r->top[p].w;
+                tp.th[p] = r->top[p].h;
+                tp.sbl[p] = c.sbl[p];
+            }
+            auto run = [=] __host__ __device__(const Dav1dGpuUnit &u, Dav1dGpuEdgeBackup &o) -> bool {
+                const int p = u.plane;
+                const int uy = u.dst_off / tp.ds[p], ux = u.dst_off % tp.ds[p], y1 = uy + tx_h(u.tx);
+                const int sby = (y1 >> tp.sbl[p]) - 1, w = min(tx_w(u.tx), tp.tw[p] - ux);
+                o = Dav1dGpuEdgeBackup{p, sby, ux, w};
+                return (y1 & ((1 << tp.sbl[p]) - 1)) == 0 && sby < tp.th[p] && w > 0;
+            };
+            X.memset(bkf + nx, 0, 4);
+            X.each(nx, [=] __host__ __device__(int i) {
+                Dav1dGpuEdgeBackup o;
+                bkf[i] = run(xu0[i], o) ? 1 : 0;
+            });
+            X.scan(bkf, bks, nx + 1);
+            X.each(nx, [=] __host__ __device__(int i) {
+                Dav1dGpuEdgeBackup o;
+                if (run(xu0[i], o)) bk[bks[i]] = o;
+            });
+        }
+        const bool top_on = r->top_on;
+        X.each(1, [=] __host__ __device__(int) {
+            hdr->n_bk = top_on && nx ? bks[nx] : 0;
+            hdr->pad_[0] = dstart[n];   // the producer entries
+        });
     }
-    lap("sort");
-    const int n_levels = n ? max_level + 1 : 0;
+    // 7. read back: the level count, the class ranges, the backup runs
+    Hdr h2;
+    int32_t x_end[NC + 1];
+    {
+        Hdr *hh = host ? hdr : (Hdr *)r->rb;
+        int32_t *xe = host ? xends : (int32_t *)((uint8_t *)r->rb + 256);
+        if (!host && hipEventRecord(r->pt1, r->pst) != hipSuccess) return fail(-3);
+        X.fetch(hh, hdr, sizeof(Hdr));
+        X.fetch(xe, xends, (NC + 1) * 4);
+        X.sync();
+        if (X.err) return fail(X.err);
+        h2 = *hh;
+        if (!host && hipEventElapsedTime(&r->prep_ms, r->pt0, r->pt1) != hipSuccess) r->prep_ms = -1;
+        memcpy(x_end, xe, sizeof(x_end));
+    }
+    if (h2.err & E_STALL) return fail(-3);
+    if (h2.err) return fail(-1);   // overlapping cells
+    const int max_level = n ? h2.max_level : 0;
+    if (max_level >= (1 << 16)) return fail(-1);
+    const int n_levels = n ? max_level + 1 : 0, n_bk = h2.n_bk;
+    const int64_t n_deps = h2.pad_[0];
     r->unit_start.assign(n_levels + 1, 0);
     r->class_start.assign((size_t)n_levels * (NC + 1), 0);
-    const size_t cb = r->bpc == 8 ? 2 : 4;
-    // the rank of every decode-order cell, and the level / class ranges: a
-    // (level, class) run ends where the sorted key's top bits change
-    std::vector<int32_t> &rank = r->rank;
-    rank.resize(n);
-    r->dep_start.assign((size_t)n + 1, 0);
-    r->pool->run(npar, [&](int t) {
-        for (int i = (int)((int64_t)n * t / npar), e = (int)((int64_t)n * (t + 1) / npar); i < e; i++) {
-            const uint64_t k = keys[i];
-            const int ci = (int)(k & ((1u << 21) - 1));
-            rank[ci] = i;
-            const uint64_t lt = k >> 36;   // level | tx
-            if (i + 1 == n || (keys[i + 1] >> 36) != lt) {   // the last of its (level, class) run
-                const int level = (int)(lt >> 5), tx = (int)(lt & 31);
-                r->class_start[(size_t)level * (NC + 1) + tx + 1] = i + 1;   // an end, made a count below
-                if (i + 1 == n || (int)(keys[i + 1] >> 41) != level) r->unit_start[level + 1] = i + 1;
-            }
-            r->dep_start[i + 1] = prod_start[ci + 1] - prod_start[ci];   // (producer lists in level order)
+    if (n_levels) {
+        const size_t ce = (size_t)n_levels * (NC + 1) * 4, le = (size_t)(n_levels + 1) * 4;
+        if (!host && ce + le > r->rb_cap) {
+            (void)hipHostFree(r->rb);
+            r->rb = nullptr;
+            r->rb_cap = 0;
+            if (hipHostMalloc(&r->rb, ce + le, 0) != hipSuccess) return fail(-3);
+            r->rb_cap = ce + le;
         }
-    });
+        int32_t *ce_h = host ? ends : (int32_t *)r->rb, *le_h = host ? lend : (int32_t *)((uint8_t *)r->rb + ce);
+        X.fetch(ce_h, ends, ce);
+        X.fetch(le_h, lend, le);
+        X.sync();
+        if (X.err) return fail(X.err);
+        memcpy(r->class_start.data(), ce_h, ce);
+        memcpy(r->unit_start.data(), le_h, le);
+        r->unit_start[0] = 0;
+    }
     {   // run ends -> counts: the runs are in (level, class) order, so a run
         // starts where the previous non-empty one ended
         int32_t prev = 0;
@@ -1460,168 +1093,85 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                     prev = e;
                 }
         }
-    }
-    for (int i = 0; i < n; i++) r->dep_start[i + 1] += r->dep_start[i];
-    r->deps.resize(prod.size());
-    for (int l = 0; l < n_levels; l++) {
-        if (r->unit_start[l + 1] < r->unit_start[l]) r->unit_start[l + 1] = r->unit_start[l];   // (levels are dense)
-        int32_t *cs = &r->class_start[(size_t)l * (NC + 1)];
-        for (int k = 0; k < NC; k++) cs[k + 1] += cs[k];
-    }
-    // 5. the upload image, written in place (page-locked, or a host vector
-    //    for DAV1D_GPU_REC_HOSTONLY): units and records scattered to their
-    //    ranks, the coefficient pool (decode order) and the emu jobs, by
-    //    several threads over disjoint ranges
-    const size_t coef_at = r->coefb.size() / cb;
-    // image: units | records | coefficients | emu jobs | per-unit aux |
-    //        launch-ahead units (class order) | their aux | aux pool
-    const size_t nx = r->xunits.size();
-    // with top_edge: the launch-ahead predictions whose bottom row ends a
-    // superblock row are backed up once that launch is done (backup runs
-    // between it and the wavefront, dav1d_backup_ipred_edge); a residual on
-    // them is added by a wavefront unit, which backs its row up again
-    std::vector<Dav1dGpuEdgeBackup> &bk = r->bk;
-    bk.clear();
-    if (r->top_on)
-        for (const Dav1dGpuUnit &u : r->xunits) {
-            const int p = u.plane, ds_px = (int)(dst[p].stride / bpp);
-            const int uy = u.dst_off / ds_px, ux = u.dst_off % ds_px, y1 = uy + kTx[u.tx].h;
-            const int sby = (y1 >> sbl[p]) - 1, w = std::min(kTx[u.tx].w, r->top[p].w - ux);
-            if ((y1 & ((1 << sbl[p]) - 1)) == 0 && sby < r->top[p].h && w > 0)
-                bk.push_back(Dav1dGpuEdgeBackup{p, sby, ux, w});
-        }
-    const size_t bu = (size_t)n * sizeof(Dav1dGpuUnit), br = (size_t)n * sizeof(Dav1dGpuIntraEdge),
-                 bc = coef_at * cb, be = r->emu.size() * sizeof(EmuJob), ba = (size_t)n * 4,
-                 bxu = nx * sizeof(Dav1dGpuUnit), bxa = nx * 4, bp = r->auxp.size(),
-                 bbk = bk.size() * sizeof(Dav1dGpuEdgeBackup);
-    const size_t o_c = bu + br, o_e = o_c + bc, o_a = o_e + be, o_xu = o_a + ba, o_xa = o_xu + bxu,
-                 o_p = o_xa + bxa, o_bk = o_p + bp, o_end = o_bk + bbk;
-    uint8_t *img;
-    if (host_only) {
-        r->h_host.resize(o_end);
-        img = r->h_host.data();
-    } else {
-        if (r->pin.grow(o_end)) return -3;
-        img = (uint8_t *)r->pin.p;
-    }
-    Dav1dGpuUnit *hu = (Dav1dGpuUnit *)img;
-    Dav1dGpuIntraEdge *hr = (Dav1dGpuIntraEdge *)(img + bu);
-    int32_t *ha = (int32_t *)(img + o_a);
-    // the launch-ahead units in class order (a counting sort by size class)
-    int32_t x_class[DGPU_N_RECT_TX_SIZES + 1] = {0};
-    if (nx) {
-        for (const Dav1dGpuUnit &u : r->xunits) x_class[u.tx + 1]++;
-        for (int k = 0; k < NC; k++) x_class[k + 1] += x_class[k];
-        int32_t at[DGPU_N_RECT_TX_SIZES];
-        memcpy(at, x_class, sizeof(at));
-        Dav1dGpuUnit *xu = (Dav1dGpuUnit *)(img + o_xu);
-        int32_t *xa = (int32_t *)(img + o_xa);
-        for (size_t i = 0; i < nx; i++) {
-            const int k = at[r->xunits[i].tx]++;
-            xu[k] = r->xunits[i];
-            xa[k] = r->xaux[i];
+        for (int l = 0; l < n_levels; l++) {
+            if (r->unit_start[l + 1] < r->unit_start[l]) r->unit_start[l + 1] = r->unit_start[l];   // (levels are dense)
+            int32_t *cs = &r->class_start[(size_t)l * (NC + 1)];
+            for (int k = 0; k < NC; k++) cs[k + 1] += cs[k];
         }
     }
-    if (bp) memcpy(img + o_p, r->auxp.data(), bp);
-    if (bbk) memcpy(img + o_bk, bk.data(), bbk);
-    {   // in rank order: the image is written sequentially, the cells read by index
-        const int nt = n < 32768 ? 1 : nthreads;
-        int32_t *deps = r->deps.data();
-        const int32_t *ds = r->dep_start.data();
-        auto work = [&](int t) {
-            const int i0 = (int)((int64_t)n * t / nt), i1 = (int)((int64_t)n * (t + 1) / nt);
-            for (int i = i0; i < i1; i++) {
-                const int ci = (int)(keys[i] & ((1u << 21) - 1));
-                const Unit &c = cells[ci];
-                hu[i] = c.u;   // coef_off / edge_off are decode-order pool offsets
-                ha[i] = c.aux;
-                Dav1dGpuIntraEdge e = c.rec;
-                e.unit = i;
-                hr[i] = e;
-                int32_t *o = deps + ds[i];
-                for (int k = prod_start[ci]; k < prod_start[ci + 1]; k++) *o++ = rank[prod[k]];
-            }
-            const size_t b0 = bc * t / nt, b1 = bc * (t + 1) / nt;
-            if (b1 > b0) memcpy(img + o_c + b0, r->coefb.data() + b0, b1 - b0);
-        };
-        r->pool->run(nt, work);
-        if (be) memcpy(img + o_e, r->emu.data(), be);
-    }
-    lap("fill");
+    int32_t x_class[NC + 1];
+    x_class[0] = 0;
+    for (int k = 0; k < NC; k++) x_class[k + 1] = x_end[k + 1] ? x_end[k + 1] : x_class[k];
+    lap("schedule");
     r->rec_start = r->unit_start;
     r->run_start.assign(n_levels + 1, 0);
     r->last_units = n;
     r->last_levels = n_levels;
-    auto drop_recording = [&] {
-        r->blocks.clear();
-        r->block_aux.clear();
-        r->baux.clear();
-        r->residuals.clear();
-        r->coefb.clear();
-    };
-    if ((!n && !nx) || host_only) {
-        // DAV1D_GPU_REC_DUMP=<file> with DAV1D_GPU_REC_HOSTONLY (diagnostics):
-        // the upload image and the schedule, appended, to compare host builds
-        static const char *dump = getenv("DAV1D_GPU_REC_DUMP");
-        if (host_only && dump) {
-            if (FILE *f = fopen(dump, "ab")) {
-                auto put = [&](const void *p, size_t nb) { if (nb) fwrite(p, 1, nb, f); };
-                const int64_t hdr[4] = {n, n_levels, (int64_t)nx, (int64_t)o_end};
-                put(hdr, sizeof(hdr));
-                put(r->h_host.data(), o_end);
-                put(r->unit_start.data(), r->unit_start.size() * 4);
-                put(r->class_start.data(), r->class_start.size() * 4);
-                put(r->dep_start.data(), r->dep_start.size() * 4);
-                put(r->deps.data(), r->deps.size() * 4);
-                put(x_class, sizeof(x_class));
-                fclose(f);
-            }
+    const size_t bu = (size_t)n * sizeof(Dav1dGpuUnit), br = (size_t)n * sizeof(Dav1dGpuIntraEdge), bc = r->coefb.n,
+                 be = (size_t)n_emu * sizeof(EmuJob), ba = (size_t)n * 4, bxu = (size_t)nx * sizeof(Dav1dGpuUnit),
+                 bxa = (size_t)nx * 4, bp = aux_end, bbk = (size_t)n_bk * sizeof(Dav1dGpuEdgeBackup);
+    if (dump) {   // image: units | records | coefficients | emu jobs | per-unit aux |
+                  // launch-ahead units (class order) | their aux | aux pool | backup runs
+        if (FILE *f = fopen(dump, "ab")) {
+            std::vector<uint8_t> tmp;
+            auto put = [&](const void *p, size_t nbytes) {
+                if (!nbytes) return;
+                if (host) {
+                    fwrite(p, 1, nbytes, f);
+                    return;
+                }
+                tmp.resize(nbytes);
+                if (hipMemcpy(tmp.data(), p, nbytes, hipMemcpyDeviceToHost) == hipSuccess) fwrite(tmp.data(), 1, nbytes, f);
+            };
+            const int64_t hdr4[4] = {n, n_levels, (int64_t)nx, (int64_t)(bu + br + bc + be + ba + bxu + bxa + bp + bbk)};
+            fwrite(hdr4, 1, sizeof(hdr4), f);
+            put(units, bu);
+            put(recs, br);
+            put(r->d_coef.p, bc);
+            put(c.emu, be);
+            put(aux, ba);
+            put(xunits, bxu);
+            put(xaux, bxa);
+            put(c.auxp, bp);
+            put(bk, bbk);
+            fwrite(r->unit_start.data(), 1, r->unit_start.size() * 4, f);
+            fwrite(r->class_start.data(), 1, r->class_start.size() * 4, f);
+            put(dstart, (size_t)(n + 1) * 4);
+            put(deps, (size_t)n_deps * 4);
+            fwrite(x_class, 1, sizeof(x_class), f);
+            fclose(f);
         }
-        drop_recording();
+    }
+    if ((!n && !nx) || host || dump) {
+        r->drop_recording();
         return 0;
     }
 
-    // upload and launch
+    // 8. the picture's work on the caller's stream, behind the prep
     hipStream_t st = (hipStream_t)stream;
+    if (hipEventRecord(r->prep, r->pst) != hipSuccess || hipStreamWaitEvent(st, r->prep, 0) != hipSuccess)
+        return fail(-3);
     Dav1dGpuIntraSchedule s;
     memset(&s, 0, sizeof(s));
     s.n_levels = n_levels;
-    s.flags = DGPU_IS_FUSED | DGPU_IS_PERSISTENT;
+    s.flags = DGPU_IS_FUSED | DGPU_IS_PERSISTENT | DGPU_IS_DEVICE_DEPS;
     s.unit_start = r->unit_start.data();
     s.class_start = r->class_start.data();
     s.rec_start = r->rec_start.data();
     s.run_start = r->run_start.data();
-    s.dep_start = r->dep_start.data();
-    s.deps = r->deps.data();
+    s.dep_start = dstart;
+    s.deps = deps;
     const int64_t wsb = n ? dav1d_gpu_intra_workspace_bytes(&s, n) : 16;
-    if (wsb < 0) return -2;
-    if (r->d_units.grow((size_t)n * sizeof(Dav1dGpuUnit)) || r->d_recs.grow((size_t)n * sizeof(Dav1dGpuIntraEdge)) ||
-        r->d_coef.grow(std::max<size_t>(coef_at * cb, 16)) || r->d_edges.grow(std::max<size_t>(edge_px * bpp, 16)) ||
-        r->d_work.grow((size_t)wsb))
-        return -3;
-    if (be && (r->d_emu_jobs.grow(be) || r->d_emu.grow((size_t)emu_rows * kEmuStride * bpp + 256))) return -3;
-    if (r->d_aux.grow(ba) || r->d_auxp.grow(std::max<size_t>(bp, 16)) ||
-        (nx && (r->d_xunits.grow(bxu) || r->d_xaux.grow(bxa))) || (bbk && r->d_bk.grow(bbk)))
-        return -3;
-    const uint8_t *pin = img;
-    // once a copy from the pinned image may be queued, a failure drains the
-    // stream before returning: a retry rewrites that image and may regrow the
-    // device buffers, which the queued copies and kernels still use
+    if (wsb < 0) return fail(-2);
+    if (r->d_edges.grow(edge_px * bpp) || r->d_work.grow((size_t)wsb) ||
+        (n_emu && r->d_emu.grow((size_t)emu_rows * kEmuStride * bpp + 256)))
+        return fail(-3);
+    // once the caller's stream may use the buffers, a failure drains it too
     auto drained = [&](int rc) {
         (void)hipStreamSynchronize(st);
-        return rc;
+        return fail(rc);
     };
-    if ((bu && hipMemcpyAsync(r->d_units.p, pin, bu, hipMemcpyHostToDevice, st)) ||
-        (br && hipMemcpyAsync(r->d_recs.p, pin + bu, br, hipMemcpyHostToDevice, st)) ||
-        (bc && hipMemcpyAsync(r->d_coef.p, pin + o_c, bc, hipMemcpyHostToDevice, st)) ||
-        (be && hipMemcpyAsync(r->d_emu_jobs.p, pin + o_e, be, hipMemcpyHostToDevice, st)) ||
-        (ba && hipMemcpyAsync(r->d_aux.p, pin + o_a, ba, hipMemcpyHostToDevice, st)) ||
-        (nx && hipMemcpyAsync(r->d_xunits.p, pin + o_xu, bxu, hipMemcpyHostToDevice, st)) ||
-        (nx && hipMemcpyAsync(r->d_xaux.p, pin + o_xa, bxa, hipMemcpyHostToDevice, st)) ||
-        (bp && hipMemcpyAsync(r->d_auxp.p, pin + o_p, bp, hipMemcpyHostToDevice, st)) ||
-        (bbk && hipMemcpyAsync(r->d_bk.p, pin + o_bk, bbk, hipMemcpyHostToDevice, st)))
-        return drained(-3);
-    if (be) {   // the clamped footprints, before the wavefront reads them
+    if (n_emu) {   // the clamped footprints, before the wavefront reads them
         EmuArgs ea;
         memset(&ea, 0, sizeof(ea));
         for (int k = 0; k < DGPU_MAX_REFS - 1; k++)
@@ -1632,8 +1182,8 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
                 ea.h[k][p] = ref[k][p].h;
             }
         ea.out = r->d_emu.p;
-        ea.jobs = (const EmuJob *)r->d_emu_jobs.p;
-        ea.n = (int32_t)r->emu.size();
+        ea.jobs = c.emu;
+        ea.n = n_emu;
         ea.rows = emu_rows;
         if (r->bpc == 8)
             k_emu_footprints<uint8_t><<<dim3(ea.n), 64, 0, st>>>(ea);
@@ -1649,24 +1199,26 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         // last byte), for the launches' range tables
         auto &bx = dgpu::bnd_extra();
         bx.clear();
-        auto reg = [&](const void *p, size_t nb, int id) {
-            if (p && nb) bx.push_back(dgpu::BndRange{p, (nb + 15) & ~(size_t)15, id});
+        auto reg = [&](const void *p, size_t nbytes, int id) {
+            if (p && nbytes) bx.push_back(dgpu::BndRange{p, (nbytes + 15) & ~(size_t)15, id});
         };
-        reg(r->d_units.p, bu, dgpu::BND_UNITS);
-        reg(r->d_recs.p, br, dgpu::BND_RECS);
+        reg(units, bu, dgpu::BND_UNITS);
+        reg(recs, br, dgpu::BND_RECS);
         // DAV1D_GPU_BND_SELFTEST=1: register the coefficient pool 64 bytes
         // short, so the diagnostics must report the last units' coefficient
         // reads (the check's positive control)
         static const bool selftest = getenv("DAV1D_GPU_BND_SELFTEST") != nullptr;
         reg(r->d_coef.p, selftest && bc > 128 ? bc - 64 : bc, dgpu::BND_COEF);
         reg(r->d_edges.p, edge_px * bpp, dgpu::BND_EDGES);
-        reg(r->d_aux.p, ba, dgpu::BND_AUX);
-        reg(r->d_auxp.p, bp, dgpu::BND_AUXPOOL);
+        reg(aux, ba, dgpu::BND_AUX);
+        reg(c.auxp, bp, dgpu::BND_AUXPOOL);
         reg(r->d_work.p, (size_t)wsb, dgpu::BND_WORK);
-        if (be) reg(r->d_emu.p, (size_t)emu_rows * kEmuStride * bpp, dgpu::BND_EMU);
+        reg(dstart, (size_t)(n + 1) * 4, dgpu::BND_WORK);
+        reg(deps, (size_t)n_deps * 4, dgpu::BND_WORK);
+        if (n_emu) reg(r->d_emu.p, (size_t)emu_rows * kEmuStride * bpp, dgpu::BND_EMU);
         if (nx) {
-            reg(r->d_xunits.p, bxu, dgpu::BND_XUNITS);
-            reg(r->d_xaux.p, bxa, dgpu::BND_XAUX);
+            reg(xunits, bxu, dgpu::BND_XUNITS);
+            reg(xaux, bxa, dgpu::BND_XAUX);
         }
     }
 #endif
@@ -1679,13 +1231,11 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         eb.pic[p] = dst[p];
         if (ref)
             for (int k = 0; k < DGPU_REC_EMU_SLOT; k++) fb.ref[k][p] = ref[k][p];
-        if (be) fb.ref[DGPU_REC_EMU_SLOT][p] = Dav1dGpuPlane{r->d_emu.p, (int64_t)kEmuStride * bpp, kEmuStride, emu_rows};
-    }
-    for (int p = 0; p < 3; p++) {
-        eb.sb_log2[p] = sbl[p];
+        if (n_emu) fb.ref[DGPU_REC_EMU_SLOT][p] = Dav1dGpuPlane{r->d_emu.p, (int64_t)kEmuStride * bpp, kEmuStride, emu_rows};
+        eb.sb_log2[p] = c.sbl[p];
         if (r->top_on) eb.top_edge[p] = r->top[p];
     }
-    fb.units = (const Dav1dGpuUnit *)r->d_units.p;
+    fb.units = units;
     fb.n_units = n;
     fb.class_start[NC] = n;
     fb.coef = r->d_coef.p;
@@ -1693,30 +1243,28 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     fb.bitdepth_max = r->bdmax;
     fb.cfl_luma = dst[0];
     fb.cfl_ss = 3;
-    fb.aux = (const int32_t *)r->d_aux.p;
-    fb.aux_pool = r->d_auxp.p;
+    fb.aux = aux;
+    fb.aux_pool = c.auxp;
     if (nx) {   // WARP / INTER_WMASK / INTER_OBMC / INTER_SCALED predictions ahead of the wavefront
         Dav1dGpuFrameBatch xb = fb;
-        xb.units = (const Dav1dGpuUnit *)r->d_xunits.p;
-        xb.n_units = (int32_t)nx;
+        xb.units = xunits;
+        xb.n_units = nx;
         for (int k = 0; k <= NC; k++) xb.class_start[k] = x_class[k];
         for (int k = 0; k < NC; k++) xb.class_warp[k] = x_class[k + 1] - x_class[k];
-        xb.aux = (const int32_t *)r->d_xaux.p;
+        xb.aux = xaux;
         const int xrc = r->bpc == 8 ? dav1d_gpu_recon_8bpc(&xb, stream) : dav1d_gpu_recon_16bpc(&xb, stream);
         if (xrc) return drained(xrc);
     }
-    if (bbk) {   // their superblock-bottom rows into top_edge, before the wavefront
-        const auto *runs = (const Dav1dGpuEdgeBackup *)r->d_bk.p;
-        const int brc = r->bpc == 8 ? dav1d_gpu_backup_ipred_edge_8bpc(&eb, runs, (int)bk.size(), stream)
-                                    : dav1d_gpu_backup_ipred_edge_16bpc(&eb, runs, (int)bk.size(), stream);
+    if (n_bk) {   // their superblock-bottom rows into top_edge, before the wavefront
+        const int brc = r->bpc == 8 ? dav1d_gpu_backup_ipred_edge_8bpc(&eb, bk, n_bk, stream)
+                                    : dav1d_gpu_backup_ipred_edge_16bpc(&eb, bk, n_bk, stream);
         if (brc) return drained(brc);
     }
-    eb.units = (Dav1dGpuUnit *)r->d_units.p;
+    eb.units = units;
     eb.edges = r->d_edges.p;
-    eb.recs = (const Dav1dGpuIntraEdge *)r->d_recs.p;
+    eb.recs = recs;
     eb.n_recs = n;
     eb.bitdepth_max = r->bdmax;
-    lap("upload");
     if (n) {
         const int rc = r->bpc == 8 ? dav1d_gpu_recon_intra_frame_8bpc(&fb, &eb, &s, stream)
                                    : dav1d_gpu_recon_intra_frame_16bpc(&fb, &eb, &s, stream);
@@ -1728,11 +1276,11 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
 #endif
     if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return drained(-3);
     // the wavefront's error word (workspace int32 [1]) follows on the stream
-    if (n && (r->flag.grow(16) ||
-              hipMemcpyAsync(r->flag.p, (const int32_t *)r->d_work.p + 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess))
+    if (n && !r->flag && hipHostMalloc(&r->flag, 16, 0) != hipSuccess) return drained(-3);
+    if (n && hipMemcpyAsync(r->flag, (const int32_t *)r->d_work.p + 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return drained(-3);
     if (hipEventRecord(r->done, st) != hipSuccess) return drained(-3);
     r->pending_check = n > 0;
-    drop_recording();
+    r->drop_recording();
     return 0;
 }

@@ -1183,6 +1183,13 @@ class Recorder:
         self.lib.dav1d_gpu_recorder_stats(self.h, ctypes.byref(n), ctypes.byref(lv))
         return n.value, lv.value
 
+    def prep_ms(self):
+        """Device time of the last flush's prep (upload, cut, levels, sort,
+        scatter on the recorder's own stream), ms."""
+        ms = ctypes.c_float()
+        self.lib.dav1d_gpu_recorder_prep_ms(self.h, ctypes.byref(ms))
+        return ms.value
+
 
 def replay(rec, fr, rows=None):
     """Feed an IntraFrame's blocks and residuals to a Recorder, in decode

@@ -702,6 +702,12 @@ int dav1d_gpu_backup_ipred_edge_16bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav
                           3x slower than the dataflow form on a 4K intra
                           frame (a longer superblock chain) */
 
+#define DGPU_IS_DEVICE_DEPS 8   /* (with PERSISTENT) dep_start / deps are device
+                                   arrays, read by the kernel where they are
+                                   and not checked on the host: the batch
+                                   recorder's schedules, built on the device
+                                   (every unit's producers in earlier tasks) */
+
 typedef struct Dav1dGpuIntraSchedule {
     int32_t n_levels;
     int32_t flags;               /* DGPU_IS_*                                   */
@@ -716,7 +722,8 @@ typedef struct Dav1dGpuIntraSchedule {
                                     counters + the task list                  */
     int64_t  workspace_bytes;    /* >= dav1d_gpu_intra_workspace_bytes()       */
     /* optional (DGPU_IS_PERSISTENT): the units each unit reads pixels of,
-       host CSR over recon->units (producers at lower levels).  Given, a
+       host CSR over recon->units (producers at lower levels; device with
+       DGPU_IS_DEVICE_DEPS).  Given, a
        wave waits only for the tasks holding its units' producers instead of
        the whole previous level (dataflow); NULL: level barriers.            */
     const int32_t *dep_start;    /* n_units + 1                                */
@@ -895,6 +902,11 @@ int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane dst[3],
 int dav1d_gpu_recorder_set_top_edge(Dav1dGpuRecorder *r, const Dav1dGpuPlane top_edge[3], int sb128);
 /* Levels and units of the last flush (diagnostics). */
 int dav1d_gpu_recorder_stats(const Dav1dGpuRecorder *r, int32_t *n_units, int32_t *n_levels);
+/* Device time of the last flush's prep (diagnostics): upload of the
+ * recording, cut, levels, sort and scatter on the recorder's own stream,
+ * from the first upload to the last step, ms (HIP events); the flush waits
+ * for it, so it is part of the flush's host time too.  0 or -1. */
+int dav1d_gpu_recorder_prep_ms(const Dav1dGpuRecorder *r, float *ms);
 /* Outcome of the last flush (waits for it): 0, -6 if its wavefront gave up
  * waiting for producers (that picture is incomplete), -3 on a HIP error.  An
  * outcome is reported once: a -6 not read here is returned by the next flush,

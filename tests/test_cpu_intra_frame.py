@@ -163,12 +163,12 @@ def _flow_tasks_py(pkg, fr, groups, cap=8):
     across a change of the group byte)."""
     abi = pkg.abi
     order = [3, 9, 10, 2, 15, 16, 7, 8, 1, 13, 14, 5, 6, 0, 4, 11, 12, 17, 18]
-    tall = {(8, 16): 8, (4, 16): 4, (8, 32): 16}
+    # the wavefront TUs (recon_ie{8,16}.hip): 4x4 / 4x8 / 8x4 units get 8
+    # lanes (DGPU_IE_SMALL_LANES), every other class one 4x2 output task per
+    # lane (DGPU_IE_WIDE_LANES: w * h / 8 lanes, 2..64)
     lanes = {}
     for t, (tw, th) in enumerate(abi.TX_WH):
-        lanes[t] = 64 if tw * th >= 1024 else tall.get((tw, th), min(max(min(tw * th // 8, max(tw, min(th, 32))), 2), 64))
-        if tw * th <= 32:   # the wavefront TUs give 4x4 / 4x8 / 8x4 units 8 lanes (recon_ie{8,16}.hip)
-            lanes[t] = 8
+        lanes[t] = 8 if tw * th <= 32 else min(max(tw * th // 8, 2), 64)
     n = 0
     for lv in range(fr.n_levels):
         cs = fr.class_start[lv]

@@ -325,3 +325,29 @@ def test_recorder_top_edge_post_filter_interleave(oracle, kw):
         got = got.view(np.uint16) if hbd else got
         assert np.array_equal(got, ho.top[p][:rows, :w]), p
     rec.close()
+
+
+def test_recorder_device_image_golden(tmp_path):
+    """The flush's cut and schedule built on the device (csrc/rec_cut.hpp,
+    csrc/recorder.hip) and read back: the upload image and schedule of
+    tools/rec_dump.py's seven frames byte for byte as the round-6 host
+    implementation made them (tests/golden/rec_dump_md5.json; the same
+    frames' host-only steps are checked in test_cpu_recorder_golden.py).
+    Dump mode launches nothing on the (dummy) pictures."""
+    import json
+    import os
+    import re
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    want = json.load(open(os.path.join(root, "tests", "golden", "rec_dump_md5.json")))["frames"]
+    env = dict(os.environ)
+    env.pop("DAV1D_GPU_REC_HOSTONLY", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rec_dump.py"), str(tmp_path / "d.bin"),
+                        "--device"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = {m.group(1): (int(m.group(3)), m.group(4)) for m in
+           re.finditer(r"frame (\d+) rc (\S+) units (\d+) .* md5 (\w+)", r.stdout)}
+    assert set(got) == set(want), r.stdout
+    for k, w in want.items():
+        assert got[k] == (w["units"], w["md5"]), (k, got[k], w)

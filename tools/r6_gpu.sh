@@ -44,6 +44,10 @@ for s in "${@:-tests}"; do
             DAV1D_GPU_REC_TIMING=1 timeout -k 10 600 python -u bench.py --steps 50 --no-families --no-configs --no-tiles \
                 --no-grain --no-superres --no-lpf --no-cpu --no-check > "$O/benchpart.json" 2> "$O/benchpart.log" \
                 || { echo "[r6] benchpart failed"; exit 1; } ;;
+    recbench) # the recorder leg alone (host laps on stderr), with the headline
+            DAV1D_GPU_REC_TIMING=1 timeout -k 10 300 python -u bench.py --steps 20 --no-families --no-configs --no-tiles \
+                --no-intra --no-grain --no-cdef --no-superres --no-lpf --no-lr --no-cpu --no-check > "$O/recbench.json" \
+                2> "$O/recbench.log" || { echo "[r6] recbench failed"; exit 1; } ;;
     checkasm) # the full checkasm-style space (no --quick), one pass per table and bitdepth
             for t in ${CKT:-mc ipred itx cdef lpf lr}; do for b in 8 16; do
                 timeout -k 10 1200 ./tests/checkasm_gpu --test=$t --bpc=$b --seed=1 > "$O/checkasm_full_${t}_${b}.log" 2>&1 \
