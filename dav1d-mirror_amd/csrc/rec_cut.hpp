@@ -266,24 +266,33 @@ __host__ __device__ inline int cut_block(const CutCtx &c, int bi) {
     const int bwc = min(b.w, c.pw[p] - b.x), bhc = min(b.h, c.ph[p] - b.y);
     const int bw4c = bwc / 4, bh4c = bhc / 4;
     const int ds_px = c.ds_px[p];
-    // the block's bases (write pass) and its running counts
-    long long B[C_N] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if constexpr (W)
-        for (int i = 0; i < C_N; i++) B[i] = c.base[bi].v[i];
+    // the block's bases (write pass; scalars, so nothing of them goes to
+    // scratch) and its running counts
+    int32_t b_aux = 0, b_erows = 0, b_edge = 0, b_cells = 0;
+    long long b_ejobs = 0, b_xu = 0;
+    if constexpr (W) {
+        const BlockCnt &q = c.base[bi];
+        b_cells = (int32_t)q.v[C_CELLS];
+        b_aux = (int32_t)q.v[C_AUX];
+        b_ejobs = q.v[C_EJOBS];
+        b_erows = (int32_t)q.v[C_EROWS];
+        b_xu = q.v[C_XU];
+        b_edge = (int32_t)q.v[C_EDGE];
+    }
     int n_cells = 0, n_ejobs = 0, n_xu = 0, n_res = 0;
     int32_t aux_end = 0, erows = 0, edge = 0;
     long long n_raw = 0;
     auto aux_alloc = [&](int nbytes) -> int32_t {   // 16-byte aligned records
         const int32_t o = (aux_end + 15) & ~15;
         aux_end = o + nbytes;
-        return (int32_t)B[C_AUX] + o;
+        return b_aux + o;
     };
     // a clamped copy of the fw x fh footprint at (x0, y0) of ref slot / plane
     // in a band of new scratch rows; returns its scratch offset
     auto emu_band = [&](int x0, int y0, int fw, int fh, int slot, int plane) -> int32_t {
-        const int32_t o = ((int32_t)B[C_EROWS] + erows) * kEmuStride;
+        const int32_t o = (b_erows + erows) * kEmuStride;
         if constexpr (W)
-            c.emu[B[C_EJOBS] + n_ejobs] = EmuJob{x0, y0, o, (uint8_t)fw, (uint8_t)fh, (uint8_t)slot, (uint8_t)plane};
+            c.emu[b_ejobs + n_ejobs] = EmuJob{x0, y0, o, (uint8_t)fw, (uint8_t)fh, (uint8_t)slot, (uint8_t)plane};
         n_ejobs++;
         erows += fh;
         return o;
@@ -394,12 +403,12 @@ __host__ __device__ inline int cut_block(const CutCtx &c, int bi) {
                     }
                     u.p.inter.src_off[0] = 0;
                     if (!all_in) {
-                        const int32_t band = ((int32_t)B[C_EROWS] + erows) * kEmuStride;
+                        const int32_t band = (b_erows + erows) * kEmuStride;
                         for (int sy = 0; sy < ny; sy++)
                             for (int sx = 0; sx < nx; sx++) {
                                 const int16_t *xy = (const int16_t *)(bdata + 16 + 8 * ((oy / 8 + sy) * gw + ox / 8 + sx));
                                 if constexpr (W) {
-                                    c.emu[B[C_EJOBS] + n_ejobs] =
+                                    c.emu[b_ejobs + n_ejobs] =
                                         EmuJob{xy[0] - 3, xy[1] - 3, band + 15 * sy * kEmuStride + 16 * sx, 15, 15,
                                                (uint8_t)rr, (uint8_t)p};
                                     int16_t *e8 = (int16_t *)(c.auxp + ao + 16 + 8 * (sy * nx + sx));
@@ -480,8 +489,8 @@ __host__ __device__ inline int cut_block(const CutCtx &c, int bi) {
                     if (n == 1) u.p.inter.weight = 0;
                 }
                 if constexpr (W) {
-                    memcpy(&c.xu[B[C_XU] + n_xu], &u, sizeof(u));
-                    c.xa[B[C_XU] + n_xu] = ao;
+                    memcpy(&c.xu[b_xu + n_xu], &u, sizeof(u));
+                    c.xa[b_xu + n_xu] = ao;
                 }
                 n_xu++;
             }
@@ -492,7 +501,7 @@ __host__ __device__ inline int cut_block(const CutCtx &c, int bi) {
     // residual-only cells that read it
     const bool iib = b.kind == DGPU_PRED_INTER_INTRA;
     const int ncx = (bwc + tw - 1) / tw, ncy = (bhc + th - 1) / th;
-    const int32_t iic_at = (int32_t)B[C_CELLS];   // the inter-intra block's prediction cell (its first)
+    const int32_t iic_at = b_cells;   // the inter-intra block's prediction cell (its first)
     for (int k = iib ? -1 : 0; k < ncx * ncy; k++) {
         const bool iic = k < 0;
         const int ox = iic ? 0 : (k % ncx) * tw, oy = iic ? 0 : (k / ncx) * th;
@@ -614,7 +623,7 @@ __host__ __device__ inline int cut_block(const CutCtx &c, int bi) {
                 u.p.cfl.luma_off = (2 * uy) * c.ds_px[0] + 2 * ux;
             }
             e.flags = (uint8_t)fl;
-            u.p.intra.edge_off = (int32_t)B[C_EDGE] + edge + 2 * th;   // CFL: the same field
+            u.p.intra.edge_off = b_edge + edge + 2 * th;   // CFL: the same field
             edge += 2 * th + 2 * tw + 1;
             const int m = remap_mode(e.mode, e.angle, hl, ht);
             nd = needs(m);
@@ -637,7 +646,7 @@ __host__ __device__ inline int cut_block(const CutCtx &c, int bi) {
         j.link = iib && !iic ? iic_at : -1;
         const int nl = lookups<false>(j, nullptr, 0, nullptr, 0, [](int32_t) {});
         if constexpr (W) {
-            const long long ci = B[C_CELLS] + n_cells;
+            const long long ci = (long long)b_cells + n_cells;
             memcpy(&c.cu[ci], &u, sizeof(u));
             memcpy(&c.crec[ci], &e, sizeof(e));
             c.caux[ci] = caux;

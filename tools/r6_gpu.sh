@@ -48,6 +48,13 @@ for s in "${@:-tests}"; do
             DAV1D_GPU_REC_TIMING=1 timeout -k 10 300 python -u bench.py --steps 20 --no-families --no-configs --no-tiles \
                 --no-intra --no-grain --no-cdef --no-superres --no-lpf --no-lr --no-cpu --no-check > "$O/recbench.json" \
                 2> "$O/recbench.log" || { echo "[r6] recbench failed"; exit 1; } ;;
+    recprep) # the recorder flush alone: host / prep / stream times, laps, then its kernels under rocprofv3
+            DAV1D_GPU_REC_TIMING=1 timeout -k 10 300 python -u tools/rec_prep_time.py --reps 5 > "$O/recprep.log" 2>&1 \
+                || { echo "[r6] recprep failed"; exit 1; }
+            tail -3 "$O/recprep.log"
+            cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/recprof" -o rec \
+                -- python3 -u "$R/tools/rec_prep_time.py" --reps 3 > "$O/recprof.log" 2>&1 || { echo "[r6] recprof failed"; exit 1; }
+            cd "$R" ;;
     checkasm) # the full checkasm-style space (no --quick), one pass per table and bitdepth
             for t in ${CKT:-mc ipred itx cdef lpf lr}; do for b in 8 16; do
                 timeout -k 10 1200 ./tests/checkasm_gpu --test=$t --bpc=$b --seed=1 > "$O/checkasm_full_${t}_${b}.log" 2>&1 \
