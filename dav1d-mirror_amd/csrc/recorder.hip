@@ -354,6 +354,8 @@ struct Dav1dGpuRecorder {
     Mem d_bkf, d_bks, d_bk, d_edges, d_work, d_emu, d_tmp;
     std::vector<int32_t> unit_start, class_start, rec_start, run_start;
     hipStream_t pst = nullptr;    // the recorder's stream (the prep)
+    hipStream_t cst = nullptr;    // the coefficient pool's upload, beside the prep
+    hipEvent_t coef_ev = nullptr;
     hipEvent_t prep = nullptr;    // the prep done, for the caller's stream
     hipEvent_t pt0 = nullptr, pt1 = nullptr;   // the prep's span (timing events)
     float prep_ms = 0;
@@ -395,11 +397,12 @@ extern "C" void dav1d_gpu_recorder_free(Dav1dGpuRecorder *r) {
             (void)hipEventSynchronize(r->done);
             (void)hipEventDestroy(r->done);
         }
-        if (r->pst) {
-            (void)hipStreamSynchronize(r->pst);
-            (void)hipStreamDestroy(r->pst);
-        }
-        for (hipEvent_t e : {r->prep, r->pt0, r->pt1})
+        for (hipStream_t q : {r->pst, r->cst})
+            if (q) {
+                (void)hipStreamSynchronize(q);
+                (void)hipStreamDestroy(q);
+            }
+        for (hipEvent_t e : {r->prep, r->pt0, r->pt1, r->coef_ev})
             if (e) (void)hipEventDestroy(e);
         if (r->rb) (void)hipHostFree(r->rb);
         if (r->flag) (void)hipHostFree(r->flag);
@@ -661,7 +664,9 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     };
     if (!host && !r->pst) {
         if (hipStreamCreateWithFlags(&r->pst, hipStreamNonBlocking) != hipSuccess) return -3;
-        if (hipEventCreateWithFlags(&r->prep, hipEventDisableTiming) != hipSuccess || hipEventCreate(&r->pt0) != hipSuccess ||
+        if (hipStreamCreateWithFlags(&r->cst, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&r->prep, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&r->coef_ev, hipEventDisableTiming) != hipSuccess || hipEventCreate(&r->pt0) != hipSuccess ||
             hipEventCreate(&r->pt1) != hipSuccess)
             return -3;
     }
@@ -670,6 +675,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     // before returning: a retry regrows buffers the queued steps still use
     auto fail = [&](int rc) {
         if (!host && r->pst) (void)hipStreamSynchronize(r->pst);
+        if (!host && r->cst) (void)hipStreamSynchronize(r->cst);
         return rc;
     };
     const int bpp = r->bpc / 8;
@@ -828,7 +834,15 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     c.xa = r->d_xa0.as<int32_t>();
     X.memset(c.auxp, 0, aux_end);
     X.memset(c.rawc + n, 0, 4);
-    X.upload(r->d_coef.p, r->coefb.p, r->coefb.n);
+    // the coefficient pool goes up on a stream of its own, beside the prep's
+    // kernels (only the wavefront reads it); the flush waits for it before
+    // returning, so the recording may reuse its staging
+    if (host) {
+        X.upload(r->d_coef.p, r->coefb.p, r->coefb.n);
+    } else if (r->coefb.n && (hipMemcpyAsync(r->d_coef.p, r->coefb.p, r->coefb.n, hipMemcpyHostToDevice, r->cst) != hipSuccess ||
+                              hipEventRecord(r->coef_ev, r->cst) != hipSuccess)) {
+        return fail(-3);
+    }
     X.each(nb, [=] __host__ __device__(int i) { (void)cut_block<true>(c, i); });
     // 3. levels and producers: a cell sits one level above every pixel its
     //    edges (or CfL luma, or an inter-intra residual's prediction) read;
@@ -1110,6 +1124,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     const size_t bu = (size_t)n * sizeof(Dav1dGpuUnit), br = (size_t)n * sizeof(Dav1dGpuIntraEdge), bc = r->coefb.n,
                  be = (size_t)n_emu * sizeof(EmuJob), ba = (size_t)n * 4, bxu = (size_t)nx * sizeof(Dav1dGpuUnit),
                  bxa = (size_t)nx * 4, bp = aux_end, bbk = (size_t)n_bk * sizeof(Dav1dGpuEdgeBackup);
+    if (!host && r->coefb.n && hipEventSynchronize(r->coef_ev) != hipSuccess) return fail(-3);
     if (dump) {   // image: units | records | coefficients | emu jobs | per-unit aux |
                   // launch-ahead units (class order) | their aux | aux pool | backup runs
         if (FILE *f = fopen(dump, "ab")) {

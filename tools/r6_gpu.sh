@@ -49,7 +49,7 @@ for s in "${@:-tests}"; do
                 --no-intra --no-grain --no-cdef --no-superres --no-lpf --no-lr --no-cpu --no-check > "$O/recbench.json" \
                 2> "$O/recbench.log" || { echo "[r6] recbench failed"; exit 1; } ;;
     recprep) # the recorder flush alone: host / prep / stream times, laps, then its kernels under rocprofv3
-            DAV1D_GPU_REC_TIMING=1 timeout -k 10 300 python -u tools/rec_prep_time.py --reps 5 > "$O/recprep.log" 2>&1 \
+            DAV1D_GPU_REC_TIMING=1 timeout -k 10 300 python -u tools/rec_prep_time.py --reps 5 --threads 4 > "$O/recprep.log" 2>&1 \
                 || { echo "[r6] recprep failed"; exit 1; }
             tail -3 "$O/recprep.log"
             cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/recprof" -o rec \

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--inter", type=float, default=0.7)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--threads", type=int, default=0, help="also: N recorders flushing at once from N threads")
     a = ap.parse_args()
     import torch
     import __graft_entry__ as ge
@@ -53,6 +54,37 @@ def main():
             rows.append(row)
     print({k: round(float(np.median([r[k] for r in rows])), 3) for k in rows[0]}, "median units", rec.stats())
     rec.close()
+    if a.threads:   # frame threads: one recorder and stream per thread, flushed together (warm)
+        import threading
+        nf = a.threads
+        recs = [intra.Recorder(8, 255, a.width, a.height) for _ in range(nf)]
+        dsts = [[torch.zeros((h, w), dtype=torch.uint8, device=dev) for (w, h) in fr.plane_wh] for _ in range(nf)]
+        sts = [torch.cuda.Stream(dev) for _ in range(nf)]
+        for rep in range(3):
+            for r_ in recs:
+                intra.replay(r_, fr)
+            torch.cuda.synchronize(dev)
+            go = threading.Barrier(nf + 1)
+            hms = [0.0] * nf
+
+            def one(i):
+                go.wait()
+                t0 = time.perf_counter()
+                recs[i].flush(dsts[i], refs, sts[i])
+                hms[i] = 1e3 * (time.perf_counter() - t0)
+            ths = [threading.Thread(target=one, args=(i,)) for i in range(nf)]
+            for t in ths:
+                t.start()
+            go.wait()
+            t0 = time.perf_counter()
+            for t in ths:
+                t.join()
+            wall = 1e3 * (time.perf_counter() - t0)
+            torch.cuda.synchronize(dev)
+            print(f"threads {nf} rep {rep}: wall {wall:.2f} ms, per frame {wall / nf:.2f} ms, host ms "
+                  f"{[round(h, 2) for h in hms]}, prep ms {[round(r_.prep_ms(), 2) for r_ in recs]}", flush=True)
+        for r_ in recs:
+            r_.close()
 
 
 if __name__ == "__main__":
