@@ -126,7 +126,7 @@ class IntraEdgeBatch(ctypes.Structure):
                 ("bitdepth_max", ctypes.c_int32)]
 
 
-IS_FUSED, IS_PERSISTENT, IS_SB, IS_DEVICE_DEPS = 1, 2, 4, 8
+IS_FUSED, IS_PERSISTENT, IS_SB, IS_DEVICE_DEPS, IS_LEVEL0_BATCH = 1, 2, 4, 8, 16
 EDGE_BACKUP_DTYPE = np.dtype([("plane", "<i4"), ("sby", "<i4"), ("x0", "<i4"), ("w", "<i4")])
 
 

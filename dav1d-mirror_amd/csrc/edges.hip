@@ -17,6 +17,7 @@
 #include "dav1d_gpu.h"
 #include "dsp_common.hpp"
 #include "intra_edge_dev.hpp"
+#include "lead_levels.hpp"
 
 // the fused reconstruction launch (recon_ie.hpp, recon_ie8/16.hip)
 int dgpu_recon_ie_8bpc(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch *e, void *stream);
@@ -165,6 +166,23 @@ static int launch_intra_frame(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraE
         if (s->n_levels && s->rec_start[0] != s->unit_start[0]) return -2;
         for (int l = 0; l <= s->n_levels; l++)
             if (s->rec_start[l] != s->unit_start[l]) return -2;
+        // DGPU_IS_LEVEL0_BATCH: the leading levels (lead_levels.hpp) in fused
+        // launches first, one per level; the persistent kernel takes the rest
+        for (int l = 0, nl = lead_levels(s); l < nl; l++) {
+            const int u0 = s->unit_start[l];
+            Dav1dGpuFrameBatch lb = *rb;
+            memset(lb.class_warp, 0, sizeof(lb.class_warp));
+            lb.units = rb->units + u0;
+            lb.n_units = s->unit_start[l + 1] - u0;
+            if (rb->aux) lb.aux = rb->aux + u0;   // (per unit, like the units)
+            memcpy(lb.class_start, s->class_start + (size_t)l * (NC + 1), sizeof(lb.class_start));
+            Dav1dGpuIntraEdgeBatch le = *eb;
+            le.units = eb->units + u0;
+            le.recs = eb->recs + u0;
+            le.n_recs = lb.n_units;
+            const int rc = BPC == 8 ? dgpu_recon_ie_8bpc(&lb, &le, stream) : dgpu_recon_ie_16bpc(&lb, &le, stream);
+            if (rc) return rc;
+        }
         return BPC == 8 ? dgpu_recon_flow_8bpc(rb, eb, s, stream) : dgpu_recon_flow_16bpc(rb, eb, s, stream);
     }
     const bool fused = s->flags & DGPU_IS_FUSED;
@@ -177,6 +195,7 @@ static int launch_intra_frame(const Dav1dGpuFrameBatch *rb, const Dav1dGpuIntraE
     for (int l = 0; l < s->n_levels; l++) {
         if (fused) {   // edges, prediction, residual and backups in one launch per level
             lb.units = rb->units + s->unit_start[l];
+            if (rb->aux) lb.aux = rb->aux + s->unit_start[l];   // (per unit, like the units)
             lb.n_units = s->unit_start[l + 1] - s->unit_start[l];
             memcpy(lb.class_start, s->class_start + (size_t)l * (NC + 1), sizeof(lb.class_start));
             le.units = eb->units + s->unit_start[l];

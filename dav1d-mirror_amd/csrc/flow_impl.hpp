@@ -20,6 +20,7 @@
 #include <mutex>
 #include <vector>
 
+#include "lead_levels.hpp"
 #include "recon_impl.hpp"
 
 #ifndef DGPU_FLOW_TRACE
@@ -401,7 +402,9 @@ static int flow_tasks(const Dav1dGpuIntraSchedule *s, int n_units, std::vector<F
     const int cap = flow_units_cap();
     tasks.clear();
     level_tasks.assign(s->n_levels > 0 ? s->n_levels : 1, 0);
-    for (int l = 0; l < s->n_levels; l++) {
+    // DGPU_IS_LEVEL0_BATCH: the leading levels ran in launches of their own
+    // (their units are marked done at launch, their level counts stay 0)
+    for (int l = lead_levels(s); l < s->n_levels; l++) {
         const int u0 = s->unit_start[l];
         const int32_t *cs = s->class_start + (size_t)l * (NC + 1);
         if (u0 < 0 || s->unit_start[l + 1] < u0 || s->unit_start[l + 1] > n_units) return -2;
@@ -730,7 +733,10 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
     std::vector<int32_t> level_tasks;
     int rc = flow_tasks(s, b->n_units, tasks, level_tasks);
     if (rc) return rc;
-    if (tasks.empty()) return 0;
+    if (tasks.empty()) {   // (everything at level 0, run by its own launch): a clear error word
+        if ((size_t)s->workspace_bytes < 16 || ((uintptr_t)s->workspace & 15)) return -5;
+        return hipMemsetAsync(s->workspace, 0, 16, stream) == hipSuccess ? 0 : -3;
+    }
     if (s->flags & DGPU_IS_SB) return flow_sb_launch(BPC, b, e, s, tasks, stream);
     const bool devdeps = s->flags & DGPU_IS_DEVICE_DEPS;
     const int64_t nd = devdeps ? 0 : flow_check_deps(s, b->n_units, tasks);
@@ -767,6 +773,9 @@ static int launch_flow(const Dav1dGpuFrameBatch *b, const Dav1dGpuIntraEdgeBatch
             memcpy(st + (Lw.deps - Lw.tasks), s->deps, (size_t)nd * 4);
         }
         if (hipMemsetAsync(ws, 0, Lw.tasks, stream) != hipSuccess) return -3;   // counters and done flags
+        const int lead = lead_levels(s);   // the leading levels' units: done (any non-zero word)
+        if (lead && dataflow && hipMemsetAsync(ws + Lw.done, 1, (size_t)s->unit_start[lead] * 4, stream) != hipSuccess)
+            return -3;
         // once the copy may be queued, the buffer is busy until the stream
         // has passed it: on a later failure drain the stream before returning
         if (hipMemcpyAsync(ws + Lw.tasks, sg->p, up, hipMemcpyHostToDevice, stream) != hipSuccess ||

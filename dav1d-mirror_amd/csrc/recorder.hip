@@ -1169,7 +1169,7 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     Dav1dGpuIntraSchedule s;
     memset(&s, 0, sizeof(s));
     s.n_levels = n_levels;
-    s.flags = DGPU_IS_FUSED | DGPU_IS_PERSISTENT | DGPU_IS_DEVICE_DEPS;
+    s.flags = DGPU_IS_FUSED | DGPU_IS_PERSISTENT | DGPU_IS_DEVICE_DEPS | DGPU_IS_LEVEL0_BATCH;
     s.unit_start = r->unit_start.data();
     s.class_start = r->class_start.data();
     s.rec_start = r->rec_start.data();

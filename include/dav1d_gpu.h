@@ -708,6 +708,17 @@ int dav1d_gpu_backup_ipred_edge_16bpc(const Dav1dGpuIntraEdgeBatch *b, const Dav
                                    recorder's schedules, built on the device
                                    (every unit's producers in earlier tasks) */
 
+#define DGPU_IS_LEVEL0_BATCH 16   /* (with PERSISTENT) level 0 -- units that
+                                   wait for nothing: a mixed frame's inter
+                                   units and first intra units -- and each
+                                   following level of at least 2048 units in
+                                   ordinary fused launches, one per level,
+                                   ahead of the persistent kernel, whose waves
+                                   then take the levels above them only (the
+                                   persistent kernel pays an atomic ticket and
+                                   an agent-scope release per task, which wide
+                                   levels do not need) */
+
 typedef struct Dav1dGpuIntraSchedule {
     int32_t n_levels;
     int32_t flags;               /* DGPU_IS_*                                   */

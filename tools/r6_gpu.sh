@@ -55,6 +55,12 @@ for s in "${@:-tests}"; do
             cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/recprof" -o rec \
                 -- python3 -u "$R/tools/rec_prep_time.py" --reps 3 > "$O/recprof.log" 2>&1 || { echo "[r6] recprof failed"; exit 1; }
             cd "$R" ;;
+    leadab) # the recorder flush's leading-level threshold (DAV1D_GPU_LEAD_UNITS), stream / host / prep times
+            for L in ${LEADU:-1000000000 8192 4096 2048 1024 512}; do
+                DAV1D_GPU_LEAD_UNITS=$L timeout -k 10 300 python -u tools/rec_prep_time.py --reps 5 > "$O/leadab_$L.log" 2>&1 \
+                    || { echo "[r6] leadab $L failed"; exit 1; }
+                echo "leadab $L $(tail -1 "$O/leadab_$L.log")"
+            done ;;
     checkasm) # the full checkasm-style space (no --quick), one pass per table and bitdepth
             for t in ${CKT:-mc ipred itx cdef lpf lr}; do for b in 8 16; do
                 timeout -k 10 1200 ./tests/checkasm_gpu --test=$t --bpc=$b --seed=1 > "$O/checkasm_full_${t}_${b}.log" 2>&1 \
