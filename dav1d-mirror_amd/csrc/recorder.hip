@@ -663,8 +663,14 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         t_0 = t;
     };
     if (!host && !r->pst) {
-        if (hipStreamCreateWithFlags(&r->pst, hipStreamNonBlocking) != hipSuccess) return -3;
-        if (hipStreamCreateWithFlags(&r->cst, hipStreamNonBlocking) != hipSuccess ||
+        // the prep's streams at the device's greatest priority: the flush
+        // waits for the prep, which must not queue behind other work that
+        // shares its hardware queue (a process has GPU_MAX_HW_QUEUES of them,
+        // 4 by default, for all its streams)
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+        if (hipStreamCreateWithPriority(&r->pst, hipStreamNonBlocking, hi) != hipSuccess) return -3;
+        if (hipStreamCreateWithPriority(&r->cst, hipStreamNonBlocking, hi) != hipSuccess ||
             hipEventCreateWithFlags(&r->prep, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&r->coef_ev, hipEventDisableTiming) != hipSuccess || hipEventCreate(&r->pt0) != hipSuccess ||
             hipEventCreate(&r->pt1) != hipSuccess)

@@ -52,6 +52,9 @@ for s in "${@:-tests}"; do
             DAV1D_GPU_REC_TIMING=1 timeout -k 10 300 python -u tools/rec_prep_time.py --reps 5 --threads 4 > "$O/recprep.log" 2>&1 \
                 || { echo "[r6] recprep failed"; exit 1; }
             tail -3 "$O/recprep.log"
+            timeout -k 10 300 python -u tools/rec_prep_time.py --reps 2 --threads 4 --busy > "$O/recprep_busy.log" 2>&1 \
+                || { echo "[r6] recprep busy failed"; exit 1; }
+            tail -3 "$O/recprep_busy.log"
             cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/recprof" -o rec \
                 -- python3 -u "$R/tools/rec_prep_time.py" --reps 3 > "$O/recprof.log" 2>&1 || { echo "[r6] recprof failed"; exit 1; }
             cd "$R" ;;

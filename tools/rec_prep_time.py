@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--inter", type=float, default=0.7)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--threads", type=int, default=0, help="also: N recorders flushing at once from N threads")
+    ap.add_argument("--busy", action="store_true",
+                    help="threads: the device kept busy by a 0.3 s kernel on the default stream meanwhile (as bench.py)")
     a = ap.parse_args()
     import torch
     import __graft_entry__ as ge
@@ -64,6 +66,8 @@ def main():
             for r_ in recs:
                 intra.replay(r_, fr)
             torch.cuda.synchronize(dev)
+            if a.busy:
+                torch.cuda._sleep(int(0.3 * 2.0e9))
             go = threading.Barrier(nf + 1)
             hms = [0.0] * nf
 
