@@ -908,12 +908,14 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         int32_t *seg = raw + raws[ci];
         int m = 0;
         const int32_t lo = cell_base, hi = cell_base + ci;   // this flush, before the cell
+        int32_t last = -1;   // (runs of one writer are common: a row of its 4x4s)
         lookups<true>(j, mp.own[j.p], mp.w[j.p], mp.own[0], mp.w[0], [&](int32_t o) {
-            if (o <= -2) {   // the inter-intra prediction cell, by index
-                seg[m++] = -2 - o;
-            } else if (o >= lo && o < hi) {
-                seg[m++] = o - cell_base;
-            }
+            int32_t v;
+            if (o <= -2) v = -2 - o;   // the inter-intra prediction cell, by index
+            else if (o >= lo && o < hi) v = o - cell_base;
+            else return;
+            if (v != last) seg[m++] = v;
+            last = v;
         });
         int u = 0;   // sorted, duplicate-free (lists are short: insertion sort in place)
         for (int a = 0; a < m; a++) {
