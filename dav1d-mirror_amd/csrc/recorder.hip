@@ -94,6 +94,7 @@ struct Mem {
 struct Stage {
     uint8_t *p = nullptr;
     size_t n = 0, cap = 0;
+    size_t up = 0;   // bytes already copied to the device mirror (streamed while recording)
     bool pinned = false;
     void *append(size_t m) {
         if (n + m > cap && reserve(n + m)) return nullptr;
@@ -370,8 +371,10 @@ struct Dav1dGpuRecorder {
     hipEvent_t done = nullptr;
     bool pending_check = false;   // the last flush's error word not read yet
     int32_t last_units = 0, last_levels = 0;
+    bool streaming = false;   // the recording goes up while it is made (after a first flush)
     void drop_recording() {
         blocks.n = baux_off.n = baux.n = res.n = coefb.n = 0;
+        blocks.up = baux_off.up = baux.up = res.up = 0;
         last_wmask = -1;
         cell_bound = 0;
     }
@@ -484,16 +487,48 @@ static int check_block(const Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, boo
     return 0;
 }
 
+// The recording streamed to the device while the decoder makes it: once a
+// first flush has made the recorder's stream and device buffers, every
+// kStreamChunk of new block / residual records is queued for upload on the
+// recorder's stream right away (the pinned staging is read in place), so a
+// flush uploads only the tail.  Only the prep reads these buffers, and every
+// flush has finished its prep before it returns.
+constexpr size_t kStreamChunk = 1 << 20;
+static void stream_up(Dav1dGpuRecorder *r, Stage &s, Mem &d) {
+    if (!r->streaming || s.n - s.up < kStreamChunk || s.n > d.cap || !s.pinned) return;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) return;
+    if (prev != r->device && hipSetDevice(r->device) != hipSuccess) return;
+    if (hipMemcpyAsync((uint8_t *)d.p + s.up, s.p + s.up, s.n - s.up, hipMemcpyHostToDevice, r->pst) == hipSuccess)
+        s.up = s.n;
+    if (prev != r->device) (void)hipSetDevice(prev);
+}
+// appends m bytes to a streamed stage: a copy may still be reading the old
+// staging when it has to grow, so the recorder's stream is drained first
+static void *stage_append(Dav1dGpuRecorder *r, Stage &s, size_t m) {
+    if (s.n + m > s.cap && s.up && r->pst) {
+        int prev = -1;
+        if (hipGetDevice(&prev) == hipSuccess) {
+            if (prev != r->device) (void)hipSetDevice(r->device);
+            (void)hipStreamSynchronize(r->pst);
+            if (prev != r->device) (void)hipSetDevice(prev);
+        }
+    }
+    return s.append(m);
+}
+
 // appends the block with its data offset (or -1, or -2 - the INTER_WMASK
 // block a COMPOUND_SEG chroma mask reads)
 static int push_block(Dav1dGpuRecorder *r, const Dav1dGpuRecBlock *b, int32_t aux_off) {
     if (r->nblocks() >= (size_t)INT32_MAX / 2) return -1;
-    void *q = r->blocks.append(sizeof(*b));
-    int32_t *o = (int32_t *)r->baux_off.append(4);
+    void *q = stage_append(r, r->blocks, sizeof(*b));
+    int32_t *o = (int32_t *)stage_append(r, r->baux_off, 4);
     if (!q || !o) return -1;
     memcpy(q, b, sizeof(*b));
     *o = aux_off;
     r->cell_bound += (int64_t)(b->w / tx_w(b->tx)) * (b->h / tx_h(b->tx)) + 1;   // (an inter-intra block adds one)
+    stream_up(r, r->blocks, r->d_blocks);
+    stream_up(r, r->baux_off, r->d_baux_off);
     return 0;
 }
 
@@ -559,14 +594,16 @@ extern "C" int dav1d_gpu_rec_block_aux(Dav1dGpuRecorder *r, const Dav1dGpuRecBlo
     if (!aux || aux_bytes != need) return -1;
     const size_t o = r->baux.n, pad = (16 - (aux_bytes & 15)) & 15;   // entries 16-byte aligned
     if (o + aux_bytes + pad > (size_t)INT32_MAX) return -1;
-    uint8_t *q = (uint8_t *)r->baux.append(aux_bytes + pad);
+    uint8_t *q = (uint8_t *)stage_append(r, r->baux, aux_bytes + pad);
     if (!q) return -1;
     memcpy(q, aux, aux_bytes);
     memset(q + aux_bytes, 0, pad);
     if (push_block(r, b, (int32_t)o)) {
         r->baux.n = o;
+        r->baux.up = std::min(r->baux.up, o);
         return -1;
     }
+    stream_up(r, r->baux, r->d_baux);
     return 0;
 }
 
@@ -595,11 +632,12 @@ extern "C" int dav1d_gpu_rec_residual(Dav1dGpuRecorder *r, int plane, int x, int
         q.nzh = nzh;
     }   // else the DC-only call (src/itx_tmpl.c:53): one coefficient, nzw = nzh = 0
     uint8_t *d = (uint8_t *)r->coefb.append((size_t)nzw * nzh * cb);
-    void *qq = r->res.append(sizeof(q));
+    void *qq = stage_append(r, r->res, sizeof(q));
     if (!d || !qq) return -1;
     for (int cx = 0; cx < nzw; cx++)   // appended in the ABI's coefficient type, column by column
         memcpy(d + (size_t)cx * nzh * cb, (const uint8_t *)coef + (size_t)cx * sh * cb, (size_t)nzh * cb);
     memcpy(qq, &q, sizeof(q));
+    stream_up(r, r->res, r->d_res);
     return 0;
 }
 
@@ -721,8 +759,16 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
     }
 
     // 0. the recording, as recorded
-    if (r->d_blocks.grow(r->blocks.n) || r->d_baux_off.grow(r->baux_off.n) || r->d_baux.grow(r->baux.n) ||
-        r->d_res.grow(r->res.n) || r->d_coef.grow(r->coefb.n) || r->d_hdr.grow(sizeof(Hdr)) ||
+    // the streamed records' mirrors sized for their staging's capacity (the
+    // next recording's chunks then fit); a reallocated mirror is refilled
+    auto mirror = [&](Mem &d, Stage &st) {
+        const void *old = d.p;
+        if (d.grow(host ? st.n : std::max(st.n, st.cap))) return -1;
+        if (d.p != old) st.up = 0;
+        return 0;
+    };
+    if (mirror(r->d_blocks, r->blocks) || mirror(r->d_baux_off, r->baux_off) || mirror(r->d_baux, r->baux) ||
+        mirror(r->d_res, r->res) || r->d_coef.grow(r->coefb.n) || r->d_hdr.grow(sizeof(Hdr)) ||
         r->d_cnt.grow((size_t)nb * sizeof(BlockCnt)) || r->d_base.grow((size_t)nb * sizeof(BlockCnt)) ||
         r->d_auxend.grow((size_t)nb * 4))
         return fail(-3);
@@ -731,10 +777,14 @@ extern "C" int dav1d_gpu_recorder_flush(Dav1dGpuRecorder *r, const Dav1dGpuPlane
         r->rb_cap = 1 << 16;
     }
     if (!host && hipEventRecord(r->pt0, r->pst) != hipSuccess) return fail(-3);
-    X.upload(r->d_blocks.p, r->blocks.p, r->blocks.n);
-    X.upload(r->d_baux_off.p, r->baux_off.p, r->baux_off.n);
-    X.upload(r->d_baux.p, r->baux.p, r->baux.n);
-    X.upload(r->d_res.p, r->res.p, r->res.n);
+    for (auto &m : {std::make_pair(&r->d_blocks, &r->blocks), std::make_pair(&r->d_baux_off, &r->baux_off),
+                    std::make_pair(&r->d_baux, &r->baux), std::make_pair(&r->d_res, &r->res)}) {
+        Stage &st = *m.second;   // the part not streamed yet
+        if (host) st.up = 0;
+        X.upload((uint8_t *)m.first->p + st.up, st.p + st.up, st.n - st.up);
+        if (!X.err) st.up = st.n;
+    }
+    r->streaming = !host && !X.err;   // from now on the recording streams up as it is made
     Hdr *hdr = r->d_hdr.as<Hdr>();
     X.memset(hdr, 0, sizeof(Hdr));
     {   // residual lookup: per plane, the top-left 4x4 cell of each residual

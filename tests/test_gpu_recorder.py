@@ -333,7 +333,9 @@ def test_recorder_device_image_golden(tmp_path):
     tools/rec_dump.py's seven frames byte for byte as the round-6 host
     implementation made them (tests/golden/rec_dump_md5.json; the same
     frames' host-only steps are checked in test_cpu_recorder_golden.py).
-    Dump mode launches nothing on the (dummy) pictures."""
+    Dump mode launches nothing on the (dummy) pictures.  Every frame is
+    flushed twice on one recorder, so the second recording streams to the
+    device while it is made."""
     import json
     import os
     import re
@@ -344,10 +346,13 @@ def test_recorder_device_image_golden(tmp_path):
     env = dict(os.environ)
     env.pop("DAV1D_GPU_REC_HOSTONLY", None)
     r = subprocess.run([sys.executable, os.path.join(root, "tools", "rec_dump.py"), str(tmp_path / "d.bin"),
-                        "--device"], env=env, capture_output=True, text=True, timeout=300)
+                        "--device", "--twice"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    got = {m.group(1): (int(m.group(3)), m.group(4)) for m in
-           re.finditer(r"frame (\d+) rc (\S+) units (\d+) .* md5 (\w+)", r.stdout)}
-    assert set(got) == set(want), r.stdout
-    for k, w in want.items():
-        assert got[k] == (w["units"], w["md5"]), (k, got[k], w)
+    # each frame flushed twice on one recorder: the second recording's records
+    # stream to the device while they are made (kStreamChunk pieces)
+    for tag in ("frame", "again"):
+        got = {m.group(1): (int(m.group(3)), m.group(4)) for m in
+               re.finditer(tag + r" (\d+) rc (\S+) units (\d+) .* md5 (\w+)", r.stdout)}
+        assert set(got) == set(want), r.stdout
+        for k, w in want.items():
+            assert got[k] == (w["units"], w["md5"]), (tag, k, got[k], w)

@@ -5,7 +5,7 @@ built by the device steps on the GPU and read back (nothing is launched on
 the pictures, whose addresses are dummies).  Compares builds, and the device
 against the host, byte for byte (tests/golden/rec_dump_md5.json).
 
-  python tools/rec_dump.py OUT.bin [--only I] [--device]   (prints one md5 per frame)"""
+  python tools/rec_dump.py OUT.bin [--only I] [--device] [--twice]   (prints one md5 per frame and flush)"""
 import ctypes
 import hashlib
 import os
@@ -64,12 +64,18 @@ def main():
             for p, (w, h) in enumerate(fr.plane_wh):
                 st = (w + 2 * fr.cfg.ref_pad) * (fr.cfg.bpc // 8)
                 r[k][p].data, r[k][p].stride, r[k][p].w, r[k][p].h = 0x1000, st, w, h
-        intra.replay(rec, fr)
-        t0 = time.perf_counter()
-        rc = rec.lib.dav1d_gpu_recorder_flush(rec.h, ctypes.byref(d), ctypes.byref(r), None)
-        t1 = time.perf_counter()
-        md5 = hashlib.md5(open(out, "rb").read()).hexdigest() if os.path.exists(out) else None
-        print(f"frame {i} rc {rc} units {rec.stats()[0]} flush {1e3 * (t1 - t0):.2f} ms md5 {md5}", flush=True)
+        # --twice: the same recording flushed again on the same recorder (its
+        # records then stream to the device while they are made)
+        for rep in range(2 if "--twice" in sys.argv else 1):
+            if os.path.exists(out):
+                os.remove(out)
+            intra.replay(rec, fr)
+            t0 = time.perf_counter()
+            rc = rec.lib.dav1d_gpu_recorder_flush(rec.h, ctypes.byref(d), ctypes.byref(r), None)
+            t1 = time.perf_counter()
+            md5 = hashlib.md5(open(out, "rb").read()).hexdigest() if os.path.exists(out) else None
+            tag = f"frame {i}" if not rep else f"again {i}"
+            print(f"{tag} rc {rc} units {rec.stats()[0]} flush {1e3 * (t1 - t0):.2f} ms md5 {md5}", flush=True)
         rec.close()
 
 
