@@ -35,7 +35,7 @@ def main():
     dev = torch.device("cuda:0")
     dst = [torch.zeros((h, w), dtype=torch.uint8, device=dev) for (w, h) in fr.plane_wh]
     refs = [[(torch.from_numpy(x.copy()).to(dev), fr.ref_origin_offset(p), fr.plane_wh[p][0], fr.plane_wh[p][1])
-             for p, x in enumerate(rp)] for rp in fr.refs]
+             for p, x in enumerate(rp)] for rp in (fr.refs or [])]
     rec = intra.Recorder(8, 255, a.width, a.height)
     s = torch.cuda.current_stream(dev)
     rows = []
