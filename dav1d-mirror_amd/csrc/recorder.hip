@@ -278,8 +278,11 @@ struct Exec {
     }
     void fetch(void *h, const void *d, size_t n) {   // queued; complete after sync()
         if (!n || err) return;
-        if (host) memcpy(h, d, n);
-        else if (hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st) != hipSuccess) err = -3;
+        if (host) {
+            if (h != d) memcpy(h, d, n);   // (host-only: the "device" buffer is often read in place)
+        } else if (hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st) != hipSuccess) {
+            err = -3;
+        }
     }
     void sync() {
         if (!host && !err && hipStreamSynchronize(st) != hipSuccess) err = -3;
