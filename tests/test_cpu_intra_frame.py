@@ -157,10 +157,11 @@ def test_sb_schedule(pkg, kw):
     assert np.all(np.diff(sds) <= 4)
 
 
-def _flow_tasks_py(pkg, fr, groups, cap=8):
+def _flow_tasks_py(pkg, fr, groups, cap=8, first_level=0):
     """The wave tasks flow_impl.hpp's flow_tasks cuts (classes largest first
     per level; above level 0 at most `cap` units, and with task groups never
-    across a change of the group byte)."""
+    across a change of the group byte); levels below first_level left out
+    (DGPU_IS_LEVEL0_BATCH)."""
     abi = pkg.abi
     order = [3, 9, 10, 2, 15, 16, 7, 8, 1, 13, 14, 5, 6, 0, 4, 11, 12, 17, 18]
     # the wavefront TUs (recon_ie{8,16}.hip): 4x4 / 4x8 / 8x4 units get 8
@@ -170,7 +171,7 @@ def _flow_tasks_py(pkg, fr, groups, cap=8):
     for t, (tw, th) in enumerate(abi.TX_WH):
         lanes[t] = 8 if tw * th <= 32 else min(max(tw * th // 8, 2), 64)
     n = 0
-    for lv in range(fr.n_levels):
+    for lv in range(first_level, fr.n_levels):
         cs = fr.class_start[lv]
         for c in order:
             full = 64 // lanes[c]
@@ -213,3 +214,19 @@ def test_flow_task_cut(pkg):
         want = (32 + 16 * nl) * 4 + ((n * 4 + 15) & ~15) + nt * 16 + nl * 4 + (n + 1) * 4 + len(fr.deps) * 4
         assert L.dav1d_gpu_intra_workspace_bytes(ctypes.byref(s), n) == want, groups is not None
     assert _flow_tasks_py(pkg, fr, tg) > _flow_tasks_py(pkg, fr, None)
+    # DGPU_IS_LEVEL0_BATCH (lead_levels.hpp): level 0 and each next level of
+    # >= 2048 units run as launches of their own, out of the task list
+    sizes = np.diff(np.asarray(fr.unit_start))
+    lead = 1
+    while lead < nl and sizes[lead] >= 2048:
+        lead += 1
+    s = abi.IntraSchedule()
+    s.n_levels = nl
+    s.flags = abi.IS_FUSED | abi.IS_PERSISTENT | abi.IS_LEVEL0_BATCH
+    s.unit_start, s.class_start = keep[0].ctypes.data, keep[1].ctypes.data
+    s.rec_start, s.run_start = keep[0].ctypes.data, keep[0].ctypes.data
+    s.dep_start, s.deps = keep[2].ctypes.data, keep[3].ctypes.data
+    nt = _flow_tasks_py(pkg, fr, None, first_level=lead)
+    want = (32 + 16 * nl) * 4 + ((n * 4 + 15) & ~15) + nt * 16 + nl * 4 + (n + 1) * 4 + len(fr.deps) * 4
+    assert L.dav1d_gpu_intra_workspace_bytes(ctypes.byref(s), n) == want
+    assert nt < _flow_tasks_py(pkg, fr, None)
