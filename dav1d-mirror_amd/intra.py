@@ -975,7 +975,7 @@ class DeviceIntraFrame:
     """An IntraFrame on one GPU; launch() runs the whole wavefront
     (dav1d_gpu_recon_intra_frame_*) on a stream."""
 
-    MODES = ("persistent", "levels", "fused", "staged", "sb")
+    MODES = ("persistent", "levels", "fused", "staged", "sb", "lead")
 
     def __init__(self, fr, device="cuda:0", top_fill=0x5A, mode="persistent", task_groups=False):
         """mode: persistent -- one launch per frame (DGPU_IS_PERSISTENT), a
@@ -989,11 +989,14 @@ class DeviceIntraFrame:
         (prediction kind and coded intra mode per unit), so a wave task of the
         persistent kernels runs one mode's code path (measured neutral on
         the 4K frames: 17.5 against 17.8 ms with one tile, 11.4 against 11.0
-        with 2x2 tiles, so off by default)."""
+        with 2x2 tiles, so off by default).  lead -- persistent with
+        DGPU_IS_LEVEL0_BATCH: level 0 and each next level of >= 2048 units
+        as fused launches ahead of the persistent kernel."""
         assert mode in self.MODES
-        dataflow = mode == "persistent"
+        lead = mode == "lead"
+        dataflow = mode in ("persistent", "lead")
         self.sb = mode == "sb"
-        mode = "persistent" if mode in ("levels", "sb") else mode
+        mode = "persistent" if mode in ("levels", "sb", "lead") else mode
         import torch
         self.torch = torch
         self.perm = None
@@ -1035,6 +1038,8 @@ class DeviceIntraFrame:
         s = abi.IntraSchedule()
         s.n_levels = len(fr.unit_start) - 1
         s.flags = {"persistent": abi.IS_FUSED | abi.IS_PERSISTENT, "fused": abi.IS_FUSED, "staged": 0}[mode]
+        if lead:
+            s.flags |= abi.IS_LEVEL0_BATCH
         if self.sb:
             s.flags |= abi.IS_SB
             s.n_sb = self.n_sb

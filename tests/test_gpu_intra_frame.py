@@ -54,7 +54,7 @@ def test_intra_frame_variants(oracle, kw, mode):
     _check(oracle, _frame(**kw), mode=mode)
 
 
-@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged", "sb"])
+@pytest.mark.parametrize("mode", ["persistent", "levels", "fused", "staged", "sb", "lead"])
 @pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
 def test_mixed_frame(oracle, mode, bpc, bdmax):
     """Inter blocks (put / compound avg from padded references) among the
@@ -103,3 +103,16 @@ def test_lossless_frame(oracle, mode, bpc, bdmax):
     fr = _frame(seed=42, inter_frac=0.4, bpc=bpc, bitdepth_max=bdmax, lossless=0.8)
     assert (fr.units["txtp"] == 16).sum() > 100
     _check(oracle, fr, mode=mode)
+
+
+@pytest.mark.parametrize("bpc,bdmax", [(8, 255), (16, 1023)])
+def test_mixed_frame_lead_levels(oracle, bpc, bdmax):
+    """DGPU_IS_LEVEL0_BATCH on a caller's schedule: a 1080p mixed frame whose
+    first levels hold >= 2048 units each, so several leading levels run as
+    fused launches (units, records and per-unit aux offset to the level)
+    before the persistent kernel takes the rest; bit-exact."""
+    import numpy as np
+    fr = _frame(seed=42, width=1920, height=1080, inter_frac=0.7, bpc=bpc, bitdepth_max=bdmax)
+    sizes = np.diff(np.asarray(fr.unit_start))
+    assert sizes[0] >= 2048 and sizes[1] >= 2048   # more than level 0 leads
+    _check(oracle, fr, mode="lead")
